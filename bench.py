@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""Benchmark of the path tracer on BASELINE.json's metric config: Sponza(-proxy) 1920x1080,
+MaxPathLength 3, one sample per pixel per frame with progressive accumulation.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+A step is one frame (DispatchRays(1920,1080,1) equivalent, DXRPathTracer.cpp:2024-2090) over the whole
+image.  With N ranks the image is split into 16-row bands (band b -> rank b % N) and every frame ends
+with an RCCL gather of the band slabs to rank 0 plus the un-permute: total work per
+frame is fixed, so scaling is "strong".  value = nominal Mrays/s of the whole job (W*H*(1+2(L-1))
+rays per frame, the reference's HUD formula DXRPathTracer.cpp:2171) over the max-over-ranks time.
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+WIDTH, HEIGHT, PATH_LENGTH = 1920, 1080, 3
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "Mrays/sec + ms/frame, Sponza 1920x1080 path-length 3 at 1/2/4/8 GPU"
+# k_trace algorithmic bytes: per ray 32 B ray in (2 x float4) + 16 B hit out, plus the
+# BVH nodes (64 B) and triangle records (48 B) it visits (counted by the instrumented kernels).
+RAY_IN_BYTES, HIT_OUT_BYTES = 32, 16
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(scene, sky, settings, threads):
+    """The CPU oracle (scalar C++ restatement, own BVH) on a bounded sample: one full 1920x1080 L=3
+    frame at CurrSampleIdx 0, on `threads` host threads."""
+    import dxrpathtracer_amd as D
+    from oracle import pyoracle as O
+    orc = O.OracleScene(scene, sky)
+    rtc = D.make_constants(scene, settings, sky, WIDTH, HEIGHT, 0)
+    t0 = time.perf_counter()
+    _, st = orc.render(rtc, settings, D.make_lights(scene), WIDTH, HEIGHT, threads=threads)
+    dt = time.perf_counter() - t0
+    nominal = WIDTH * HEIGHT * (1 + 2 * (PATH_LENGTH - 1))
+    return {"value": round(nominal / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"one full {WIDTH}x{HEIGHT} L={PATH_LENGTH} frame (sample 0) of the same scene, "
+                      f"{dt:.2f} s wall, {st.radiance_rays + st.shadow_rays} rays traced, oracle BVH",
+            "frame_s": round(dt, 3)}
+
+
+def pmc_traffic():
+    """HBM bytes per k_trace launch from the committed rocprofv3 PMC summary, if one exists for this
+    config (profiles/*_pmc_k_trace.json, written by scripts/pmc_summary.py); else None."""
+    import glob
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_k_trace.json")), reverse=True):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if d.get("config") == f"sponza-proxy {WIDTH}x{HEIGHT} L={PATH_LENGTH}":
+            return d.get("hbm_bytes_per_launch"), os.path.basename(p)
+    return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import dxrpathtracer_amd as D
+    import dxrpathtracer_amd._abi as A
+    from dxrpathtracer_amd.distributed import band_layout, gather_frame, source_index
+    from dxrpathtracer_amd.tracer import DXRPathTracer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    # ---- scene + acceleration structure (untimed, like the reference's InitializeScene + AS build)
+    t0 = time.perf_counter()
+    scene = D.Scene("sponza")
+    settings = scene.settings(MaxPathLength=PATH_LENGTH)
+    sky = D.make_sky(settings)
+    tracer = DXRPathTracer(local_rank)
+    tracer.initialize_scene(scene, sky)
+    bvh = tracer.build_rt_acceleration_structure()
+    setup_s = time.perf_counter() - t0
+    lights = D.make_lights(scene)
+    lay = band_layout(WIDTH, HEIGHT, world)
+    tiles = lay.rank_tiles(rank) if world > 1 else None
+    n_local = lay.counts[rank] if world > 1 else WIDTH * HEIGHT
+    accum = torch.zeros((max(lay.max_count, n_local), 4), dtype=torch.float32, device="cuda")
+    full = idx = None
+    if world > 1 and rank == 0:
+        full = torch.zeros((WIDTH * HEIGHT, 4), dtype=torch.float32, device="cuda")
+        idx = torch.tensor(source_index(lay), dtype=torch.long, device="cuda")
+    consts = [D.make_constants(scene, settings, sky, WIDTH, HEIGHT, s) for s in range(16)]
+
+    def frame(f):
+        tracer.render_raw(consts[f % 16], settings, accum.data_ptr(), WIDTH, HEIGHT, tiles=tiles, stream=sh,
+                          lights=lights)
+        if world > 1:
+            gather_frame(accum, lay, rank, full, idx)
+
+    # ---- traversal work census (instrumented kernels, untimed): nodes / triangles per ray
+    tracer.set_option(A.OPT_COUNT_TRAVERSAL, 1)
+    frame(0)
+    census = tracer.stats()
+    tracer.set_option(A.OPT_COUNT_TRAVERSAL, 0)
+
+    for f in range(args.warmup):
+        frame(f)
+    torch.cuda.synchronize()
+
+    # ---- timed region
+    tracer.set_option(A.OPT_KERNEL_TIMING, 1)
+    tracer.reset_timing()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for f in range(args.steps):
+        frame(args.warmup + f)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    stats = tracer.stats()
+    tracer.set_option(A.OPT_KERNEL_TIMING, 0)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    nominal_per_frame = WIDTH * HEIGHT * (1 + 2 * (PATH_LENGTH - 1))
+    ms_per_step = elapsed / args.steps * 1e3
+    value = nominal_per_frame * args.steps / elapsed / 1e6
+
+    # ---- roofline of the dominant kernel (measured live with HIP events on the render stream)
+    kms = {A.KERNEL_NAMES[k]: stats.kernel_ms[k] for k in range(A.K_COUNT)}
+    dominant = max(kms, key=kms.get)
+    rays = census.radiance_rays
+    trace_bytes_frame = (rays * (RAY_IN_BYTES + HIT_OUT_BYTES) + census.node_visits_radiance * bvh.node_bytes
+                         + census.tri_tests_radiance * bvh.tri_bytes)
+    trace_launches_per_frame = PATH_LENGTH - 1
+    trace_ms_avg = stats.kernel_ms[A.K_TRACE] / max(1, stats.kernel_launches[A.K_TRACE])
+    achieved = (trace_bytes_frame / trace_launches_per_frame) / (trace_ms_avg * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic()
+
+    result = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(scene, sky, settings, args.cpu_threads)
+        frames = stats.timed_frames or 1
+        result = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: seeded procedural Sponza proxy (Sponza.fbx absent from the reference snapshot)",
+            "config": {"workload": f"sponza-proxy {WIDTH}x{HEIGHT} L={PATH_LENGTH} 1spp/frame progressive",
+                       "width": WIDTH, "height": HEIGHT, "max_path_length": PATH_LENGTH,
+                       "sqrt_num_samples": 4, "triangles": scene.num_triangles,
+                       "parallelism": f"screen bands x{world}" + (" + RCCL gather" if world > 1 else "")},
+            "roofline": {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "bytes_per_launch": int(trace_bytes_frame / trace_launches_per_frame),
+                         "avg_launch_ms": round(trace_ms_avg, 4), "traffic_source": traffic_src},
+            "cpu_baseline": cpu,
+            "detail": {
+                "counted_rays_per_frame": int(stats.radiance_rays + stats.shadow_rays),
+                "counted_Mrays_s": round((stats.radiance_rays + stats.shadow_rays) * world * args.steps / elapsed / 1e6, 2)
+                if world == 1 else None,
+                "kernel_ms_per_frame": {k: round(v / frames, 4) for k, v in kms.items()},
+                "dominant_kernel": dominant,
+                "gpu_frame_ms_events": round(stats.frame_ms / frames, 4),
+                "nodes_per_radiance_ray": round(census.node_visits_radiance / max(1, rays), 2),
+                "tris_per_radiance_ray": round(census.tri_tests_radiance / max(1, rays), 2),
+                "nodes_per_shadow_ray": round(census.node_visits_shadow / max(1, census.shadow_rays), 2),
+                "bvh": {"nodes": bvh.num_nodes, "max_depth": bvh.max_depth, "build_ms": round(bvh.build_ms, 1),
+                        "sah": round(bvh.sah_cost, 2)},
+                "setup_s": round(setup_s, 2),
+            },
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    tracer.close()
+
+
+if __name__ == "__main__":
+    main()

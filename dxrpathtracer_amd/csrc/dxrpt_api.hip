@@ -1,0 +1,633 @@
+// dxrpt_api.hip — the C ABI (include/dxrpt.h): context, scene upload, BVH build, render.
+//
+// Host-side counterpart of DXRPathTracer::BuildRTAccelerationStructure (DXRPathTracer.cpp:2331-2488)
+// and DXRPathTracer::RenderRayTracing (DXRPathTracer.cpp:2024-2090).  No exception crosses the ABI:
+// every entry point catches, stores a message for dxrpt_last_error and returns a DXRPT_E_* code.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/dxrpt.h"
+#include "bvh_build.h"
+#include "pt_kernels.h"
+#include "pt_layout.h"
+
+using namespace dxrpt;
+
+namespace {
+
+struct ApiError : std::runtime_error {
+    int code;
+    ApiError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIP_CHECK(expr)                                                                                   \
+    do {                                                                                                  \
+        hipError_t e_ = (expr);                                                                           \
+        if (e_ != hipSuccess)                                                                             \
+            throw ApiError(DXRPT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));                \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    void ensure(size_t n) {
+        if (n <= bytes && p) return;
+        release();
+        if (n == 0) n = 16;
+        hipError_t e = hipMalloc(&p, n);
+        if (e != hipSuccess) throw ApiError(DXRPT_E_OOM, "hipMalloc(" + std::to_string(n) + "): " + hipGetErrorString(e));
+        bytes = n;
+    }
+    void upload(const void* src, size_t n) {
+        ensure(n);
+        if (n) HIP_CHECK(hipMemcpy(p, src, n, hipMemcpyHostToDevice));
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+}  // namespace
+
+struct dxrpt_ctx {
+    int device = 0;
+    std::string err;
+    // host copies of the scene
+    std::vector<dxrpt_mesh_vertex> vertices;
+    std::vector<uint32_t> indices;
+    std::vector<dxrpt_geometry_info> geos;
+    std::vector<dxrpt_material> mats;
+    std::vector<TexDesc> texdesc;
+    std::vector<uint32_t> texels;
+    bool scene_set = false, bvh_built = false, sky_set = false, tex_dirty = true;
+    uint32_t sky_res = 0;
+    // device copies
+    DevBuf d_vertices, d_indices, d_geos, d_mats, d_texdesc, d_texels, d_sky, d_lut, d_nodes, d_tris;
+    DevBuf d_lights, d_tiles, d_tile_prefix;
+    // per-frame wavefront buffers
+    DevBuf f_thr, f_rad, f_pix, f_qorg0, f_qorg1, f_qdir0, f_qdir1, f_hit, f_shn, f_shorg, f_shdir, f_shcon, f_counters;
+    FrameBuffers fb;
+    dxrpt_bvh_info bvh{};
+    std::vector<dxrpt_tile> tiles_cache;
+    std::vector<dxrpt_spot_light> lights_cache;
+    hipStream_t last_stream = nullptr;
+    dxrpt_stats last{};
+    int last_L = 0;
+    bool rendered = false;
+    // options
+    bool opt_count = false, opt_timing = false;
+    DevBuf d_trav;  // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
+    // kernel timing: a ring of per-frame event sets, harvested lazily
+    struct FrameEvents {
+        std::vector<hipEvent_t> ev;
+        int L = 0;
+        bool pending = false;
+    };
+    std::vector<FrameEvents> ring;
+    size_t ring_head = 0;
+    double kernel_ms[DXRPT_K_COUNT] = {};
+    uint64_t kernel_launches[DXRPT_K_COUNT] = {};
+    uint64_t timed_frames = 0;
+    double frame_ms = 0.0;
+
+    ~dxrpt_ctx() {
+        DevBuf* all[] = {&d_vertices, &d_indices, &d_geos, &d_mats, &d_texdesc, &d_texels, &d_sky, &d_lut, &d_nodes,
+                         &d_tris, &d_lights, &d_tiles, &d_tile_prefix, &f_thr, &f_rad, &f_pix, &f_qorg0, &f_qorg1,
+                         &f_qdir0, &f_qdir1, &f_hit, &f_shn, &f_shorg, &f_shdir, &f_shcon, &f_counters};
+        for (DevBuf* b : all) b->release();
+        d_trav.release();
+        for (auto& f : ring)
+            for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
+    }
+};
+
+namespace {
+
+template <class F>
+int guarded(dxrpt_ctx* ctx, F&& f) {
+    try {
+        if (ctx) HIP_CHECK(hipSetDevice(ctx->device));
+        f();
+        return DXRPT_OK;
+    } catch (const ApiError& e) {
+        if (ctx) ctx->err = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        if (ctx) ctx->err = "host out of memory";
+        return DXRPT_E_OOM;
+    } catch (const std::exception& e) {
+        if (ctx) ctx->err = e.what();
+        return DXRPT_E_INVALID_ARG;
+    }
+}
+
+void require(bool c, const std::string& msg, int code = DXRPT_E_INVALID_ARG) {
+    if (!c) throw ApiError(code, msg);
+}
+
+// 256-entry decode tables: [0,256) unorm c/255, [256,512) sRGB -> linear (IEC 61966-2-1), computed in
+// double and rounded once; oracle/oracle.cpp builds the same table the same way.
+std::vector<float> make_lut() {
+    std::vector<float> l(512);
+    for (int i = 0; i < 256; ++i) {
+        l[i] = float(i) / 255.0f;
+        double c = double(i) / 255.0;
+        double lin = c <= 0.04045 ? c / 12.92 : std::pow((c + 0.055) / 1.055, 2.4);
+        l[256 + i] = float(lin);
+    }
+    return l;
+}
+
+SceneDev scene_dev(const dxrpt_ctx* c) {
+    SceneDev s;
+    s.nodes = c->d_nodes.as<BvhNode>();
+    s.tris = c->d_tris.as<TriRecord>();
+    s.vertices = c->d_vertices.as<dxrpt_mesh_vertex>();
+    s.indices = c->d_indices.as<uint32_t>();
+    s.geoinfo = c->d_geos.as<dxrpt_geometry_info>();
+    s.materials = c->d_mats.as<dxrpt_material>();
+    s.texdesc = c->d_texdesc.as<TexDesc>();
+    s.texels = c->d_texels.as<uint32_t>();
+    s.sky = c->d_sky.as<uint16_t>();
+    s.lut = c->d_lut.as<float>();
+    s.sky_res = c->sky_res;
+    s.num_textures = uint32_t(c->texdesc.size());
+    return s;
+}
+
+void upload_textures(dxrpt_ctx* c) {
+    if (!c->tex_dirty) return;
+    c->d_texdesc.upload(c->texdesc.data(), c->texdesc.size() * sizeof(TexDesc));
+    c->d_texels.upload(c->texels.data(), c->texels.size() * sizeof(uint32_t));
+    c->tex_dirty = false;
+}
+
+void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
+    FrameBuffers& f = c->fb;
+    if (paths <= f.capacity && slots <= f.shadow_slots && f.counters) return;
+    uint32_t cap = std::max(paths, f.capacity);
+    uint32_t sl = std::max(slots, std::max(f.shadow_slots, 2u));
+    c->f_thr.ensure(size_t(cap) * 16);
+    c->f_rad.ensure(size_t(cap) * 16);
+    c->f_pix.ensure(size_t(cap) * 8);
+    c->f_qorg0.ensure(size_t(cap) * 16);
+    c->f_qorg1.ensure(size_t(cap) * 16);
+    c->f_qdir0.ensure(size_t(cap) * 16);
+    c->f_qdir1.ensure(size_t(cap) * 16);
+    c->f_hit.ensure(size_t(cap) * 16);
+    c->f_shn.ensure(size_t(cap) * 4);
+    c->f_shorg.ensure(size_t(cap) * sl * 16);
+    c->f_shdir.ensure(size_t(cap) * sl * 16);
+    c->f_shcon.ensure(size_t(cap) * sl * 16);
+    c->f_counters.ensure(64 * sizeof(uint32_t));
+    f.ps_thr = c->f_thr.as<float4>();
+    f.ps_rad = c->f_rad.as<float4>();
+    f.ps_pix = c->f_pix.as<uint2>();
+    f.q_org[0] = c->f_qorg0.as<float4>();
+    f.q_org[1] = c->f_qorg1.as<float4>();
+    f.q_dir[0] = c->f_qdir0.as<float4>();
+    f.q_dir[1] = c->f_qdir1.as<float4>();
+    f.hit = c->f_hit.as<float4>();
+    f.sh_n = c->f_shn.as<uint32_t>();
+    f.sh_org = c->f_shorg.as<float4>();
+    f.sh_dir = c->f_shdir.as<float4>();
+    f.sh_con = c->f_shcon.as<float4>();
+    f.counters = c->f_counters.as<uint32_t>();
+    f.capacity = cap;
+    f.shadow_slots = sl;
+}
+
+// Adds one timed frame's event intervals to the per-kernel sums (blocks until the frame is done).
+void harvest(dxrpt_ctx* c, dxrpt_ctx::FrameEvents& f) {
+    if (!f.pending) return;
+    HIP_CHECK(hipEventSynchronize(f.ev.back()));
+    auto span = [&](int a, int b) {
+        float ms = 0.f;
+        HIP_CHECK(hipEventElapsedTime(&ms, f.ev[a], f.ev[b]));
+        return double(ms);
+    };
+    int e = 0;
+    c->kernel_ms[DXRPT_K_RAYGEN] += span(e, e + 1);
+    c->kernel_launches[DXRPT_K_RAYGEN]++;
+    ++e;
+    for (int d = 1; d <= f.L - 1; ++d) {
+        c->kernel_ms[DXRPT_K_TRACE] += span(e, e + 1);
+        c->kernel_ms[DXRPT_K_SHADE] += span(e + 1, e + 2);
+        c->kernel_ms[DXRPT_K_SHADOW] += span(e + 2, e + 3);
+        c->kernel_launches[DXRPT_K_TRACE]++;
+        c->kernel_launches[DXRPT_K_SHADE]++;
+        c->kernel_launches[DXRPT_K_SHADOW]++;
+        e += 3;
+    }
+    c->kernel_ms[DXRPT_K_ACCUMULATE] += span(e, e + 1);
+    c->kernel_launches[DXRPT_K_ACCUMULATE]++;
+    c->frame_ms += span(0, e + 1);
+    c->timed_frames++;
+    f.pending = false;
+}
+
+void harvest_all(dxrpt_ctx* c) {
+    for (auto& f : c->ring) harvest(c, f);
+}
+
+}  // namespace
+
+extern "C" {
+
+int dxrpt_abi_version(void) { return DXRPT_ABI_VERSION; }
+
+void dxrpt_default_settings(dxrpt_app_settings* s) {
+    if (!s) return;
+    std::memset(s, 0, sizeof(*s));
+    // AppSettings.cpp:95-208
+    s->EnableSun = 1;
+    s->EnableSky = 1;
+    s->SunAreaLightApproximation = 1;
+    s->SunSize = 1.0f;
+    s->SunDirection[0] = 0.26f;
+    s->SunDirection[1] = 0.987f;
+    s->SunDirection[2] = -0.16f;
+    s->MSAAMode = 2;  // MSAA4x (raster only)
+    s->RenderLights = 1;
+    s->EnableRayTracing = 1;
+    s->ClampRoughness = 0;
+    s->AvoidCausticPaths = 0;
+    s->SqrtNumSamples = 4;
+    s->MaxPathLength = 3;
+    s->MaxAnyHitPathLength = 1;
+    s->Exposure = -14.0f;
+    s->BloomExposure = -4.0f;
+    s->BloomMagnitude = 1.0f;
+    s->BloomBlurSigma = 2.5f;
+    s->EnableAlbedoMaps = 1;
+    s->EnableNormalMaps = 1;
+    s->EnableDiffuse = 1;
+    s->EnableSpecular = 1;
+    s->EnableDirect = 1;
+    s->EnableIndirect = 1;
+    s->EnableIndirectSpecular = 0;
+    s->ApplyMultiscatteringEnergyCompensation = 1;
+    s->RoughnessScale = 1.0f;
+    s->MetallicScale = 1.0f;
+    s->EnableWhiteFurnaceMode = 0;
+    s->EnableLightMapRender = 1;
+}
+
+int dxrpt_create(int hip_device, dxrpt_ctx** out_ctx) {
+    if (!out_ctx) return DXRPT_E_INVALID_ARG;
+    *out_ctx = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return DXRPT_E_NO_DEVICE;
+    if (hip_device < 0 || hip_device >= n) return DXRPT_E_INVALID_ARG;
+    dxrpt_ctx* c = new (std::nothrow) dxrpt_ctx();
+    if (!c) return DXRPT_E_OOM;
+    c->device = hip_device;
+    int rc = guarded(c, [&] {
+        hipDeviceProp_t prop;
+        HIP_CHECK(hipGetDeviceProperties(&prop, hip_device));
+        require(std::strncmp(prop.gcnArchName, "gfx9", 4) == 0,
+                std::string("unsupported device architecture ") + prop.gcnArchName, DXRPT_E_UNSUPPORTED);
+        require(prop.sharedMemPerBlock >= 64 * 1024, "device LDS per workgroup < 64 KiB", DXRPT_E_UNSUPPORTED);
+        std::vector<float> lut = make_lut();
+        c->d_lut.upload(lut.data(), lut.size() * sizeof(float));
+    });
+    if (rc != DXRPT_OK) {
+        delete c;
+        return rc;
+    }
+    *out_ctx = c;
+    return DXRPT_OK;
+}
+
+int dxrpt_destroy(dxrpt_ctx* ctx) {
+    if (!ctx) return DXRPT_E_INVALID_ARG;
+    (void)hipSetDevice(ctx->device);
+    delete ctx;
+    return DXRPT_OK;
+}
+
+const char* dxrpt_last_error(const dxrpt_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
+    if (!ctx) return DXRPT_E_INVALID_ARG;
+    return guarded(ctx, [&] {
+        if (option == DXRPT_OPT_COUNT_TRAVERSAL) {
+            ctx->opt_count = value != 0;
+            if (ctx->opt_count) ctx->d_trav.ensure(4 * sizeof(unsigned long long));
+        } else if (option == DXRPT_OPT_KERNEL_TIMING) {
+            ctx->opt_timing = value != 0;
+        } else {
+            throw ApiError(DXRPT_E_INVALID_ARG, "dxrpt_set_option: unknown option " + std::to_string(option));
+        }
+    });
+}
+
+int dxrpt_reset_timing(dxrpt_ctx* ctx) {
+    if (!ctx) return DXRPT_E_INVALID_ARG;
+    return guarded(ctx, [&] {
+        harvest_all(ctx);
+        for (int k = 0; k < DXRPT_K_COUNT; ++k) {
+            ctx->kernel_ms[k] = 0.0;
+            ctx->kernel_launches[k] = 0;
+        }
+        ctx->timed_frames = 0;
+        ctx->frame_ms = 0.0;
+    });
+}
+
+int dxrpt_set_scene(dxrpt_ctx* ctx, const dxrpt_mesh_vertex* vertices, uint32_t num_vertices, const void* indices,
+                    uint32_t idx_bytes, uint32_t num_indices, const dxrpt_geometry_info* geometries,
+                    uint32_t num_geometries, const dxrpt_material* materials, uint32_t num_materials) {
+    if (!ctx) return DXRPT_E_INVALID_ARG;
+    return guarded(ctx, [&] {
+        require(vertices && indices && geometries && materials, "dxrpt_set_scene: null array");
+        require(idx_bytes == 2 || idx_bytes == 4, "dxrpt_set_scene: idx_bytes must be 2 or 4");
+        require(num_indices % 3 == 0 && num_indices > 0, "dxrpt_set_scene: num_indices must be a positive multiple of 3");
+        require(num_geometries > 0 && num_materials > 0, "dxrpt_set_scene: empty geometry/material table");
+        ctx->vertices.assign(vertices, vertices + num_vertices);
+        ctx->indices.resize(num_indices);
+        if (idx_bytes == 2) {
+            const uint16_t* s = static_cast<const uint16_t*>(indices);
+            for (uint32_t i = 0; i < num_indices; ++i) ctx->indices[i] = s[i];
+        } else {
+            std::memcpy(ctx->indices.data(), indices, size_t(num_indices) * 4);
+        }
+        ctx->geos.assign(geometries, geometries + num_geometries);
+        ctx->mats.assign(materials, materials + num_materials);
+        for (uint32_t g = 0; g < num_geometries; ++g) {
+            const dxrpt_geometry_info& gi = geometries[g];
+            require(gi.IdxOffset % 3 == 0 && gi.IdxOffset < num_indices, "dxrpt_set_scene: bad IdxOffset in geometry " + std::to_string(g));
+            require(gi.MaterialIdx < num_materials, "dxrpt_set_scene: bad MaterialIdx in geometry " + std::to_string(g));
+        }
+        ctx->d_vertices.upload(ctx->vertices.data(), ctx->vertices.size() * sizeof(dxrpt_mesh_vertex));
+        ctx->d_indices.upload(ctx->indices.data(), ctx->indices.size() * 4);
+        ctx->d_geos.upload(ctx->geos.data(), ctx->geos.size() * sizeof(dxrpt_geometry_info));
+        ctx->d_mats.upload(ctx->mats.data(), ctx->mats.size() * sizeof(dxrpt_material));
+        ctx->scene_set = true;
+        ctx->bvh_built = false;
+    });
+}
+
+int dxrpt_add_texture(dxrpt_ctx* ctx, uint32_t w, uint32_t h, uint32_t fmt, const void* texels, uint32_t* out_index) {
+    if (!ctx) return DXRPT_E_INVALID_ARG;
+    return guarded(ctx, [&] {
+        require(texels && w > 0 && h > 0, "dxrpt_add_texture: empty texture");
+        require(w <= 16384 && h <= 16384, "dxrpt_add_texture: texture larger than 16384");
+        require(fmt <= DXRPT_TEX_R8_UNORM, "dxrpt_add_texture: unknown format");
+        TexDesc d;
+        d.offset = uint32_t(ctx->texels.size());
+        d.width = w;
+        d.height = h;
+        d.fmt = fmt;
+        const size_t n = size_t(w) * h;
+        if (fmt == DXRPT_TEX_R8_UNORM) {
+            const size_t words = (n + 3) / 4;
+            size_t at = ctx->texels.size();
+            ctx->texels.resize(at + words, 0u);
+            std::memcpy(ctx->texels.data() + at, texels, n);
+        } else {
+            const uint32_t* s = static_cast<const uint32_t*>(texels);
+            ctx->texels.insert(ctx->texels.end(), s, s + n);
+        }
+        require(ctx->texels.size() < (size_t(1) << 32), "dxrpt_add_texture: texel pool exceeds 2^32 words");
+        if (out_index) *out_index = uint32_t(ctx->texdesc.size());
+        ctx->texdesc.push_back(d);
+        ctx->tex_dirty = true;
+    });
+}
+
+int dxrpt_set_sky(dxrpt_ctx* ctx, const uint16_t* cube, uint32_t res) {
+    if (!ctx) return DXRPT_E_INVALID_ARG;
+    return guarded(ctx, [&] {
+        require(cube && res > 0 && res <= 4096, "dxrpt_set_sky: bad cube");
+        ctx->d_sky.upload(cube, size_t(res) * res * 6 * 4 * sizeof(uint16_t));
+        ctx->sky_res = res;
+        ctx->sky_set = true;
+    });
+}
+
+int dxrpt_build_bvh(dxrpt_ctx* ctx) {
+    if (!ctx) return DXRPT_E_INVALID_ARG;
+    return guarded(ctx, [&] {
+        require(ctx->scene_set, "dxrpt_build_bvh: no scene (call dxrpt_set_scene first)", DXRPT_E_STATE);
+        auto t0 = std::chrono::steady_clock::now();
+        // Global triangle list: gtri = IdxOffset/3 + PrimitiveIndex for every geometry.
+        const uint32_t ntris = uint32_t(ctx->indices.size() / 3);
+        std::vector<uint32_t> tri_geom(ntris, 0xFFFFFFFFu);
+        const uint32_t ng = uint32_t(ctx->geos.size());
+        for (uint32_t g = 0; g < ng; ++g) {
+            uint32_t begin = ctx->geos[g].IdxOffset / 3;
+            uint32_t end = (g + 1 < ng) ? ctx->geos[g + 1].IdxOffset / 3 : ntris;
+            require(end >= begin, "dxrpt_build_bvh: geometries must be sorted by IdxOffset");
+            for (uint32_t t = begin; t < end; ++t) tri_geom[t] = g;
+        }
+        std::vector<float> pos(size_t(ntris) * 9);
+        for (uint32_t t = 0; t < ntris; ++t) {
+            uint32_t g = tri_geom[t];
+            require(g != 0xFFFFFFFFu, "dxrpt_build_bvh: triangle not covered by any geometry");
+            for (int k = 0; k < 3; ++k) {
+                uint32_t vi = ctx->indices[size_t(t) * 3 + k] + ctx->geos[g].VtxOffset;
+                require(vi < ctx->vertices.size(), "dxrpt_build_bvh: index out of range");
+                std::memcpy(&pos[size_t(t) * 9 + k * 3], ctx->vertices[vi].Position, 12);
+            }
+        }
+        BvhBuildResult res;
+        std::string err;
+        if (!build_bvh(pos.data(), ntris, res, err)) throw ApiError(DXRPT_E_INVALID_ARG, err);
+        std::vector<TriRecord> tris(ntris);
+        for (uint32_t i = 0; i < ntris; ++i) {
+            const uint32_t t = res.tri_order[i];
+            const float* v = &pos[size_t(t) * 9];
+            TriRecord& r = tris[i];
+            const uint32_t g = tri_geom[t];
+            const bool opaque = ctx->mats[ctx->geos[g].MaterialIdx].Opacity == DXRPT_INVALID_INDEX;
+            uint32_t flags = opaque ? kTriOpaque : 0u;
+            r.p0[0] = v[0]; r.p0[1] = v[1]; r.p0[2] = v[2];
+            r.p1[0] = v[3] - v[0]; r.p1[1] = v[4] - v[1]; r.p1[2] = v[5] - v[2];
+            r.p2[0] = v[6] - v[0]; r.p2[1] = v[7] - v[1]; r.p2[2] = v[8] - v[2];
+            std::memcpy(&r.p0[3], &t, 4);
+            std::memcpy(&r.p1[3], &g, 4);
+            std::memcpy(&r.p2[3], &flags, 4);
+        }
+        ctx->d_nodes.upload(res.nodes.data(), res.nodes.size() * sizeof(BvhNode));
+        ctx->d_tris.upload(tris.data(), tris.size() * sizeof(TriRecord));
+        auto t1 = std::chrono::steady_clock::now();
+        ctx->bvh.num_nodes = uint32_t(res.nodes.size());
+        ctx->bvh.num_leaves = res.num_leaves;
+        ctx->bvh.num_tris = ntris;
+        ctx->bvh.max_depth = res.max_depth;
+        ctx->bvh.node_bytes = sizeof(BvhNode);
+        ctx->bvh.tri_bytes = sizeof(TriRecord);
+        ctx->bvh.build_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        ctx->bvh.sah_cost = res.sah_cost;
+        ctx->bvh_built = true;
+    });
+}
+
+int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info) {
+    if (!ctx || !info) return DXRPT_E_INVALID_ARG;
+    if (!ctx->bvh_built) return DXRPT_E_STATE;
+    *info = ctx->bvh;
+    return DXRPT_OK;
+}
+
+int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxrpt_app_settings* settings,
+                 const dxrpt_light_constants* lights, float* accum, uint32_t width, uint32_t height,
+                 const dxrpt_tile* tiles, uint32_t num_tiles, void* stream) {
+    if (!ctx) return DXRPT_E_INVALID_ARG;
+    return guarded(ctx, [&] {
+        require(ctx->bvh_built, "dxrpt_render: acceleration structure not built", DXRPT_E_STATE);
+        require(ctx->sky_set, "dxrpt_render: sky cubemap not set", DXRPT_E_STATE);
+        require(rtc && settings && accum, "dxrpt_render: null argument");
+        require(width > 0 && height > 0, "dxrpt_render: empty image");
+        require(uint64_t(width) * height == rtc->TotalNumPixels, "dxrpt_render: TotalNumPixels != width*height");
+        require(settings->SqrtNumSamples >= 1, "dxrpt_render: SqrtNumSamples must be >= 1");
+        require(settings->MaxPathLength >= 1 && settings->MaxPathLength <= int(DXRPT_MAX_PATH_LENGTH),
+                "dxrpt_render: MaxPathLength must be in [1, 8]");
+        const bool useLights = settings->RenderLights && rtc->NumLights > 0;
+        require(!useLights || (lights && rtc->NumLights <= DXRPT_MAX_SPOT_LIGHTS), "dxrpt_render: bad lights");
+        upload_textures(ctx);
+        for (const dxrpt_material& m : ctx->mats) {
+            const uint32_t nt = uint32_t(ctx->texdesc.size());
+            require(m.Albedo < nt && m.Normal < nt && m.Roughness < nt && m.Metallic < nt && m.Emissive < nt &&
+                        (m.Opacity == DXRPT_INVALID_INDEX || m.Opacity < nt),
+                    "dxrpt_render: material references a texture that was not added");
+        }
+        std::vector<dxrpt_tile> tl;
+        if (!tiles || num_tiles == 0) {
+            dxrpt_tile t{};
+            t.x0 = 0; t.y0 = 0; t.w = width; t.h = height; t.accum_offset = 0; t.accum_pitch = width;
+            tl.push_back(t);
+        } else {
+            tl.assign(tiles, tiles + num_tiles);
+        }
+        std::vector<uint32_t> prefix(tl.size() + 1, 0);
+        uint64_t total = 0;
+        for (size_t k = 0; k < tl.size(); ++k) {
+            const dxrpt_tile& t = tl[k];
+            require(t.w > 0 && t.h > 0 && uint64_t(t.x0) + t.w <= width && uint64_t(t.y0) + t.h <= height,
+                    "dxrpt_render: tile " + std::to_string(k) + " outside the image");
+            require(t.accum_pitch >= t.w, "dxrpt_render: tile accum_pitch < width");
+            require(t.accum_offset + uint64_t(t.h - 1) * t.accum_pitch + t.w <= 0xFFFFFFFFull,
+                    "dxrpt_render: accumulation index exceeds 32 bits");
+            prefix[k] = uint32_t(total);
+            total += uint64_t(t.w) * t.h;
+            require(total < 0x7FFFFFFFull, "dxrpt_render: too many pixels in one call");
+        }
+        prefix[tl.size()] = uint32_t(total);
+        const uint32_t paths = uint32_t(total);
+        if (tl.size() != ctx->tiles_cache.size() || std::memcmp(tl.data(), ctx->tiles_cache.data(), tl.size() * sizeof(dxrpt_tile)) != 0) {
+            ctx->d_tiles.upload(tl.data(), tl.size() * sizeof(dxrpt_tile));
+            ctx->d_tile_prefix.upload(prefix.data(), prefix.size() * sizeof(uint32_t));
+            ctx->tiles_cache = tl;
+        }
+        uint32_t nl = useLights ? rtc->NumLights : 0u;
+        if (nl) {
+            std::vector<dxrpt_spot_light> L(lights->Lights, lights->Lights + nl);
+            if (L.size() != ctx->lights_cache.size() || std::memcmp(L.data(), ctx->lights_cache.data(), nl * sizeof(dxrpt_spot_light)) != 0) {
+                ctx->d_lights.upload(L.data(), nl * sizeof(dxrpt_spot_light));
+                ctx->lights_cache = L;
+            }
+        }
+        ensure_frame(ctx, paths, 2u + nl);
+        FrameParams fp;
+        fp.rtc = *rtc;
+        fp.rtc.NumLights = nl;
+        fp.set = *settings;
+        fp.lights = nl ? ctx->d_lights.as<dxrpt_spot_light>() : nullptr;
+        fp.tiles = ctx->d_tiles.as<dxrpt_tile>();
+        fp.tile_prefix = ctx->d_tile_prefix.as<uint32_t>();
+        fp.accum = reinterpret_cast<float4*>(accum);
+        fp.num_tiles = uint32_t(tl.size());
+        fp.num_paths = paths;
+        fp.width = width;
+        fp.height = height;
+        fp.trav = nullptr;
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        if (ctx->opt_count) {
+            fp.trav = ctx->d_trav.as<unsigned long long>();
+            HIP_CHECK(hipMemsetAsync(fp.trav, 0, 4 * sizeof(unsigned long long), s));
+        }
+        const int L = settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength;
+        hipEvent_t* ev = nullptr;
+        if (ctx->opt_timing) {
+            if (ctx->ring.empty()) ctx->ring.resize(64);
+            dxrpt_ctx::FrameEvents& f = ctx->ring[ctx->ring_head];
+            ctx->ring_head = (ctx->ring_head + 1) % ctx->ring.size();
+            harvest(ctx, f);  // recycles the oldest slot (blocks only if it is still in flight)
+            const int need = frame_event_count(L);
+            while (int(f.ev.size()) < need) {
+                hipEvent_t e;
+                HIP_CHECK(hipEventCreate(&e));
+                f.ev.push_back(e);
+            }
+            f.L = L;
+            f.pending = true;
+            ev = f.ev.data();
+        }
+        HIP_CHECK(launch_frame(scene_dev(ctx), ctx->fb, fp, s, ev));
+        ctx->last_stream = s;
+        ctx->last_L = settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength;
+        std::memset(&ctx->last, 0, sizeof(ctx->last));
+        ctx->last.pixels = paths;
+        ctx->last.nominal_rays = uint64_t(paths) * uint64_t(1 + (ctx->last_L - 1) * 2);
+        ctx->rendered = true;
+    });
+}
+
+int dxrpt_get_stats(dxrpt_ctx* ctx, dxrpt_stats* out) {
+    if (!ctx || !out) return DXRPT_E_INVALID_ARG;
+    return guarded(ctx, [&] {
+        require(ctx->rendered, "dxrpt_get_stats: nothing rendered yet", DXRPT_E_STATE);
+        HIP_CHECK(hipStreamSynchronize(ctx->last_stream));
+        uint32_t cnt[32];
+        HIP_CHECK(hipMemcpy(cnt, ctx->fb.counters, sizeof(cnt), hipMemcpyDeviceToHost));
+        dxrpt_stats s = ctx->last;
+        for (int d = 1; d < ctx->last_L && d < int(DXRPT_MAX_PATH_LENGTH); ++d) {
+            s.radiance_rays_per_depth[d] = cnt[d];
+            s.shadow_rays_per_depth[d] = cnt[16 + d];
+            s.radiance_rays += cnt[d];
+            s.shadow_rays += cnt[16 + d];
+        }
+        if (ctx->opt_count && ctx->d_trav.p) {
+            unsigned long long tr[4];
+            HIP_CHECK(hipMemcpy(tr, ctx->d_trav.p, sizeof(tr), hipMemcpyDeviceToHost));
+            s.node_visits_radiance = tr[0];
+            s.tri_tests_radiance = tr[1];
+            s.node_visits_shadow = tr[2];
+            s.tri_tests_shadow = tr[3];
+        }
+        harvest_all(ctx);
+        for (int k = 0; k < DXRPT_K_COUNT; ++k) {
+            s.kernel_ms[k] = ctx->kernel_ms[k];
+            s.kernel_launches[k] = ctx->kernel_launches[k];
+        }
+        s.timed_frames = ctx->timed_frames;
+        s.frame_ms = ctx->frame_ms;
+        *out = s;
+    });
+}
+
+int dxrpt_trace_rays(dxrpt_ctx* ctx, const float* rays, uint32_t num_rays, uint32_t flags, float* hits, void* stream) {
+    if (!ctx) return DXRPT_E_INVALID_ARG;
+    return guarded(ctx, [&] {
+        require(ctx->bvh_built, "dxrpt_trace_rays: acceleration structure not built", DXRPT_E_STATE);
+        require(num_rays == 0 || (rays && hits), "dxrpt_trace_rays: null argument");
+        upload_textures(ctx);
+        HIP_CHECK(launch_trace_rays(scene_dev(ctx), reinterpret_cast<const float4*>(rays), num_rays, flags,
+                                    reinterpret_cast<float4*>(hits), static_cast<hipStream_t>(stream)));
+    });
+}
+
+}  // extern "C"

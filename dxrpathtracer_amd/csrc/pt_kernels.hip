@@ -1,0 +1,680 @@
+// pt_kernels.hip — wavefront path tracer for gfx950 (MI355X).
+//
+// Replaces the recursive DXR pipeline of DXRPathTracer/RayTrace.hlsl (RaygenShader 92-149,
+// PathTrace 151-441, ClosestHit 476-483, AnyHit 485-507, Miss 509-530, ShadowHit/Miss 532-542)
+// with one kernel per stage and depth:
+//
+//   k_raygen        (1 thread / pixel)       CMJ set-0 jitter, unproject, primary ray -> queue[1]
+//   for d = 1 .. MaxPathLength-1:            (d = PathLength of the radiance rays in queue[d])
+//     k_trace       (1 thread / queued ray)  closest hit; alpha-tested any-hit iff d <= MaxAnyHitPathLength
+//     k_shade       (1 thread / queued ray)  miss: sky/sun disc.  hit: PathTrace -> emissive, sun/spot
+//                                            shadow rays with their pending CalcLighting terms, BRDF
+//                                            sample, continuation ray (wave64 ballot compaction into
+//                                            queue[d+1]) or the final sky-visibility ray
+//     k_shadow      (1 thread / queued ray)  any-hit traversal of that ray's shadow rays, adds
+//                                            contribution * visibility to the path's radiance
+//   k_accumulate    (1 thread / pixel)       clamp to FP16Max, lerp into the RGBA32F target
+//
+// Recursion becomes a loop: path throughput (product of the BRDF throughputs of earlier vertices)
+// is carried in the path state so every term can be added to the pixel directly.  Each path owns
+// its pixel's radiance, every add happens in one thread in a fixed order: results are deterministic
+// run to run and independent of the tiling.
+//
+// BVH traversal: BVH2 (pt_layout.h), one ray per lane, short per-lane stack in LDS
+// (kTraversalStack x 4 B x 256 lanes = 32 KiB per workgroup), exact Moller-Trumbore triangle test
+// (same arithmetic as the oracle) behind conservative (padded) slab tests.
+#include <hip/hip_runtime.h>
+
+#include "pt_kernels.h"
+#include "pt_math.h"
+
+namespace dxrpt {
+
+constexpr int kBlock = 256;
+constexpr uint32_t kMiss = 0xFFFFFFFFu;
+constexpr float kRayTMin = 0.00001f;          // RayTrace.hlsl:243, 382
+constexpr float kSpotShadowNearClip = 0.1f;   // AppSettings.hlsl:56
+
+PT_DEV uint32_t fbits(float f) { return __float_as_uint(f); }
+PT_DEV float bitsf(uint32_t u) { return __uint_as_float(u); }
+
+// ---- texture sampling ---------------------------------------------------------------------------
+// SampleLevel(MeshSampler, uv, 0): MeshSampler is anisotropic x16 with WRAP addressing
+// (Graphics/DX12_Helpers.cpp:327-338); at LOD 0 on mip 0 this is defined here as bilinear with
+// wrap, texel centres at (i + 0.5) / size, weights lerp(lerp(t00,t10,fx), lerp(t01,t11,fx), fy).
+PT_DEV int wrap_coord(int i, uint32_t n) {
+    if ((n & (n - 1u)) == 0u) return i & int(n - 1u);
+    int m = i % int(n);
+    return m < 0 ? m + int(n) : m;
+}
+
+struct Texel4 {
+    float r, g, b, a;
+};
+
+PT_DEV Texel4 fetch_texel(const SceneDev& S, const TexDesc& td, int x, int y) {
+    uint32_t idx = uint32_t(y) * td.width + uint32_t(x);
+    Texel4 t;
+    if (td.fmt == DXRPT_TEX_R8_UNORM) {
+        uint32_t w = S.texels[td.offset + (idx >> 2)];
+        float v = S.lut[(w >> ((idx & 3u) * 8u)) & 0xFFu];
+        t.r = v; t.g = v; t.b = v; t.a = 1.0f;
+    } else {
+        uint32_t w = S.texels[td.offset + idx];
+        const float* l = S.lut + (td.fmt == DXRPT_TEX_RGBA8_SRGB ? 256 : 0);
+        t.r = l[w & 0xFFu];
+        t.g = l[(w >> 8) & 0xFFu];
+        t.b = l[(w >> 16) & 0xFFu];
+        t.a = S.lut[w >> 24];
+    }
+    return t;
+}
+
+PT_DEV Texel4 sample_tex(const SceneDev& S, uint32_t texIdx, float u, float v) {
+    const TexDesc td = S.texdesc[texIdx];
+    float x = u * float(td.width) - 0.5f;
+    float y = v * float(td.height) - 0.5f;
+    float x0 = floorf(x), y0 = floorf(y);
+    float fx = x - x0, fy = y - y0;
+    int ix0 = wrap_coord(int(x0), td.width), ix1 = wrap_coord(int(x0) + 1, td.width);
+    int iy0 = wrap_coord(int(y0), td.height), iy1 = wrap_coord(int(y0) + 1, td.height);
+    Texel4 t00 = fetch_texel(S, td, ix0, iy0), t10 = fetch_texel(S, td, ix1, iy0);
+    Texel4 t01 = fetch_texel(S, td, ix0, iy1), t11 = fetch_texel(S, td, ix1, iy1);
+    Texel4 r;
+    r.r = lerpf(lerpf(t00.r, t10.r, fx), lerpf(t01.r, t11.r, fx), fy);
+    r.g = lerpf(lerpf(t00.g, t10.g, fx), lerpf(t01.g, t11.g, fx), fy);
+    r.b = lerpf(lerpf(t00.b, t10.b, fx), lerpf(t01.b, t11.b, fx), fy);
+    r.a = lerpf(lerpf(t00.a, t10.a, fx), lerpf(t01.a, t11.a, fx), fy);
+    return r;
+}
+
+// Sky cube SampleLevel(LinearSampler, dir, 0) (RayTrace.hlsl:434, 521): LinearSampler is
+// linear/clamp (DX12_Helpers.cpp:282-293).  Defined here as: D3D major-axis face selection (ties
+// resolve x before y before z), bilinear within the face, clamped to the face edge.
+PT_DEV float half_to_float(uint16_t h) { return float(__builtin_bit_cast(_Float16, h)); }
+
+PT_DEV f3 sample_sky(const SceneDev& S, f3 d) {
+    float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    int face;
+    float ma, sc, tc;
+    if (ax >= ay && ax >= az) {
+        face = d.x >= 0.0f ? 0 : 1; ma = ax; sc = d.x >= 0.0f ? -d.z : d.z; tc = -d.y;
+    } else if (ay >= az) {
+        face = d.y >= 0.0f ? 2 : 3; ma = ay; sc = d.x; tc = d.y >= 0.0f ? d.z : -d.z;
+    } else {
+        face = d.z >= 0.0f ? 4 : 5; ma = az; sc = d.z >= 0.0f ? d.x : -d.x; tc = -d.y;
+    }
+    const float res = float(S.sky_res);
+    float u = (sc / ma + 1.0f) * 0.5f;
+    float v = (tc / ma + 1.0f) * 0.5f;
+    float x = u * res - 0.5f, y = v * res - 0.5f;
+    float x0 = floorf(x), y0 = floorf(y);
+    float fx = x - x0, fy = y - y0;
+    const int rmax = int(S.sky_res) - 1;
+    int ix0 = min(max(int(x0), 0), rmax), ix1 = min(max(int(x0) + 1, 0), rmax);
+    int iy0 = min(max(int(y0), 0), rmax), iy1 = min(max(int(y0) + 1, 0), rmax);
+    const uint16_t* base = S.sky + size_t(face) * S.sky_res * S.sky_res * 4u;
+    const ushort4* t = reinterpret_cast<const ushort4*>(base);
+    ushort4 a = t[iy0 * S.sky_res + ix0], b = t[iy0 * S.sky_res + ix1];
+    ushort4 c = t[iy1 * S.sky_res + ix0], e = t[iy1 * S.sky_res + ix1];
+    f3 r;
+    r.x = lerpf(lerpf(half_to_float(a.x), half_to_float(b.x), fx), lerpf(half_to_float(c.x), half_to_float(e.x), fx), fy);
+    r.y = lerpf(lerpf(half_to_float(a.y), half_to_float(b.y), fx), lerpf(half_to_float(c.y), half_to_float(e.y), fx), fy);
+    r.z = lerpf(lerpf(half_to_float(a.z), half_to_float(b.z), fx), lerpf(half_to_float(c.z), half_to_float(e.z), fx), fy);
+    return r;
+}
+
+// ---- hit surface (RayTrace.hlsl:444-474, Shaders/RayTracing.hlsl:43-53) --------------------------
+struct Surface {
+    f3 pos, n, t, b;
+    float u, v;
+};
+
+PT_DEV float bary_lerp(float a, float b, float c, float w0, float w1, float w2) { return (a * w0 + b * w1) + c * w2; }
+
+PT_DEV Surface get_hit_surface(const SceneDev& S, uint32_t geom, uint32_t gtri, float b1, float b2) {
+    const dxrpt_geometry_info gi = S.geoinfo[geom];
+    const float w0 = (1.0f - b1) - b2;
+    const uint32_t base = gtri * 3u;  // == PrimitiveIndex()*3 + IdxOffset
+    const float4* V = reinterpret_cast<const float4*>(S.vertices);
+    float4 q[3][4];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t vi = S.indices[base + k] + gi.VtxOffset;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[k][j] = V[size_t(vi) * 4 + j];
+    }
+    // MeshVertex layout: q[.][0] = pos.xyz, n.x ; [1] = n.yz, uv ; [2] = t.xyz, b.x ; [3] = b.yz, lmuv
+    Surface s;
+    s.pos = f3{bary_lerp(q[0][0].x, q[1][0].x, q[2][0].x, w0, b1, b2), bary_lerp(q[0][0].y, q[1][0].y, q[2][0].y, w0, b1, b2),
+               bary_lerp(q[0][0].z, q[1][0].z, q[2][0].z, w0, b1, b2)};
+    s.n = normalize3(f3{bary_lerp(q[0][0].w, q[1][0].w, q[2][0].w, w0, b1, b2), bary_lerp(q[0][1].x, q[1][1].x, q[2][1].x, w0, b1, b2),
+                        bary_lerp(q[0][1].y, q[1][1].y, q[2][1].y, w0, b1, b2)});
+    s.u = bary_lerp(q[0][1].z, q[1][1].z, q[2][1].z, w0, b1, b2);
+    s.v = bary_lerp(q[0][1].w, q[1][1].w, q[2][1].w, w0, b1, b2);
+    s.t = normalize3(f3{bary_lerp(q[0][2].x, q[1][2].x, q[2][2].x, w0, b1, b2), bary_lerp(q[0][2].y, q[1][2].y, q[2][2].y, w0, b1, b2),
+                        bary_lerp(q[0][2].z, q[1][2].z, q[2][2].z, w0, b1, b2)});
+    s.b = normalize3(f3{bary_lerp(q[0][2].w, q[1][2].w, q[2][2].w, w0, b1, b2), bary_lerp(q[0][3].x, q[1][3].x, q[2][3].x, w0, b1, b2),
+                        bary_lerp(q[0][3].y, q[1][3].y, q[2][3].y, w0, b1, b2)});
+    return s;
+}
+
+// AnyHitShader / ShadowAnyHitShader (RayTrace.hlsl:485-507): opacity.x < 0.35 -> IgnoreHit.
+PT_DEV bool alpha_accepts(const SceneDev& S, uint32_t geom, uint32_t gtri, float b1, float b2) {
+    const dxrpt_geometry_info gi = S.geoinfo[geom];
+    const uint32_t opacity = S.materials[gi.MaterialIdx].Opacity;
+    if (opacity == DXRPT_INVALID_INDEX) return true;
+    const float w0 = (1.0f - b1) - b2;
+    const uint32_t base = gtri * 3u;
+    const float2* V = reinterpret_cast<const float2*>(S.vertices);
+    float2 uv[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) uv[k] = V[size_t(S.indices[base + k] + gi.VtxOffset) * 8 + 3];  // float2 #3 = UV
+    float u = bary_lerp(uv[0].x, uv[1].x, uv[2].x, w0, b1, b2);
+    float v = bary_lerp(uv[0].y, uv[1].y, uv[2].y, w0, b1, b2);
+    return !(sample_tex(S, opacity, u, v).r < 0.35f);
+}
+
+// ---- traversal ------------------------------------------------------------------------------------
+// Moller-Trumbore, two-sided (no culling flags are set in the reference, Timing.txt:3).  The
+// arithmetic below is bit-identical to oracle/oracle.cpp:intersect_triangle.
+PT_DEV bool intersect_triangle(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float* t, float* u, float* v) {
+    f3 pvec = cross3(d, e2);
+    float det = dot3(e1, pvec);
+    if (det == 0.0f) return false;
+    float inv = 1.0f / det;
+    f3 tvec = sub(o, v0);
+    float uu = dot3(tvec, pvec) * inv;
+    if (uu < 0.0f || uu > 1.0f) return false;
+    f3 qvec = cross3(tvec, e1);
+    float vv = dot3(d, qvec) * inv;
+    if (vv < 0.0f || uu + vv > 1.0f) return false;
+    *t = dot3(e2, qvec) * inv;
+    *u = uu;
+    *v = vv;
+    return true;
+}
+
+struct HitRec {
+    float t, b1, b2;
+    uint32_t tri;   // global triangle id, kMiss if none
+    uint32_t geom;
+};
+
+// kAnyHit: shadow ray semantics (ACCEPT_FIRST_HIT_AND_END_SEARCH): returns true on the first
+// accepted hit.  Otherwise closest hit: smallest t, ties -> smallest global triangle id.
+template <bool kAnyHit, bool kCount>
+PT_DEV bool traverse(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, int* stk, HitRec& h,
+                     uint32_t& nvisit, uint32_t& ntest) {
+    f3 inv;
+    inv.x = 1.0f / (fabsf(d.x) > 1e-20f ? d.x : copysignf(1e-20f, d.x));
+    inv.y = 1.0f / (fabsf(d.y) > 1e-20f ? d.y : copysignf(1e-20f, d.y));
+    inv.z = 1.0f / (fabsf(d.z) > 1e-20f ? d.z : copysignf(1e-20f, d.z));
+    const f3 ood = mul(o, inv);
+    h.t = tmax;
+    h.tri = kMiss;
+    h.b1 = h.b2 = 0.0f;
+    h.geom = 0;
+    int node = 0;
+    int sp = 0;
+    const float4* N = reinterpret_cast<const float4*>(S.nodes);
+    while (true) {
+        while (node >= 0) {
+            if (kCount) ++nvisit;
+            const float4 a = N[node * 4 + 0];
+            const float4 b = N[node * 4 + 1];
+            const float4 c = N[node * 4 + 2];
+            const int4 ch = reinterpret_cast<const int4*>(N)[node * 4 + 3];
+            const float tmx = h.t;
+            float l0x = __builtin_fmaf(a.x, inv.x, -ood.x), h0x = __builtin_fmaf(a.y, inv.x, -ood.x);
+            float l0y = __builtin_fmaf(a.z, inv.y, -ood.y), h0y = __builtin_fmaf(a.w, inv.y, -ood.y);
+            float l0z = __builtin_fmaf(c.x, inv.z, -ood.z), h0z = __builtin_fmaf(c.y, inv.z, -ood.z);
+            float l1x = __builtin_fmaf(b.x, inv.x, -ood.x), h1x = __builtin_fmaf(b.y, inv.x, -ood.x);
+            float l1y = __builtin_fmaf(b.z, inv.y, -ood.y), h1y = __builtin_fmaf(b.w, inv.y, -ood.y);
+            float l1z = __builtin_fmaf(c.z, inv.z, -ood.z), h1z = __builtin_fmaf(c.w, inv.z, -ood.z);
+            float n0 = fmaxf(fmaxf(fminf(l0x, h0x), fminf(l0y, h0y)), fmaxf(fminf(l0z, h0z), tmin));
+            float f0 = fminf(fminf(fmaxf(l0x, h0x), fmaxf(l0y, h0y)), fminf(fmaxf(l0z, h0z), tmx));
+            float n1 = fmaxf(fmaxf(fminf(l1x, h1x), fminf(l1y, h1y)), fmaxf(fminf(l1z, h1z), tmin));
+            float f1 = fminf(fminf(fmaxf(l1x, h1x), fmaxf(l1y, h1y)), fminf(fmaxf(l1z, h1z), tmx));
+            const bool hit0 = n0 <= f0, hit1 = n1 <= f1;
+            if (hit0 && hit1) {
+                int first = ch.x, second = ch.y;
+                if (n1 < n0) { first = ch.y; second = ch.x; }
+                stk[sp * kBlock] = second;
+                ++sp;
+                node = first;
+            } else if (hit0 || hit1) {
+                node = hit0 ? ch.x : ch.y;
+            } else {
+                if (sp == 0) return kAnyHit ? false : h.tri != kMiss;
+                --sp;
+                node = stk[sp * kBlock];
+            }
+        }
+        // leaf
+        const uint32_t code = ~uint32_t(node);
+        const uint32_t first = code >> 3, count = (code & 7u) + 1u;
+        const float4* T = reinterpret_cast<const float4*>(S.tris);
+        for (uint32_t k = 0; k < count; ++k) {
+            if (kCount) ++ntest;
+            const float4 p0 = T[(first + k) * 3 + 0];
+            const float4 p1 = T[(first + k) * 3 + 1];
+            const float4 p2 = T[(first + k) * 3 + 2];
+            float t, u, v;
+            if (!intersect_triangle(o, d, ld3(p0), ld3(p1), ld3(p2), &t, &u, &v)) continue;
+            const uint32_t gtri = fbits(p0.w);
+            if (!(t >= tmin)) continue;
+            if (kAnyHit) {
+                if (!(t <= tmax)) continue;
+            } else {
+                if (!(t < h.t || (t == h.t && gtri < h.tri))) continue;
+            }
+            const uint32_t geom = fbits(p1.w);
+            if (alpha && !(fbits(p2.w) & kTriOpaque) && !alpha_accepts(S, geom, gtri, u, v)) continue;
+            if (kAnyHit) return true;
+            h.t = t;
+            h.tri = gtri;
+            h.b1 = u;
+            h.b2 = v;
+            h.geom = geom;
+        }
+        if (sp == 0) return kAnyHit ? false : h.tri != kMiss;
+        --sp;
+        node = stk[sp * kBlock];
+    }
+}
+
+// ---- kernels --------------------------------------------------------------------------------------
+struct KArgs {
+    SceneDev S;
+    FrameBuffers F;
+    FrameParams P;
+};
+
+// RaygenShader, RayTrace.hlsl:92-126 (+ SamplePoint 85-90)
+__global__ __launch_bounds__(kBlock) void k_raygen(KArgs A) {
+    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= A.P.num_paths) return;
+    // path slot -> tile (binary search over the prefix table) -> pixel
+    uint32_t lo = 0, hi = A.P.num_tiles;
+    while (hi - lo > 1u) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (A.P.tile_prefix[mid] <= p) lo = mid; else hi = mid;
+    }
+    const dxrpt_tile tl = A.P.tiles[lo];
+    const uint32_t local = p - A.P.tile_prefix[lo];
+    const uint32_t lx = local % tl.w, ly = local / tl.w;
+    const uint32_t x = tl.x0 + lx, y = tl.y0 + ly;
+    const uint32_t pixelIdx = y * A.P.width + x;
+    const uint32_t accumIdx = uint32_t(tl.accum_offset) + ly * tl.accum_pitch + lx;
+
+    const uint32_t nS = uint32_t(A.P.set.SqrtNumSamples);
+    float sx, sy;
+    sample_cmj2d(A.P.rtc.CurrSampleIdx, nS, nS, 0u * A.P.rtc.TotalNumPixels + pixelIdx, &sx, &sy);
+    const float px = float(x) + sx, py = float(y) + sy;
+    float ncx = px / (float(A.P.width) * 0.5f) - 1.0f;
+    float ncy = py / (float(A.P.height) * 0.5f) - 1.0f;
+    ncy *= -1.0f;
+    const float* M = A.P.rtc.InvViewProjection;
+    float s[4], e[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        s[j] = ((ncx * M[0 * 4 + j] + ncy * M[1 * 4 + j]) + 0.0f * M[2 * 4 + j]) + 1.0f * M[3 * 4 + j];
+        e[j] = ((ncx * M[0 * 4 + j] + ncy * M[1 * 4 + j]) + 1.0f * M[2 * 4 + j]) + 1.0f * M[3 * 4 + j];
+    }
+    const f3 start = f3{s[0] / s[3], s[1] / s[3], s[2] / s[3]};
+    const f3 end = f3{e[0] / e[3], e[1] / e[3], e[2] / e[3]};
+    const f3 diff = sub(end, start);
+    const f3 dir = normalize3(diff);
+    const float rayLength = len3(diff);
+    A.F.q_org[1][p] = make_float4(start.x, start.y, start.z, rayLength);
+    A.F.q_dir[1][p] = make_float4(dir.x, dir.y, dir.z, bitsf(p));
+    A.F.ps_thr[p] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+    A.F.ps_rad[p] = make_float4(0.0f, 0.0f, 0.0f, bitsf(0u));
+    A.F.ps_pix[p] = make_uint2(pixelIdx, accumIdx);
+    if (p == 0) A.F.counters[1] = A.P.num_paths;
+}
+
+template <bool kCount>
+__global__ __launch_bounds__(kBlock) void k_trace(KArgs A, int depth) {
+    __shared__ int stack[kTraversalStack * kBlock];
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= A.F.counters[depth]) return;
+    const float4 o4 = A.F.q_org[depth & 1][i];
+    const float4 d4 = A.F.q_dir[depth & 1][i];
+    // Primary rays start at TMin 0 (RayTrace.hlsl:118); continuation rays at 1e-5 (:382).
+    const float tmin = depth == 1 ? 0.0f : kRayTMin;
+    // RAY_FLAG_FORCE_OPAQUE iff PathLength > MaxAnyHitPathLength (RayTrace.hlsl:132, 401)
+    const bool alpha = depth <= A.P.set.MaxAnyHitPathLength;
+    HitRec h;
+    uint32_t nv = 0, nt = 0;
+    traverse<false, kCount>(A.S, ld3(o4), ld3(d4), tmin, o4.w, alpha, stack + threadIdx.x, h, nv, nt);
+    A.F.hit[i] = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
+    if (kCount) {
+        atomicAdd(&A.P.trav[0], (unsigned long long)nv);
+        atomicAdd(&A.P.trav[1], (unsigned long long)nt);
+    }
+}
+
+PT_DEV void emit_shadow(const KArgs& A, uint32_t i, uint32_t& n, f3 o, f3 d, float tmin, float tmax, f3 contrib,
+                        uint32_t pathSlot, bool forceOpaque) {
+    const size_t s = size_t(n) * A.F.capacity + i;
+    A.F.sh_org[s] = make_float4(o.x, o.y, o.z, tmax);
+    A.F.sh_dir[s] = make_float4(d.x, d.y, d.z, tmin);
+    A.F.sh_con[s] = make_float4(contrib.x, contrib.y, contrib.z, bitsf((pathSlot << 1) | (forceOpaque ? 1u : 0u)));
+    ++n;
+}
+
+PT_DEV bool nonzero3(f3 c) { return !(c.x == 0.0f && c.y == 0.0f && c.z == 0.0f); }
+
+// MissShader (RayTrace.hlsl:509-530) and ClosestHitShader -> PathTrace (151-441)
+__global__ __launch_bounds__(kBlock) void k_shade(KArgs A, int depth) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= A.F.counters[depth]) return;
+    const dxrpt_app_settings& set = A.P.set;
+    const dxrpt_ray_trace_constants& rtc = A.P.rtc;
+    const float4 o4 = A.F.q_org[depth & 1][i];
+    const float4 d4 = A.F.q_dir[depth & 1][i];
+    const uint32_t pathSlot = fbits(d4.w);
+    const float4 hit = A.F.hit[i];
+    const float4 thr4 = A.F.ps_thr[pathSlot];
+    float4 rad4 = A.F.ps_rad[pathSlot];
+    const f3 pathThr = ld3(thr4);
+    const f3 inDir = ld3(d4);
+    const f3 inOrigin = ld3(o4);
+    const bool furnace = set.EnableWhiteFurnaceMode != 0;
+    uint32_t nsh = 0;
+    bool cont = false;
+    f3 local = f3{0.0f, 0.0f, 0.0f};
+    f3 nextThr = f3{0.0f, 0.0f, 0.0f};
+    f3 nextOrigin = f3{0.0f, 0.0f, 0.0f}, nextDir = f3{0.0f, 0.0f, 0.0f};
+    float nextRoughness = 0.0f;
+    bool nextIsDiffuse = false;
+    const uint32_t tri = fbits(hit.z);
+
+    if (tri == kMiss) {
+        // MissShader
+        if (furnace) {
+            local = f3{1.0f, 1.0f, 1.0f};
+        } else {
+            local = set.EnableSky ? sample_sky(A.S, inDir) : f3{0.0f, 0.0f, 0.0f};
+            if (depth == 1) {
+                float cosSunAngle = dot3(inDir, f3{rtc.SunDirectionWS[0], rtc.SunDirectionWS[1], rtc.SunDirectionWS[2]});
+                if (cosSunAngle >= rtc.CosSunAngularRadius)
+                    local = f3{rtc.SunRenderColor[0], rtc.SunRenderColor[1], rtc.SunRenderColor[2]};
+            }
+        }
+    } else do {
+        // PathTrace early outs (RayTrace.hlsl:153-158): local radiance 0, the path ends.
+        if ((!set.EnableDiffuse && !set.EnableSpecular) || (!set.EnableDirect && !set.EnableIndirect)) break;
+        if (depth > 1 && !set.EnableIndirect) break;
+        const uint32_t geom = fbits(hit.w);
+        const Surface surf = get_hit_surface(A.S, geom, tri, hit.x, hit.y);
+        const dxrpt_material mat = A.S.materials[A.S.geoinfo[geom].MaterialIdx];
+        const f3 T = surf.t, Bt = surf.b;
+        f3 Nrow = surf.n;
+        const f3 positionWS = surf.pos;
+        f3 normalWS = surf.n;
+        if (set.EnableNormalMaps) {
+            Texel4 nm = sample_tex(A.S, mat.Normal, surf.u, surf.v);
+            f3 nts;
+            nts.x = nm.r * 2.0f - 1.0f;
+            nts.y = nm.g * 2.0f - 1.0f;
+            nts.z = sqrtf(1.0f - saturate(nts.x * nts.x + nts.y * nts.y));
+            normalWS = normalize3(add(add(scl(T, nts.x), scl(Bt, nts.y)), scl(surf.n, nts.z)));
+            Nrow = normalWS;
+        }
+        f3 baseColor = f3{1.0f, 1.0f, 1.0f};
+        if (set.EnableAlbedoMaps && !furnace) {
+            Texel4 a = sample_tex(A.S, mat.Albedo, surf.u, surf.v);
+            baseColor = f3{a.r, a.g, a.b};
+        }
+        const float metallic = saturate((furnace ? 1.0f : sample_tex(A.S, mat.Metallic, surf.u, surf.v).r) * set.MetallicScale);
+        const bool enableDiffuse = (set.EnableDiffuse && metallic < 1.0f) || furnace;
+        const bool payloadIsDiffuse = (fbits(rad4.w) & 1u) != 0u;
+        const bool enableSpecular =
+            set.EnableSpecular && (set.EnableIndirectSpecular ? !(set.AvoidCausticPaths && payloadIsDiffuse) : (depth == 1));
+        if (!enableDiffuse && !enableSpecular) break;
+        const float sqrtRoughness = saturate((furnace ? 1.0f : sample_tex(A.S, mat.Roughness, surf.u, surf.v).r) * set.RoughnessScale);
+        const float dsel = enableDiffuse ? 1.0f : 0.0f, ssel = enableSpecular ? 1.0f : 0.0f;
+        const f3 diffuseAlbedo = scl(f3{lerpf(baseColor.x, 0.0f, metallic), lerpf(baseColor.y, 0.0f, metallic), lerpf(baseColor.z, 0.0f, metallic)}, dsel);
+        const f3 specularAlbedo = scl(f3{lerpf(0.03f, baseColor.x, metallic), lerpf(0.03f, baseColor.y, metallic), lerpf(0.03f, baseColor.z, metallic)}, ssel);
+        float roughness = sqrtRoughness * sqrtRoughness;
+        if (set.ClampRoughness) roughness = fmaxf(roughness, thr4.w);
+        f3 msEC = f3{1.0f, 1.0f, 1.0f};
+        if (set.ApplyMultiscatteringEnergyCompensation) {
+            const float Ess = ggx_env_brdf_scale(saturate(dot3(normalWS, neg(inDir))), sqrtRoughness);
+            const float k = 1.0f / Ess - 1.0f;
+            msEC = f3{1.0f + specularAlbedo.x * k, 1.0f + specularAlbedo.y * k, 1.0f + specularAlbedo.z * k};
+        }
+        if (!furnace) {
+            Texel4 em = sample_tex(A.S, mat.Emissive, surf.u, surf.v);
+            local = f3{em.r, em.g, em.b};
+        }
+        const bool directZero = (depth == 1 && !set.EnableDirect);  // RayTrace.hlsl:385-386
+        const bool shadowOpaque = depth > set.MaxAnyHitPathLength;
+        // Sun (RayTrace.hlsl:224-262)
+        if (set.EnableSun && !furnace && !directZero) {
+            const f3 D = f3{rtc.SunDirectionWS[0], rtc.SunDirectionWS[1], rtc.SunDirectionWS[2]};
+            f3 sunDirection = D;
+            if (set.SunAreaLightApproximation) {
+                const f3 R = reflect3(inDir, normalWS);
+                const float r = rtc.SinSunAngularRadius;
+                const float dd = rtc.CosSunAngularRadius;
+                const float DDotR = dot3(D, R);
+                const f3 Sv = sub(R, scl(D, DDotR));
+                sunDirection = DDotR < dd ? normalize3(add(scl(D, dd), scl(normalize3(Sv), r))) : R;
+            }
+            const f3 c = calc_lighting(normalWS, sunDirection, f3{rtc.SunIrradiance[0], rtc.SunIrradiance[1], rtc.SunIrradiance[2]},
+                                       diffuseAlbedo, specularAlbedo, roughness, positionWS, inOrigin, msEC);
+            if (nonzero3(c))
+                emit_shadow(A, i, nsh, positionWS, D, kRayTMin, kFP32Max, mul(pathThr, c), pathSlot, shadowOpaque);
+        }
+        // Spot lights (RayTrace.hlsl:265-313)
+        if (set.RenderLights && !furnace && !directZero) {
+            for (uint32_t l = 0; l < rtc.NumLights; ++l) {
+                const dxrpt_spot_light sl = A.P.lights[l];
+                const f3 lp = f3{sl.Position[0], sl.Position[1], sl.Position[2]};
+                f3 surfaceToLight = sub(lp, positionWS);
+                const float distanceToLight = len3(surfaceToLight);
+                surfaceToLight = f3{surfaceToLight.x / distanceToLight, surfaceToLight.y / distanceToLight, surfaceToLight.z / distanceToLight};
+                const float angleFactor = saturate(dot3(surfaceToLight, f3{sl.Direction[0], sl.Direction[1], sl.Direction[2]}));
+                float angularAttenuation = smoothstepf(sl.AngularAttenuationY, sl.AngularAttenuationX, angleFactor);
+                const float dn = distanceToLight / sl.Range;
+                float falloff = saturate(1.0f - (dn * dn * dn * dn));
+                falloff = (falloff * falloff) / (distanceToLight * distanceToLight + 1.0f);
+                angularAttenuation *= falloff;
+                if (angularAttenuation > 0.0f) {
+                    const f3 intensity = scl(f3{sl.Intensity[0], sl.Intensity[1], sl.Intensity[2]}, angularAttenuation);
+                    const f3 c = calc_lighting(normalWS, surfaceToLight, intensity, diffuseAlbedo, specularAlbedo, roughness,
+                                               positionWS, inOrigin, msEC);
+                    if (nonzero3(c))
+                        emit_shadow(A, i, nsh, add(positionWS, scl(normalWS, 0.01f)), surfaceToLight, kSpotShadowNearClip,
+                                    distanceToLight - kSpotShadowNearClip, mul(pathThr, c), pathSlot, shadowOpaque);
+                }
+            }
+        }
+        if (directZero) local = f3{0.0f, 0.0f, 0.0f};
+        // BRDF importance sampling (RayTrace.hlsl:315-376); sample set = PathLength
+        float bx, by;
+        sample_cmj2d(rtc.CurrSampleIdx, uint32_t(set.SqrtNumSamples), uint32_t(set.SqrtNumSamples),
+                     uint32_t(depth) * rtc.TotalNumPixels + A.F.ps_pix[pathSlot].x, &bx, &by);
+        f3 throughput, rayDirTS;
+        float selector = bx;
+        if (!enableSpecular) selector = 0.0f;
+        else if (!enableDiffuse) selector = 1.0f;
+        if (selector < 0.5f) {
+            if (enableSpecular) bx *= 2.0f;
+            rayDirTS = sample_cosine_hemisphere(bx, by);
+            throughput = diffuseAlbedo;
+        } else {
+            if (enableDiffuse) bx = (bx - 0.5f) * 2.0f;
+            const f3 inTS = normalize3(f3{dot3(inDir, T), dot3(inDir, Bt), dot3(inDir, Nrow)});
+            const f3 mTS = sample_ggx_visible_normal(neg(inTS), roughness, roughness, bx, by);
+            const f3 sampleDirTS = reflect3(inTS, mTS);
+            const f3 F = furnace ? f3{1.0f, 1.0f, 1.0f} : fresnel(specularAlbedo, mTS, sampleDirTS);
+            const float a2 = roughness * roughness;
+            const float G1 = smith_ggx_masking(-inTS.z, a2);
+            const float G2 = smith_ggx_masking_shadowing(sampleDirTS.z, -inTS.z, a2);
+            throughput = scl(F, G2 / G1);
+            rayDirTS = sampleDirTS;
+            if (set.ApplyMultiscatteringEnergyCompensation) {
+                // dot(normalTS, -incomingRayDirWS): the reference mixes spaces here (RayTrace.hlsl:361)
+                const float Ess = ggx_env_brdf_scale(saturate(-inDir.z), sqrtRoughness);
+                const float k = 1.0f / Ess - 1.0f;
+                throughput = mul(throughput, f3{1.0f + specularAlbedo.x * k, 1.0f + specularAlbedo.y * k, 1.0f + specularAlbedo.z * k});
+            }
+        }
+        const f3 rayDirWS = normalize3(add(add(scl(T, rayDirTS.x), scl(Bt, rayDirTS.y)), scl(Nrow, rayDirTS.z)));
+        if (enableDiffuse && enableSpecular) throughput = scl(throughput, 2.0f);
+        if (set.EnableIndirect && (depth + 1 < set.MaxPathLength) && !furnace) {
+            cont = true;
+            nextThr = mul(pathThr, throughput);
+            nextOrigin = positionWS;
+            nextDir = rayDirWS;
+            nextRoughness = roughness;
+            nextIsDiffuse = selector < 0.5f;
+        } else if (furnace) {
+            local = throughput;  // RayTrace.hlsl:427-430 (visibility unused)
+        } else {
+            const f3 sky = set.EnableSky ? sample_sky(A.S, rayDirWS) : f3{0.0f, 0.0f, 0.0f};
+            const f3 c = mul(sky, throughput);
+            if (nonzero3(c))
+                emit_shadow(A, i, nsh, positionWS, rayDirWS, kRayTMin, kFP32Max, mul(pathThr, c), pathSlot, depth + 1 > set.MaxAnyHitPathLength);
+        }
+    } while (false);
+
+    // Always add (also when zero): keeps NaN/inf propagation identical to the recursive form.
+    rad4.x += pathThr.x * local.x;
+    rad4.y += pathThr.y * local.y;
+    rad4.z += pathThr.z * local.z;
+    if (cont) rad4.w = bitsf(nextIsDiffuse ? 1u : 0u);  // payload.IsDiffuse for the next vertex
+    A.F.ps_rad[pathSlot] = rad4;
+    A.F.sh_n[i] = nsh;
+
+    // wave64 compaction of continuation rays into queue[depth+1]
+    const unsigned long long active = __ballot(1);
+    const unsigned long long m = __ballot(cont);
+    const int lane = __lane_id();
+    const int leader = __ffsll(static_cast<long long>(active)) - 1;
+    uint32_t base = 0;
+    if (lane == leader && m != 0ull) base = atomicAdd(&A.F.counters[depth + 1], uint32_t(__popcll(m)));
+    base = __shfl(base, leader);
+    if (cont) {
+        const uint32_t off = base + uint32_t(__popcll(m & ((1ull << lane) - 1ull)));
+        A.F.q_org[(depth + 1) & 1][off] = make_float4(nextOrigin.x, nextOrigin.y, nextOrigin.z, kFP32Max);
+        A.F.q_dir[(depth + 1) & 1][off] = make_float4(nextDir.x, nextDir.y, nextDir.z, bitsf(pathSlot));
+        A.F.ps_thr[pathSlot] = make_float4(nextThr.x, nextThr.y, nextThr.z, nextRoughness);
+    }
+}
+
+// ShadowHitShader / ShadowMissShader / ShadowAnyHitShader (RayTrace.hlsl:497-507, 532-542)
+template <bool kCount>
+__global__ __launch_bounds__(kBlock) void k_shadow(KArgs A, int depth) {
+    __shared__ int stack[kTraversalStack * kBlock];
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= A.F.counters[depth]) return;
+    const uint32_t n = A.F.sh_n[i];
+    if (n == 0) return;
+    uint32_t pathSlot = 0;
+    uint32_t nv = 0, nt = 0;
+    f3 acc = f3{0.0f, 0.0f, 0.0f};
+    for (uint32_t k = 0; k < n; ++k) {
+        const size_t s = size_t(k) * A.F.capacity + i;
+        const float4 o4 = A.F.sh_org[s];
+        const float4 d4 = A.F.sh_dir[s];
+        const float4 c4 = A.F.sh_con[s];
+        const uint32_t tag = fbits(c4.w);
+        pathSlot = tag >> 1;
+        HitRec h;
+        const bool occluded =
+            traverse<true, kCount>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, (tag & 1u) == 0u, stack + threadIdx.x, h, nv, nt);
+        const float vis = occluded ? 0.0f : 1.0f;
+        acc = add(acc, scl(ld3(c4), vis));
+    }
+    atomicAdd(&A.F.counters[16 + depth], n);
+    if (kCount) {
+        atomicAdd(&A.P.trav[2], (unsigned long long)nv);
+        atomicAdd(&A.P.trav[3], (unsigned long long)nt);
+    }
+    float4 r = A.F.ps_rad[pathSlot];
+    r.x += acc.x;
+    r.y += acc.y;
+    r.z += acc.z;
+    A.F.ps_rad[pathSlot] = r;
+}
+
+// RayTrace.hlsl:140-148
+__global__ __launch_bounds__(kBlock) void k_accumulate(KArgs A) {
+    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= A.P.num_paths) return;
+    const float4 r = A.F.ps_rad[p];
+    const uint32_t a = A.F.ps_pix[p].y;
+    const float rx = fminf(fmaxf(r.x, 0.0f), kFP16Max);
+    const float ry = fminf(fmaxf(r.y, 0.0f), kFP16Max);
+    const float rz = fminf(fmaxf(r.z, 0.0f), kFP16Max);
+    const float s = float(A.P.rtc.CurrSampleIdx);
+    const float f = s / (s + 1.0f);
+    const float4 cur = A.P.accum[a];
+    A.P.accum[a] = make_float4(lerpf(rx, cur.x, f), lerpf(ry, cur.y, f), lerpf(rz, cur.z, f), 1.0f);
+}
+
+// Arbitrary ray queries (dxrpt_trace_rays): flags bit0 = any-hit (shadow) semantics,
+// bit1 = alpha test enabled (not FORCE_OPAQUE).
+__global__ __launch_bounds__(kBlock) void k_trace_rays(SceneDev S, const float4* rays, uint32_t n, uint32_t flags, float4* hits) {
+    __shared__ int stack[kTraversalStack * kBlock];
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float4 a = rays[2 * i], b = rays[2 * i + 1];
+    HitRec h;
+    uint32_t nv = 0, nt = 0;
+    const bool alpha = (flags & 2u) != 0u;
+    if (flags & 1u) {
+        bool occ = traverse<true, false>(S, ld3(a), ld3(b), a.w, b.w, alpha, stack + threadIdx.x, h, nv, nt);
+        hits[i] = make_float4(occ ? 1.0f : -1.0f, 0.0f, 0.0f, bitsf(kMiss));
+    } else {
+        bool any = traverse<false, false>(S, ld3(a), ld3(b), a.w, b.w, alpha, stack + threadIdx.x, h, nv, nt);
+        hits[i] = any ? make_float4(h.t, h.b1, h.b2, bitsf(h.tri)) : make_float4(-1.0f, 0.0f, 0.0f, bitsf(kMiss));
+    }
+}
+
+static inline uint32_t grid_for(uint32_t n) { return (n + kBlock - 1) / kBlock; }
+
+hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream,
+                        hipEvent_t* ev) {
+    KArgs A{scene, fb, fp};
+    const uint32_t g = grid_for(fp.num_paths);
+    const bool count = fp.trav != nullptr;
+    int e_i = 0;
+    auto mark = [&]() {
+        if (ev) (void)hipEventRecord(ev[e_i++], stream);
+    };
+    hipError_t e = hipMemsetAsync(fb.counters, 0, 32 * sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    mark();
+    hipLaunchKernelGGL(k_raygen, dim3(g), dim3(kBlock), 0, stream, A);
+    mark();
+    const int L = fp.set.MaxPathLength < 2 ? 2 : fp.set.MaxPathLength;
+    for (int d = 1; d <= L - 1; ++d) {
+        if (count) hipLaunchKernelGGL(k_trace<true>, dim3(g), dim3(kBlock), 0, stream, A, d);
+        else hipLaunchKernelGGL(k_trace<false>, dim3(g), dim3(kBlock), 0, stream, A, d);
+        mark();
+        hipLaunchKernelGGL(k_shade, dim3(g), dim3(kBlock), 0, stream, A, d);
+        mark();
+        if (count) hipLaunchKernelGGL(k_shadow<true>, dim3(g), dim3(kBlock), 0, stream, A, d);
+        else hipLaunchKernelGGL(k_shadow<false>, dim3(g), dim3(kBlock), 0, stream, A, d);
+        mark();
+    }
+    hipLaunchKernelGGL(k_accumulate, dim3(g), dim3(kBlock), 0, stream, A);
+    mark();
+    return hipGetLastError();
+}
+
+hipError_t launch_trace_rays(const SceneDev& scene, const float4* rays, uint32_t n, uint32_t flags, float4* hits,
+                             hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_trace_rays, dim3(grid_for(n)), dim3(kBlock), 0, stream, scene, rays, n, flags, hits);
+    return hipGetLastError();
+}
+
+}  // namespace dxrpt

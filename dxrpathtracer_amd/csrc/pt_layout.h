@@ -1,0 +1,64 @@
+// pt_layout.h — device-memory layouts shared by the host-side builders (bvh_build.cpp,
+// dxrpt_api.hip) and the gfx950 kernels (pt_kernels.hip).  Plain C++ PODs only.
+//
+// HBM layout of one context (all arrays 256-B aligned, built once per scene):
+//   nodes     BvhNode[num_nodes]        64 B   BVH2, two child AABBs per node (replaces the DXR BLAS,
+//                                              DXRPathTracer.cpp:2331-2488)
+//   tris      TriRecord[num_tris]       48 B   leaf-ordered triangles: v0, e1=v1-v0, e2=v2-v0 + ids
+//   vertices  dxrpt_mesh_vertex[nv]     64 B   AoS, exactly the reference MeshVertex (Model.h:25-67)
+//   indices   uint32[ni]                 4 B   mesh-local, R16 inputs are widened on upload
+//   geoinfo   dxrpt_geometry_info[ng]   16 B
+//   materials dxrpt_material[nm]        24 B
+//   texdesc   TexDesc[nt]               16 B   -> texels (one pool of 32-bit words)
+//   sky       uint16[6*res*res*4]        8 B/texel RGBA16F cube
+// Per-frame (wavefront) buffers are described in pt_kernels.hip.
+#pragma once
+#include <stdint.h>
+
+namespace dxrpt {
+
+// BVH2 node, 64 B (four 16-B words, read with two/four dwordx4 loads).
+//   a = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
+//   b = (c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y)
+//   c = (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)
+//   d = (child0, child1, 0, 0): child >= 0 -> internal node index;
+//       child < 0 -> leaf, ~child = (first_tri << 3) | (count - 1), 1 <= count <= 8.
+struct BvhNode {
+    float a[4];
+    float b[4];
+    float c[4];
+    int32_t d[4];
+};
+static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 B");
+
+constexpr int kMaxLeafTris = 8;
+constexpr int kTraversalStack = 32;   // LDS stack entries per lane; builder caps depth to fit.
+
+__attribute__((always_inline)) inline int32_t encode_leaf(uint32_t first, uint32_t count) {
+    return ~static_cast<int32_t>((first << 3) | (count - 1u));
+}
+
+// Leaf triangle record, 48 B.
+//   p0 = (v0.x, v0.y, v0.z, bits(gtri))      gtri = global triangle id = IdxOffset/3 + PrimitiveIndex
+//   p1 = (e1.x, e1.y, e1.z, bits(geometry))  geometry = GeometryIndex()
+//   p2 = (e2.x, e2.y, e2.z, bits(flags))     flags bit0 = opaque geometry
+struct TriRecord {
+    float p0[4];
+    float p1[4];
+    float p2[4];
+};
+static_assert(sizeof(TriRecord) == 48, "TriRecord must be 48 B");
+
+constexpr uint32_t kTriOpaque = 1u;
+
+// Texture descriptor, 16 B.  Texels live in one pool of 32-bit words starting at `offset`.
+//   fmt DXRPT_TEX_RGBA8_*: one word per texel (r | g<<8 | b<<16 | a<<24)
+//   fmt DXRPT_TEX_R8_UNORM: four texels per word (row-major, texel i in byte i&3 of word i>>2)
+struct TexDesc {
+    uint32_t offset;
+    uint32_t width;
+    uint32_t height;
+    uint32_t fmt;
+};
+
+}  // namespace dxrpt

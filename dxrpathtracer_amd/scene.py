@@ -1,0 +1,147 @@
+"""Host scene inputs: wraps libdxrpt_host.so (scenes, camera, sky) with numpy views.
+
+Reference roles: Model::GenerateBoxTestScene / CreateWithAssimp (Graphics/Model.cpp:435-780), the
+per-scene camera/sun tables (DXRPathTracer.cpp:83-98), FirstPersonCamera (Graphics/Camera.cpp:202-229)
+and SkyCache::Init (Graphics/Skybox.cpp:48-215).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _abi as A
+
+SPONZA_SEED = 0x53504F4E5A41  # "SPONZA" 
+SCENE_NAMES = {"sponza": A.SCENE_SPONZA, "suntemple": A.SCENE_SUNTEMPLE, "boxtest": A.SCENE_BOXTEST,
+               "whitefurnace": A.SCENE_WHITEFURNACE}
+
+# DXRPathTracer.cpp:265 camera.Initialize(aspect, Pi_4, 0.1f, 100.0f)
+CAMERA_FOV = math.pi / 4
+CAMERA_NEAR = 0.1
+CAMERA_FAR = 100.0
+# AppSettings.cpp:104-113 sky defaults
+DEFAULT_TURBIDITY = 2.0
+DEFAULT_GROUND_ALBEDO = (0.25, 0.25, 0.25)
+SKY_RES = 128  # Skybox.cpp:164
+
+
+class Scene:
+    """A host scene (vertices, indices, geometries, materials, textures, lights + camera/sun pose)."""
+
+    def __init__(self, scene: str | int = "boxtest", seed: int = SPONZA_SEED, detail: int = 0):
+        sid = SCENE_NAMES[scene] if isinstance(scene, str) else int(scene)
+        H = A.host()
+        p = C.POINTER(A.HostScene)()
+        rc = H.dxrpt_host_scene_create(sid, seed, detail, C.byref(p))
+        if rc != 0:
+            raise RuntimeError(f"dxrpt_host_scene_create({sid}) failed: {H.dxrpt_host_last_error().decode()}")
+        self._p = p
+        s = p.contents
+        self.scene_id = sid
+        self.num_triangles = int(s.num_triangles)
+        self.vertices = np.frombuffer((C.c_uint8 * (64 * s.num_vertices)).from_address(C.cast(s.vertices, C.c_void_p).value),
+                                      dtype=np.float32).reshape(s.num_vertices, 16)
+        idt = np.uint16 if s.idx_bytes == 2 else np.uint32
+        self.indices = np.frombuffer((C.c_uint8 * (s.idx_bytes * s.num_indices)).from_address(s.indices), dtype=idt)
+        self.geometries = np.frombuffer((C.c_uint8 * (16 * s.num_geometries)).from_address(
+            C.cast(s.geometries, C.c_void_p).value), dtype=np.uint32).reshape(s.num_geometries, 4)
+        self.materials = np.frombuffer((C.c_uint8 * (24 * s.num_materials)).from_address(
+            C.cast(s.materials, C.c_void_p).value), dtype=np.uint32).reshape(s.num_materials, 6)
+        self.textures = []
+        for i in range(s.num_textures):
+            t = s.textures[i]
+            nbytes = t.width * t.height * (1 if t.fmt == A.TEX_R8_UNORM else 4)
+            data = np.frombuffer((C.c_uint8 * nbytes).from_address(t.texels), dtype=np.uint8)
+            self.textures.append((int(t.width), int(t.height), int(t.fmt), data))
+        self.spot_lights = [s.spot_lights[i] for i in range(s.num_spot_lights)]
+        self.camera_position = tuple(s.camera_position)
+        self.camera_rotation = tuple(s.camera_rotation)
+        self.sun_direction = tuple(s.sun_direction)
+        self.white_furnace = bool(s.white_furnace)
+        self._host = s
+
+    def close(self):
+        if self._p:
+            A.host().dxrpt_host_scene_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def idx_bytes(self) -> int:
+        return int(self._host.idx_bytes)
+
+    def texture_bytes(self) -> int:
+        return sum(d.nbytes for _, _, _, d in self.textures)
+
+    # ---- camera + sky ---------------------------------------------------------------------------
+    def inv_view_projection(self, width: int, height: int) -> np.ndarray:
+        out = (C.c_float * 16)()
+        pos = (C.c_float * 3)(*self.camera_position)
+        A.host().dxrpt_host_inv_view_projection(pos, self.camera_rotation[0], self.camera_rotation[1], CAMERA_FOV,
+                                                width / height, CAMERA_NEAR, CAMERA_FAR, out)
+        return np.array(out, dtype=np.float32)
+
+    def settings(self, **overrides) -> A.AppSettings:
+        s = A.default_settings()
+        s.SunDirection[:] = self.sun_direction          # AppSettings::SunDirection.SetValue (DXRPathTracer.cpp:963)
+        s.EnableWhiteFurnaceMode = 1 if self.white_furnace else 0  # DXRPathTracer.cpp:935
+        for k, v in overrides.items():
+            if k == "SunDirection":
+                s.SunDirection[:] = v
+            else:
+                setattr(s, k, v)
+        return s
+
+
+@dataclass
+class Sky:
+    cube: np.ndarray          # uint16, 6*res*res*4 (RGBA16F)
+    res: int
+    sun_irradiance: tuple
+    sun_render_color: tuple
+
+
+def make_sky(settings: A.AppSettings, turbidity: float = DEFAULT_TURBIDITY,
+             ground_albedo=DEFAULT_GROUND_ALBEDO, res: int = SKY_RES) -> Sky:
+    cube = np.zeros(6 * res * res * 4, dtype=np.uint16)
+    irr = (C.c_float * 3)()
+    ren = (C.c_float * 3)()
+    sun = (C.c_float * 3)(*settings.SunDirection)
+    alb = (C.c_float * 3)(*ground_albedo)
+    rc = A.host().dxrpt_host_sky_create(sun, settings.SunSize, turbidity, alb, res, cube.ctypes.data, irr, ren)
+    if rc != 0:
+        raise RuntimeError("dxrpt_host_sky_create failed")
+    return Sky(cube, res, tuple(irr), tuple(ren))
+
+
+def make_constants(scene: Scene, settings: A.AppSettings, sky: Sky, width: int, height: int,
+                   sample_idx: int) -> A.RayTraceConstants:
+    """RenderRayTracing's constant fill (DXRPathTracer.cpp:2048-2067)."""
+    inv = (C.c_float * 16)(*scene.inv_view_projection(width, height))
+    pos = (C.c_float * 3)(*scene.camera_position)
+    rtc = A.RayTraceConstants()
+    nl = min(len(scene.spot_lights), A.DXRPT_MAX_SPOT_LIGHTS)
+    A.host().dxrpt_host_fill_constants(inv, pos, C.byref(settings), (C.c_float * 3)(*sky.sun_irradiance),
+                                       (C.c_float * 3)(*sky.sun_render_color), sample_idx, width, height, nl,
+                                       C.byref(rtc))
+    return rtc
+
+
+def make_lights(scene: Scene) -> A.LightConstants:
+    lc = A.LightConstants()
+    for i, l in enumerate(scene.spot_lights[:A.DXRPT_MAX_SPOT_LIGHTS]):
+        lc.Lights[i] = l
+    return lc
+
+
+def nominal_rays(width: int, height: int, max_path_length: int) -> int:
+    """HUD ray count, DXRPathTracer.cpp:2171."""
+    return width * height * (1 + (max_path_length - 1) * 2)

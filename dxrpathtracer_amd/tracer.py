@@ -1,0 +1,153 @@
+"""DXRPathTracer host driver over the C ABI (libdxrpt.so).
+
+Mirrors the reference's path-tracer-facing methods of class DXRPathTracer (DXRPathTracer.h:32-202):
+InitializeScene (DXRPathTracer.cpp:932-985), BuildRTAccelerationStructure (2331-2488), the sample-index
+/ restart bookkeeping of Update (1416-1461) and RenderRayTracing (2024-2090).  There is no CPU
+fallback: every method goes through the HIP library and raises on a non-zero status.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi as A
+from .scene import Scene, Sky, make_constants, make_lights
+
+
+class DxrptError(RuntimeError):
+    pass
+
+
+class DXRPathTracer:
+    def __init__(self, device: int = 0):
+        self._L = A.lib()
+        self._ctx = C.c_void_p()
+        rc = self._L.dxrpt_create(device, C.byref(self._ctx))
+        if rc != A.DXRPT_OK:
+            raise DxrptError(f"dxrpt_create({device}) failed with status {rc}")
+        self.rt_curr_sample_idx = 0
+        self.rt_should_restart = True
+        self.scene: Scene | None = None
+        self.sky: Sky | None = None
+
+    def _check(self, rc: int, what: str):
+        if rc != A.DXRPT_OK:
+            msg = self._L.dxrpt_last_error(self._ctx)
+            raise DxrptError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    def close(self):
+        if self._ctx:
+            self._L.dxrpt_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- InitializeScene (DXRPathTracer.cpp:932-985) + material/texture tables --------------------
+    def initialize_scene(self, scene: Scene, sky: Sky):
+        L = self._L
+        for (w, h, fmt, data) in scene.textures:
+            idx = C.c_uint32()
+            self._check(L.dxrpt_add_texture(self._ctx, w, h, fmt, data.ctypes.data, C.byref(idx)), "dxrpt_add_texture")
+        s = scene._host
+        self._check(L.dxrpt_set_scene(self._ctx, s.vertices, s.num_vertices, s.indices, s.idx_bytes, s.num_indices,
+                                      s.geometries, s.num_geometries, s.materials, s.num_materials), "dxrpt_set_scene")
+        self.set_sky(sky)
+        self.scene = scene
+        self.rt_should_restart = True
+
+    def set_sky(self, sky: Sky):
+        self._check(self._L.dxrpt_set_sky(self._ctx, sky.cube.ctypes.data, sky.res), "dxrpt_set_sky")
+        self.sky = sky
+
+    def build_rt_acceleration_structure(self) -> A.BvhInfo:
+        self._check(self._L.dxrpt_build_bvh(self._ctx), "dxrpt_build_bvh")
+        return self.bvh_info()
+
+    def bvh_info(self) -> A.BvhInfo:
+        info = A.BvhInfo()
+        self._check(self._L.dxrpt_get_bvh_info(self._ctx, C.byref(info)), "dxrpt_get_bvh_info")
+        return info
+
+    # ---- Update restart logic (DXRPathTracer.cpp:1416-1461) ----------------------------------------
+    def restart(self):
+        self.rt_should_restart = True
+
+    def update(self):
+        if self.rt_should_restart:
+            self.rt_curr_sample_idx = 0
+            self.rt_should_restart = False
+
+    # ---- RenderRayTracing (DXRPathTracer.cpp:2024-2090) ---------------------------------------------
+    def render_ray_tracing(self, accum_ptr: int, width: int, height: int, settings: A.AppSettings,
+                           tiles=None, stream: int = 0, sample_idx: int | None = None,
+                           lights: A.LightConstants | None = None) -> bool:
+        """Enqueues one DispatchRays(W,H,1) equivalent.  Returns False (and does nothing) once the
+        sample count reached SqrtNumSamples^2 (DXRPathTracer.cpp:2027-2028)."""
+        idx = self.rt_curr_sample_idx if sample_idx is None else sample_idx
+        if idx >= settings.SqrtNumSamples * settings.SqrtNumSamples:
+            return False
+        rtc = make_constants(self.scene, settings, self.sky, width, height, idx)
+        self.render_raw(rtc, settings, accum_ptr, width, height, tiles, stream,
+                        lights if lights is not None else make_lights(self.scene))
+        if sample_idx is None:
+            self.rt_curr_sample_idx += 1
+        return True
+
+    def render_raw(self, rtc: A.RayTraceConstants, settings: A.AppSettings, accum_ptr: int, width: int,
+                   height: int, tiles=None, stream: int = 0, lights: A.LightConstants | None = None):
+        tarr, nt = None, 0
+        if tiles:
+            tarr = (A.Tile * len(tiles))()
+            for i, t in enumerate(tiles):
+                tarr[i] = t if isinstance(t, A.Tile) else A.Tile(*t)
+            nt = len(tiles)
+        lp = C.byref(lights) if lights is not None else None
+        self._check(self._L.dxrpt_render(self._ctx, C.byref(rtc), C.byref(settings), lp, C.c_void_p(accum_ptr),
+                                         width, height, tarr, nt, C.c_void_p(stream)), "dxrpt_render")
+
+    def set_option(self, option: int, value: int):
+        self._check(self._L.dxrpt_set_option(self._ctx, option, value), "dxrpt_set_option")
+
+    def reset_timing(self):
+        self._check(self._L.dxrpt_reset_timing(self._ctx), "dxrpt_reset_timing")
+
+    def stats(self) -> A.Stats:
+        st = A.Stats()
+        self._check(self._L.dxrpt_get_stats(self._ctx, C.byref(st)), "dxrpt_get_stats")
+        return st
+
+    def trace_rays(self, rays_ptr: int, n: int, flags: int, hits_ptr: int, stream: int = 0):
+        self._check(self._L.dxrpt_trace_rays(self._ctx, C.c_void_p(rays_ptr), n, flags, C.c_void_p(hits_ptr),
+                                             C.c_void_p(stream)), "dxrpt_trace_rays")
+
+
+def row_band_tiles(width: int, height: int, rank: int, world: int, band: int = 16):
+    """Screen-space sharding: bands of `band` full rows, band b -> rank b % world,
+    written compactly (band after band) into the rank's local buffer."""
+    tiles = []
+    off = 0
+    for b, y0 in enumerate(range(0, height, band)):
+        if b % world != rank:
+            continue
+        h = min(band, height - y0)
+        tiles.append(A.Tile(0, y0, width, h, off, width, 0))
+        off += width * h
+    return tiles, off
+
+
+def unpermute_bands(parts, width: int, height: int, world: int, band: int = 16) -> np.ndarray:
+    """Host reference of the gather's un-permute: parts[r] is rank r's compact (n_r, 4) buffer."""
+    out = np.zeros((height * width, 4), dtype=np.float32)
+    offs = [0] * world
+    for b, y0 in enumerate(range(0, height, band)):
+        r = b % world
+        h = min(band, height - y0)
+        n = width * h
+        out[y0 * width:(y0 + h) * width] = parts[r][offs[r]:offs[r] + n]
+        offs[r] += n
+    return out.reshape(height, width, 4)

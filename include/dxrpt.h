@@ -1,0 +1,294 @@
+/*
+ * dxrpt.h — C ABI of the MI355X-native path tracer (gfx950 / HIP).
+ *
+ * This is the drop-in boundary for the reference's DXR `DispatchRays` path
+ * (WANG-Ruipeng/DXRPathTracer).  Every entry point below replaces one piece of
+ * the reference's D3D12 binding of that path; the replaced interface is cited
+ * as file:line relative to the reference tree.
+ *
+ *   reference                                   replaced by
+ *   ------------------------------------------  --------------------------------
+ *   Model::CreateBuffers vertex/index SRVs      dxrpt_set_scene
+ *     (SampleFramework12/v1.02/Graphics/Model.cpp:851-881)
+ *   GeometryInfo buffer (DXRPathTracer.cpp:2363-2367, 2477-2484)
+ *   Material SRV table (MeshRenderer.cpp:158-186)
+ *   LoadMaterialResources texture SRVs         dxrpt_add_texture
+ *     (Graphics/Model.cpp:104-149)
+ *   SkyCache::CubeMap (Graphics/Skybox.cpp:160-201)   dxrpt_set_sky
+ *   BuildRTAccelerationStructure               dxrpt_build_bvh
+ *     (DXRPathTracer.cpp:2331-2488)
+ *   RenderRayTracing / DispatchRays(W,H,1)     dxrpt_render
+ *     (DXRPathTracer.cpp:2024-2090)
+ *   HUD ray count (DXRPathTracer.cpp:2171-2174) dxrpt_get_stats
+ *   DXCall/Exception (Exceptions.h:260-290)    int status + dxrpt_last_error
+ *
+ * Conventions
+ *   - All functions return 0 (DXRPT_OK) on success, a negative DXRPT_E_* code on
+ *     failure; no C++ exception crosses the ABI.  dxrpt_last_error() returns a
+ *     human-readable description of the last failure on that context.
+ *   - Host pointers are only read during the call (scene data is deep-copied to
+ *     device memory owned by the context).
+ *   - The accumulation target is CALLER-owned device memory (the reference's
+ *     `rtTarget` RGBA32F UAV, DXRPathTracer.cpp:919-927).
+ *   - dxrpt_render only enqueues work on `stream` (a hipStream_t, or NULL for
+ *     the default stream); the caller synchronises.
+ *   - One host thread per context.
+ */
+#ifndef DXRPT_H_
+#define DXRPT_H_
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DXRPT_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------------------------- */
+#define DXRPT_OK 0
+#define DXRPT_E_INVALID_ARG (-1)
+#define DXRPT_E_HIP (-2)
+#define DXRPT_E_NO_DEVICE (-3)
+#define DXRPT_E_STATE (-4)      /* call out of order (e.g. render before build_bvh) */
+#define DXRPT_E_OOM (-5)
+#define DXRPT_E_UNSUPPORTED (-6)
+
+/* ---- limits mirrored from AppSettings.hlsl:53-60 ----------------------------------------------- */
+#define DXRPT_MAX_SPOT_LIGHTS 32u           /* MaxSpotLights (AppSettings.hlsl:53) */
+#define DXRPT_MAX_PATH_LENGTH 8u            /* MaxPathLengthSetting (AppSettings.hlsl:60) */
+#define DXRPT_SPOT_SHADOW_NEAR_CLIP 0.1f    /* SpotShadowNearClip (AppSettings.hlsl:56) */
+#define DXRPT_INVALID_INDEX 0xFFFFFFFFu     /* Material.Opacity when no opacity map (MeshRenderer.cpp:158-186) */
+
+/* ---- texture formats (dxrpt_add_texture) ------------------------------------------------------ */
+#define DXRPT_TEX_RGBA8_UNORM 0u  /* 4 x u8, linear */
+#define DXRPT_TEX_RGBA8_SRGB 1u   /* 4 x u8, rgb sRGB-decoded per texel (ForceSRGB albedo, Model.cpp:140) */
+#define DXRPT_TEX_R8_UNORM 2u     /* 1 x u8 (e.g. BC4 opacity decoded on the host) */
+
+/* ---- POD types, byte-identical to the reference layouts ---------------------------------------- */
+
+/* MeshVertex, 64 B: SampleFramework12/v1.02/Graphics/Model.h:25-67, Shaders/RayTracing.hlsl:13-21 */
+typedef struct dxrpt_mesh_vertex {
+    float Position[3];
+    float Normal[3];
+    float UV[2];
+    float Tangent[3];
+    float Bitangent[3];
+    float LightmapUV[2];
+} dxrpt_mesh_vertex;
+
+/* GeometryInfo, 16 B: DXRPathTracer/SharedTypes.h:58-64 */
+typedef struct dxrpt_geometry_info {
+    uint32_t VtxOffset;   /* in vertices */
+    uint32_t IdxOffset;   /* in indices (not bytes) */
+    uint32_t MaterialIdx;
+    uint32_t PadTo16Bytes;
+} dxrpt_geometry_info;
+
+/* Material, 24 B: DXRPathTracer/SharedTypes.h:30-38.  Each field is a texture index returned by
+ * dxrpt_add_texture (the reference stores SRV descriptor indices). Opacity == DXRPT_INVALID_INDEX
+ * marks the geometry opaque (D3D12_RAYTRACING_GEOMETRY_FLAG_OPAQUE, DXRPathTracer.cpp:2348,2361). */
+typedef struct dxrpt_material {
+    uint32_t Albedo;
+    uint32_t Normal;
+    uint32_t Roughness;
+    uint32_t Metallic;
+    uint32_t Opacity;
+    uint32_t Emissive;
+} dxrpt_material;
+
+/* SpotLight, 48 B: DXRPathTracer/SharedTypes.h:40-48 */
+typedef struct dxrpt_spot_light {
+    float Position[3];
+    float AngularAttenuationX;
+    float Direction[3];
+    float AngularAttenuationY;
+    float Intensity[3];
+    float Range;
+} dxrpt_spot_light;
+
+/* LightConstants, 3584 B: DXRPathTracer.cpp:131-135, RayTrace.hlsl:46-50 */
+typedef struct dxrpt_light_constants {
+    dxrpt_spot_light Lights[DXRPT_MAX_SPOT_LIGHTS];
+    float ShadowMatrices[DXRPT_MAX_SPOT_LIGHTS][16];
+} dxrpt_light_constants;
+
+/* RayTraceConstants, 156 B: DXRPathTracer.cpp:145-165, RayTrace.hlsl:24-44.
+ * InvViewProjection is row-major and used with the row-vector convention mul(float4, M).
+ * The five *Idx fields are bindless SRV indices in the reference; here the context owns the
+ * buffers and they are ignored (kept for layout identity). */
+typedef struct dxrpt_ray_trace_constants {
+    float InvViewProjection[16];
+    float SunDirectionWS[3];
+    float CosSunAngularRadius;
+    float SunIrradiance[3];
+    float SinSunAngularRadius;
+    float SunRenderColor[3];
+    uint32_t Padding;
+    float CameraPosWS[3];
+    uint32_t CurrSampleIdx;
+    uint32_t TotalNumPixels;
+    uint32_t VtxBufferIdx;
+    uint32_t IdxBufferIdx;
+    uint32_t GeometryInfoBufferIdx;
+    uint32_t MaterialBufferIdx;
+    uint32_t SkyTextureIdx;
+    uint32_t NumLights;
+} dxrpt_ray_trace_constants;
+
+/* AppSettingsCBuffer, 124 B: DXRPathTracer/AppSettings.h:97-128 (bool32 -> uint32_t), defaults in
+ * AppSettings.cpp:95-208 (dxrpt_default_settings fills them). */
+typedef struct dxrpt_app_settings {
+    uint32_t EnableSun;
+    uint32_t EnableSky;
+    uint32_t SunAreaLightApproximation;
+    float SunSize;
+    float SunDirection[3];
+    int32_t MSAAMode;
+    uint32_t RenderLights;
+    uint32_t EnableRayTracing;
+    uint32_t ClampRoughness;
+    uint32_t AvoidCausticPaths;
+    int32_t SqrtNumSamples;
+    int32_t MaxPathLength;
+    int32_t MaxAnyHitPathLength;
+    float Exposure;
+    float BloomExposure;
+    float BloomMagnitude;
+    float BloomBlurSigma;
+    uint32_t EnableAlbedoMaps;
+    uint32_t EnableNormalMaps;
+    uint32_t EnableDiffuse;
+    uint32_t EnableSpecular;
+    uint32_t EnableDirect;
+    uint32_t EnableIndirect;
+    uint32_t EnableIndirectSpecular;
+    uint32_t ApplyMultiscatteringEnergyCompensation;
+    float RoughnessScale;
+    float MetallicScale;
+    uint32_t EnableWhiteFurnaceMode;
+    uint32_t EnableLightMapRender;
+} dxrpt_app_settings;
+
+/* A screen-space tile of the W x H image rendered by one dxrpt_render call.  Pixel (x, y) of the
+ * tile (x0 <= x < x0+w, y0 <= y < y0+h) is written to
+ *     accum[accum_offset + (y - y0) * accum_pitch + (x - x0)]      (float4 units)
+ * The CMJ pattern always uses the GLOBAL pixel index y * W + x and TotalNumPixels (RayTrace.hlsl:85-96),
+ * so any tiling produces bit-identical pixels.  A NULL tile list means one full-frame tile with
+ * accum_offset 0 and accum_pitch W (the reference's rtTarget). */
+typedef struct dxrpt_tile {
+    uint32_t x0, y0, w, h;
+    uint64_t accum_offset;
+    uint32_t accum_pitch;
+    uint32_t pad;
+} dxrpt_tile;
+
+/* Kernel kinds for the per-kernel timings in dxrpt_stats. */
+#define DXRPT_K_RAYGEN 0
+#define DXRPT_K_TRACE 1       /* closest-hit traversal of radiance rays (all depths) */
+#define DXRPT_K_SHADE 2
+#define DXRPT_K_SHADOW 3      /* any-hit traversal of shadow rays (all depths) */
+#define DXRPT_K_ACCUMULATE 4
+#define DXRPT_K_COUNT 5
+
+/* Counters of the last dxrpt_render call (read back with a stream sync in dxrpt_get_stats), plus
+ * per-kernel HIP-event timings accumulated since dxrpt_reset_timing (DXRPT_OPT_KERNEL_TIMING). */
+typedef struct dxrpt_stats {
+    uint64_t pixels;                   /* paths started */
+    uint64_t radiance_rays;            /* closest-hit rays traced (all depths) */
+    uint64_t shadow_rays;              /* any-hit rays traced */
+    uint64_t nominal_rays;             /* W*H*(1+2(L-1)) of the rendered pixels, DXRPathTracer.cpp:2171 */
+    uint64_t radiance_rays_per_depth[DXRPT_MAX_PATH_LENGTH];
+    uint64_t shadow_rays_per_depth[DXRPT_MAX_PATH_LENGTH];
+    /* DXRPT_OPT_COUNT_TRAVERSAL only (last render): BVH nodes visited / triangles tested */
+    uint64_t node_visits_radiance, tri_tests_radiance, node_visits_shadow, tri_tests_shadow;
+    /* DXRPT_OPT_KERNEL_TIMING only: summed kernel durations (ms) and launches since the last reset */
+    double kernel_ms[DXRPT_K_COUNT];
+    uint64_t kernel_launches[DXRPT_K_COUNT];
+    uint64_t timed_frames;
+    double frame_ms;                   /* summed raygen-start -> accumulate-end time of the timed frames */
+} dxrpt_stats;
+
+/* BVH summary (dxrpt_get_bvh_info). */
+typedef struct dxrpt_bvh_info {
+    uint32_t num_nodes;
+    uint32_t num_leaves;
+    uint32_t num_tris;
+    uint32_t max_depth;
+    uint32_t node_bytes;      /* bytes per node of the layout traversed on the GPU */
+    uint32_t tri_bytes;       /* bytes per leaf triangle record */
+    double build_ms;          /* host build time */
+    double sah_cost;
+} dxrpt_bvh_info;
+
+typedef struct dxrpt_ctx dxrpt_ctx;
+
+/* ---- lifecycle -------------------------------------------------------------------------------- */
+/* Capability check at create: gfx9xx device with >= 64 KiB LDS (replaces the SM 6.6 / DXR 1.1 checks
+ * of Graphics/DX12.cpp:141-165). */
+int dxrpt_create(int hip_device, dxrpt_ctx** out_ctx);
+int dxrpt_destroy(dxrpt_ctx* ctx);
+const char* dxrpt_last_error(const dxrpt_ctx* ctx);
+int dxrpt_abi_version(void);
+/* Fill `s` with the reference defaults (AppSettings.cpp:95-208). */
+void dxrpt_default_settings(dxrpt_app_settings* s);
+
+/* ---- scene ------------------------------------------------------------------------------------ */
+/* Vertex/index/geometry/material tables (Model.cpp:851-881, DXRPathTracer.cpp:2363-2367).
+ * idx_bytes is 2 (R16_UINT) or 4 (R32_UINT); indices are mesh-local, offset by VtxOffset. */
+int dxrpt_set_scene(dxrpt_ctx* ctx,
+                    const dxrpt_mesh_vertex* vertices, uint32_t num_vertices,
+                    const void* indices, uint32_t idx_bytes, uint32_t num_indices,
+                    const dxrpt_geometry_info* geometries, uint32_t num_geometries,
+                    const dxrpt_material* materials, uint32_t num_materials);
+/* Adds a w x h texture (mip 0) of format DXRPT_TEX_*; out_index receives the index to store in
+ * dxrpt_material fields.  Indices are assigned 0, 1, 2, ... in call order. */
+int dxrpt_add_texture(dxrpt_ctx* ctx, uint32_t w, uint32_t h, uint32_t fmt, const void* texels,
+                      uint32_t* out_index);
+/* Sky cubemap: 6 faces (+x,-x,+y,-y,+z,-z) of res x res RGBA16F texels, face-major then row-major
+ * (the SkyCache::CubeMap layout, Graphics/Skybox.cpp:160-201). */
+int dxrpt_set_sky(dxrpt_ctx* ctx, const uint16_t* rgba16f_cube, uint32_t res);
+/* Builds the acceleration structure over the scene set by dxrpt_set_scene (one BLAS over all
+ * geometries + identity instance in the reference; here one binned-SAH BVH over all triangles). */
+int dxrpt_build_bvh(dxrpt_ctx* ctx);
+int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
+
+/* ---- options ---------------------------------------------------------------------------------- */
+#define DXRPT_OPT_COUNT_TRAVERSAL 1u  /* 1: instrumented kernels count node visits / triangle tests (slower) */
+#define DXRPT_OPT_KERNEL_TIMING 2u    /* 1: record a hipEvent after every launch of dxrpt_render */
+int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
+/* Zeroes the accumulated kernel timings. */
+int dxrpt_reset_timing(dxrpt_ctx* ctx);
+
+/* ---- the hot path ----------------------------------------------------------------------------- */
+/* One sample per pixel for every pixel of `tiles` (one DispatchRays(W,H,1)), progressively
+ * accumulated into `accum` (device float4): accum = lerp(new, accum, s/(s+1)), s = CurrSampleIdx
+ * (RayTrace.hlsl:140-148).  rtc->TotalNumPixels must equal W*H.  `stream` is a hipStream_t. */
+int dxrpt_render(dxrpt_ctx* ctx,
+                 const dxrpt_ray_trace_constants* rtc,
+                 const dxrpt_app_settings* settings,
+                 const dxrpt_light_constants* lights,
+                 float* accum, uint32_t width, uint32_t height,
+                 const dxrpt_tile* tiles, uint32_t num_tiles,
+                 void* stream);
+/* Synchronises the context's last stream and returns the counters of the last dxrpt_render. */
+int dxrpt_get_stats(dxrpt_ctx* ctx, dxrpt_stats* out);
+
+/* TraceRay on arbitrary rays against the built acceleration structure (the DXR TraceRay call sites
+ * RayTrace.hlsl:138,258,305,407,425 without the shading).  `rays` (device) holds num_rays pairs of
+ * float4: (origin.xyz, tmin), (direction.xyz, tmax).  `hits` (device) receives one float4 per ray:
+ *   closest-hit (flags bit0 = 0): (t, b1, b2, bits(global triangle id)), t = -1 and id = ~0 on miss;
+ *   any-hit     (flags bit0 = 1): (+1 occluded / -1 visible, 0, 0, ~0).
+ * flags bit1 = run the alpha-test any-hit on non-opaque geometry (i.e. not RAY_FLAG_FORCE_OPAQUE).
+ * The global triangle id is GeometryInfo.IdxOffset/3 + PrimitiveIndex(). */
+#define DXRPT_TRACE_ANY_HIT 1u
+#define DXRPT_TRACE_ALPHA 2u
+int dxrpt_trace_rays(dxrpt_ctx* ctx, const float* rays, uint32_t num_rays, uint32_t flags, float* hits,
+                     void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DXRPT_H_ */

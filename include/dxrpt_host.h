@@ -1,0 +1,96 @@
+/*
+ * dxrpt_host.h — host-side inputs of the path tracer (libdxrpt_host.so, plain C++, no GPU).
+ *
+ * These are the CALLER side of the boundary in include/dxrpt.h: the pieces of the reference that
+ * produce the path tracer's inputs, restated for a headless Linux host.
+ *
+ *   reference                                             here
+ *   ----------------------------------------------------  ---------------------------------------
+ *   Model::GenerateBoxTestScene (Graphics/Model.cpp:761-780,  dxrpt_host_scene_create(BOXTEST)
+ *     InitBox 235-343, default textures 74-82, 115-117)
+ *   Model::CreateWithAssimp(Sponza/SunTemple .fbx)          dxrpt_host_scene_create(SPONZA/SUNTEMPLE):
+ *     (Graphics/Model.cpp:435-722; the .fbx files are         seeded procedural proxies (the assets are
+ *     absent, .MISSING_LARGE_BLOBS:1-4)                       not in the reference snapshot)
+ *   scene tables (DXRPathTracer.cpp:83-98)                  camera pose / sun direction fields
+ *   FirstPersonCamera + XMMatrixPerspectiveFovLH            dxrpt_host_inv_view_projection
+ *     (Graphics/Camera.cpp:202-229, DXRPathTracer.cpp:265)
+ *   SkyCache::Init (Graphics/Skybox.cpp:48-215)             dxrpt_host_sky_create
+ *   RenderRayTracing constant fill (DXRPathTracer.cpp:2048-2067)  dxrpt_host_fill_constants
+ */
+#ifndef DXRPT_HOST_H_
+#define DXRPT_HOST_H_
+
+#include <stdint.h>
+#include "dxrpt.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Scene ids = the reference's Scenes enum (AppSettings.h:22-30). */
+#define DXRPT_SCENE_SPONZA 0u
+#define DXRPT_SCENE_SUNTEMPLE 1u
+#define DXRPT_SCENE_BOXTEST 2u
+#define DXRPT_SCENE_WHITEFURNACE 3u
+
+typedef struct dxrpt_host_texture {
+    uint32_t width, height, fmt, pad; /* fmt = DXRPT_TEX_* */
+    const void* texels;               /* w*h*4 bytes (RGBA8) or w*h bytes (R8) */
+} dxrpt_host_texture;
+
+typedef struct dxrpt_host_scene {
+    const dxrpt_mesh_vertex* vertices;
+    uint32_t num_vertices;
+    uint32_t idx_bytes; /* 2 or 4 */
+    const void* indices;
+    uint32_t num_indices;
+    uint32_t num_geometries;
+    const dxrpt_geometry_info* geometries;
+    const dxrpt_material* materials;
+    uint32_t num_materials;
+    uint32_t num_textures;
+    const dxrpt_host_texture* textures; /* material fields index this array */
+    const dxrpt_spot_light* spot_lights;
+    uint32_t num_spot_lights;
+    uint32_t scene_id;
+    float camera_position[3];  /* SceneCameraPositions (DXRPathTracer.cpp:96) */
+    float camera_rotation[2];  /* SceneCameraRotations: x = pitch, y = yaw (DXRPathTracer.cpp:97) */
+    float sun_direction[3];    /* SceneSunDirections (DXRPathTracer.cpp:98), not normalised */
+    uint32_t white_furnace;    /* EnableWhiteFurnaceMode forced for the scene (DXRPathTracer.cpp:935) */
+    uint64_t seed;
+    uint64_t num_triangles;
+    void* internal;
+} dxrpt_host_scene;
+
+/* detail: 0 = default (the BASELINE.json-sized proxy); >0 = tessellation multiplier for tests. */
+int dxrpt_host_scene_create(uint32_t scene_id, uint64_t seed, uint32_t detail, dxrpt_host_scene** out);
+void dxrpt_host_scene_destroy(dxrpt_host_scene* scene);
+const char* dxrpt_host_last_error(void);
+
+/* InvViewProjection (row-major, row-vector convention) of a FirstPersonCamera at `position` with
+ * pitch `xrot`, yaw `yrot` and an LH perspective projection (fov, aspect, near, far). */
+void dxrpt_host_inv_view_projection(const float position[3], float xrot, float yrot, float fov, float aspect,
+                                    float nearz, float farz, float out_inv_view_projection[16]);
+
+/* SkyCache::Init: a res x res x 6 RGBA16F sky cube (sun excluded) + sun irradiance/render colour,
+ * all pre-scaled by FP16Scale = 2^-10.  Sky model: Preetham-Shirley-Smits analytic sky (a documented
+ * proxy for the Hosek-Wilkie tables of the reference).  out_cube holds res*res*6*4 halfs. */
+int dxrpt_host_sky_create(const float sun_direction[3], float sun_size_deg, float turbidity,
+                          const float ground_albedo[3], uint32_t res, uint16_t* out_cube,
+                          float out_sun_irradiance[3], float out_sun_render_color[3]);
+
+/* RenderRayTracing's RayTraceConstants fill (DXRPathTracer.cpp:2048-2067). */
+void dxrpt_host_fill_constants(const float inv_view_projection[16], const float camera_position[3],
+                               const dxrpt_app_settings* settings, const float sun_irradiance[3],
+                               const float sun_render_color[3], uint32_t curr_sample_idx, uint32_t width,
+                               uint32_t height, uint32_t num_lights, dxrpt_ray_trace_constants* out);
+
+/* IEEE binary16 <-> binary32 (round to nearest even), used for the cube texels. */
+uint16_t dxrpt_host_float_to_half(float f);
+float dxrpt_host_half_to_float(uint16_t h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DXRPT_HOST_H_ */

@@ -1,0 +1,114 @@
+"""ctypes binding of the CPU parity oracle (oracle/_build/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg as the checker / CPU baseline, never by the product (dxrpathtracer_amd).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+
+class OracleStats(C.Structure):
+    _fields_ = [("radiance_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("node_visits", C.c_uint64),
+                ("tri_tests", C.c_uint64)]
+
+
+class OracleTexture(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("fmt", C.c_uint32), ("pad", C.c_uint32),
+                ("texels", C.c_void_p)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        P = C.c_void_p
+        L.oracle_cmj2d.argtypes = [C.c_uint32] * 4 + [C.POINTER(C.c_float)]
+        L.oracle_cmj2d.restype = None
+        L.oracle_sincos.argtypes = [C.c_float, C.POINTER(C.c_float)]
+        L.oracle_sincos.restype = None
+        L.oracle_scene_create.argtypes = [P, C.c_uint32, P, C.c_uint32, C.c_uint32, P, C.c_uint32, P, C.c_uint32,
+                                          P, C.c_uint32, P, C.c_uint32]
+        L.oracle_scene_create.restype = P
+        L.oracle_scene_destroy.argtypes = [P]
+        L.oracle_scene_destroy.restype = None
+        L.oracle_scene_build_ms.argtypes = [P]
+        L.oracle_scene_build_ms.restype = C.c_double
+        L.oracle_render.argtypes = [P, P, P, P] + [C.c_uint32] * 6 + [P, C.c_uint32, C.POINTER(OracleStats)]
+        L.oracle_trace_rays.argtypes = [P, P, C.c_uint32, C.c_uint32, P]
+        _lib = L
+    return _lib
+
+
+def cmj2d(sample_idx: int, nx: int, ny: int, pattern: int) -> tuple[float, float]:
+    out = (C.c_float * 2)()
+    lib().oracle_cmj2d(sample_idx, nx, ny, pattern & 0xFFFFFFFF, out)
+    return out[0], out[1]
+
+
+def sincos(x: float) -> tuple[float, float]:
+    out = (C.c_float * 2)()
+    lib().oracle_sincos(x, out)
+    return out[0], out[1]
+
+
+class OracleScene:
+    """The oracle's own copy of a dxrpathtracer_amd.scene.Scene (plus its own BVH)."""
+
+    def __init__(self, scene, sky):
+        L = lib()
+        self._keep = (scene, sky)
+        self._tex = (OracleTexture * max(1, len(scene.textures)))()
+        for i, (w, h, fmt, data) in enumerate(scene.textures):
+            self._tex[i] = OracleTexture(w, h, fmt, 0, data.ctypes.data)
+        self.ptr = L.oracle_scene_create(scene.vertices.ctypes.data, scene.vertices.shape[0], scene.indices.ctypes.data,
+                                         scene.idx_bytes, scene.indices.size, scene.geometries.ctypes.data,
+                                         scene.geometries.shape[0], scene.materials.ctypes.data,
+                                         scene.materials.shape[0], C.cast(self._tex, C.c_void_p),
+                                         len(scene.textures), sky.cube.ctypes.data, sky.res)
+        self.build_ms = L.oracle_scene_build_ms(self.ptr)
+
+    def close(self):
+        if self.ptr:
+            lib().oracle_scene_destroy(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def render(self, rtc, settings, lights, width, height, crop=None, accum=None, threads=0):
+        """One sample over `crop` = (x0, y0, w, h); returns (accum (h, w, 4) float32, OracleStats)."""
+        x0, y0, w, h = crop if crop is not None else (0, 0, width, height)
+        if accum is None:
+            accum = np.zeros((h, w, 4), dtype=np.float32)
+        assert accum.dtype == np.float32 and accum.flags.c_contiguous and accum.shape == (h, w, 4)
+        st = OracleStats()
+        rc = lib().oracle_render(self.ptr, C.addressof(rtc), C.addressof(settings),
+                                 C.addressof(lights) if lights is not None else None, width, height, x0, y0, w, h,
+                                 accum.ctypes.data, threads, C.byref(st))
+        if rc != 0:
+            raise RuntimeError("oracle_render failed")
+        return accum, st
+
+    def trace_rays(self, rays: np.ndarray, flags: int) -> np.ndarray:
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+        hits = np.zeros((rays.shape[0], 4), dtype=np.float32)
+        lib().oracle_trace_rays(self.ptr, rays.ctypes.data, rays.shape[0], flags, hits.ctypes.data)
+        return hits

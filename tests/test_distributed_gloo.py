@@ -1,0 +1,66 @@
+"""CPU, world_size 2 (gloo): the multi-GPU path's partition + frame-end gather + un-permute.
+
+Each rank renders only its row bands (here with the CPU oracle standing in for the HIP kernel, which
+tests/test_gpu_parity.py checks separately with the same tiles) into a compact slab; rank 0 gathers
+the slabs and must reproduce the single-rank frame bit for bit, because CMJ seeds use global pixel
+indices (RayTrace.hlsl:85-96)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, W, H, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import dxrpathtracer_amd as D
+        from dxrpathtracer_amd.distributed import band_layout, gather_frame, source_index
+        from tests._common import oracle_scene, scene_bundle
+        sc, sky = scene_bundle("boxtest")
+        st = sc.settings(MaxPathLength=3)
+        rtc = D.make_constants(sc, st, sky, W, H, 1)
+        lay = band_layout(W, H, world)
+        local = np.zeros((lay.max_count, 4), dtype=np.float32)
+        orc = oracle_scene("boxtest")
+        for t in lay.rank_tiles(rank):
+            img, _ = orc.render(rtc, st, D.make_lights(sc), W, H, crop=(t.x0, t.y0, t.w, t.h))
+            local[t.accum_offset:t.accum_offset + t.w * t.h] = img.reshape(-1, 4)
+        full = torch.zeros((W * H, 4), dtype=torch.float32) if rank == 0 else None
+        idx = torch.tensor(source_index(lay), dtype=torch.long) if rank == 0 else None
+        gather_frame(torch.from_numpy(local), lay, rank, full, idx)
+        if rank == 0:
+            ref, _ = orc.render(rtc, st, D.make_lights(sc), W, H)
+            q.put(bool(np.array_equal(full.numpy().reshape(H, W, 4), ref)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_band_gather_reproduces_single_rank_frame(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    W, H = 48, 72  # 5 bands of 16 rows (last one partial)
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) is True

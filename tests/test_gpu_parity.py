@@ -1,0 +1,283 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle on the same inputs.
+
+Gate (BASELINE.json north_star): per-pixel RGB within 1e-4 relative at matched CMJ indices
+(tests/_common.py RTOL).  Every branch decision (hits, alpha tests, lobe selection) is computed with
+identical float arithmetic on both sides; the only permitted difference is the summation order of
+the radiance terms (recursive in the oracle, unrolled with path throughput on the GPU).
+Full-size configurations (BASELINE.json configs 2-5) are checked on crops via dxrpt tiles, which
+use global pixel indices, plus size-independent properties (tiling invariance, accumulation).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import dxrpathtracer_amd as D
+import dxrpathtracer_amd._abi as A
+from dxrpathtracer_amd.tracer import DXRPathTracer
+from dxrpathtracer_amd.distributed import band_layout
+from tests._common import assert_parity, oracle_scene, scene_bundle
+
+pytestmark = pytest.mark.gpu
+
+_TRACERS = {}
+
+
+def tracer(name):
+    if name not in _TRACERS:
+        sc, sky = scene_bundle(name)
+        t = DXRPathTracer(0)
+        t.initialize_scene(sc, sky)
+        t.build_rt_acceleration_structure()
+        _TRACERS[name] = t
+    return _TRACERS[name]
+
+
+def gpu_render(torch, name, W, H, settings, sample, tiles=None, n_out=None, accum=None, rtc=None, lights=None):
+    sc, sky = scene_bundle(name)
+    t = tracer(name)
+    if rtc is None:
+        rtc = D.make_constants(sc, settings, sky, W, H, sample)
+    n = n_out if n_out is not None else W * H
+    if accum is None:
+        accum = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
+    t.render_raw(rtc, settings, accum.data_ptr(), W, H, tiles=tiles,
+                 stream=torch.cuda.current_stream().cuda_stream,
+                 lights=lights if lights is not None else D.make_lights(sc))
+    torch.cuda.synchronize()
+    return accum
+
+
+def crop_tiles(crops, W):
+    tiles, off = [], 0
+    for (x0, y0, w, h) in crops:
+        tiles.append(A.Tile(x0, y0, w, h, off, w, 0))
+        off += w * h
+    return tiles, off
+
+
+def check_crops(torch, name, W, H, crops, sample=0, **overrides):
+    sc, sky = scene_bundle(name)
+    st = sc.settings(**overrides)
+    tiles, n = crop_tiles(crops, W)
+    out = gpu_render(torch, name, W, H, st, sample, tiles=tiles, n_out=n).cpu().numpy()
+    rtc = D.make_constants(sc, st, sky, W, H, sample)
+    off = 0
+    for (x0, y0, w, h) in crops:
+        ref, _ = oracle_scene(name).render(rtc, st, D.make_lights(sc), W, H, crop=(x0, y0, w, h))
+        assert_parity(out[off:off + w * h].reshape(h, w, 4), ref, f"{name} {W}x{H} crop {(x0, y0, w, h)} s{sample}")
+        off += w * h
+
+
+def test_boxtest_256_full_frame(torch_cuda):
+    # BASELINE.json configs[0]: BoxTest 256x256, MaxPathLength 2 (the reference minimum; == 1)
+    torch = torch_cuda
+    W = H = 256
+    sc, sky = scene_bundle("boxtest")
+    for L in (1, 2, 3):
+        st = sc.settings(MaxPathLength=L)
+        acc = None
+        ref = None
+        for s in range(3):
+            acc = gpu_render(torch, "boxtest", W, H, st, s, accum=acc)
+            rtc = D.make_constants(sc, st, sky, W, H, s)
+            ref, _ = oracle_scene("boxtest").render(rtc, st, D.make_lights(sc), W, H, accum=ref)
+            assert_parity(acc.cpu().numpy().reshape(H, W, 4), ref, f"boxtest L{L} s{s}")
+
+
+SPONZA_CROPS = [(900, 480, 96, 96), (0, 0, 64, 64), (1700, 900, 80, 64), (300, 700, 128, 48), (1500, 200, 64, 96)]
+
+
+@pytest.mark.parametrize("sample", [0, 7])
+def test_sponza_1080p_L3_crops(torch_cuda, sample):
+    # BASELINE.json metric config: Sponza(-proxy) 1920x1080, MaxPathLength 3
+    check_crops(torch_cuda, "sponza", 1920, 1080, SPONZA_CROPS, sample=sample, MaxPathLength=3)
+
+
+def test_sponza_720p_L3_crops(torch_cuda):
+    check_crops(torch_cuda, "sponza", 1280, 720, [(600, 300, 96, 96), (10, 600, 64, 64)], sample=3, MaxPathLength=3)
+
+
+def test_sponza_1080p_L8_crops(torch_cuda):
+    # BASELINE.json configs[2]: path length 8
+    check_crops(torch_cuda, "sponza", 1920, 1080, [(960, 540, 64, 64), (200, 300, 48, 48)], sample=15, MaxPathLength=8)
+
+
+def test_sponza_4k_L6_crops(torch_cuda):
+    # BASELINE.json configs[4] (single-GPU slice of it)
+    check_crops(torch_cuda, "sponza", 3840, 2160, [(1900, 1000, 64, 64), (3000, 1800, 48, 48)], sample=2, MaxPathLength=6)
+
+
+@pytest.mark.parametrize("any_hit_len", [1, 8])
+def test_suntemple_alpha_tested_crops(torch_cuda, any_hit_len):
+    # BASELINE.json configs[3]: alpha-tested foliage (any-hit path)
+    check_crops(torch_cuda, "suntemple", 1920, 1080, [(800, 400, 96, 96), (1200, 600, 96, 64), (100, 200, 64, 64)],
+                sample=1, MaxPathLength=3, MaxAnyHitPathLength=any_hit_len)
+
+
+def test_white_furnace_full_frame(torch_cuda):
+    check_crops(torch_cuda, "whitefurnace", 128, 128, [(0, 0, 128, 128)], sample=4)
+
+
+@pytest.mark.parametrize("overrides", [
+    dict(EnableNormalMaps=0), dict(EnableAlbedoMaps=0), dict(EnableSpecular=0), dict(EnableDiffuse=0),
+    dict(EnableDirect=0), dict(EnableIndirect=0), dict(EnableSun=0), dict(EnableSky=0),
+    dict(SunAreaLightApproximation=0), dict(ApplyMultiscatteringEnergyCompensation=0),
+    dict(EnableIndirectSpecular=1), dict(EnableIndirectSpecular=1, AvoidCausticPaths=1),
+    dict(ClampRoughness=1, EnableIndirectSpecular=1), dict(RoughnessScale=0.3, MetallicScale=1.7),
+    dict(SqrtNumSamples=7), dict(MaxAnyHitPathLength=0),
+])
+def test_settings_toggles(torch_cuda, overrides):
+    ov = dict(MaxPathLength=4)
+    ov.update(overrides)
+    check_crops(torch_cuda, "sponza", 640, 360, [(200, 100, 96, 96), (400, 250, 64, 64)], sample=5, **ov)
+
+
+def test_spot_lights(torch_cuda):
+    # RayTrace.hlsl:265-313 with lights passed through LightConstants (BoxTest has none of its own)
+    torch = torch_cuda
+    sc, sky = scene_bundle("boxtest")
+    st = sc.settings(MaxPathLength=3, EnableSun=0)
+    W, H = 160, 120
+    lights = D.make_lights(sc)
+    import math
+    for i, (p, d) in enumerate([((1.5, 4.0, -2.0), (-0.3, -1.0, 0.4)), ((-2.5, 1.5, -1.5), (0.8, -0.2, 0.5))]):
+        n = math.sqrt(sum(x * x for x in d))
+        L = lights.Lights[i]
+        L.Position[:] = p
+        L.Direction[:] = tuple(x / n for x in d)
+        L.Intensity[:] = (2500.0 * 0.02, 2500.0 * 0.018, 2500.0 * 0.015)  # DXRPathTracer.cpp:977
+        L.AngularAttenuationX = math.cos(0.6 * 0.5)
+        L.AngularAttenuationY = math.cos(1.2 * 0.5)
+        L.Range = 7.5  # SpotLightRange (AppSettings.hlsl:55)
+    rtc = D.make_constants(sc, st, sky, W, H, 2)
+    rtc.NumLights = 2
+    out = gpu_render(torch, "boxtest", W, H, st, 2, rtc=rtc, lights=lights).cpu().numpy().reshape(H, W, 4)
+    ref, stats = oracle_scene("boxtest").render(rtc, st, lights, W, H)
+    assert stats.shadow_rays > W * H  # the spot shadow rays were traced
+    assert_parity(out, ref, "boxtest spot lights")
+    rtc.NumLights = 0
+    dark = gpu_render(torch, "boxtest", W, H, st, 2, rtc=rtc, lights=lights).cpu().numpy().reshape(H, W, 4)
+    assert out[..., :3].sum() > dark[..., :3].sum()
+
+
+def test_tiling_is_bit_identical(torch_cuda):
+    # the multi-GPU band partition (any world size) renders exactly the full-frame pixels
+    torch = torch_cuda
+    W, H = 320, 180
+    sc, _ = scene_bundle("sponza")
+    st = sc.settings(MaxPathLength=3)
+    full = gpu_render(torch, "sponza", W, H, st, 3).cpu().numpy().reshape(H, W, 4)
+    for world in (2, 3, 8):
+        lay = band_layout(W, H, world)
+        for r in range(world):
+            part = gpu_render(torch, "sponza", W, H, st, 3, tiles=lay.rank_tiles(r), n_out=lay.counts[r]).cpu().numpy()
+            for t in lay.rank_tiles(r):
+                got = part[t.accum_offset:t.accum_offset + t.w * t.h].reshape(t.h, t.w, 4)
+                np.testing.assert_array_equal(got, full[t.y0:t.y0 + t.h, t.x0:t.x0 + t.w])
+
+
+def test_deterministic_run_to_run(torch_cuda):
+    torch = torch_cuda
+    sc, _ = scene_bundle("sponza")
+    st = sc.settings(MaxPathLength=3)
+    a = gpu_render(torch, "sponza", 480, 270, st, 1).cpu().numpy()
+    b = gpu_render(torch, "sponza", 480, 270, st, 1).cpu().numpy()
+    np.testing.assert_array_equal(a, b)
+
+
+def _random_rays(rng, n, lo, hi):
+    o = rng.uniform(lo, hi, size=(n, 3)).astype(np.float32)
+    d = rng.standard_normal((n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.zeros((n, 8), dtype=np.float32)
+    rays[:, 0:3] = o
+    rays[:, 3] = 0.0
+    rays[:, 4:7] = d
+    rays[:, 7] = 1e30
+    return rays
+
+
+@pytest.mark.parametrize("name,flags", [("sponza", 0), ("sponza", A.TRACE_ANY_HIT), ("suntemple", A.TRACE_ALPHA),
+                                        ("suntemple", A.TRACE_ANY_HIT | A.TRACE_ALPHA), ("boxtest", 0)])
+def test_trace_rays_matches_oracle_exactly(torch_cuda, name, flags):
+    # TraceRay (RayTrace.hlsl:138,258,305,407,425) on random rays: same hit, same t, same barycentrics
+    torch = torch_cuda
+    rng = np.random.default_rng(42)
+    rays = _random_rays(rng, 200_000, (-15, 0.2, -8), (15, 12, 8))
+    ref = oracle_scene(name).trace_rays(rays, flags)
+    dr = torch.from_numpy(rays).cuda()
+    dh = torch.zeros((rays.shape[0], 4), dtype=torch.float32, device="cuda")
+    tracer(name).trace_rays(dr.data_ptr(), rays.shape[0], flags, dh.data_ptr(),
+                            torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = dh.cpu().numpy()
+    hits = ref[:, 0] >= 0
+    assert hits.mean() > 0.3
+    np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_stats_and_counting_option(torch_cuda):
+    torch = torch_cuda
+    t = tracer("sponza")
+    sc, _ = scene_bundle("sponza")
+    st = sc.settings(MaxPathLength=3)
+    W, H = 640, 360
+    a = gpu_render(torch, "sponza", W, H, st, 0).cpu().numpy()
+    s = t.stats()
+    assert s.pixels == W * H and s.nominal_rays == W * H * 5
+    assert s.radiance_rays_per_depth[1] == W * H
+    assert 0 < s.radiance_rays_per_depth[2] <= W * H
+    assert s.radiance_rays == s.radiance_rays_per_depth[1] + s.radiance_rays_per_depth[2]
+    assert 0 < s.shadow_rays <= 2 * W * H * 2
+    t.set_option(A.OPT_COUNT_TRAVERSAL, 1)
+    try:
+        b = gpu_render(torch, "sponza", W, H, st, 0).cpu().numpy()
+        s2 = t.stats()
+    finally:
+        t.set_option(A.OPT_COUNT_TRAVERSAL, 0)
+    np.testing.assert_array_equal(a, b)
+    assert s2.node_visits_radiance > s2.radiance_rays and s2.tri_tests_radiance > 0
+    assert s2.node_visits_shadow > 0
+
+
+def test_kernel_timing_option(torch_cuda):
+    torch = torch_cuda
+    t = tracer("boxtest")
+    sc, _ = scene_bundle("boxtest")
+    st = sc.settings(MaxPathLength=3)
+    t.set_option(A.OPT_KERNEL_TIMING, 1)
+    t.reset_timing()
+    try:
+        for s in range(5):
+            gpu_render(torch, "boxtest", 128, 128, st, s)
+        stt = t.stats()
+    finally:
+        t.set_option(A.OPT_KERNEL_TIMING, 0)
+    assert stt.timed_frames == 5
+    assert stt.kernel_launches[A.K_TRACE] == 10 and stt.kernel_launches[A.K_RAYGEN] == 5
+    assert all(stt.kernel_ms[k] > 0 for k in range(A.K_COUNT))
+    assert stt.frame_ms >= sum(stt.kernel_ms[k] for k in range(A.K_COUNT)) * 0.99
+
+
+def test_errors_are_reported_not_raised(torch_cuda):
+    # DXRPT_E_* status + dxrpt_last_error instead of the reference's DXCall exceptions
+    torch = torch_cuda
+    t = tracer("boxtest")
+    sc, sky = scene_bundle("boxtest")
+    st = sc.settings()
+    buf = torch.zeros((64 * 64, 4), dtype=torch.float32, device="cuda")
+    with pytest.raises(Exception, match="null argument"):
+        t.render_raw(D.make_constants(sc, st, sky, 64, 64, 0), st, 0, 64, 64)
+    rtc = D.make_constants(sc, st, sky, 64, 64, 0)
+    rtc.TotalNumPixels = 5  # != W*H
+    with pytest.raises(Exception, match="TotalNumPixels"):
+        t.render_raw(rtc, st, buf.data_ptr(), 64, 64)
+    bad = sc.settings(MaxPathLength=9)
+    with pytest.raises(Exception, match="MaxPathLength"):
+        t.render_raw(D.make_constants(sc, bad, sky, 64, 64, 0), bad, buf.data_ptr(), 64, 64)
+    with pytest.raises(Exception, match="outside the image"):
+        t.render_raw(D.make_constants(sc, st, sky, 64, 64, 0), st, buf.data_ptr(), 64, 64,
+                     tiles=[A.Tile(60, 0, 8, 8, 0, 8, 0)])
+    torch.cuda.synchronize()
+    assert float(buf.abs().sum()) == 0.0  # nothing was launched
