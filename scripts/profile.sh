@@ -1,0 +1,17 @@
+#!/bin/bash
+# rocprofv3 passes over the bench (kernel trace + stats, then one PMC group per pass; never combined
+# with other tracing domains).  Outputs under gpurun_out/prof/; summarise with scripts/pmc_summary.py.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/prof
+mkdir -p $OUT
+B="python3 bench.py --no-cpu-baseline"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- $B --steps 32 --warmup 5 \
+    > $OUT/kt_bench.json 2> $OUT/kt.err || exit $?
+echo "kernel trace ok"; cat $OUT/kt_bench.json
+for pmc in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES"; do
+  tag=$(echo $pmc | tr ' ' '_')
+  timeout -k 10 600 rocprofv3 --pmc $pmc -d $OUT/pmc_$tag -o run --output-format csv -- $B --steps 8 --warmup 2 \
+      > $OUT/pmc_$tag.json 2> $OUT/pmc_$tag.err || { echo "pmc $pmc failed rc=$?"; tail -5 $OUT/pmc_$tag.err; exit 1; }
+  echo "pmc $pmc ok"
+done
