@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 outputs of scripts/profile.sh into profiles/<round>_*.
+
+Per kernel: launches, average duration (kernel trace), and per-launch PMC averages.  HBM traffic per
+launch follows MI355X_MICROARCH.md section HBM: FETCH_SIZE and WRITE_SIZE come from separate passes,
+are in KiB, and on gfx950 FETCH_SIZE reports half the bytes of 16-B/lane reads, so the read side is
+doubled (our traversal loads are 16-B/lane dwordx4; the guide marks other shapes uncalibrated, so the
+raw value is kept next to the corrected one).
+usage: scripts/pmc_summary.py gpurun_out/prof r01
+"""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+CONFIG = "sponza-proxy 1920x1080 L=3"
+
+
+def short(name):
+    for k in ("k_trace<false>", "k_shadow<false>", "k_trace<true>", "k_shadow<true>", "k_shade", "k_raygen",
+              "k_accumulate"):
+        if k in name:
+            return k
+    return None
+
+
+def counters(path):
+    acc = defaultdict(lambda: defaultdict(list))
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            k = short(row["Kernel_Name"])
+            if k:
+                acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
+
+
+def main(prof, rnd):
+    stats = {}
+    with open(os.path.join(prof, "kt", "run_kernel_stats.csv")) as f:
+        for row in csv.DictReader(f):
+            k = short(row["Name"])
+            if k:
+                stats[k] = {"calls": int(row["Calls"]), "avg_ms": float(row["AverageNs"]) / 1e6,
+                            "total_ms": float(row["TotalDurationNs"]) / 1e6, "pct": float(row["Percentage"])}
+    pmc = {}
+    for d in sorted(os.listdir(prof)):
+        p = os.path.join(prof, d, "run_counter_collection.csv")
+        if d.startswith("pmc_") and os.path.exists(p):
+            for k, cs in counters(p).items():
+                pmc.setdefault(k, {}).update(cs)
+    out = {"config": CONFIG, "source": f"rocprofv3 via scripts/profile.sh ({prof})", "kernels": {}}
+    for k in sorted(set(stats) | set(pmc)):
+        e = dict(stats.get(k, {}))
+        c = pmc.get(k, {})
+        e["pmc"] = c
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            e["hbm_read_bytes_raw"] = c["FETCH_SIZE"] * 1024
+            e["hbm_bytes_per_launch"] = c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024
+        if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c and c["TCC_HIT_sum"] + c["TCC_MISS_sum"] > 0:
+            e["l2_hit_rate"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+        out["kernels"][k] = e
+    os.makedirs("profiles", exist_ok=True)
+    with open(f"profiles/{rnd}_kernels.json", "w") as f:
+        json.dump(out, f, indent=2)
+    kt = out["kernels"].get("k_trace<false>", {})
+    with open(f"profiles/{rnd}_pmc_k_trace.json", "w") as f:
+        json.dump({"config": CONFIG, "kernel": "k_trace<false>", "avg_ms": kt.get("avg_ms"),
+                   "hbm_bytes_per_launch": kt.get("hbm_bytes_per_launch"),
+                   "hbm_read_bytes_raw": kt.get("hbm_read_bytes_raw"), "l2_hit_rate": kt.get("l2_hit_rate"),
+                   "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 16-B/lane read correction) + WRITE_SIZE KiB x1024"},
+                  f, indent=2)
+    for src in ("kt/run_kernel_stats.csv",):
+        with open(os.path.join(prof, src)) as f, open(f"profiles/{rnd}_kernel_stats.csv", "w") as g:
+            g.write(f.read())
+    for k, e in out["kernels"].items():
+        print(f"{k:18s} calls {e.get('calls', 0):4d} avg {e.get('avg_ms', 0):8.4f} ms  "
+              f"hbm/launch {e.get('hbm_bytes_per_launch', 0) / 1e6:9.1f} MB  L2 hit {e.get('l2_hit_rate', 0):.3f}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
