@@ -74,7 +74,7 @@ class Tile(C.Structure):
 
 K_RAYGEN, K_TRACE, K_SHADE, K_SHADOW, K_ACCUMULATE, K_COUNT = range(6)
 KERNEL_NAMES = ("k_raygen", "k_trace", "k_shade", "k_shadow", "k_accumulate")
-OPT_COUNT_TRAVERSAL, OPT_KERNEL_TIMING = 1, 2
+OPT_COUNT_TRAVERSAL, OPT_KERNEL_TIMING, OPT_BVH_WIDTH, OPT_TRAVERSAL_MODE, OPT_REFILL_LANES = 1, 2, 3, 4, 5
 
 
 class Stats(C.Structure):
@@ -89,7 +89,8 @@ class Stats(C.Structure):
 
 class BvhInfo(C.Structure):
     _fields_ = [("num_nodes", u32), ("num_leaves", u32), ("num_tris", u32), ("max_depth", u32),
-                ("node_bytes", u32), ("tri_bytes", u32), ("build_ms", C.c_double), ("sah_cost", C.c_double)]
+                ("node_bytes", u32), ("tri_bytes", u32), ("width", u32), ("pad", u32), ("build_ms", C.c_double),
+                ("sah_cost", C.c_double)]
 
 
 class HostTexture(C.Structure):

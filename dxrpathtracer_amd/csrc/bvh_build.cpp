@@ -1,11 +1,12 @@
-// bvh_build.cpp — binned-SAH BVH2 for the software traversal kernels.
+// bvh_build.cpp — binned-SAH binary tree, emitted as BVH2 or as a compressed BVH8.
 //
 // The reference builds one BLAS with one GEOMETRY_DESC per mesh plus an identity TLAS instance
 // (DXRPathTracer.cpp:2331-2488) and lets the driver choose the tree.  Here the tree is built on the
-// host once per scene: 32-bin SAH over triangle centroids, leaves of <= 8 triangles (<= 4 preferred),
-// depth capped so the per-lane LDS traversal stack (kTraversalStack entries) can never overflow.
-// Child boxes are padded outward so that the (fast, FMA-using) slab test on the GPU is conservative:
-// the exact triangle test alone decides hits, which keeps results independent of the tree.
+// host once per scene: 32-bin SAH over triangle centroids, small leaves, and a depth budget that
+// falls back to object-median splits so the per-lane LDS traversal stacks can never overflow.
+// Child boxes are padded outward so that the (fast, FMA-using) slab tests on the GPU are
+// conservative: the exact triangle test alone decides hits, which keeps results independent of the
+// tree (the parity oracle builds its own).
 #include "bvh_build.h"
 
 #include <algorithm>
@@ -40,56 +41,27 @@ struct Box {
 };
 
 constexpr int kBins = 32;
-constexpr int kPreferLeaf = 4;
-constexpr uint32_t kMaxDepth = kTraversalStack;  // a node at depth d has at most d stack entries above it
+constexpr uint32_t kMaxDepth2 = kTraversalStack;  // a BVH2 node at depth d has <= d stack entries above it
 
-struct Task {
-    int32_t node;    // node whose child slot we fill
-    int slot;        // 0 or 1
-    uint32_t begin, end, depth;
+// Generic binary tree node.
+struct TNode {
+    Box box;
+    int32_t child[2] = {-1, -1};
+    uint32_t first = 0, count = 0;  // leaf when count > 0
 };
 
 struct Builder {
-    const float* pos;
     std::vector<Box> tri_box;
-    std::vector<float> cen;  // 3 per tri
+    std::vector<float> cen;
     std::vector<uint32_t> refs;
-    std::vector<BvhNode> nodes;
-    float pad_abs = 0.f;
-    uint32_t max_depth = 0, num_leaves = 0;
-    double sah_sum = 0.0;  // sum over nodes of area * cost contribution
+    std::vector<TNode> tree;
+    uint32_t leaf_max = kMaxLeafTris;
+    uint32_t prefer_leaf = 4;
 
     Box range_box(uint32_t b, uint32_t e) const {
         Box r;
         for (uint32_t i = b; i < e; ++i) r.grow(tri_box[refs[i]]);
         return r;
-    }
-
-    void write_child(int32_t node, int slot, const Box& bx, int32_t child) {
-        BvhNode& n = nodes[node];
-        float lo[3], hi[3];
-        if (bx.empty()) {
-            for (int k = 0; k < 3; ++k) { lo[k] = FLT_MAX; hi[k] = -FLT_MAX; }
-        } else {
-            for (int k = 0; k < 3; ++k) {
-                float m = std::max(std::fabs(bx.lo[k]), std::fabs(bx.hi[k]));
-                float p = m * 7.62939453125e-06f + pad_abs;  // |coord| * 2^-17 + scene-relative term
-                lo[k] = bx.lo[k] - p;
-                hi[k] = bx.hi[k] + p;
-            }
-        }
-        float* ab = slot == 0 ? n.a : n.b;
-        ab[0] = lo[0]; ab[1] = hi[0]; ab[2] = lo[1]; ab[3] = hi[1];
-        n.c[slot * 2 + 0] = lo[2];
-        n.c[slot * 2 + 1] = hi[2];
-        n.d[slot] = child;
-    }
-
-    int32_t new_node() {
-        BvhNode n;
-        std::memset(&n, 0, sizeof(n));
-        nodes.push_back(n);
-        return int32_t(nodes.size() - 1);
     }
 
     // Returns the split position (refs partitioned) or 0 when the range should become a leaf.
@@ -139,14 +111,14 @@ struct Builder {
                 }
             }
         }
-        const bool must_split = n > uint32_t(kMaxLeafTris);
-        if (!must_split && n <= uint32_t(kPreferLeaf) && leaf_cost <= best_cost) return 0;
-        if (!must_split && depth + 1 >= kMaxDepth) return 0;
-        // Depth budget: halving splits need `levels` more levels to reach <= kMaxLeafTris; once the SAH
+        const bool must_split = n > leaf_max;
+        if (!must_split && n <= prefer_leaf && leaf_cost <= best_cost) return 0;
+        if (!must_split && depth + 1 >= kMaxDepth2) return 0;
+        // Depth budget: halving splits need `levels` more levels to reach <= leaf_max; once the SAH
         // split could no longer meet the cap, fall back to object-median splits.
         uint32_t levels = 0;
-        for (uint32_t m = (n + kMaxLeafTris - 1) / kMaxLeafTris; m > 1; m = (m + 1) / 2) ++levels;
-        const bool tight = depth + levels + 3 >= kMaxDepth;
+        for (uint32_t m = (n + leaf_max - 1) / leaf_max; m > 1; m = (m + 1) / 2) ++levels;
+        const bool tight = depth + levels + 3 >= kMaxDepth2;
         if (best_axis >= 0 && !tight && (must_split || best_cost < leaf_cost)) {
             const float ext = cb.hi[best_axis] - cb.lo[best_axis];
             const float scale = float(kBins) / ext;
@@ -159,7 +131,6 @@ struct Builder {
             if (m > b && m < e) return m;
         }
         if (!must_split) return 0;
-        // Object-median fallback (degenerate centroids): split by index along the widest axis.
         int ax = 0;
         for (int k = 1; k < 3; ++k)
             if (cb.hi[k] - cb.lo[k] > cb.hi[ax] - cb.lo[ax]) ax = k;
@@ -170,11 +141,271 @@ struct Builder {
         });
         return m;
     }
+
+    // Builds the binary tree; tree[0] is the root (may be a leaf).
+    bool build(uint32_t ntris, std::string& err, double& sah) {
+        struct Task {
+            int32_t node;
+            uint32_t begin, end, depth;
+        };
+        tree.clear();
+        tree.reserve(size_t(ntris) * 2 / 3 + 16);
+        tree.emplace_back();
+        std::vector<Task> stack{{0, 0, ntris, 0}};
+        const double root_area = std::max(range_box(0, ntris).area(), 1e-30);
+        sah = 0.0;
+        while (!stack.empty()) {
+            Task t = stack.back();
+            stack.pop_back();
+            Box bx = range_box(t.begin, t.end);
+            tree[t.node].box = bx;
+            uint32_t m = split(t.begin, t.end, t.depth, bx);
+            if (m == 0) {
+                if (t.end - t.begin > leaf_max) {
+                    err = "build_bvh: cannot form a leaf within the depth cap";
+                    return false;
+                }
+                tree[t.node].first = t.begin;
+                tree[t.node].count = t.end - t.begin;
+                sah += bx.area() / root_area * double(t.end - t.begin);
+            } else {
+                if (t.depth + 1 > kMaxDepth2) {
+                    err = "build_bvh: depth cap exceeded";
+                    return false;
+                }
+                int32_t c0 = int32_t(tree.size()), c1 = c0 + 1;
+                tree.emplace_back();
+                tree.emplace_back();
+                tree[t.node].child[0] = c0;
+                tree[t.node].child[1] = c1;
+                sah += bx.area() / root_area;
+                stack.push_back({c1, m, t.end, t.depth + 1});
+                stack.push_back({c0, t.begin, m, t.depth + 1});
+            }
+        }
+        return true;
+    }
+};
+
+// Outward padding so that GPU slab tests with FMA rounding stay conservative.
+Box padded(const Box& bx, float pad_abs) {
+    if (bx.empty()) return bx;
+    Box o;
+    for (int k = 0; k < 3; ++k) {
+        float m = std::max(std::fabs(bx.lo[k]), std::fabs(bx.hi[k]));
+        float p = m * 7.62939453125e-06f + pad_abs;  // |coord| * 2^-17 + scene-relative term
+        o.lo[k] = bx.lo[k] - p;
+        o.hi[k] = bx.hi[k] + p;
+    }
+    return o;
+}
+
+// ---- BVH2 emission -------------------------------------------------------------------------------------
+struct Emit2 {
+    const std::vector<TNode>& tree;
+    float pad;
+    std::vector<BvhNode> nodes;
+    uint32_t max_depth = 0, leaves = 0;
+
+    void write_child(uint32_t node, int slot, const Box& b, int32_t link) {
+        BvhNode& n = nodes[node];
+        Box p = padded(b, pad);
+        float lo[3], hi[3];
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = b.empty() ? FLT_MAX : p.lo[k];
+            hi[k] = b.empty() ? -FLT_MAX : p.hi[k];
+        }
+        float* ab = slot == 0 ? n.a : n.b;
+        ab[0] = lo[0]; ab[1] = hi[0]; ab[2] = lo[1]; ab[3] = hi[1];
+        n.c[slot * 2 + 0] = lo[2];
+        n.c[slot * 2 + 1] = hi[2];
+        n.d[slot] = link;
+    }
+    int32_t link_of(int32_t t, uint32_t depth) {
+        const TNode& tn = tree[t];
+        if (tn.count) {
+            leaves++;
+            return encode_leaf(tn.first, tn.count);
+        }
+        uint32_t idx = uint32_t(nodes.size());
+        nodes.emplace_back();
+        std::memset(&nodes.back(), 0, sizeof(BvhNode));
+        max_depth = std::max(max_depth, depth);
+        for (int s = 0; s < 2; ++s) {
+            int32_t c = tn.child[s];
+            int32_t l = link_of(c, depth + 1);
+            write_child(idx, s, tree[c].box, l);
+        }
+        return int32_t(idx);
+    }
+    void run() {
+        const TNode& root = tree[0];
+        if (root.count) {  // the root is always an internal node: leaf in child 0, empty child 1
+            nodes.emplace_back();
+            std::memset(&nodes.back(), 0, sizeof(BvhNode));
+            write_child(0, 0, root.box, encode_leaf(root.first, root.count));
+            write_child(0, 1, Box(), encode_leaf(0, 1));
+            leaves = 1;
+            max_depth = 1;
+        } else {
+            link_of(0, 0);
+        }
+    }
+};
+
+// ---- BVH8 emission -------------------------------------------------------------------------------------
+struct Emit8 {
+    const std::vector<TNode>& tree;
+    const std::vector<uint32_t>& refs;
+    float pad;
+    std::vector<Bvh8Node> nodes;
+    std::vector<uint32_t> tri_order;
+    uint32_t max_depth = 0, leaves = 0;
+
+    static float sgn(int o, int bit) { return (o & bit) ? -1.0f : 1.0f; }
+
+    // Collapse: open the largest-area internal child until there are 8 children.
+    void gather_children(int32_t t, std::vector<int32_t>& ch) {
+        const TNode& tn = tree[t];
+        ch.clear();
+        if (tn.count) {
+            ch.push_back(t);
+            return;
+        }
+        ch.push_back(tn.child[0]);
+        ch.push_back(tn.child[1]);
+        while (ch.size() < 8) {
+            int best = -1;
+            double ba = -1.0;
+            for (size_t i = 0; i < ch.size(); ++i) {
+                const TNode& c = tree[ch[i]];
+                if (c.count) continue;
+                double a = c.box.area();
+                if (a > ba) { ba = a; best = int(i); }
+            }
+            if (best < 0) break;
+            int32_t open = ch[best];
+            ch[best] = tree[open].child[0];
+            ch.push_back(tree[open].child[1]);
+        }
+    }
+
+    void emit(uint32_t idx, int32_t t, uint32_t depth) {
+        max_depth = std::max(max_depth, depth);
+        std::vector<int32_t> ch;
+        gather_children(t, ch);
+        // slot assignment: slot s is nearest for rays of octant 7 ^ s (greedy auction on centroids)
+        Box nb;
+        for (int32_t c : ch) nb.grow(tree[c].box);
+        float pc[3];
+        for (int k = 0; k < 3; ++k) pc[k] = 0.5f * (nb.lo[k] + nb.hi[k]);
+        int32_t slot_of[8];
+        std::fill(slot_of, slot_of + 8, -1);
+        std::vector<bool> used(ch.size(), false);
+        std::vector<bool> taken(8, false);
+        for (size_t round = 0; round < ch.size(); ++round) {
+            float best = -FLT_MAX;
+            int bc = -1, bs = -1;
+            for (size_t c = 0; c < ch.size(); ++c) {
+                if (used[c]) continue;
+                const Box& b = tree[ch[c]].box;
+                float off[3];
+                for (int k = 0; k < 3; ++k) off[k] = 0.5f * (b.lo[k] + b.hi[k]) - pc[k];
+                for (int s = 0; s < 8; ++s) {
+                    if (taken[s]) continue;
+                    const int o = 7 ^ s;  // the octant for which slot s is visited first
+                    float cost = -(off[0] * sgn(o, 4) + off[1] * sgn(o, 2) + off[2] * sgn(o, 1));
+                    if (cost > best) { best = cost; bc = int(c); bs = s; }
+                }
+            }
+            used[bc] = true;
+            taken[bs] = true;
+            slot_of[bs] = ch[bc];
+        }
+        Bvh8Node& n0 = nodes[idx];
+        std::memset(&n0, 0, sizeof(Bvh8Node));
+        // quantisation frame: padded union box
+        Box pb[8];
+        Box ub;
+        for (int s = 0; s < 8; ++s)
+            if (slot_of[s] >= 0) {
+                pb[s] = padded(tree[slot_of[s]].box, pad);
+                ub.grow(pb[s]);
+            }
+        float scale[3];
+        for (int k = 0; k < 3; ++k) {
+            n0.p[k] = ub.lo[k];
+            float ext = ub.hi[k] - ub.lo[k];
+            int e = -100;
+            if (ext > 0.0f) {
+                e = int(std::ceil(std::log2(double(ext) / 255.0)));
+                e = std::max(e, -100);
+            }
+            for (;;) {  // make every child fit in [0, 255] quanta with float decode p + q * 2^e
+                scale[k] = std::ldexp(1.0f, e);
+                bool ok = true;
+                for (int s = 0; s < 8 && ok; ++s) {
+                    if (slot_of[s] < 0) continue;
+                    double qh = std::ceil((double(pb[s].hi[k]) - n0.p[k]) / scale[k]);
+                    if (qh > 255.0) ok = false;
+                    else if (std::fmaf(float(qh), scale[k], n0.p[k]) < pb[s].hi[k] && qh + 1.0 > 255.0) ok = false;
+                }
+                if (ok) break;
+                ++e;
+            }
+            n0.e[k] = uint8_t(e + 127);
+        }
+        // children
+        uint32_t n_internal = 0;
+        for (int s = 0; s < 8; ++s)
+            if (slot_of[s] >= 0 && tree[slot_of[s]].count == 0) n_internal++;
+        const uint32_t base_child = uint32_t(nodes.size());
+        const uint32_t base_tri = uint32_t(tri_order.size());
+        nodes.resize(nodes.size() + n_internal);
+        Bvh8Node& n = nodes[idx];  // (re-fetched: the resize may have moved the array)
+        n.base_child = base_child;
+        n.base_tri = base_tri;
+        uint32_t tri_off = 0, rank = 0;
+        int32_t child_node[8];
+        std::fill(child_node, child_node + 8, -1);
+        for (int s = 0; s < 8; ++s) {
+            if (slot_of[s] < 0) continue;
+            const TNode& c = tree[slot_of[s]];
+            for (int k = 0; k < 3; ++k) {
+                double ql = std::floor((double(pb[s].lo[k]) - n.p[k]) / scale[k]);
+                double qh = std::ceil((double(pb[s].hi[k]) - n.p[k]) / scale[k]);
+                ql = std::min(std::max(ql, 0.0), 255.0);
+                qh = std::min(std::max(qh, 0.0), 255.0);
+                while (ql > 0.0 && std::fmaf(float(ql), scale[k], n.p[k]) > pb[s].lo[k]) ql -= 1.0;
+                while (qh < 255.0 && std::fmaf(float(qh), scale[k], n.p[k]) < pb[s].hi[k]) qh += 1.0;
+                n.qlo[k][s] = uint8_t(ql);
+                n.qhi[k][s] = uint8_t(qh);
+            }
+            if (c.count) {
+                n.meta[s] = uint8_t((c.count << 5) | tri_off);
+                for (uint32_t i = 0; i < c.count; ++i) tri_order.push_back(refs[c.first + i]);
+                tri_off += c.count;
+                leaves++;
+            } else {
+                n.imask |= uint8_t(1u << s);
+                n.meta[s] = uint8_t(kMetaInternal | s);
+                child_node[s] = int32_t(base_child + rank);
+                rank++;
+            }
+        }
+        for (int s = 0; s < 8; ++s)
+            if (child_node[s] >= 0) emit(uint32_t(child_node[s]), slot_of[s], depth + 1);
+    }
+
+    void run() {
+        nodes.emplace_back();
+        emit(0, 0, 0);
+    }
 };
 
 }  // namespace
 
-bool build_bvh(const float* tri_positions, uint32_t ntris, BvhBuildResult& out, std::string& err) {
+bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildResult& out, std::string& err) {
     if (ntris == 0) {
         err = "build_bvh: scene has no triangles";
         return false;
@@ -183,8 +414,13 @@ bool build_bvh(const float* tri_positions, uint32_t ntris, BvhBuildResult& out, 
         err = "build_bvh: too many triangles (leaf encoding holds 2^28)";
         return false;
     }
+    if (width != 2 && width != 8) {
+        err = "build_bvh: width must be 2 or 8";
+        return false;
+    }
     Builder B;
-    B.pos = tri_positions;
+    B.leaf_max = width == 8 ? uint32_t(kMaxLeafTris8) : uint32_t(kMaxLeafTris);
+    B.prefer_leaf = width == 8 ? 3u : 4u;
     B.tri_box.resize(ntris);
     B.cen.resize(size_t(ntris) * 3);
     B.refs.resize(ntris);
@@ -199,61 +435,34 @@ bool build_bvh(const float* tri_positions, uint32_t ntris, BvhBuildResult& out, 
     }
     float ext = 0.f;
     for (int k = 0; k < 3; ++k) ext = std::max(ext, scene.hi[k] - scene.lo[k]);
-    B.pad_abs = ext * 1e-6f + 1e-7f;
-    B.nodes.reserve(size_t(ntris) * 2 / 3 + 16);
-
-    const double root_area = scene.area() > 0 ? scene.area() : 1.0;
+    const float pad = ext * 1e-6f + 1e-7f;
     double sah = 0.0;
-    int32_t root = B.new_node();
-    std::vector<Task> stack;
-    // The root always is an internal node: split the whole range (or put everything in child 0).
-    {
-        uint32_t m = B.split(0, ntris, 0, scene);
-        if (m == 0) {
-            B.write_child(root, 0, scene, encode_leaf(0, ntris));
-            B.write_child(root, 1, Box(), encode_leaf(0, 1));
-            B.num_leaves = 1;
-            sah = 1.0 + ntris;
-            B.max_depth = 1;
-        } else {
-            stack.push_back({root, 1, m, ntris, 1});
-            stack.push_back({root, 0, 0, m, 1});
-            sah = 1.0;
-        }
-    }
-    while (!stack.empty()) {
-        Task t = stack.back();
-        stack.pop_back();
-        Box bx = B.range_box(t.begin, t.end);
-        B.max_depth = std::max(B.max_depth, t.depth);
-        uint32_t m = (t.depth + 1 >= kMaxDepth && t.end - t.begin <= uint32_t(kMaxLeafTris))
-                         ? 0
-                         : B.split(t.begin, t.end, t.depth, bx);
-        if (m == 0) {
-            if (t.end - t.begin > uint32_t(kMaxLeafTris)) {
-                err = "build_bvh: cannot form a leaf within the depth cap";
-                return false;
-            }
-            B.write_child(t.node, t.slot, bx, encode_leaf(t.begin, t.end - t.begin));
-            B.num_leaves++;
-            sah += bx.area() / root_area * double(t.end - t.begin);
-        } else {
-            if (t.depth + 1 > kMaxDepth) {
-                err = "build_bvh: depth cap exceeded";
-                return false;
-            }
-            int32_t nn = B.new_node();
-            B.write_child(t.node, t.slot, bx, nn);
-            sah += bx.area() / root_area * 1.0;
-            stack.push_back({nn, 1, m, t.end, t.depth + 1});
-            stack.push_back({nn, 0, t.begin, m, t.depth + 1});
-        }
-    }
-    out.nodes = std::move(B.nodes);
-    out.tri_order = std::move(B.refs);
-    out.max_depth = B.max_depth;
-    out.num_leaves = B.num_leaves;
+    if (!B.build(ntris, err, sah)) return false;
+    out = BvhBuildResult();
     out.sah_cost = sah;
+    if (width == 2) {
+        Emit2 E{B.tree, pad, {}, 0, 0};
+        E.run();
+        out.nodes = std::move(E.nodes);
+        out.tri_order = std::move(B.refs);
+        out.max_depth = E.max_depth;
+        out.num_leaves = E.leaves;
+    } else {
+        Emit8 E{B.tree, B.refs, pad, {}, {}, 0, 0};
+        E.run();
+        if (E.max_depth + 1 > uint32_t(kTraversalStack8)) {
+            err = "build_bvh: BVH8 deeper than the traversal stack (" + std::to_string(E.max_depth) + ")";
+            return false;
+        }
+        out.nodes8 = std::move(E.nodes);
+        out.tri_order = std::move(E.tri_order);
+        out.max_depth = E.max_depth;
+        out.num_leaves = E.leaves;
+        if (out.tri_order.size() != ntris) {
+            err = "build_bvh: BVH8 emission lost triangles";
+            return false;
+        }
+    }
     return true;
 }
 

@@ -1,5 +1,8 @@
-// bvh_build.h — host binned-SAH BVH2 builder (replaces the driver-side DXR BLAS build invoked at
+// bvh_build.h — host BVH builders (replace the driver-side DXR BLAS build invoked at
 // DXRPathTracer.cpp:2465-2473 with PREFER_FAST_TRACE).
+//
+// One binned-SAH binary tree is built over all triangles; it is then emitted either as the BVH2
+// layout (BvhNode, 64 B) or collapsed into the compressed 8-wide layout (Bvh8Node, 80 B).
 #pragma once
 #include <stdint.h>
 #include <string>
@@ -10,15 +13,17 @@
 namespace dxrpt {
 
 struct BvhBuildResult {
-    std::vector<BvhNode> nodes;       // nodes[0] is the root; DFS order
+    std::vector<BvhNode> nodes;       // BVH2: nodes[0] is the root; DFS order
+    std::vector<Bvh8Node> nodes8;     // BVH8: nodes8[0] is the root
     std::vector<uint32_t> tri_order;  // leaf order -> global triangle id
-    uint32_t max_depth = 0;
+    uint32_t max_depth = 0;           // of the emitted layout
     uint32_t num_leaves = 0;
-    double sah_cost = 0.0;            // C_trav = 1, C_tri = 1, relative to root area
+    double sah_cost = 0.0;            // binary tree, C_trav = 1, C_tri = 1, relative to root area
 };
 
 // tri_positions: ntris * 9 floats (v0.xyz, v1.xyz, v2.xyz) in global triangle order.
+// width 2 -> BVH2 (leaves <= kMaxLeafTris), width 8 -> compressed BVH8 (leaves <= kMaxLeafTris8).
 // Deterministic: the same input always yields the same tree.
-bool build_bvh(const float* tri_positions, uint32_t ntris, BvhBuildResult& out, std::string& err);
+bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildResult& out, std::string& err);
 
 }  // namespace dxrpt

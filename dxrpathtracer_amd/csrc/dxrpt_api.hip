@@ -73,10 +73,10 @@ struct dxrpt_ctx {
     bool scene_set = false, bvh_built = false, sky_set = false, tex_dirty = true;
     uint32_t sky_res = 0;
     // device copies
-    DevBuf d_vertices, d_indices, d_geos, d_mats, d_texdesc, d_texels, d_sky, d_lut, d_nodes, d_tris;
+    DevBuf d_vertices, d_indices, d_geos, d_mats, d_texdesc, d_texels, d_sky, d_lut, d_nodes, d_nodes8, d_tris;
     DevBuf d_lights, d_tiles, d_tile_prefix;
     // per-frame wavefront buffers
-    DevBuf f_thr, f_rad, f_pix, f_qorg0, f_qorg1, f_qdir0, f_qdir1, f_hit, f_shn, f_shorg, f_shdir, f_shcon, f_counters;
+    DevBuf f_thr, f_rad, f_pix, f_qorg0, f_qorg1, f_qdir0, f_qdir1, f_hit, f_shn, f_shq, f_shorg, f_shdir, f_shcon, f_counters;
     FrameBuffers fb;
     dxrpt_bvh_info bvh{};
     std::vector<dxrpt_tile> tiles_cache;
@@ -87,6 +87,11 @@ struct dxrpt_ctx {
     bool rendered = false;
     // options
     bool opt_count = false, opt_timing = false;
+    int opt_width = 8;   // DXRPT_OPT_BVH_WIDTH
+    uint32_t num_cus = 256;
+    uint32_t opt_trav_mode = 0;     // DXRPT_OPT_TRAVERSAL_MODE: 0 one thread per ray, 1 persistent
+    uint32_t opt_refill = 16;       // DXRPT_OPT_REFILL_LANES
+    int built_width = 0;
     DevBuf d_trav;  // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
     // kernel timing: a ring of per-frame event sets, harvested lazily
     struct FrameEvents {
@@ -103,8 +108,8 @@ struct dxrpt_ctx {
 
     ~dxrpt_ctx() {
         DevBuf* all[] = {&d_vertices, &d_indices, &d_geos, &d_mats, &d_texdesc, &d_texels, &d_sky, &d_lut, &d_nodes,
-                         &d_tris, &d_lights, &d_tiles, &d_tile_prefix, &f_thr, &f_rad, &f_pix, &f_qorg0, &f_qorg1,
-                         &f_qdir0, &f_qdir1, &f_hit, &f_shn, &f_shorg, &f_shdir, &f_shcon, &f_counters};
+                         &d_nodes8, &d_tris, &d_lights, &d_tiles, &d_tile_prefix, &f_thr, &f_rad, &f_pix, &f_qorg0, &f_qorg1,
+                         &f_qdir0, &f_qdir1, &f_hit, &f_shn, &f_shq, &f_shorg, &f_shdir, &f_shcon, &f_counters};
         for (DevBuf* b : all) b->release();
         d_trav.release();
         for (auto& f : ring)
@@ -152,6 +157,8 @@ std::vector<float> make_lut() {
 SceneDev scene_dev(const dxrpt_ctx* c) {
     SceneDev s;
     s.nodes = c->d_nodes.as<BvhNode>();
+    s.nodes8 = c->d_nodes8.as<Bvh8Node>();
+    s.width = c->built_width;
     s.tris = c->d_tris.as<TriRecord>();
     s.vertices = c->d_vertices.as<dxrpt_mesh_vertex>();
     s.indices = c->d_indices.as<uint32_t>();
@@ -187,6 +194,7 @@ void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
     c->f_qdir1.ensure(size_t(cap) * 16);
     c->f_hit.ensure(size_t(cap) * 16);
     c->f_shn.ensure(size_t(cap) * 4);
+    c->f_shq.ensure(size_t(cap) * sl * 4);
     c->f_shorg.ensure(size_t(cap) * sl * 16);
     c->f_shdir.ensure(size_t(cap) * sl * 16);
     c->f_shcon.ensure(size_t(cap) * sl * 16);
@@ -200,6 +208,7 @@ void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
     f.q_dir[1] = c->f_qdir1.as<float4>();
     f.hit = c->f_hit.as<float4>();
     f.sh_n = c->f_shn.as<uint32_t>();
+    f.sh_queue = c->f_shq.as<uint32_t>();
     f.sh_org = c->f_shorg.as<float4>();
     f.sh_dir = c->f_shdir.as<float4>();
     f.sh_con = c->f_shcon.as<float4>();
@@ -299,6 +308,7 @@ int dxrpt_create(int hip_device, dxrpt_ctx** out_ctx) {
         require(std::strncmp(prop.gcnArchName, "gfx9", 4) == 0,
                 std::string("unsupported device architecture ") + prop.gcnArchName, DXRPT_E_UNSUPPORTED);
         require(prop.sharedMemPerBlock >= 64 * 1024, "device LDS per workgroup < 64 KiB", DXRPT_E_UNSUPPORTED);
+        c->num_cus = uint32_t(prop.multiProcessorCount);
         std::vector<float> lut = make_lut();
         c->d_lut.upload(lut.data(), lut.size() * sizeof(float));
     });
@@ -327,6 +337,15 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
             if (ctx->opt_count) ctx->d_trav.ensure(4 * sizeof(unsigned long long));
         } else if (option == DXRPT_OPT_KERNEL_TIMING) {
             ctx->opt_timing = value != 0;
+        } else if (option == DXRPT_OPT_TRAVERSAL_MODE) {
+            require(value <= 1, "dxrpt_set_option: traversal mode must be 0 or 1");
+            ctx->opt_trav_mode = uint32_t(value);
+        } else if (option == DXRPT_OPT_REFILL_LANES) {
+            require(value >= 1 && value <= 64, "dxrpt_set_option: refill lanes must be in [1, 64]");
+            ctx->opt_refill = uint32_t(value);
+        } else if (option == DXRPT_OPT_BVH_WIDTH) {
+            require(value == 2 || value == 8, "dxrpt_set_option: BVH width must be 2 or 8");
+            ctx->opt_width = int(value);  // takes effect at the next dxrpt_build_bvh
         } else {
             throw ApiError(DXRPT_E_INVALID_ARG, "dxrpt_set_option: unknown option " + std::to_string(option));
         }
@@ -444,7 +463,7 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
         }
         BvhBuildResult res;
         std::string err;
-        if (!build_bvh(pos.data(), ntris, res, err)) throw ApiError(DXRPT_E_INVALID_ARG, err);
+        if (!build_bvh(pos.data(), ntris, ctx->opt_width, res, err)) throw ApiError(DXRPT_E_INVALID_ARG, err);
         std::vector<TriRecord> tris(ntris);
         for (uint32_t i = 0; i < ntris; ++i) {
             const uint32_t t = res.tri_order[i];
@@ -460,17 +479,23 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
             std::memcpy(&r.p1[3], &g, 4);
             std::memcpy(&r.p2[3], &flags, 4);
         }
-        ctx->d_nodes.upload(res.nodes.data(), res.nodes.size() * sizeof(BvhNode));
+        if (ctx->opt_width == 8) {
+            ctx->d_nodes8.upload(res.nodes8.data(), res.nodes8.size() * sizeof(Bvh8Node));
+        } else {
+            ctx->d_nodes.upload(res.nodes.data(), res.nodes.size() * sizeof(BvhNode));
+        }
         ctx->d_tris.upload(tris.data(), tris.size() * sizeof(TriRecord));
         auto t1 = std::chrono::steady_clock::now();
-        ctx->bvh.num_nodes = uint32_t(res.nodes.size());
+        ctx->bvh.num_nodes = uint32_t(ctx->opt_width == 8 ? res.nodes8.size() : res.nodes.size());
         ctx->bvh.num_leaves = res.num_leaves;
         ctx->bvh.num_tris = ntris;
         ctx->bvh.max_depth = res.max_depth;
-        ctx->bvh.node_bytes = sizeof(BvhNode);
+        ctx->bvh.node_bytes = ctx->opt_width == 8 ? uint32_t(sizeof(Bvh8Node)) : uint32_t(sizeof(BvhNode));
+        ctx->bvh.width = uint32_t(ctx->opt_width);
         ctx->bvh.tri_bytes = sizeof(TriRecord);
         ctx->bvh.build_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
         ctx->bvh.sah_cost = res.sah_cost;
+        ctx->built_width = ctx->opt_width;
         ctx->bvh_built = true;
     });
 }
@@ -554,6 +579,9 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.width = width;
         fp.height = height;
         fp.trav = nullptr;
+        // 32 KiB of LDS per 256-thread workgroup -> 5 resident workgroups per CU (160 KiB)
+        fp.persistent_blocks = ctx->opt_trav_mode == 1 ? ctx->num_cus * 5u : 0u;
+        fp.refill_lanes = ctx->opt_refill;
         hipStream_t s = static_cast<hipStream_t>(stream);
         if (ctx->opt_count) {
             fp.trav = ctx->d_trav.as<unsigned long long>();

@@ -17,12 +17,12 @@ namespace dxrpt {
 //     q_org[d&1][i] float4 (origin xyz, tmax)       rays in SoA-of-float4: one dwordx4 per lane
 //     q_dir[d&1][i] float4 (direction xyz, bits(path slot))
 //     hit[i]        float4 (b1, b2, bits(global tri id) or ~0u on miss, bits(geometry index))
-//     sh_n[i]       uint32 number of shadow rays emitted by the shade of ray i (<= kShadowSlots)
-//   shadow slot k of queue index i lives at [k * capacity + i]:
+//   shadow slot k of path p lives at [k * capacity + p]; sh_n[p] = pending slots of path p:
 //     sh_org  float4 (origin xyz, tmax)
 //     sh_dir  float4 (direction xyz, tmin)
-//     sh_con  float4 (contribution rgb = pathThroughput * CalcLighting or sky*throughput,
-//                     bits(path slot << 1 | force_opaque))
+//     sh_con  float4 (contribution rgb = pathThroughput * CalcLighting or sky*throughput, bits(force_opaque));
+//                    k_shadow multiplies it by the visibility in place
+//   sh_queue[j]   uint32 slot id of the j-th shadow ray of the current depth (compacted)
 struct FrameBuffers {
     float4* ps_thr = nullptr;
     float4* ps_rad = nullptr;
@@ -31,6 +31,7 @@ struct FrameBuffers {
     float4* q_dir[2] = {nullptr, nullptr};
     float4* hit = nullptr;
     uint32_t* sh_n = nullptr;
+    uint32_t* sh_queue = nullptr;
     float4* sh_org = nullptr;
     float4* sh_dir = nullptr;
     float4* sh_con = nullptr;
@@ -40,7 +41,8 @@ struct FrameBuffers {
 };
 
 struct SceneDev {
-    const BvhNode* nodes = nullptr;
+    const BvhNode* nodes = nullptr;     // width 2
+    const Bvh8Node* nodes8 = nullptr;   // width 8
     const TriRecord* tris = nullptr;
     const dxrpt_mesh_vertex* vertices = nullptr;
     const uint32_t* indices = nullptr;
@@ -52,6 +54,7 @@ struct SceneDev {
     const float* lut = nullptr;  // [0..255] unorm, [256..511] sRGB->linear
     uint32_t sky_res = 0;
     uint32_t num_textures = 0;
+    int width = 8;  // BVH width actually built: 2 or 8
 };
 
 struct FrameParams {
@@ -65,6 +68,8 @@ struct FrameParams {
     uint32_t num_paths;
     uint32_t width, height;
     unsigned long long* trav;        // non-null: count traversal work ([0..1] closest node/tri, [2..3] shadow)
+    uint32_t persistent_blocks;      // grid of the persistent BVH8 traversal kernels; 0 = one thread per ray
+    uint32_t refill_lanes;           // persistent kernels: refill once this many lanes of a wave are idle
 };
 
 // Kernel sequence of one frame: raygen, then (trace, shade, shadow) per depth 1..L-1, then accumulate.

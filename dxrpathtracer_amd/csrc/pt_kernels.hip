@@ -31,6 +31,7 @@
 namespace dxrpt {
 
 constexpr int kBlock = 256;
+constexpr uint32_t kShadowGrid = 256u * 20u;  // grid-stride cap: ~20 workgroups per CU
 constexpr uint32_t kMiss = 0xFFFFFFFFu;
 constexpr float kRayTMin = 0.00001f;          // RayTrace.hlsl:243, 382
 constexpr float kSpotShadowNearClip = 0.1f;   // AppSettings.hlsl:56
@@ -201,20 +202,49 @@ struct HitRec {
     uint32_t geom;
 };
 
-// kAnyHit: shadow ray semantics (ACCEPT_FIRST_HIT_AND_END_SEARCH): returns true on the first
-// accepted hit.  Otherwise closest hit: smallest t, ties -> smallest global triangle id.
-template <bool kAnyHit, bool kCount>
-PT_DEV bool traverse(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, int* stk, HitRec& h,
-                     uint32_t& nvisit, uint32_t& ntest) {
+// One candidate triangle (the "intersection + any-hit" stage of a DXR traversal).  Returns true
+// when an any-hit ray is done (accepted occluder).  Closest hit: smallest t, ties -> smallest global
+// triangle id, which makes the result independent of traversal order.
+template <bool kAnyHit>
+PT_DEV bool test_triangle(const SceneDev& S, uint32_t rec, f3 o, f3 d, float tmin, float tmax, bool alpha, HitRec& h) {
+    const float4* T = reinterpret_cast<const float4*>(S.tris);
+    const float4 p0 = T[rec * 3 + 0];
+    const float4 p1 = T[rec * 3 + 1];
+    const float4 p2 = T[rec * 3 + 2];
+    float t, u, v;
+    if (!intersect_triangle(o, d, ld3(p0), ld3(p1), ld3(p2), &t, &u, &v)) return false;
+    const uint32_t gtri = fbits(p0.w);
+    if (!(t >= tmin)) return false;
+    if (kAnyHit) {
+        if (!(t <= tmax)) return false;
+    } else {
+        if (!(t < h.t || (t == h.t && gtri < h.tri))) return false;
+    }
+    const uint32_t geom = fbits(p1.w);
+    if (alpha && !(fbits(p2.w) & kTriOpaque) && !alpha_accepts(S, geom, gtri, u, v)) return false;
+    h.t = t;
+    h.tri = gtri;
+    h.b1 = u;
+    h.b2 = v;
+    h.geom = geom;
+    return kAnyHit;
+}
+
+PT_DEV f3 safe_inverse(f3 d) {
     f3 inv;
     inv.x = 1.0f / (fabsf(d.x) > 1e-20f ? d.x : copysignf(1e-20f, d.x));
     inv.y = 1.0f / (fabsf(d.y) > 1e-20f ? d.y : copysignf(1e-20f, d.y));
     inv.z = 1.0f / (fabsf(d.z) > 1e-20f ? d.z : copysignf(1e-20f, d.z));
+    return inv;
+}
+
+// BVH2 traversal ("while-while", Aila & Laine 2009): nearer child first, farther pushed on a per-lane
+// LDS stack (stk[sp * kBlock]).
+template <bool kAnyHit, bool kCount>
+PT_DEV bool traverse2(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, int* stk, HitRec& h,
+                      uint32_t& nvisit, uint32_t& ntest) {
+    const f3 inv = safe_inverse(d);
     const f3 ood = mul(o, inv);
-    h.t = tmax;
-    h.tri = kMiss;
-    h.b1 = h.b2 = 0.0f;
-    h.geom = 0;
     int node = 0;
     int sp = 0;
     const float4* N = reinterpret_cast<const float4*>(S.nodes);
@@ -251,38 +281,140 @@ PT_DEV bool traverse(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool
                 node = stk[sp * kBlock];
             }
         }
-        // leaf
         const uint32_t code = ~uint32_t(node);
         const uint32_t first = code >> 3, count = (code & 7u) + 1u;
-        const float4* T = reinterpret_cast<const float4*>(S.tris);
         for (uint32_t k = 0; k < count; ++k) {
             if (kCount) ++ntest;
-            const float4 p0 = T[(first + k) * 3 + 0];
-            const float4 p1 = T[(first + k) * 3 + 1];
-            const float4 p2 = T[(first + k) * 3 + 2];
-            float t, u, v;
-            if (!intersect_triangle(o, d, ld3(p0), ld3(p1), ld3(p2), &t, &u, &v)) continue;
-            const uint32_t gtri = fbits(p0.w);
-            if (!(t >= tmin)) continue;
-            if (kAnyHit) {
-                if (!(t <= tmax)) continue;
-            } else {
-                if (!(t < h.t || (t == h.t && gtri < h.tri))) continue;
-            }
-            const uint32_t geom = fbits(p1.w);
-            if (alpha && !(fbits(p2.w) & kTriOpaque) && !alpha_accepts(S, geom, gtri, u, v)) continue;
-            if (kAnyHit) return true;
-            h.t = t;
-            h.tri = gtri;
-            h.b1 = u;
-            h.b2 = v;
-            h.geom = geom;
+            if (test_triangle<kAnyHit>(S, first + k, o, d, tmin, tmax, alpha, h)) return true;
         }
         if (sp == 0) return kAnyHit ? false : h.tri != kMiss;
         --sp;
         node = stk[sp * kBlock];
     }
 }
+
+// Compressed BVH8 traversal (Ylitie, Karras & Laine 2017, adapted to one ray per wave64 lane).
+// A node visit intersects all 8 quantised child boxes at once; internal hits form a "node group"
+// (base_child, hit bits keyed by slot ^ octant, imask) visited highest key first (near to far), leaf
+// hits are tested right away.  The rest of a group is pushed when descending: <= 1 push per level,
+// 2 x 4 B per entry in LDS (stk[sp * kBlock], stk[(kTraversalStack8 + sp) * kBlock]).
+// The traversal is a resumable state machine (Ray8 + node + sp) so persistent kernels can advance
+// every lane by one node visit per iteration and refill lanes whose ray finished.
+struct Ray8 {
+    f3 o, d, inv, ood;
+    float tmin, tmax;
+    uint32_t oct;
+    bool alpha;
+};
+
+PT_DEV void ray8_init(Ray8& R, f3 o, f3 d, float tmin, float tmax, bool alpha, HitRec& h) {
+    R.o = o;
+    R.d = d;
+    R.inv = safe_inverse(d);
+    R.ood = mul(o, R.inv);
+    R.tmin = tmin;
+    R.tmax = tmax;
+    R.oct = (R.inv.x < 0.0f ? 4u : 0u) | (R.inv.y < 0.0f ? 2u : 0u) | (R.inv.z < 0.0f ? 1u : 0u);
+    R.alpha = alpha;
+    h.t = tmax;
+    h.tri = kMiss;
+    h.b1 = h.b2 = 0.0f;
+    h.geom = 0;
+}
+
+// Visits `node`, then selects the next node (pops when the current group is exhausted).  Returns true
+// when the ray is finished: h.tri != kMiss means hit (closest) / occluded (any-hit).
+template <bool kAnyHit, bool kCount>
+PT_DEV bool trav8_step(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp, int* stk, HitRec& h,
+                       uint32_t& nvisit, uint32_t& ntest) {
+    if (kCount) ++nvisit;
+    const uint4* N = reinterpret_cast<const uint4*>(S.nodes8);
+    const uint4 w0 = N[node * 5 + 0];
+    const uint4 w1 = N[node * 5 + 1];
+    const uint4 w2 = N[node * 5 + 2];
+    const uint4 w3 = N[node * 5 + 3];
+    const uint4 w4 = N[node * 5 + 4];
+    const float ax = __uint_as_float((w0.w & 0xFFu) << 23) * R.inv.x;
+    const float ay = __uint_as_float(((w0.w >> 8) & 0xFFu) << 23) * R.inv.y;
+    const float az = __uint_as_float(((w0.w >> 16) & 0xFFu) << 23) * R.inv.z;
+    const float bx = __builtin_fmaf(__uint_as_float(w0.x), R.inv.x, -R.ood.x);
+    const float by = __builtin_fmaf(__uint_as_float(w0.y), R.inv.y, -R.ood.y);
+    const float bz = __builtin_fmaf(__uint_as_float(w0.z), R.inv.z, -R.ood.z);
+    const float tmx = h.t;
+    uint32_t ihits = 0, thits = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const uint32_t sh = 8u * uint32_t(c & 3);
+        const uint32_t m = ((c < 4 ? w1.z : w1.w) >> sh) & 0xFFu;
+        const float qlx = float(((c < 4 ? w2.x : w2.y) >> sh) & 0xFFu);
+        const float qly = float(((c < 4 ? w2.z : w2.w) >> sh) & 0xFFu);
+        const float qlz = float(((c < 4 ? w3.x : w3.y) >> sh) & 0xFFu);
+        const float qhx = float(((c < 4 ? w3.z : w3.w) >> sh) & 0xFFu);
+        const float qhy = float(((c < 4 ? w4.x : w4.y) >> sh) & 0xFFu);
+        const float qhz = float(((c < 4 ? w4.z : w4.w) >> sh) & 0xFFu);
+        const float tlx = __builtin_fmaf(qlx, ax, bx), thx = __builtin_fmaf(qhx, ax, bx);
+        const float tly = __builtin_fmaf(qly, ay, by), thy = __builtin_fmaf(qhy, ay, by);
+        const float tlz = __builtin_fmaf(qlz, az, bz), thz = __builtin_fmaf(qhz, az, bz);
+        const float tn = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), R.tmin));
+        const float tf = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tmx));
+        const bool hit = m != 0u && tn <= tf;
+        if (hit) {
+            if (m & kMetaInternal) ihits |= 1u << ((m & 7u) ^ R.oct);
+            else thits |= ((1u << (m >> 5)) - 1u) << (m & 31u);
+        }
+    }
+    while (thits) {
+        const uint32_t b = uint32_t(__builtin_ctz(thits));
+        thits &= thits - 1u;
+        if (kCount) ++ntest;
+        if (test_triangle<kAnyHit>(S, w1.y + b, R.o, R.d, R.tmin, R.tmax, R.alpha, h)) return true;
+    }
+    uint32_t gbase = w1.x;
+    uint32_t gword = (ihits << 24) | (w0.w >> 24);
+    while (true) {
+        if (gword >> 24) {
+            const uint32_t k = 31u - uint32_t(__builtin_clz(gword));
+            gword &= ~(1u << k);
+            const uint32_t slot = (k - 24u) ^ R.oct;
+            node = gbase + uint32_t(__builtin_popcount(gword & 0xFFu & ((1u << slot) - 1u)));
+            if (gword >> 24) {
+                stk[sp * kBlock] = int(gbase);
+                stk[(kTraversalStack8 + sp) * kBlock] = int(gword);
+                ++sp;
+            }
+            return false;
+        }
+        if (sp == 0) return true;
+        --sp;
+        gbase = uint32_t(stk[sp * kBlock]);
+        gword = uint32_t(stk[(kTraversalStack8 + sp) * kBlock]);
+    }
+}
+
+template <bool kAnyHit, bool kCount>
+PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, int* stk, HitRec& h,
+                      uint32_t& nvisit, uint32_t& ntest) {
+    Ray8 R;
+    ray8_init(R, o, d, tmin, tmax, alpha, h);
+    uint32_t node = 0;
+    int sp = 0;
+    while (!trav8_step<kAnyHit, kCount>(S, R, node, sp, stk, h, nvisit, ntest)) {
+    }
+    return h.tri != kMiss;
+}
+
+template <int W, bool kAnyHit, bool kCount>
+PT_DEV bool traverse(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, int* stk, HitRec& h,
+                     uint32_t& nvisit, uint32_t& ntest) {
+    h.t = tmax;
+    h.tri = kMiss;
+    h.b1 = h.b2 = 0.0f;
+    h.geom = 0;
+    if (W == 8) return traverse8<kAnyHit, kCount>(S, o, d, tmin, tmax, alpha, stk, h, nvisit, ntest);
+    return traverse2<kAnyHit, kCount>(S, o, d, tmin, tmax, alpha, stk, h, nvisit, ntest);
+}
+
+static_assert(2 * kTraversalStack8 <= kTraversalStack, "BVH8 group stack must fit the LDS stack array");
 
 // ---- kernels --------------------------------------------------------------------------------------
 struct KArgs {
@@ -303,7 +435,17 @@ __global__ __launch_bounds__(kBlock) void k_raygen(KArgs A) {
     }
     const dxrpt_tile tl = A.P.tiles[lo];
     const uint32_t local = p - A.P.tile_prefix[lo];
-    const uint32_t lx = local % tl.w, ly = local / tl.w;
+    uint32_t lx, ly;
+    if ((tl.w & 7u) == 0u && (tl.h & 7u) == 0u) {
+        // one wave = one 8x8 pixel block (blocks row-major in the tile): coherent primary rays.
+        // Only the path-slot order changes; pixels, CMJ seeds and outputs do not.
+        const uint32_t blk = local >> 6, in = local & 63u, bw = tl.w >> 3;
+        lx = (blk % bw) * 8u + (in & 7u);
+        ly = (blk / bw) * 8u + (in >> 3);
+    } else {
+        lx = local % tl.w;
+        ly = local / tl.w;
+    }
     const uint32_t x = tl.x0 + lx, y = tl.y0 + ly;
     const uint32_t pixelIdx = y * A.P.width + x;
     const uint32_t accumIdx = uint32_t(tl.accum_offset) + ly * tl.accum_pitch + lx;
@@ -332,10 +474,11 @@ __global__ __launch_bounds__(kBlock) void k_raygen(KArgs A) {
     A.F.ps_thr[p] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
     A.F.ps_rad[p] = make_float4(0.0f, 0.0f, 0.0f, bitsf(0u));
     A.F.ps_pix[p] = make_uint2(pixelIdx, accumIdx);
+    A.F.sh_n[p] = 0u;
     if (p == 0) A.F.counters[1] = A.P.num_paths;
 }
 
-template <bool kCount>
+template <bool kCount, int W>
 __global__ __launch_bounds__(kBlock) void k_trace(KArgs A, int depth) {
     __shared__ int stack[kTraversalStack * kBlock];
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -348,7 +491,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(KArgs A, int depth) {
     const bool alpha = depth <= A.P.set.MaxAnyHitPathLength;
     HitRec h;
     uint32_t nv = 0, nt = 0;
-    traverse<false, kCount>(A.S, ld3(o4), ld3(d4), tmin, o4.w, alpha, stack + threadIdx.x, h, nv, nt);
+    traverse<W, false, kCount>(A.S, ld3(o4), ld3(d4), tmin, o4.w, alpha, stack + threadIdx.x, h, nv, nt);
     A.F.hit[i] = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
     if (kCount) {
         atomicAdd(&A.P.trav[0], (unsigned long long)nv);
@@ -356,13 +499,27 @@ __global__ __launch_bounds__(kBlock) void k_trace(KArgs A, int depth) {
     }
 }
 
-PT_DEV void emit_shadow(const KArgs& A, uint32_t i, uint32_t& n, f3 o, f3 d, float tmin, float tmax, f3 contrib,
-                        uint32_t pathSlot, bool forceOpaque) {
-    const size_t s = size_t(n) * A.F.capacity + i;
+// Shadow ray k of path p lives in slot [k * capacity + p]; the contribution is multiplied by the
+// visibility in place by k_shadow and added to the path's radiance, in k order, by the next k_shade
+// of that path or by k_accumulate (deterministic, no atomics on radiance).
+PT_DEV void emit_shadow(const KArgs& A, uint32_t pathSlot, uint32_t& n, f3 o, f3 d, float tmin, float tmax, f3 contrib,
+                        bool forceOpaque) {
+    const size_t s = size_t(n) * A.F.capacity + pathSlot;
     A.F.sh_org[s] = make_float4(o.x, o.y, o.z, tmax);
     A.F.sh_dir[s] = make_float4(d.x, d.y, d.z, tmin);
-    A.F.sh_con[s] = make_float4(contrib.x, contrib.y, contrib.z, bitsf((pathSlot << 1) | (forceOpaque ? 1u : 0u)));
+    A.F.sh_con[s] = make_float4(contrib.x, contrib.y, contrib.z, bitsf(forceOpaque ? 1u : 0u));
     ++n;
+}
+
+// Adds the (visibility-weighted) contributions of the path's pending shadow rays.
+PT_DEV void resolve_shadows(const KArgs& A, uint32_t pathSlot, float4& rad) {
+    const uint32_t n = A.F.sh_n[pathSlot];
+    for (uint32_t k = 0; k < n; ++k) {
+        const float4 c = A.F.sh_con[size_t(k) * A.F.capacity + pathSlot];
+        rad.x += c.x;
+        rad.y += c.y;
+        rad.z += c.z;
+    }
 }
 
 PT_DEV bool nonzero3(f3 c) { return !(c.x == 0.0f && c.y == 0.0f && c.z == 0.0f); }
@@ -379,6 +536,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(KArgs A, int depth) {
     const float4 hit = A.F.hit[i];
     const float4 thr4 = A.F.ps_thr[pathSlot];
     float4 rad4 = A.F.ps_rad[pathSlot];
+    resolve_shadows(A, pathSlot, rad4);  // shadow rays of depth-1 vertex
     const f3 pathThr = ld3(thr4);
     const f3 inDir = ld3(d4);
     const f3 inOrigin = ld3(o4);
@@ -468,7 +626,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(KArgs A, int depth) {
             const f3 c = calc_lighting(normalWS, sunDirection, f3{rtc.SunIrradiance[0], rtc.SunIrradiance[1], rtc.SunIrradiance[2]},
                                        diffuseAlbedo, specularAlbedo, roughness, positionWS, inOrigin, msEC);
             if (nonzero3(c))
-                emit_shadow(A, i, nsh, positionWS, D, kRayTMin, kFP32Max, mul(pathThr, c), pathSlot, shadowOpaque);
+                emit_shadow(A, pathSlot, nsh, positionWS, D, kRayTMin, kFP32Max, mul(pathThr, c), shadowOpaque);
         }
         // Spot lights (RayTrace.hlsl:265-313)
         if (set.RenderLights && !furnace && !directZero) {
@@ -489,8 +647,8 @@ __global__ __launch_bounds__(kBlock) void k_shade(KArgs A, int depth) {
                     const f3 c = calc_lighting(normalWS, surfaceToLight, intensity, diffuseAlbedo, specularAlbedo, roughness,
                                                positionWS, inOrigin, msEC);
                     if (nonzero3(c))
-                        emit_shadow(A, i, nsh, add(positionWS, scl(normalWS, 0.01f)), surfaceToLight, kSpotShadowNearClip,
-                                    distanceToLight - kSpotShadowNearClip, mul(pathThr, c), pathSlot, shadowOpaque);
+                        emit_shadow(A, pathSlot, nsh, add(positionWS, scl(normalWS, 0.01f)), surfaceToLight, kSpotShadowNearClip,
+                                    distanceToLight - kSpotShadowNearClip, mul(pathThr, c), shadowOpaque);
                 }
             }
         }
@@ -540,7 +698,8 @@ __global__ __launch_bounds__(kBlock) void k_shade(KArgs A, int depth) {
             const f3 sky = set.EnableSky ? sample_sky(A.S, rayDirWS) : f3{0.0f, 0.0f, 0.0f};
             const f3 c = mul(sky, throughput);
             if (nonzero3(c))
-                emit_shadow(A, i, nsh, positionWS, rayDirWS, kRayTMin, kFP32Max, mul(pathThr, c), pathSlot, depth + 1 > set.MaxAnyHitPathLength);
+                emit_shadow(A, pathSlot, nsh, positionWS, rayDirWS, kRayTMin, kFP32Max, mul(pathThr, c),
+                            depth + 1 > set.MaxAnyHitPathLength);
         }
     } while (false);
 
@@ -550,13 +709,23 @@ __global__ __launch_bounds__(kBlock) void k_shade(KArgs A, int depth) {
     rad4.z += pathThr.z * local.z;
     if (cont) rad4.w = bitsf(nextIsDiffuse ? 1u : 0u);  // payload.IsDiffuse for the next vertex
     A.F.ps_rad[pathSlot] = rad4;
-    A.F.sh_n[i] = nsh;
+    A.F.sh_n[pathSlot] = nsh;
 
-    // wave64 compaction of continuation rays into queue[depth+1]
+    // wave64 compaction (ballot + popcount + one atomic per wave) of the shadow rays into the shadow
+    // queue of this depth and of the continuation rays into queue[depth+1]
     const unsigned long long active = __ballot(1);
-    const unsigned long long m = __ballot(cont);
     const int lane = __lane_id();
     const int leader = __ffsll(static_cast<long long>(active)) - 1;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (uint32_t k = 0;; ++k) {
+        const unsigned long long mk = __ballot(nsh > k);
+        if (mk == 0ull) break;
+        uint32_t b = 0;
+        if (lane == leader) b = atomicAdd(&A.F.counters[16 + depth], uint32_t(__popcll(mk)));
+        b = __shfl(b, leader);
+        if (nsh > k) A.F.sh_queue[b + uint32_t(__popcll(mk & lt))] = k * A.F.capacity + pathSlot;
+    }
+    const unsigned long long m = __ballot(cont);
     uint32_t base = 0;
     if (lane == leader && m != 0ull) base = atomicAdd(&A.F.counters[depth + 1], uint32_t(__popcll(m)));
     base = __shfl(base, leader);
@@ -568,47 +737,113 @@ __global__ __launch_bounds__(kBlock) void k_shade(KArgs A, int depth) {
     }
 }
 
-// ShadowHitShader / ShadowMissShader / ShadowAnyHitShader (RayTrace.hlsl:497-507, 532-542)
-template <bool kCount>
+// ShadowHitShader / ShadowMissShader / ShadowAnyHitShader (RayTrace.hlsl:497-507, 532-542):
+// one thread per queued shadow ray (grid-stride); occluded -> contribution * 0 (keeps NaN/Inf).
+template <bool kCount, int W>
 __global__ __launch_bounds__(kBlock) void k_shadow(KArgs A, int depth) {
     __shared__ int stack[kTraversalStack * kBlock];
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= A.F.counters[depth]) return;
-    const uint32_t n = A.F.sh_n[i];
-    if (n == 0) return;
-    uint32_t pathSlot = 0;
+    const uint32_t count = A.F.counters[16 + depth];
     uint32_t nv = 0, nt = 0;
-    f3 acc = f3{0.0f, 0.0f, 0.0f};
-    for (uint32_t k = 0; k < n; ++k) {
-        const size_t s = size_t(k) * A.F.capacity + i;
-        const float4 o4 = A.F.sh_org[s];
-        const float4 d4 = A.F.sh_dir[s];
-        const float4 c4 = A.F.sh_con[s];
-        const uint32_t tag = fbits(c4.w);
-        pathSlot = tag >> 1;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < count; i += gridDim.x * kBlock) {
+        const uint32_t slot = A.F.sh_queue[i];
+        const float4 o4 = A.F.sh_org[slot];
+        const float4 d4 = A.F.sh_dir[slot];
+        const float4 c4 = A.F.sh_con[slot];
         HitRec h;
         const bool occluded =
-            traverse<true, kCount>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, (tag & 1u) == 0u, stack + threadIdx.x, h, nv, nt);
-        const float vis = occluded ? 0.0f : 1.0f;
-        acc = add(acc, scl(ld3(c4), vis));
+            traverse<W, true, kCount>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stack + threadIdx.x, h, nv, nt);
+        if (occluded) A.F.sh_con[slot] = make_float4(c4.x * 0.0f, c4.y * 0.0f, c4.z * 0.0f, c4.w);
     }
-    atomicAdd(&A.F.counters[16 + depth], n);
     if (kCount) {
         atomicAdd(&A.P.trav[2], (unsigned long long)nv);
         atomicAdd(&A.P.trav[3], (unsigned long long)nt);
     }
-    float4 r = A.F.ps_rad[pathSlot];
-    r.x += acc.x;
-    r.y += acc.y;
-    r.z += acc.z;
-    A.F.ps_rad[pathSlot] = r;
+}
+
+// Persistent BVH8 traversal for the radiance (kShadow = false) and shadow (true) queues of one depth.
+// The grid is sized to the resident capacity.  Wave w owns the 64-ray chunks w, w + nwaves,
+// w + 2 nwaves, ... of the queue (coherent within a chunk, balanced over the image) and advances every
+// lane by one node visit per iteration; lanes whose ray finished are refilled from the wave's sequence
+// once >= refill lanes are idle (Aila & Laine 2009, "replacing terminated rays").  No atomics.
+template <bool kCount, bool kShadow>
+__global__ __launch_bounds__(kBlock) void k_traverse8p(KArgs A, int depth) {
+    __shared__ int stack[kTraversalStack * kBlock];
+    int* stk = stack + threadIdx.x;
+    const uint32_t count = kShadow ? A.F.counters[16 + depth] : A.F.counters[depth];
+    const uint32_t nwaves = gridDim.x * (kBlock / 64u);
+    const uint32_t wave = blockIdx.x * (kBlock / 64u) + threadIdx.x / 64u;
+    const uint32_t nchunks = (count + 63u) / 64u;
+    const uint32_t mychunks = nchunks > wave ? (nchunks - wave + nwaves - 1u) / nwaves : 0u;
+    const uint32_t end = mychunks * 64u;  // length of this wave's item sequence j = 0 .. end-1
+    uint32_t next = 0;
+    const uint32_t refill = A.P.refill_lanes;
+    const unsigned long long lt = (1ull << __lane_id()) - 1ull;
+    // Radiance rays: FORCE_OPAQUE iff PathLength > MaxAnyHitPathLength (RayTrace.hlsl:132, 401);
+    // primary rays start at TMin 0 (:118), continuation rays at 1e-5 (:382).
+    const bool alphaR = depth <= A.P.set.MaxAnyHitPathLength;
+    const float tminR = depth == 1 ? 0.0f : kRayTMin;
+    bool active = false;
+    uint32_t item = 0;
+    Ray8 R;
+    HitRec h;
+    uint32_t node = 0;
+    int sp = 0;
+    uint32_t nv = 0, nt = 0;
+    while (true) {
+        const unsigned long long idle = __ballot(!active);
+        const uint32_t nidle = uint32_t(__popcll(idle));
+        if (next < end && nidle >= refill) {
+            if (!active) {
+                const uint32_t j = next + uint32_t(__popcll(idle & lt));
+                const uint32_t idx = (wave + (j >> 6) * nwaves) * 64u + (j & 63u);
+                if (j < end && idx < count) {
+                    if (kShadow) {
+                        item = A.F.sh_queue[idx];
+                        const float4 o4 = A.F.sh_org[item];
+                        const float4 d4 = A.F.sh_dir[item];
+                        const bool alpha = fbits(A.F.sh_con[item].w) == 0u;
+                        ray8_init(R, ld3(o4), ld3(d4), d4.w, o4.w, alpha, h);
+                    } else {
+                        item = idx;
+                        const float4 o4 = A.F.q_org[depth & 1][idx];
+                        const float4 d4 = A.F.q_dir[depth & 1][idx];
+                        ray8_init(R, ld3(o4), ld3(d4), tminR, o4.w, alphaR, h);
+                    }
+                    node = 0;
+                    sp = 0;
+                    active = true;
+                }
+            }
+            next += nidle;
+        }
+        if (__ballot(active) == 0ull) {
+            if (next >= end) break;
+            continue;
+        }
+        if (active && trav8_step<kShadow, kCount>(A.S, R, node, sp, stk, h, nv, nt)) {
+            active = false;
+            if (kShadow) {
+                if (h.tri != kMiss) {  // occluded: contribution * 0 (keeps NaN/Inf like the reference)
+                    const float4 c4 = A.F.sh_con[item];
+                    A.F.sh_con[item] = make_float4(c4.x * 0.0f, c4.y * 0.0f, c4.z * 0.0f, c4.w);
+                }
+            } else {
+                A.F.hit[item] = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
+            }
+        }
+    }
+    if (kCount) {
+        atomicAdd(&A.P.trav[kShadow ? 2 : 0], (unsigned long long)nv);
+        atomicAdd(&A.P.trav[kShadow ? 3 : 1], (unsigned long long)nt);
+    }
 }
 
 // RayTrace.hlsl:140-148
 __global__ __launch_bounds__(kBlock) void k_accumulate(KArgs A) {
     const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
     if (p >= A.P.num_paths) return;
-    const float4 r = A.F.ps_rad[p];
+    float4 r = A.F.ps_rad[p];
+    resolve_shadows(A, p, r);  // shadow rays of the last vertex
     const uint32_t a = A.F.ps_pix[p].y;
     const float rx = fminf(fmaxf(r.x, 0.0f), kFP16Max);
     const float ry = fminf(fmaxf(r.y, 0.0f), kFP16Max);
@@ -621,6 +856,7 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(KArgs A) {
 
 // Arbitrary ray queries (dxrpt_trace_rays): flags bit0 = any-hit (shadow) semantics,
 // bit1 = alpha test enabled (not FORCE_OPAQUE).
+template <int W>
 __global__ __launch_bounds__(kBlock) void k_trace_rays(SceneDev S, const float4* rays, uint32_t n, uint32_t flags, float4* hits) {
     __shared__ int stack[kTraversalStack * kBlock];
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -630,10 +866,10 @@ __global__ __launch_bounds__(kBlock) void k_trace_rays(SceneDev S, const float4*
     uint32_t nv = 0, nt = 0;
     const bool alpha = (flags & 2u) != 0u;
     if (flags & 1u) {
-        bool occ = traverse<true, false>(S, ld3(a), ld3(b), a.w, b.w, alpha, stack + threadIdx.x, h, nv, nt);
+        bool occ = traverse<W, true, false>(S, ld3(a), ld3(b), a.w, b.w, alpha, stack + threadIdx.x, h, nv, nt);
         hits[i] = make_float4(occ ? 1.0f : -1.0f, 0.0f, 0.0f, bitsf(kMiss));
     } else {
-        bool any = traverse<false, false>(S, ld3(a), ld3(b), a.w, b.w, alpha, stack + threadIdx.x, h, nv, nt);
+        bool any = traverse<W, false, false>(S, ld3(a), ld3(b), a.w, b.w, alpha, stack + threadIdx.x, h, nv, nt);
         hits[i] = any ? make_float4(h.t, h.b1, h.b2, bitsf(h.tri)) : make_float4(-1.0f, 0.0f, 0.0f, bitsf(kMiss));
     }
 }
@@ -656,13 +892,33 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
     mark();
     const int L = fp.set.MaxPathLength < 2 ? 2 : fp.set.MaxPathLength;
     for (int d = 1; d <= L - 1; ++d) {
-        if (count) hipLaunchKernelGGL(k_trace<true>, dim3(g), dim3(kBlock), 0, stream, A, d);
-        else hipLaunchKernelGGL(k_trace<false>, dim3(g), dim3(kBlock), 0, stream, A, d);
+        const bool w8 = scene.width == 8;
+        const bool pers = w8 && fp.persistent_blocks > 0;
+        const uint32_t gp = fp.persistent_blocks;
+        if (w8 && !pers) {
+            if (count) hipLaunchKernelGGL((k_trace<true, 8>), dim3(g), dim3(kBlock), 0, stream, A, d);
+            else hipLaunchKernelGGL((k_trace<false, 8>), dim3(g), dim3(kBlock), 0, stream, A, d);
+        } else if (pers) {
+            if (count) hipLaunchKernelGGL((k_traverse8p<true, false>), dim3(gp), dim3(kBlock), 0, stream, A, d);
+            else hipLaunchKernelGGL((k_traverse8p<false, false>), dim3(gp), dim3(kBlock), 0, stream, A, d);
+        } else {
+            if (count) hipLaunchKernelGGL((k_trace<true, 2>), dim3(g), dim3(kBlock), 0, stream, A, d);
+            else hipLaunchKernelGGL((k_trace<false, 2>), dim3(g), dim3(kBlock), 0, stream, A, d);
+        }
         mark();
         hipLaunchKernelGGL(k_shade, dim3(g), dim3(kBlock), 0, stream, A, d);
         mark();
-        if (count) hipLaunchKernelGGL(k_shadow<true>, dim3(g), dim3(kBlock), 0, stream, A, d);
-        else hipLaunchKernelGGL(k_shadow<false>, dim3(g), dim3(kBlock), 0, stream, A, d);
+        const uint32_t gs = std::min<uint32_t>(grid_for(fp.num_paths * fb.shadow_slots), kShadowGrid);
+        if (w8 && !pers) {
+            if (count) hipLaunchKernelGGL((k_shadow<true, 8>), dim3(gs), dim3(kBlock), 0, stream, A, d);
+            else hipLaunchKernelGGL((k_shadow<false, 8>), dim3(gs), dim3(kBlock), 0, stream, A, d);
+        } else if (pers) {
+            if (count) hipLaunchKernelGGL((k_traverse8p<true, true>), dim3(gp), dim3(kBlock), 0, stream, A, d);
+            else hipLaunchKernelGGL((k_traverse8p<false, true>), dim3(gp), dim3(kBlock), 0, stream, A, d);
+        } else {
+            if (count) hipLaunchKernelGGL((k_shadow<true, 2>), dim3(gs), dim3(kBlock), 0, stream, A, d);
+            else hipLaunchKernelGGL((k_shadow<false, 2>), dim3(gs), dim3(kBlock), 0, stream, A, d);
+        }
         mark();
     }
     hipLaunchKernelGGL(k_accumulate, dim3(g), dim3(kBlock), 0, stream, A);
@@ -673,7 +929,10 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
 hipError_t launch_trace_rays(const SceneDev& scene, const float4* rays, uint32_t n, uint32_t flags, float4* hits,
                              hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_trace_rays, dim3(grid_for(n)), dim3(kBlock), 0, stream, scene, rays, n, flags, hits);
+    if (scene.width == 8)
+        hipLaunchKernelGGL((k_trace_rays<8>), dim3(grid_for(n)), dim3(kBlock), 0, stream, scene, rays, n, flags, hits);
+    else
+        hipLaunchKernelGGL((k_trace_rays<2>), dim3(grid_for(n)), dim3(kBlock), 0, stream, scene, rays, n, flags, hits);
     return hipGetLastError();
 }
 

@@ -38,6 +38,32 @@ __attribute__((always_inline)) inline int32_t encode_leaf(uint32_t first, uint32
     return ~static_cast<int32_t>((first << 3) | (count - 1u));
 }
 
+// Compressed 8-wide node, 80 B (five 16-B words), after Ylitie et al. 2017 ("Efficient incoherent
+// ray traversal on GPUs through compressed wide BVHs"): child boxes quantised to 8 bits against the
+// node's origin p and per-axis power-of-two scales 2^(e-127).
+//   w0 = (p.x, p.y, p.z, e.x | e.y<<8 | e.z<<16 | imask<<24)     imask bit s = slot s is internal
+//   w1 = (base_child, base_tri, meta[0..3], meta[4..7])
+//   w2..w4 = qlo_x[8], qlo_y[8], qlo_z[8], qhi_x[8], qhi_y[8], qhi_z[8]
+// meta[s]: 0 = empty; 0x80 | s = internal child (stored at base_child + popcount(imask below s));
+//          (count << 5) | offset = leaf with count (1..3) triangles at base_tri + offset (offset < 24).
+// Slots are assigned so that visiting keys (slot ^ octant(ray)) from high to low is roughly
+// front-to-back: slot s is the nearest child for rays whose octant is 7 ^ s.
+struct Bvh8Node {
+    float p[3];
+    uint8_t e[3];
+    uint8_t imask;
+    uint32_t base_child;
+    uint32_t base_tri;
+    uint8_t meta[8];
+    uint8_t qlo[3][8];
+    uint8_t qhi[3][8];
+};
+static_assert(sizeof(Bvh8Node) == 80, "Bvh8Node must be 80 B");
+
+constexpr int kMaxLeafTris8 = 3;
+constexpr int kTraversalStack8 = 16;  // LDS group-stack entries per lane; builder caps BVH8 depth to fit.
+constexpr uint8_t kMetaInternal = 0x80;
+
 // Leaf triangle record, 48 B.
 //   p0 = (v0.x, v0.y, v0.z, bits(gtri))      gtri = global triangle id = IdxOffset/3 + PrimitiveIndex
 //   p1 = (e1.x, e1.y, e1.z, bits(geometry))  geometry = GeometryIndex()

@@ -218,6 +218,8 @@ typedef struct dxrpt_bvh_info {
     uint32_t max_depth;
     uint32_t node_bytes;      /* bytes per node of the layout traversed on the GPU */
     uint32_t tri_bytes;       /* bytes per leaf triangle record */
+    uint32_t width;           /* 2 (BVH2, 64-B nodes) or 8 (compressed BVH8, 80-B nodes) */
+    uint32_t pad;
     double build_ms;          /* host build time */
     double sah_cost;
 } dxrpt_bvh_info;
@@ -257,6 +259,9 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 /* ---- options ---------------------------------------------------------------------------------- */
 #define DXRPT_OPT_COUNT_TRAVERSAL 1u  /* 1: instrumented kernels count node visits / triangle tests (slower) */
 #define DXRPT_OPT_KERNEL_TIMING 2u    /* 1: record a hipEvent after every launch of dxrpt_render */
+#define DXRPT_OPT_BVH_WIDTH 3u        /* 2 or 8 (default): layout built by the next dxrpt_build_bvh */
+#define DXRPT_OPT_TRAVERSAL_MODE 4u   /* BVH8: 0 = one thread per ray (default), 1 = persistent waves */
+#define DXRPT_OPT_REFILL_LANES 5u     /* persistent mode: refill a wave once this many lanes are idle */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""A/B of traversal variants in ONE process (interleaved rounds, median per variant), on the bench
+workload (Sponza proxy 1920x1080, L=3).  Prints per-kernel ms per frame from the HIP-event timings.
+
+    python scripts/ab_variants.py [--frames 16] [--rounds 3] [--variants w8m0,w8m1r16,...]
+variant syntax: w<2|8> m<0|1> [r<lanes>]
+"""
+import argparse
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def parse(v):
+    w = int(v[1:v.index("m")])
+    rest = v[v.index("m") + 1:]
+    if "r" in rest:
+        m, r = rest.split("r")
+        return w, int(m), int(r)
+    return w, int(rest), 16
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", default="w2m0,w8m0,w8m1r16,w8m1r32,w8m1r48")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--L", type=int, default=3)
+    ap.add_argument("--scene", default="sponza")
+    args = ap.parse_args()
+    import torch
+    import dxrpathtracer_amd as D
+    import dxrpathtracer_amd._abi as A
+    from dxrpathtracer_amd.tracer import DXRPathTracer
+
+    W, H = args.width, args.height
+    sc = D.Scene(args.scene)
+    st = sc.settings(MaxPathLength=args.L)
+    sky = D.make_sky(st)
+    tracers = {}
+    for width in sorted({parse(v)[0] for v in args.variants.split(",")}):
+        t = DXRPathTracer(0)
+        t.set_option(A.OPT_BVH_WIDTH, width)
+        t.initialize_scene(sc, sky)
+        t.build_rt_acceleration_structure()
+        tracers[width] = t
+    accum = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+    consts = [D.make_constants(sc, st, sky, W, H, s) for s in range(16)]
+    lights = D.make_lights(sc)
+    sh = torch.cuda.current_stream().cuda_stream
+    res = {v: [] for v in args.variants.split(",")}
+    for rnd in range(args.rounds):
+        for v in res:
+            w, m, r = parse(v)
+            t = tracers[w]
+            t.set_option(A.OPT_TRAVERSAL_MODE, m)
+            t.set_option(A.OPT_REFILL_LANES, r)
+            for f in range(3):
+                t.render_raw(consts[f], st, accum.data_ptr(), W, H, stream=sh, lights=lights)
+            torch.cuda.synchronize()
+            t.set_option(A.OPT_KERNEL_TIMING, 1)
+            t.reset_timing()
+            t0 = time.perf_counter()
+            for f in range(args.frames):
+                t.render_raw(consts[f % 16], st, accum.data_ptr(), W, H, stream=sh, lights=lights)
+            torch.cuda.synchronize()
+            wall = (time.perf_counter() - t0) / args.frames * 1e3
+            s = t.stats()
+            t.set_option(A.OPT_KERNEL_TIMING, 0)
+            n = max(1, s.timed_frames)
+            res[v].append((wall, [s.kernel_ms[k] / n for k in range(A.K_COUNT)]))
+    print(f"{args.scene} {W}x{H} L={args.L}: median of {args.rounds} rounds x {args.frames} frames (ms/frame)")
+    print(f"{'variant':12s} {'wall':>8s} " + " ".join(f"{k:>12s}" for k in A.KERNEL_NAMES))
+    for v, rows in res.items():
+        wall = statistics.median(r[0] for r in rows)
+        ks = [statistics.median(r[1][k] for r in rows) for k in range(A.K_COUNT)]
+        print(f"{v:12s} {wall:8.3f} " + " ".join(f"{x:12.3f}" for x in ks))
+
+
+if __name__ == "__main__":
+    main()

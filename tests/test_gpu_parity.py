@@ -23,19 +23,23 @@ pytestmark = pytest.mark.gpu
 _TRACERS = {}
 
 
-def tracer(name):
-    if name not in _TRACERS:
+def tracer(name, width=8):
+    """A context per (scene, BVH width): 8 = compressed BVH8 (default), 2 = BVH2."""
+    if (name, width) not in _TRACERS:
         sc, sky = scene_bundle(name)
         t = DXRPathTracer(0)
+        t.set_option(A.OPT_BVH_WIDTH, width)
         t.initialize_scene(sc, sky)
-        t.build_rt_acceleration_structure()
-        _TRACERS[name] = t
-    return _TRACERS[name]
+        info = t.build_rt_acceleration_structure()
+        assert info.width == width
+        _TRACERS[(name, width)] = t
+    return _TRACERS[(name, width)]
 
 
-def gpu_render(torch, name, W, H, settings, sample, tiles=None, n_out=None, accum=None, rtc=None, lights=None):
+def gpu_render(torch, name, W, H, settings, sample, tiles=None, n_out=None, accum=None, rtc=None, lights=None,
+               width=8):
     sc, sky = scene_bundle(name)
-    t = tracer(name)
+    t = tracer(name, width)
     if rtc is None:
         rtc = D.make_constants(sc, settings, sky, W, H, sample)
     n = n_out if n_out is not None else W * H
@@ -56,11 +60,11 @@ def crop_tiles(crops, W):
     return tiles, off
 
 
-def check_crops(torch, name, W, H, crops, sample=0, **overrides):
+def check_crops(torch, name, W, H, crops, sample=0, width=8, **overrides):
     sc, sky = scene_bundle(name)
     st = sc.settings(**overrides)
     tiles, n = crop_tiles(crops, W)
-    out = gpu_render(torch, name, W, H, st, sample, tiles=tiles, n_out=n).cpu().numpy()
+    out = gpu_render(torch, name, W, H, st, sample, tiles=tiles, n_out=n, width=width).cpu().numpy()
     rtc = D.make_constants(sc, st, sky, W, H, sample)
     off = 0
     for (x0, y0, w, h) in crops:
@@ -88,10 +92,10 @@ def test_boxtest_256_full_frame(torch_cuda):
 SPONZA_CROPS = [(900, 480, 96, 96), (0, 0, 64, 64), (1700, 900, 80, 64), (300, 700, 128, 48), (1500, 200, 64, 96)]
 
 
-@pytest.mark.parametrize("sample", [0, 7])
-def test_sponza_1080p_L3_crops(torch_cuda, sample):
-    # BASELINE.json metric config: Sponza(-proxy) 1920x1080, MaxPathLength 3
-    check_crops(torch_cuda, "sponza", 1920, 1080, SPONZA_CROPS, sample=sample, MaxPathLength=3)
+@pytest.mark.parametrize("sample,width", [(0, 8), (7, 8), (7, 2)])
+def test_sponza_1080p_L3_crops(torch_cuda, sample, width):
+    # BASELINE.json metric config: Sponza(-proxy) 1920x1080, MaxPathLength 3 (both BVH layouts)
+    check_crops(torch_cuda, "sponza", 1920, 1080, SPONZA_CROPS, sample=sample, width=width, MaxPathLength=3)
 
 
 def test_sponza_720p_L3_crops(torch_cuda):
@@ -108,11 +112,11 @@ def test_sponza_4k_L6_crops(torch_cuda):
     check_crops(torch_cuda, "sponza", 3840, 2160, [(1900, 1000, 64, 64), (3000, 1800, 48, 48)], sample=2, MaxPathLength=6)
 
 
-@pytest.mark.parametrize("any_hit_len", [1, 8])
-def test_suntemple_alpha_tested_crops(torch_cuda, any_hit_len):
+@pytest.mark.parametrize("any_hit_len,width", [(1, 8), (8, 8), (1, 2)])
+def test_suntemple_alpha_tested_crops(torch_cuda, any_hit_len, width):
     # BASELINE.json configs[3]: alpha-tested foliage (any-hit path)
     check_crops(torch_cuda, "suntemple", 1920, 1080, [(800, 400, 96, 96), (1200, 600, 96, 64), (100, 200, 64, 64)],
-                sample=1, MaxPathLength=3, MaxAnyHitPathLength=any_hit_len)
+                sample=1, width=width, MaxPathLength=3, MaxAnyHitPathLength=any_hit_len)
 
 
 def test_white_furnace_full_frame(torch_cuda):
@@ -199,9 +203,10 @@ def _random_rays(rng, n, lo, hi):
     return rays
 
 
+@pytest.mark.parametrize("width", [2, 8])
 @pytest.mark.parametrize("name,flags", [("sponza", 0), ("sponza", A.TRACE_ANY_HIT), ("suntemple", A.TRACE_ALPHA),
                                         ("suntemple", A.TRACE_ANY_HIT | A.TRACE_ALPHA), ("boxtest", 0)])
-def test_trace_rays_matches_oracle_exactly(torch_cuda, name, flags):
+def test_trace_rays_matches_oracle_exactly(torch_cuda, name, flags, width):
     # TraceRay (RayTrace.hlsl:138,258,305,407,425) on random rays: same hit, same t, same barycentrics
     torch = torch_cuda
     rng = np.random.default_rng(42)
@@ -211,8 +216,8 @@ def test_trace_rays_matches_oracle_exactly(torch_cuda, name, flags):
     ref = oracle_scene(name).trace_rays(rays, flags)
     dr = torch.from_numpy(rays).cuda()
     dh = torch.zeros((rays.shape[0], 4), dtype=torch.float32, device="cuda")
-    tracer(name).trace_rays(dr.data_ptr(), rays.shape[0], flags, dh.data_ptr(),
-                            torch.cuda.current_stream().cuda_stream)
+    tracer(name, width).trace_rays(dr.data_ptr(), rays.shape[0], flags, dh.data_ptr(),
+                                   torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     got = dh.cpu().numpy()
     hits = ref[:, 0] >= 0
