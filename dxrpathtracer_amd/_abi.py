@@ -72,8 +72,8 @@ class Tile(C.Structure):
                 ("accum_pitch", u32), ("pad", u32)]
 
 
-K_RAYGEN, K_TRACE, K_SHADE, K_SHADOW, K_ACCUMULATE, K_COUNT = range(6)
-KERNEL_NAMES = ("k_raygen", "k_trace", "k_shade", "k_shadow", "k_accumulate")
+K_RAYGEN, K_TRACE, K_SHADE, K_SHADOW, K_ACCUMULATE, K_RESOLVE, K_COUNT = range(7)
+KERNEL_NAMES = ("k_raygen", "k_trace", "k_shade", "k_shadow", "k_accumulate", "k_resolve")
 OPT_COUNT_TRAVERSAL, OPT_KERNEL_TIMING, OPT_BVH_WIDTH, OPT_TRAVERSAL_MODE, OPT_REFILL_LANES = 1, 2, 3, 4, 5
 
 

@@ -76,7 +76,8 @@ struct dxrpt_ctx {
     DevBuf d_vertices, d_indices, d_geos, d_mats, d_texdesc, d_texels, d_sky, d_lut, d_nodes, d_nodes8, d_tris;
     DevBuf d_lights, d_tiles, d_tile_prefix;
     // per-frame wavefront buffers
-    DevBuf f_thr, f_rad, f_pix, f_qorg0, f_qorg1, f_qdir0, f_qdir1, f_hit, f_shn, f_shq, f_shorg, f_shdir, f_shcon, f_counters;
+    DevBuf f_pix, f_pxrad, f_hit, f_fwd, f_shn, f_shq, f_shorg, f_shdir, f_shcon, f_counters;
+    DevBuf f_q[2][5];  // RayQueue org, dir, thr, rad, pix per depth parity
     FrameBuffers fb;
     dxrpt_bvh_info bvh{};
     std::vector<dxrpt_tile> tiles_cache;
@@ -108,9 +109,11 @@ struct dxrpt_ctx {
 
     ~dxrpt_ctx() {
         DevBuf* all[] = {&d_vertices, &d_indices, &d_geos, &d_mats, &d_texdesc, &d_texels, &d_sky, &d_lut, &d_nodes,
-                         &d_nodes8, &d_tris, &d_lights, &d_tiles, &d_tile_prefix, &f_thr, &f_rad, &f_pix, &f_qorg0, &f_qorg1,
-                         &f_qdir0, &f_qdir1, &f_hit, &f_shn, &f_shq, &f_shorg, &f_shdir, &f_shcon, &f_counters};
+                         &d_nodes8, &d_tris, &d_lights, &d_tiles, &d_tile_prefix, &f_pix, &f_pxrad, &f_hit, &f_fwd,
+                         &f_shn, &f_shq, &f_shorg, &f_shdir, &f_shcon, &f_counters};
         for (DevBuf* b : all) b->release();
+        for (auto& qb : f_q)
+            for (DevBuf& b : qb) b.release();
         d_trav.release();
         for (auto& f : ring)
             for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
@@ -159,6 +162,11 @@ SceneDev scene_dev(const dxrpt_ctx* c) {
     s.nodes = c->d_nodes.as<BvhNode>();
     s.nodes8 = c->d_nodes8.as<Bvh8Node>();
     s.width = c->built_width;
+    {
+        const uint32_t entries = std::min<uint32_t>(c->bvh.max_depth + 1u,
+                                                    c->built_width == 8 ? uint32_t(kTraversalStack8) : uint32_t(kTraversalStack));
+        s.stack_ints = c->built_width == 8 ? 2u * entries : entries;
+    }
     s.tris = c->d_tris.as<TriRecord>();
     s.vertices = c->d_vertices.as<dxrpt_mesh_vertex>();
     s.indices = c->d_indices.as<uint32_t>();
@@ -183,30 +191,34 @@ void upload_textures(dxrpt_ctx* c) {
 void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
     FrameBuffers& f = c->fb;
     if (paths <= f.capacity && slots <= f.shadow_slots && f.counters) return;
-    uint32_t cap = std::max(paths, f.capacity);
-    uint32_t sl = std::max(slots, std::max(f.shadow_slots, 2u));
-    c->f_thr.ensure(size_t(cap) * 16);
-    c->f_rad.ensure(size_t(cap) * 16);
+    const uint32_t cap = std::max(paths, f.capacity);
+    const uint32_t sl = std::max(slots, std::max(f.shadow_slots, 2u));
+    const uint32_t cap_r = queue_shard_capacity(cap);
+    const size_t qsize = size_t(kQueueShards) * cap_r;
+    require(qsize * sl < (size_t(1) << 32), "frame too large for 32-bit shadow slot ids", DXRPT_E_INVALID_ARG);
     c->f_pix.ensure(size_t(cap) * 8);
-    c->f_qorg0.ensure(size_t(cap) * 16);
-    c->f_qorg1.ensure(size_t(cap) * 16);
-    c->f_qdir0.ensure(size_t(cap) * 16);
-    c->f_qdir1.ensure(size_t(cap) * 16);
-    c->f_hit.ensure(size_t(cap) * 16);
-    c->f_shn.ensure(size_t(cap) * 4);
-    c->f_shq.ensure(size_t(cap) * sl * 4);
-    c->f_shorg.ensure(size_t(cap) * sl * 16);
-    c->f_shdir.ensure(size_t(cap) * sl * 16);
-    c->f_shcon.ensure(size_t(cap) * sl * 16);
-    c->f_counters.ensure(64 * sizeof(uint32_t));
-    f.ps_thr = c->f_thr.as<float4>();
-    f.ps_rad = c->f_rad.as<float4>();
+    c->f_pxrad.ensure(size_t(cap) * 16);
+    for (int b = 0; b < 2; ++b) {
+        for (int k = 0; k < 4; ++k) c->f_q[b][k].ensure(qsize * 16);
+        c->f_q[b][4].ensure(qsize * 4);
+        f.q[b].org = c->f_q[b][0].as<float4>();
+        f.q[b].dir = c->f_q[b][1].as<float4>();
+        f.q[b].thr = c->f_q[b][2].as<float4>();
+        f.q[b].rad = c->f_q[b][3].as<float4>();
+        f.q[b].pix = c->f_q[b][4].as<uint32_t>();
+    }
+    c->f_hit.ensure(qsize * 16);
+    c->f_fwd.ensure(qsize * 4);
+    c->f_shn.ensure(qsize * 4);
+    c->f_shq.ensure(qsize * sl * 4);
+    c->f_shorg.ensure(qsize * sl * 16);
+    c->f_shdir.ensure(qsize * sl * 16);
+    c->f_shcon.ensure(qsize * sl * 16);
+    c->f_counters.ensure(2 * kMaxDepthQueues * kQueueShards * sizeof(uint32_t));
     f.ps_pix = c->f_pix.as<uint2>();
-    f.q_org[0] = c->f_qorg0.as<float4>();
-    f.q_org[1] = c->f_qorg1.as<float4>();
-    f.q_dir[0] = c->f_qdir0.as<float4>();
-    f.q_dir[1] = c->f_qdir1.as<float4>();
+    f.px_rad = c->f_pxrad.as<float4>();
     f.hit = c->f_hit.as<float4>();
+    f.fwd = c->f_fwd.as<uint32_t>();
     f.sh_n = c->f_shn.as<uint32_t>();
     f.sh_queue = c->f_shq.as<uint32_t>();
     f.sh_org = c->f_shorg.as<float4>();
@@ -214,6 +226,8 @@ void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
     f.sh_con = c->f_shcon.as<float4>();
     f.counters = c->f_counters.as<uint32_t>();
     f.capacity = cap;
+    f.cap_r = cap_r;
+    f.qsize = uint32_t(qsize);
     f.shadow_slots = sl;
 }
 
@@ -234,10 +248,12 @@ void harvest(dxrpt_ctx* c, dxrpt_ctx::FrameEvents& f) {
         c->kernel_ms[DXRPT_K_TRACE] += span(e, e + 1);
         c->kernel_ms[DXRPT_K_SHADE] += span(e + 1, e + 2);
         c->kernel_ms[DXRPT_K_SHADOW] += span(e + 2, e + 3);
+        c->kernel_ms[DXRPT_K_RESOLVE] += span(e + 3, e + 4);
         c->kernel_launches[DXRPT_K_TRACE]++;
         c->kernel_launches[DXRPT_K_SHADE]++;
         c->kernel_launches[DXRPT_K_SHADOW]++;
-        e += 3;
+        c->kernel_launches[DXRPT_K_RESOLVE]++;
+        e += 4;
     }
     c->kernel_ms[DXRPT_K_ACCUMULATE] += span(e, e + 1);
     c->kernel_launches[DXRPT_K_ACCUMULATE]++;
@@ -619,8 +635,11 @@ int dxrpt_get_stats(dxrpt_ctx* ctx, dxrpt_stats* out) {
     return guarded(ctx, [&] {
         require(ctx->rendered, "dxrpt_get_stats: nothing rendered yet", DXRPT_E_STATE);
         HIP_CHECK(hipStreamSynchronize(ctx->last_stream));
-        uint32_t cnt[32];
-        HIP_CHECK(hipMemcpy(cnt, ctx->fb.counters, sizeof(cnt), hipMemcpyDeviceToHost));
+        uint32_t shards[2 * kMaxDepthQueues * kQueueShards];
+        HIP_CHECK(hipMemcpy(shards, ctx->fb.counters, sizeof(shards), hipMemcpyDeviceToHost));
+        uint32_t cnt[2 * kMaxDepthQueues] = {};
+        for (uint32_t q = 0; q < 2 * kMaxDepthQueues; ++q)
+            for (uint32_t k = 0; k < kQueueShards; ++k) cnt[q] += shards[q * kQueueShards + k];
         dxrpt_stats s = ctx->last;
         for (int d = 1; d < ctx->last_L && d < int(DXRPT_MAX_PATH_LENGTH); ++d) {
             s.radiance_rays_per_depth[d] = cnt[d];

@@ -8,37 +8,67 @@
 
 namespace dxrpt {
 
-// Per-frame wavefront buffers (all indexed as documented; sized for `capacity` paths).
+// Queue counters are sharded: a producer wave w appends to shard (w % kQueueShards) of the queue,
+// so concurrent waves spread their atomics over kQueueShards addresses instead of one.  Shard s of a
+// queue owns positions [s * cap, (s + 1) * cap); consumers enumerate item i of the queue by walking
+// the shard counts (queue_pos in pt_kernels.hip).
+constexpr uint32_t kQueueShards = 32;
+constexpr uint32_t kMaxDepthQueues = 16;  // radiance queues 0..15 by depth, shadow queues 16..31
+
+// Radiance ray queue of one depth (SoA of 16-B words: one dwordx4 per lane, coalesced).  The path
+// state travels with its ray, so every per-depth kernel reads and writes it at the queue position.
+//   org[pos] float4 (origin xyz, tmax)
+//   dir[pos] float4 (direction xyz, bits(path slot p))
+//   thr[pos] float4 (path throughput rgb, payload roughness)                RayTrace.hlsl:63-71
+//   rad[pos] float4 (radiance rgb accumulated so far, bits(payload IsDiffuse))
+//   pix[pos] uint32 global pixel index y*W+x (CMJ pattern seed)
+struct RayQueue {
+    float4* org = nullptr;
+    float4* dir = nullptr;
+    float4* thr = nullptr;
+    float4* rad = nullptr;
+    uint32_t* pix = nullptr;
+};
+
+// Per-frame wavefront buffers.
 //   path slot p in [0, num_paths): one path per pixel of the rendered tiles
-//     ps_thr[p]  float4  (path throughput rgb, payload roughness)          RayTrace.hlsl:63-71
-//     ps_rad[p]  float4  (radiance rgb accumulated so far, bits(isDiffuse))
-//     ps_pix[p]  uint2   (global pixel index y*W+x, accumulation index)
-//   queue index i in [0, q_count[d]) at radiance depth d (PathLength):
-//     q_org[d&1][i] float4 (origin xyz, tmax)       rays in SoA-of-float4: one dwordx4 per lane
-//     q_dir[d&1][i] float4 (direction xyz, bits(path slot))
-//     hit[i]        float4 (b1, b2, bits(global tri id) or ~0u on miss, bits(geometry index))
-//   shadow slot k of path p lives at [k * capacity + p]; sh_n[p] = pending slots of path p:
-//     sh_org  float4 (origin xyz, tmax)
-//     sh_dir  float4 (direction xyz, tmin)
-//     sh_con  float4 (contribution rgb = pathThroughput * CalcLighting or sky*throughput, bits(force_opaque));
-//                    k_shadow multiplies it by the visibility in place
-//   sh_queue[j]   uint32 slot id of the j-th shadow ray of the current depth (compacted)
+//     ps_pix[p]  uint2   (global pixel index, accumulation index), written by raygen
+//     px_rad[p]  float4  final path radiance: written once by k_shade when the path ends, plus the
+//                        path's last pending shadow contributions (k_resolve)
+//   queue position pos in [0, qsize) of depth d (sharded layout, see above):
+//     q[d&1]     RayQueue
+//     hit[pos]   float4 (b1, b2, bits(global tri id) or ~0u on miss, bits(geometry index))
+//     fwd[pos]   uint32 position of the path's continuation ray in queue d+1, ~0u if the path ended
+//     sh_n[pos]  uint32 number of shadow rays the vertex emitted; ray k lives in slot k * qsize + pos:
+//       sh_org  float4 (origin xyz, tmax)
+//       sh_dir  float4 (direction xyz, tmin)
+//       sh_con  float4 (contribution rgb = pathThroughput * CalcLighting or sky*throughput,
+//                       bits(force_opaque)); k_shadow multiplies it by the visibility in place
+//   sh_queue[spos]  uint32 slot id of a queued shadow ray (sharded layout with shard capacity cap_s)
 struct FrameBuffers {
-    float4* ps_thr = nullptr;
-    float4* ps_rad = nullptr;
     uint2* ps_pix = nullptr;
-    float4* q_org[2] = {nullptr, nullptr};
-    float4* q_dir[2] = {nullptr, nullptr};
+    float4* px_rad = nullptr;
+    RayQueue q[2];
     float4* hit = nullptr;
+    uint32_t* fwd = nullptr;
     uint32_t* sh_n = nullptr;
     uint32_t* sh_queue = nullptr;
     float4* sh_org = nullptr;
     float4* sh_dir = nullptr;
     float4* sh_con = nullptr;
-    uint32_t* counters = nullptr;  // [0..15] queue counts by depth, [16..31] shadow ray counts by depth
+    uint32_t* counters = nullptr;  // [queue][shard]: 2 * kMaxDepthQueues * kQueueShards
     uint32_t capacity = 0;         // paths
-    uint32_t shadow_slots = 0;     // slots per queue entry
+    uint32_t cap_r = 0;            // radiance queue shard capacity (multiple of 64)
+    uint32_t qsize = 0;            // kQueueShards * cap_r >= capacity
+    uint32_t shadow_slots = 0;     // slots per queue position; shadow shard capacity = shadow_slots * cap_r
 };
+
+// Shard capacity for producers of at most `paths` items (one wave of consumers produces <= 64 per
+// queue; waves w, w + kQueueShards, ... share a shard).
+inline uint32_t queue_shard_capacity(uint32_t paths) {
+    const uint32_t nw = (paths + 63u) / 64u;
+    return 64u * ((nw + kQueueShards - 1u) / kQueueShards);
+}
 
 struct SceneDev {
     const BvhNode* nodes = nullptr;     // width 2
@@ -55,6 +85,10 @@ struct SceneDev {
     uint32_t sky_res = 0;
     uint32_t num_textures = 0;
     int width = 8;  // BVH width actually built: 2 or 8
+    // LDS traversal stack, ints per lane: BVH2 one node index per entry, BVH8 two words (node-group
+    // base, hit/internal masks) per entry; entries = built tree depth + 1 (<= kTraversalStack /
+    // kTraversalStack8).  A shallower tree -> less LDS per workgroup -> more resident waves.
+    uint32_t stack_ints = kTraversalStack;
 };
 
 struct FrameParams {
@@ -72,9 +106,10 @@ struct FrameParams {
     uint32_t refill_lanes;           // persistent kernels: refill once this many lanes of a wave are idle
 };
 
-// Kernel sequence of one frame: raygen, then (trace, shade, shadow) per depth 1..L-1, then accumulate.
-// When `ev` is non-null, 2 + 3(L-1) + 1 events are recorded: before raygen and after each launch.
-inline int frame_event_count(int L) { return 2 + 3 * (L - 1) + 1; }
+// Kernel sequence of one frame: raygen, then (trace, shade, shadow, resolve) per depth 1..L-1, then
+// accumulate.  When `ev` is non-null, 2 + 4(L-1) + 1 events are recorded: before raygen and after each
+// launch.
+inline int frame_event_count(int L) { return 2 + 4 * (L - 1) + 1; }
 hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream,
                         hipEvent_t* ev);
 

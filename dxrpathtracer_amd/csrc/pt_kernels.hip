@@ -20,9 +20,10 @@
 // its pixel's radiance, every add happens in one thread in a fixed order: results are deterministic
 // run to run and independent of the tiling.
 //
-// BVH traversal: BVH2 (pt_layout.h), one ray per lane, short per-lane stack in LDS
-// (kTraversalStack x 4 B x 256 lanes = 32 KiB per workgroup), exact Moller-Trumbore triangle test
-// (same arithmetic as the oracle) behind conservative (padded) slab tests.
+// BVH traversal: BVH2 or compressed BVH8 (pt_layout.h), one ray per lane, per-lane stack in LDS sized
+// to the built tree's depth (SceneDev::stack_ints x 4 B x 256 lanes per workgroup, dynamic shared
+// memory), exact Moller-Trumbore triangle test (same arithmetic as the oracle) behind conservative
+// (padded) slab tests.
 #include <hip/hip_runtime.h>
 
 #include "pt_kernels.h"
@@ -378,16 +379,16 @@ PT_DEV bool trav8_step(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp
             const uint32_t slot = (k - 24u) ^ R.oct;
             node = gbase + uint32_t(__builtin_popcount(gword & 0xFFu & ((1u << slot) - 1u)));
             if (gword >> 24) {
-                stk[sp * kBlock] = int(gbase);
-                stk[(kTraversalStack8 + sp) * kBlock] = int(gword);
+                stk[(2 * sp) * kBlock] = int(gbase);
+                stk[(2 * sp + 1) * kBlock] = int(gword);
                 ++sp;
             }
             return false;
         }
         if (sp == 0) return true;
         --sp;
-        gbase = uint32_t(stk[sp * kBlock]);
-        gword = uint32_t(stk[(kTraversalStack8 + sp) * kBlock]);
+        gbase = uint32_t(stk[(2 * sp) * kBlock]);
+        gword = uint32_t(stk[(2 * sp + 1) * kBlock]);
     }
 }
 
@@ -414,7 +415,6 @@ PT_DEV bool traverse(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool
     return traverse2<kAnyHit, kCount>(S, o, d, tmin, tmax, alpha, stk, h, nvisit, ntest);
 }
 
-static_assert(2 * kTraversalStack8 <= kTraversalStack, "BVH8 group stack must fit the LDS stack array");
 
 // ---- kernels --------------------------------------------------------------------------------------
 struct KArgs {
@@ -423,10 +423,61 @@ struct KArgs {
     FrameParams P;
 };
 
-// RaygenShader, RayTrace.hlsl:92-126 (+ SamplePoint 85-90)
+PT_DEV const uint32_t* radiance_counts(const FrameBuffers& F, int depth) { return F.counters + uint32_t(depth) * kQueueShards; }
+PT_DEV const uint32_t* shadow_counts(const FrameBuffers& F, int depth) {
+    return F.counters + (kMaxDepthQueues + uint32_t(depth)) * kQueueShards;
+}
+
+// Item count of a sharded queue (wave-uniform: the counts are read with scalar loads).
+PT_DEV uint32_t queue_total(const uint32_t* __restrict__ cnt) {
+    uint32_t t = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < kQueueShards; ++s) t += cnt[s];
+    return t;
+}
+
+// Position of item i (< queue_total) of a sharded queue with shard capacity cap: the items of shard 0
+// come first, then shard 1, ...
+PT_DEV uint32_t queue_pos(const uint32_t* __restrict__ cnt, uint32_t cap, uint32_t i) {
+    uint32_t pos = 0, base = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < kQueueShards; ++s) {
+        const uint32_t c = cnt[s];
+        if (i >= base && i - base < c) pos = s * cap + (i - base);
+        base += c;
+    }
+    return pos;
+}
+
+// Wave-aggregated append to shard (wave % kQueueShards) of a queue: one atomic per wave.  Returns the
+// position of this lane's item (only meaningful where `want`).  Must be called by all active lanes.
+PT_DEV uint32_t queue_append(uint32_t* counters, uint32_t cap, bool want) {
+    const unsigned long long m = __ballot(want);
+    const int lane = __lane_id();
+    const int leader = __ffsll(static_cast<long long>(__ballot(1))) - 1;
+    const uint32_t shard = ((blockIdx.x * kBlock + threadIdx.x) >> 6) % kQueueShards;
+    uint32_t base = 0;
+    if (lane == leader && m != 0ull) base = atomicAdd(&counters[shard], uint32_t(__popcll(m)));
+    base = __shfl(base, leader);
+    return shard * cap + base + uint32_t(__popcll(m & ((1ull << lane) - 1ull)));
+}
+
+// RaygenShader, RayTrace.hlsl:92-126 (+ SamplePoint 85-90).  Path slot p goes to queue-1 position
+// (shard w % K, offset (w / K) * 64 + lane) of its wave w = p / 64, so the queue layout matches what
+// a wave-ordered append would have produced; the shard counts are analytic.
 __global__ __launch_bounds__(kBlock) void k_raygen(KArgs A) {
     const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-    if (p >= A.P.num_paths) return;
+    const uint32_t P = A.P.num_paths;
+    if (p == 0) {
+        const uint32_t nw = (P + 63u) / 64u;
+        uint32_t* cnt = A.F.counters + 1u * kQueueShards;
+        for (uint32_t s = 0; s < kQueueShards && s < nw; ++s) {
+            uint32_t items = ((nw - 1u - s) / kQueueShards + 1u) * 64u;
+            if ((nw - 1u) % kQueueShards == s) items -= nw * 64u - P;
+            cnt[s] = items;
+        }
+    }
+    if (p >= P) return;
     // path slot -> tile (binary search over the prefix table) -> pixel
     uint32_t lo = 0, hi = A.P.num_tiles;
     while (hi - lo > 1u) {
@@ -469,22 +520,26 @@ __global__ __launch_bounds__(kBlock) void k_raygen(KArgs A) {
     const f3 diff = sub(end, start);
     const f3 dir = normalize3(diff);
     const float rayLength = len3(diff);
-    A.F.q_org[1][p] = make_float4(start.x, start.y, start.z, rayLength);
-    A.F.q_dir[1][p] = make_float4(dir.x, dir.y, dir.z, bitsf(p));
-    A.F.ps_thr[p] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
-    A.F.ps_rad[p] = make_float4(0.0f, 0.0f, 0.0f, bitsf(0u));
+    const uint32_t w = p >> 6;
+    const uint32_t pos = (w % kQueueShards) * A.F.cap_r + (w / kQueueShards) * 64u + (p & 63u);
+    const RayQueue& Q = A.F.q[1];
+    Q.org[pos] = make_float4(start.x, start.y, start.z, rayLength);
+    Q.dir[pos] = make_float4(dir.x, dir.y, dir.z, bitsf(p));
+    Q.thr[pos] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+    Q.rad[pos] = make_float4(0.0f, 0.0f, 0.0f, bitsf(0u));
+    Q.pix[pos] = pixelIdx;
     A.F.ps_pix[p] = make_uint2(pixelIdx, accumIdx);
-    A.F.sh_n[p] = 0u;
-    if (p == 0) A.F.counters[1] = A.P.num_paths;
 }
 
 template <bool kCount, int W>
 __global__ __launch_bounds__(kBlock) void k_trace(KArgs A, int depth) {
-    __shared__ int stack[kTraversalStack * kBlock];
+    extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved (launch_lds_bytes)
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= A.F.counters[depth]) return;
-    const float4 o4 = A.F.q_org[depth & 1][i];
-    const float4 d4 = A.F.q_dir[depth & 1][i];
+    const uint32_t* cnt = radiance_counts(A.F, depth);
+    if (i >= queue_total(cnt)) return;
+    const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
+    const float4 o4 = A.F.q[depth & 1].org[pos];
+    const float4 d4 = A.F.q[depth & 1].dir[pos];
     // Primary rays start at TMin 0 (RayTrace.hlsl:118); continuation rays at 1e-5 (:382).
     const float tmin = depth == 1 ? 0.0f : kRayTMin;
     // RAY_FLAG_FORCE_OPAQUE iff PathLength > MaxAnyHitPathLength (RayTrace.hlsl:132, 401)
@@ -492,34 +547,23 @@ __global__ __launch_bounds__(kBlock) void k_trace(KArgs A, int depth) {
     HitRec h;
     uint32_t nv = 0, nt = 0;
     traverse<W, false, kCount>(A.S, ld3(o4), ld3(d4), tmin, o4.w, alpha, stack + threadIdx.x, h, nv, nt);
-    A.F.hit[i] = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
+    A.F.hit[pos] = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
     if (kCount) {
         atomicAdd(&A.P.trav[0], (unsigned long long)nv);
         atomicAdd(&A.P.trav[1], (unsigned long long)nt);
     }
 }
 
-// Shadow ray k of path p lives in slot [k * capacity + p]; the contribution is multiplied by the
-// visibility in place by k_shadow and added to the path's radiance, in k order, by the next k_shade
-// of that path or by k_accumulate (deterministic, no atomics on radiance).
-PT_DEV void emit_shadow(const KArgs& A, uint32_t pathSlot, uint32_t& n, f3 o, f3 d, float tmin, float tmax, f3 contrib,
+// Shadow ray k of the vertex at queue position pos lives in slot [k * qsize + pos]; k_shadow multiplies
+// its contribution by the visibility in place and k_resolve adds the slots, in k order, to the path's
+// radiance (deterministic, no atomics on radiance).
+PT_DEV void emit_shadow(const KArgs& A, uint32_t pos, uint32_t& n, f3 o, f3 d, float tmin, float tmax, f3 contrib,
                         bool forceOpaque) {
-    const size_t s = size_t(n) * A.F.capacity + pathSlot;
+    const size_t s = size_t(n) * A.F.qsize + pos;
     A.F.sh_org[s] = make_float4(o.x, o.y, o.z, tmax);
     A.F.sh_dir[s] = make_float4(d.x, d.y, d.z, tmin);
     A.F.sh_con[s] = make_float4(contrib.x, contrib.y, contrib.z, bitsf(forceOpaque ? 1u : 0u));
     ++n;
-}
-
-// Adds the (visibility-weighted) contributions of the path's pending shadow rays.
-PT_DEV void resolve_shadows(const KArgs& A, uint32_t pathSlot, float4& rad) {
-    const uint32_t n = A.F.sh_n[pathSlot];
-    for (uint32_t k = 0; k < n; ++k) {
-        const float4 c = A.F.sh_con[size_t(k) * A.F.capacity + pathSlot];
-        rad.x += c.x;
-        rad.y += c.y;
-        rad.z += c.z;
-    }
 }
 
 PT_DEV bool nonzero3(f3 c) { return !(c.x == 0.0f && c.y == 0.0f && c.z == 0.0f); }
@@ -527,16 +571,18 @@ PT_DEV bool nonzero3(f3 c) { return !(c.x == 0.0f && c.y == 0.0f && c.z == 0.0f)
 // MissShader (RayTrace.hlsl:509-530) and ClosestHitShader -> PathTrace (151-441)
 __global__ __launch_bounds__(kBlock) void k_shade(KArgs A, int depth) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= A.F.counters[depth]) return;
+    const uint32_t* cnt = radiance_counts(A.F, depth);
+    if (i >= queue_total(cnt)) return;
+    const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
     const dxrpt_app_settings& set = A.P.set;
     const dxrpt_ray_trace_constants& rtc = A.P.rtc;
-    const float4 o4 = A.F.q_org[depth & 1][i];
-    const float4 d4 = A.F.q_dir[depth & 1][i];
+    const RayQueue& Q = A.F.q[depth & 1];
+    const float4 o4 = Q.org[pos];
+    const float4 d4 = Q.dir[pos];
     const uint32_t pathSlot = fbits(d4.w);
-    const float4 hit = A.F.hit[i];
-    const float4 thr4 = A.F.ps_thr[pathSlot];
-    float4 rad4 = A.F.ps_rad[pathSlot];
-    resolve_shadows(A, pathSlot, rad4);  // shadow rays of depth-1 vertex
+    const float4 hit = A.F.hit[pos];
+    const float4 thr4 = Q.thr[pos];
+    float4 rad4 = Q.rad[pos];
     const f3 pathThr = ld3(thr4);
     const f3 inDir = ld3(d4);
     const f3 inOrigin = ld3(o4);
@@ -626,7 +672,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(KArgs A, int depth) {
             const f3 c = calc_lighting(normalWS, sunDirection, f3{rtc.SunIrradiance[0], rtc.SunIrradiance[1], rtc.SunIrradiance[2]},
                                        diffuseAlbedo, specularAlbedo, roughness, positionWS, inOrigin, msEC);
             if (nonzero3(c))
-                emit_shadow(A, pathSlot, nsh, positionWS, D, kRayTMin, kFP32Max, mul(pathThr, c), shadowOpaque);
+                emit_shadow(A, pos, nsh, positionWS, D, kRayTMin, kFP32Max, mul(pathThr, c), shadowOpaque);
         }
         // Spot lights (RayTrace.hlsl:265-313)
         if (set.RenderLights && !furnace && !directZero) {
@@ -647,7 +693,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(KArgs A, int depth) {
                     const f3 c = calc_lighting(normalWS, surfaceToLight, intensity, diffuseAlbedo, specularAlbedo, roughness,
                                                positionWS, inOrigin, msEC);
                     if (nonzero3(c))
-                        emit_shadow(A, pathSlot, nsh, add(positionWS, scl(normalWS, 0.01f)), surfaceToLight, kSpotShadowNearClip,
+                        emit_shadow(A, pos, nsh, add(positionWS, scl(normalWS, 0.01f)), surfaceToLight, kSpotShadowNearClip,
                                     distanceToLight - kSpotShadowNearClip, mul(pathThr, c), shadowOpaque);
                 }
             }
@@ -656,7 +702,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(KArgs A, int depth) {
         // BRDF importance sampling (RayTrace.hlsl:315-376); sample set = PathLength
         float bx, by;
         sample_cmj2d(rtc.CurrSampleIdx, uint32_t(set.SqrtNumSamples), uint32_t(set.SqrtNumSamples),
-                     uint32_t(depth) * rtc.TotalNumPixels + A.F.ps_pix[pathSlot].x, &bx, &by);
+                     uint32_t(depth) * rtc.TotalNumPixels + Q.pix[pos], &bx, &by);
         f3 throughput, rayDirTS;
         float selector = bx;
         if (!enableSpecular) selector = 0.0f;
@@ -698,7 +744,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(KArgs A, int depth) {
             const f3 sky = set.EnableSky ? sample_sky(A.S, rayDirWS) : f3{0.0f, 0.0f, 0.0f};
             const f3 c = mul(sky, throughput);
             if (nonzero3(c))
-                emit_shadow(A, pathSlot, nsh, positionWS, rayDirWS, kRayTMin, kFP32Max, mul(pathThr, c),
+                emit_shadow(A, pos, nsh, positionWS, rayDirWS, kRayTMin, kFP32Max, mul(pathThr, c),
                             depth + 1 > set.MaxAnyHitPathLength);
         }
     } while (false);
@@ -707,33 +753,29 @@ __global__ __launch_bounds__(kBlock) void k_shade(KArgs A, int depth) {
     rad4.x += pathThr.x * local.x;
     rad4.y += pathThr.y * local.y;
     rad4.z += pathThr.z * local.z;
-    if (cont) rad4.w = bitsf(nextIsDiffuse ? 1u : 0u);  // payload.IsDiffuse for the next vertex
-    A.F.ps_rad[pathSlot] = rad4;
-    A.F.sh_n[pathSlot] = nsh;
+    A.F.sh_n[pos] = nsh;
 
-    // wave64 compaction (ballot + popcount + one atomic per wave) of the shadow rays into the shadow
-    // queue of this depth and of the continuation rays into queue[depth+1]
-    const unsigned long long active = __ballot(1);
-    const int lane = __lane_id();
-    const int leader = __ffsll(static_cast<long long>(active)) - 1;
-    const unsigned long long lt = (1ull << lane) - 1ull;
+    // wave64 compaction (ballot + popcount + one atomic per wave and shard) of the shadow rays into the
+    // shadow queue of this depth and of the continuation rays into queue[depth+1]
+    uint32_t* shcnt = A.F.counters + (kMaxDepthQueues + uint32_t(depth)) * kQueueShards;
+    const uint32_t cap_s = A.F.shadow_slots * A.F.cap_r;
     for (uint32_t k = 0;; ++k) {
-        const unsigned long long mk = __ballot(nsh > k);
-        if (mk == 0ull) break;
-        uint32_t b = 0;
-        if (lane == leader) b = atomicAdd(&A.F.counters[16 + depth], uint32_t(__popcll(mk)));
-        b = __shfl(b, leader);
-        if (nsh > k) A.F.sh_queue[b + uint32_t(__popcll(mk & lt))] = k * A.F.capacity + pathSlot;
+        if (__ballot(nsh > k) == 0ull) break;
+        const uint32_t spos = queue_append(shcnt, cap_s, nsh > k);
+        if (nsh > k) A.F.sh_queue[spos] = k * A.F.qsize + pos;
     }
-    const unsigned long long m = __ballot(cont);
-    uint32_t base = 0;
-    if (lane == leader && m != 0ull) base = atomicAdd(&A.F.counters[depth + 1], uint32_t(__popcll(m)));
-    base = __shfl(base, leader);
+    const uint32_t npos = queue_append(A.F.counters + uint32_t(depth + 1) * kQueueShards, A.F.cap_r, cont);
     if (cont) {
-        const uint32_t off = base + uint32_t(__popcll(m & ((1ull << lane) - 1ull)));
-        A.F.q_org[(depth + 1) & 1][off] = make_float4(nextOrigin.x, nextOrigin.y, nextOrigin.z, kFP32Max);
-        A.F.q_dir[(depth + 1) & 1][off] = make_float4(nextDir.x, nextDir.y, nextDir.z, bitsf(pathSlot));
-        A.F.ps_thr[pathSlot] = make_float4(nextThr.x, nextThr.y, nextThr.z, nextRoughness);
+        const RayQueue& N = A.F.q[(depth + 1) & 1];
+        N.org[npos] = make_float4(nextOrigin.x, nextOrigin.y, nextOrigin.z, kFP32Max);
+        N.dir[npos] = make_float4(nextDir.x, nextDir.y, nextDir.z, bitsf(pathSlot));
+        N.thr[npos] = make_float4(nextThr.x, nextThr.y, nextThr.z, nextRoughness);
+        N.rad[npos] = make_float4(rad4.x, rad4.y, rad4.z, bitsf(nextIsDiffuse ? 1u : 0u));  // payload.IsDiffuse
+        N.pix[npos] = Q.pix[pos];
+        A.F.fwd[pos] = npos;
+    } else {
+        A.F.px_rad[pathSlot] = rad4;
+        A.F.fwd[pos] = ~0u;
     }
 }
 
@@ -741,11 +783,13 @@ __global__ __launch_bounds__(kBlock) void k_shade(KArgs A, int depth) {
 // one thread per queued shadow ray (grid-stride); occluded -> contribution * 0 (keeps NaN/Inf).
 template <bool kCount, int W>
 __global__ __launch_bounds__(kBlock) void k_shadow(KArgs A, int depth) {
-    __shared__ int stack[kTraversalStack * kBlock];
-    const uint32_t count = A.F.counters[16 + depth];
+    extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved (launch_lds_bytes)
+    const uint32_t* cnt = shadow_counts(A.F, depth);
+    const uint32_t count = queue_total(cnt);
+    const uint32_t cap_s = A.F.shadow_slots * A.F.cap_r;
     uint32_t nv = 0, nt = 0;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < count; i += gridDim.x * kBlock) {
-        const uint32_t slot = A.F.sh_queue[i];
+        const uint32_t slot = A.F.sh_queue[queue_pos(cnt, cap_s, i)];
         const float4 o4 = A.F.sh_org[slot];
         const float4 d4 = A.F.sh_dir[slot];
         const float4 c4 = A.F.sh_con[slot];
@@ -760,6 +804,27 @@ __global__ __launch_bounds__(kBlock) void k_shadow(KArgs A, int depth) {
     }
 }
 
+// Adds the visibility-weighted shadow contributions of each depth-d vertex, in slot order, to the
+// radiance of its path: in the continuation ray's queue entry, or in px_rad if the path ended.
+__global__ __launch_bounds__(kBlock) void k_resolve(KArgs A, int depth) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t* cnt = radiance_counts(A.F, depth);
+    if (i >= queue_total(cnt)) return;
+    const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
+    const uint32_t n = A.F.sh_n[pos];
+    if (n == 0u) return;
+    const uint32_t f = A.F.fwd[pos];
+    float4* dst = f != ~0u ? &A.F.q[(depth + 1) & 1].rad[f] : &A.F.px_rad[fbits(A.F.q[depth & 1].dir[pos].w)];
+    float4 r = *dst;
+    for (uint32_t k = 0; k < n; ++k) {
+        const float4 c = A.F.sh_con[size_t(k) * A.F.qsize + pos];
+        r.x += c.x;
+        r.y += c.y;
+        r.z += c.z;
+    }
+    *dst = r;
+}
+
 // Persistent BVH8 traversal for the radiance (kShadow = false) and shadow (true) queues of one depth.
 // The grid is sized to the resident capacity.  Wave w owns the 64-ray chunks w, w + nwaves,
 // w + 2 nwaves, ... of the queue (coherent within a chunk, balanced over the image) and advances every
@@ -767,9 +832,11 @@ __global__ __launch_bounds__(kBlock) void k_shadow(KArgs A, int depth) {
 // once >= refill lanes are idle (Aila & Laine 2009, "replacing terminated rays").  No atomics.
 template <bool kCount, bool kShadow>
 __global__ __launch_bounds__(kBlock) void k_traverse8p(KArgs A, int depth) {
-    __shared__ int stack[kTraversalStack * kBlock];
+    extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved (launch_lds_bytes)
     int* stk = stack + threadIdx.x;
-    const uint32_t count = kShadow ? A.F.counters[16 + depth] : A.F.counters[depth];
+    const uint32_t* cnt = kShadow ? shadow_counts(A.F, depth) : radiance_counts(A.F, depth);
+    const uint32_t cap = kShadow ? A.F.shadow_slots * A.F.cap_r : A.F.cap_r;
+    const uint32_t count = queue_total(cnt);
     const uint32_t nwaves = gridDim.x * (kBlock / 64u);
     const uint32_t wave = blockIdx.x * (kBlock / 64u) + threadIdx.x / 64u;
     const uint32_t nchunks = (count + 63u) / 64u;
@@ -797,16 +864,17 @@ __global__ __launch_bounds__(kBlock) void k_traverse8p(KArgs A, int depth) {
                 const uint32_t j = next + uint32_t(__popcll(idle & lt));
                 const uint32_t idx = (wave + (j >> 6) * nwaves) * 64u + (j & 63u);
                 if (j < end && idx < count) {
+                    const uint32_t pos = queue_pos(cnt, cap, idx);
                     if (kShadow) {
-                        item = A.F.sh_queue[idx];
+                        item = A.F.sh_queue[pos];
                         const float4 o4 = A.F.sh_org[item];
                         const float4 d4 = A.F.sh_dir[item];
                         const bool alpha = fbits(A.F.sh_con[item].w) == 0u;
                         ray8_init(R, ld3(o4), ld3(d4), d4.w, o4.w, alpha, h);
                     } else {
-                        item = idx;
-                        const float4 o4 = A.F.q_org[depth & 1][idx];
-                        const float4 d4 = A.F.q_dir[depth & 1][idx];
+                        item = pos;
+                        const float4 o4 = A.F.q[depth & 1].org[pos];
+                        const float4 d4 = A.F.q[depth & 1].dir[pos];
                         ray8_init(R, ld3(o4), ld3(d4), tminR, o4.w, alphaR, h);
                     }
                     node = 0;
@@ -842,8 +910,7 @@ __global__ __launch_bounds__(kBlock) void k_traverse8p(KArgs A, int depth) {
 __global__ __launch_bounds__(kBlock) void k_accumulate(KArgs A) {
     const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
     if (p >= A.P.num_paths) return;
-    float4 r = A.F.ps_rad[p];
-    resolve_shadows(A, p, r);  // shadow rays of the last vertex
+    const float4 r = A.F.px_rad[p];
     const uint32_t a = A.F.ps_pix[p].y;
     const float rx = fminf(fmaxf(r.x, 0.0f), kFP16Max);
     const float ry = fminf(fmaxf(r.y, 0.0f), kFP16Max);
@@ -858,7 +925,7 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(KArgs A) {
 // bit1 = alpha test enabled (not FORCE_OPAQUE).
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_trace_rays(SceneDev S, const float4* rays, uint32_t n, uint32_t flags, float4* hits) {
-    __shared__ int stack[kTraversalStack * kBlock];
+    extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved (launch_lds_bytes)
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const float4 a = rays[2 * i], b = rays[2 * i + 1];
@@ -880,12 +947,13 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
                         hipEvent_t* ev) {
     KArgs A{scene, fb, fp};
     const uint32_t g = grid_for(fp.num_paths);
+    const size_t lds = size_t(scene.stack_ints) * kBlock * sizeof(int);
     const bool count = fp.trav != nullptr;
     int e_i = 0;
     auto mark = [&]() {
         if (ev) (void)hipEventRecord(ev[e_i++], stream);
     };
-    hipError_t e = hipMemsetAsync(fb.counters, 0, 32 * sizeof(uint32_t), stream);
+    hipError_t e = hipMemsetAsync(fb.counters, 0, 2 * kMaxDepthQueues * kQueueShards * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     mark();
     hipLaunchKernelGGL(k_raygen, dim3(g), dim3(kBlock), 0, stream, A);
@@ -896,29 +964,31 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
         const bool pers = w8 && fp.persistent_blocks > 0;
         const uint32_t gp = fp.persistent_blocks;
         if (w8 && !pers) {
-            if (count) hipLaunchKernelGGL((k_trace<true, 8>), dim3(g), dim3(kBlock), 0, stream, A, d);
-            else hipLaunchKernelGGL((k_trace<false, 8>), dim3(g), dim3(kBlock), 0, stream, A, d);
+            if (count) hipLaunchKernelGGL((k_trace<true, 8>), dim3(g), dim3(kBlock), lds, stream, A, d);
+            else hipLaunchKernelGGL((k_trace<false, 8>), dim3(g), dim3(kBlock), lds, stream, A, d);
         } else if (pers) {
-            if (count) hipLaunchKernelGGL((k_traverse8p<true, false>), dim3(gp), dim3(kBlock), 0, stream, A, d);
-            else hipLaunchKernelGGL((k_traverse8p<false, false>), dim3(gp), dim3(kBlock), 0, stream, A, d);
+            if (count) hipLaunchKernelGGL((k_traverse8p<true, false>), dim3(gp), dim3(kBlock), lds, stream, A, d);
+            else hipLaunchKernelGGL((k_traverse8p<false, false>), dim3(gp), dim3(kBlock), lds, stream, A, d);
         } else {
-            if (count) hipLaunchKernelGGL((k_trace<true, 2>), dim3(g), dim3(kBlock), 0, stream, A, d);
-            else hipLaunchKernelGGL((k_trace<false, 2>), dim3(g), dim3(kBlock), 0, stream, A, d);
+            if (count) hipLaunchKernelGGL((k_trace<true, 2>), dim3(g), dim3(kBlock), lds, stream, A, d);
+            else hipLaunchKernelGGL((k_trace<false, 2>), dim3(g), dim3(kBlock), lds, stream, A, d);
         }
         mark();
         hipLaunchKernelGGL(k_shade, dim3(g), dim3(kBlock), 0, stream, A, d);
         mark();
         const uint32_t gs = std::min<uint32_t>(grid_for(fp.num_paths * fb.shadow_slots), kShadowGrid);
         if (w8 && !pers) {
-            if (count) hipLaunchKernelGGL((k_shadow<true, 8>), dim3(gs), dim3(kBlock), 0, stream, A, d);
-            else hipLaunchKernelGGL((k_shadow<false, 8>), dim3(gs), dim3(kBlock), 0, stream, A, d);
+            if (count) hipLaunchKernelGGL((k_shadow<true, 8>), dim3(gs), dim3(kBlock), lds, stream, A, d);
+            else hipLaunchKernelGGL((k_shadow<false, 8>), dim3(gs), dim3(kBlock), lds, stream, A, d);
         } else if (pers) {
-            if (count) hipLaunchKernelGGL((k_traverse8p<true, true>), dim3(gp), dim3(kBlock), 0, stream, A, d);
-            else hipLaunchKernelGGL((k_traverse8p<false, true>), dim3(gp), dim3(kBlock), 0, stream, A, d);
+            if (count) hipLaunchKernelGGL((k_traverse8p<true, true>), dim3(gp), dim3(kBlock), lds, stream, A, d);
+            else hipLaunchKernelGGL((k_traverse8p<false, true>), dim3(gp), dim3(kBlock), lds, stream, A, d);
         } else {
-            if (count) hipLaunchKernelGGL((k_shadow<true, 2>), dim3(gs), dim3(kBlock), 0, stream, A, d);
-            else hipLaunchKernelGGL((k_shadow<false, 2>), dim3(gs), dim3(kBlock), 0, stream, A, d);
+            if (count) hipLaunchKernelGGL((k_shadow<true, 2>), dim3(gs), dim3(kBlock), lds, stream, A, d);
+            else hipLaunchKernelGGL((k_shadow<false, 2>), dim3(gs), dim3(kBlock), lds, stream, A, d);
         }
+        mark();
+        hipLaunchKernelGGL(k_resolve, dim3(g), dim3(kBlock), 0, stream, A, d);
         mark();
     }
     hipLaunchKernelGGL(k_accumulate, dim3(g), dim3(kBlock), 0, stream, A);
@@ -929,10 +999,11 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
 hipError_t launch_trace_rays(const SceneDev& scene, const float4* rays, uint32_t n, uint32_t flags, float4* hits,
                              hipStream_t stream) {
     if (n == 0) return hipSuccess;
+    const size_t lds = size_t(scene.stack_ints) * kBlock * sizeof(int);
     if (scene.width == 8)
-        hipLaunchKernelGGL((k_trace_rays<8>), dim3(grid_for(n)), dim3(kBlock), 0, stream, scene, rays, n, flags, hits);
+        hipLaunchKernelGGL((k_trace_rays<8>), dim3(grid_for(n)), dim3(kBlock), lds, stream, scene, rays, n, flags, hits);
     else
-        hipLaunchKernelGGL((k_trace_rays<2>), dim3(grid_for(n)), dim3(kBlock), 0, stream, scene, rays, n, flags, hits);
+        hipLaunchKernelGGL((k_trace_rays<2>), dim3(grid_for(n)), dim3(kBlock), lds, stream, scene, rays, n, flags, hits);
     return hipGetLastError();
 }
 

@@ -190,7 +190,8 @@ typedef struct dxrpt_tile {
 #define DXRPT_K_SHADE 2
 #define DXRPT_K_SHADOW 3      /* any-hit traversal of shadow rays (all depths) */
 #define DXRPT_K_ACCUMULATE 4
-#define DXRPT_K_COUNT 5
+#define DXRPT_K_RESOLVE 5     /* adds visibility-weighted shadow contributions to path radiance */
+#define DXRPT_K_COUNT 6
 
 /* Counters of the last dxrpt_render call (read back with a stream sync in dxrpt_get_stats), plus
  * per-kernel HIP-event timings accumulated since dxrpt_reset_timing (DXRPT_OPT_KERNEL_TIMING). */
