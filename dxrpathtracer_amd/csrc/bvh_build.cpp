@@ -48,6 +48,7 @@ struct TNode {
     Box box;
     int32_t child[2] = {-1, -1};
     uint32_t first = 0, count = 0;  // leaf when count > 0
+    uint32_t begin = 0, end = 0;    // triangle (refs) range of the whole subtree
 };
 
 struct Builder {
@@ -57,6 +58,7 @@ struct Builder {
     std::vector<TNode> tree;
     uint32_t leaf_max = kMaxLeafTris;
     uint32_t prefer_leaf = 4;
+    uint32_t depth_cap = kMaxDepth2;
 
     Box range_box(uint32_t b, uint32_t e) const {
         Box r;
@@ -113,12 +115,12 @@ struct Builder {
         }
         const bool must_split = n > leaf_max;
         if (!must_split && n <= prefer_leaf && leaf_cost <= best_cost) return 0;
-        if (!must_split && depth + 1 >= kMaxDepth2) return 0;
+        if (!must_split && depth + 1 >= depth_cap) return 0;
         // Depth budget: halving splits need `levels` more levels to reach <= leaf_max; once the SAH
         // split could no longer meet the cap, fall back to object-median splits.
         uint32_t levels = 0;
         for (uint32_t m = (n + leaf_max - 1) / leaf_max; m > 1; m = (m + 1) / 2) ++levels;
-        const bool tight = depth + levels + 3 >= kMaxDepth2;
+        const bool tight = depth + levels + 3 >= depth_cap;
         if (best_axis >= 0 && !tight && (must_split || best_cost < leaf_cost)) {
             const float ext = cb.hi[best_axis] - cb.lo[best_axis];
             const float scale = float(kBins) / ext;
@@ -159,6 +161,8 @@ struct Builder {
             stack.pop_back();
             Box bx = range_box(t.begin, t.end);
             tree[t.node].box = bx;
+            tree[t.node].begin = t.begin;
+            tree[t.node].end = t.end;
             uint32_t m = split(t.begin, t.end, t.depth, bx);
             if (m == 0) {
                 if (t.end - t.begin > leaf_max) {
@@ -169,7 +173,7 @@ struct Builder {
                 tree[t.node].count = t.end - t.begin;
                 sah += bx.area() / root_area * double(t.end - t.begin);
             } else {
-                if (t.depth + 1 > kMaxDepth2) {
+                if (t.depth + 1 > depth_cap) {
                     err = "build_bvh: depth cap exceeded";
                     return false;
                 }
@@ -264,30 +268,87 @@ struct Emit8 {
 
     static float sgn(int o, int bit) { return (o & bit) ? -1.0f : 1.0f; }
 
-    // Collapse: open the largest-area internal child until there are 8 children.
-    void gather_children(int32_t t, std::vector<int32_t>& ch) {
-        const TNode& tn = tree[t];
-        ch.clear();
-        if (tn.count) {
+    // SAH-optimal collapse of the binary tree into the 8-wide tree (Ylitie et al. 2017, sec. 3.1),
+    // by dynamic programming over (binary node n, i = number of wide-node slots it may occupy):
+    //   C(n, 1)  = min(leaf: A(n) * C_prim * tris(n)  [tris(n) <= kMaxLeafTris8],
+    //                  node: A(n) * C_node + D(n, 8))
+    //   D(n, i)  = min_k C(left, k) + C(right, i - k)     (split the slots between the children)
+    //   C(n, i)  = min(C(n, i - 1), D(n, i))              (i >= 2)
+    // C_prim / C_node ~ the measured VALU cost of a triangle test vs an 8-child node test.
+    static constexpr double kCNode = 1.0, kCPrim = 0.35;
+    std::vector<double> cost;     // [n * 8 + i], i in 1..7 (index 0: D(n, 8) for the node case)
+    std::vector<uint8_t> pick;    // [n * 8 + i]: i == 1: 0 leaf / 1 node; i >= 2: 0 = use C(n, i-1), k = split
+    std::vector<uint8_t> dsplit;  // k of D(n, 8)
+
+    static uint32_t ntris(const TNode& n) { return n.end - n.begin; }
+    bool is_leaf(int32_t t) const { return pick[size_t(t) * 8 + 1] == 0; }
+
+    void solve() {
+        const size_t nn = tree.size();
+        cost.assign(nn * 8, 0.0);
+        pick.assign(nn * 8, 0);
+        dsplit.assign(nn, 0);
+        // children have larger indices than their parent (builder appends), so a reverse sweep is
+        // a post-order
+        for (size_t ni = nn; ni-- > 0;) {
+            const TNode& n = tree[ni];
+            const double A = n.box.area();
+            double* C = &cost[ni * 8];
+            uint8_t* P = &pick[ni * 8];
+            const double leaf = ntris(n) <= uint32_t(kMaxLeafTris8) ? A * kCPrim * double(ntris(n)) : DBL_MAX;
+            if (n.count) {  // binary leaf
+                for (int i = 1; i < 8; ++i) { C[i] = leaf; P[i] = 0; }
+                C[0] = DBL_MAX;
+                continue;
+            }
+            const double* L = &cost[size_t(n.child[0]) * 8];
+            const double* R = &cost[size_t(n.child[1]) * 8];
+            auto D = [&](int i, uint8_t& bk) {
+                double best = DBL_MAX;
+                for (int k = 1; k < i; ++k) {
+                    double c = L[k] + R[i - k];
+                    if (c < best) { best = c; bk = uint8_t(k); }
+                }
+                return best;
+            };
+            uint8_t k8 = 1;
+            const double d8 = D(8, k8);
+            dsplit[ni] = k8;
+            C[0] = d8;
+            const double node = A * kCNode + d8;
+            C[1] = std::min(leaf, node);
+            P[1] = leaf <= node ? 0 : 1;
+            for (int i = 2; i < 8; ++i) {
+                uint8_t k = 1;
+                const double d = D(i, k);
+                if (d < C[i - 1]) { C[i] = d; P[i] = k; }
+                else { C[i] = C[i - 1]; P[i] = 0; }
+            }
+        }
+    }
+
+    // Children of binary subtree t occupying at most i slots.
+    void expand(int32_t t, int i, std::vector<int32_t>& ch) {
+        while (i > 1 && pick[size_t(t) * 8 + i] == 0) --i;
+        if (i == 1 || tree[t].count) {
             ch.push_back(t);
             return;
         }
-        ch.push_back(tn.child[0]);
-        ch.push_back(tn.child[1]);
-        while (ch.size() < 8) {
-            int best = -1;
-            double ba = -1.0;
-            for (size_t i = 0; i < ch.size(); ++i) {
-                const TNode& c = tree[ch[i]];
-                if (c.count) continue;
-                double a = c.box.area();
-                if (a > ba) { ba = a; best = int(i); }
-            }
-            if (best < 0) break;
-            int32_t open = ch[best];
-            ch[best] = tree[open].child[0];
-            ch.push_back(tree[open].child[1]);
+        const int k = pick[size_t(t) * 8 + i];
+        expand(tree[t].child[0], k, ch);
+        expand(tree[t].child[1], i - k, ch);
+    }
+
+    // The wide node for binary subtree t: its children per D(t, 8).
+    void gather_children(int32_t t, std::vector<int32_t>& ch) {
+        ch.clear();
+        if (tree[t].count) {
+            ch.push_back(t);
+            return;
         }
+        const int k = dsplit[t];
+        expand(tree[t].child[0], k, ch);
+        expand(tree[t].child[1], 8 - k, ch);
     }
 
     void emit(uint32_t idx, int32_t t, uint32_t depth) {
@@ -358,7 +419,7 @@ struct Emit8 {
         // children
         uint32_t n_internal = 0;
         for (int s = 0; s < 8; ++s)
-            if (slot_of[s] >= 0 && tree[slot_of[s]].count == 0) n_internal++;
+            if (slot_of[s] >= 0 && !is_leaf(slot_of[s])) n_internal++;
         const uint32_t base_child = uint32_t(nodes.size());
         const uint32_t base_tri = uint32_t(tri_order.size());
         nodes.resize(nodes.size() + n_internal);
@@ -381,10 +442,11 @@ struct Emit8 {
                 n.qlo[k][s] = uint8_t(ql);
                 n.qhi[k][s] = uint8_t(qh);
             }
-            if (c.count) {
-                n.meta[s] = uint8_t((c.count << 5) | tri_off);
-                for (uint32_t i = 0; i < c.count; ++i) tri_order.push_back(refs[c.first + i]);
-                tri_off += c.count;
+            if (is_leaf(slot_of[s])) {
+                const uint32_t cnt = ntris(c);
+                n.meta[s] = uint8_t((cnt << 5) | tri_off);
+                for (uint32_t i = c.begin; i < c.end; ++i) tri_order.push_back(refs[i]);
+                tri_off += cnt;
                 leaves++;
             } else {
                 n.imask |= uint8_t(1u << s);
@@ -398,6 +460,7 @@ struct Emit8 {
     }
 
     void run() {
+        solve();
         nodes.emplace_back();
         emit(0, 0, 0);
     }
@@ -405,7 +468,8 @@ struct Emit8 {
 
 }  // namespace
 
-bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildResult& out, std::string& err) {
+bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildResult& out, std::string& err,
+               const BvhBuildParams* params) {
     if (ntris == 0) {
         err = "build_bvh: scene has no triangles";
         return false;
@@ -419,8 +483,10 @@ bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildRe
         return false;
     }
     Builder B;
-    B.leaf_max = width == 8 ? uint32_t(kMaxLeafTris8) : uint32_t(kMaxLeafTris);
-    B.prefer_leaf = width == 8 ? 3u : 4u;
+    // BVH8: full binary split (single-triangle leaves); the collapse forms the wide leaves.
+    B.leaf_max = width == 8 ? 1u : uint32_t(kMaxLeafTris);
+    B.prefer_leaf = width == 8 ? 1u : 4u;
+    B.depth_cap = kMaxDepth2;
     B.tri_box.resize(ntris);
     B.cen.resize(size_t(ntris) * 3);
     B.refs.resize(ntris);
@@ -436,34 +502,50 @@ bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildRe
     float ext = 0.f;
     for (int k = 0; k < 3; ++k) ext = std::max(ext, scene.hi[k] - scene.lo[k]);
     const float pad = ext * 1e-6f + 1e-7f;
-    double sah = 0.0;
-    if (!B.build(ntris, err, sah)) return false;
     out = BvhBuildResult();
-    out.sah_cost = sah;
     if (width == 2) {
+        double sah = 0.0;
+        if (!B.build(ntris, err, sah)) return false;
+        out.sah_cost = sah;
         Emit2 E{B.tree, pad, {}, 0, 0};
         E.run();
         out.nodes = std::move(E.nodes);
         out.tri_order = std::move(B.refs);
         out.max_depth = E.max_depth;
         out.num_leaves = E.leaves;
-    } else {
-        Emit8 E{B.tree, B.refs, pad, {}, {}, 0, 0};
+        return true;
+    }
+    // BVH8: the SAH collapse does not bound the wide depth, so tighten the binary tree's depth cap
+    // until the wide tree fits the traversal stack (kTraversalStack8 entries).
+    static const uint32_t kCaps[] = {32u, 30u, 28u, 26u, 24u, 22u, 20u};
+    const uint32_t max_depth8 = params && params->max_wide_depth ? params->max_wide_depth : uint32_t(kTraversalStack8) - 1u;
+    std::vector<uint32_t> caps;
+    if (params && params->binary_depth_cap) caps.push_back(params->binary_depth_cap);
+    else caps.assign(std::begin(kCaps), std::end(kCaps));
+    uint32_t last_depth = 0;
+    for (uint32_t cap : caps) {
+        for (uint32_t t = 0; t < ntris; ++t) B.refs[t] = t;
+        B.depth_cap = cap;
+        double sah = 0.0;
+        if (!B.build(ntris, err, sah)) return false;
+        Emit8 E{B.tree, B.refs, pad, {}, {}, 0, 0, {}, {}, {}};
         E.run();
-        if (E.max_depth + 1 > uint32_t(kTraversalStack8)) {
-            err = "build_bvh: BVH8 deeper than the traversal stack (" + std::to_string(E.max_depth) + ")";
+        last_depth = E.max_depth;
+        if (E.max_depth > max_depth8) continue;
+        if (E.tri_order.size() != ntris) {
+            err = "build_bvh: BVH8 emission lost triangles";
             return false;
         }
+        out.sah_cost = sah;
         out.nodes8 = std::move(E.nodes);
         out.tri_order = std::move(E.tri_order);
         out.max_depth = E.max_depth;
         out.num_leaves = E.leaves;
-        if (out.tri_order.size() != ntris) {
-            err = "build_bvh: BVH8 emission lost triangles";
-            return false;
-        }
+        out.binary_depth_cap = cap;
+        return true;
     }
-    return true;
+    err = "build_bvh: BVH8 deeper than the traversal stack (" + std::to_string(last_depth) + ")";
+    return false;
 }
 
 }  // namespace dxrpt

@@ -19,11 +19,19 @@ struct BvhBuildResult {
     uint32_t max_depth = 0;           // of the emitted layout
     uint32_t num_leaves = 0;
     double sah_cost = 0.0;            // binary tree, C_trav = 1, C_tri = 1, relative to root area
+    uint32_t binary_depth_cap = 0;    // BVH8: depth cap of the binary tree that was collapsed
+};
+
+// Optional builder parameters (diagnostics; the product uses the defaults).
+struct BvhBuildParams {
+    uint32_t binary_depth_cap = 0;  // BVH8: force this binary depth cap (0: tighten until the tree fits)
+    uint32_t max_wide_depth = 0;    // BVH8: accepted wide depth (0: kTraversalStack8 - 1)
 };
 
 // tri_positions: ntris * 9 floats (v0.xyz, v1.xyz, v2.xyz) in global triangle order.
 // width 2 -> BVH2 (leaves <= kMaxLeafTris), width 8 -> compressed BVH8 (leaves <= kMaxLeafTris8).
 // Deterministic: the same input always yields the same tree.
-bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildResult& out, std::string& err);
+bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildResult& out, std::string& err,
+               const BvhBuildParams* params = nullptr);
 
 }  // namespace dxrpt

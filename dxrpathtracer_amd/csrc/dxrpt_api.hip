@@ -92,8 +92,10 @@ struct dxrpt_ctx {
     uint32_t num_cus = 256;
     uint32_t opt_trav_mode = 0;     // DXRPT_OPT_TRAVERSAL_MODE: 0 one thread per ray, 1 persistent
     uint32_t opt_refill = 16;       // DXRPT_OPT_REFILL_LANES
+    uint32_t opt_chunks = 4;        // DXRPT_OPT_CHUNKS_PER_WAVE
     int built_width = 0;
-    DevBuf d_trav;  // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
+    DevBuf d_trav;   // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
+    DevBuf d_spill;  // BVH8 traversal stack entries beyond the LDS part (deep trees only)
     // kernel timing: a ring of per-frame event sets, harvested lazily
     struct FrameEvents {
         std::vector<hipEvent_t> ev;
@@ -115,6 +117,7 @@ struct dxrpt_ctx {
         for (auto& qb : f_q)
             for (DevBuf& b : qb) b.release();
         d_trav.release();
+        d_spill.release();
         for (auto& f : ring)
             for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
     }
@@ -157,15 +160,23 @@ std::vector<float> make_lut() {
     return l;
 }
 
-SceneDev scene_dev(const dxrpt_ctx* c) {
+// Device view of the scene for launches of up to `traversal_threads` global threads (sizes the
+// BVH8 stack spill slab, allocated only when the tree is deeper than the LDS part of the stack).
+SceneDev scene_dev(dxrpt_ctx* c, uint32_t traversal_threads) {
     SceneDev s;
     s.nodes = c->d_nodes.as<BvhNode>();
     s.nodes8 = c->d_nodes8.as<Bvh8Node>();
     s.width = c->built_width;
-    {
-        const uint32_t entries = std::min<uint32_t>(c->bvh.max_depth + 1u,
-                                                    c->built_width == 8 ? uint32_t(kTraversalStack8) : uint32_t(kTraversalStack));
-        s.stack_ints = c->built_width == 8 ? 2u * entries : entries;
+    const uint32_t entries = c->bvh.max_depth + 1u;
+    if (c->built_width == 8) {
+        s.stack_ints = 2u * std::min<uint32_t>(entries, uint32_t(kStackLds8));
+        if (entries > uint32_t(kStackLds8)) {
+            c->d_spill.ensure(size_t(kTraversalStack8 - kStackLds8) * traversal_threads * sizeof(uint2));
+            s.spill8 = c->d_spill.as<uint2>();
+            s.spill_stride = traversal_threads;
+        }
+    } else {
+        s.stack_ints = std::min<uint32_t>(entries, uint32_t(kTraversalStack));
     }
     s.tris = c->d_tris.as<TriRecord>();
     s.vertices = c->d_vertices.as<dxrpt_mesh_vertex>();
@@ -356,6 +367,9 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_TRAVERSAL_MODE) {
             require(value <= 1, "dxrpt_set_option: traversal mode must be 0 or 1");
             ctx->opt_trav_mode = uint32_t(value);
+        } else if (option == DXRPT_OPT_CHUNKS_PER_WAVE) {
+            require(value >= 1 && value <= 64, "dxrpt_set_option: chunks per wave must be 1..64");
+            ctx->opt_chunks = uint32_t(value);
         } else if (option == DXRPT_OPT_REFILL_LANES) {
             require(value >= 1 && value <= 64, "dxrpt_set_option: refill lanes must be in [1, 64]");
             ctx->opt_refill = uint32_t(value);
@@ -596,7 +610,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.height = height;
         fp.trav = nullptr;
         // 32 KiB of LDS per 256-thread workgroup -> 5 resident workgroups per CU (160 KiB)
-        fp.persistent_blocks = ctx->opt_trav_mode == 1 ? ctx->num_cus * 5u : 0u;
+        fp.chunks_per_wave = ctx->opt_trav_mode == 1 ? ctx->opt_chunks : 0u;
         fp.refill_lanes = ctx->opt_refill;
         hipStream_t s = static_cast<hipStream_t>(stream);
         if (ctx->opt_count) {
@@ -620,7 +634,8 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             f.pending = true;
             ev = f.ev.data();
         }
-        HIP_CHECK(launch_frame(scene_dev(ctx), ctx->fb, fp, s, ev));
+        const SceneDev sd = scene_dev(ctx, frame_traversal_threads(paths, ctx->fb.shadow_slots, fp.chunks_per_wave));
+        HIP_CHECK(launch_frame(sd, ctx->fb, fp, s, ev));
         ctx->last_stream = s;
         ctx->last_L = settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength;
         std::memset(&ctx->last, 0, sizeof(ctx->last));
@@ -672,7 +687,7 @@ int dxrpt_trace_rays(dxrpt_ctx* ctx, const float* rays, uint32_t num_rays, uint3
         require(ctx->bvh_built, "dxrpt_trace_rays: acceleration structure not built", DXRPT_E_STATE);
         require(num_rays == 0 || (rays && hits), "dxrpt_trace_rays: null argument");
         upload_textures(ctx);
-        HIP_CHECK(launch_trace_rays(scene_dev(ctx), reinterpret_cast<const float4*>(rays), num_rays, flags,
+        HIP_CHECK(launch_trace_rays(scene_dev(ctx, trace_rays_threads(num_rays)), reinterpret_cast<const float4*>(rays), num_rays, flags,
                                     reinterpret_cast<float4*>(hits), static_cast<hipStream_t>(stream)));
     });
 }

@@ -85,10 +85,13 @@ struct SceneDev {
     uint32_t sky_res = 0;
     uint32_t num_textures = 0;
     int width = 8;  // BVH width actually built: 2 or 8
-    // LDS traversal stack, ints per lane: BVH2 one node index per entry, BVH8 two words (node-group
-    // base, hit/internal masks) per entry; entries = built tree depth + 1 (<= kTraversalStack /
-    // kTraversalStack8).  A shallower tree -> less LDS per workgroup -> more resident waves.
+    // LDS traversal stack, ints per lane: BVH2 one node index per entry, entries = tree depth + 1
+    // (<= kTraversalStack); BVH8 two words (node-group base, hit/internal masks) per entry, entries =
+    // min(tree depth + 1, kStackLds8).  Less LDS per workgroup -> more resident waves.
     uint32_t stack_ints = kTraversalStack;
+    // BVH8 group-stack entries kStackLds8 .. kTraversalStack8-1: [entry * spill_stride + global thread]
+    uint2* spill8 = nullptr;
+    uint32_t spill_stride = 0;  // >= the global thread count of every BVH8 traversal launch
 };
 
 struct FrameParams {
@@ -102,8 +105,8 @@ struct FrameParams {
     uint32_t num_paths;
     uint32_t width, height;
     unsigned long long* trav;        // non-null: count traversal work ([0..1] closest node/tri, [2..3] shadow)
-    uint32_t persistent_blocks;      // grid of the persistent BVH8 traversal kernels; 0 = one thread per ray
-    uint32_t refill_lanes;           // persistent kernels: refill once this many lanes of a wave are idle
+    uint32_t chunks_per_wave;        // BVH8 wave-pool traversal: 64-ray chunks per wave; 0 = one thread per ray
+    uint32_t refill_lanes;           // wave-pool kernels: refill once this many lanes of a wave are idle
 };
 
 // Kernel sequence of one frame: raygen, then (trace, shade, shadow, resolve) per depth 1..L-1, then
@@ -117,5 +120,10 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
 // (d.xyz, tmax) pairs; hits are (t, b1, b2, bits(global tri)) with t = -1 and tri = ~0 on miss.
 hipError_t launch_trace_rays(const SceneDev& scene, const float4* rays, uint32_t n, uint32_t flags, float4* hits,
                              hipStream_t stream);
+
+// Global thread count of the largest BVH8 traversal launch of a frame / of a trace_rays call (sizes
+// the stack spill slab).
+uint32_t frame_traversal_threads(uint32_t num_paths, uint32_t shadow_slots, uint32_t chunks_per_wave);
+uint32_t trace_rays_threads(uint32_t n);
 
 }  // namespace dxrpt

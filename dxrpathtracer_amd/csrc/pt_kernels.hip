@@ -342,27 +342,44 @@ PT_DEV bool trav8_step(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp
     const float by = __builtin_fmaf(__uint_as_float(w0.y), R.inv.y, -R.ood.y);
     const float bz = __builtin_fmaf(__uint_as_float(w0.z), R.inv.z, -R.ood.z);
     const float tmx = h.t;
-    uint32_t ihits = 0, thits = 0;
+    // Near/far quantised planes per axis chosen once per node from the ray octant (Ylitie et al. 2017,
+    // sec. 3.2): with inv >= 0 the near plane of every child is qlo, else qhi, so this equals the
+    // min/max of the two slab distances.  Words: w2 = (qlo_x 0-3, 4-7, qlo_y 0-3, 4-7),
+    // w3 = (qlo_z .., qhi_x ..), w4 = (qhi_y .., qhi_z ..).
+    const bool sxn = (R.oct & 4u) != 0u, syn = (R.oct & 2u) != 0u, szn = (R.oct & 1u) != 0u;
+    const uint32_t nx0 = sxn ? w3.z : w2.x, nx1 = sxn ? w3.w : w2.y, fx0 = sxn ? w2.x : w3.z, fx1 = sxn ? w2.y : w3.w;
+    const uint32_t ny0 = syn ? w4.x : w2.z, ny1 = syn ? w4.y : w2.w, fy0 = syn ? w2.z : w4.x, fy1 = syn ? w2.w : w4.y;
+    const uint32_t nz0 = szn ? w4.z : w3.x, nz1 = szn ? w4.w : w3.y, fz0 = szn ? w3.x : w4.z, fz1 = szn ? w3.y : w4.w;
+    uint32_t hm = 0;  // hit children, slot space
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
         const uint32_t sh = 8u * uint32_t(c & 3);
+        const float tnx = __builtin_fmaf(float(((c < 4 ? nx0 : nx1) >> sh) & 0xFFu), ax, bx);
+        const float tny = __builtin_fmaf(float(((c < 4 ? ny0 : ny1) >> sh) & 0xFFu), ay, by);
+        const float tnz = __builtin_fmaf(float(((c < 4 ? nz0 : nz1) >> sh) & 0xFFu), az, bz);
+        const float tfx = __builtin_fmaf(float(((c < 4 ? fx0 : fx1) >> sh) & 0xFFu), ax, bx);
+        const float tfy = __builtin_fmaf(float(((c < 4 ? fy0 : fy1) >> sh) & 0xFFu), ay, by);
+        const float tfz = __builtin_fmaf(float(((c < 4 ? fz0 : fz1) >> sh) & 0xFFu), az, bz);
+        const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, R.tmin));
+        const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tmx));
         const uint32_t m = ((c < 4 ? w1.z : w1.w) >> sh) & 0xFFu;
-        const float qlx = float(((c < 4 ? w2.x : w2.y) >> sh) & 0xFFu);
-        const float qly = float(((c < 4 ? w2.z : w2.w) >> sh) & 0xFFu);
-        const float qlz = float(((c < 4 ? w3.x : w3.y) >> sh) & 0xFFu);
-        const float qhx = float(((c < 4 ? w3.z : w3.w) >> sh) & 0xFFu);
-        const float qhy = float(((c < 4 ? w4.x : w4.y) >> sh) & 0xFFu);
-        const float qhz = float(((c < 4 ? w4.z : w4.w) >> sh) & 0xFFu);
-        const float tlx = __builtin_fmaf(qlx, ax, bx), thx = __builtin_fmaf(qhx, ax, bx);
-        const float tly = __builtin_fmaf(qly, ay, by), thy = __builtin_fmaf(qhy, ay, by);
-        const float tlz = __builtin_fmaf(qlz, az, bz), thz = __builtin_fmaf(qhz, az, bz);
-        const float tn = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), R.tmin));
-        const float tf = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tmx));
-        const bool hit = m != 0u && tn <= tf;
-        if (hit) {
-            if (m & kMetaInternal) ihits |= 1u << ((m & 7u) ^ R.oct);
-            else thits |= ((1u << (m >> 5)) - 1u) << (m & 31u);
-        }
+        hm |= uint32_t(m != 0u && tn <= tf) << c;
+    }
+    const uint32_t imask = w0.w >> 24;
+    // internal hits to key space (bit slot ^ oct): three conditional bit-group swaps
+    uint32_t ihits = hm & imask;
+    if (R.oct & 1u) ihits = ((ihits & 0x55u) << 1) | ((ihits >> 1) & 0x55u);
+    if (R.oct & 2u) ihits = ((ihits & 0x33u) << 2) | ((ihits >> 2) & 0x33u);
+    if (R.oct & 4u) ihits = ((ihits & 0x0Fu) << 4) | ((ihits >> 4) & 0x0Fu);
+    // leaf hits -> triangle bits ((count << 5) | offset per leaf slot)
+    uint32_t thits = 0;
+    uint32_t lh = hm & ~imask;
+    const unsigned long long meta = (static_cast<unsigned long long>(w1.w) << 32) | w1.z;
+    while (lh) {
+        const uint32_t c = uint32_t(__builtin_ctz(lh));
+        lh &= lh - 1u;
+        const uint32_t m = uint32_t(meta >> (8u * c)) & 0xFFu;
+        thits |= ((1u << (m >> 5)) - 1u) << (m & 31u);
     }
     while (thits) {
         const uint32_t b = uint32_t(__builtin_ctz(thits));
@@ -371,7 +388,7 @@ PT_DEV bool trav8_step(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp
         if (test_triangle<kAnyHit>(S, w1.y + b, R.o, R.d, R.tmin, R.tmax, R.alpha, h)) return true;
     }
     uint32_t gbase = w1.x;
-    uint32_t gword = (ihits << 24) | (w0.w >> 24);
+    uint32_t gword = (ihits << 24) | imask;
     while (true) {
         if (gword >> 24) {
             const uint32_t k = 31u - uint32_t(__builtin_clz(gword));
@@ -379,16 +396,27 @@ PT_DEV bool trav8_step(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp
             const uint32_t slot = (k - 24u) ^ R.oct;
             node = gbase + uint32_t(__builtin_popcount(gword & 0xFFu & ((1u << slot) - 1u)));
             if (gword >> 24) {
-                stk[(2 * sp) * kBlock] = int(gbase);
-                stk[(2 * sp + 1) * kBlock] = int(gword);
+                if (sp < kStackLds8) {
+                    stk[(2 * sp) * kBlock] = int(gbase);
+                    stk[(2 * sp + 1) * kBlock] = int(gword);
+                } else {  // rare: deeper entries spill to this thread's global slab
+                    S.spill8[size_t(sp - kStackLds8) * S.spill_stride + blockIdx.x * kBlock + threadIdx.x] =
+                        make_uint2(gbase, gword);
+                }
                 ++sp;
             }
             return false;
         }
         if (sp == 0) return true;
         --sp;
-        gbase = uint32_t(stk[(2 * sp) * kBlock]);
-        gword = uint32_t(stk[(2 * sp + 1) * kBlock]);
+        if (sp < kStackLds8) {
+            gbase = uint32_t(stk[(2 * sp) * kBlock]);
+            gword = uint32_t(stk[(2 * sp + 1) * kBlock]);
+        } else {
+            const uint2 e = S.spill8[size_t(sp - kStackLds8) * S.spill_stride + blockIdx.x * kBlock + threadIdx.x];
+            gbase = e.x;
+            gword = e.y;
+        }
     }
 }
 
@@ -825,11 +853,12 @@ __global__ __launch_bounds__(kBlock) void k_resolve(KArgs A, int depth) {
     *dst = r;
 }
 
-// Persistent BVH8 traversal for the radiance (kShadow = false) and shadow (true) queues of one depth.
-// The grid is sized to the resident capacity.  Wave w owns the 64-ray chunks w, w + nwaves,
-// w + 2 nwaves, ... of the queue (coherent within a chunk, balanced over the image) and advances every
-// lane by one node visit per iteration; lanes whose ray finished are refilled from the wave's sequence
-// once >= refill lanes are idle (Aila & Laine 2009, "replacing terminated rays").  No atomics.
+// Wave-pool BVH8 traversal for the radiance (kShadow = false) and shadow (true) queues of one depth.
+// Wave w owns the queue items [w * K * 64, (w + 1) * K * 64) (K = chunks_per_wave consecutive 64-ray
+// chunks) and advances every lane by one node visit per iteration; lanes whose ray finished are
+// refilled from the pool once >= refill lanes are idle (Aila & Laine 2009, "replacing terminated
+// rays"), so a wave's time follows the pool's total work instead of K times its slowest ray.  The
+// grid covers the queue; the dispatcher balances waves across CUs.  No atomics.
 template <bool kCount, bool kShadow>
 __global__ __launch_bounds__(kBlock) void k_traverse8p(KArgs A, int depth) {
     extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved (launch_lds_bytes)
@@ -837,12 +866,12 @@ __global__ __launch_bounds__(kBlock) void k_traverse8p(KArgs A, int depth) {
     const uint32_t* cnt = kShadow ? shadow_counts(A.F, depth) : radiance_counts(A.F, depth);
     const uint32_t cap = kShadow ? A.F.shadow_slots * A.F.cap_r : A.F.cap_r;
     const uint32_t count = queue_total(cnt);
-    const uint32_t nwaves = gridDim.x * (kBlock / 64u);
     const uint32_t wave = blockIdx.x * (kBlock / 64u) + threadIdx.x / 64u;
-    const uint32_t nchunks = (count + 63u) / 64u;
-    const uint32_t mychunks = nchunks > wave ? (nchunks - wave + nwaves - 1u) / nwaves : 0u;
-    const uint32_t end = mychunks * 64u;  // length of this wave's item sequence j = 0 .. end-1
-    uint32_t next = 0;
+    const uint32_t pool = A.P.chunks_per_wave * 64u;
+    const uint32_t begin = wave * pool;
+    if (begin >= count) return;
+    const uint32_t end = min(count, begin + pool);
+    uint32_t next = begin;
     const uint32_t refill = A.P.refill_lanes;
     const unsigned long long lt = (1ull << __lane_id()) - 1ull;
     // Radiance rays: FORCE_OPAQUE iff PathLength > MaxAnyHitPathLength (RayTrace.hlsl:132, 401);
@@ -862,9 +891,8 @@ __global__ __launch_bounds__(kBlock) void k_traverse8p(KArgs A, int depth) {
         if (next < end && nidle >= refill) {
             if (!active) {
                 const uint32_t j = next + uint32_t(__popcll(idle & lt));
-                const uint32_t idx = (wave + (j >> 6) * nwaves) * 64u + (j & 63u);
-                if (j < end && idx < count) {
-                    const uint32_t pos = queue_pos(cnt, cap, idx);
+                if (j < end) {
+                    const uint32_t pos = queue_pos(cnt, cap, j);
                     if (kShadow) {
                         item = A.F.sh_queue[pos];
                         const float4 o4 = A.F.sh_org[item];
@@ -943,6 +971,22 @@ __global__ __launch_bounds__(kBlock) void k_trace_rays(SceneDev S, const float4*
 
 static inline uint32_t grid_for(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 
+// Grid of the wave-pool kernel over a queue of at most n items (4 waves per workgroup).
+static inline uint32_t pool_grid(uint32_t n, uint32_t chunks_per_wave) {
+    const uint32_t waves = (n + 64u * chunks_per_wave - 1u) / (64u * chunks_per_wave);
+    return (waves + kBlock / 64u - 1u) / (kBlock / 64u);
+}
+
+uint32_t frame_traversal_threads(uint32_t num_paths, uint32_t shadow_slots, uint32_t chunks_per_wave) {
+    const uint32_t gs = std::min<uint32_t>(grid_for(num_paths * shadow_slots), kShadowGrid);
+    uint32_t g = std::max(grid_for(num_paths), gs);
+    if (chunks_per_wave)
+        g = std::max(g, std::max(pool_grid(num_paths, chunks_per_wave), pool_grid(num_paths * shadow_slots, chunks_per_wave)));
+    return g * kBlock;
+}
+
+uint32_t trace_rays_threads(uint32_t n) { return grid_for(n) * kBlock; }
+
 hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream,
                         hipEvent_t* ev) {
     KArgs A{scene, fb, fp};
@@ -961,8 +1005,9 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
     const int L = fp.set.MaxPathLength < 2 ? 2 : fp.set.MaxPathLength;
     for (int d = 1; d <= L - 1; ++d) {
         const bool w8 = scene.width == 8;
-        const bool pers = w8 && fp.persistent_blocks > 0;
-        const uint32_t gp = fp.persistent_blocks;
+        const bool pers = w8 && fp.chunks_per_wave > 0;
+        const uint32_t gp = pers ? pool_grid(fp.num_paths, fp.chunks_per_wave) : 0u;
+        const uint32_t gps = pers ? pool_grid(fp.num_paths * fb.shadow_slots, fp.chunks_per_wave) : 0u;
         if (w8 && !pers) {
             if (count) hipLaunchKernelGGL((k_trace<true, 8>), dim3(g), dim3(kBlock), lds, stream, A, d);
             else hipLaunchKernelGGL((k_trace<false, 8>), dim3(g), dim3(kBlock), lds, stream, A, d);
@@ -981,8 +1026,8 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
             if (count) hipLaunchKernelGGL((k_shadow<true, 8>), dim3(gs), dim3(kBlock), lds, stream, A, d);
             else hipLaunchKernelGGL((k_shadow<false, 8>), dim3(gs), dim3(kBlock), lds, stream, A, d);
         } else if (pers) {
-            if (count) hipLaunchKernelGGL((k_traverse8p<true, true>), dim3(gp), dim3(kBlock), lds, stream, A, d);
-            else hipLaunchKernelGGL((k_traverse8p<false, true>), dim3(gp), dim3(kBlock), lds, stream, A, d);
+            if (count) hipLaunchKernelGGL((k_traverse8p<true, true>), dim3(gps), dim3(kBlock), lds, stream, A, d);
+            else hipLaunchKernelGGL((k_traverse8p<false, true>), dim3(gps), dim3(kBlock), lds, stream, A, d);
         } else {
             if (count) hipLaunchKernelGGL((k_shadow<true, 2>), dim3(gs), dim3(kBlock), lds, stream, A, d);
             else hipLaunchKernelGGL((k_shadow<false, 2>), dim3(gs), dim3(kBlock), lds, stream, A, d);

@@ -61,7 +61,9 @@ struct Bvh8Node {
 static_assert(sizeof(Bvh8Node) == 80, "Bvh8Node must be 80 B");
 
 constexpr int kMaxLeafTris8 = 3;
-constexpr int kTraversalStack8 = 16;  // LDS group-stack entries per lane; builder caps BVH8 depth to fit.
+constexpr int kTraversalStack8 = 16;  // group-stack entries per lane; the builder caps BVH8 depth to fit.
+constexpr int kStackLds8 = 6;         // of which the first entries live in LDS, the rest in a global slab
+                                      // (traversals deeper than 6 pending groups are rare: see DESIGN.md)
 constexpr uint8_t kMetaInternal = 0x80;
 
 // Leaf triangle record, 48 B.

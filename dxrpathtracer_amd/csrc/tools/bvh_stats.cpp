@@ -1,0 +1,267 @@
+// bvh_stats — host-side BVH quality report for the builder (no GPU needed).
+//
+// Builds the BVH2 and BVH8 layouts of a host scene exactly as dxrpt_build_bvh does, then walks them with
+// a scalar restatement of the device traversal (same node decode, same visit order) for three ray sets:
+// primary camera rays, one cosine-distributed bounce per primary hit, and sun shadow rays from the
+// primary hits.  Prints node visits and triangle tests per ray, the quantities the traversal kernels'
+// VALU cost scales with, so builder changes can be compared on CPU before spending GPU time.
+//
+//   make tools && ./build/bvh_stats [scene_id=0] [grid_w=320] [grid_h=180]
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "../../../include/dxrpt.h"
+#include "../../../include/dxrpt_host.h"
+#include "../bvh_build.h"
+
+using namespace dxrpt;
+
+namespace {
+
+struct V3 {
+    float x, y, z;
+};
+V3 sub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+V3 cross(V3 a, V3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+V3 norm(V3 a) {
+    float l = sqrtf(dot(a, a));
+    return {a.x / l, a.y / l, a.z / l};
+}
+
+struct Counters {
+    uint64_t rays = 0, nodes = 0, tris = 0, hits = 0;
+    uint64_t stack_hist[40] = {};  // rays by maximum stack occupancy
+};
+
+struct Scene {
+    std::vector<float> pos;  // ntris * 9
+    uint32_t ntris = 0;
+};
+
+float hit_tri(const Scene& S, uint32_t t, V3 o, V3 d, float tmin, float tmax) {
+    const float* p = &S.pos[size_t(t) * 9];
+    V3 v0{p[0], p[1], p[2]}, v1{p[3], p[4], p[5]}, v2{p[6], p[7], p[8]};
+    V3 e1 = sub(v1, v0), e2 = sub(v2, v0);
+    V3 pv = cross(d, e2);
+    float det = dot(e1, pv);
+    if (det == 0.0f) return -1.0f;
+    float inv = 1.0f / det;
+    V3 tv = sub(o, v0);
+    float u = dot(tv, pv) * inv;
+    if (u < 0.0f || u > 1.0f) return -1.0f;
+    V3 qv = cross(tv, e1);
+    float v = dot(d, qv) * inv;
+    if (v < 0.0f || u + v > 1.0f) return -1.0f;
+    float tt = dot(e2, qv) * inv;
+    return (tt >= tmin && tt < tmax) ? tt : -1.0f;
+}
+
+// Scalar BVH8 traversal: the same decode and visit order as trav8_step (pt_kernels.hip).
+float trace8(const Scene& S, const BvhBuildResult& B, V3 o, V3 d, float tmin, float tmax, bool any, Counters& c,
+             uint32_t* out_tri) {
+    V3 inv{1.0f / (fabsf(d.x) > 1e-20f ? d.x : copysignf(1e-20f, d.x)), 1.0f / (fabsf(d.y) > 1e-20f ? d.y : copysignf(1e-20f, d.y)),
+           1.0f / (fabsf(d.z) > 1e-20f ? d.z : copysignf(1e-20f, d.z))};
+    V3 ood{o.x * inv.x, o.y * inv.y, o.z * inv.z};
+    const uint32_t oct = (inv.x < 0 ? 4u : 0u) | (inv.y < 0 ? 2u : 0u) | (inv.z < 0 ? 1u : 0u);
+    float best = tmax;
+    uint32_t best_tri = ~0u;
+    std::vector<std::pair<uint32_t, uint32_t>> stk;
+    uint32_t node = 0;
+    size_t max_sp = 0;
+    c.rays++;
+    struct Hist {
+        Counters& c;
+        size_t& m;
+        ~Hist() { c.stack_hist[std::min<size_t>(m, 39)]++; }
+    } hist{c, max_sp};
+    for (;;) {
+        c.nodes++;
+        const Bvh8Node& n = B.nodes8[node];
+        float a[3], b[3];
+        const float* invp = &inv.x;
+        const float* oodp = &ood.x;
+        for (int k = 0; k < 3; ++k) {
+            uint32_t eb = uint32_t(n.e[k]) << 23;
+            float sc;
+            memcpy(&sc, &eb, 4);
+            a[k] = sc * invp[k];
+            b[k] = fmaf(n.p[k], invp[k], -oodp[k]);
+        }
+        uint32_t ihits = 0, thits = 0;
+        for (int s = 0; s < 8; ++s) {
+            uint32_t m = n.meta[s];
+            if (!m) continue;
+            float tn = tmin, tf = best;
+            for (int k = 0; k < 3; ++k) {
+                float t0 = fmaf(float(n.qlo[k][s]), a[k], b[k]), t1 = fmaf(float(n.qhi[k][s]), a[k], b[k]);
+                tn = std::max(tn, std::min(t0, t1));
+                tf = std::min(tf, std::max(t0, t1));
+            }
+            if (tn > tf) continue;
+            if (m & kMetaInternal) ihits |= 1u << ((m & 7u) ^ oct);
+            else thits |= ((1u << (m >> 5)) - 1u) << (m & 31u);
+        }
+        while (thits) {
+            uint32_t bit = __builtin_ctz(thits);
+            thits &= thits - 1;
+            c.tris++;
+            uint32_t t = B.tri_order[n.base_tri + bit];
+            float tt = hit_tri(S, t, o, d, tmin, best);
+            if (tt >= 0.0f) {
+                best = tt;
+                best_tri = t;
+                if (any) {
+                    c.hits++;
+                    if (out_tri) *out_tri = t;
+                    return best;
+                }
+            }
+        }
+        uint32_t gbase = n.base_child, gword = (ihits << 24) | n.imask;
+        for (;;) {
+            if (gword >> 24) {
+                uint32_t k = 31u - __builtin_clz(gword);
+                gword &= ~(1u << k);
+                uint32_t slot = (k - 24u) ^ oct;
+                node = gbase + __builtin_popcount(gword & 0xFFu & ((1u << slot) - 1u));
+                if (gword >> 24) stk.push_back({gbase, gword});
+                max_sp = std::max(max_sp, stk.size());
+                break;
+            }
+            if (stk.empty()) {
+                if (best_tri != ~0u) c.hits++;
+                if (out_tri) *out_tri = best_tri;
+                return best_tri != ~0u ? best : -1.0f;
+            }
+            gbase = stk.back().first;
+            gword = stk.back().second;
+            stk.pop_back();
+        }
+    }
+}
+
+uint64_t splitmix(uint64_t& s) {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+float rnd(uint64_t& s) { return float(splitmix(s) >> 40) * (1.0f / 16777216.0f); }
+
+void report(const char* name, const Counters& c) {
+    printf("  %-9s rays %8llu  nodes/ray %6.2f  tris/ray %6.2f  hit %5.1f%%  stack>4 %.3f%% >6 %.4f%% >8 %.5f%% max ",
+           name, (unsigned long long)c.rays, double(c.nodes) / c.rays, double(c.tris) / c.rays, 100.0 * c.hits / c.rays,
+           [&] { uint64_t n = 0; for (int i = 5; i < 40; ++i) n += c.stack_hist[i]; return 100.0 * n / c.rays; }(),
+           [&] { uint64_t n = 0; for (int i = 7; i < 40; ++i) n += c.stack_hist[i]; return 100.0 * n / c.rays; }(),
+           [&] { uint64_t n = 0; for (int i = 9; i < 40; ++i) n += c.stack_hist[i]; return 100.0 * n / c.rays; }());
+    int mx = 0;
+    for (int i = 0; i < 40; ++i)
+        if (c.stack_hist[i]) mx = i;
+    printf("%d\n", mx);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const uint32_t scene_id = argc > 1 ? uint32_t(atoi(argv[1])) : 0u;
+    const uint32_t gw = argc > 2 ? uint32_t(atoi(argv[2])) : 320u;
+    const uint32_t gh = argc > 3 ? uint32_t(atoi(argv[3])) : 180u;
+    BvhBuildParams params;  // argv[4]: binary depth cap to explore (the wide depth is then unbounded)
+    if (argc > 4) {
+        params.binary_depth_cap = uint32_t(atoi(argv[4]));
+        params.max_wide_depth = 1000u;
+    }
+    dxrpt_host_scene* hs = nullptr;
+    if (dxrpt_host_scene_create(scene_id, 0, 0, &hs) != 0) {
+        fprintf(stderr, "scene: %s\n", dxrpt_host_last_error());
+        return 1;
+    }
+    Scene S;
+    S.ntris = hs->num_indices / 3;
+    S.pos.resize(size_t(S.ntris) * 9);
+    for (uint32_t g = 0; g < hs->num_geometries; ++g) {
+        const dxrpt_geometry_info& gi = hs->geometries[g];
+        uint32_t end = g + 1 < hs->num_geometries ? hs->geometries[g + 1].IdxOffset / 3 : S.ntris;
+        for (uint32_t t = gi.IdxOffset / 3; t < end; ++t)
+            for (int k = 0; k < 3; ++k) {
+                uint32_t idx = hs->idx_bytes == 2 ? static_cast<const uint16_t*>(hs->indices)[t * 3 + k]
+                                                  : static_cast<const uint32_t*>(hs->indices)[t * 3 + k];
+                memcpy(&S.pos[size_t(t) * 9 + k * 3], hs->vertices[idx + gi.VtxOffset].Position, 12);
+            }
+    }
+    printf("scene %u: %u triangles\n", scene_id, S.ntris);
+    BvhBuildResult B;
+    std::string err;
+    auto t0 = std::chrono::steady_clock::now();
+    if (!build_bvh(S.pos.data(), S.ntris, 8, B, err, &params)) {
+        fprintf(stderr, "build: %s\n", err.c_str());
+        return 1;
+    }
+    double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    uint64_t slots = 0, leaf_tris = 0, leaves = 0;
+    for (const Bvh8Node& n : B.nodes8)
+        for (int s = 0; s < 8; ++s)
+            if (n.meta[s]) {
+                slots++;
+                if (!(n.meta[s] & kMetaInternal)) {
+                    leaves++;
+                    leaf_tris += n.meta[s] >> 5;
+                }
+            }
+    printf("BVH8: %zu nodes, depth %u (binary cap %u), %.2f children/node, %llu leaves, %.2f tris/leaf, build %.0f ms, SAH(bin) %.2f\n",
+           B.nodes8.size(), B.max_depth, B.binary_depth_cap, double(slots) / B.nodes8.size(), (unsigned long long)leaves,
+           double(leaf_tris) / leaves, ms, B.sah_cost);
+
+    float M[16];
+    dxrpt_host_inv_view_projection(hs->camera_position, hs->camera_rotation[0], hs->camera_rotation[1], 3.14159265f / 4.0f,
+                                   16.0f / 9.0f, 0.1f, 100.0f, M);
+    V3 sun = norm({hs->sun_direction[0], hs->sun_direction[1], hs->sun_direction[2]});
+    Counters prim, bounce, shadow;
+    uint64_t rng = 12345;
+    for (uint32_t y = 0; y < gh; ++y)
+        for (uint32_t x = 0; x < gw; ++x) {
+            float ncx = (x + 0.5f) / gw * 2.0f - 1.0f, ncy = -((y + 0.5f) / gh * 2.0f - 1.0f);
+            float s[4], e[4];
+            for (int j = 0; j < 4; ++j) {
+                s[j] = ncx * M[j] + ncy * M[4 + j] + M[12 + j];
+                e[j] = ncx * M[j] + ncy * M[4 + j] + M[8 + j] + M[12 + j];
+            }
+            V3 o{s[0] / s[3], s[1] / s[3], s[2] / s[3]};
+            V3 en{e[0] / e[3], e[1] / e[3], e[2] / e[3]};
+            V3 dd = sub(en, o);
+            float len = sqrtf(dot(dd, dd));
+            V3 d = norm(dd);
+            uint32_t tri = ~0u;
+            float t = trace8(S, B, o, d, 0.0f, len, false, prim, &tri);
+            if (t < 0.0f) continue;
+            V3 p{o.x + d.x * t, o.y + d.y * t, o.z + d.z * t};
+            const float* v = &S.pos[size_t(tri) * 9];
+            V3 nrm = norm(cross(sub({v[3], v[4], v[5]}, {v[0], v[1], v[2]}), sub({v[6], v[7], v[8]}, {v[0], v[1], v[2]})));
+            if (dot(nrm, d) > 0.0f) nrm = {-nrm.x, -nrm.y, -nrm.z};
+            trace8(S, B, p, sun, 1e-4f, 3.4e38f, true, shadow, nullptr);
+            // cosine-distributed bounce around the facing normal
+            float r1 = rnd(rng), r2 = rnd(rng);
+            float r = sqrtf(r1), phi = 6.2831853f * r2;
+            V3 tt = fabsf(nrm.x) > 0.5f ? norm(cross(nrm, {0, 1, 0})) : norm(cross(nrm, {1, 0, 0}));
+            V3 bb = cross(nrm, tt);
+            float lx = r * cosf(phi), ly = r * sinf(phi), lz = sqrtf(std::max(0.0f, 1.0f - r1));
+            V3 bd = norm({tt.x * lx + bb.x * ly + nrm.x * lz, tt.y * lx + bb.y * ly + nrm.y * lz, tt.z * lx + bb.z * ly + nrm.z * lz});
+            trace8(S, B, p, bd, 1e-4f, 3.4e38f, false, bounce, nullptr);
+        }
+    report("primary", prim);
+    report("bounce", bounce);
+    report("shadow", shadow);
+    // relative VALU cost model of the BVH8 kernels (~225 ops per node visit, ~80 per triangle test)
+    auto cost = [](const Counters& c) { return (225.0 * c.nodes + 80.0 * c.tris) / c.rays; };
+    printf("  cost model (VALU ops/ray): primary %.0f bounce %.0f shadow %.0f\n", cost(prim), cost(bounce), cost(shadow));
+    dxrpt_host_scene_destroy(hs);
+    return 0;
+}

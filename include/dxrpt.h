@@ -261,8 +261,9 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 #define DXRPT_OPT_COUNT_TRAVERSAL 1u  /* 1: instrumented kernels count node visits / triangle tests (slower) */
 #define DXRPT_OPT_KERNEL_TIMING 2u    /* 1: record a hipEvent after every launch of dxrpt_render */
 #define DXRPT_OPT_BVH_WIDTH 3u        /* 2 or 8 (default): layout built by the next dxrpt_build_bvh */
-#define DXRPT_OPT_TRAVERSAL_MODE 4u   /* BVH8: 0 = one thread per ray (default), 1 = persistent waves */
-#define DXRPT_OPT_REFILL_LANES 5u     /* persistent mode: refill a wave once this many lanes are idle */
+#define DXRPT_OPT_TRAVERSAL_MODE 4u   /* BVH8: 0 = one thread per ray (default), 1 = wave pools with lane refill */
+#define DXRPT_OPT_REFILL_LANES 5u     /* wave-pool mode: refill a wave once this many lanes are idle */
+#define DXRPT_OPT_CHUNKS_PER_WAVE 6u  /* wave-pool mode: 64-ray chunks owned by each wave (1..64, default 4) */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

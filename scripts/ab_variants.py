@@ -3,7 +3,7 @@
 workload (Sponza proxy 1920x1080, L=3).  Prints per-kernel ms per frame from the HIP-event timings.
 
     python scripts/ab_variants.py [--frames 16] [--rounds 3] [--variants w8m0,w8m1r16,...]
-variant syntax: w<2|8> m<0|1> [r<lanes>]
+variant syntax: w<2|8> m<0|1> [r<lanes>] [k<chunks per wave>]
 """
 import argparse
 import os
@@ -16,12 +16,12 @@ sys.path.insert(0, REPO)
 
 
 def parse(v):
-    w = int(v[1:v.index("m")])
-    rest = v[v.index("m") + 1:]
-    if "r" in rest:
-        m, r = rest.split("r")
-        return w, int(m), int(r)
-    return w, int(rest), 16
+    """w<width>m<mode>[r<refill lanes>][k<chunks per wave>] -> (width, mode, refill, chunks)"""
+    import re
+    m = re.fullmatch(r"w(\d+)m(\d+)(?:r(\d+))?(?:k(\d+))?", v)
+    if not m:
+        raise SystemExit(f"bad variant {v}")
+    return int(m[1]), int(m[2]), int(m[3] or 16), int(m[4] or 4)
 
 
 def main():
@@ -57,10 +57,11 @@ def main():
     res = {v: [] for v in args.variants.split(",")}
     for rnd in range(args.rounds):
         for v in res:
-            w, m, r = parse(v)
+            w, m, r, k = parse(v)
             t = tracers[w]
             t.set_option(A.OPT_TRAVERSAL_MODE, m)
             t.set_option(A.OPT_REFILL_LANES, r)
+            t.set_option(A.OPT_CHUNKS_PER_WAVE, k)
             for f in range(3):
                 t.render_raw(consts[f], st, accum.data_ptr(), W, H, stream=sh, lights=lights)
             torch.cuda.synchronize()

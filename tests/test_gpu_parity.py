@@ -191,6 +191,26 @@ def test_deterministic_run_to_run(torch_cuda):
     np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("chunks,refill", [(1, 64), (4, 16), (8, 32)])
+def test_wave_pool_traversal_is_bit_identical(torch_cuda, chunks, refill):
+    # DXRPT_OPT_TRAVERSAL_MODE 1 (wave pools with lane refill) only changes which lane traces which
+    # ray: frames must equal the one-thread-per-ray kernels bit for bit (SunTemple: alpha any-hit too)
+    torch = torch_cuda
+    for name in ("sponza", "suntemple"):
+        sc, _ = scene_bundle(name)
+        st = sc.settings(MaxPathLength=4)
+        t = tracer(name)
+        ref = gpu_render(torch, name, 480, 270, st, 2).cpu().numpy()
+        t.set_option(A.OPT_TRAVERSAL_MODE, 1)
+        t.set_option(A.OPT_CHUNKS_PER_WAVE, chunks)
+        t.set_option(A.OPT_REFILL_LANES, refill)
+        try:
+            got = gpu_render(torch, name, 480, 270, st, 2).cpu().numpy()
+        finally:
+            t.set_option(A.OPT_TRAVERSAL_MODE, 0)
+        np.testing.assert_array_equal(got, ref)
+
+
 def _random_rays(rng, n, lo, hi):
     o = rng.uniform(lo, hi, size=(n, 3)).astype(np.float32)
     d = rng.standard_normal((n, 3)).astype(np.float32)
