@@ -93,6 +93,9 @@ struct dxrpt_ctx {
     uint32_t opt_trav_mode = 0;     // DXRPT_OPT_TRAVERSAL_MODE: 0 one thread per ray, 1 persistent
     uint32_t opt_refill = 16;       // DXRPT_OPT_REFILL_LANES
     uint32_t opt_chunks = 4;        // DXRPT_OPT_CHUNKS_PER_WAVE
+    uint32_t opt_postpone = 0;      // DXRPT_OPT_POSTPONE_TRIS
+    uint32_t opt_trace_block = 64;  // DXRPT_OPT_TRACE_BLOCK
+    uint32_t opt_occupancy = 8;     // DXRPT_OPT_OCCUPANCY
     int built_width = 0;
     DevBuf d_trav;   // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
     DevBuf d_spill;  // BVH8 traversal stack entries beyond the LDS part (deep trees only)
@@ -367,6 +370,15 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_TRAVERSAL_MODE) {
             require(value <= 1, "dxrpt_set_option: traversal mode must be 0 or 1");
             ctx->opt_trav_mode = uint32_t(value);
+        } else if (option == DXRPT_OPT_TRACE_BLOCK) {
+            require(value == 64 || value == 128 || value == 256, "dxrpt_set_option: trace block must be 64, 128 or 256");
+            ctx->opt_trace_block = uint32_t(value);
+        } else if (option == DXRPT_OPT_OCCUPANCY) {
+            require(value == 0 || value == 7 || value == 8, "dxrpt_set_option: occupancy must be 0, 7 or 8");
+            ctx->opt_occupancy = uint32_t(value);
+        } else if (option == DXRPT_OPT_POSTPONE_TRIS) {
+            require(value <= 64, "dxrpt_set_option: postpone threshold must be 0..64 lanes");
+            ctx->opt_postpone = uint32_t(value);
         } else if (option == DXRPT_OPT_CHUNKS_PER_WAVE) {
             require(value >= 1 && value <= 64, "dxrpt_set_option: chunks per wave must be 1..64");
             ctx->opt_chunks = uint32_t(value);
@@ -612,6 +624,9 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // 32 KiB of LDS per 256-thread workgroup -> 5 resident workgroups per CU (160 KiB)
         fp.chunks_per_wave = ctx->opt_trav_mode == 1 ? ctx->opt_chunks : 0u;
         fp.refill_lanes = ctx->opt_refill;
+        fp.postpone_tris = ctx->opt_postpone;
+        fp.trace_block = ctx->opt_trace_block;
+        fp.occupancy = ctx->opt_occupancy;
         hipStream_t s = static_cast<hipStream_t>(stream);
         if (ctx->opt_count) {
             fp.trav = ctx->d_trav.as<unsigned long long>();

@@ -107,6 +107,10 @@ struct FrameParams {
     unsigned long long* trav;        // non-null: count traversal work ([0..1] closest node/tri, [2..3] shadow)
     uint32_t chunks_per_wave;        // BVH8 wave-pool traversal: 64-ray chunks per wave; 0 = one thread per ray
     uint32_t refill_lanes;           // wave-pool kernels: refill once this many lanes of a wave are idle
+    uint32_t trace_block;            // workgroup size of the one-thread-per-ray traversal kernels (64..256)
+    uint32_t occupancy;              // BVH8 traversal kernels: 0 compiler default, 7 or 8 waves per SIMD
+    uint32_t postpone_tris;          // wave-pool kernels: test pending triangles once this many lanes hold
+                                     // some (0 = with their node visit)
 };
 
 // Kernel sequence of one frame: raygen, then (trace, shade, shadow, resolve) per depth 1..L-1, then

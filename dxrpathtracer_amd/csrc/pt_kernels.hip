@@ -240,7 +240,7 @@ PT_DEV f3 safe_inverse(f3 d) {
 }
 
 // BVH2 traversal ("while-while", Aila & Laine 2009): nearer child first, farther pushed on a per-lane
-// LDS stack (stk[sp * kBlock]).
+// LDS stack (stk[sp * blockDim.x]).
 template <bool kAnyHit, bool kCount>
 PT_DEV bool traverse2(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, int* stk, HitRec& h,
                       uint32_t& nvisit, uint32_t& ntest) {
@@ -271,7 +271,7 @@ PT_DEV bool traverse2(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
             if (hit0 && hit1) {
                 int first = ch.x, second = ch.y;
                 if (n1 < n0) { first = ch.y; second = ch.x; }
-                stk[sp * kBlock] = second;
+                stk[sp * blockDim.x] = second;
                 ++sp;
                 node = first;
             } else if (hit0 || hit1) {
@@ -279,7 +279,7 @@ PT_DEV bool traverse2(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
             } else {
                 if (sp == 0) return kAnyHit ? false : h.tri != kMiss;
                 --sp;
-                node = stk[sp * kBlock];
+                node = stk[sp * blockDim.x];
             }
         }
         const uint32_t code = ~uint32_t(node);
@@ -290,7 +290,7 @@ PT_DEV bool traverse2(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
         }
         if (sp == 0) return kAnyHit ? false : h.tri != kMiss;
         --sp;
-        node = stk[sp * kBlock];
+        node = stk[sp * blockDim.x];
     }
 }
 
@@ -298,7 +298,7 @@ PT_DEV bool traverse2(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
 // A node visit intersects all 8 quantised child boxes at once; internal hits form a "node group"
 // (base_child, hit bits keyed by slot ^ octant, imask) visited highest key first (near to far), leaf
 // hits are tested right away.  The rest of a group is pushed when descending: <= 1 push per level,
-// 2 x 4 B per entry in LDS (stk[sp * kBlock], stk[(kTraversalStack8 + sp) * kBlock]).
+// 2 x 4 B per entry in LDS (stk[sp * blockDim.x], stk[(kTraversalStack8 + sp) * blockDim.x]).
 // The traversal is a resumable state machine (Ray8 + node + sp) so persistent kernels can advance
 // every lane by one node visit per iteration and refill lanes whose ray finished.
 struct Ray8 {
@@ -323,11 +323,13 @@ PT_DEV void ray8_init(Ray8& R, f3 o, f3 d, float tmin, float tmax, bool alpha, H
     h.geom = 0;
 }
 
-// Visits `node`, then selects the next node (pops when the current group is exhausted).  Returns true
-// when the ray is finished: h.tri != kMiss means hit (closest) / occluded (any-hit).
-template <bool kAnyHit, bool kCount>
-PT_DEV bool trav8_step(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp, int* stk, HitRec& h,
-                       uint32_t& nvisit, uint32_t& ntest) {
+// Visits `node`: its hit leaf triangles become the pending group (tbase, tbits); then selects the next
+// node (pops when the current group is exhausted).  Returns false when no node is left to visit.  The
+// pending triangles must be tested (trav8_tris) before the next node visit, so that the visit order
+// and hence the result are the same however tests and visits of different lanes are interleaved.
+template <bool kCount>
+PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp, int* stk, const HitRec& h,
+                       uint32_t& tbase, uint32_t& tbits, uint32_t& nvisit) {
     if (kCount) ++nvisit;
     const uint4* N = reinterpret_cast<const uint4*>(S.nodes8);
     const uint4 w0 = N[node * 5 + 0];
@@ -381,12 +383,8 @@ PT_DEV bool trav8_step(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp
         const uint32_t m = uint32_t(meta >> (8u * c)) & 0xFFu;
         thits |= ((1u << (m >> 5)) - 1u) << (m & 31u);
     }
-    while (thits) {
-        const uint32_t b = uint32_t(__builtin_ctz(thits));
-        thits &= thits - 1u;
-        if (kCount) ++ntest;
-        if (test_triangle<kAnyHit>(S, w1.y + b, R.o, R.d, R.tmin, R.tmax, R.alpha, h)) return true;
-    }
+    tbase = w1.y;
+    tbits = thits;
     uint32_t gbase = w1.x;
     uint32_t gword = (ihits << 24) | imask;
     while (true) {
@@ -397,27 +395,50 @@ PT_DEV bool trav8_step(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp
             node = gbase + uint32_t(__builtin_popcount(gword & 0xFFu & ((1u << slot) - 1u)));
             if (gword >> 24) {
                 if (sp < kStackLds8) {
-                    stk[(2 * sp) * kBlock] = int(gbase);
-                    stk[(2 * sp + 1) * kBlock] = int(gword);
+                    stk[(2 * sp) * blockDim.x] = int(gbase);
+                    stk[(2 * sp + 1) * blockDim.x] = int(gword);
                 } else {  // rare: deeper entries spill to this thread's global slab
-                    S.spill8[size_t(sp - kStackLds8) * S.spill_stride + blockIdx.x * kBlock + threadIdx.x] =
+                    S.spill8[size_t(sp - kStackLds8) * S.spill_stride + blockIdx.x * blockDim.x + threadIdx.x] =
                         make_uint2(gbase, gword);
                 }
                 ++sp;
             }
-            return false;
+            return true;
         }
-        if (sp == 0) return true;
+        if (sp == 0) return false;
         --sp;
         if (sp < kStackLds8) {
-            gbase = uint32_t(stk[(2 * sp) * kBlock]);
-            gword = uint32_t(stk[(2 * sp + 1) * kBlock]);
+            gbase = uint32_t(stk[(2 * sp) * blockDim.x]);
+            gword = uint32_t(stk[(2 * sp + 1) * blockDim.x]);
         } else {
-            const uint2 e = S.spill8[size_t(sp - kStackLds8) * S.spill_stride + blockIdx.x * kBlock + threadIdx.x];
+            const uint2 e = S.spill8[size_t(sp - kStackLds8) * S.spill_stride + blockIdx.x * blockDim.x + threadIdx.x];
             gbase = e.x;
             gword = e.y;
         }
     }
+}
+
+// Tests the pending triangle group.  Returns true when an any-hit ray found an occluder.
+template <bool kAnyHit, bool kCount>
+PT_DEV bool trav8_tris(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32_t tbits, HitRec& h, uint32_t& ntest) {
+    while (tbits) {
+        const uint32_t b = uint32_t(__builtin_ctz(tbits));
+        tbits &= tbits - 1u;
+        if (kCount) ++ntest;
+        if (test_triangle<kAnyHit>(S, tbase + b, R.o, R.d, R.tmin, R.tmax, R.alpha, h)) return true;
+    }
+    return false;
+}
+
+// One node visit and its triangles.  Returns true when the ray is finished: h.tri != kMiss means hit
+// (closest) / occluded (any-hit).
+template <bool kAnyHit, bool kCount>
+PT_DEV bool trav8_step(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp, int* stk, HitRec& h,
+                       uint32_t& nvisit, uint32_t& ntest) {
+    uint32_t tbase = 0, tbits = 0;
+    const bool more = trav8_node<kCount>(S, R, node, sp, stk, h, tbase, tbits, nvisit);
+    if (tbits && trav8_tris<kAnyHit, kCount>(S, R, tbase, tbits, h, ntest)) return true;
+    return !more;
 }
 
 template <bool kAnyHit, bool kCount>
@@ -559,10 +580,13 @@ __global__ __launch_bounds__(kBlock) void k_raygen(KArgs A) {
     A.F.ps_pix[p] = make_uint2(pixelIdx, accumIdx);
 }
 
-template <bool kCount, int W>
-__global__ __launch_bounds__(kBlock) void k_trace(KArgs A, int depth) {
+// kOcc > 0 asks the compiler for kOcc resident waves per SIMD (register budget 512 / kOcc).
+// Workgroups of 64..256 threads (FrameParams::trace_block).
+template <bool kCount, int W, int kOcc>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
+void k_trace(KArgs A, int depth) {
     extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved (launch_lds_bytes)
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t* cnt = radiance_counts(A.F, depth);
     if (i >= queue_total(cnt)) return;
     const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
@@ -809,14 +833,15 @@ __global__ __launch_bounds__(kBlock) void k_shade(KArgs A, int depth) {
 
 // ShadowHitShader / ShadowMissShader / ShadowAnyHitShader (RayTrace.hlsl:497-507, 532-542):
 // one thread per queued shadow ray (grid-stride); occluded -> contribution * 0 (keeps NaN/Inf).
-template <bool kCount, int W>
-__global__ __launch_bounds__(kBlock) void k_shadow(KArgs A, int depth) {
+template <bool kCount, int W, int kOcc>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
+void k_shadow(KArgs A, int depth) {
     extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved (launch_lds_bytes)
     const uint32_t* cnt = shadow_counts(A.F, depth);
     const uint32_t count = queue_total(cnt);
     const uint32_t cap_s = A.F.shadow_slots * A.F.cap_r;
     uint32_t nv = 0, nt = 0;
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < count; i += gridDim.x * kBlock) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < count; i += gridDim.x * blockDim.x) {
         const uint32_t slot = A.F.sh_queue[queue_pos(cnt, cap_s, i)];
         const float4 o4 = A.F.sh_org[slot];
         const float4 d4 = A.F.sh_dir[slot];
@@ -878,8 +903,9 @@ __global__ __launch_bounds__(kBlock) void k_traverse8p(KArgs A, int depth) {
     // primary rays start at TMin 0 (:118), continuation rays at 1e-5 (:382).
     const bool alphaR = depth <= A.P.set.MaxAnyHitPathLength;
     const float tminR = depth == 1 ? 0.0f : kRayTMin;
-    bool active = false;
-    uint32_t item = 0;
+    const uint32_t postpone = A.P.postpone_tris;
+    bool active = false, more = false;
+    uint32_t item = 0, tbase = 0, tbits = 0;
     Ray8 R;
     HitRec h;
     uint32_t node = 0;
@@ -907,6 +933,8 @@ __global__ __launch_bounds__(kBlock) void k_traverse8p(KArgs A, int depth) {
                     }
                     node = 0;
                     sp = 0;
+                    tbits = 0;
+                    more = true;
                     active = true;
                 }
             }
@@ -916,7 +944,32 @@ __global__ __launch_bounds__(kBlock) void k_traverse8p(KArgs A, int depth) {
             if (next >= end) break;
             continue;
         }
-        if (active && trav8_step<kShadow, kCount>(A.S, R, node, sp, stk, h, nv, nt)) {
+        bool finished = false;
+        if (postpone == 0u) {  // triangles inline with their node visit
+            if (active) {
+                more = trav8_node<kCount>(A.S, R, node, sp, stk, h, tbase, tbits, nv);
+                const bool occ = tbits && trav8_tris<kShadow, kCount>(A.S, R, tbase, tbits, h, nt);
+                tbits = 0;
+                finished = occ || !more;
+            }
+        } else {
+            // Triangle postponement (Ylitie et al. 2017, sec. 4): pending groups wait until >= postpone
+            // lanes hold one (or no lane can visit a node), then those lanes test them together.
+            const uint32_t ntri = uint32_t(__popcll(__ballot(active && tbits != 0u)));
+            const bool node_lane = active && tbits == 0u && more;
+            const uint32_t nnode = uint32_t(__popcll(__ballot(node_lane)));
+            if (ntri >= postpone || nnode == 0u) {
+                if (active && tbits != 0u) {
+                    const bool occ = trav8_tris<kShadow, kCount>(A.S, R, tbase, tbits, h, nt);
+                    tbits = 0;
+                    finished = occ || !more;
+                }
+            } else if (node_lane) {
+                more = trav8_node<kCount>(A.S, R, node, sp, stk, h, tbase, tbits, nv);
+                finished = !more && tbits == 0u;
+            }
+        }
+        if (finished) {
             active = false;
             if (kShadow) {
                 if (h.tri != kMiss) {  // occluded: contribution * 0 (keeps NaN/Inf like the reference)
@@ -1003,34 +1056,49 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
     hipLaunchKernelGGL(k_raygen, dim3(g), dim3(kBlock), 0, stream, A);
     mark();
     const int L = fp.set.MaxPathLength < 2 ? 2 : fp.set.MaxPathLength;
+    const uint32_t tb = fp.trace_block;
+    const uint32_t gt = (fp.num_paths + tb - 1u) / tb;
+    const uint32_t gst = std::min<uint32_t>((fp.num_paths * fb.shadow_slots + tb - 1u) / tb, kShadowGrid * (kBlock / tb));
+    const size_t ldst = size_t(scene.stack_ints) * tb * sizeof(int);
+    const bool w8 = scene.width == 8;
+    const bool pers = w8 && fp.chunks_per_wave > 0;
+    const uint32_t gp = pers ? pool_grid(fp.num_paths, fp.chunks_per_wave) : 0u;
+    const uint32_t gps = pers ? pool_grid(fp.num_paths * fb.shadow_slots, fp.chunks_per_wave) : 0u;
+    // one-thread-per-ray traversal kernels: <count, width, occupancy>
+    auto trace = [&](int d) {
+#define DXRPT_LAUNCH(K, C, W, O, G) hipLaunchKernelGGL((K<C, W, O>), dim3(G), dim3(tb), ldst, stream, A, d)
+        const bool shadow = d < 0;
+        d = shadow ? -d : d;
+        const uint32_t G = shadow ? gst : gt;
+        if (!w8) {
+            if (shadow) { if (count) DXRPT_LAUNCH(k_shadow, true, 2, 0, G); else DXRPT_LAUNCH(k_shadow, false, 2, 0, G); }
+            else { if (count) DXRPT_LAUNCH(k_trace, true, 2, 0, G); else DXRPT_LAUNCH(k_trace, false, 2, 0, G); }
+        } else if (count) {
+            if (shadow) DXRPT_LAUNCH(k_shadow, true, 8, 0, G); else DXRPT_LAUNCH(k_trace, true, 8, 0, G);
+        } else if (fp.occupancy == 7) {
+            if (shadow) DXRPT_LAUNCH(k_shadow, false, 8, 7, G); else DXRPT_LAUNCH(k_trace, false, 8, 7, G);
+        } else if (fp.occupancy == 8) {
+            if (shadow) DXRPT_LAUNCH(k_shadow, false, 8, 8, G); else DXRPT_LAUNCH(k_trace, false, 8, 8, G);
+        } else {
+            if (shadow) DXRPT_LAUNCH(k_shadow, false, 8, 0, G); else DXRPT_LAUNCH(k_trace, false, 8, 0, G);
+        }
+#undef DXRPT_LAUNCH
+    };
     for (int d = 1; d <= L - 1; ++d) {
-        const bool w8 = scene.width == 8;
-        const bool pers = w8 && fp.chunks_per_wave > 0;
-        const uint32_t gp = pers ? pool_grid(fp.num_paths, fp.chunks_per_wave) : 0u;
-        const uint32_t gps = pers ? pool_grid(fp.num_paths * fb.shadow_slots, fp.chunks_per_wave) : 0u;
-        if (w8 && !pers) {
-            if (count) hipLaunchKernelGGL((k_trace<true, 8>), dim3(g), dim3(kBlock), lds, stream, A, d);
-            else hipLaunchKernelGGL((k_trace<false, 8>), dim3(g), dim3(kBlock), lds, stream, A, d);
-        } else if (pers) {
+        if (pers) {
             if (count) hipLaunchKernelGGL((k_traverse8p<true, false>), dim3(gp), dim3(kBlock), lds, stream, A, d);
             else hipLaunchKernelGGL((k_traverse8p<false, false>), dim3(gp), dim3(kBlock), lds, stream, A, d);
         } else {
-            if (count) hipLaunchKernelGGL((k_trace<true, 2>), dim3(g), dim3(kBlock), lds, stream, A, d);
-            else hipLaunchKernelGGL((k_trace<false, 2>), dim3(g), dim3(kBlock), lds, stream, A, d);
+            trace(d);
         }
         mark();
         hipLaunchKernelGGL(k_shade, dim3(g), dim3(kBlock), 0, stream, A, d);
         mark();
-        const uint32_t gs = std::min<uint32_t>(grid_for(fp.num_paths * fb.shadow_slots), kShadowGrid);
-        if (w8 && !pers) {
-            if (count) hipLaunchKernelGGL((k_shadow<true, 8>), dim3(gs), dim3(kBlock), lds, stream, A, d);
-            else hipLaunchKernelGGL((k_shadow<false, 8>), dim3(gs), dim3(kBlock), lds, stream, A, d);
-        } else if (pers) {
+        if (pers) {
             if (count) hipLaunchKernelGGL((k_traverse8p<true, true>), dim3(gps), dim3(kBlock), lds, stream, A, d);
             else hipLaunchKernelGGL((k_traverse8p<false, true>), dim3(gps), dim3(kBlock), lds, stream, A, d);
         } else {
-            if (count) hipLaunchKernelGGL((k_shadow<true, 2>), dim3(gs), dim3(kBlock), lds, stream, A, d);
-            else hipLaunchKernelGGL((k_shadow<false, 2>), dim3(gs), dim3(kBlock), lds, stream, A, d);
+            trace(-d);
         }
         mark();
         hipLaunchKernelGGL(k_resolve, dim3(g), dim3(kBlock), 0, stream, A, d);

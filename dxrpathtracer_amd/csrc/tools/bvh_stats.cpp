@@ -6,7 +6,8 @@
 // primary hits.  Prints node visits and triangle tests per ray, the quantities the traversal kernels'
 // VALU cost scales with, so builder changes can be compared on CPU before spending GPU time.
 //
-//   make tools && ./build/bvh_stats [scene_id=0] [grid_w=320] [grid_h=180]
+//   make tools && ./build/bvh_stats [scene_id=0] [grid_w=320] [grid_h=180] [binary_depth_cap]
+// (grid_w and grid_h multiples of 8)
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -39,6 +40,7 @@ V3 norm(V3 a) {
 struct Counters {
     uint64_t rays = 0, nodes = 0, tris = 0, hits = 0;
     uint64_t stack_hist[40] = {};  // rays by maximum stack occupancy
+    std::vector<std::vector<uint8_t>> seqs;  // per ray: triangles tested at each node visit, in order
 };
 
 struct Scene {
@@ -77,6 +79,8 @@ float trace8(const Scene& S, const BvhBuildResult& B, V3 o, V3 d, float tmin, fl
     uint32_t node = 0;
     size_t max_sp = 0;
     c.rays++;
+    c.seqs.emplace_back();
+    std::vector<uint8_t>& seq = c.seqs.back();
     struct Hist {
         Counters& c;
         size_t& m;
@@ -109,6 +113,7 @@ float trace8(const Scene& S, const BvhBuildResult& B, V3 o, V3 d, float tmin, fl
             if (m & kMetaInternal) ihits |= 1u << ((m & 7u) ^ oct);
             else thits |= ((1u << (m >> 5)) - 1u) << (m & 31u);
         }
+        seq.push_back(uint8_t(__builtin_popcount(thits)));
         while (thits) {
             uint32_t bit = __builtin_ctz(thits);
             thits &= thits - 1;
@@ -155,6 +160,108 @@ uint64_t splitmix(uint64_t& s) {
     return z ^ (z >> 31);
 }
 float rnd(uint64_t& s) { return float(splitmix(s) >> 40) * (1.0f / 16777216.0f); }
+
+// SIMT replay of the recorded traversals: waves of 64 lanes over consecutive rays (the device queue
+// order), one node visit per lane per iteration.  Policies:
+//   inline   : a lane tests the triangles of the node it just visited in the same iteration (today)
+//   postpone : triangles wait until >= T lanes have some (or no lane can visit a node), then all
+//              those lanes test theirs together (Ylitie et al. 2017, sec. 4)
+//   pool K/R : a wave owns K * 64 rays and refills idle lanes once >= R are idle
+// Cost units: C_node per node iteration, C_tri per triangle-loop trip, C_refill per refill.
+struct Policy {
+    const char* name;
+    int postpone_T;  // 0 = inline
+    int pool_chunks;
+    int refill;
+};
+double simulate(const std::vector<std::vector<uint8_t>>& seqs, const Policy& P) {
+    const double Cn = 250.0, Ct = 90.0, Cr = 150.0;
+    double cost = 0.0;
+    const size_t pool = size_t(64) * P.pool_chunks;
+    for (size_t base = 0; base < seqs.size(); base += pool) {
+        const size_t end = std::min(seqs.size(), base + pool);
+        size_t next = base;
+        const std::vector<uint8_t>* seq[64] = {};
+        size_t j[64] = {};
+        int pend[64] = {};
+        bool active[64] = {};
+        for (;;) {
+            int idle = 0;
+            for (int l = 0; l < 64; ++l) idle += !active[l];
+            if (next < end && (idle >= P.refill || idle == 64)) {
+                for (int l = 0; l < 64 && next < end; ++l)
+                    if (!active[l]) {
+                        seq[l] = &seqs[next++];
+                        j[l] = 0;
+                        pend[l] = 0;
+                        active[l] = !seq[l]->empty();
+                    }
+                cost += Cr;
+            }
+            int nact = 0;
+            for (int l = 0; l < 64; ++l) nact += active[l];
+            if (!nact) {
+                if (next >= end) break;
+                continue;
+            }
+            if (P.postpone_T == 0) {
+                int mk = 0;
+                for (int l = 0; l < 64; ++l)
+                    if (active[l]) {
+                        mk = std::max(mk, int((*seq[l])[j[l]]));
+                        if (++j[l] == seq[l]->size()) active[l] = false;
+                    }
+                cost += Cn + Ct * mk;
+            } else {
+                int ntri = 0, nnode = 0, mk = 0;
+                for (int l = 0; l < 64; ++l) {
+                    if (!active[l]) continue;
+                    if (pend[l]) { ntri++; mk = std::max(mk, pend[l]); }
+                    else nnode++;
+                }
+                if (ntri >= P.postpone_T || nnode == 0) {
+                    cost += Ct * mk;
+                    for (int l = 0; l < 64; ++l)
+                        if (active[l] && pend[l]) {
+                            pend[l] = 0;
+                            if (j[l] == seq[l]->size()) active[l] = false;
+                        }
+                } else {
+                    cost += Cn;
+                    for (int l = 0; l < 64; ++l)
+                        if (active[l] && !pend[l]) {
+                            pend[l] = (*seq[l])[j[l]];
+                            if (++j[l] == seq[l]->size() && !pend[l]) active[l] = false;
+                        }
+                }
+            }
+        }
+    }
+    return cost;
+}
+
+void simulate_all(const char* name, const Counters& c) {
+    static const Policy kPolicies[] = {
+        {"inline", 0, 1, 64},      {"postpone8", 8, 1, 64},    {"postpone16", 16, 1, 64},
+        {"postpone32", 32, 1, 64}, {"pool2r16", 0, 2, 16},     {"pool4r16", 0, 4, 16},
+        {"pool4r32", 0, 4, 32},    {"pool8r16", 0, 8, 16},     {"pool4r16+pp16", 16, 4, 16},
+        {"pool8r16+pp16", 16, 8, 16}, {"pool4r8", 0, 4, 8},
+    };
+    double ideal = 0.0;
+    for (const auto& s : c.seqs) {
+        ideal += 250.0 * s.size();
+        for (uint8_t k : s) ideal += 90.0 * k;
+    }
+    ideal /= 64.0;
+    double base = 0.0;
+    printf("  %-8s SIMT cost / ideal (lower is better):", name);
+    for (const Policy& P : kPolicies) {
+        double v = simulate(c.seqs, P);
+        if (&P == &kPolicies[0]) base = v;
+        printf(" %s %.2f", P.name, v / ideal);
+    }
+    printf("  [inline = %.0f units/ray]\n", base / c.seqs.size());
+}
 
 void report(const char* name, const Counters& c) {
     printf("  %-9s rays %8llu  nodes/ray %6.2f  tris/ray %6.2f  hit %5.1f%%  stack>4 %.3f%% >6 %.4f%% >8 %.5f%% max ",
@@ -226,8 +333,10 @@ int main(int argc, char** argv) {
     V3 sun = norm({hs->sun_direction[0], hs->sun_direction[1], hs->sun_direction[2]});
     Counters prim, bounce, shadow;
     uint64_t rng = 12345;
-    for (uint32_t y = 0; y < gh; ++y)
-        for (uint32_t x = 0; x < gw; ++x) {
+    // rays in the device's order: 8x8 pixel blocks (one wave each), blocks row-major
+    for (uint32_t pix = 0; pix < gw * gh; ++pix) {
+            const uint32_t blk = pix / 64, in = pix % 64, bw = gw / 8;
+            const uint32_t x = (blk % bw) * 8 + in % 8, y = (blk / bw) * 8 + in / 8;
             float ncx = (x + 0.5f) / gw * 2.0f - 1.0f, ncy = -((y + 0.5f) / gh * 2.0f - 1.0f);
             float s[4], e[4];
             for (int j = 0; j < 4; ++j) {
@@ -259,6 +368,9 @@ int main(int argc, char** argv) {
     report("primary", prim);
     report("bounce", bounce);
     report("shadow", shadow);
+    simulate_all("primary", prim);
+    simulate_all("bounce", bounce);
+    simulate_all("shadow", shadow);
     // relative VALU cost model of the BVH8 kernels (~225 ops per node visit, ~80 per triangle test)
     auto cost = [](const Counters& c) { return (225.0 * c.nodes + 80.0 * c.tris) / c.rays; };
     printf("  cost model (VALU ops/ray): primary %.0f bounce %.0f shadow %.0f\n", cost(prim), cost(bounce), cost(shadow));

@@ -264,6 +264,10 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 #define DXRPT_OPT_TRAVERSAL_MODE 4u   /* BVH8: 0 = one thread per ray (default), 1 = wave pools with lane refill */
 #define DXRPT_OPT_REFILL_LANES 5u     /* wave-pool mode: refill a wave once this many lanes are idle */
 #define DXRPT_OPT_CHUNKS_PER_WAVE 6u  /* wave-pool mode: 64-ray chunks owned by each wave (1..64, default 4) */
+#define DXRPT_OPT_POSTPONE_TRIS 7u    /* wave-pool mode: batch triangle tests until this many lanes have some
+                                         (0 = test with the node visit, default) */
+#define DXRPT_OPT_TRACE_BLOCK 8u      /* workgroup size of the one-thread-per-ray traversal kernels: 64 (default), 128, 256 */
+#define DXRPT_OPT_OCCUPANCY 9u        /* BVH8 traversal register budget: 0 = compiler default, 7 or 8 (default) waves/SIMD */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

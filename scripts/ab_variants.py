@@ -3,7 +3,8 @@
 workload (Sponza proxy 1920x1080, L=3).  Prints per-kernel ms per frame from the HIP-event timings.
 
     python scripts/ab_variants.py [--frames 16] [--rounds 3] [--variants w8m0,w8m1r16,...]
-variant syntax: w<2|8> m<0|1> [r<lanes>] [k<chunks per wave>]
+variant syntax: letter+number tokens, e.g. w8m0b64o7 (w width, m mode, r refill lanes, k chunks per
+wave, p postpone lanes, b trace block, o occupancy)
 """
 import argparse
 import os
@@ -15,13 +16,24 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
+KEYS = {"w": "width", "m": "mode", "r": "refill", "k": "chunks", "p": "postpone", "b": "block", "o": "occ"}
+DEFAULTS = {"width": 8, "mode": 0, "refill": 16, "chunks": 4, "postpone": 0, "block": 64, "occ": 8}
+
+
 def parse(v):
-    """w<width>m<mode>[r<refill lanes>][k<chunks per wave>] -> (width, mode, refill, chunks)"""
+    """'w8m1r16k4p16b64o7' -> dict(width, mode, refill, chunks, postpone, block, occ); unspecified keys
+    take DEFAULTS."""
     import re
-    m = re.fullmatch(r"w(\d+)m(\d+)(?:r(\d+))?(?:k(\d+))?", v)
-    if not m:
+    out = dict(DEFAULTS)
+    pos = 0
+    for m in re.finditer(r"([a-z])(\d+)", v):
+        if m.start() != pos or m[1] not in KEYS:
+            raise SystemExit(f"bad variant {v}")
+        out[KEYS[m[1]]] = int(m[2])
+        pos = m.end()
+    if pos != len(v):
         raise SystemExit(f"bad variant {v}")
-    return int(m[1]), int(m[2]), int(m[3] or 16), int(m[4] or 4)
+    return out
 
 
 def main():
@@ -44,7 +56,7 @@ def main():
     st = sc.settings(MaxPathLength=args.L)
     sky = D.make_sky(st)
     tracers = {}
-    for width in sorted({parse(v)[0] for v in args.variants.split(",")}):
+    for width in sorted({parse(v)["width"] for v in args.variants.split(",")}):
         t = DXRPathTracer(0)
         t.set_option(A.OPT_BVH_WIDTH, width)
         t.initialize_scene(sc, sky)
@@ -57,11 +69,14 @@ def main():
     res = {v: [] for v in args.variants.split(",")}
     for rnd in range(args.rounds):
         for v in res:
-            w, m, r, k = parse(v)
-            t = tracers[w]
-            t.set_option(A.OPT_TRAVERSAL_MODE, m)
-            t.set_option(A.OPT_REFILL_LANES, r)
-            t.set_option(A.OPT_CHUNKS_PER_WAVE, k)
+            o = parse(v)
+            t = tracers[o["width"]]
+            t.set_option(A.OPT_POSTPONE_TRIS, o["postpone"])
+            t.set_option(A.OPT_TRAVERSAL_MODE, o["mode"])
+            t.set_option(A.OPT_REFILL_LANES, o["refill"])
+            t.set_option(A.OPT_CHUNKS_PER_WAVE, o["chunks"])
+            t.set_option(A.OPT_TRACE_BLOCK, o["block"])
+            t.set_option(A.OPT_OCCUPANCY, o["occ"])
             for f in range(3):
                 t.render_raw(consts[f], st, accum.data_ptr(), W, H, stream=sh, lights=lights)
             torch.cuda.synchronize()

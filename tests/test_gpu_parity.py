@@ -191,10 +191,11 @@ def test_deterministic_run_to_run(torch_cuda):
     np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("chunks,refill", [(1, 64), (4, 16), (8, 32)])
-def test_wave_pool_traversal_is_bit_identical(torch_cuda, chunks, refill):
-    # DXRPT_OPT_TRAVERSAL_MODE 1 (wave pools with lane refill) only changes which lane traces which
-    # ray: frames must equal the one-thread-per-ray kernels bit for bit (SunTemple: alpha any-hit too)
+@pytest.mark.parametrize("chunks,refill,postpone", [(1, 64, 0), (4, 16, 0), (8, 32, 0), (4, 16, 16), (8, 16, 8)])
+def test_wave_pool_traversal_is_bit_identical(torch_cuda, chunks, refill, postpone):
+    # DXRPT_OPT_TRAVERSAL_MODE 1 (wave pools with lane refill, optional triangle postponement) only
+    # changes which lane traces which ray when: frames must equal the one-thread-per-ray kernels bit
+    # for bit (SunTemple: alpha-tested any-hit too)
     torch = torch_cuda
     for name in ("sponza", "suntemple"):
         sc, _ = scene_bundle(name)
@@ -204,11 +205,30 @@ def test_wave_pool_traversal_is_bit_identical(torch_cuda, chunks, refill):
         t.set_option(A.OPT_TRAVERSAL_MODE, 1)
         t.set_option(A.OPT_CHUNKS_PER_WAVE, chunks)
         t.set_option(A.OPT_REFILL_LANES, refill)
+        t.set_option(A.OPT_POSTPONE_TRIS, postpone)
         try:
             got = gpu_render(torch, name, 480, 270, st, 2).cpu().numpy()
         finally:
             t.set_option(A.OPT_TRAVERSAL_MODE, 0)
         np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("block,occ", [(256, 0), (128, 7), (256, 8), (64, 0)])
+def test_traversal_launch_options_are_bit_identical(torch_cuda, block, occ):
+    # DXRPT_OPT_TRACE_BLOCK / DXRPT_OPT_OCCUPANCY change the launch shape and register budget only
+    torch = torch_cuda
+    sc, _ = scene_bundle("suntemple")
+    st = sc.settings(MaxPathLength=3)
+    t = tracer("suntemple")
+    ref = gpu_render(torch, "suntemple", 480, 270, st, 5).cpu().numpy()
+    t.set_option(A.OPT_TRACE_BLOCK, block)
+    t.set_option(A.OPT_OCCUPANCY, occ)
+    try:
+        got = gpu_render(torch, "suntemple", 480, 270, st, 5).cpu().numpy()
+    finally:
+        t.set_option(A.OPT_TRACE_BLOCK, 64)
+        t.set_option(A.OPT_OCCUPANCY, 8)
+    np.testing.assert_array_equal(got, ref)
 
 
 def _random_rays(rng, n, lo, hi):
