@@ -37,21 +37,41 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(scene, sky, settings, threads):
     """The CPU oracle (scalar C++ restatement, own BVH) on a bounded sample: one full 1920x1080 L=3
-    frame at CurrSampleIdx 0, on `threads` host threads."""
+    frame at CurrSampleIdx 0 on `threads` host threads, plus a single-thread figure on a 1920x68 band
+    of the same frame."""
     import dxrpathtracer_amd as D
     from oracle import pyoracle as O
     orc = O.OracleScene(scene, sky)
     rtc = D.make_constants(scene, settings, sky, WIDTH, HEIGHT, 0)
+    lights = D.make_lights(scene)
     t0 = time.perf_counter()
-    _, st = orc.render(rtc, settings, D.make_lights(scene), WIDTH, HEIGHT, threads=threads)
+    _, st = orc.render(rtc, settings, lights, WIDTH, HEIGHT, threads=threads)
     dt = time.perf_counter() - t0
-    nominal = WIDTH * HEIGHT * (1 + 2 * (PATH_LENGTH - 1))
+    band = (0, HEIGHT // 2 - 34, WIDTH, 68)
+    t1 = time.perf_counter()
+    orc.render(rtc, settings, lights, WIDTH, HEIGHT, crop=band, threads=1)
+    dt1 = time.perf_counter() - t1
+    per_px = 1 + 2 * (PATH_LENGTH - 1)
+    nominal = WIDTH * HEIGHT * per_px
     return {"value": round(nominal / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"one full {WIDTH}x{HEIGHT} L={PATH_LENGTH} frame (sample 0) of the same scene, "
                       f"{dt:.2f} s wall, {st.radiance_rays + st.shadow_rays} rays traced, oracle BVH",
-            "frame_s": round(dt, 3)}
+            "frame_s": round(dt, 3),
+            "single_thread_Mrays_s": round(band[2] * band[3] * per_px / dt1 / 1e6, 3),
+            "single_thread_sample": f"{band[2]}x{band[3]} band at rows {band[1]}..{band[1] + band[3] - 1}, {dt1:.2f} s",
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count()}
 
 
 def pmc_traffic():
@@ -64,8 +84,8 @@ def pmc_traffic():
         except Exception:
             continue
         if d.get("config") == f"sponza-proxy {WIDTH}x{HEIGHT} L={PATH_LENGTH}":
-            return d.get("hbm_bytes_per_launch"), os.path.basename(p)
-    return None, None
+            return d, os.path.basename(p)
+    return {}, None
 
 
 def main():
@@ -138,8 +158,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     for f in range(args.steps):
+        ev[f][0].record(stream)
         frame(args.warmup + f)
+        ev[f][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -151,6 +174,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    frame_ms = np.array([a.elapsed_time(b) for a, b in ev])  # per frame on the render stream
     nominal_per_frame = WIDTH * HEIGHT * (1 + 2 * (PATH_LENGTH - 1))
     ms_per_step = elapsed / args.steps * 1e3
     value = nominal_per_frame * args.steps / elapsed / 1e6
@@ -164,7 +188,8 @@ def main():
     trace_launches_per_frame = PATH_LENGTH - 1
     trace_ms_avg = stats.kernel_ms[A.K_TRACE] / max(1, stats.kernel_launches[A.K_TRACE])
     achieved = (trace_bytes_frame / trace_launches_per_frame) / (trace_ms_avg * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic()
+    pmc, traffic_src = pmc_traffic()
+    traffic = pmc.get("hbm_bytes_per_launch")
 
     result = None
     if rank == 0:
@@ -193,7 +218,8 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "bytes_per_launch": int(trace_bytes_frame / trace_launches_per_frame),
-                         "avg_launch_ms": round(trace_ms_avg, 4), "traffic_source": traffic_src},
+                         "avg_launch_ms": round(trace_ms_avg, 4), "traffic_source": traffic_src,
+                         "traffic_kernel": pmc.get("kernel"), "l2_hit_rate": pmc.get("l2_hit_rate")},
             "cpu_baseline": cpu,
             "detail": {
                 "counted_rays_per_frame": int(stats.radiance_rays + stats.shadow_rays),
@@ -202,6 +228,8 @@ def main():
                 "kernel_ms_per_frame": {k: round(v / frames, 4) for k, v in kms.items()},
                 "dominant_kernel": dominant,
                 "gpu_frame_ms_events": round(stats.frame_ms / frames, 4),
+                "frame_ms": {"mean": round(float(frame_ms.mean()), 4), "median": round(float(np.median(frame_ms)), 4),
+                             "max": round(float(frame_ms.max()), 4)},
                 "nodes_per_radiance_ray": round(census.node_visits_radiance / max(1, rays), 2),
                 "tris_per_radiance_ray": round(census.tri_tests_radiance / max(1, rays), 2),
                 "nodes_per_shadow_ray": round(census.node_visits_shadow / max(1, census.shadow_rays), 2),

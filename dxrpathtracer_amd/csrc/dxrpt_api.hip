@@ -96,6 +96,8 @@ struct dxrpt_ctx {
     uint32_t opt_postpone = 0;      // DXRPT_OPT_POSTPONE_TRIS
     uint32_t opt_trace_block = 64;  // DXRPT_OPT_TRACE_BLOCK
     uint32_t opt_occupancy = 8;     // DXRPT_OPT_OCCUPANCY
+    uint32_t opt_shade_block = 256; // DXRPT_OPT_SHADE_BLOCK
+    uint32_t opt_shade_occ = 0;     // DXRPT_OPT_SHADE_OCCUPANCY
     int built_width = 0;
     DevBuf d_trav;   // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
     DevBuf d_spill;  // BVH8 traversal stack entries beyond the LDS part (deep trees only)
@@ -376,6 +378,12 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_OCCUPANCY) {
             require(value == 0 || value == 7 || value == 8, "dxrpt_set_option: occupancy must be 0, 7 or 8");
             ctx->opt_occupancy = uint32_t(value);
+        } else if (option == DXRPT_OPT_SHADE_BLOCK) {
+            require(value == 64 || value == 128 || value == 256, "dxrpt_set_option: shade block must be 64, 128 or 256");
+            ctx->opt_shade_block = uint32_t(value);
+        } else if (option == DXRPT_OPT_SHADE_OCCUPANCY) {
+            require(value == 0 || (value >= 6 && value <= 8), "dxrpt_set_option: shade occupancy must be 0, 6, 7 or 8");
+            ctx->opt_shade_occ = uint32_t(value);
         } else if (option == DXRPT_OPT_POSTPONE_TRIS) {
             require(value <= 64, "dxrpt_set_option: postpone threshold must be 0..64 lanes");
             ctx->opt_postpone = uint32_t(value);
@@ -627,6 +635,8 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.postpone_tris = ctx->opt_postpone;
         fp.trace_block = ctx->opt_trace_block;
         fp.occupancy = ctx->opt_occupancy;
+        fp.shade_block = ctx->opt_shade_block;
+        fp.shade_occupancy = ctx->opt_shade_occ;
         hipStream_t s = static_cast<hipStream_t>(stream);
         if (ctx->opt_count) {
             fp.trav = ctx->d_trav.as<unsigned long long>();

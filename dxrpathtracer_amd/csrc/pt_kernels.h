@@ -109,6 +109,8 @@ struct FrameParams {
     uint32_t refill_lanes;           // wave-pool kernels: refill once this many lanes of a wave are idle
     uint32_t trace_block;            // workgroup size of the one-thread-per-ray traversal kernels (64..256)
     uint32_t occupancy;              // BVH8 traversal kernels: 0 compiler default, 7 or 8 waves per SIMD
+    uint32_t shade_block;            // workgroup size of k_shade (64..256)
+    uint32_t shade_occupancy;        // k_shade register budget: 0 compiler default, 6, 7 or 8 waves per SIMD
     uint32_t postpone_tris;          // wave-pool kernels: test pending triangles once this many lanes hold
                                      // some (0 = with their node visit)
 };

@@ -504,7 +504,7 @@ PT_DEV uint32_t queue_append(uint32_t* counters, uint32_t cap, bool want) {
     const unsigned long long m = __ballot(want);
     const int lane = __lane_id();
     const int leader = __ffsll(static_cast<long long>(__ballot(1))) - 1;
-    const uint32_t shard = ((blockIdx.x * kBlock + threadIdx.x) >> 6) % kQueueShards;
+    const uint32_t shard = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) % kQueueShards;
     uint32_t base = 0;
     if (lane == leader && m != 0ull) base = atomicAdd(&counters[shard], uint32_t(__popcll(m)));
     base = __shfl(base, leader);
@@ -620,9 +620,12 @@ PT_DEV void emit_shadow(const KArgs& A, uint32_t pos, uint32_t& n, f3 o, f3 d, f
 
 PT_DEV bool nonzero3(f3 c) { return !(c.x == 0.0f && c.y == 0.0f && c.z == 0.0f); }
 
-// MissShader (RayTrace.hlsl:509-530) and ClosestHitShader -> PathTrace (151-441)
-__global__ __launch_bounds__(kBlock) void k_shade(KArgs A, int depth) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+// MissShader (RayTrace.hlsl:509-530) and ClosestHitShader -> PathTrace (151-441).
+// kOcc > 0: register budget for kOcc waves per SIMD; workgroups of FrameParams::shade_block threads.
+template <int kOcc>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
+void k_shade(KArgs A, int depth) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t* cnt = radiance_counts(A.F, depth);
     if (i >= queue_total(cnt)) return;
     const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
@@ -1092,7 +1095,15 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
             trace(d);
         }
         mark();
-        hipLaunchKernelGGL(k_shade, dim3(g), dim3(kBlock), 0, stream, A, d);
+        {
+            const uint32_t sb = fp.shade_block, gsh = (fp.num_paths + sb - 1u) / sb;
+            switch (fp.shade_occupancy) {
+                case 6: hipLaunchKernelGGL((k_shade<6>), dim3(gsh), dim3(sb), 0, stream, A, d); break;
+                case 7: hipLaunchKernelGGL((k_shade<7>), dim3(gsh), dim3(sb), 0, stream, A, d); break;
+                case 8: hipLaunchKernelGGL((k_shade<8>), dim3(gsh), dim3(sb), 0, stream, A, d); break;
+                default: hipLaunchKernelGGL((k_shade<0>), dim3(gsh), dim3(sb), 0, stream, A, d); break;
+            }
+        }
         mark();
         if (pers) {
             if (count) hipLaunchKernelGGL((k_traverse8p<true, true>), dim3(gps), dim3(kBlock), lds, stream, A, d);

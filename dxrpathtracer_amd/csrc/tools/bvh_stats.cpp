@@ -38,6 +38,7 @@ V3 norm(V3 a) {
 }
 
 struct Counters {
+    std::vector<uint64_t> keys;  // optional per-ray sort keys (bounce rays)
     uint64_t rays = 0, nodes = 0, tris = 0, hits = 0;
     uint64_t stack_hist[40] = {};  // rays by maximum stack occupancy
     std::vector<std::vector<uint8_t>> seqs;  // per ray: triangles tested at each node visit, in order
@@ -331,6 +332,11 @@ int main(int argc, char** argv) {
     dxrpt_host_inv_view_projection(hs->camera_position, hs->camera_rotation[0], hs->camera_rotation[1], 3.14159265f / 4.0f,
                                    16.0f / 9.0f, 0.1f, 100.0f, M);
     V3 sun = norm({hs->sun_direction[0], hs->sun_direction[1], hs->sun_direction[2]});
+    float scene_lo[3] = {3.4e38f, 3.4e38f, 3.4e38f}, scene_hi[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+    for (size_t i = 0; i < S.pos.size(); ++i) {
+        scene_lo[i % 3] = std::min(scene_lo[i % 3], S.pos[i]);
+        scene_hi[i % 3] = std::max(scene_hi[i % 3], S.pos[i]);
+    }
     Counters prim, bounce, shadow;
     uint64_t rng = 12345;
     // rays in the device's order: 8x8 pixel blocks (one wave each), blocks row-major
@@ -364,12 +370,50 @@ int main(int argc, char** argv) {
             float lx = r * cosf(phi), ly = r * sinf(phi), lz = sqrtf(std::max(0.0f, 1.0f - r1));
             V3 bd = norm({tt.x * lx + bb.x * ly + nrm.x * lz, tt.y * lx + bb.y * ly + nrm.y * lz, tt.z * lx + bb.z * ly + nrm.z * lz});
             trace8(S, B, p, bd, 1e-4f, 3.4e38f, false, bounce, nullptr);
+            {   // sort key: direction octant (3 bits) | 30-bit Morton code of the origin in the scene box
+                auto q = [](float v, float lo, float hi) {
+                    float t = (v - lo) / (hi - lo);
+                    return uint32_t(std::min(std::max(t, 0.0f), 0.999999f) * 1024.0f);
+                };
+                auto spread = [](uint64_t v) {
+                    uint64_t r = 0;
+                    for (int b = 0; b < 10; ++b) r |= ((v >> b) & 1ull) << (3 * b);
+                    return r;
+                };
+                const float* lo = scene_lo;
+                const float* hi = scene_hi;
+                uint64_t m = spread(q(p.x, lo[0], hi[0])) | (spread(q(p.y, lo[1], hi[1])) << 1) | (spread(q(p.z, lo[2], hi[2])) << 2);
+                uint64_t oct = (bd.x < 0 ? 4u : 0u) | (bd.y < 0 ? 2u : 0u) | (bd.z < 0 ? 1u : 0u);
+                // finer direction bin: 4x4 cells on the octant's face of the direction cube
+                float ax = fabsf(bd.x), ay = fabsf(bd.y), az = fabsf(bd.z);
+                uint32_t face = ax >= ay && ax >= az ? 0 : (ay >= az ? 1 : 2);
+                float u = face == 0 ? ay / ax : ax / (face == 1 ? ay : az), v = face == 2 ? ay / az : az / (face == 0 ? ax : ay);
+                uint64_t dbin = (face << 4) | (uint32_t(std::min(u, 0.999f) * 4) << 2) | uint32_t(std::min(v, 0.999f) * 4);
+                bounce.keys.push_back((oct << 60) | (dbin << 52) | (uint64_t(bounce.keys.size()) << 0) | (m << 22) * 0);
+                bounce.keys.back() = (oct << 61) | (dbin << 55) | (m << 25);
+            }
         }
     report("primary", prim);
     report("bounce", bounce);
     report("shadow", shadow);
     simulate_all("primary", prim);
     simulate_all("bounce", bounce);
+    {   // the same bounce rays re-ordered by sort keys
+        auto reorder = [&](const char* nm, auto keyfn) {
+            std::vector<size_t> idx(bounce.seqs.size());
+            for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+            std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return keyfn(a) < keyfn(b); });
+            Counters c2;
+            c2.rays = bounce.rays;
+            for (size_t i : idx) c2.seqs.push_back(bounce.seqs[i]);
+            simulate_all(nm, c2);
+        };
+        reorder("b:oct", [&](size_t i) { return bounce.keys[i] >> 61; });
+        reorder("b:oct+dir", [&](size_t i) { return bounce.keys[i] >> 55; });
+        reorder("b:oct+org", [&](size_t i) { return (bounce.keys[i] >> 61 << 40) | ((bounce.keys[i] >> 25) & ((1ull << 30) - 1)); });
+        reorder("b:o+d+org", [&](size_t i) { return bounce.keys[i]; });
+        reorder("b:org", [&](size_t i) { return (bounce.keys[i] >> 25) & ((1ull << 30) - 1); });
+    }
     simulate_all("shadow", shadow);
     // relative VALU cost model of the BVH8 kernels (~225 ops per node visit, ~80 per triangle test)
     auto cost = [](const Counters& c) { return (225.0 * c.nodes + 80.0 * c.tris) / c.rays; };

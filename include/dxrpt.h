@@ -268,6 +268,8 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                          (0 = test with the node visit, default) */
 #define DXRPT_OPT_TRACE_BLOCK 8u      /* workgroup size of the one-thread-per-ray traversal kernels: 64 (default), 128, 256 */
 #define DXRPT_OPT_OCCUPANCY 9u        /* BVH8 traversal register budget: 0 = compiler default, 7 or 8 (default) waves/SIMD */
+#define DXRPT_OPT_SHADE_BLOCK 10u     /* workgroup size of the shading kernel: 64, 128, 256 (default) */
+#define DXRPT_OPT_SHADE_OCCUPANCY 11u /* shading kernel register budget: 0 = compiler default, 6, 7 or 8 waves/SIMD */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

@@ -16,8 +16,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
-KEYS = {"w": "width", "m": "mode", "r": "refill", "k": "chunks", "p": "postpone", "b": "block", "o": "occ"}
-DEFAULTS = {"width": 8, "mode": 0, "refill": 16, "chunks": 4, "postpone": 0, "block": 64, "occ": 8}
+KEYS = {"w": "width", "m": "mode", "r": "refill", "k": "chunks", "p": "postpone", "b": "block", "o": "occ",
+        "s": "sblock", "q": "socc"}
+DEFAULTS = {"width": 8, "mode": 0, "refill": 16, "chunks": 4, "postpone": 0, "block": 64, "occ": 8, "sblock": 256,
+            "socc": 0}
 
 
 def parse(v):
@@ -77,6 +79,8 @@ def main():
             t.set_option(A.OPT_CHUNKS_PER_WAVE, o["chunks"])
             t.set_option(A.OPT_TRACE_BLOCK, o["block"])
             t.set_option(A.OPT_OCCUPANCY, o["occ"])
+            t.set_option(A.OPT_SHADE_BLOCK, o["sblock"])
+            t.set_option(A.OPT_SHADE_OCCUPANCY, o["socc"])
             for f in range(3):
                 t.render_raw(consts[f], st, accum.data_ptr(), W, H, stream=sh, lights=lights)
             torch.cuda.synchronize()

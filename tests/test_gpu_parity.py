@@ -213,9 +213,10 @@ def test_wave_pool_traversal_is_bit_identical(torch_cuda, chunks, refill, postpo
         np.testing.assert_array_equal(got, ref)
 
 
-@pytest.mark.parametrize("block,occ", [(256, 0), (128, 7), (256, 8), (64, 0)])
-def test_traversal_launch_options_are_bit_identical(torch_cuda, block, occ):
-    # DXRPT_OPT_TRACE_BLOCK / DXRPT_OPT_OCCUPANCY change the launch shape and register budget only
+@pytest.mark.parametrize("block,occ,sblock,socc", [(256, 0, 64, 6), (128, 7, 128, 7), (256, 8, 256, 8), (64, 0, 64, 0)])
+def test_traversal_launch_options_are_bit_identical(torch_cuda, block, occ, sblock, socc):
+    # DXRPT_OPT_TRACE_BLOCK / _OCCUPANCY / _SHADE_BLOCK / _SHADE_OCCUPANCY change the launch shape and
+    # register budget only
     torch = torch_cuda
     sc, _ = scene_bundle("suntemple")
     st = sc.settings(MaxPathLength=3)
@@ -223,11 +224,15 @@ def test_traversal_launch_options_are_bit_identical(torch_cuda, block, occ):
     ref = gpu_render(torch, "suntemple", 480, 270, st, 5).cpu().numpy()
     t.set_option(A.OPT_TRACE_BLOCK, block)
     t.set_option(A.OPT_OCCUPANCY, occ)
+    t.set_option(A.OPT_SHADE_BLOCK, sblock)
+    t.set_option(A.OPT_SHADE_OCCUPANCY, socc)
     try:
         got = gpu_render(torch, "suntemple", 480, 270, st, 5).cpu().numpy()
     finally:
         t.set_option(A.OPT_TRACE_BLOCK, 64)
         t.set_option(A.OPT_OCCUPANCY, 8)
+        t.set_option(A.OPT_SHADE_BLOCK, 256)
+        t.set_option(A.OPT_SHADE_OCCUPANCY, 0)
     np.testing.assert_array_equal(got, ref)
 
 
