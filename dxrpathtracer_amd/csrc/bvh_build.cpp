@@ -191,6 +191,311 @@ struct Builder {
     }
 };
 
+// Spatial-split binary builder (SBVH, Stich et al. 2009) for the BVH8 path: at nodes whose best
+// object split leaves overlapping children, it also bins the node box into slabs, clips each
+// triangle reference to the slabs it crosses, and may split along a plane, duplicating straddling
+// references (with clipped boxes) into both children.  Cuts the child-box overlap that long thin
+// architectural triangles cause, hence node visits per ray.  Duplicates are harmless for the
+// traversal: a triangle tested twice yields the same hit (tie rule: smaller t, then smaller id).
+struct SpatialBuilder {
+    struct Ref {
+        uint32_t tri;
+        Box box;
+    };
+    const float* pos = nullptr;  // ntris * 9
+    std::vector<TNode> tree;
+    std::vector<uint32_t> refs;  // leaf order, duplicates allowed
+    uint32_t depth_cap = 32;
+    double root_area = 1.0;
+    double alpha = 1e-5;         // overlap / root area that enables a spatial search
+    size_t ref_budget = 0;       // maximum live references (duplication budget)
+    size_t live_refs = 0;
+    double sah = 0.0;            // binary tree, C_trav = 1, C_tri = 1, relative to the root area
+
+    // Splits `r` at `plane` on `axis` into the parts of its triangle on each side (boxes clipped to r.box).
+    void split_ref(const Ref& r, int axis, float plane, Box& left, Box& right) const {
+        left = Box();
+        right = Box();
+        const float* v = pos + size_t(r.tri) * 9;
+        for (int i = 0; i < 3; ++i) {
+            const float* a = v + 3 * i;
+            const float* b = v + 3 * ((i + 1) % 3);
+            if (a[axis] <= plane) left.grow(a);
+            if (a[axis] >= plane) right.grow(a);
+            if ((a[axis] < plane && b[axis] > plane) || (b[axis] < plane && a[axis] > plane)) {
+                const float t = std::min(std::max((plane - a[axis]) / (b[axis] - a[axis]), 0.0f), 1.0f);
+                float p[3];
+                for (int k = 0; k < 3; ++k) p[k] = a[k] + (b[k] - a[k]) * t;
+                p[axis] = plane;
+                left.grow(p);
+                right.grow(p);
+            }
+        }
+        for (int k = 0; k < 3; ++k) {
+            left.lo[k] = std::max(left.lo[k], r.box.lo[k]);
+            left.hi[k] = std::min(left.hi[k], r.box.hi[k]);
+            right.lo[k] = std::max(right.lo[k], r.box.lo[k]);
+            right.hi[k] = std::min(right.hi[k], r.box.hi[k]);
+        }
+        left.hi[axis] = std::min(left.hi[axis], plane);
+        right.lo[axis] = std::max(right.lo[axis], plane);
+    }
+
+    static Box bounds_of(const std::vector<Ref>& rs) {
+        Box b;
+        for (const Ref& r : rs) b.grow(r.box);
+        return b;
+    }
+
+    struct ObjSplit {
+        double cost = DBL_MAX;
+        int axis = -1, bin = -1;
+        Box left, right;
+        float lo = 0.f, scale = 0.f;
+    };
+
+    ObjSplit object_split(const std::vector<Ref>& rs) const {
+        ObjSplit best;
+        Box cb;
+        for (const Ref& r : rs) {
+            float c[3];
+            for (int k = 0; k < 3; ++k) c[k] = 0.5f * (r.box.lo[k] + r.box.hi[k]);
+            cb.grow(c);
+        }
+        for (int ax = 0; ax < 3; ++ax) {
+            const float ext = cb.hi[ax] - cb.lo[ax];
+            if (!(ext > 0.f)) continue;
+            Box bb[kBins];
+            uint32_t bc[kBins] = {};
+            const float scale = float(kBins) / ext;
+            for (const Ref& r : rs) {
+                int k = int((0.5f * (r.box.lo[ax] + r.box.hi[ax]) - cb.lo[ax]) * scale);
+                k = std::min(std::max(k, 0), kBins - 1);
+                bc[k]++;
+                bb[k].grow(r.box);
+            }
+            Box racc[kBins];
+            uint32_t rcnt[kBins];
+            Box acc;
+            uint32_t cnt = 0;
+            for (int k = kBins - 1; k > 0; --k) {
+                acc.grow(bb[k]);
+                cnt += bc[k];
+                racc[k] = acc;
+                rcnt[k] = cnt;
+            }
+            acc = Box();
+            cnt = 0;
+            for (int k = 0; k < kBins - 1; ++k) {
+                acc.grow(bb[k]);
+                cnt += bc[k];
+                if (cnt == 0 || rcnt[k + 1] == 0) continue;
+                const double c = acc.area() * cnt + racc[k + 1].area() * rcnt[k + 1];
+                if (c < best.cost) {
+                    best.cost = c;
+                    best.axis = ax;
+                    best.bin = k;
+                    best.left = acc;
+                    best.right = racc[k + 1];
+                    best.lo = cb.lo[ax];
+                    best.scale = scale;
+                }
+            }
+        }
+        return best;
+    }
+
+    struct SpatSplit {
+        double cost = DBL_MAX;
+        int axis = -1;
+        float plane = 0.f;
+    };
+
+    SpatSplit spatial_split(const std::vector<Ref>& rs, const Box& nb) const {
+        SpatSplit best;
+        for (int ax = 0; ax < 3; ++ax) {
+            const float lo = nb.lo[ax], ext = nb.hi[ax] - nb.lo[ax];
+            if (!(ext > 0.f)) continue;
+            const float bs = ext / float(kBins);
+            Box bb[kBins];
+            uint32_t enter[kBins] = {}, exit_[kBins] = {};
+            for (const Ref& r : rs) {
+                int b0 = int((r.box.lo[ax] - lo) / bs), b1 = int((r.box.hi[ax] - lo) / bs);
+                b0 = std::min(std::max(b0, 0), kBins - 1);
+                b1 = std::min(std::max(b1, b0), kBins - 1);
+                Ref cur = r;
+                for (int b = b0; b < b1; ++b) {
+                    Box L, R;
+                    split_ref(cur, ax, lo + bs * float(b + 1), L, R);
+                    bb[b].grow(L);
+                    cur.box = R;
+                }
+                bb[b1].grow(cur.box);
+                enter[b0]++;
+                exit_[b1]++;
+            }
+            Box racc[kBins];
+            uint32_t rcnt[kBins];
+            Box acc;
+            uint32_t cnt = 0;
+            for (int k = kBins - 1; k > 0; --k) {
+                acc.grow(bb[k]);
+                cnt += exit_[k];
+                racc[k] = acc;
+                rcnt[k] = cnt;
+            }
+            acc = Box();
+            cnt = 0;
+            for (int k = 0; k < kBins - 1; ++k) {
+                acc.grow(bb[k]);
+                cnt += enter[k];
+                if (cnt == 0 || rcnt[k + 1] == 0) continue;
+                const double c = acc.area() * cnt + racc[k + 1].area() * rcnt[k + 1];
+                if (c < best.cost) {
+                    best.cost = c;
+                    best.axis = ax;
+                    best.plane = lo + bs * float(k + 1);
+                }
+            }
+        }
+        return best;
+    }
+
+    bool build(uint32_t ntris, const std::vector<Box>& tri_box, std::string& err) {
+        struct Task {
+            int32_t node;
+            std::vector<Ref> rs;
+            uint32_t depth;
+        };
+        tree.clear();
+        refs.clear();
+        tree.reserve(size_t(ntris) * 3);
+        tree.emplace_back();
+        std::vector<Ref> all(ntris);
+        for (uint32_t t = 0; t < ntris; ++t) all[t] = Ref{t, tri_box[t]};
+        root_area = std::max(bounds_of(all).area(), 1e-30);
+        live_refs = ntris;
+        std::vector<Task> stack;
+        stack.push_back(Task{0, std::move(all), 0});
+        while (!stack.empty()) {
+            Task t = std::move(stack.back());
+            stack.pop_back();
+            const Box nb = bounds_of(t.rs);
+            tree[t.node].box = nb;
+            const size_t n = t.rs.size();
+            if (n <= 1) {
+                tree[t.node].first = uint32_t(refs.size());
+                tree[t.node].count = uint32_t(n);
+                tree[t.node].begin = uint32_t(refs.size());
+                for (const Ref& r : t.rs) refs.push_back(r.tri);
+                tree[t.node].end = uint32_t(refs.size());
+                continue;
+            }
+            if (t.depth + 1 > depth_cap) {
+                err = "build_bvh: depth cap exceeded";
+                return false;
+            }
+            uint32_t levels = 0;
+            for (size_t m = n; m > 1; m = (m + 1) / 2) ++levels;
+            const bool tight = t.depth + levels + 3 >= depth_cap;
+            std::vector<Ref> L, R;
+            bool done = false;
+            if (!tight) {
+                const ObjSplit os = object_split(t.rs);
+                SpatSplit ss;
+                if (os.axis >= 0) {
+                    Box ov;
+                    for (int k = 0; k < 3; ++k) {
+                        ov.lo[k] = std::max(os.left.lo[k], os.right.lo[k]);
+                        ov.hi[k] = std::min(os.left.hi[k], os.right.hi[k]);
+                    }
+                    bool overlap = true;
+                    for (int k = 0; k < 3; ++k) overlap = overlap && ov.lo[k] <= ov.hi[k];
+                    if (overlap && ov.area() > alpha * root_area && live_refs < ref_budget) ss = spatial_split(t.rs, nb);
+                } else {
+                    ss = spatial_split(t.rs, nb);
+                }
+                if (ss.axis >= 0 && ss.cost < os.cost) {
+                    for (const Ref& r : t.rs) {
+                        if (r.box.hi[ss.axis] <= ss.plane) L.push_back(r);
+                        else if (r.box.lo[ss.axis] >= ss.plane) R.push_back(r);
+                        else {
+                            Box bl, br;
+                            split_ref(r, ss.axis, ss.plane, bl, br);
+                            if (!bl.empty() && !br.empty() && bl.lo[ss.axis] <= bl.hi[ss.axis] && br.lo[ss.axis] <= br.hi[ss.axis]) {
+                                L.push_back(Ref{r.tri, bl});
+                                R.push_back(Ref{r.tri, br});
+                                live_refs++;
+                            } else if (0.5f * (r.box.lo[ss.axis] + r.box.hi[ss.axis]) < ss.plane) {
+                                L.push_back(r);
+                            } else {
+                                R.push_back(r);
+                            }
+                        }
+                    }
+                    done = !L.empty() && !R.empty();
+                    if (!done) {
+                        L.clear();
+                        R.clear();
+                    }
+                }
+                if (!done && os.axis >= 0) {
+                    for (const Ref& r : t.rs) {
+                        int k = int((0.5f * (r.box.lo[os.axis] + r.box.hi[os.axis]) - os.lo) * os.scale);
+                        k = std::min(std::max(k, 0), kBins - 1);
+                        (k <= os.bin ? L : R).push_back(r);
+                    }
+                    done = !L.empty() && !R.empty();
+                    if (!done) {
+                        L.clear();
+                        R.clear();
+                    }
+                }
+            }
+            if (!done) {  // object median along the widest centroid axis
+                Box cb;
+                for (const Ref& r : t.rs) {
+                    float c[3];
+                    for (int k = 0; k < 3; ++k) c[k] = 0.5f * (r.box.lo[k] + r.box.hi[k]);
+                    cb.grow(c);
+                }
+                int ax = 0;
+                for (int k = 1; k < 3; ++k)
+                    if (cb.hi[k] - cb.lo[k] > cb.hi[ax] - cb.lo[ax]) ax = k;
+                const size_t m = n / 2;
+                std::nth_element(t.rs.begin(), t.rs.begin() + m, t.rs.end(), [&](const Ref& x, const Ref& y) {
+                    const float cx = x.box.lo[ax] + x.box.hi[ax], cy = y.box.lo[ax] + y.box.hi[ax];
+                    return cx < cy || (cx == cy && x.tri < y.tri);
+                });
+                L.assign(t.rs.begin(), t.rs.begin() + m);
+                R.assign(t.rs.begin() + m, t.rs.end());
+            }
+            std::vector<Ref>().swap(t.rs);
+            const int32_t c0 = int32_t(tree.size()), c1 = c0 + 1;
+            tree.emplace_back();
+            tree.emplace_back();
+            tree[t.node].child[0] = c0;
+            tree[t.node].child[1] = c1;
+            stack.push_back(Task{c1, std::move(R), t.depth + 1});
+            stack.push_back(Task{c0, std::move(L), t.depth + 1});
+        }
+        // subtree ranges: children follow their parent, and DFS left-first emission keeps each
+        // subtree's references contiguous
+        sah = 0.0;
+        for (size_t i = tree.size(); i-- > 0;) {
+            TNode& nd = tree[i];
+            if (!nd.count) {
+                nd.begin = tree[nd.child[0]].begin;
+                nd.end = tree[nd.child[1]].end;
+                sah += nd.box.area() / root_area;
+            } else {
+                sah += nd.box.area() / root_area * double(nd.count);
+            }
+        }
+        return true;
+    }
+};
+
 // Outward padding so that GPU slab tests with FMA rounding stay conservative.
 Box padded(const Box& bx, float pad_abs) {
     if (bx.empty()) return bx;
@@ -274,8 +579,9 @@ struct Emit8 {
     //                  node: A(n) * C_node + D(n, 8))
     //   D(n, i)  = min_k C(left, k) + C(right, i - k)     (split the slots between the children)
     //   C(n, i)  = min(C(n, i - 1), D(n, i))              (i >= 2)
-    // C_prim / C_node ~ the measured VALU cost of a triangle test vs an 8-child node test.
-    static constexpr double kCNode = 1.0, kCPrim = 0.35;
+    // C_prim / C_node: the traversal is memory-latency bound and each triangle test is a dependent
+    // round trip like a node visit, so a triangle is priced at 1.5 node visits (tuned on the GPU).
+    double kCNode = 1.0, kCPrim = 1.5;  // set from BvhBuildParams::leaf_cost
     std::vector<double> cost;     // [n * 8 + i], i in 1..7 (index 0: D(n, 8) for the node case)
     std::vector<uint8_t> pick;    // [n * 8 + i]: i == 1: 0 leaf / 1 node; i >= 2: 0 = use C(n, i-1), k = split
     std::vector<uint8_t> dsplit;  // k of D(n, 8)
@@ -523,16 +829,30 @@ bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildRe
     if (params && params->binary_depth_cap) caps.push_back(params->binary_depth_cap);
     else caps.assign(std::begin(kCaps), std::end(kCaps));
     uint32_t last_depth = 0;
+    const bool spatial = !params || params->spatial_splits;
     for (uint32_t cap : caps) {
-        for (uint32_t t = 0; t < ntris; ++t) B.refs[t] = t;
-        B.depth_cap = cap;
         double sah = 0.0;
-        if (!B.build(ntris, err, sah)) return false;
-        Emit8 E{B.tree, B.refs, pad, {}, {}, 0, 0, {}, {}, {}};
+        SpatialBuilder SB;
+        const std::vector<TNode>* tree = &B.tree;
+        const std::vector<uint32_t>* refs = &B.refs;
+        if (spatial) {
+            SB.pos = tri_positions;
+            SB.depth_cap = cap;
+            SB.ref_budget = size_t(double(ntris) * (params ? params->ref_budget : BvhBuildParams().ref_budget));
+            if (!SB.build(ntris, B.tri_box, err)) return false;
+            sah = SB.sah;
+            tree = &SB.tree;
+            refs = &SB.refs;
+        } else {
+            for (uint32_t t = 0; t < ntris; ++t) B.refs[t] = t;
+            B.depth_cap = cap;
+            if (!B.build(ntris, err, sah)) return false;
+        }
+        Emit8 E{*tree, *refs, pad, {}, {}, 0, 0, 1.0, params ? params->leaf_cost : BvhBuildParams().leaf_cost, {}, {}, {}};
         E.run();
         last_depth = E.max_depth;
         if (E.max_depth > max_depth8) continue;
-        if (E.tri_order.size() != ntris) {
+        if (E.tri_order.size() != refs->size()) {
             err = "build_bvh: BVH8 emission lost triangles";
             return false;
         }

@@ -15,7 +15,8 @@ namespace dxrpt {
 struct BvhBuildResult {
     std::vector<BvhNode> nodes;       // BVH2: nodes[0] is the root; DFS order
     std::vector<Bvh8Node> nodes8;     // BVH8: nodes8[0] is the root
-    std::vector<uint32_t> tri_order;  // leaf order -> global triangle id
+    std::vector<uint32_t> tri_order;  // leaf order -> global triangle id (BVH8 with spatial splits:
+                                      // a triangle may appear more than once)
     uint32_t max_depth = 0;           // of the emitted layout
     uint32_t num_leaves = 0;
     double sah_cost = 0.0;            // binary tree, C_trav = 1, C_tri = 1, relative to root area
@@ -26,6 +27,10 @@ struct BvhBuildResult {
 struct BvhBuildParams {
     uint32_t binary_depth_cap = 0;  // BVH8: force this binary depth cap (0: tighten until the tree fits)
     uint32_t max_wide_depth = 0;    // BVH8: accepted wide depth (0: kTraversalStack8 - 1)
+    bool spatial_splits = true;     // BVH8: SBVH spatial splits
+    double ref_budget = 1.5;        // BVH8: maximum triangle references / triangles with spatial splits
+    double leaf_cost = 1.5;         // BVH8 collapse: SAH cost of a triangle test relative to a node visit
+                                    // (latency-bound traversal: each test is a dependent memory round trip)
 };
 
 // tri_positions: ntris * 9 floats (v0.xyz, v1.xyz, v2.xyz) in global triangle order.

@@ -98,6 +98,7 @@ struct dxrpt_ctx {
     uint32_t opt_occupancy = 8;     // DXRPT_OPT_OCCUPANCY
     uint32_t opt_shade_block = 256; // DXRPT_OPT_SHADE_BLOCK
     uint32_t opt_shade_occ = 0;     // DXRPT_OPT_SHADE_OCCUPANCY
+    BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
     int built_width = 0;
     DevBuf d_trav;   // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
     DevBuf d_spill;  // BVH8 traversal stack entries beyond the LDS part (deep trees only)
@@ -378,6 +379,13 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_OCCUPANCY) {
             require(value == 0 || value == 7 || value == 8, "dxrpt_set_option: occupancy must be 0, 7 or 8");
             ctx->opt_occupancy = uint32_t(value);
+        } else if (option == DXRPT_OPT_SPATIAL_SPLITS) {
+            require(value <= 400, "dxrpt_set_option: spatial-split budget must be 0..400 (percent of triangles)");
+            ctx->build_params.spatial_splits = value > 100;
+            ctx->build_params.ref_budget = double(value) / 100.0;
+        } else if (option == DXRPT_OPT_LEAF_COST) {
+            require(value >= 5 && value <= 1000, "dxrpt_set_option: leaf cost must be 5..1000 (percent of a node visit)");
+            ctx->build_params.leaf_cost = double(value) / 100.0;
         } else if (option == DXRPT_OPT_SHADE_BLOCK) {
             require(value == 64 || value == 128 || value == 256, "dxrpt_set_option: shade block must be 64, 128 or 256");
             ctx->opt_shade_block = uint32_t(value);
@@ -513,9 +521,12 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
         }
         BvhBuildResult res;
         std::string err;
-        if (!build_bvh(pos.data(), ntris, ctx->opt_width, res, err)) throw ApiError(DXRPT_E_INVALID_ARG, err);
-        std::vector<TriRecord> tris(ntris);
-        for (uint32_t i = 0; i < ntris; ++i) {
+        if (!build_bvh(pos.data(), ntris, ctx->opt_width, res, err, &ctx->build_params))
+            throw ApiError(DXRPT_E_INVALID_ARG, err);
+        // one record per leaf reference (BVH8 spatial splits may reference a triangle more than once)
+        const uint32_t nrefs = uint32_t(res.tri_order.size());
+        std::vector<TriRecord> tris(nrefs);
+        for (uint32_t i = 0; i < nrefs; ++i) {
             const uint32_t t = res.tri_order[i];
             const float* v = &pos[size_t(t) * 9];
             TriRecord& r = tris[i];

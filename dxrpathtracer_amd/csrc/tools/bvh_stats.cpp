@@ -6,7 +6,7 @@
 // primary hits.  Prints node visits and triangle tests per ray, the quantities the traversal kernels'
 // VALU cost scales with, so builder changes can be compared on CPU before spending GPU time.
 //
-//   make tools && ./build/bvh_stats [scene_id=0] [grid_w=320] [grid_h=180] [binary_depth_cap]
+//   make tools && ./build/bvh_stats [scene_id=0] [grid_w=320] [grid_h=180] [binary_depth_cap] [ref_budget]
 // (grid_w and grid_h multiples of 8)
 #include <math.h>
 #include <stdio.h>
@@ -282,10 +282,14 @@ int main(int argc, char** argv) {
     const uint32_t scene_id = argc > 1 ? uint32_t(atoi(argv[1])) : 0u;
     const uint32_t gw = argc > 2 ? uint32_t(atoi(argv[2])) : 320u;
     const uint32_t gh = argc > 3 ? uint32_t(atoi(argv[3])) : 180u;
-    BvhBuildParams params;  // argv[4]: binary depth cap to explore (the wide depth is then unbounded)
-    if (argc > 4) {
+    BvhBuildParams params;  // argv[4]: binary depth cap to explore (0: default; the wide depth is then unbounded)
+    if (argc > 4 && atoi(argv[4]) > 0) {
         params.binary_depth_cap = uint32_t(atoi(argv[4]));
         params.max_wide_depth = 1000u;
+    }
+    if (argc > 5) {  // argv[5]: spatial-split reference budget (0: no spatial splits)
+        params.ref_budget = atof(argv[5]);
+        params.spatial_splits = params.ref_budget > 0.0;
     }
     dxrpt_host_scene* hs = nullptr;
     if (dxrpt_host_scene_create(scene_id, 0, 0, &hs) != 0) {

@@ -17,9 +17,10 @@ sys.path.insert(0, REPO)
 
 
 KEYS = {"w": "width", "m": "mode", "r": "refill", "k": "chunks", "p": "postpone", "b": "block", "o": "occ",
-        "s": "sblock", "q": "socc"}
+        "s": "sblock", "q": "socc", "x": "spatial", "c": "leafcost"}
 DEFAULTS = {"width": 8, "mode": 0, "refill": 16, "chunks": 4, "postpone": 0, "block": 64, "occ": 8, "sblock": 256,
-            "socc": 0}
+            "socc": 0, "spatial": 150, "leafcost": 150}
+BUILD_KEYS = ("width", "spatial", "leafcost")  # a separate context (BVH) per combination
 
 
 def parse(v):
@@ -58,12 +59,15 @@ def main():
     st = sc.settings(MaxPathLength=args.L)
     sky = D.make_sky(st)
     tracers = {}
-    for width in sorted({parse(v)["width"] for v in args.variants.split(",")}):
+    for bk in sorted({tuple(parse(v)[k] for k in BUILD_KEYS) for v in args.variants.split(",")}):
         t = DXRPathTracer(0)
-        t.set_option(A.OPT_BVH_WIDTH, width)
+        t.set_option(A.OPT_BVH_WIDTH, bk[0])
+        t.set_option(A.OPT_SPATIAL_SPLITS, bk[1])
+        t.set_option(A.OPT_LEAF_COST, bk[2])
         t.initialize_scene(sc, sky)
-        t.build_rt_acceleration_structure()
-        tracers[width] = t
+        info = t.build_rt_acceleration_structure()
+        print(f"bvh {bk}: {info.num_nodes} nodes depth {info.max_depth} build {info.build_ms:.0f} ms", flush=True)
+        tracers[bk] = t
     accum = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
     consts = [D.make_constants(sc, st, sky, W, H, s) for s in range(16)]
     lights = D.make_lights(sc)
@@ -72,7 +76,7 @@ def main():
     for rnd in range(args.rounds):
         for v in res:
             o = parse(v)
-            t = tracers[o["width"]]
+            t = tracers[tuple(o[k] for k in BUILD_KEYS)]
             t.set_option(A.OPT_POSTPONE_TRIS, o["postpone"])
             t.set_option(A.OPT_TRAVERSAL_MODE, o["mode"])
             t.set_option(A.OPT_REFILL_LANES, o["refill"])
