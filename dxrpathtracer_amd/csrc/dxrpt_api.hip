@@ -75,6 +75,7 @@ struct dxrpt_ctx {
     // device copies
     DevBuf d_vertices, d_indices, d_geos, d_mats, d_texdesc, d_texels, d_sky, d_lut, d_nodes, d_nodes8, d_tris;
     DevBuf d_lights, d_tiles, d_tile_prefix;
+    DevBuf d_tri_verts;  // per global triangle: its 3 MeshVertex records (3 x 64 B), built with the BVH
     // per-frame wavefront buffers
     DevBuf f_pix, f_pxrad, f_hit, f_fwd, f_shn, f_shq, f_shorg, f_shdir, f_shcon, f_counters;
     DevBuf f_q[2][5];  // RayQueue org, dir, thr, rad, pix per depth parity
@@ -95,7 +96,8 @@ struct dxrpt_ctx {
     uint32_t opt_chunks = 4;        // DXRPT_OPT_CHUNKS_PER_WAVE
     uint32_t opt_postpone = 0;      // DXRPT_OPT_POSTPONE_TRIS
     uint32_t opt_trace_block = 64;  // DXRPT_OPT_TRACE_BLOCK
-    uint32_t opt_occupancy = 8;     // DXRPT_OPT_OCCUPANCY
+    uint32_t opt_occupancy = 7;     // DXRPT_OPT_OCCUPANCY
+    uint32_t opt_shadow_occ = 8;    // DXRPT_OPT_SHADOW_OCCUPANCY
     uint32_t opt_shade_block = 256; // DXRPT_OPT_SHADE_BLOCK
     uint32_t opt_shade_occ = 0;     // DXRPT_OPT_SHADE_OCCUPANCY
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
@@ -117,7 +119,7 @@ struct dxrpt_ctx {
 
     ~dxrpt_ctx() {
         DevBuf* all[] = {&d_vertices, &d_indices, &d_geos, &d_mats, &d_texdesc, &d_texels, &d_sky, &d_lut, &d_nodes,
-                         &d_nodes8, &d_tris, &d_lights, &d_tiles, &d_tile_prefix, &f_pix, &f_pxrad, &f_hit, &f_fwd,
+                         &d_nodes8, &d_tris, &d_tri_verts, &d_lights, &d_tiles, &d_tile_prefix, &f_pix, &f_pxrad, &f_hit, &f_fwd,
                          &f_shn, &f_shq, &f_shorg, &f_shdir, &f_shcon, &f_counters};
         for (DevBuf* b : all) b->release();
         for (auto& qb : f_q)
@@ -185,6 +187,7 @@ SceneDev scene_dev(dxrpt_ctx* c, uint32_t traversal_threads) {
         s.stack_ints = std::min<uint32_t>(entries, uint32_t(kTraversalStack));
     }
     s.tris = c->d_tris.as<TriRecord>();
+    s.tri_verts = c->d_tri_verts.as<float4>();
     s.vertices = c->d_vertices.as<dxrpt_mesh_vertex>();
     s.indices = c->d_indices.as<uint32_t>();
     s.geoinfo = c->d_geos.as<dxrpt_geometry_info>();
@@ -376,9 +379,9 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_TRACE_BLOCK) {
             require(value == 64 || value == 128 || value == 256, "dxrpt_set_option: trace block must be 64, 128 or 256");
             ctx->opt_trace_block = uint32_t(value);
-        } else if (option == DXRPT_OPT_OCCUPANCY) {
+        } else if (option == DXRPT_OPT_OCCUPANCY || option == DXRPT_OPT_SHADOW_OCCUPANCY) {
             require(value == 0 || value == 7 || value == 8, "dxrpt_set_option: occupancy must be 0, 7 or 8");
-            ctx->opt_occupancy = uint32_t(value);
+            (option == DXRPT_OPT_OCCUPANCY ? ctx->opt_occupancy : ctx->opt_shadow_occ) = uint32_t(value);
         } else if (option == DXRPT_OPT_SPATIAL_SPLITS) {
             require(value <= 400, "dxrpt_set_option: spatial-split budget must be 0..400 (percent of triangles)");
             ctx->build_params.spatial_splits = value > 100;
@@ -467,16 +470,23 @@ int dxrpt_add_texture(dxrpt_ctx* ctx, uint32_t w, uint32_t h, uint32_t fmt, cons
         d.width = w;
         d.height = h;
         d.fmt = fmt;
-        const size_t n = size_t(w) * h;
-        if (fmt == DXRPT_TEX_R8_UNORM) {
-            const size_t words = (n + 3) / 4;
-            size_t at = ctx->texels.size();
-            ctx->texels.resize(at + words, 0u);
-            std::memcpy(ctx->texels.data() + at, texels, n);
-        } else {
-            const uint32_t* s = static_cast<const uint32_t*>(texels);
-            ctx->texels.insert(ctx->texels.end(), s, s + n);
-        }
+        // 128-B tiles (pt_layout.h TexDesc): a bilinear footprint usually falls in one cache line
+        const bool r8 = fmt == DXRPT_TEX_R8_UNORM;
+        const uint32_t tw = r8 ? kTexTileW8 : kTexTileW32, th = r8 ? kTexTileH8 : kTexTileH32;
+        const uint32_t tiles_x = (w + tw - 1) / tw, tiles_y = (h + th - 1) / th;
+        const size_t at = ctx->texels.size();
+        ctx->texels.resize(at + size_t(tiles_x) * tiles_y * kTexTileWords, 0u);
+        uint32_t* dst = ctx->texels.data() + at;
+        for (uint32_t y = 0; y < h; ++y)
+            for (uint32_t x = 0; x < w; ++x) {
+                const size_t word = tex_tile_word(x, y, tiles_x, r8);
+                if (r8) {
+                    const uint32_t b = static_cast<const uint8_t*>(texels)[size_t(y) * w + x];
+                    dst[word] |= b << (8u * (x & 3u));
+                } else {
+                    dst[word] = static_cast<const uint32_t*>(texels)[size_t(y) * w + x];
+                }
+            }
         require(ctx->texels.size() < (size_t(1) << 32), "dxrpt_add_texture: texel pool exceeds 2^32 words");
         if (out_index) *out_index = uint32_t(ctx->texdesc.size());
         ctx->texdesc.push_back(d);
@@ -546,6 +556,14 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
             ctx->d_nodes.upload(res.nodes.data(), res.nodes.size() * sizeof(BvhNode));
         }
         ctx->d_tris.upload(tris.data(), tris.size() * sizeof(TriRecord));
+        {   // shading-side copy of each triangle's vertices: one contiguous 192-B record per gtri, so a
+            // hit gathers 2 cache lines in one round trip instead of 3 indices then 3 vertices
+            std::vector<dxrpt_mesh_vertex> tv(size_t(ntris) * 3);
+            for (uint32_t t = 0; t < ntris; ++t)
+                for (int k = 0; k < 3; ++k)
+                    tv[size_t(t) * 3 + k] = ctx->vertices[ctx->indices[size_t(t) * 3 + k] + ctx->geos[tri_geom[t]].VtxOffset];
+            ctx->d_tri_verts.upload(tv.data(), tv.size() * sizeof(dxrpt_mesh_vertex));
+        }
         auto t1 = std::chrono::steady_clock::now();
         ctx->bvh.num_nodes = uint32_t(ctx->opt_width == 8 ? res.nodes8.size() : res.nodes.size());
         ctx->bvh.num_leaves = res.num_leaves;
@@ -646,6 +664,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.postpone_tris = ctx->opt_postpone;
         fp.trace_block = ctx->opt_trace_block;
         fp.occupancy = ctx->opt_occupancy;
+        fp.shadow_occupancy = ctx->opt_shadow_occ;
         fp.shade_block = ctx->opt_shade_block;
         fp.shade_occupancy = ctx->opt_shade_occ;
         hipStream_t s = static_cast<hipStream_t>(stream);

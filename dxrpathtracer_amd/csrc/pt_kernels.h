@@ -8,6 +8,13 @@
 
 namespace dxrpt {
 
+// Word index of texel (x, y) relative to TexDesc::offset; tiles_x = ceil(width / tile width).
+__host__ __device__ __attribute__((always_inline)) inline uint32_t tex_tile_word(uint32_t x, uint32_t y, uint32_t tiles_x,
+                                                                                 bool r8) {
+    if (r8) return ((y >> 3) * tiles_x + (x >> 4)) * kTexTileWords + (y & 7u) * 4u + ((x & 15u) >> 2);
+    return ((y >> 2) * tiles_x + (x >> 3)) * kTexTileWords + (y & 3u) * 8u + (x & 7u);
+}
+
 // Queue counters are sharded: a producer wave w appends to shard (w % kQueueShards) of the queue,
 // so concurrent waves spread their atomics over kQueueShards addresses instead of one.  Shard s of a
 // queue owns positions [s * cap, (s + 1) * cap); consumers enumerate item i of the queue by walking
@@ -74,6 +81,7 @@ struct SceneDev {
     const BvhNode* nodes = nullptr;     // width 2
     const Bvh8Node* nodes8 = nullptr;   // width 8
     const TriRecord* tris = nullptr;
+    const float4* tri_verts = nullptr;  // per global triangle: 3 MeshVertex records = 12 float4
     const dxrpt_mesh_vertex* vertices = nullptr;
     const uint32_t* indices = nullptr;
     const dxrpt_geometry_info* geoinfo = nullptr;
@@ -108,7 +116,8 @@ struct FrameParams {
     uint32_t chunks_per_wave;        // BVH8 wave-pool traversal: 64-ray chunks per wave; 0 = one thread per ray
     uint32_t refill_lanes;           // wave-pool kernels: refill once this many lanes of a wave are idle
     uint32_t trace_block;            // workgroup size of the one-thread-per-ray traversal kernels (64..256)
-    uint32_t occupancy;              // BVH8 traversal kernels: 0 compiler default, 7 or 8 waves per SIMD
+    uint32_t occupancy;              // BVH8 closest-hit kernel: 0 compiler default, 7 or 8 waves per SIMD
+    uint32_t shadow_occupancy;       // BVH8 any-hit kernel: 0 compiler default, 7 or 8 waves per SIMD
     uint32_t shade_block;            // workgroup size of k_shade (64..256)
     uint32_t shade_occupancy;        // k_shade register budget: 0 compiler default, 6, 7 or 8 waves per SIMD
     uint32_t postpone_tris;          // wave-pool kernels: test pending triangles once this many lanes hold

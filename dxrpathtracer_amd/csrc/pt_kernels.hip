@@ -55,14 +55,16 @@ struct Texel4 {
 };
 
 PT_DEV Texel4 fetch_texel(const SceneDev& S, const TexDesc& td, int x, int y) {
-    uint32_t idx = uint32_t(y) * td.width + uint32_t(x);
+    const bool r8 = td.fmt == DXRPT_TEX_R8_UNORM;
+    const uint32_t tiles_x = (td.width + (r8 ? kTexTileW8 : kTexTileW32) - 1u) / (r8 ? kTexTileW8 : kTexTileW32);
+    const uint32_t word = tex_tile_word(uint32_t(x), uint32_t(y), tiles_x, r8);
     Texel4 t;
-    if (td.fmt == DXRPT_TEX_R8_UNORM) {
-        uint32_t w = S.texels[td.offset + (idx >> 2)];
-        float v = S.lut[(w >> ((idx & 3u) * 8u)) & 0xFFu];
+    if (r8) {
+        uint32_t w = S.texels[td.offset + word];
+        float v = S.lut[(w >> ((uint32_t(x) & 3u) * 8u)) & 0xFFu];
         t.r = v; t.g = v; t.b = v; t.a = 1.0f;
     } else {
-        uint32_t w = S.texels[td.offset + idx];
+        uint32_t w = S.texels[td.offset + word];
         const float* l = S.lut + (td.fmt == DXRPT_TEX_RGBA8_SRGB ? 256 : 0);
         t.r = l[w & 0xFFu];
         t.g = l[(w >> 8) & 0xFFu];
@@ -134,18 +136,15 @@ struct Surface {
 
 PT_DEV float bary_lerp(float a, float b, float c, float w0, float w1, float w2) { return (a * w0 + b * w1) + c * w2; }
 
-PT_DEV Surface get_hit_surface(const SceneDev& S, uint32_t geom, uint32_t gtri, float b1, float b2) {
-    const dxrpt_geometry_info gi = S.geoinfo[geom];
+PT_DEV Surface get_hit_surface(const SceneDev& S, uint32_t gtri, float b1, float b2) {
     const float w0 = (1.0f - b1) - b2;
-    const uint32_t base = gtri * 3u;  // == PrimitiveIndex()*3 + IdxOffset
-    const float4* V = reinterpret_cast<const float4*>(S.vertices);
+    // the triangle's vertices idx[gtri*3 + k] + VtxOffset, copied contiguously at build time
+    const float4* V = S.tri_verts + size_t(gtri) * 12u;
     float4 q[3][4];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const uint32_t vi = S.indices[base + k] + gi.VtxOffset;
+    for (int k = 0; k < 3; ++k)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) q[k][j] = V[size_t(vi) * 4 + j];
-    }
+        for (int j = 0; j < 4; ++j) q[k][j] = V[k * 4 + j];
     // MeshVertex layout: q[.][0] = pos.xyz, n.x ; [1] = n.yz, uv ; [2] = t.xyz, b.x ; [3] = b.yz, lmuv
     Surface s;
     s.pos = f3{bary_lerp(q[0][0].x, q[1][0].x, q[2][0].x, w0, b1, b2), bary_lerp(q[0][0].y, q[1][0].y, q[2][0].y, w0, b1, b2),
@@ -167,11 +166,10 @@ PT_DEV bool alpha_accepts(const SceneDev& S, uint32_t geom, uint32_t gtri, float
     const uint32_t opacity = S.materials[gi.MaterialIdx].Opacity;
     if (opacity == DXRPT_INVALID_INDEX) return true;
     const float w0 = (1.0f - b1) - b2;
-    const uint32_t base = gtri * 3u;
-    const float2* V = reinterpret_cast<const float2*>(S.vertices);
+    const float2* V = reinterpret_cast<const float2*>(S.tri_verts + size_t(gtri) * 12u);
     float2 uv[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) uv[k] = V[size_t(S.indices[base + k] + gi.VtxOffset) * 8 + 3];  // float2 #3 = UV
+    for (int k = 0; k < 3; ++k) uv[k] = V[k * 8 + 3];  // float2 #3 of MeshVertex k = UV
     float u = bary_lerp(uv[0].x, uv[1].x, uv[2].x, w0, b1, b2);
     float v = bary_lerp(uv[0].y, uv[1].y, uv[2].y, w0, b1, b2);
     return !(sample_tex(S, opacity, u, v).r < 0.35f);
@@ -668,7 +666,7 @@ void k_shade(KArgs A, int depth) {
         if ((!set.EnableDiffuse && !set.EnableSpecular) || (!set.EnableDirect && !set.EnableIndirect)) break;
         if (depth > 1 && !set.EnableIndirect) break;
         const uint32_t geom = fbits(hit.w);
-        const Surface surf = get_hit_surface(A.S, geom, tri, hit.x, hit.y);
+        const Surface surf = get_hit_surface(A.S, tri, hit.x, hit.y);
         const dxrpt_material mat = A.S.materials[A.S.geoinfo[geom].MaterialIdx];
         const f3 T = surf.t, Bt = surf.b;
         f3 Nrow = surf.n;
@@ -1078,12 +1076,11 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
             else { if (count) DXRPT_LAUNCH(k_trace, true, 2, 0, G); else DXRPT_LAUNCH(k_trace, false, 2, 0, G); }
         } else if (count) {
             if (shadow) DXRPT_LAUNCH(k_shadow, true, 8, 0, G); else DXRPT_LAUNCH(k_trace, true, 8, 0, G);
-        } else if (fp.occupancy == 7) {
-            if (shadow) DXRPT_LAUNCH(k_shadow, false, 8, 7, G); else DXRPT_LAUNCH(k_trace, false, 8, 7, G);
-        } else if (fp.occupancy == 8) {
-            if (shadow) DXRPT_LAUNCH(k_shadow, false, 8, 8, G); else DXRPT_LAUNCH(k_trace, false, 8, 8, G);
         } else {
-            if (shadow) DXRPT_LAUNCH(k_shadow, false, 8, 0, G); else DXRPT_LAUNCH(k_trace, false, 8, 0, G);
+            const uint32_t occ = shadow ? fp.shadow_occupancy : fp.occupancy;
+            if (occ == 7) { if (shadow) DXRPT_LAUNCH(k_shadow, false, 8, 7, G); else DXRPT_LAUNCH(k_trace, false, 8, 7, G); }
+            else if (occ == 8) { if (shadow) DXRPT_LAUNCH(k_shadow, false, 8, 8, G); else DXRPT_LAUNCH(k_trace, false, 8, 8, G); }
+            else { if (shadow) DXRPT_LAUNCH(k_shadow, false, 8, 0, G); else DXRPT_LAUNCH(k_trace, false, 8, 0, G); }
         }
 #undef DXRPT_LAUNCH
     };

@@ -79,14 +79,22 @@ static_assert(sizeof(TriRecord) == 48, "TriRecord must be 48 B");
 
 constexpr uint32_t kTriOpaque = 1u;
 
-// Texture descriptor, 16 B.  Texels live in one pool of 32-bit words starting at `offset`.
-//   fmt DXRPT_TEX_RGBA8_*: one word per texel (r | g<<8 | b<<16 | a<<24)
-//   fmt DXRPT_TEX_R8_UNORM: four texels per word (row-major, texel i in byte i&3 of word i>>2)
+// Texture descriptor, 16 B.  Texels live in one pool of 32-bit words starting at `offset`, in
+// 128-B tiles (one L2 line) laid out row-major by tile; width and height are padded up to whole tiles
+// (padding texels are never sampled: coordinates wrap at the true size).
+//   fmt DXRPT_TEX_RGBA8_*: one word per texel (r | g<<8 | b<<16 | a<<24), 8 x 4 texels per tile
+//   fmt DXRPT_TEX_R8_UNORM: four texels per word (x & 3 selects the byte), 16 x 8 texels per tile
 struct TexDesc {
     uint32_t offset;
     uint32_t width;
     uint32_t height;
     uint32_t fmt;
 };
+
+constexpr uint32_t kTexTileWords = 32;  // 128 B
+constexpr uint32_t kTexTileW32 = 8, kTexTileH32 = 4;
+constexpr uint32_t kTexTileW8 = 16, kTexTileH8 = 8;
+
+
 
 }  // namespace dxrpt

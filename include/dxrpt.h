@@ -267,12 +267,13 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 #define DXRPT_OPT_POSTPONE_TRIS 7u    /* wave-pool mode: batch triangle tests until this many lanes have some
                                          (0 = test with the node visit, default) */
 #define DXRPT_OPT_TRACE_BLOCK 8u      /* workgroup size of the one-thread-per-ray traversal kernels: 64 (default), 128, 256 */
-#define DXRPT_OPT_OCCUPANCY 9u        /* BVH8 traversal register budget: 0 = compiler default, 7 or 8 (default) waves/SIMD */
+#define DXRPT_OPT_OCCUPANCY 9u        /* BVH8 closest-hit register budget: 0 = compiler default, 7 (default) or 8 waves/SIMD */
 #define DXRPT_OPT_SHADE_BLOCK 10u     /* workgroup size of the shading kernel: 64, 128, 256 (default) */
 #define DXRPT_OPT_SHADE_OCCUPANCY 11u /* shading kernel register budget: 0 = compiler default, 6, 7 or 8 waves/SIMD */
 #define DXRPT_OPT_SPATIAL_SPLITS 12u  /* BVH8 build: spatial-split reference budget in percent of the triangle count
                                          (101..400; <= 100 disables spatial splits; default 150) */
 #define DXRPT_OPT_LEAF_COST 13u       /* BVH8 build: triangle-test cost in percent of a node visit (default 150) */
+#define DXRPT_OPT_SHADOW_OCCUPANCY 14u /* BVH8 any-hit register budget: 0 = compiler default, 7 or 8 (default) waves/SIMD */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

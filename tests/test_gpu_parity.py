@@ -224,15 +224,17 @@ def test_traversal_launch_options_are_bit_identical(torch_cuda, block, occ, sblo
     ref = gpu_render(torch, "suntemple", 480, 270, st, 5).cpu().numpy()
     t.set_option(A.OPT_TRACE_BLOCK, block)
     t.set_option(A.OPT_OCCUPANCY, occ)
+    t.set_option(A.OPT_SHADOW_OCCUPANCY, 15 - occ if occ else 0)
     t.set_option(A.OPT_SHADE_BLOCK, sblock)
     t.set_option(A.OPT_SHADE_OCCUPANCY, socc)
     try:
         got = gpu_render(torch, "suntemple", 480, 270, st, 5).cpu().numpy()
     finally:
         t.set_option(A.OPT_TRACE_BLOCK, 64)
-        t.set_option(A.OPT_OCCUPANCY, 8)
+        t.set_option(A.OPT_OCCUPANCY, 7)
         t.set_option(A.OPT_SHADE_BLOCK, 256)
         t.set_option(A.OPT_SHADE_OCCUPANCY, 0)
+        t.set_option(A.OPT_SHADOW_OCCUPANCY, 8)
     np.testing.assert_array_equal(got, ref)
 
 
