@@ -98,6 +98,7 @@ struct dxrpt_ctx {
     uint32_t opt_trace_block = 64;  // DXRPT_OPT_TRACE_BLOCK
     uint32_t opt_occupancy = 7;     // DXRPT_OPT_OCCUPANCY
     uint32_t opt_shadow_occ = 8;    // DXRPT_OPT_SHADOW_OCCUPANCY
+    uint32_t opt_shadow_grid = 0;   // DXRPT_OPT_SHADOW_GRID
     uint32_t opt_shade_block = 256; // DXRPT_OPT_SHADE_BLOCK
     uint32_t opt_shade_occ = 0;     // DXRPT_OPT_SHADE_OCCUPANCY
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
@@ -389,6 +390,9 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_LEAF_COST) {
             require(value >= 5 && value <= 1000, "dxrpt_set_option: leaf cost must be 5..1000 (percent of a node visit)");
             ctx->build_params.leaf_cost = double(value) / 100.0;
+        } else if (option == DXRPT_OPT_SHADOW_GRID) {
+            require(value <= 1u << 20, "dxrpt_set_option: shadow grid cap too large");
+            ctx->opt_shadow_grid = uint32_t(value);
         } else if (option == DXRPT_OPT_SHADE_BLOCK) {
             require(value == 64 || value == 128 || value == 256, "dxrpt_set_option: shade block must be 64, 128 or 256");
             ctx->opt_shade_block = uint32_t(value);
@@ -665,6 +669,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.trace_block = ctx->opt_trace_block;
         fp.occupancy = ctx->opt_occupancy;
         fp.shadow_occupancy = ctx->opt_shadow_occ;
+        fp.shadow_grid = ctx->opt_shadow_grid;
         fp.shade_block = ctx->opt_shade_block;
         fp.shade_occupancy = ctx->opt_shade_occ;
         hipStream_t s = static_cast<hipStream_t>(stream);

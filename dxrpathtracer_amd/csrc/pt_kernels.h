@@ -118,6 +118,7 @@ struct FrameParams {
     uint32_t trace_block;            // workgroup size of the one-thread-per-ray traversal kernels (64..256)
     uint32_t occupancy;              // BVH8 closest-hit kernel: 0 compiler default, 7 or 8 waves per SIMD
     uint32_t shadow_occupancy;       // BVH8 any-hit kernel: 0 compiler default, 7 or 8 waves per SIMD
+    uint32_t shadow_grid;            // any-hit kernel grid cap in 256-thread workgroups (0 = one thread per ray)
     uint32_t shade_block;            // workgroup size of k_shade (64..256)
     uint32_t shade_occupancy;        // k_shade register budget: 0 compiler default, 6, 7 or 8 waves per SIMD
     uint32_t postpone_tris;          // wave-pool kernels: test pending triangles once this many lanes hold

@@ -32,7 +32,6 @@
 namespace dxrpt {
 
 constexpr int kBlock = 256;
-constexpr uint32_t kShadowGrid = 256u * 20u;  // grid-stride cap: ~20 workgroups per CU
 constexpr uint32_t kMiss = 0xFFFFFFFFu;
 constexpr float kRayTMin = 0.00001f;          // RayTrace.hlsl:243, 382
 constexpr float kSpotShadowNearClip = 0.1f;   // AppSettings.hlsl:56
@@ -325,8 +324,25 @@ PT_DEV void ray8_init(Ray8& R, f3 o, f3 d, float tmin, float tmax, bool alpha, H
 // node (pops when the current group is exhausted).  Returns false when no node is left to visit.  The
 // pending triangles must be tested (trav8_tris) before the next node visit, so that the visit order
 // and hence the result are the same however tests and visits of different lanes are interleaved.
+// Group stack: `sp` entries; the top one lives in registers (`tos`), entries 0 .. sp-2 in LDS
+// (first kStackLds8) and in the thread's global spill slab (deeper), so a pop hands over the next
+// group at once and the LDS refill of `tos` overlaps the next node fetch.
+PT_DEV void stack8_store(const SceneDev& S, int* stk, int j, uint2 e) {
+    if (j < kStackLds8) {
+        stk[(2 * j) * blockDim.x] = int(e.x);
+        stk[(2 * j + 1) * blockDim.x] = int(e.y);
+    } else {  // rare: deep entries spill to this thread's global slab
+        S.spill8[size_t(j - kStackLds8) * S.spill_stride + blockIdx.x * blockDim.x + threadIdx.x] = e;
+    }
+}
+
+PT_DEV uint2 stack8_load(const SceneDev& S, const int* stk, int j) {
+    if (j < kStackLds8) return make_uint2(uint32_t(stk[(2 * j) * blockDim.x]), uint32_t(stk[(2 * j + 1) * blockDim.x]));
+    return S.spill8[size_t(j - kStackLds8) * S.spill_stride + blockIdx.x * blockDim.x + threadIdx.x];
+}
+
 template <bool kCount>
-PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp, int* stk, const HitRec& h,
+PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp, int* stk, uint2& tos, const HitRec& h,
                        uint32_t& tbase, uint32_t& tbits, uint32_t& nvisit) {
     if (kCount) ++nvisit;
     const uint4* N = reinterpret_cast<const uint4*>(S.nodes8);
@@ -391,28 +407,17 @@ PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp
             gword &= ~(1u << k);
             const uint32_t slot = (k - 24u) ^ R.oct;
             node = gbase + uint32_t(__builtin_popcount(gword & 0xFFu & ((1u << slot) - 1u)));
-            if (gword >> 24) {
-                if (sp < kStackLds8) {
-                    stk[(2 * sp) * blockDim.x] = int(gbase);
-                    stk[(2 * sp + 1) * blockDim.x] = int(gword);
-                } else {  // rare: deeper entries spill to this thread's global slab
-                    S.spill8[size_t(sp - kStackLds8) * S.spill_stride + blockIdx.x * blockDim.x + threadIdx.x] =
-                        make_uint2(gbase, gword);
-                }
+            if (gword >> 24) {  // push the rest of the group
+                if (sp > 0) stack8_store(S, stk, sp - 1, tos);
+                tos = make_uint2(gbase, gword);
                 ++sp;
             }
             return true;
         }
         if (sp == 0) return false;
-        --sp;
-        if (sp < kStackLds8) {
-            gbase = uint32_t(stk[(2 * sp) * blockDim.x]);
-            gword = uint32_t(stk[(2 * sp + 1) * blockDim.x]);
-        } else {
-            const uint2 e = S.spill8[size_t(sp - kStackLds8) * S.spill_stride + blockIdx.x * blockDim.x + threadIdx.x];
-            gbase = e.x;
-            gword = e.y;
-        }
+        gbase = tos.x;  // pop
+        gword = tos.y;
+        if (--sp > 0) tos = stack8_load(S, stk, sp - 1);
     }
 }
 
@@ -431,10 +436,10 @@ PT_DEV bool trav8_tris(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32_
 // One node visit and its triangles.  Returns true when the ray is finished: h.tri != kMiss means hit
 // (closest) / occluded (any-hit).
 template <bool kAnyHit, bool kCount>
-PT_DEV bool trav8_step(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp, int* stk, HitRec& h,
+PT_DEV bool trav8_step(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp, int* stk, uint2& tos, HitRec& h,
                        uint32_t& nvisit, uint32_t& ntest) {
     uint32_t tbase = 0, tbits = 0;
-    const bool more = trav8_node<kCount>(S, R, node, sp, stk, h, tbase, tbits, nvisit);
+    const bool more = trav8_node<kCount>(S, R, node, sp, stk, tos, h, tbase, tbits, nvisit);
     if (tbits && trav8_tris<kAnyHit, kCount>(S, R, tbase, tbits, h, ntest)) return true;
     return !more;
 }
@@ -446,7 +451,8 @@ PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
     ray8_init(R, o, d, tmin, tmax, alpha, h);
     uint32_t node = 0;
     int sp = 0;
-    while (!trav8_step<kAnyHit, kCount>(S, R, node, sp, stk, h, nvisit, ntest)) {
+    uint2 tos = make_uint2(0u, 0u);
+    while (!trav8_step<kAnyHit, kCount>(S, R, node, sp, stk, tos, h, nvisit, ntest)) {
     }
     return h.tri != kMiss;
 }
@@ -907,6 +913,7 @@ __global__ __launch_bounds__(kBlock) void k_traverse8p(KArgs A, int depth) {
     const uint32_t postpone = A.P.postpone_tris;
     bool active = false, more = false;
     uint32_t item = 0, tbase = 0, tbits = 0;
+    uint2 tos = make_uint2(0u, 0u);
     Ray8 R;
     HitRec h;
     uint32_t node = 0;
@@ -948,7 +955,7 @@ __global__ __launch_bounds__(kBlock) void k_traverse8p(KArgs A, int depth) {
         bool finished = false;
         if (postpone == 0u) {  // triangles inline with their node visit
             if (active) {
-                more = trav8_node<kCount>(A.S, R, node, sp, stk, h, tbase, tbits, nv);
+                more = trav8_node<kCount>(A.S, R, node, sp, stk, tos, h, tbase, tbits, nv);
                 const bool occ = tbits && trav8_tris<kShadow, kCount>(A.S, R, tbase, tbits, h, nt);
                 tbits = 0;
                 finished = occ || !more;
@@ -966,7 +973,7 @@ __global__ __launch_bounds__(kBlock) void k_traverse8p(KArgs A, int depth) {
                     finished = occ || !more;
                 }
             } else if (node_lane) {
-                more = trav8_node<kCount>(A.S, R, node, sp, stk, h, tbase, tbits, nv);
+                more = trav8_node<kCount>(A.S, R, node, sp, stk, tos, h, tbase, tbits, nv);
                 finished = !more && tbits == 0u;
             }
         }
@@ -1032,7 +1039,7 @@ static inline uint32_t pool_grid(uint32_t n, uint32_t chunks_per_wave) {
 }
 
 uint32_t frame_traversal_threads(uint32_t num_paths, uint32_t shadow_slots, uint32_t chunks_per_wave) {
-    const uint32_t gs = std::min<uint32_t>(grid_for(num_paths * shadow_slots), kShadowGrid);
+    const uint32_t gs = grid_for(num_paths * shadow_slots);
     uint32_t g = std::max(grid_for(num_paths), gs);
     if (chunks_per_wave)
         g = std::max(g, std::max(pool_grid(num_paths, chunks_per_wave), pool_grid(num_paths * shadow_slots, chunks_per_wave)));
@@ -1059,7 +1066,10 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
     const int L = fp.set.MaxPathLength < 2 ? 2 : fp.set.MaxPathLength;
     const uint32_t tb = fp.trace_block;
     const uint32_t gt = (fp.num_paths + tb - 1u) / tb;
-    const uint32_t gst = std::min<uint32_t>((fp.num_paths * fb.shadow_slots + tb - 1u) / tb, kShadowGrid * (kBlock / tb));
+    // any-hit grid: one thread per queued shadow ray (upper bound num_paths * slots; surplus waves
+    // exit at once), or a grid-stride loop over a capped grid of shadow_grid 256-thread equivalents
+    const uint32_t gst_full = (fp.num_paths * fb.shadow_slots + tb - 1u) / tb;
+    const uint32_t gst = fp.shadow_grid ? std::min<uint32_t>(gst_full, fp.shadow_grid * (kBlock / tb)) : gst_full;
     const size_t ldst = size_t(scene.stack_ints) * tb * sizeof(int);
     const bool w8 = scene.width == 8;
     const bool pers = w8 && fp.chunks_per_wave > 0;

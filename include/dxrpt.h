@@ -274,6 +274,8 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                          (101..400; <= 100 disables spatial splits; default 150) */
 #define DXRPT_OPT_LEAF_COST 13u       /* BVH8 build: triangle-test cost in percent of a node visit (default 150) */
 #define DXRPT_OPT_SHADOW_OCCUPANCY 14u /* BVH8 any-hit register budget: 0 = compiler default, 7 or 8 (default) waves/SIMD */
+#define DXRPT_OPT_SHADOW_GRID 15u     /* any-hit kernel: grid-stride cap in 256-thread workgroups;
+                                         0 = one thread per queued shadow ray (default) */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

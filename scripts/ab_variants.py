@@ -17,9 +17,9 @@ sys.path.insert(0, REPO)
 
 
 KEYS = {"w": "width", "m": "mode", "r": "refill", "k": "chunks", "p": "postpone", "b": "block", "o": "occ",
-        "s": "sblock", "q": "socc", "x": "spatial", "c": "leafcost", "h": "hocc"}
+        "s": "sblock", "q": "socc", "x": "spatial", "c": "leafcost", "h": "hocc", "g": "sgrid"}
 DEFAULTS = {"width": 8, "mode": 0, "refill": 16, "chunks": 4, "postpone": 0, "block": 64, "occ": 7, "sblock": 256,
-            "socc": 0, "spatial": 150, "leafcost": 150, "hocc": 8}
+            "socc": 0, "spatial": 150, "leafcost": 150, "hocc": 8, "sgrid": 0}
 BUILD_KEYS = ("width", "spatial", "leafcost")  # a separate context (BVH) per combination
 
 
@@ -84,6 +84,7 @@ def main():
             t.set_option(A.OPT_TRACE_BLOCK, o["block"])
             t.set_option(A.OPT_OCCUPANCY, o["occ"])
             t.set_option(A.OPT_SHADOW_OCCUPANCY, o["hocc"])
+            t.set_option(A.OPT_SHADOW_GRID, o["sgrid"])
             t.set_option(A.OPT_SHADE_BLOCK, o["sblock"])
             t.set_option(A.OPT_SHADE_OCCUPANCY, o["socc"])
             for f in range(3):

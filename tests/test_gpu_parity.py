@@ -225,6 +225,7 @@ def test_traversal_launch_options_are_bit_identical(torch_cuda, block, occ, sblo
     t.set_option(A.OPT_TRACE_BLOCK, block)
     t.set_option(A.OPT_OCCUPANCY, occ)
     t.set_option(A.OPT_SHADOW_OCCUPANCY, 15 - occ if occ else 0)
+    t.set_option(A.OPT_SHADOW_GRID, 0 if block == 256 else 512)  # grid-stride any-hit loop vs one ray per thread
     t.set_option(A.OPT_SHADE_BLOCK, sblock)
     t.set_option(A.OPT_SHADE_OCCUPANCY, socc)
     try:
@@ -235,6 +236,7 @@ def test_traversal_launch_options_are_bit_identical(torch_cuda, block, occ, sblo
         t.set_option(A.OPT_SHADE_BLOCK, 256)
         t.set_option(A.OPT_SHADE_OCCUPANCY, 0)
         t.set_option(A.OPT_SHADOW_OCCUPANCY, 8)
+        t.set_option(A.OPT_SHADOW_GRID, 0)
     np.testing.assert_array_equal(got, ref)
 
 
