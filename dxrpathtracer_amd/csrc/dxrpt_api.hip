@@ -99,6 +99,9 @@ struct dxrpt_ctx {
     uint32_t opt_occupancy = 7;     // DXRPT_OPT_OCCUPANCY
     uint32_t opt_shadow_occ = 8;    // DXRPT_OPT_SHADOW_OCCUPANCY
     uint32_t opt_shadow_grid = 0;   // DXRPT_OPT_SHADOW_GRID
+    uint32_t opt_concurrency = 1;   // DXRPT_OPT_CONCURRENCY
+    hipStream_t aux = nullptr;      // any-hit pass stream (created on first use)
+    std::vector<hipEvent_t> fork_ev;
     uint32_t opt_shade_block = 256; // DXRPT_OPT_SHADE_BLOCK
     uint32_t opt_shade_occ = 0;     // DXRPT_OPT_SHADE_OCCUPANCY
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
@@ -129,6 +132,11 @@ struct dxrpt_ctx {
         d_spill.release();
         for (auto& f : ring)
             for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
+        if (aux) {
+            (void)hipStreamSynchronize(aux);
+            (void)hipStreamDestroy(aux);
+        }
+        for (hipEvent_t e : fork_ev) (void)hipEventDestroy(e);
     }
 };
 
@@ -255,29 +263,25 @@ void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
 // Adds one timed frame's event intervals to the per-kernel sums (blocks until the frame is done).
 void harvest(dxrpt_ctx* c, dxrpt_ctx::FrameEvents& f) {
     if (!f.pending) return;
-    HIP_CHECK(hipEventSynchronize(f.ev.back()));
+    HIP_CHECK(hipEventSynchronize(f.ev[frame_event_count(f.L) - 1]));
     auto span = [&](int a, int b) {
         float ms = 0.f;
         HIP_CHECK(hipEventElapsedTime(&ms, f.ev[a], f.ev[b]));
         return double(ms);
     };
-    int e = 0;
-    c->kernel_ms[DXRPT_K_RAYGEN] += span(e, e + 1);
+    auto slot = [&](int i) { return span(2 * i, 2 * i + 1); };
+    c->kernel_ms[DXRPT_K_RAYGEN] += slot(0);
     c->kernel_launches[DXRPT_K_RAYGEN]++;
-    ++e;
-    for (int d = 1; d <= f.L - 1; ++d) {
-        c->kernel_ms[DXRPT_K_TRACE] += span(e, e + 1);
-        c->kernel_ms[DXRPT_K_SHADE] += span(e + 1, e + 2);
-        c->kernel_ms[DXRPT_K_SHADOW] += span(e + 2, e + 3);
-        c->kernel_ms[DXRPT_K_RESOLVE] += span(e + 3, e + 4);
-        c->kernel_launches[DXRPT_K_TRACE]++;
-        c->kernel_launches[DXRPT_K_SHADE]++;
-        c->kernel_launches[DXRPT_K_SHADOW]++;
-        c->kernel_launches[DXRPT_K_RESOLVE]++;
-        e += 4;
-    }
-    c->kernel_ms[DXRPT_K_ACCUMULATE] += span(e, e + 1);
+    static const int kinds[4] = {DXRPT_K_TRACE, DXRPT_K_SHADE, DXRPT_K_SHADOW, DXRPT_K_RESOLVE};
+    for (int d = 1; d <= f.L - 1; ++d)
+        for (int k = 0; k < 4; ++k) {
+            c->kernel_ms[kinds[k]] += slot(1 + 4 * (d - 1) + k);
+            c->kernel_launches[kinds[k]]++;
+        }
+    const int acc = 1 + 4 * (f.L - 1);
+    c->kernel_ms[DXRPT_K_ACCUMULATE] += slot(acc);
     c->kernel_launches[DXRPT_K_ACCUMULATE]++;
+    const int e = 2 * acc;
     c->frame_ms += span(0, e + 1);
     c->timed_frames++;
     f.pending = false;
@@ -390,6 +394,9 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_LEAF_COST) {
             require(value >= 5 && value <= 1000, "dxrpt_set_option: leaf cost must be 5..1000 (percent of a node visit)");
             ctx->build_params.leaf_cost = double(value) / 100.0;
+        } else if (option == DXRPT_OPT_CONCURRENCY) {
+            require(value <= 1, "dxrpt_set_option: concurrency must be 0 or 1");
+            ctx->opt_concurrency = uint32_t(value);
         } else if (option == DXRPT_OPT_SHADOW_GRID) {
             require(value <= 1u << 20, "dxrpt_set_option: shadow grid cap too large");
             ctx->opt_shadow_grid = uint32_t(value);
@@ -695,7 +702,16 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             ev = f.ev.data();
         }
         const SceneDev sd = scene_dev(ctx, frame_traversal_threads(paths, ctx->fb.shadow_slots, fp.chunks_per_wave));
-        HIP_CHECK(launch_frame(sd, ctx->fb, fp, s, ev));
+        hipStream_t aux = nullptr;
+        if (ctx->opt_concurrency) {
+            if (!ctx->aux) {
+                HIP_CHECK(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+                ctx->fork_ev.resize(2 * kMaxDepthQueues);
+                for (auto& e : ctx->fork_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            }
+            aux = ctx->aux;
+        }
+        HIP_CHECK(launch_frame(sd, ctx->fb, fp, s, ev, aux, aux ? ctx->fork_ev.data() : nullptr));
         ctx->last_stream = s;
         ctx->last_L = settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength;
         std::memset(&ctx->last, 0, sizeof(ctx->last));

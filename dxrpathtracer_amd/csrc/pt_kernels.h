@@ -126,11 +126,13 @@ struct FrameParams {
 };
 
 // Kernel sequence of one frame: raygen, then (trace, shade, shadow, resolve) per depth 1..L-1, then
-// accumulate.  When `ev` is non-null, 2 + 4(L-1) + 1 events are recorded: before raygen and after each
-// launch.
-inline int frame_event_count(int L) { return 2 + 4 * (L - 1) + 1; }
+// accumulate.  With `aux` and 2 * kMaxDepthQueues `fork_ev` events, each depth's any-hit pass runs on
+// `aux` concurrently with the next depth's closest-hit pass.  When `ev` is non-null (per-kernel
+// timing), launch slot i = raygen, 1 + 4(d-1) + {trace, shade, shadow, resolve}, 1 + 4(L-1) =
+// accumulate is bracketed by events ev[2i], ev[2i+1] on the stream it runs on.
+inline int frame_event_count(int L) { return 2 * (2 + 4 * (L - 1)); }
 hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream,
-                        hipEvent_t* ev);
+                        hipEvent_t* ev, hipStream_t aux = nullptr, hipEvent_t* fork_ev = nullptr);
 
 // Closest-hit / any-hit queries on arbitrary rays (dxrpt_trace_rays): rays are (o.xyz, tmin),
 // (d.xyz, tmax) pairs; hits are (t, b1, b2, bits(global tri)) with t = -1 and tri = ~0 on miss.

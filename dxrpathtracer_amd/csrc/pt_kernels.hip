@@ -1049,20 +1049,25 @@ uint32_t frame_traversal_threads(uint32_t num_paths, uint32_t shadow_slots, uint
 uint32_t trace_rays_threads(uint32_t n) { return grid_for(n) * kBlock; }
 
 hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream,
-                        hipEvent_t* ev) {
+                        hipEvent_t* ev, hipStream_t aux, hipEvent_t* fork_ev) {
     KArgs A{scene, fb, fp};
     const uint32_t g = grid_for(fp.num_paths);
     const size_t lds = size_t(scene.stack_ints) * kBlock * sizeof(int);
     const bool count = fp.trav != nullptr;
-    int e_i = 0;
-    auto mark = [&]() {
-        if (ev) (void)hipEventRecord(ev[e_i++], stream);
+    // per-kernel timing: launch slot i (raygen, then trace/shade/shadow/resolve per depth, then
+    // accumulate) is bracketed by ev[2i], ev[2i+1] recorded on the stream the kernel runs on
+    auto start = [&](int slot, hipStream_t st) {
+        if (ev) (void)hipEventRecord(ev[2 * slot], st);
     };
+    auto stop = [&](int slot, hipStream_t st) {
+        if (ev) (void)hipEventRecord(ev[2 * slot + 1], st);
+    };
+    auto slot_of = [](int d, int kind) { return 1 + 4 * (d - 1) + kind; };  // kind 0 trace 1 shade 2 shadow 3 resolve
     hipError_t e = hipMemsetAsync(fb.counters, 0, 2 * kMaxDepthQueues * kQueueShards * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    mark();
+    start(0, stream);
     hipLaunchKernelGGL(k_raygen, dim3(g), dim3(kBlock), 0, stream, A);
-    mark();
+    stop(0, stream);
     const int L = fp.set.MaxPathLength < 2 ? 2 : fp.set.MaxPathLength;
     const uint32_t tb = fp.trace_block;
     const uint32_t gt = (fp.num_paths + tb - 1u) / tb;
@@ -1076,8 +1081,8 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
     const uint32_t gp = pers ? pool_grid(fp.num_paths, fp.chunks_per_wave) : 0u;
     const uint32_t gps = pers ? pool_grid(fp.num_paths * fb.shadow_slots, fp.chunks_per_wave) : 0u;
     // one-thread-per-ray traversal kernels: <count, width, occupancy>
-    auto trace = [&](int d) {
-#define DXRPT_LAUNCH(K, C, W, O, G) hipLaunchKernelGGL((K<C, W, O>), dim3(G), dim3(tb), ldst, stream, A, d)
+    auto trace = [&](int d, hipStream_t st) {
+#define DXRPT_LAUNCH(K, C, W, O, G) hipLaunchKernelGGL((K<C, W, O>), dim3(G), dim3(tb), ldst, st, A, d)
         const bool shadow = d < 0;
         d = shadow ? -d : d;
         const uint32_t G = shadow ? gst : gt;
@@ -1094,14 +1099,33 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
         }
 #undef DXRPT_LAUNCH
     };
-    for (int d = 1; d <= L - 1; ++d) {
+    auto radiance = [&](int d, hipStream_t st) {
+        start(slot_of(d, 0), st);
         if (pers) {
-            if (count) hipLaunchKernelGGL((k_traverse8p<true, false>), dim3(gp), dim3(kBlock), lds, stream, A, d);
-            else hipLaunchKernelGGL((k_traverse8p<false, false>), dim3(gp), dim3(kBlock), lds, stream, A, d);
+            if (count) hipLaunchKernelGGL((k_traverse8p<true, false>), dim3(gp), dim3(kBlock), lds, st, A, d);
+            else hipLaunchKernelGGL((k_traverse8p<false, false>), dim3(gp), dim3(kBlock), lds, st, A, d);
         } else {
-            trace(d);
+            trace(d, st);
         }
-        mark();
+        stop(slot_of(d, 0), st);
+    };
+    auto shadow = [&](int d, hipStream_t st) {
+        start(slot_of(d, 2), st);
+        if (pers) {
+            if (count) hipLaunchKernelGGL((k_traverse8p<true, true>), dim3(gps), dim3(kBlock), lds, st, A, d);
+            else hipLaunchKernelGGL((k_traverse8p<false, true>), dim3(gps), dim3(kBlock), lds, st, A, d);
+        } else {
+            trace(-d, st);
+        }
+        stop(slot_of(d, 2), st);
+    };
+    // Fork/join (aux != null): k_shadow(d) and k_trace(d+1) both only need k_shade(d), so the any-hit
+    // pass runs on `aux` concurrently with the next closest-hit pass; k_resolve(d) joins both before
+    // k_shade(d+1).
+    const bool fork = aux != nullptr && fork_ev != nullptr;
+    for (int d = 1; d <= L - 1; ++d) {
+        if (d == 1 || !fork) radiance(d, stream);
+        start(slot_of(d, 1), stream);
         {
             const uint32_t sb = fp.shade_block, gsh = (fp.num_paths + sb - 1u) / sb;
             switch (fp.shade_occupancy) {
@@ -1111,19 +1135,24 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
                 default: hipLaunchKernelGGL((k_shade<0>), dim3(gsh), dim3(sb), 0, stream, A, d); break;
             }
         }
-        mark();
-        if (pers) {
-            if (count) hipLaunchKernelGGL((k_traverse8p<true, true>), dim3(gps), dim3(kBlock), lds, stream, A, d);
-            else hipLaunchKernelGGL((k_traverse8p<false, true>), dim3(gps), dim3(kBlock), lds, stream, A, d);
+        stop(slot_of(d, 1), stream);
+        if (fork) {
+            if ((e = hipEventRecord(fork_ev[2 * d], stream)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(aux, fork_ev[2 * d], 0)) != hipSuccess) return e;
+            shadow(d, aux);
+            if ((e = hipEventRecord(fork_ev[2 * d + 1], aux)) != hipSuccess) return e;
+            if (d + 1 <= L - 1) radiance(d + 1, stream);
+            if ((e = hipStreamWaitEvent(stream, fork_ev[2 * d + 1], 0)) != hipSuccess) return e;
         } else {
-            trace(-d);
+            shadow(d, stream);
         }
-        mark();
+        start(slot_of(d, 3), stream);
         hipLaunchKernelGGL(k_resolve, dim3(g), dim3(kBlock), 0, stream, A, d);
-        mark();
+        stop(slot_of(d, 3), stream);
     }
+    start(slot_of(L, 0), stream);
     hipLaunchKernelGGL(k_accumulate, dim3(g), dim3(kBlock), 0, stream, A);
-    mark();
+    stop(slot_of(L, 0), stream);
     return hipGetLastError();
 }
 

@@ -276,6 +276,10 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 #define DXRPT_OPT_SHADOW_OCCUPANCY 14u /* BVH8 any-hit register budget: 0 = compiler default, 7 or 8 (default) waves/SIMD */
 #define DXRPT_OPT_SHADOW_GRID 15u     /* any-hit kernel: grid-stride cap in 256-thread workgroups;
                                          0 = one thread per queued shadow ray (default) */
+#define DXRPT_OPT_CONCURRENCY 16u     /* 1 (default): each depth's any-hit pass runs on an internal stream
+                                         concurrently with the next closest-hit pass (joined before the
+                                         next shading pass); 0: one stream.  Per-kernel timing
+                                         (DXRPT_OPT_KERNEL_TIMING) always runs in order on one stream. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

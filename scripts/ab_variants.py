@@ -17,9 +17,10 @@ sys.path.insert(0, REPO)
 
 
 KEYS = {"w": "width", "m": "mode", "r": "refill", "k": "chunks", "p": "postpone", "b": "block", "o": "occ",
-        "s": "sblock", "q": "socc", "x": "spatial", "c": "leafcost", "h": "hocc", "g": "sgrid"}
+        "s": "sblock", "q": "socc", "x": "spatial", "c": "leafcost", "h": "hocc", "g": "sgrid",
+        "j": "conc"}
 DEFAULTS = {"width": 8, "mode": 0, "refill": 16, "chunks": 4, "postpone": 0, "block": 64, "occ": 7, "sblock": 256,
-            "socc": 0, "spatial": 150, "leafcost": 150, "hocc": 8, "sgrid": 0}
+            "socc": 0, "spatial": 150, "leafcost": 150, "hocc": 8, "sgrid": 0, "conc": 1}
 BUILD_KEYS = ("width", "spatial", "leafcost")  # a separate context (BVH) per combination
 
 
@@ -85,18 +86,24 @@ def main():
             t.set_option(A.OPT_OCCUPANCY, o["occ"])
             t.set_option(A.OPT_SHADOW_OCCUPANCY, o["hocc"])
             t.set_option(A.OPT_SHADOW_GRID, o["sgrid"])
+            t.set_option(A.OPT_CONCURRENCY, o["conc"])
             t.set_option(A.OPT_SHADE_BLOCK, o["sblock"])
             t.set_option(A.OPT_SHADE_OCCUPANCY, o["socc"])
             for f in range(3):
                 t.render_raw(consts[f], st, accum.data_ptr(), W, H, stream=sh, lights=lights)
             torch.cuda.synchronize()
-            t.set_option(A.OPT_KERNEL_TIMING, 1)
-            t.reset_timing()
+            # wall-clock pass without per-kernel timing (which serialises the concurrent passes)
             t0 = time.perf_counter()
             for f in range(args.frames):
                 t.render_raw(consts[f % 16], st, accum.data_ptr(), W, H, stream=sh, lights=lights)
             torch.cuda.synchronize()
             wall = (time.perf_counter() - t0) / args.frames * 1e3
+            # per-kernel breakdown pass
+            t.set_option(A.OPT_KERNEL_TIMING, 1)
+            t.reset_timing()
+            for f in range(args.frames):
+                t.render_raw(consts[f % 16], st, accum.data_ptr(), W, H, stream=sh, lights=lights)
+            torch.cuda.synchronize()
             s = t.stats()
             t.set_option(A.OPT_KERNEL_TIMING, 0)
             n = max(1, s.timed_frames)

@@ -226,6 +226,7 @@ def test_traversal_launch_options_are_bit_identical(torch_cuda, block, occ, sblo
     t.set_option(A.OPT_OCCUPANCY, occ)
     t.set_option(A.OPT_SHADOW_OCCUPANCY, 15 - occ if occ else 0)
     t.set_option(A.OPT_SHADOW_GRID, 0 if block == 256 else 512)  # grid-stride any-hit loop vs one ray per thread
+    t.set_option(A.OPT_CONCURRENCY, 0 if occ == 7 else 1)
     t.set_option(A.OPT_SHADE_BLOCK, sblock)
     t.set_option(A.OPT_SHADE_OCCUPANCY, socc)
     try:
@@ -237,6 +238,7 @@ def test_traversal_launch_options_are_bit_identical(torch_cuda, block, occ, sblo
         t.set_option(A.OPT_SHADE_OCCUPANCY, 0)
         t.set_option(A.OPT_SHADOW_OCCUPANCY, 8)
         t.set_option(A.OPT_SHADOW_GRID, 0)
+        t.set_option(A.OPT_CONCURRENCY, 1)
     np.testing.assert_array_equal(got, ref)
 
 
@@ -298,11 +300,13 @@ def test_stats_and_counting_option(torch_cuda):
     assert s2.node_visits_shadow > 0
 
 
-def test_kernel_timing_option(torch_cuda):
+@pytest.mark.parametrize("concurrency", [0, 1])
+def test_kernel_timing_option(torch_cuda, concurrency):
     torch = torch_cuda
     t = tracer("boxtest")
     sc, _ = scene_bundle("boxtest")
     st = sc.settings(MaxPathLength=3)
+    t.set_option(A.OPT_CONCURRENCY, concurrency)
     t.set_option(A.OPT_KERNEL_TIMING, 1)
     t.reset_timing()
     try:
@@ -311,10 +315,15 @@ def test_kernel_timing_option(torch_cuda):
         stt = t.stats()
     finally:
         t.set_option(A.OPT_KERNEL_TIMING, 0)
+        t.set_option(A.OPT_CONCURRENCY, 1)
     assert stt.timed_frames == 5
     assert stt.kernel_launches[A.K_TRACE] == 10 and stt.kernel_launches[A.K_RAYGEN] == 5
     assert all(stt.kernel_ms[k] > 0 for k in range(A.K_COUNT))
-    assert stt.frame_ms >= sum(stt.kernel_ms[k] for k in range(A.K_COUNT)) * 0.99
+    busy = sum(stt.kernel_ms[k] for k in range(A.K_COUNT))
+    if concurrency == 0:  # one stream: the frame spans every kernel
+        assert stt.frame_ms >= busy * 0.99
+    else:  # the any-hit passes overlap the next closest-hit passes
+        assert stt.frame_ms >= (busy - stt.kernel_ms[A.K_SHADOW]) * 0.99
 
 
 def test_errors_are_reported_not_raised(torch_cuda):
