@@ -762,13 +762,27 @@ struct Emit8 {
             }
         }
         for (int s = 0; s < 8; ++s)
-            if (child_node[s] >= 0) emit(uint32_t(child_node[s]), slot_of[s], depth + 1);
+            if (child_node[s] >= 0) pending.push_back({uint32_t(child_node[s]), slot_of[s], depth + 1});
     }
+
+    // Breadth-first emission: the wide nodes of each level are contiguous and the top levels come
+    // first, so a prefix of the node array is the top of the tree (the traversal kernels keep such a
+    // prefix in LDS, DXRPT_OPT_LDS_NODES).  A node's internal children stay contiguous.
+    struct Pending {
+        uint32_t idx;
+        int32_t t;
+        uint32_t depth;
+    };
+    std::vector<Pending> pending;
 
     void run() {
         solve();
         nodes.emplace_back();
-        emit(0, 0, 0);
+        pending.push_back({0u, 0, 0u});
+        for (size_t q = 0; q < pending.size(); ++q) {
+            const Pending p = pending[q];
+            emit(p.idx, p.t, p.depth);
+        }
     }
 };
 
@@ -848,7 +862,7 @@ bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildRe
             B.depth_cap = cap;
             if (!B.build(ntris, err, sah)) return false;
         }
-        Emit8 E{*tree, *refs, pad, {}, {}, 0, 0, 1.0, params ? params->leaf_cost : BvhBuildParams().leaf_cost, {}, {}, {}};
+        Emit8 E{*tree, *refs, pad, {}, {}, 0, 0, 1.0, params ? params->leaf_cost : BvhBuildParams().leaf_cost, {}, {}, {}, {}};
         E.run();
         last_depth = E.max_depth;
         if (E.max_depth > max_depth8) continue;

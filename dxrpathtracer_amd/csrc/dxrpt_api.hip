@@ -99,6 +99,9 @@ struct dxrpt_ctx {
     uint32_t opt_occupancy = 7;     // DXRPT_OPT_OCCUPANCY
     uint32_t opt_shadow_occ = 8;    // DXRPT_OPT_SHADOW_OCCUPANCY
     uint32_t opt_shadow_grid = 0;   // DXRPT_OPT_SHADOW_GRID
+    uint32_t opt_pipeline = 0;      // DXRPT_OPT_TRAVERSAL_PIPELINE
+    uint32_t opt_packet = 1;        // DXRPT_OPT_PACKET_TRAVERSAL
+    uint32_t opt_lds_nodes = 0;     // DXRPT_OPT_LDS_NODES
     uint32_t opt_concurrency = 1;   // DXRPT_OPT_CONCURRENCY
     hipStream_t aux = nullptr;      // any-hit pass stream (created on first use)
     std::vector<hipEvent_t> fork_ev;
@@ -186,6 +189,7 @@ SceneDev scene_dev(dxrpt_ctx* c, uint32_t traversal_threads) {
     s.width = c->built_width;
     const uint32_t entries = c->bvh.max_depth + 1u;
     if (c->built_width == 8) {
+        s.num_nodes = c->bvh.num_nodes;
         s.stack_ints = 2u * std::min<uint32_t>(entries, uint32_t(kStackLds8));
         if (entries > uint32_t(kStackLds8)) {
             c->d_spill.ensure(size_t(kTraversalStack8 - kStackLds8) * traversal_threads * sizeof(uint2));
@@ -400,6 +404,15 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_SHADOW_GRID) {
             require(value <= 1u << 20, "dxrpt_set_option: shadow grid cap too large");
             ctx->opt_shadow_grid = uint32_t(value);
+        } else if (option == DXRPT_OPT_TRAVERSAL_PIPELINE) {
+            require(value <= 3, "dxrpt_set_option: traversal pipeline must be 0..3");
+            ctx->opt_pipeline = uint32_t(value);
+        } else if (option == DXRPT_OPT_PACKET_TRAVERSAL) {
+            require(value <= 15, "dxrpt_set_option: packet traversal mask must be 0..15");
+            ctx->opt_packet = uint32_t(value);
+        } else if (option == DXRPT_OPT_LDS_NODES) {
+            require(value <= 1024, "dxrpt_set_option: LDS node cache must be 0..1024 nodes");
+            ctx->opt_lds_nodes = uint32_t(value);
         } else if (option == DXRPT_OPT_SHADE_BLOCK) {
             require(value == 64 || value == 128 || value == 256, "dxrpt_set_option: shade block must be 64, 128 or 256");
             ctx->opt_shade_block = uint32_t(value);
@@ -677,6 +690,9 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.occupancy = ctx->opt_occupancy;
         fp.shadow_occupancy = ctx->opt_shadow_occ;
         fp.shadow_grid = ctx->opt_shadow_grid;
+        fp.pipeline = ctx->opt_pipeline;
+        fp.packet = ctx->opt_packet;
+        fp.lds_nodes = ctx->opt_lds_nodes;
         fp.shade_block = ctx->opt_shade_block;
         fp.shade_occupancy = ctx->opt_shade_occ;
         hipStream_t s = static_cast<hipStream_t>(stream);

@@ -100,6 +100,7 @@ struct SceneDev {
     // BVH8 group-stack entries kStackLds8 .. kTraversalStack8-1: [entry * spill_stride + global thread]
     uint2* spill8 = nullptr;
     uint32_t spill_stride = 0;  // >= the global thread count of every BVH8 traversal launch
+    uint32_t num_nodes = 0;     // BVH8 nodes (bounds the LDS node cache)
 };
 
 struct FrameParams {
@@ -120,6 +121,9 @@ struct FrameParams {
     uint32_t shadow_occupancy;       // BVH8 any-hit kernel: 0 compiler default, 7 or 8 waves per SIMD
     uint32_t shadow_grid;            // any-hit kernel grid cap in 256-thread workgroups (0 = one thread per ray)
     uint32_t shade_block;            // workgroup size of k_shade (64..256)
+    uint32_t packet;                 // wave-coherent traversal: bit 0/1 closest/any hit at depth 1, bit 2/3 at depth >= 2
+    uint32_t lds_nodes;              // BVH8 per-lane traversal: top nodes kept in LDS per workgroup (0 = none)
+    uint32_t pipeline;               // BVH8 one-thread-per-ray traversal: bit 0 triangle pairs, bit 1 next-node prefetch
     uint32_t shade_occupancy;        // k_shade register budget: 0 compiler default, 6, 7 or 8 waves per SIMD
     uint32_t postpone_tris;          // wave-pool kernels: test pending triangles once this many lanes hold
                                      // some (0 = with their node visit)

@@ -203,12 +203,26 @@ struct HitRec {
 // One candidate triangle (the "intersection + any-hit" stage of a DXR traversal).  Returns true
 // when an any-hit ray is done (accepted occluder).  Closest hit: smallest t, ties -> smallest global
 // triangle id, which makes the result independent of traversal order.
-template <bool kAnyHit>
-PT_DEV bool test_triangle(const SceneDev& S, uint32_t rec, f3 o, f3 d, float tmin, float tmax, bool alpha, HitRec& h) {
+// A leaf-ordered triangle record: v0, e1, e2 as float4 (.w = global tri id / geometry / flags).
+struct TriRec {
+    float4 p0, p1, p2;
+};
+
+PT_DEV TriRec load_tri(const SceneDev& S, uint32_t rec) {
     const float4* T = reinterpret_cast<const float4*>(S.tris);
-    const float4 p0 = T[rec * 3 + 0];
-    const float4 p1 = T[rec * 3 + 1];
-    const float4 p2 = T[rec * 3 + 2];
+    return TriRec{T[rec * 3 + 0], T[rec * 3 + 1], T[rec * 3 + 2]};
+}
+
+// Keeps a loaded record in registers at this point: the compiler otherwise sinks the v0 load behind
+// the det != 0 branch, which costs a second dependent round trip per triangle.
+PT_DEV void pin_tri(const TriRec& r) {
+    asm volatile("" ::"v"(r.p0.x), "v"(r.p0.y), "v"(r.p0.z), "v"(r.p0.w), "v"(r.p1.x), "v"(r.p1.y), "v"(r.p1.z),
+                 "v"(r.p1.w), "v"(r.p2.x), "v"(r.p2.y), "v"(r.p2.z), "v"(r.p2.w));
+}
+
+template <bool kAnyHit>
+PT_DEV bool test_tri_rec(const SceneDev& S, const TriRec& r, f3 o, f3 d, float tmin, float tmax, bool alpha, HitRec& h) {
+    const float4 p0 = r.p0, p1 = r.p1, p2 = r.p2;
     float t, u, v;
     if (!intersect_triangle(o, d, ld3(p0), ld3(p1), ld3(p2), &t, &u, &v)) return false;
     const uint32_t gtri = fbits(p0.w);
@@ -226,6 +240,11 @@ PT_DEV bool test_triangle(const SceneDev& S, uint32_t rec, f3 o, f3 d, float tmi
     h.b2 = v;
     h.geom = geom;
     return kAnyHit;
+}
+
+template <bool kAnyHit>
+PT_DEV bool test_triangle(const SceneDev& S, uint32_t rec, f3 o, f3 d, float tmin, float tmax, bool alpha, HitRec& h) {
+    return test_tri_rec<kAnyHit>(S, load_tri(S, rec), o, d, tmin, tmax, alpha, h);
 }
 
 PT_DEV f3 safe_inverse(f3 d) {
@@ -341,23 +360,48 @@ PT_DEV uint2 stack8_load(const SceneDev& S, const int* stk, int j) {
     return S.spill8[size_t(j - kStackLds8) * S.spill_stride + blockIdx.x * blockDim.x + threadIdx.x];
 }
 
-template <bool kCount>
-PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp, int* stk, uint2& tos, const HitRec& h,
-                       uint32_t& tbase, uint32_t& tbits, uint32_t& nvisit) {
-    if (kCount) ++nvisit;
+// The 80-B node as five 16-B words (pt_layout.h Bvh8Node).
+struct Node8Words {
+    uint4 w0, w1, w2, w3, w4;
+};
+
+// The first `n` nodes (the top levels: the builder emits breadth first) copied to LDS by the
+// workgroup (node_cache_fill); visits there read LDS instead of issuing vector memory loads.
+struct NodeCache {
+    const uint4* lds;
+    uint32_t n;
+};
+
+PT_DEV Node8Words load_node8(const SceneDev& S, uint32_t node) {
     const uint4* N = reinterpret_cast<const uint4*>(S.nodes8);
-    const uint4 w0 = N[node * 5 + 0];
-    const uint4 w1 = N[node * 5 + 1];
-    const uint4 w2 = N[node * 5 + 2];
-    const uint4 w3 = N[node * 5 + 3];
-    const uint4 w4 = N[node * 5 + 4];
+    return Node8Words{N[node * 5 + 0], N[node * 5 + 1], N[node * 5 + 2], N[node * 5 + 3], N[node * 5 + 4]};
+}
+
+PT_DEV Node8Words load_node8(const SceneDev& S, const NodeCache& nc, uint32_t node) {
+    if (node < nc.n) {
+        const uint4* L = nc.lds;
+        return Node8Words{L[node * 5 + 0], L[node * 5 + 1], L[node * 5 + 2], L[node * 5 + 3], L[node * 5 + 4]};
+    }
+    return load_node8(S, node);
+}
+
+// Copies the top `n` nodes into `lds` (all threads of the workgroup; ends with a barrier).
+PT_DEV NodeCache node_cache_fill(const SceneDev& S, uint4* lds, uint32_t n) {
+    const uint4* N = reinterpret_cast<const uint4*>(S.nodes8);
+    for (uint32_t j = threadIdx.x; j < n * 5u; j += blockDim.x) lds[j] = N[j];
+    __syncthreads();
+    return NodeCache{lds, n};
+}
+
+// Slot mask of the node's children whose quantised box the ray enters within [tmin, tmx].
+PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx) {
+    const uint4 w0 = W.w0, w1 = W.w1, w2 = W.w2, w3 = W.w3, w4 = W.w4;
     const float ax = __uint_as_float((w0.w & 0xFFu) << 23) * R.inv.x;
     const float ay = __uint_as_float(((w0.w >> 8) & 0xFFu) << 23) * R.inv.y;
     const float az = __uint_as_float(((w0.w >> 16) & 0xFFu) << 23) * R.inv.z;
     const float bx = __builtin_fmaf(__uint_as_float(w0.x), R.inv.x, -R.ood.x);
     const float by = __builtin_fmaf(__uint_as_float(w0.y), R.inv.y, -R.ood.y);
     const float bz = __builtin_fmaf(__uint_as_float(w0.z), R.inv.z, -R.ood.z);
-    const float tmx = h.t;
     // Near/far quantised planes per axis chosen once per node from the ray octant (Ylitie et al. 2017,
     // sec. 3.2): with inv >= 0 the near plane of every child is qlo, else qhi, so this equals the
     // min/max of the two slab distances.  Words: w2 = (qlo_x 0-3, 4-7, qlo_y 0-3, 4-7),
@@ -381,6 +425,16 @@ PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp
         const uint32_t m = ((c < 4 ? w1.z : w1.w) >> sh) & 0xFFu;
         hm |= uint32_t(m != 0u && tn <= tf) << c;
     }
+    return hm;
+}
+
+// Node visit on already-loaded words (lets the caller issue the next node's loads early).
+template <bool kCount>
+PT_DEV bool trav8_node_w(const SceneDev& S, const Ray8& R, const Node8Words& W, uint32_t& node, int& sp, int* stk,
+                         uint2& tos, const HitRec& h, uint32_t& tbase, uint32_t& tbits, uint32_t& nvisit) {
+    if (kCount) ++nvisit;
+    const uint4 w0 = W.w0, w1 = W.w1;
+    const uint32_t hm = box8_hits(R, W, h.t);  // hit children, slot space
     const uint32_t imask = w0.w >> 24;
     // internal hits to key space (bit slot ^ oct): three conditional bit-group swaps
     uint32_t ihits = hm & imask;
@@ -421,6 +475,12 @@ PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp
     }
 }
 
+template <bool kCount>
+PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp, int* stk, uint2& tos, const HitRec& h,
+                       uint32_t& tbase, uint32_t& tbits, uint32_t& nvisit, const NodeCache& nc = NodeCache{nullptr, 0u}) {
+    return trav8_node_w<kCount>(S, R, load_node8(S, nc, node), node, sp, stk, tos, h, tbase, tbits, nvisit);
+}
+
 // Tests the pending triangle group.  Returns true when an any-hit ray found an occluder.
 template <bool kAnyHit, bool kCount>
 PT_DEV bool trav8_tris(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32_t tbits, HitRec& h, uint32_t& ntest) {
@@ -433,38 +493,198 @@ PT_DEV bool trav8_tris(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32_
     return false;
 }
 
+// Tests the pending group two records at a time: both records are loaded before either test, so a
+// lane pays one memory round trip per pair.  Tests still run in bit order (same results).
+template <bool kAnyHit, bool kCount>
+PT_DEV bool trav8_tris2(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32_t tbits, HitRec& h, uint32_t& ntest) {
+    while (tbits) {
+        const uint32_t b0 = uint32_t(__builtin_ctz(tbits));
+        tbits &= tbits - 1u;
+        const bool two = tbits != 0u;
+        const uint32_t b1 = two ? uint32_t(__builtin_ctz(tbits)) : b0;
+        tbits &= tbits - 1u;
+        const TriRec ra = load_tri(S, tbase + b0);
+        const TriRec rb = load_tri(S, tbase + b1);
+        pin_tri(ra);
+        pin_tri(rb);
+        if (kCount) ntest += two ? 2u : 1u;
+        if (test_tri_rec<kAnyHit>(S, ra, R.o, R.d, R.tmin, R.tmax, R.alpha, h)) return true;
+        if (two && test_tri_rec<kAnyHit>(S, rb, R.o, R.d, R.tmin, R.tmax, R.alpha, h)) return true;
+    }
+    return false;
+}
+
+// Traversal with the memory round trips overlapped (kPipe bit 0: triangle pairs, bit 1: the next
+// node's words are loaded right after its address is known, before the current node's triangle
+// tests).  Visit order, tests and results are those of traverse8.
+template <bool kAnyHit, bool kCount, int kPipe>
+PT_DEV bool traverse8_pipe(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, int* stk, HitRec& h,
+                           uint32_t& nvisit, uint32_t& ntest, const NodeCache& nc) {
+    Ray8 R;
+    ray8_init(R, o, d, tmin, tmax, alpha, h);
+    uint32_t node = 0;
+    int sp = 0;
+    uint2 tos = make_uint2(0u, 0u);
+    Node8Words w = load_node8(S, nc, 0);
+    while (true) {
+        uint32_t tbase = 0, tbits = 0;
+        const bool more = trav8_node_w<kCount>(S, R, w, node, sp, stk, tos, h, tbase, tbits, nvisit);
+        if (kPipe & 2) w = load_node8(S, nc, node);
+        if (tbits) {
+            const bool done = (kPipe & 1) ? trav8_tris2<kAnyHit, kCount>(S, R, tbase, tbits, h, ntest)
+                                          : trav8_tris<kAnyHit, kCount>(S, R, tbase, tbits, h, ntest);
+            if (done) return true;
+        }
+        if (!more) break;
+        if (!(kPipe & 2)) w = load_node8(S, nc, node);
+    }
+    return h.tri != kMiss;
+}
+
+// ---- wave-coherent ("packet") BVH8 traversal ------------------------------------------------------
+// The 64 rays of a wave walk ONE node sequence: a child is entered when any live lane's ray enters its
+// box (each lane tests with its own ray and its own closest t), leaf triangles hit by any lane are
+// tested by every live lane.  Node and triangle addresses are therefore wave-uniform and are fetched
+// with scalar loads (constant address space -> s_load through the scalar cache), so the traversal
+// issues no vector memory instructions at all; the vector memory pipeline (TA/TD), which bounds the
+// per-lane traversal, is left to the shading passes.  The group stack is wave-uniform too: entry j
+// lives in lane j of two VGPRs (push = v_cndmask, pop = v_readlane), no LDS.
+// Each lane tests a superset of the leaves its own traversal would test, and closest hit is the
+// minimum (t, triangle id) over tested triangles while any-hit is a boolean over them, so the results
+// are those of traverse8 bit for bit.  Pays off for coherent rays (primary rays of an 8x8 pixel block,
+// their sun shadow rays); incoherent rays visit the union of their paths.
+typedef unsigned int U32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(4))) const U32x4 ConstU4;
+
+PT_DEV uint4 u4(U32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
+PT_DEV float4 f4(U32x4 v) {
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+
+PT_DEV Node8Words load_node8_uniform(const SceneDev& S, uint32_t node) {
+    ConstU4* N = (ConstU4*)(S.nodes8);  // NOLINT: generic -> constant address space
+    const uint32_t b = node * 5u;
+    return Node8Words{u4(N[b + 0]), u4(N[b + 1]), u4(N[b + 2]), u4(N[b + 3]), u4(N[b + 4])};
+}
+
+PT_DEV TriRec load_tri_uniform(const SceneDev& S, uint32_t rec) {
+    ConstU4* T = (ConstU4*)(S.tris);  // NOLINT
+    const uint32_t b = rec * 3u;
+    return TriRec{f4(T[b + 0]), f4(T[b + 1]), f4(T[b + 2])};
+}
+
+PT_DEV uint32_t wave_or8(uint32_t m) {
+    uint32_t u = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) u |= uint32_t(__ballot((m >> c) & 1u) != 0ull) << c;
+    return u;
+}
+
+// `live`: this lane holds a ray (lanes past the end of the queue join with live = false).  Returns
+// this lane's result like traverse8 (h.tri != kMiss: hit / occluded).
+template <bool kAnyHit>
+PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, bool live, HitRec& h) {
+    Ray8 R;
+    ray8_init(R, o, d, tmin, tmax, alpha, h);
+    unsigned long long lv = __ballot(live);
+    if (lv == 0ull) return false;
+    // key order of the first live lane's octant for the whole wave (any order gives the same results)
+    const uint32_t oct = uint32_t(__builtin_amdgcn_readlane(int(R.oct), __ffsll(static_cast<long long>(lv)) - 1));
+    const uint32_t lane = uint32_t(__lane_id());
+    uint32_t sbase = 0, sword = 0;  // stack entry j in lane j
+    uint32_t sp = 0;
+    uint32_t node = 0;
+    while (true) {
+        const Node8Words W = load_node8_uniform(S, node);
+        const uint32_t hm = live ? box8_hits(R, W, h.t) : 0u;
+        const uint32_t um = wave_or8(hm);
+        const uint32_t imask = W.w0.w >> 24;
+        // leaf triangles hit by any lane: (count << 5) | offset per leaf slot
+        uint32_t tbits = 0;
+        uint32_t lh = um & ~imask;
+        const unsigned long long meta = (static_cast<unsigned long long>(W.w1.w) << 32) | W.w1.z;
+        while (lh) {
+            const uint32_t c = uint32_t(__builtin_ctz(lh));
+            lh &= lh - 1u;
+            const uint32_t m = uint32_t(meta >> (8u * c)) & 0xFFu;
+            tbits |= ((1u << (m >> 5)) - 1u) << (m & 31u);
+        }
+        const uint32_t tbase = W.w1.y;
+        while (tbits) {
+            const uint32_t b = uint32_t(__builtin_ctz(tbits));
+            tbits &= tbits - 1u;
+            const TriRec r = load_tri_uniform(S, tbase + b);
+            if (live && test_tri_rec<kAnyHit>(S, r, R.o, R.d, R.tmin, R.tmax, R.alpha, h)) live = false;  // occluded
+        }
+        if (kAnyHit && __ballot(live) == 0ull) break;
+        uint32_t ihits = um & imask;
+        if (oct & 1u) ihits = ((ihits & 0x55u) << 1) | ((ihits >> 1) & 0x55u);
+        if (oct & 2u) ihits = ((ihits & 0x33u) << 2) | ((ihits >> 2) & 0x33u);
+        if (oct & 4u) ihits = ((ihits & 0x0Fu) << 4) | ((ihits >> 4) & 0x0Fu);
+        uint32_t gbase = W.w1.x;
+        uint32_t gword = (ihits << 24) | imask;
+        bool found = false;
+        while (true) {
+            if (gword >> 24) {
+                const uint32_t k = 31u - uint32_t(__builtin_clz(gword));
+                gword &= ~(1u << k);
+                const uint32_t slot = (k - 24u) ^ oct;
+                node = gbase + uint32_t(__builtin_popcount(gword & 0xFFu & ((1u << slot) - 1u)));
+                if (gword >> 24) {  // push the rest of the group
+                    if (lane == sp) {
+                        sbase = gbase;
+                        sword = gword;
+                    }
+                    ++sp;
+                }
+                found = true;
+                break;
+            }
+            if (sp == 0u) break;
+            --sp;
+            gbase = uint32_t(__builtin_amdgcn_readlane(int(sbase), int(sp)));
+            gword = uint32_t(__builtin_amdgcn_readlane(int(sword), int(sp)));
+        }
+        if (!found) break;
+    }
+    return h.tri != kMiss;
+}
+
 // One node visit and its triangles.  Returns true when the ray is finished: h.tri != kMiss means hit
 // (closest) / occluded (any-hit).
 template <bool kAnyHit, bool kCount>
 PT_DEV bool trav8_step(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp, int* stk, uint2& tos, HitRec& h,
-                       uint32_t& nvisit, uint32_t& ntest) {
+                       uint32_t& nvisit, uint32_t& ntest, const NodeCache& nc) {
     uint32_t tbase = 0, tbits = 0;
-    const bool more = trav8_node<kCount>(S, R, node, sp, stk, tos, h, tbase, tbits, nvisit);
+    const bool more = trav8_node<kCount>(S, R, node, sp, stk, tos, h, tbase, tbits, nvisit, nc);
     if (tbits && trav8_tris<kAnyHit, kCount>(S, R, tbase, tbits, h, ntest)) return true;
     return !more;
 }
 
 template <bool kAnyHit, bool kCount>
 PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, int* stk, HitRec& h,
-                      uint32_t& nvisit, uint32_t& ntest) {
+                      uint32_t& nvisit, uint32_t& ntest, const NodeCache& nc) {
     Ray8 R;
     ray8_init(R, o, d, tmin, tmax, alpha, h);
     uint32_t node = 0;
     int sp = 0;
     uint2 tos = make_uint2(0u, 0u);
-    while (!trav8_step<kAnyHit, kCount>(S, R, node, sp, stk, tos, h, nvisit, ntest)) {
+    while (!trav8_step<kAnyHit, kCount>(S, R, node, sp, stk, tos, h, nvisit, ntest, nc)) {
     }
     return h.tri != kMiss;
 }
 
-template <int W, bool kAnyHit, bool kCount>
+template <int W, bool kAnyHit, bool kCount, int kPipe = 0>
 PT_DEV bool traverse(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, int* stk, HitRec& h,
-                     uint32_t& nvisit, uint32_t& ntest) {
+                     uint32_t& nvisit, uint32_t& ntest, const NodeCache& nc = NodeCache{nullptr, 0u}) {
     h.t = tmax;
     h.tri = kMiss;
     h.b1 = h.b2 = 0.0f;
     h.geom = 0;
-    if (W == 8) return traverse8<kAnyHit, kCount>(S, o, d, tmin, tmax, alpha, stk, h, nvisit, ntest);
+    if (W == 8) {
+        if (kPipe) return traverse8_pipe<kAnyHit, kCount, kPipe>(S, o, d, tmin, tmax, alpha, stk, h, nvisit, ntest, nc);
+        return traverse8<kAnyHit, kCount>(S, o, d, tmin, tmax, alpha, stk, h, nvisit, ntest, nc);
+    }
     return traverse2<kAnyHit, kCount>(S, o, d, tmin, tmax, alpha, stk, h, nvisit, ntest);
 }
 
@@ -586,10 +806,13 @@ __global__ __launch_bounds__(kBlock) void k_raygen(KArgs A) {
 
 // kOcc > 0 asks the compiler for kOcc resident waves per SIMD (register budget 512 / kOcc).
 // Workgroups of 64..256 threads (FrameParams::trace_block).
-template <bool kCount, int W, int kOcc>
+template <bool kCount, int W, int kOcc, int kPipe = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
 void k_trace(KArgs A, int depth) {
-    extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved (launch_lds_bytes)
+    extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved, then the node cache
+    NodeCache nc{nullptr, 0u};
+    if (W == 8 && !kCount && A.P.lds_nodes)
+        nc = node_cache_fill(A.S, reinterpret_cast<uint4*>(stack + A.S.stack_ints * blockDim.x), A.P.lds_nodes);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t* cnt = radiance_counts(A.F, depth);
     if (i >= queue_total(cnt)) return;
@@ -602,7 +825,7 @@ void k_trace(KArgs A, int depth) {
     const bool alpha = depth <= A.P.set.MaxAnyHitPathLength;
     HitRec h;
     uint32_t nv = 0, nt = 0;
-    traverse<W, false, kCount>(A.S, ld3(o4), ld3(d4), tmin, o4.w, alpha, stack + threadIdx.x, h, nv, nt);
+    traverse<W, false, kCount, kPipe>(A.S, ld3(o4), ld3(d4), tmin, o4.w, alpha, stack + threadIdx.x, h, nv, nt, nc);
     A.F.hit[pos] = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
     if (kCount) {
         atomicAdd(&A.P.trav[0], (unsigned long long)nv);
@@ -840,10 +1063,13 @@ void k_shade(KArgs A, int depth) {
 
 // ShadowHitShader / ShadowMissShader / ShadowAnyHitShader (RayTrace.hlsl:497-507, 532-542):
 // one thread per queued shadow ray (grid-stride); occluded -> contribution * 0 (keeps NaN/Inf).
-template <bool kCount, int W, int kOcc>
+template <bool kCount, int W, int kOcc, int kPipe = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
 void k_shadow(KArgs A, int depth) {
-    extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved (launch_lds_bytes)
+    extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved, then the node cache
+    NodeCache nc{nullptr, 0u};
+    if (W == 8 && !kCount && A.P.lds_nodes)
+        nc = node_cache_fill(A.S, reinterpret_cast<uint4*>(stack + A.S.stack_ints * blockDim.x), A.P.lds_nodes);
     const uint32_t* cnt = shadow_counts(A.F, depth);
     const uint32_t count = queue_total(cnt);
     const uint32_t cap_s = A.F.shadow_slots * A.F.cap_r;
@@ -855,13 +1081,57 @@ void k_shadow(KArgs A, int depth) {
         const float4 c4 = A.F.sh_con[slot];
         HitRec h;
         const bool occluded =
-            traverse<W, true, kCount>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stack + threadIdx.x, h, nv, nt);
+            traverse<W, true, kCount, kPipe>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stack + threadIdx.x, h, nv, nt, nc);
         if (occluded) A.F.sh_con[slot] = make_float4(c4.x * 0.0f, c4.y * 0.0f, c4.z * 0.0f, c4.w);
     }
     if (kCount) {
         atomicAdd(&A.P.trav[2], (unsigned long long)nv);
         atomicAdd(&A.P.trav[3], (unsigned long long)nt);
     }
+}
+
+// Packet variants of k_trace / k_shadow (traverse8_packet): one item per lane, whole waves exit
+// past the end of the queue, the rest run with live = false on the surplus lanes.
+template <int kOcc>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
+void k_trace_packet(KArgs A, int depth) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t* cnt = radiance_counts(A.F, depth);
+    const uint32_t n = queue_total(cnt);
+    if ((i & ~63u) >= n) return;
+    const bool live = i < n;
+    const uint32_t pos = live ? queue_pos(cnt, A.F.cap_r, i) : 0u;
+    float4 o4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d4 = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
+    if (live) {
+        o4 = A.F.q[depth & 1].org[pos];
+        d4 = A.F.q[depth & 1].dir[pos];
+    }
+    const float tmin = depth == 1 ? 0.0f : kRayTMin;
+    const bool alpha = depth <= A.P.set.MaxAnyHitPathLength;
+    HitRec h;
+    traverse8_packet<false>(A.S, ld3(o4), ld3(d4), tmin, o4.w, alpha, live, h);
+    if (live) A.F.hit[pos] = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
+}
+
+template <int kOcc>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
+void k_shadow_packet(KArgs A, int depth) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t* cnt = shadow_counts(A.F, depth);
+    const uint32_t n = queue_total(cnt);
+    if ((i & ~63u) >= n) return;
+    const bool live = i < n;
+    const uint32_t cap_s = A.F.shadow_slots * A.F.cap_r;
+    const uint32_t slot = live ? A.F.sh_queue[queue_pos(cnt, cap_s, i)] : 0u;
+    float4 o4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d4 = make_float4(0.0f, 0.0f, 1.0f, 0.0f), c4 = o4;
+    if (live) {
+        o4 = A.F.sh_org[slot];
+        d4 = A.F.sh_dir[slot];
+        c4 = A.F.sh_con[slot];
+    }
+    HitRec h;
+    const bool occluded = traverse8_packet<true>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live, h);
+    if (live && occluded) A.F.sh_con[slot] = make_float4(c4.x * 0.0f, c4.y * 0.0f, c4.z * 0.0f, c4.w);
 }
 
 // Adds the visibility-weighted shadow contributions of each depth-d vertex, in slot order, to the
@@ -1051,6 +1321,7 @@ uint32_t trace_rays_threads(uint32_t n) { return grid_for(n) * kBlock; }
 hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream,
                         hipEvent_t* ev, hipStream_t aux, hipEvent_t* fork_ev) {
     KArgs A{scene, fb, fp};
+    A.P.lds_nodes = scene.width == 8 ? std::min(fp.lds_nodes, scene.num_nodes) : 0u;
     const uint32_t g = grid_for(fp.num_paths);
     const size_t lds = size_t(scene.stack_ints) * kBlock * sizeof(int);
     const bool count = fp.trav != nullptr;
@@ -1076,28 +1347,53 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
     const uint32_t gst_full = (fp.num_paths * fb.shadow_slots + tb - 1u) / tb;
     const uint32_t gst = fp.shadow_grid ? std::min<uint32_t>(gst_full, fp.shadow_grid * (kBlock / tb)) : gst_full;
     const size_t ldst = size_t(scene.stack_ints) * tb * sizeof(int);
+    const size_t ldsc = ldst + size_t(A.P.lds_nodes) * 80u;  // + the node cache (uncounted BVH8 kernels)
     const bool w8 = scene.width == 8;
     const bool pers = w8 && fp.chunks_per_wave > 0;
     const uint32_t gp = pers ? pool_grid(fp.num_paths, fp.chunks_per_wave) : 0u;
     const uint32_t gps = pers ? pool_grid(fp.num_paths * fb.shadow_slots, fp.chunks_per_wave) : 0u;
     // one-thread-per-ray traversal kernels: <count, width, occupancy>
     auto trace = [&](int d, hipStream_t st) {
-#define DXRPT_LAUNCH(K, C, W, O, G) hipLaunchKernelGGL((K<C, W, O>), dim3(G), dim3(tb), ldst, st, A, d)
+#define DXRPT_LAUNCH(K, C, W, O, GG) hipLaunchKernelGGL((K<C, W, O>), dim3(GG), dim3(tb), ldst, st, A, d)
+#define DXRPT_LAUNCH_P(K, O, GG)                                                                              \
+    switch (fp.pipeline) {                                                                                 \
+        case 1: hipLaunchKernelGGL((K<false, 8, O, 1>), dim3(GG), dim3(tb), ldsc, st, A, d); break;         \
+        case 2: hipLaunchKernelGGL((K<false, 8, O, 2>), dim3(GG), dim3(tb), ldsc, st, A, d); break;         \
+        case 3: hipLaunchKernelGGL((K<false, 8, O, 3>), dim3(GG), dim3(tb), ldsc, st, A, d); break;         \
+        default: hipLaunchKernelGGL((K<false, 8, O, 0>), dim3(GG), dim3(tb), ldsc, st, A, d); break;        \
+    }
         const bool shadow = d < 0;
         d = shadow ? -d : d;
-        const uint32_t G = shadow ? gst : gt;
+        const uint32_t G = shadow ? gst_full : gt;
+        // packet traversal: bit 0 closest hit at depth 1, bit 1 any hit at depth 1, bits 2/3 deeper
+        const uint32_t pbit = (shadow ? 2u : 1u) << (d == 1 ? 0 : 2);
+        if (w8 && !count && (fp.packet & pbit)) {
+            const uint32_t occ = shadow ? fp.shadow_occupancy : fp.occupancy;
+            if (shadow) {
+                if (occ == 7) hipLaunchKernelGGL((k_shadow_packet<7>), dim3(G), dim3(tb), 0, st, A, d);
+                else if (occ == 8) hipLaunchKernelGGL((k_shadow_packet<8>), dim3(G), dim3(tb), 0, st, A, d);
+                else hipLaunchKernelGGL((k_shadow_packet<0>), dim3(G), dim3(tb), 0, st, A, d);
+            } else {
+                if (occ == 7) hipLaunchKernelGGL((k_trace_packet<7>), dim3(G), dim3(tb), 0, st, A, d);
+                else if (occ == 8) hipLaunchKernelGGL((k_trace_packet<8>), dim3(G), dim3(tb), 0, st, A, d);
+                else hipLaunchKernelGGL((k_trace_packet<0>), dim3(G), dim3(tb), 0, st, A, d);
+            }
+            return;
+        }
+        const uint32_t G2 = shadow ? gst : gt;
         if (!w8) {
-            if (shadow) { if (count) DXRPT_LAUNCH(k_shadow, true, 2, 0, G); else DXRPT_LAUNCH(k_shadow, false, 2, 0, G); }
-            else { if (count) DXRPT_LAUNCH(k_trace, true, 2, 0, G); else DXRPT_LAUNCH(k_trace, false, 2, 0, G); }
+            if (shadow) { if (count) DXRPT_LAUNCH(k_shadow, true, 2, 0, G2); else DXRPT_LAUNCH(k_shadow, false, 2, 0, G2); }
+            else { if (count) DXRPT_LAUNCH(k_trace, true, 2, 0, G2); else DXRPT_LAUNCH(k_trace, false, 2, 0, G2); }
         } else if (count) {
-            if (shadow) DXRPT_LAUNCH(k_shadow, true, 8, 0, G); else DXRPT_LAUNCH(k_trace, true, 8, 0, G);
+            if (shadow) DXRPT_LAUNCH(k_shadow, true, 8, 0, G2); else DXRPT_LAUNCH(k_trace, true, 8, 0, G2);
         } else {
             const uint32_t occ = shadow ? fp.shadow_occupancy : fp.occupancy;
-            if (occ == 7) { if (shadow) DXRPT_LAUNCH(k_shadow, false, 8, 7, G); else DXRPT_LAUNCH(k_trace, false, 8, 7, G); }
-            else if (occ == 8) { if (shadow) DXRPT_LAUNCH(k_shadow, false, 8, 8, G); else DXRPT_LAUNCH(k_trace, false, 8, 8, G); }
-            else { if (shadow) DXRPT_LAUNCH(k_shadow, false, 8, 0, G); else DXRPT_LAUNCH(k_trace, false, 8, 0, G); }
+            if (occ == 7) { if (shadow) DXRPT_LAUNCH_P(k_shadow, 7, G2) else DXRPT_LAUNCH_P(k_trace, 7, G2) }
+            else if (occ == 8) { if (shadow) DXRPT_LAUNCH_P(k_shadow, 8, G2) else DXRPT_LAUNCH_P(k_trace, 8, G2) }
+            else { if (shadow) DXRPT_LAUNCH_P(k_shadow, 0, G2) else DXRPT_LAUNCH_P(k_trace, 0, G2) }
         }
 #undef DXRPT_LAUNCH
+#undef DXRPT_LAUNCH_P
     };
     auto radiance = [&](int d, hipStream_t st) {
         start(slot_of(d, 0), st);

@@ -280,6 +280,16 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                          concurrently with the next closest-hit pass (joined before the
                                          next shading pass); 0: one stream.  Per-kernel timing
                                          (DXRPT_OPT_KERNEL_TIMING) always runs in order on one stream. */
+#define DXRPT_OPT_TRAVERSAL_PIPELINE 17u /* BVH8 one-thread-per-ray traversal: bit 0 = load leaf triangles two at a
+                                            time, bit 1 = load the next node before the current node's triangle
+                                            tests (default 0).  Results are identical for every value. */
+#define DXRPT_OPT_PACKET_TRAVERSAL 18u /* BVH8 wave-coherent traversal (the 64 rays of a wave share one node
+                                          sequence fetched with scalar loads) per pass, bit mask: 1 = closest
+                                          hit at depth 1 (primary rays), 2 = any hit at depth 1, 4 = closest
+                                          hit at depth >= 2, 8 = any hit at depth >= 2.  Identical results. */
+#define DXRPT_OPT_LDS_NODES 19u       /* BVH8 per-lane traversal: each workgroup copies the top this-many nodes
+                                         (breadth-first prefix of the tree, 80 B each) into LDS and visits them
+                                         there (0..1024, default 0).  Identical results. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);
