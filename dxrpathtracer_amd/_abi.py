@@ -124,7 +124,10 @@ DXRPT_SYMBOLS = ("dxrpt_abi_version", "dxrpt_default_settings", "dxrpt_create", 
                  "dxrpt_render", "dxrpt_get_stats", "dxrpt_trace_rays", "dxrpt_set_option", "dxrpt_reset_timing")
 DXRPT_HOST_SYMBOLS = ("dxrpt_host_scene_create", "dxrpt_host_scene_destroy", "dxrpt_host_last_error",
                       "dxrpt_host_inv_view_projection", "dxrpt_host_sky_create", "dxrpt_host_fill_constants",
-                      "dxrpt_host_float_to_half", "dxrpt_host_half_to_float")
+                      "dxrpt_host_float_to_half", "dxrpt_host_half_to_float", "dxrpt_host_hosek_load",
+                      "dxrpt_host_hosek_destroy", "dxrpt_host_hosek_last_error", "dxrpt_host_sky_create_hosek",
+                      "dxrpt_host_hosek_rgb_radiance", "dxrpt_host_hosek_solar_radiance", "dxrpt_host_spectrum_to_rgb",
+                      "dxrpt_host_spectrum_from_rgb_reflectance")
 
 _lib = None
 _host = None
@@ -189,6 +192,21 @@ def host() -> C.CDLL:
         H.dxrpt_host_float_to_half.restype = C.c_uint16
         H.dxrpt_host_half_to_float.argtypes = [C.c_uint16]
         H.dxrpt_host_half_to_float.restype = f32
+        H.dxrpt_host_hosek_load.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(P)]
+        H.dxrpt_host_hosek_destroy.argtypes = [P]
+        H.dxrpt_host_hosek_destroy.restype = None
+        H.dxrpt_host_hosek_last_error.restype = C.c_char_p
+        H.dxrpt_host_sky_create_hosek.argtypes = [P, C.POINTER(f32), f32, f32, C.POINTER(f32), u32, P, C.POINTER(f32),
+                                                  C.POINTER(f32)]
+        d = C.c_double
+        H.dxrpt_host_hosek_rgb_radiance.argtypes = [P, d, d, d, d, d, C.c_int]
+        H.dxrpt_host_hosek_rgb_radiance.restype = d
+        H.dxrpt_host_hosek_solar_radiance.argtypes = [P, d, d, d, d, d, d]
+        H.dxrpt_host_hosek_solar_radiance.restype = d
+        H.dxrpt_host_spectrum_to_rgb.argtypes = [P, C.POINTER(f32), C.POINTER(f32)]
+        H.dxrpt_host_spectrum_to_rgb.restype = None
+        H.dxrpt_host_spectrum_from_rgb_reflectance.argtypes = [P, C.POINTER(f32), C.POINTER(f32)]
+        H.dxrpt_host_spectrum_from_rgb_reflectance.restype = None
         _host = H
     return _host
 

@@ -107,19 +107,100 @@ class Sky:
     res: int
     sun_irradiance: tuple
     sun_render_color: tuple
+    model: str = "analytic"
+
+
+class HosekData:
+    """The Hosek-Wilkie datasets (dxrpt_host_hosek_load): `hosek_dir` holds the reference's
+    ArHosekSkyModelData_RGB.h / _Spectral.h, `spectrum_source` is its Graphics/Spectrum.cpp."""
+
+    def __init__(self, hosek_dir: str, spectrum_source: str):
+        H = A.host()
+        self._p = C.c_void_p()
+        if H.dxrpt_host_hosek_load(hosek_dir.encode(), spectrum_source.encode(), C.byref(self._p)) != 0:
+            raise RuntimeError(H.dxrpt_host_hosek_last_error().decode())
+
+    @property
+    def handle(self):
+        return self._p
+
+    def rgb_radiance(self, turbidity, albedo, elevation, theta, gamma, channel):
+        return A.host().dxrpt_host_hosek_rgb_radiance(self._p, turbidity, albedo, elevation, theta, gamma, channel)
+
+    def solar_radiance(self, solar_elevation, turbidity, albedo, theta, gamma, wavelength):
+        return A.host().dxrpt_host_hosek_solar_radiance(self._p, solar_elevation, turbidity, albedo, theta, gamma,
+                                                        wavelength)
+
+    def spectrum_to_rgb(self, spectrum):
+        sp = (C.c_float * 60)(*spectrum)
+        out = (C.c_float * 3)()
+        A.host().dxrpt_host_spectrum_to_rgb(self._p, sp, out)
+        return tuple(out)
+
+    def spectrum_from_rgb(self, rgb):
+        out = (C.c_float * 60)()
+        A.host().dxrpt_host_spectrum_from_rgb_reflectance(self._p, (C.c_float * 3)(*rgb), out)
+        return list(out)
+
+    def __del__(self):
+        if getattr(self, "_p", None):
+            A.host().dxrpt_host_hosek_destroy(self._p)
+            self._p = None
+
+
+def hosek_dataset_paths():
+    """Where the Hosek-Wilkie datasets are: $DXRPT_HOSEK_DIR / $DXRPT_SPECTRUM_SOURCE, else the
+    reference checkout's SampleFramework12/v1.02 ($DXRPT_REFERENCE_ROOT, default /root/reference).
+    None when they are not readable (then make_sky falls back to the analytic sky)."""
+    import os
+    root = os.path.join(os.environ.get("DXRPT_REFERENCE_ROOT", "/root/reference"), "SampleFramework12", "v1.02")
+    hd = os.environ.get("DXRPT_HOSEK_DIR", os.path.join(root, "HosekSky"))
+    sp = os.environ.get("DXRPT_SPECTRUM_SOURCE", os.path.join(root, "Graphics", "Spectrum.cpp"))
+    ok = all(os.path.isfile(p) for p in (os.path.join(hd, "ArHosekSkyModelData_RGB.h"),
+                                          os.path.join(hd, "ArHosekSkyModelData_Spectral.h"), sp))
+    return (hd, sp) if ok else None
+
+
+_HOSEK = {}
+
+
+def load_hosek():
+    """The process-wide HosekData, or None when the datasets are not available."""
+    paths = hosek_dataset_paths()
+    if paths is None:
+        return None
+    if paths not in _HOSEK:
+        _HOSEK[paths] = HosekData(*paths)
+    return _HOSEK[paths]
 
 
 def make_sky(settings: A.AppSettings, turbidity: float = DEFAULT_TURBIDITY,
-             ground_albedo=DEFAULT_GROUND_ALBEDO, res: int = SKY_RES) -> Sky:
+             ground_albedo=DEFAULT_GROUND_ALBEDO, res: int = SKY_RES, model: str = "auto") -> Sky:
+    """SkyCache::Init.  model: "hosek" (the reference's Hosek-Wilkie sky, needs the datasets),
+    "analytic" (Preetham proxy), "auto" (hosek when the datasets are available)."""
     cube = np.zeros(6 * res * res * 4, dtype=np.uint16)
     irr = (C.c_float * 3)()
     ren = (C.c_float * 3)()
     sun = (C.c_float * 3)(*settings.SunDirection)
     alb = (C.c_float * 3)(*ground_albedo)
-    rc = A.host().dxrpt_host_sky_create(sun, settings.SunSize, turbidity, alb, res, cube.ctypes.data, irr, ren)
+    data = None
+    if model in ("auto", "hosek"):
+        data = load_hosek()
+        if data is None and model == "hosek":
+            raise RuntimeError("Hosek-Wilkie datasets not found (set DXRPT_HOSEK_DIR / DXRPT_SPECTRUM_SOURCE)")
+    elif model != "analytic":
+        raise ValueError(f"unknown sky model {model!r}")
+    H = A.host()
+    if data is not None:
+        rc = H.dxrpt_host_sky_create_hosek(data.handle, sun, settings.SunSize, turbidity, alb, res, cube.ctypes.data,
+                                           irr, ren)
+        if rc != 0:
+            raise RuntimeError(H.dxrpt_host_hosek_last_error().decode())
+        return Sky(cube, res, tuple(irr), tuple(ren), "hosek")
+    rc = H.dxrpt_host_sky_create(sun, settings.SunSize, turbidity, alb, res, cube.ctypes.data, irr, ren)
     if rc != 0:
         raise RuntimeError("dxrpt_host_sky_create failed")
-    return Sky(cube, res, tuple(irr), tuple(ren))
+    return Sky(cube, res, tuple(irr), tuple(ren), "analytic")
 
 
 def make_constants(scene: Scene, settings: A.AppSettings, sky: Sky, width: int, height: int,

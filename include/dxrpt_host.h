@@ -73,11 +73,37 @@ void dxrpt_host_inv_view_projection(const float position[3], float xrot, float y
                                     float nearz, float farz, float out_inv_view_projection[16]);
 
 /* SkyCache::Init: a res x res x 6 RGBA16F sky cube (sun excluded) + sun irradiance/render colour,
- * all pre-scaled by FP16Scale = 2^-10.  Sky model: Preetham-Shirley-Smits analytic sky (a documented
- * proxy for the Hosek-Wilkie tables of the reference).  out_cube holds res*res*6*4 halfs. */
+ * all pre-scaled by FP16Scale = 2^-10.  Sky model: Preetham-Shirley-Smits analytic sky, the fallback
+ * when the Hosek-Wilkie datasets are not available (dxrpt_host_sky_create_hosek is the reference's
+ * model).  out_cube holds res*res*6*4 halfs. */
 int dxrpt_host_sky_create(const float sun_direction[3], float sun_size_deg, float turbidity,
                           const float ground_albedo[3], uint32_t res, uint16_t* out_cube,
                           float out_sun_irradiance[3], float out_sun_render_color[3]);
+
+/* ---- Hosek-Wilkie sky (the reference's sky model) ----------------------------------------------
+ * SkyCache::Init (Graphics/Skybox.cpp:48-215, Sample 252-270) with the Hosek-Wilkie RGB sky
+ * (HosekSky/ArHosekSkyModel.cpp:604-652) and the spectral solar disc (:310-345, 521-566, 658-818)
+ * converted to RGB through the pbrt SampledSpectrum helpers (Graphics/Spectrum.{h,cpp}).  The model
+ * coefficient tables and the CIE / RGB-to-spectrum tables are data, read at run time from the
+ * reference's dataset sources: `hosek_dir` holds ArHosekSkyModelData_RGB.h and
+ * ArHosekSkyModelData_Spectral.h, `spectrum_source` is Graphics/Spectrum.cpp. */
+typedef struct dxrpt_host_hosek dxrpt_host_hosek;
+int dxrpt_host_hosek_load(const char* hosek_dir, const char* spectrum_source, dxrpt_host_hosek** out);
+void dxrpt_host_hosek_destroy(dxrpt_host_hosek* data);
+const char* dxrpt_host_hosek_last_error(void);
+/* Same outputs and layout as dxrpt_host_sky_create, from the Hosek-Wilkie model (turbidity 1..10). */
+int dxrpt_host_sky_create_hosek(const dxrpt_host_hosek* data, const float sun_direction[3], float sun_size_deg,
+                                float turbidity, const float ground_albedo[3], uint32_t res, uint16_t* out_cube,
+                                float out_sun_irradiance[3], float out_sun_render_color[3]);
+/* Single evaluations (tests): arhosek_tristim_skymodel_radiance of an RGB state, and
+ * arhosekskymodel_solar_radiance of a spectral state. */
+double dxrpt_host_hosek_rgb_radiance(const dxrpt_host_hosek* data, double turbidity, double albedo, double elevation,
+                                     double theta, double gamma, int channel);
+double dxrpt_host_hosek_solar_radiance(const dxrpt_host_hosek* data, double solar_elevation, double turbidity,
+                                       double albedo, double theta, double gamma, double wavelength);
+/* SampledSpectrum::ToRGB and SampledSpectrum::FromRGB(rgb, Reflectance) over 60 bins of 400-700 nm. */
+void dxrpt_host_spectrum_to_rgb(const dxrpt_host_hosek* data, const float spectrum[60], float rgb[3]);
+void dxrpt_host_spectrum_from_rgb_reflectance(const dxrpt_host_hosek* data, const float rgb[3], float spectrum[60]);
 
 /* RenderRayTracing's RayTraceConstants fill (DXRPathTracer.cpp:2048-2067). */
 void dxrpt_host_fill_constants(const float inv_view_projection[16], const float camera_position[3],

@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""Regression vectors for the Hosek-Wilkie sky (dxrpt_host_sky_create_hosek), written by OUR
+restatement (host/hosek.cpp) from the reference's dataset sources.  These pin the implementation
+against drift; the pin against the reference itself is the zenith probe of SURVEY.md 8(c) (3.04945,
+computed there from the reference's ArHosekSkyModel.cpp), asserted in tests/test_hosek_sky.py.
+
+    python tests/golden/make_hosek_golden.py   (needs the datasets, see scene.hosek_dataset_paths)
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import dxrpathtracer_amd as D  # noqa: E402
+
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hosek_sky.json")
+PROBE_TEXELS = [(s, y, x) for s in range(6) for (y, x) in ((0, 0), (31, 97), (64, 64), (127, 5))]
+
+
+def main():
+    assert D.scene.load_hosek() is not None, "Hosek datasets not found"
+    out = {"generator": "tests/golden/make_hosek_golden.py (host/hosek.cpp restatement)", "scenes": {}}
+    for name in ("sponza", "suntemple", "boxtest"):
+        st = D.Scene(name).settings()
+        sky = D.make_sky(st, model="hosek")
+        cube = sky.cube.reshape(6, sky.res, sky.res, 4)
+        out["scenes"][name] = {
+            "sun_direction": [float(v) for v in st.SunDirection],
+            "sun_irradiance": [float(v) for v in sky.sun_irradiance],
+            "sun_render_color": [float(v) for v in sky.sun_render_color],
+            "texels": {f"{s},{y},{x}": [int(v) for v in cube[s, y, x]] for (s, y, x) in PROBE_TEXELS},
+            "cube_u16_sum": int(sky.cube.astype(np.uint64).sum()),
+        }
+    with open(OUT, "w") as f:
+        json.dump(out, f, indent=1)
+    print("wrote", OUT)
+
+
+if __name__ == "__main__":
+    main()
