@@ -18,6 +18,7 @@
 #include "bvh_build.h"
 #include "pt_kernels.h"
 #include "pt_layout.h"
+#include "post_kernels.h"
 
 using namespace dxrpt;
 
@@ -75,6 +76,7 @@ struct dxrpt_ctx {
     // device copies
     DevBuf d_vertices, d_indices, d_geos, d_mats, d_texdesc, d_texels, d_sky, d_lut, d_nodes, d_nodes8, d_tris;
     DevBuf d_lights, d_tiles, d_tile_prefix;
+    DevBuf p_bloom0, p_bloom1;  // post-processing scratch (RGBA16F half-res)
     DevBuf d_tri_verts;  // per global triangle: its 3 MeshVertex records (3 x 64 B), built with the BVH
     // per-frame wavefront buffers
     DevBuf f_pix, f_pxrad, f_hit, f_fwd, f_shn, f_shq, f_shorg, f_shdir, f_shcon, f_counters;
@@ -127,7 +129,7 @@ struct dxrpt_ctx {
     ~dxrpt_ctx() {
         DevBuf* all[] = {&d_vertices, &d_indices, &d_geos, &d_mats, &d_texdesc, &d_texels, &d_sky, &d_lut, &d_nodes,
                          &d_nodes8, &d_tris, &d_tri_verts, &d_lights, &d_tiles, &d_tile_prefix, &f_pix, &f_pxrad, &f_hit, &f_fwd,
-                         &f_shn, &f_shq, &f_shorg, &f_shdir, &f_shcon, &f_counters};
+                         &f_shn, &f_shq, &f_shorg, &f_shdir, &f_shcon, &f_counters, &p_bloom0, &p_bloom1};
         for (DevBuf* b : all) b->release();
         for (auto& qb : f_q)
             for (DevBuf& b : qb) b.release();
@@ -781,6 +783,39 @@ int dxrpt_trace_rays(dxrpt_ctx* ctx, const float* rays, uint32_t num_rays, uint3
         upload_textures(ctx);
         HIP_CHECK(launch_trace_rays(scene_dev(ctx, trace_rays_threads(num_rays)), reinterpret_cast<const float4*>(rays), num_rays, flags,
                                     reinterpret_cast<float4*>(hits), static_cast<hipStream_t>(stream)));
+    });
+}
+
+// PostProcessor::Render (DXRPathTracer/PostProcessor.cpp:43-92): bloom + exposure + filmic tone map.
+int dxrpt_post_process(dxrpt_ctx* ctx, const dxrpt_app_settings* settings, const float* accum, uint32_t width,
+                       uint32_t height, void* out, uint32_t out_format, void* stream) {
+    if (!ctx) return DXRPT_E_INVALID_ARG;
+    return guarded(ctx, [&] {
+        require(settings && accum && out, "dxrpt_post_process: null argument");
+        require(width >= 2 && height >= 2, "dxrpt_post_process: image must be at least 2 x 2");
+        require(out_format == DXRPT_POST_FLOAT4 || out_format == DXRPT_POST_RGBA8, "dxrpt_post_process: bad output format");
+        const size_t half = size_t(width / 2) * (height / 2) * 8u;
+        ctx->p_bloom0.ensure(half);
+        ctx->p_bloom1.ensure(half);
+        PostParams p{};
+        p.accum = accum;
+        p.bloom0 = ctx->p_bloom0.p;
+        p.bloom1 = ctx->p_bloom1.p;
+        p.out = out;
+        p.width = width;
+        p.height = height;
+        p.out_format = out_format;
+        // PostProcessing.hlsl:21-25, 125-130; evaluated in double, rounded to float
+        const double sigma = double(settings->BloomBlurSigma);
+        const double g = 1.0 / std::sqrt(2.0 * 3.14159 * sigma * sigma);
+        for (int k = 0; k < 14; ++k) {
+            const int d = k - 7;
+            p.weights.w[k] = float(g * std::exp(-double(d * d) / (2.0 * sigma * sigma)));
+        }
+        p.bloom_magnitude = settings->BloomMagnitude;
+        p.bloom_exp2 = float(std::exp2(double(settings->BloomExposure)));
+        p.exposure_scale = float(std::exp2(double(settings->Exposure)) / 0.0009765625);
+        HIP_CHECK(launch_post_process(p, static_cast<hipStream_t>(stream)));
     });
 }
 

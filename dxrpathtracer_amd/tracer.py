@@ -121,6 +121,13 @@ class DXRPathTracer:
         self._check(self._L.dxrpt_get_stats(self._ctx, C.byref(st)), "dxrpt_get_stats")
         return st
 
+    def post_process(self, settings: A.AppSettings, accum_ptr: int, width: int, height: int, out_ptr: int,
+                     out_format: int = A.POST_FLOAT4, stream: int = 0):
+        """PostProcessor::Render (PostProcessor.cpp:43-92): bloom + exposure + filmic tone map of the
+        accumulation buffer into `out` (device W*H float4 or RGBA8)."""
+        self._check(A.lib().dxrpt_post_process(self._ctx, C.byref(settings), accum_ptr, width, height, out_ptr,
+                                               out_format, stream), "dxrpt_post_process")
+
     def trace_rays(self, rays_ptr: int, n: int, flags: int, hits_ptr: int, stream: int = 0):
         self._check(self._L.dxrpt_trace_rays(self._ctx, C.c_void_p(rays_ptr), n, flags, C.c_void_p(hits_ptr),
                                              C.c_void_p(stream)), "dxrpt_trace_rays")

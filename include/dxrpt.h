@@ -305,6 +305,16 @@ int dxrpt_render(dxrpt_ctx* ctx,
                  float* accum, uint32_t width, uint32_t height,
                  const dxrpt_tile* tiles, uint32_t num_tiles,
                  void* stream);
+/* ---- post-processing (the consumer of the accumulation buffer) --------------------------------
+ * PostProcessor::Render (DXRPathTracer/PostProcessor.cpp:43-92, PostProcessing.hlsl): half-res bloom
+ * (2x2 gather, 2 x separable 14-tap Gaussian in RGBA16F), exposure 2^Exposure / FP16Scale and the
+ * filmic ALU tone map, from `accum` (device float4 W*H, the dxrpt_render target) into `out` (device,
+ * W*H float4 or RGBA8 UNORM).  Uses settings->Exposure, BloomExposure, BloomMagnitude, BloomBlurSigma.
+ * Needs no scene; scratch buffers are owned by ctx.  Stream-ordered like dxrpt_render. */
+#define DXRPT_POST_FLOAT4 0u
+#define DXRPT_POST_RGBA8 1u
+int dxrpt_post_process(dxrpt_ctx* ctx, const dxrpt_app_settings* settings, const float* accum, uint32_t width,
+                       uint32_t height, void* out, uint32_t out_format, void* stream);
 /* Synchronises the context's last stream and returns the counters of the last dxrpt_render. */
 int dxrpt_get_stats(dxrpt_ctx* ctx, dxrpt_stats* out);
 
