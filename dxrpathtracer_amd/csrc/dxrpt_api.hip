@@ -91,6 +91,7 @@ struct dxrpt_ctx {
     bool rendered = false;
     // options
     bool opt_count = false, opt_timing = false;
+    uint32_t opt_timing_mask = (1u << DXRPT_K_COUNT) - 1u;  // DXRPT_OPT_KERNEL_TIMING_MASK
     int opt_width = 8;   // DXRPT_OPT_BVH_WIDTH
     uint32_t num_cus = 256;
     uint32_t opt_trav_mode = 0;     // DXRPT_OPT_TRAVERSAL_MODE: 0 one thread per ray, 1 persistent
@@ -117,6 +118,7 @@ struct dxrpt_ctx {
     struct FrameEvents {
         std::vector<hipEvent_t> ev;
         int L = 0;
+        uint32_t mask = 0;  // kernel kinds whose events were recorded
         bool pending = false;
     };
     std::vector<FrameEvents> ring;
@@ -276,17 +278,17 @@ void harvest(dxrpt_ctx* c, dxrpt_ctx::FrameEvents& f) {
         return double(ms);
     };
     auto slot = [&](int i) { return span(2 * i, 2 * i + 1); };
-    c->kernel_ms[DXRPT_K_RAYGEN] += slot(0);
-    c->kernel_launches[DXRPT_K_RAYGEN]++;
+    auto add = [&](int kind, int i) {
+        if (!((f.mask >> kind) & 1u)) return;
+        c->kernel_ms[kind] += slot(i);
+        c->kernel_launches[kind]++;
+    };
+    add(DXRPT_K_RAYGEN, 0);
     static const int kinds[4] = {DXRPT_K_TRACE, DXRPT_K_SHADE, DXRPT_K_SHADOW, DXRPT_K_RESOLVE};
     for (int d = 1; d <= f.L - 1; ++d)
-        for (int k = 0; k < 4; ++k) {
-            c->kernel_ms[kinds[k]] += slot(1 + 4 * (d - 1) + k);
-            c->kernel_launches[kinds[k]]++;
-        }
+        for (int k = 0; k < 4; ++k) add(kinds[k], 1 + 4 * (d - 1) + k);
     const int acc = 1 + 4 * (f.L - 1);
-    c->kernel_ms[DXRPT_K_ACCUMULATE] += slot(acc);
-    c->kernel_launches[DXRPT_K_ACCUMULATE]++;
+    add(DXRPT_K_ACCUMULATE, acc);
     const int e = 2 * acc;
     c->frame_ms += span(0, e + 1);
     c->timed_frames++;
@@ -415,6 +417,9 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_LDS_NODES) {
             require(value <= 1024, "dxrpt_set_option: LDS node cache must be 0..1024 nodes");
             ctx->opt_lds_nodes = uint32_t(value);
+        } else if (option == DXRPT_OPT_KERNEL_TIMING_MASK) {
+            require(value != 0 && value < (1u << DXRPT_K_COUNT), "dxrpt_set_option: timing mask must select kernel kinds");
+            ctx->opt_timing_mask = uint32_t(value);
         } else if (option == DXRPT_OPT_SHADE_BLOCK) {
             require(value == 64 || value == 128 || value == 256, "dxrpt_set_option: shade block must be 64, 128 or 256");
             ctx->opt_shade_block = uint32_t(value);
@@ -695,6 +700,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.pipeline = ctx->opt_pipeline;
         fp.packet = ctx->opt_packet;
         fp.lds_nodes = ctx->opt_lds_nodes;
+        fp.timing_mask = ctx->opt_timing_mask;
         fp.shade_block = ctx->opt_shade_block;
         fp.shade_occupancy = ctx->opt_shade_occ;
         hipStream_t s = static_cast<hipStream_t>(stream);
@@ -716,6 +722,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
                 f.ev.push_back(e);
             }
             f.L = L;
+            f.mask = ctx->opt_timing_mask;
             f.pending = true;
             ev = f.ev.data();
         }

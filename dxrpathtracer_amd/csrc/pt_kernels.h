@@ -122,6 +122,7 @@ struct FrameParams {
     uint32_t shadow_grid;            // any-hit kernel grid cap in 256-thread workgroups (0 = one thread per ray)
     uint32_t shade_block;            // workgroup size of k_shade (64..256)
     uint32_t packet;                 // wave-coherent traversal: bit 0/1 closest/any hit at depth 1, bit 2/3 at depth >= 2
+    uint32_t timing_mask;            // per-kernel timing events: kinds (1 << DXRPT_K_*) bracketed
     uint32_t lds_nodes;              // BVH8 per-lane traversal: top nodes kept in LDS per workgroup (0 = none)
     uint32_t pipeline;               // BVH8 one-thread-per-ray traversal: bit 0 triangle pairs, bit 1 next-node prefetch
     uint32_t shade_occupancy;        // k_shade register budget: 0 compiler default, 6, 7 or 8 waves per SIMD

@@ -1327,11 +1327,19 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
     const bool count = fp.trav != nullptr;
     // per-kernel timing: launch slot i (raygen, then trace/shade/shadow/resolve per depth, then
     // accumulate) is bracketed by ev[2i], ev[2i+1] recorded on the stream the kernel runs on
+    // (the frame's first start and last stop events are always recorded: they bracket the frame)
+    const int L_ = fp.set.MaxPathLength < 2 ? 2 : fp.set.MaxPathLength;
+    const int last_slot = 1 + 4 * (L_ - 1);
+    auto timed = [&](int slot) {
+        static const uint32_t kinds[4] = {DXRPT_K_TRACE, DXRPT_K_SHADE, DXRPT_K_SHADOW, DXRPT_K_RESOLVE};
+        const uint32_t kind = slot == 0 ? DXRPT_K_RAYGEN : slot == last_slot ? DXRPT_K_ACCUMULATE : kinds[(slot - 1) % 4];
+        return (fp.timing_mask >> kind) & 1u;
+    };
     auto start = [&](int slot, hipStream_t st) {
-        if (ev) (void)hipEventRecord(ev[2 * slot], st);
+        if (ev && (slot == 0 || timed(slot))) (void)hipEventRecord(ev[2 * slot], st);
     };
     auto stop = [&](int slot, hipStream_t st) {
-        if (ev) (void)hipEventRecord(ev[2 * slot + 1], st);
+        if (ev && (slot == last_slot || timed(slot))) (void)hipEventRecord(ev[2 * slot + 1], st);
     };
     auto slot_of = [](int d, int kind) { return 1 + 4 * (d - 1) + kind; };  // kind 0 trace 1 shade 2 shadow 3 resolve
     hipError_t e = hipMemsetAsync(fb.counters, 0, 2 * kMaxDepthQueues * kQueueShards * sizeof(uint32_t), stream);

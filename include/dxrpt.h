@@ -290,6 +290,9 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 #define DXRPT_OPT_LDS_NODES 19u       /* BVH8 per-lane traversal: each workgroup copies the top this-many nodes
                                          (breadth-first prefix of the tree, 80 B each) into LDS and visits them
                                          there (0..1024, default 0).  Identical results. */
+#define DXRPT_OPT_KERNEL_TIMING_MASK 20u /* kernel kinds bracketed by events when DXRPT_OPT_KERNEL_TIMING is on
+                                            (bit 1 << DXRPT_K_*, default all); the frame span is always timed.
+                                            Fewer events, less timing overhead in the measured frames. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

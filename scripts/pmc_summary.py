@@ -62,14 +62,21 @@ def main(prof, rnd):
     os.makedirs("profiles", exist_ok=True)
     with open(f"profiles/{rnd}_kernels.json", "w") as f:
         json.dump(out, f, indent=2)
-    # the timed closest-hit kernel: the uninstrumented k_trace instantiation with the most time
-    cands = [k for k in out["kernels"] if k.startswith("k_trace<false")]
-    ktn = max(cands, key=lambda k: out["kernels"][k].get("total_ms", 0.0)) if cands else None
-    kt = out["kernels"].get(ktn, {})
+    # the timed closest-hit kind (DXRPT_K_TRACE): the uninstrumented closest-hit instantiations of the
+    # frame (k_trace_packet for the primary rays, k_trace<false, ...> for deeper ones), launch-weighted
+    cands = [k for k in out["kernels"] if k.startswith("k_trace<false") or k.startswith("k_trace_packet")]
+    calls = sum(out["kernels"][k].get("calls", 0) for k in cands)
+    def wavg(key):
+        vals = [(out["kernels"][k].get("calls", 0), out["kernels"][k].get(key)) for k in cands]
+        if not calls or any(v is None for _, v in vals):
+            return None
+        return sum(c * v for c, v in vals) / calls
     with open(f"profiles/{rnd}_pmc_k_trace.json", "w") as f:
-        json.dump({"config": CONFIG, "kernel": ktn, "calls": kt.get("calls"), "avg_ms": kt.get("avg_ms"),
-                   "hbm_bytes_per_launch": kt.get("hbm_bytes_per_launch"),
-                   "hbm_read_bytes_raw": kt.get("hbm_read_bytes_raw"), "l2_hit_rate": kt.get("l2_hit_rate"),
+        json.dump({"config": CONFIG, "kernel": " + ".join(sorted(cands)), "calls": calls,
+                   "avg_ms": (sum(out["kernels"][k].get("total_ms", 0.0) for k in cands) / calls) if calls else None,
+                   "per_kernel_avg_ms": {k: out["kernels"][k].get("avg_ms") for k in cands},
+                   "hbm_bytes_per_launch": wavg("hbm_bytes_per_launch"),
+                   "hbm_read_bytes_raw": wavg("hbm_read_bytes_raw"), "l2_hit_rate": wavg("l2_hit_rate"),
                    "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 16-B/lane read correction) + WRITE_SIZE KiB x1024"},
                   f, indent=2)
     for src in ("kt/run_kernel_stats.csv",):

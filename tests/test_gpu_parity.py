@@ -355,6 +355,28 @@ def test_kernel_timing_option(torch_cuda, concurrency):
         assert stt.frame_ms >= (busy - stt.kernel_ms[A.K_SHADOW]) * 0.99
 
 
+def test_kernel_timing_mask(torch_cuda):
+    # DXRPT_OPT_KERNEL_TIMING_MASK: only the selected kinds are bracketed (the frame span always is)
+    torch = torch_cuda
+    t = tracer("boxtest")
+    sc, _ = scene_bundle("boxtest")
+    st = sc.settings(MaxPathLength=4)
+    t.set_option(A.OPT_KERNEL_TIMING_MASK, 1 << A.K_TRACE)
+    t.set_option(A.OPT_KERNEL_TIMING, 1)
+    t.reset_timing()
+    try:
+        for s in range(3):
+            gpu_render(torch, "boxtest", 96, 96, st, s)
+        stt = t.stats()
+    finally:
+        t.set_option(A.OPT_KERNEL_TIMING, 0)
+        t.set_option(A.OPT_KERNEL_TIMING_MASK, (1 << A.K_COUNT) - 1)
+    assert stt.timed_frames == 3 and stt.frame_ms > 0
+    assert stt.kernel_launches[A.K_TRACE] == 9 and stt.kernel_ms[A.K_TRACE] > 0
+    assert all(stt.kernel_launches[k] == 0 for k in range(A.K_COUNT) if k != A.K_TRACE)
+    assert stt.frame_ms >= stt.kernel_ms[A.K_TRACE]
+
+
 def test_errors_are_reported_not_raised(torch_cuda):
     # DXRPT_E_* status + dxrpt_last_error instead of the reference's DXCall exceptions
     torch = torch_cuda
