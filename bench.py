@@ -28,9 +28,13 @@ sys.path.insert(0, REPO)
 WIDTH, HEIGHT, PATH_LENGTH = 1920, 1080, 3
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "Mrays/sec + ms/frame, Sponza 1920x1080 path-length 3 at 1/2/4/8 GPU"
-# k_trace algorithmic bytes: per ray 32 B ray in (2 x float4) + 16 B hit out, plus the
-# BVH nodes (64 B) and triangle records (48 B) it visits (counted by the instrumented kernels).
+# Algorithmic bytes, per ray, plus the BVH nodes (80 B) and triangle records (48 B) it
+# visits (counted by the instrumented kernels):
+#   k_trace  (closest hit): 32 B ray in (2 x float4) + 16 B hit out
+#   k_shadow (any hit):     4 B queue entry + 48 B shadow slot in (origin, direction, contribution);
+#                           the 16-B contribution write of occluded rays is not counted (lower bound)
 RAY_IN_BYTES, HIT_OUT_BYTES = 32, 16
+SHADOW_IN_BYTES = 52
 
 
 def log(*a):
@@ -74,11 +78,11 @@ def cpu_baseline(scene, sky, settings, threads):
             "cpu_model": cpu_model(), "host_cpus": os.cpu_count()}
 
 
-def pmc_traffic():
-    """HBM bytes per k_trace launch from the committed rocprofv3 PMC summary, if one exists for this
-    config (profiles/*_pmc_k_trace.json, written by scripts/pmc_summary.py); else None."""
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` (k_trace / k_shadow) from the committed rocprofv3 PMC summary, if
+    one exists for this config (profiles/*_pmc_<kernel>.json, written by scripts/pmc_summary.py)."""
     import glob
-    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_k_trace.json")), reverse=True):
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", f"*_pmc_{kernel}.json")), reverse=True):
         try:
             d = json.load(open(p))
         except Exception:
@@ -151,11 +155,24 @@ def main():
         frame(f)
     torch.cuda.synchronize()
 
-    # ---- timed region: production schedule (any-hit / closest-hit stream overlap) with events around the
-    # k_trace launches only (the roofline kernel) plus the frame span; the all-kernel breakdown below is
-    # a separate, untimed pass because ~26 events per frame cost ~0.1 ms of frame time
-    tracer.set_option(A.OPT_KERNEL_TIMING_MASK, 1 << A.K_TRACE)
+    # ---- per-kernel breakdown (all kinds, untimed pass before the timed region): picks the dominant
+    # kernel whose roofline is reported.  ~26 events per frame cost ~0.1 ms of frame time, so the timed
+    # region below brackets only the dominant kernel's launches (plus the frame span).
+    tracer.set_option(A.OPT_KERNEL_TIMING_MASK, (1 << A.K_COUNT) - 1)
     tracer.set_option(A.OPT_KERNEL_TIMING, 1)
+    tracer.reset_timing()
+    for f in range(min(args.steps, 16)):
+        frame(f)
+    torch.cuda.synchronize()
+    breakdown = tracer.stats()
+    kms = {A.KERNEL_NAMES[k]: breakdown.kernel_ms[k] for k in range(A.K_COUNT)}
+    dominant = max(kms, key=kms.get)
+    roof_kernel = dominant if dominant in ("k_trace", "k_shadow") else "k_trace"
+    K_ROOF = A.K_TRACE if roof_kernel == "k_trace" else A.K_SHADOW
+
+    # ---- timed region: production schedule (any-hit / closest-hit stream overlap), events on the
+    # launching streams around the roofline kernel's launches only
+    tracer.set_option(A.OPT_KERNEL_TIMING_MASK, 1 << K_ROOF)
     tracer.reset_timing()
     if world > 1:
         dist.barrier()
@@ -171,16 +188,9 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     stats = tracer.stats()
-    trace_ms_avg = stats.kernel_ms[A.K_TRACE] / max(1, stats.kernel_launches[A.K_TRACE])
-    gpu_frame_ms = stats.frame_ms / max(1, stats.timed_frames)
-    # per-kernel breakdown (all kinds; after the timed region)
-    tracer.set_option(A.OPT_KERNEL_TIMING_MASK, (1 << A.K_COUNT) - 1)
-    tracer.reset_timing()
-    for f in range(min(args.steps, 16)):
-        frame(f)
-    torch.cuda.synchronize()
-    breakdown = tracer.stats()
     tracer.set_option(A.OPT_KERNEL_TIMING, 0)
+    roof_ms_avg = stats.kernel_ms[K_ROOF] / max(1, stats.kernel_launches[K_ROOF])
+    gpu_frame_ms = stats.frame_ms / max(1, stats.timed_frames)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -191,16 +201,22 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = nominal_per_frame * args.steps / elapsed / 1e6
 
-    # ---- roofline of the dominant kernel (measured live with HIP events on the render stream)
-    kms = {A.KERNEL_NAMES[k]: breakdown.kernel_ms[k] for k in range(A.K_COUNT)}
-    dominant = max(kms, key=kms.get)
-    rays = census.radiance_rays
-    trace_bytes_frame = (rays * (RAY_IN_BYTES + HIT_OUT_BYTES) + census.node_visits_radiance * bvh.node_bytes
-                         + census.tri_tests_radiance * bvh.tri_bytes)
-    trace_launches_per_frame = PATH_LENGTH - 1
-    achieved = (trace_bytes_frame / trace_launches_per_frame) / (trace_ms_avg * 1e-3) / 1e9
-    pmc, traffic_src = pmc_traffic()
+    # ---- roofline of the dominant kernel (measured live with HIP events on its launching stream)
+    launches_per_frame = PATH_LENGTH - 1  # one closest-hit and one any-hit pass per depth
+    trace_bytes_frame = (census.radiance_rays * (RAY_IN_BYTES + HIT_OUT_BYTES)
+                         + census.node_visits_radiance * bvh.node_bytes + census.tri_tests_radiance * bvh.tri_bytes)
+    shadow_bytes_frame = (census.shadow_rays * SHADOW_IN_BYTES
+                          + census.node_visits_shadow * bvh.node_bytes + census.tri_tests_shadow * bvh.tri_bytes)
+    roof_bytes = (trace_bytes_frame if roof_kernel == "k_trace" else shadow_bytes_frame) / launches_per_frame
+    achieved = roof_bytes / (roof_ms_avg * 1e-3) / 1e9
+    pmc, traffic_src = pmc_traffic(roof_kernel)
     traffic = pmc.get("hbm_bytes_per_launch")
+    # the other traversal kernel, from the breakdown pass (for the record)
+    other = "k_shadow" if roof_kernel == "k_trace" else "k_trace"
+    K_OTHER = A.K_SHADOW if other == "k_shadow" else A.K_TRACE
+    other_ms = breakdown.kernel_ms[K_OTHER] / max(1, breakdown.kernel_launches[K_OTHER])
+    other_bytes = (shadow_bytes_frame if other == "k_shadow" else trace_bytes_frame) / launches_per_frame
+    other_pmc, _ = pmc_traffic(other)
 
     result = None
     if rank == 0:
@@ -225,11 +241,10 @@ def main():
                        "width": WIDTH, "height": HEIGHT, "max_path_length": PATH_LENGTH,
                        "sqrt_num_samples": 4, "triangles": scene.num_triangles,
                        "parallelism": f"screen bands x{world}" + (" + RCCL gather" if world > 1 else "")},
-            "roofline": {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": roof_kernel, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic,
-                         "bytes_per_launch": int(trace_bytes_frame / trace_launches_per_frame),
-                         "avg_launch_ms": round(trace_ms_avg, 4), "traffic_source": traffic_src,
+                         "traffic": traffic, "bytes_per_launch": int(roof_bytes),
+                         "avg_launch_ms": round(roof_ms_avg, 4), "traffic_source": traffic_src,
                          "traffic_kernel": pmc.get("kernel"), "l2_hit_rate": pmc.get("l2_hit_rate")},
             "cpu_baseline": cpu,
             "detail": {
@@ -238,12 +253,18 @@ def main():
                 if world == 1 else None,
                 "kernel_ms_per_frame": {k: round(v / frames, 4) for k, v in kms.items()},
                 "dominant_kernel": dominant,
+                "roofline_other": {"kernel": other, "bytes_per_launch": int(other_bytes),
+                                   "avg_launch_ms": round(other_ms, 4),
+                                   "achieved_GBs": round(other_bytes / (other_ms * 1e-3) / 1e9, 1),
+                                   "traffic": other_pmc.get("hbm_bytes_per_launch"),
+                                   "l2_hit_rate": other_pmc.get("l2_hit_rate")},
                 "gpu_frame_ms_events": round(gpu_frame_ms, 4),
-                "kernel_breakdown_note": "kernel_ms_per_frame from a separate all-kernel event pass after the timed region",
+                "kernel_breakdown_note": "kernel_ms_per_frame from a separate all-kernel event pass before the timed region",
                 "frame_ms": {"mean": round(float(frame_ms.mean()), 4), "median": round(float(np.median(frame_ms)), 4),
                              "max": round(float(frame_ms.max()), 4)},
-                "nodes_per_radiance_ray": round(census.node_visits_radiance / max(1, rays), 2),
-                "tris_per_radiance_ray": round(census.tri_tests_radiance / max(1, rays), 2),
+                "nodes_per_radiance_ray": round(census.node_visits_radiance / max(1, census.radiance_rays), 2),
+                "tris_per_radiance_ray": round(census.tri_tests_radiance / max(1, census.radiance_rays), 2),
+                "tris_per_shadow_ray": round(census.tri_tests_shadow / max(1, census.shadow_rays), 2),
                 "nodes_per_shadow_ray": round(census.node_visits_shadow / max(1, census.shadow_rays), 2),
                 "bvh": {"nodes": bvh.num_nodes, "max_depth": bvh.max_depth, "build_ms": round(bvh.build_ms, 1),
                         "sah": round(bvh.sah_cost, 2)},

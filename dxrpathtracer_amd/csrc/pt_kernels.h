@@ -19,7 +19,7 @@ __host__ __device__ __attribute__((always_inline)) inline uint32_t tex_tile_word
 // so concurrent waves spread their atomics over kQueueShards addresses instead of one.  Shard s of a
 // queue owns positions [s * cap, (s + 1) * cap); consumers enumerate item i of the queue by walking
 // the shard counts (queue_pos in pt_kernels.hip).
-constexpr uint32_t kQueueShards = 32;
+constexpr uint32_t kQueueShards = 64;
 constexpr uint32_t kMaxDepthQueues = 16;  // radiance queues 0..15 by depth, shadow queues 16..31
 
 // Radiance ray queue of one depth (SoA of 16-B words: one dwordx4 per lane, coalesced).  The path

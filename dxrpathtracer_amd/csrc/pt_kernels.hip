@@ -39,6 +39,16 @@ constexpr float kSpotShadowNearClip = 0.1f;   // AppSettings.hlsl:56
 PT_DEV uint32_t fbits(float f) { return __float_as_uint(f); }
 PT_DEV float bitsf(uint32_t u) { return __uint_as_float(u); }
 
+// Per-lane traversal stacks in LDS: wave w of the workgroup owns S.stack_ints x 64 ints, entry j of
+// lane l at [j * 64 + l] (conflict-free, and the stride is a compile-time constant so every stack
+// access is one ds_read/ds_write with an immediate offset).  The LDS address space is explicit so
+// the spill path (global) never merges with it into flat accesses.
+typedef __attribute__((address_space(3))) int lds_int;
+constexpr int kStkStride = 64;
+PT_DEV lds_int* lane_stack(const SceneDev& S, int* stack) {
+    return (lds_int*)(stack) + (threadIdx.x >> 6) * S.stack_ints * 64u + (threadIdx.x & 63u);
+}
+
 // ---- texture sampling ---------------------------------------------------------------------------
 // SampleLevel(MeshSampler, uv, 0): MeshSampler is anisotropic x16 with WRAP addressing
 // (Graphics/DX12_Helpers.cpp:327-338); at LOD 0 on mip 0 this is defined here as bilinear with
@@ -256,9 +266,9 @@ PT_DEV f3 safe_inverse(f3 d) {
 }
 
 // BVH2 traversal ("while-while", Aila & Laine 2009): nearer child first, farther pushed on a per-lane
-// LDS stack (stk[sp * blockDim.x]).
+// LDS stack (stk[sp * kStkStride]).
 template <bool kAnyHit, bool kCount>
-PT_DEV bool traverse2(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, int* stk, HitRec& h,
+PT_DEV bool traverse2(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, lds_int* stk, HitRec& h,
                       uint32_t& nvisit, uint32_t& ntest) {
     const f3 inv = safe_inverse(d);
     const f3 ood = mul(o, inv);
@@ -287,7 +297,7 @@ PT_DEV bool traverse2(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
             if (hit0 && hit1) {
                 int first = ch.x, second = ch.y;
                 if (n1 < n0) { first = ch.y; second = ch.x; }
-                stk[sp * blockDim.x] = second;
+                stk[sp * kStkStride] = second;
                 ++sp;
                 node = first;
             } else if (hit0 || hit1) {
@@ -295,7 +305,7 @@ PT_DEV bool traverse2(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
             } else {
                 if (sp == 0) return kAnyHit ? false : h.tri != kMiss;
                 --sp;
-                node = stk[sp * blockDim.x];
+                node = stk[sp * kStkStride];
             }
         }
         const uint32_t code = ~uint32_t(node);
@@ -306,7 +316,7 @@ PT_DEV bool traverse2(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
         }
         if (sp == 0) return kAnyHit ? false : h.tri != kMiss;
         --sp;
-        node = stk[sp * blockDim.x];
+        node = stk[sp * kStkStride];
     }
 }
 
@@ -314,7 +324,7 @@ PT_DEV bool traverse2(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
 // A node visit intersects all 8 quantised child boxes at once; internal hits form a "node group"
 // (base_child, hit bits keyed by slot ^ octant, imask) visited highest key first (near to far), leaf
 // hits are tested right away.  The rest of a group is pushed when descending: <= 1 push per level,
-// 2 x 4 B per entry in LDS (stk[sp * blockDim.x], stk[(kTraversalStack8 + sp) * blockDim.x]).
+// 2 x 4 B per entry in LDS (stk[2 sp * kStkStride], stk[(2 sp + 1) * kStkStride]).
 // The traversal is a resumable state machine (Ray8 + node + sp) so persistent kernels can advance
 // every lane by one node visit per iteration and refill lanes whose ray finished.
 struct Ray8 {
@@ -346,17 +356,17 @@ PT_DEV void ray8_init(Ray8& R, f3 o, f3 d, float tmin, float tmax, bool alpha, H
 // Group stack: `sp` entries; the top one lives in registers (`tos`), entries 0 .. sp-2 in LDS
 // (first kStackLds8) and in the thread's global spill slab (deeper), so a pop hands over the next
 // group at once and the LDS refill of `tos` overlaps the next node fetch.
-PT_DEV void stack8_store(const SceneDev& S, int* stk, int j, uint2 e) {
+PT_DEV void stack8_store(const SceneDev& S, lds_int* stk, int j, uint2 e) {
     if (j < kStackLds8) {
-        stk[(2 * j) * blockDim.x] = int(e.x);
-        stk[(2 * j + 1) * blockDim.x] = int(e.y);
+        stk[(2 * j) * kStkStride] = int(e.x);
+        stk[(2 * j + 1) * kStkStride] = int(e.y);
     } else {  // rare: deep entries spill to this thread's global slab
         S.spill8[size_t(j - kStackLds8) * S.spill_stride + blockIdx.x * blockDim.x + threadIdx.x] = e;
     }
 }
 
-PT_DEV uint2 stack8_load(const SceneDev& S, const int* stk, int j) {
-    if (j < kStackLds8) return make_uint2(uint32_t(stk[(2 * j) * blockDim.x]), uint32_t(stk[(2 * j + 1) * blockDim.x]));
+PT_DEV uint2 stack8_load(const SceneDev& S, const lds_int* stk, int j) {
+    if (j < kStackLds8) return make_uint2(uint32_t(stk[(2 * j) * kStkStride]), uint32_t(stk[(2 * j + 1) * kStkStride]));
     return S.spill8[size_t(j - kStackLds8) * S.spill_stride + blockIdx.x * blockDim.x + threadIdx.x];
 }
 
@@ -430,7 +440,7 @@ PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx) {
 
 // Node visit on already-loaded words (lets the caller issue the next node's loads early).
 template <bool kCount>
-PT_DEV bool trav8_node_w(const SceneDev& S, const Ray8& R, const Node8Words& W, uint32_t& node, int& sp, int* stk,
+PT_DEV bool trav8_node_w(const SceneDev& S, const Ray8& R, const Node8Words& W, uint32_t& node, int& sp, lds_int* stk,
                          uint2& tos, const HitRec& h, uint32_t& tbase, uint32_t& tbits, uint32_t& nvisit) {
     if (kCount) ++nvisit;
     const uint4 w0 = W.w0, w1 = W.w1;
@@ -476,7 +486,7 @@ PT_DEV bool trav8_node_w(const SceneDev& S, const Ray8& R, const Node8Words& W, 
 }
 
 template <bool kCount>
-PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp, int* stk, uint2& tos, const HitRec& h,
+PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp, lds_int* stk, uint2& tos, const HitRec& h,
                        uint32_t& tbase, uint32_t& tbits, uint32_t& nvisit, const NodeCache& nc = NodeCache{nullptr, 0u}) {
     return trav8_node_w<kCount>(S, R, load_node8(S, nc, node), node, sp, stk, tos, h, tbase, tbits, nvisit);
 }
@@ -518,7 +528,7 @@ PT_DEV bool trav8_tris2(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32
 // node's words are loaded right after its address is known, before the current node's triangle
 // tests).  Visit order, tests and results are those of traverse8.
 template <bool kAnyHit, bool kCount, int kPipe>
-PT_DEV bool traverse8_pipe(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, int* stk, HitRec& h,
+PT_DEV bool traverse8_pipe(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, lds_int* stk, HitRec& h,
                            uint32_t& nvisit, uint32_t& ntest, const NodeCache& nc) {
     Ray8 R;
     ray8_init(R, o, d, tmin, tmax, alpha, h);
@@ -653,7 +663,7 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
 // One node visit and its triangles.  Returns true when the ray is finished: h.tri != kMiss means hit
 // (closest) / occluded (any-hit).
 template <bool kAnyHit, bool kCount>
-PT_DEV bool trav8_step(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp, int* stk, uint2& tos, HitRec& h,
+PT_DEV bool trav8_step(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp, lds_int* stk, uint2& tos, HitRec& h,
                        uint32_t& nvisit, uint32_t& ntest, const NodeCache& nc) {
     uint32_t tbase = 0, tbits = 0;
     const bool more = trav8_node<kCount>(S, R, node, sp, stk, tos, h, tbase, tbits, nvisit, nc);
@@ -662,7 +672,7 @@ PT_DEV bool trav8_step(const SceneDev& S, const Ray8& R, uint32_t& node, int& sp
 }
 
 template <bool kAnyHit, bool kCount>
-PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, int* stk, HitRec& h,
+PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, lds_int* stk, HitRec& h,
                       uint32_t& nvisit, uint32_t& ntest, const NodeCache& nc) {
     Ray8 R;
     ray8_init(R, o, d, tmin, tmax, alpha, h);
@@ -675,14 +685,14 @@ PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
 }
 
 template <int W, bool kAnyHit, bool kCount, int kPipe = 0>
-PT_DEV bool traverse(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, int* stk, HitRec& h,
+PT_DEV bool traverse(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, lds_int* stk, HitRec& h,
                      uint32_t& nvisit, uint32_t& ntest, const NodeCache& nc = NodeCache{nullptr, 0u}) {
     h.t = tmax;
     h.tri = kMiss;
     h.b1 = h.b2 = 0.0f;
     h.geom = 0;
     if (W == 8) {
-        if (kPipe) return traverse8_pipe<kAnyHit, kCount, kPipe>(S, o, d, tmin, tmax, alpha, stk, h, nvisit, ntest, nc);
+        if (kPipe & 3) return traverse8_pipe<kAnyHit, kCount, kPipe & 3>(S, o, d, tmin, tmax, alpha, stk, h, nvisit, ntest, nc);
         return traverse8<kAnyHit, kCount>(S, o, d, tmin, tmax, alpha, stk, h, nvisit, ntest, nc);
     }
     return traverse2<kAnyHit, kCount>(S, o, d, tmin, tmax, alpha, stk, h, nvisit, ntest);
@@ -710,8 +720,8 @@ PT_DEV uint32_t queue_total(const uint32_t* __restrict__ cnt) {
 }
 
 // Position of item i (< queue_total) of a sharded queue with shard capacity cap: the items of shard 0
-// come first, then shard 1, ...
-PT_DEV uint32_t queue_pos(const uint32_t* __restrict__ cnt, uint32_t cap, uint32_t i) {
+// come first, then shard 1, ...  Any item order across lanes.
+PT_DEV uint32_t queue_pos_any(const uint32_t* __restrict__ cnt, uint32_t cap, uint32_t i) {
     uint32_t pos = 0, base = 0;
 #pragma unroll
     for (uint32_t s = 0; s < kQueueShards; ++s) {
@@ -720,6 +730,17 @@ PT_DEV uint32_t queue_pos(const uint32_t* __restrict__ cnt, uint32_t cap, uint32
         base += c;
     }
     return pos;
+}
+
+// Same, for lanes holding consecutive items (i grows with the lane id, so the first active lane holds
+// the smallest): a wave-uniform scalar scan finds the shard of that item, then each lane steps
+// forward over the (few) shards its own item lies past.
+PT_DEV uint32_t queue_pos(const uint32_t* __restrict__ cnt, uint32_t cap, uint32_t i) {
+    const uint32_t i0 = uint32_t(__builtin_amdgcn_readfirstlane(int(i)));
+    uint32_t s = 0, base = 0;
+    while (s + 1u < kQueueShards && base + cnt[s] <= i0) base += cnt[s++];
+    while (s + 1u < kQueueShards && base + cnt[s] <= i) base += cnt[s++];
+    return s * cap + (i - base);
 }
 
 // Wave-aggregated append to shard (wave % kQueueShards) of a queue: one atomic per wave.  Returns the
@@ -811,7 +832,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0
 void k_trace(KArgs A, int depth) {
     extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved, then the node cache
     NodeCache nc{nullptr, 0u};
-    if (W == 8 && !kCount && A.P.lds_nodes)
+    if (W == 8 && !kCount && (kPipe & 4))  // LDS node cache: a separate instantiation, so that the
+        // default kernels' node loads are plain global loads (no LDS/global pointer select -> flat loads)
         nc = node_cache_fill(A.S, reinterpret_cast<uint4*>(stack + A.S.stack_ints * blockDim.x), A.P.lds_nodes);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t* cnt = radiance_counts(A.F, depth);
@@ -825,7 +847,7 @@ void k_trace(KArgs A, int depth) {
     const bool alpha = depth <= A.P.set.MaxAnyHitPathLength;
     HitRec h;
     uint32_t nv = 0, nt = 0;
-    traverse<W, false, kCount, kPipe>(A.S, ld3(o4), ld3(d4), tmin, o4.w, alpha, stack + threadIdx.x, h, nv, nt, nc);
+    traverse<W, false, kCount, kPipe>(A.S, ld3(o4), ld3(d4), tmin, o4.w, alpha, lane_stack(A.S, stack), h, nv, nt, nc);
     A.F.hit[pos] = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
     if (kCount) {
         atomicAdd(&A.P.trav[0], (unsigned long long)nv);
@@ -1041,10 +1063,27 @@ void k_shade(KArgs A, int depth) {
     // shadow queue of this depth and of the continuation rays into queue[depth+1]
     uint32_t* shcnt = A.F.counters + (kMaxDepthQueues + uint32_t(depth)) * kQueueShards;
     const uint32_t cap_s = A.F.shadow_slots * A.F.cap_r;
-    for (uint32_t k = 0;; ++k) {
-        if (__ballot(nsh > k) == 0ull) break;
-        const uint32_t spos = queue_append(shcnt, cap_s, nsh > k);
-        if (nsh > k) A.F.sh_queue[spos] = k * A.F.qsize + pos;
+    {
+        // one atomic for all of the wave's shadow rays: ray k of every lane after rays 0..k-1 of all lanes
+        const int lane = __lane_id();
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        uint32_t total = 0;
+        for (uint32_t k = 0;; ++k) {
+            const unsigned long long m = __ballot(nsh > k);
+            if (m == 0ull) break;
+            total += uint32_t(__popcll(m));
+        }
+        const int leader = __ffsll(static_cast<long long>(__ballot(1))) - 1;
+        const uint32_t shard = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) % kQueueShards;
+        uint32_t base = 0;
+        if (lane == leader && total != 0u) base = atomicAdd(&shcnt[shard], total);
+        base = uint32_t(__shfl(int(base), leader)) + shard * cap_s;
+        for (uint32_t k = 0;; ++k) {
+            const unsigned long long m = __ballot(nsh > k);
+            if (m == 0ull) break;
+            if (nsh > k) A.F.sh_queue[base + uint32_t(__popcll(m & lt))] = k * A.F.qsize + pos;
+            base += uint32_t(__popcll(m));
+        }
     }
     const uint32_t npos = queue_append(A.F.counters + uint32_t(depth + 1) * kQueueShards, A.F.cap_r, cont);
     if (cont) {
@@ -1068,7 +1107,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0
 void k_shadow(KArgs A, int depth) {
     extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved, then the node cache
     NodeCache nc{nullptr, 0u};
-    if (W == 8 && !kCount && A.P.lds_nodes)
+    if (W == 8 && !kCount && (kPipe & 4))  // LDS node cache: a separate instantiation, so that the
+        // default kernels' node loads are plain global loads (no LDS/global pointer select -> flat loads)
         nc = node_cache_fill(A.S, reinterpret_cast<uint4*>(stack + A.S.stack_ints * blockDim.x), A.P.lds_nodes);
     const uint32_t* cnt = shadow_counts(A.F, depth);
     const uint32_t count = queue_total(cnt);
@@ -1081,7 +1121,7 @@ void k_shadow(KArgs A, int depth) {
         const float4 c4 = A.F.sh_con[slot];
         HitRec h;
         const bool occluded =
-            traverse<W, true, kCount, kPipe>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stack + threadIdx.x, h, nv, nt, nc);
+            traverse<W, true, kCount, kPipe>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, lane_stack(A.S, stack), h, nv, nt, nc);
         if (occluded) A.F.sh_con[slot] = make_float4(c4.x * 0.0f, c4.y * 0.0f, c4.z * 0.0f, c4.w);
     }
     if (kCount) {
@@ -1164,7 +1204,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(KArgs A, int depth) {
 template <bool kCount, bool kShadow>
 __global__ __launch_bounds__(kBlock) void k_traverse8p(KArgs A, int depth) {
     extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved (launch_lds_bytes)
-    int* stk = stack + threadIdx.x;
+    lds_int* stk = lane_stack(A.S, stack);
     const uint32_t* cnt = kShadow ? shadow_counts(A.F, depth) : radiance_counts(A.F, depth);
     const uint32_t cap = kShadow ? A.F.shadow_slots * A.F.cap_r : A.F.cap_r;
     const uint32_t count = queue_total(cnt);
@@ -1196,7 +1236,7 @@ __global__ __launch_bounds__(kBlock) void k_traverse8p(KArgs A, int depth) {
             if (!active) {
                 const uint32_t j = next + uint32_t(__popcll(idle & lt));
                 if (j < end) {
-                    const uint32_t pos = queue_pos(cnt, cap, j);
+                    const uint32_t pos = queue_pos_any(cnt, cap, j);
                     if (kShadow) {
                         item = A.F.sh_queue[pos];
                         const float4 o4 = A.F.sh_org[item];
@@ -1292,10 +1332,10 @@ __global__ __launch_bounds__(kBlock) void k_trace_rays(SceneDev S, const float4*
     uint32_t nv = 0, nt = 0;
     const bool alpha = (flags & 2u) != 0u;
     if (flags & 1u) {
-        bool occ = traverse<W, true, false>(S, ld3(a), ld3(b), a.w, b.w, alpha, stack + threadIdx.x, h, nv, nt);
+        bool occ = traverse<W, true, false>(S, ld3(a), ld3(b), a.w, b.w, alpha, lane_stack(S, stack), h, nv, nt);
         hits[i] = make_float4(occ ? 1.0f : -1.0f, 0.0f, 0.0f, bitsf(kMiss));
     } else {
-        bool any = traverse<W, false, false>(S, ld3(a), ld3(b), a.w, b.w, alpha, stack + threadIdx.x, h, nv, nt);
+        bool any = traverse<W, false, false>(S, ld3(a), ld3(b), a.w, b.w, alpha, lane_stack(S, stack), h, nv, nt);
         hits[i] = any ? make_float4(h.t, h.b1, h.b2, bitsf(h.tri)) : make_float4(-1.0f, 0.0f, 0.0f, bitsf(kMiss));
     }
 }
@@ -1364,7 +1404,8 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
     auto trace = [&](int d, hipStream_t st) {
 #define DXRPT_LAUNCH(K, C, W, O, GG) hipLaunchKernelGGL((K<C, W, O>), dim3(GG), dim3(tb), ldst, st, A, d)
 #define DXRPT_LAUNCH_P(K, O, GG)                                                                              \
-    switch (fp.pipeline) {                                                                                 \
+    switch (A.P.lds_nodes ? 4u : fp.pipeline) {                                                            \
+        case 4: hipLaunchKernelGGL((K<false, 8, O, 4>), dim3(GG), dim3(tb), ldsc, st, A, d); break;         \
         case 1: hipLaunchKernelGGL((K<false, 8, O, 1>), dim3(GG), dim3(tb), ldsc, st, A, d); break;         \
         case 2: hipLaunchKernelGGL((K<false, 8, O, 2>), dim3(GG), dim3(tb), ldsc, st, A, d); break;         \
         case 3: hipLaunchKernelGGL((K<false, 8, O, 3>), dim3(GG), dim3(tb), ldsc, st, A, d); break;         \

@@ -278,8 +278,9 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                          0 = one thread per queued shadow ray (default) */
 #define DXRPT_OPT_CONCURRENCY 16u     /* 1 (default): each depth's any-hit pass runs on an internal stream
                                          concurrently with the next closest-hit pass (joined before the
-                                         next shading pass); 0: one stream.  Per-kernel timing
-                                         (DXRPT_OPT_KERNEL_TIMING) always runs in order on one stream. */
+                                         next shading pass); 0: one stream.  Per-kernel timing events
+                                         (DXRPT_OPT_KERNEL_TIMING) are recorded on the stream each kernel
+                                         runs on, so concurrent passes are timed as they overlap. */
 #define DXRPT_OPT_TRAVERSAL_PIPELINE 17u /* BVH8 one-thread-per-ray traversal: bit 0 = load leaf triangles two at a
                                             time, bit 1 = load the next node before the current node's triangle
                                             tests (default 0).  Results are identical for every value. */
@@ -289,7 +290,8 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                           hit at depth >= 2, 8 = any hit at depth >= 2.  Identical results. */
 #define DXRPT_OPT_LDS_NODES 19u       /* BVH8 per-lane traversal: each workgroup copies the top this-many nodes
                                          (breadth-first prefix of the tree, 80 B each) into LDS and visits them
-                                         there (0..1024, default 0).  Identical results. */
+                                         there (0..1024, default 0; when set, it replaces
+                                         DXRPT_OPT_TRAVERSAL_PIPELINE).  Identical results. */
 #define DXRPT_OPT_KERNEL_TIMING_MASK 20u /* kernel kinds bracketed by events when DXRPT_OPT_KERNEL_TIMING is on
                                             (bit 1 << DXRPT_K_*, default all); the frame span is always timed.
                                             Fewer events, less timing overhead in the measured frames. */

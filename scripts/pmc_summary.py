@@ -62,23 +62,26 @@ def main(prof, rnd):
     os.makedirs("profiles", exist_ok=True)
     with open(f"profiles/{rnd}_kernels.json", "w") as f:
         json.dump(out, f, indent=2)
-    # the timed closest-hit kind (DXRPT_K_TRACE): the uninstrumented closest-hit instantiations of the
-    # frame (k_trace_packet for the primary rays, k_trace<false, ...> for deeper ones), launch-weighted
-    cands = [k for k in out["kernels"] if k.startswith("k_trace<false") or k.startswith("k_trace_packet")]
-    calls = sum(out["kernels"][k].get("calls", 0) for k in cands)
-    def wavg(key):
-        vals = [(out["kernels"][k].get("calls", 0), out["kernels"][k].get(key)) for k in cands]
-        if not calls or any(v is None for _, v in vals):
-            return None
-        return sum(c * v for c, v in vals) / calls
-    with open(f"profiles/{rnd}_pmc_k_trace.json", "w") as f:
-        json.dump({"config": CONFIG, "kernel": " + ".join(sorted(cands)), "calls": calls,
-                   "avg_ms": (sum(out["kernels"][k].get("total_ms", 0.0) for k in cands) / calls) if calls else None,
-                   "per_kernel_avg_ms": {k: out["kernels"][k].get("avg_ms") for k in cands},
-                   "hbm_bytes_per_launch": wavg("hbm_bytes_per_launch"),
-                   "hbm_read_bytes_raw": wavg("hbm_read_bytes_raw"), "l2_hit_rate": wavg("l2_hit_rate"),
-                   "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 16-B/lane read correction) + WRITE_SIZE KiB x1024"},
-                  f, indent=2)
+    # the timed kinds (DXRPT_K_TRACE / DXRPT_K_SHADOW): the uninstrumented instantiations of the frame
+    # (packet and per-lane variants), launch-weighted
+    for kind, prefixes in (("k_trace", ("k_trace<false", "k_trace_packet")),
+                           ("k_shadow", ("k_shadow<false", "k_shadow_packet"))):
+        cands = [k for k in out["kernels"] if k.startswith(prefixes)]
+        calls = sum(out["kernels"][k].get("calls", 0) for k in cands)
+
+        def wavg(key):
+            vals = [(out["kernels"][k].get("calls", 0), out["kernels"][k].get(key)) for k in cands]
+            if not calls or any(v is None for _, v in vals):
+                return None
+            return sum(c * v for c, v in vals) / calls
+        with open(f"profiles/{rnd}_pmc_{kind}.json", "w") as f:
+            json.dump({"config": CONFIG, "kernel": " + ".join(sorted(cands)), "calls": calls,
+                       "avg_ms": (sum(out["kernels"][k].get("total_ms", 0.0) for k in cands) / calls) if calls else None,
+                       "per_kernel_avg_ms": {k: out["kernels"][k].get("avg_ms") for k in cands},
+                       "hbm_bytes_per_launch": wavg("hbm_bytes_per_launch"),
+                       "hbm_read_bytes_raw": wavg("hbm_read_bytes_raw"), "l2_hit_rate": wavg("l2_hit_rate"),
+                       "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 16-B/lane read correction) + WRITE_SIZE KiB x1024"},
+                      f, indent=2)
     for src in ("kt/run_kernel_stats.csv",):
         with open(os.path.join(prof, src)) as f, open(f"profiles/{rnd}_kernel_stats.csv", "w") as g:
             g.write(f.read())
