@@ -736,7 +736,13 @@ struct Emit8 {
         int32_t child_node[8];
         std::fill(child_node, child_node + 8, -1);
         for (int s = 0; s < 8; ++s) {
-            if (slot_of[s] < 0) continue;
+            if (slot_of[s] < 0) {  // empty slot: an inverted box the slab test never enters, meta 0
+                for (int k = 0; k < 3; ++k) {
+                    n.qlo[k][s] = 255;
+                    n.qhi[k][s] = 0;
+                }
+                continue;
+            }
             const TNode& c = tree[slot_of[s]];
             for (int k = 0; k < 3; ++k) {
                 double ql = std::floor((double(pb[s].lo[k]) - n.p[k]) / scale[k]);

@@ -70,11 +70,15 @@ struct FrameBuffers {
     uint32_t shadow_slots = 0;     // slots per queue position; shadow shard capacity = shadow_slots * cap_r
 };
 
-// Shard capacity for producers of at most `paths` items (one wave of consumers produces <= 64 per
-// queue; waves w, w + kQueueShards, ... share a shard).
+// Shard capacity for producers of at most `paths` items (one wave of producers adds <= 64 items per
+// queue).  Unbinned: waves w, w + kQueueShards, ... share a shard.  XCD mapping (region_shard): shard
+// 8r + j holds the waves = j (mod 8) of region r, <= ceil(nw / 8) consecutive waves.  The larger of
+// the two (+1 wave of slack) serves both mappings.
 inline uint32_t queue_shard_capacity(uint32_t paths) {
     const uint32_t nw = (paths + 63u) / 64u;
-    return 64u * ((nw + kQueueShards - 1u) / kQueueShards);
+    const uint32_t a = (nw + kQueueShards - 1u) / kQueueShards;
+    const uint32_t b = ((nw + 7u) / 8u + 7u) / 8u;
+    return 64u * ((a > b ? a : b) + 1u);
 }
 
 struct SceneDev {
@@ -128,6 +132,7 @@ struct FrameParams {
     uint32_t shade_occupancy;        // k_shade register budget: 0 compiler default, 6, 7 or 8 waves per SIMD
     uint32_t postpone_tris;          // wave-pool kernels: test pending triangles once this many lanes hold
                                      // some (0 = with their node visit)
+    uint32_t xcd_map;                // 1: XCD-aware queue ranges and region shards (xcd_block / region_shard)
 };
 
 // Kernel sequence of one frame: raygen, then (trace, shade, shadow, resolve) per depth 1..L-1, then

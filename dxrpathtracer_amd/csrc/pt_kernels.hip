@@ -59,6 +59,8 @@ PT_DEV int wrap_coord(int i, uint32_t n) {
     return m < 0 ? m + int(n) : m;
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
 struct Texel4 {
     float r, g, b, a;
 };
@@ -405,7 +407,7 @@ PT_DEV NodeCache node_cache_fill(const SceneDev& S, uint4* lds, uint32_t n) {
 
 // Slot mask of the node's children whose quantised box the ray enters within [tmin, tmx].
 PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx) {
-    const uint4 w0 = W.w0, w1 = W.w1, w2 = W.w2, w3 = W.w3, w4 = W.w4;
+    const uint4 w0 = W.w0, w2 = W.w2, w3 = W.w3, w4 = W.w4;
     const float ax = __uint_as_float((w0.w & 0xFFu) << 23) * R.inv.x;
     const float ay = __uint_as_float(((w0.w >> 8) & 0xFFu) << 23) * R.inv.y;
     const float az = __uint_as_float(((w0.w >> 16) & 0xFFu) << 23) * R.inv.z;
@@ -421,19 +423,22 @@ PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx) {
     const uint32_t ny0 = syn ? w4.x : w2.z, ny1 = syn ? w4.y : w2.w, fy0 = syn ? w2.z : w4.x, fy1 = syn ? w2.w : w4.y;
     const uint32_t nz0 = szn ? w4.z : w3.x, nz1 = szn ? w4.w : w3.y, fz0 = szn ? w3.x : w4.z, fz1 = szn ? w3.y : w4.w;
     uint32_t hm = 0;  // hit children, slot space
+    // near and far plane of one axis in one packed FMA (v_pk_fma_f32): (qn, qf) * (a, a) + (b, b)
+    const f2v A2x = {ax, ax}, A2y = {ay, ay}, A2z = {az, az};
+    const f2v B2x = {bx, bx}, B2y = {by, by}, B2z = {bz, bz};
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
         const uint32_t sh = 8u * uint32_t(c & 3);
-        const float tnx = __builtin_fmaf(float(((c < 4 ? nx0 : nx1) >> sh) & 0xFFu), ax, bx);
-        const float tny = __builtin_fmaf(float(((c < 4 ? ny0 : ny1) >> sh) & 0xFFu), ay, by);
-        const float tnz = __builtin_fmaf(float(((c < 4 ? nz0 : nz1) >> sh) & 0xFFu), az, bz);
-        const float tfx = __builtin_fmaf(float(((c < 4 ? fx0 : fx1) >> sh) & 0xFFu), ax, bx);
-        const float tfy = __builtin_fmaf(float(((c < 4 ? fy0 : fy1) >> sh) & 0xFFu), ay, by);
-        const float tfz = __builtin_fmaf(float(((c < 4 ? fz0 : fz1) >> sh) & 0xFFu), az, bz);
-        const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, R.tmin));
-        const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tmx));
-        const uint32_t m = ((c < 4 ? w1.z : w1.w) >> sh) & 0xFFu;
-        hm |= uint32_t(m != 0u && tn <= tf) << c;
+        const f2v qx = {float(((c < 4 ? nx0 : nx1) >> sh) & 0xFFu), float(((c < 4 ? fx0 : fx1) >> sh) & 0xFFu)};
+        const f2v qy = {float(((c < 4 ? ny0 : ny1) >> sh) & 0xFFu), float(((c < 4 ? fy0 : fy1) >> sh) & 0xFFu)};
+        const f2v qz = {float(((c < 4 ? nz0 : nz1) >> sh) & 0xFFu), float(((c < 4 ? fz0 : fz1) >> sh) & 0xFFu)};
+        const f2v tx = __builtin_elementwise_fma(qx, A2x, B2x);
+        const f2v ty = __builtin_elementwise_fma(qy, A2y, B2y);
+        const f2v tz = __builtin_elementwise_fma(qz, A2z, B2z);
+        const float tn = fmaxf(fmaxf(tx.x, ty.x), fmaxf(tz.x, R.tmin));
+        const float tf = fminf(fminf(tx.y, ty.y), fminf(tz.y, tmx));
+        // empty slots carry inverted boxes (qlo 255, qhi 0: never entered) and meta 0 (no triangles)
+        hm |= uint32_t(tn <= tf) << c;
     }
     return hm;
 }
@@ -743,31 +748,82 @@ PT_DEV uint32_t queue_pos(const uint32_t* __restrict__ cnt, uint32_t cap, uint32
     return s * cap + (i - base);
 }
 
-// Wave-aggregated append to shard (wave % kQueueShards) of a queue: one atomic per wave.  Returns the
+// Wave-aggregated append to `shard` (wave-uniform) of a queue: one atomic per wave.  Returns the
 // position of this lane's item (only meaningful where `want`).  Must be called by all active lanes.
-PT_DEV uint32_t queue_append(uint32_t* counters, uint32_t cap, bool want) {
+PT_DEV uint32_t queue_append(uint32_t* counters, uint32_t cap, bool want, uint32_t shard) {
     const unsigned long long m = __ballot(want);
     const int lane = __lane_id();
     const int leader = __ffsll(static_cast<long long>(__ballot(1))) - 1;
-    const uint32_t shard = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) % kQueueShards;
     uint32_t base = 0;
     if (lane == leader && m != 0ull) base = atomicAdd(&counters[shard], uint32_t(__popcll(m)));
     base = __shfl(base, leader);
     return shard * cap + base + uint32_t(__popcll(m & ((1ull << lane) - 1ull)));
 }
 
-// RaygenShader, RayTrace.hlsl:92-126 (+ SamplePoint 85-90).  Path slot p goes to queue-1 position
-// (shard w % K, offset (w / K) * 64 + lane) of its wave w = p / 64, so the queue layout matches what
-// a wave-ordered append would have produced; the shard counts are analytic.
+// ---- XCD-aware work mapping -----------------------------------------------------------------------
+// MI355X dispatches workgroups round-robin over its 8 XCDs (block b -> XCD b % 8), and each XCD has its
+// own 4 MB L2.  With FrameParams::xcd_map the queue of a pass is cut into 8 contiguous ranges of
+// workgroups and XCD x runs range x (xcd_block), and producers append their rays to the shards of their
+// own range (region_shard: shards 8r .. 8r+7 belong to range r), so range r of every queue holds the
+// paths of one screen region (the primary queue is written in pixel-block order) and each XCD's L2
+// works on the BVH nodes, triangles and texels of its region only.  The b % 8 placement is an
+// affinity, not a guarantee (MI355X_MICROARCH.md): every mapping here is a bijection, so the placement
+// only affects speed.  Without xcd_map: identity blocks, shard = wave % kQueueShards.
+constexpr uint32_t kXcds = 8;
+static_assert(kQueueShards == kXcds * 8u, "xcd_map: 8 shards per XCD range");
+
+// Logical workgroup of this block when nb workgroups cover the pass; false: no work for this block.
+PT_DEV bool xcd_block(bool xcd, uint32_t nb, uint32_t& lb) {
+    const uint32_t b = blockIdx.x;
+    if (!xcd) {
+        lb = b;
+        return b < nb;
+    }
+    const uint32_t x = b % kXcds, k = b / kXcds, q = nb / kXcds, r = nb % kXcds;
+    if (k >= q + (x < r ? 1u : 0u)) return false;
+    lb = x * q + min(x, r) + k;
+    return true;
+}
+
+// Shard of logical wave lw of a pass over nw waves.
+PT_DEV __host__ uint32_t region_shard(bool xcd, uint32_t lw, uint32_t nw) {
+    return xcd ? (uint32_t((uint64_t(lw) * kXcds) / nw) * 8u + (lw & 7u)) : lw % kQueueShards;
+}
+
+// First queue item of this lane (i = lb * blockDim + threadIdx) for a pass over n items; false if the
+// whole workgroup is past the end.  lw_out: the lane's logical wave.
+PT_DEV bool xcd_item(bool xcd, uint32_t n, uint32_t& i, uint32_t& lw) {
+    const uint32_t bd = blockDim.x;
+    uint32_t lb;
+    if (!xcd_block(xcd, (n + bd - 1u) / bd, lb)) return false;
+    i = lb * bd + threadIdx.x;
+    lw = i >> 6;
+    return true;
+}
+
+// RaygenShader, RayTrace.hlsl:92-126 (+ SamplePoint 85-90).  Path slot p goes to the queue-1 position
+// a wave-ordered append of its wave w = p / 64 would have produced (shard region_shard(w), waves of
+// one shard in order); the shard counts are analytic.
 __global__ __launch_bounds__(kBlock) void k_raygen(KArgs A) {
     const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t P = A.P.num_paths;
+    const bool xcd = A.P.xcd_map != 0u;
+    const uint32_t nw = (P + 63u) / 64u;
     if (p == 0) {
-        const uint32_t nw = (P + 63u) / 64u;
         uint32_t* cnt = A.F.counters + 1u * kQueueShards;
-        for (uint32_t s = 0; s < kQueueShards && s < nw; ++s) {
-            uint32_t items = ((nw - 1u - s) / kQueueShards + 1u) * 64u;
-            if ((nw - 1u) % kQueueShards == s) items -= nw * 64u - P;
+        for (uint32_t s = 0; s < kQueueShards; ++s) {
+            uint32_t waves = 0;
+            if (!xcd) {
+                waves = s < nw ? (nw - 1u - s) / kQueueShards + 1u : 0u;
+            } else {  // waves of region r = s / 8 are [ceil(r nw / 8), ceil((r + 1) nw / 8)), those = s mod 8
+                const uint32_t r = s / 8u, sub = s % 8u;
+                const uint32_t b = uint32_t((uint64_t(r) * nw + kXcds - 1u) / kXcds);
+                const uint32_t e = uint32_t((uint64_t(r + 1u) * nw + kXcds - 1u) / kXcds);
+                const uint32_t f = b + ((sub + 8u - b % 8u) % 8u);
+                waves = f < e ? (e - 1u - f) / 8u + 1u : 0u;
+            }
+            uint32_t items = waves * 64u;
+            if (nw > 0u && region_shard(xcd, nw - 1u, nw) == s) items -= nw * 64u - P;
             cnt[s] = items;
         }
     }
@@ -815,7 +871,15 @@ __global__ __launch_bounds__(kBlock) void k_raygen(KArgs A) {
     const f3 dir = normalize3(diff);
     const float rayLength = len3(diff);
     const uint32_t w = p >> 6;
-    const uint32_t pos = (w % kQueueShards) * A.F.cap_r + (w / kQueueShards) * 64u + (p & 63u);
+    uint32_t widx;  // index of wave w among the waves of its shard
+    if (!xcd) {
+        widx = w / kQueueShards;
+    } else {
+        const uint32_t r = uint32_t((uint64_t(w) * kXcds) / nw);
+        const uint32_t b = uint32_t((uint64_t(r) * nw + kXcds - 1u) / kXcds);
+        widx = (w - (b + ((w % 8u + 8u - b % 8u) % 8u))) / 8u;
+    }
+    const uint32_t pos = region_shard(xcd, w, nw) * A.F.cap_r + widx * 64u + (p & 63u);
     const RayQueue& Q = A.F.q[1];
     Q.org[pos] = make_float4(start.x, start.y, start.z, rayLength);
     Q.dir[pos] = make_float4(dir.x, dir.y, dir.z, bitsf(p));
@@ -835,9 +899,10 @@ void k_trace(KArgs A, int depth) {
     if (W == 8 && !kCount && (kPipe & 4))  // LDS node cache: a separate instantiation, so that the
         // default kernels' node loads are plain global loads (no LDS/global pointer select -> flat loads)
         nc = node_cache_fill(A.S, reinterpret_cast<uint4*>(stack + A.S.stack_ints * blockDim.x), A.P.lds_nodes);
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t* cnt = radiance_counts(A.F, depth);
-    if (i >= queue_total(cnt)) return;
+    const uint32_t n = queue_total(cnt);
+    uint32_t i, lw;
+    if (!xcd_item(A.P.xcd_map != 0u, n, i, lw) || i >= n) return;
     const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
     const float4 o4 = A.F.q[depth & 1].org[pos];
     const float4 d4 = A.F.q[depth & 1].dir[pos];
@@ -874,9 +939,13 @@ PT_DEV bool nonzero3(f3 c) { return !(c.x == 0.0f && c.y == 0.0f && c.z == 0.0f)
 template <int kOcc>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
 void k_shade(KArgs A, int depth) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t* cnt = radiance_counts(A.F, depth);
-    if (i >= queue_total(cnt)) return;
+    const uint32_t nq = queue_total(cnt);
+    const bool xcd = A.P.xcd_map != 0u;
+    uint32_t i, lw;
+    if (!xcd_item(xcd, nq, i, lw) || i >= nq) return;
+    // the wave's shard in the queues it produces (all lanes of a wave share lw)
+    const uint32_t shard = region_shard(xcd, lw, (nq + 63u) / 64u);
     const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
     const dxrpt_app_settings& set = A.P.set;
     const dxrpt_ray_trace_constants& rtc = A.P.rtc;
@@ -1074,7 +1143,6 @@ void k_shade(KArgs A, int depth) {
             total += uint32_t(__popcll(m));
         }
         const int leader = __ffsll(static_cast<long long>(__ballot(1))) - 1;
-        const uint32_t shard = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) % kQueueShards;
         uint32_t base = 0;
         if (lane == leader && total != 0u) base = atomicAdd(&shcnt[shard], total);
         base = uint32_t(__shfl(int(base), leader)) + shard * cap_s;
@@ -1085,7 +1153,7 @@ void k_shade(KArgs A, int depth) {
             base += uint32_t(__popcll(m));
         }
     }
-    const uint32_t npos = queue_append(A.F.counters + uint32_t(depth + 1) * kQueueShards, A.F.cap_r, cont);
+    const uint32_t npos = queue_append(A.F.counters + uint32_t(depth + 1) * kQueueShards, A.F.cap_r, cont, shard);
     if (cont) {
         const RayQueue& N = A.F.q[(depth + 1) & 1];
         N.org[npos] = make_float4(nextOrigin.x, nextOrigin.y, nextOrigin.z, kFP32Max);
@@ -1114,7 +1182,10 @@ void k_shadow(KArgs A, int depth) {
     const uint32_t count = queue_total(cnt);
     const uint32_t cap_s = A.F.shadow_slots * A.F.cap_r;
     uint32_t nv = 0, nt = 0;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < count; i += gridDim.x * blockDim.x) {
+    uint32_t lb;
+    const uint32_t nb = min((count + blockDim.x - 1u) / blockDim.x, gridDim.x);
+    if (!xcd_block(A.P.xcd_map != 0u, nb, lb)) return;
+    for (uint32_t i = lb * blockDim.x + threadIdx.x; i < count; i += gridDim.x * blockDim.x) {
         const uint32_t slot = A.F.sh_queue[queue_pos(cnt, cap_s, i)];
         const float4 o4 = A.F.sh_org[slot];
         const float4 d4 = A.F.sh_dir[slot];
@@ -1135,10 +1206,10 @@ void k_shadow(KArgs A, int depth) {
 template <int kOcc>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
 void k_trace_packet(KArgs A, int depth) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t* cnt = radiance_counts(A.F, depth);
     const uint32_t n = queue_total(cnt);
-    if ((i & ~63u) >= n) return;
+    uint32_t i, lw;
+    if (!xcd_item(A.P.xcd_map != 0u, n, i, lw) || (i & ~63u) >= n) return;
     const bool live = i < n;
     const uint32_t pos = live ? queue_pos(cnt, A.F.cap_r, i) : 0u;
     float4 o4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d4 = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
@@ -1156,10 +1227,10 @@ void k_trace_packet(KArgs A, int depth) {
 template <int kOcc>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
 void k_shadow_packet(KArgs A, int depth) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t* cnt = shadow_counts(A.F, depth);
     const uint32_t n = queue_total(cnt);
-    if ((i & ~63u) >= n) return;
+    uint32_t i, lw;
+    if (!xcd_item(A.P.xcd_map != 0u, n, i, lw) || (i & ~63u) >= n) return;
     const bool live = i < n;
     const uint32_t cap_s = A.F.shadow_slots * A.F.cap_r;
     const uint32_t slot = live ? A.F.sh_queue[queue_pos(cnt, cap_s, i)] : 0u;

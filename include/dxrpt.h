@@ -295,6 +295,11 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 #define DXRPT_OPT_KERNEL_TIMING_MASK 20u /* kernel kinds bracketed by events when DXRPT_OPT_KERNEL_TIMING is on
                                             (bit 1 << DXRPT_K_*, default all); the frame span is always timed.
                                             Fewer events, less timing overhead in the measured frames. */
+#define DXRPT_OPT_XCD_MAPPING 21u   /* 1: each pass's queue is cut into 8 ranges run by the 8 XCDs (workgroup
+                                         b -> XCD b % 8) and rays are queued by screen region, so each XCD's L2
+                                         serves one region of the image; 0 (default): dispatch order (all XCDs
+                                         sweep the image together, which measured faster: no load imbalance
+                                         between regions).  Identical results. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

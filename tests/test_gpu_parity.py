@@ -271,6 +271,40 @@ def test_traversal_variants_are_bit_identical(torch_cuda, packet, pipe, lds):
         np.testing.assert_array_equal(got, ref)
 
 
+@pytest.mark.parametrize("packet,shadow_grid", [(0, 0), (1, 0), (15, 0), (1, 64)])
+def test_xcd_mapping_is_bit_identical(torch_cuda, packet, shadow_grid):
+    # DXRPT_OPT_XCD_MAPPING (per-XCD queue ranges, region shards) only changes which workgroup takes
+    # which ray and the queue order: frames must equal dispatch-order queues bit for bit, for L=8 paths,
+    # odd image sizes (partial waves, partial regions) and several shadow rays per vertex (spot lights)
+    torch = torch_cuda
+    for name, W, H in (("sponza", 400, 224), ("suntemple", 333, 187), ("boxtest", 97, 61)):
+        sc, sky = scene_bundle(name)
+        st = sc.settings(MaxPathLength=8)
+        rtc = D.make_constants(sc, st, sky, W, H, 5)
+        lights = D.make_lights(sc)
+        if name == "boxtest":
+            for i, (p, d) in enumerate([((1.5, 4.0, -2.0), (0.3, 1.0, -0.4)), ((-2.5, 1.5, -1.5), (-0.8, 0.2, -0.5))]):
+                L = lights.Lights[i]
+                L.Position[:] = p
+                L.Direction[:] = d
+                L.Intensity[:] = (50.0, 45.0, 37.5)
+                L.AngularAttenuationX, L.AngularAttenuationY, L.Range = 0.99, 0.95, 7.5
+            rtc.NumLights = 2
+        t = tracer(name)
+        t.set_option(A.OPT_PACKET_TRAVERSAL, packet)
+        t.set_option(A.OPT_SHADOW_GRID, shadow_grid)
+        try:
+            t.set_option(A.OPT_XCD_MAPPING, 0)
+            ref = gpu_render(torch, name, W, H, st, 5, rtc=rtc, lights=lights).cpu().numpy()
+            t.set_option(A.OPT_XCD_MAPPING, 1)
+            got = gpu_render(torch, name, W, H, st, 5, rtc=rtc, lights=lights).cpu().numpy()
+        finally:
+            t.set_option(A.OPT_XCD_MAPPING, A.DEFAULT_XCD_MAPPING)
+            t.set_option(A.OPT_PACKET_TRAVERSAL, A.DEFAULT_PACKET_TRAVERSAL)
+            t.set_option(A.OPT_SHADOW_GRID, 0)
+        np.testing.assert_array_equal(got, ref)
+
+
 def _random_rays(rng, n, lo, hi):
     o = rng.uniform(lo, hi, size=(n, 3)).astype(np.float32)
     d = rng.standard_normal((n, 3)).astype(np.float32)
