@@ -77,13 +77,14 @@ KERNEL_NAMES = ("k_raygen", "k_trace", "k_shade", "k_shadow", "k_accumulate", "k
 (OPT_COUNT_TRAVERSAL, OPT_KERNEL_TIMING, OPT_BVH_WIDTH, OPT_TRAVERSAL_MODE, OPT_REFILL_LANES, OPT_CHUNKS_PER_WAVE,
  OPT_POSTPONE_TRIS, OPT_TRACE_BLOCK, OPT_OCCUPANCY, OPT_SHADE_BLOCK, OPT_SHADE_OCCUPANCY, OPT_SPATIAL_SPLITS,
  OPT_LEAF_COST, OPT_SHADOW_OCCUPANCY, OPT_SHADOW_GRID, OPT_CONCURRENCY, OPT_TRAVERSAL_PIPELINE, OPT_PACKET_TRAVERSAL, OPT_LDS_NODES,
- OPT_KERNEL_TIMING_MASK, OPT_XCD_MAPPING) = range(1, 22)
+ OPT_KERNEL_TIMING_MASK, OPT_XCD_MAPPING, OPT_PACKET_SWITCH) = range(1, 23)
 # context defaults of the traversal options (dxrpt_api.hip)
 DEFAULT_TRAVERSAL_PIPELINE = 0
 POST_FLOAT4, POST_RGBA8 = 0, 1  # dxrpt_post_process output formats
 DEFAULT_PACKET_TRAVERSAL = 1
 DEFAULT_LDS_NODES = 0
 DEFAULT_XCD_MAPPING = 0
+DEFAULT_PACKET_SWITCH = 0
 
 
 class Stats(C.Structure):

@@ -111,6 +111,7 @@ struct dxrpt_ctx {
     uint32_t opt_shade_block = 256; // DXRPT_OPT_SHADE_BLOCK
     uint32_t opt_shade_occ = 0;     // DXRPT_OPT_SHADE_OCCUPANCY
     uint32_t opt_xcd = 0;           // DXRPT_OPT_XCD_MAPPING
+    uint32_t opt_packet_switch = 0; // DXRPT_OPT_PACKET_SWITCH
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
     int built_width = 0;
     DevBuf d_trav;   // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
@@ -439,6 +440,9 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_XCD_MAPPING) {
             require(value <= 1, "dxrpt_set_option: XCD mapping must be 0 or 1");
             ctx->opt_xcd = uint32_t(value);
+        } else if (option == DXRPT_OPT_PACKET_SWITCH) {
+            require(value <= 100, "dxrpt_set_option: packet switch threshold must be 0..100 (percent)");
+            ctx->opt_packet_switch = uint32_t(value);
         } else if (option == DXRPT_OPT_BVH_WIDTH) {
             require(value == 2 || value == 8, "dxrpt_set_option: BVH width must be 2 or 8");
             ctx->opt_width = int(value);  // takes effect at the next dxrpt_build_bvh
@@ -708,6 +712,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.shade_block = ctx->opt_shade_block;
         fp.shade_occupancy = ctx->opt_shade_occ;
         fp.xcd_map = ctx->opt_xcd;
+        fp.packet_switch = ctx->opt_packet_switch;
         hipStream_t s = static_cast<hipStream_t>(stream);
         if (ctx->opt_count) {
             fp.trav = ctx->d_trav.as<unsigned long long>();

@@ -133,6 +133,7 @@ struct FrameParams {
     uint32_t postpone_tris;          // wave-pool kernels: test pending triangles once this many lanes hold
                                      // some (0 = with their node visit)
     uint32_t xcd_map;                // 1: XCD-aware queue ranges and region shards (xcd_block / region_shard)
+    uint32_t packet_switch;          // packet traversal: fall back to one ray per lane below this coherence (%)
 };
 
 // Kernel sequence of one frame: raygen, then (trace, shade, shadow, resolve) per depth 1..L-1, then

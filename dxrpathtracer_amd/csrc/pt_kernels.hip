@@ -597,12 +597,24 @@ PT_DEV uint32_t wave_or8(uint32_t m) {
 
 // `live`: this lane holds a ray (lanes past the end of the queue join with live = false).  Returns
 // this lane's result like traverse8 (h.tri != kMiss: hit / occluded).
+// Adaptive mode (switch_pct > 0): the wave tracks the fraction of its live lanes that enter some child
+// of each visited node; once that fraction, over all visits so far (>= kSwitchMinVisits), falls below
+// switch_pct percent, the packet is incoherent and the wave continues one ray per lane (traverse8_from
+// from the root, keeping each lane's best hit as its bound: it tests every triangle the lane's own
+// traversal would, so the result is still that of traverse8).
+constexpr uint32_t kSwitchMinVisits = 4;
+
 template <bool kAnyHit>
-PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, bool live, HitRec& h) {
+PT_DEV bool traverse8_from(const SceneDev& S, const Ray8& R, lds_int* stk, HitRec& h);
+
+template <bool kAnyHit>
+PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, bool live, HitRec& h,
+                             uint32_t switch_pct = 0u, lds_int* stk = nullptr) {
     Ray8 R;
     ray8_init(R, o, d, tmin, tmax, alpha, h);
     unsigned long long lv = __ballot(live);
     if (lv == 0ull) return false;
+    uint32_t visits = 0, lanes_live = 0, lanes_useful = 0;  // wave-uniform coherence census
     // key order of the first live lane's octant for the whole wave (any order gives the same results)
     const uint32_t oct = uint32_t(__builtin_amdgcn_readlane(int(R.oct), __ffsll(static_cast<long long>(lv)) - 1));
     const uint32_t lane = uint32_t(__lane_id());
@@ -613,6 +625,15 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
         const Node8Words W = load_node8_uniform(S, node);
         const uint32_t hm = live ? box8_hits(R, W, h.t) : 0u;
         const uint32_t um = wave_or8(hm);
+        if (switch_pct) {
+            ++visits;
+            lanes_live += uint32_t(__popcll(__ballot(live)));
+            lanes_useful += uint32_t(__popcll(__ballot(hm != 0u)));
+            if (visits >= kSwitchMinVisits && lanes_useful * 100u < lanes_live * switch_pct) {
+                if (live) traverse8_from<kAnyHit>(S, R, stk, h);
+                return h.tri != kMiss;
+            }
+        }
         const uint32_t imask = W.w0.w >> 24;
         // leaf triangles hit by any lane: (count << 5) | offset per leaf slot
         uint32_t tbits = 0;
@@ -685,6 +706,17 @@ PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
     int sp = 0;
     uint2 tos = make_uint2(0u, 0u);
     while (!trav8_step<kAnyHit, kCount>(S, R, node, sp, stk, tos, h, nvisit, ntest, nc)) {
+    }
+    return h.tri != kMiss;
+}
+
+// Per-lane traversal from the root with the lane's current best hit kept as the bound.
+template <bool kAnyHit>
+PT_DEV bool traverse8_from(const SceneDev& S, const Ray8& R, lds_int* stk, HitRec& h) {
+    uint32_t node = 0, nv = 0, nt = 0;
+    int sp = 0;
+    uint2 tos = make_uint2(0u, 0u);
+    while (!trav8_step<kAnyHit, false>(S, R, node, sp, stk, tos, h, nv, nt, NodeCache{nullptr, 0u})) {
     }
     return h.tri != kMiss;
 }
@@ -1220,7 +1252,8 @@ void k_trace_packet(KArgs A, int depth) {
     const float tmin = depth == 1 ? 0.0f : kRayTMin;
     const bool alpha = depth <= A.P.set.MaxAnyHitPathLength;
     HitRec h;
-    traverse8_packet<false>(A.S, ld3(o4), ld3(d4), tmin, o4.w, alpha, live, h);
+    extern __shared__ int stack[];  // per-lane stacks for the adaptive fallback (FrameParams::packet_switch)
+    traverse8_packet<false>(A.S, ld3(o4), ld3(d4), tmin, o4.w, alpha, live, h, A.P.packet_switch, lane_stack(A.S, stack));
     if (live) A.F.hit[pos] = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
 }
 
@@ -1241,7 +1274,9 @@ void k_shadow_packet(KArgs A, int depth) {
         c4 = A.F.sh_con[slot];
     }
     HitRec h;
-    const bool occluded = traverse8_packet<true>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live, h);
+    extern __shared__ int stack[];
+    const bool occluded = traverse8_packet<true>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live, h,
+                                                 A.P.packet_switch, lane_stack(A.S, stack));
     if (live && occluded) A.F.sh_con[slot] = make_float4(c4.x * 0.0f, c4.y * 0.0f, c4.z * 0.0f, c4.w);
 }
 
@@ -1490,13 +1525,13 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
         if (w8 && !count && (fp.packet & pbit)) {
             const uint32_t occ = shadow ? fp.shadow_occupancy : fp.occupancy;
             if (shadow) {
-                if (occ == 7) hipLaunchKernelGGL((k_shadow_packet<7>), dim3(G), dim3(tb), 0, st, A, d);
-                else if (occ == 8) hipLaunchKernelGGL((k_shadow_packet<8>), dim3(G), dim3(tb), 0, st, A, d);
-                else hipLaunchKernelGGL((k_shadow_packet<0>), dim3(G), dim3(tb), 0, st, A, d);
+                if (occ == 7) hipLaunchKernelGGL((k_shadow_packet<7>), dim3(G), dim3(tb), ldst, st, A, d);
+                else if (occ == 8) hipLaunchKernelGGL((k_shadow_packet<8>), dim3(G), dim3(tb), ldst, st, A, d);
+                else hipLaunchKernelGGL((k_shadow_packet<0>), dim3(G), dim3(tb), ldst, st, A, d);
             } else {
-                if (occ == 7) hipLaunchKernelGGL((k_trace_packet<7>), dim3(G), dim3(tb), 0, st, A, d);
-                else if (occ == 8) hipLaunchKernelGGL((k_trace_packet<8>), dim3(G), dim3(tb), 0, st, A, d);
-                else hipLaunchKernelGGL((k_trace_packet<0>), dim3(G), dim3(tb), 0, st, A, d);
+                if (occ == 7) hipLaunchKernelGGL((k_trace_packet<7>), dim3(G), dim3(tb), ldst, st, A, d);
+                else if (occ == 8) hipLaunchKernelGGL((k_trace_packet<8>), dim3(G), dim3(tb), ldst, st, A, d);
+                else hipLaunchKernelGGL((k_trace_packet<0>), dim3(G), dim3(tb), ldst, st, A, d);
             }
             return;
         }

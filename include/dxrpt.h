@@ -300,6 +300,9 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                          serves one region of the image; 0 (default): dispatch order (all XCDs
                                          sweep the image together, which measured faster: no load imbalance
                                          between regions).  Identical results. */
+#define DXRPT_OPT_PACKET_SWITCH 22u /* packet traversal: a wave whose share of live lanes entering the visited
+                                         nodes falls below this percentage continues one ray per lane
+                                         (0 = never).  Identical results. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

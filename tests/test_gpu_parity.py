@@ -242,12 +242,15 @@ def test_traversal_launch_options_are_bit_identical(torch_cuda, block, occ, sblo
     np.testing.assert_array_equal(got, ref)
 
 
-@pytest.mark.parametrize("packet,pipe,lds", [(0, 1, 0), (0, 2, 0), (0, 3, 0), (1, 0, 0), (2, 0, 0), (3, 0, 0), (12, 0, 0),
-                                             (15, 0, 0), (15, 3, 0), (0, 0, 73), (1, 3, 256), (0, 0, 1024)])
-def test_traversal_variants_are_bit_identical(torch_cuda, packet, pipe, lds):
+@pytest.mark.parametrize("packet,pipe,lds,switch", [(0, 1, 0, 0), (0, 2, 0, 0), (0, 3, 0, 0), (1, 0, 0, 0), (2, 0, 0, 0),
+                                                    (3, 0, 0, 0), (12, 0, 0, 0), (15, 0, 0, 0), (15, 3, 0, 0),
+                                                    (0, 0, 73, 0), (1, 3, 256, 0), (0, 0, 1024, 0), (15, 0, 0, 30),
+                                                    (3, 0, 0, 60), (15, 0, 0, 100)])
+def test_traversal_variants_are_bit_identical(torch_cuda, packet, pipe, lds, switch):
     # DXRPT_OPT_PACKET_TRAVERSAL (wave-coherent traversal with scalar node/triangle loads) and
     # DXRPT_OPT_TRAVERSAL_PIPELINE (paired triangle loads, next-node prefetch) and DXRPT_OPT_LDS_NODES
-    # (top of the tree read from LDS) change which triangles a
+    # (top of the tree read from LDS) and DXRPT_OPT_PACKET_SWITCH (packet waves that turn incoherent
+    # continue one ray per lane) change which triangles a
     # lane tests and when, never the closest (t, id) or the occlusion boolean: frames must equal the
     # per-lane traversal bit for bit (SunTemple: alpha-tested any-hit at depth 1)
     torch = torch_cuda
@@ -263,8 +266,10 @@ def test_traversal_variants_are_bit_identical(torch_cuda, packet, pipe, lds):
             t.set_option(A.OPT_PACKET_TRAVERSAL, packet)
             t.set_option(A.OPT_TRAVERSAL_PIPELINE, pipe)
             t.set_option(A.OPT_LDS_NODES, lds)
+            t.set_option(A.OPT_PACKET_SWITCH, switch)
             got = gpu_render(torch, name, 480, 270, st, 4).cpu().numpy()
         finally:
+            t.set_option(A.OPT_PACKET_SWITCH, A.DEFAULT_PACKET_SWITCH)
             t.set_option(A.OPT_PACKET_TRAVERSAL, A.DEFAULT_PACKET_TRAVERSAL)
             t.set_option(A.OPT_TRAVERSAL_PIPELINE, A.DEFAULT_TRAVERSAL_PIPELINE)
             t.set_option(A.OPT_LDS_NODES, A.DEFAULT_LDS_NODES)
