@@ -21,7 +21,7 @@ DXRPT_MAX_SPOT_LIGHTS = 32
 DXRPT_MAX_PATH_LENGTH = 8
 TEX_RGBA8_UNORM, TEX_RGBA8_SRGB, TEX_R8_UNORM = 0, 1, 2
 TRACE_ANY_HIT, TRACE_ALPHA = 1, 2
-SCENE_SPONZA, SCENE_SUNTEMPLE, SCENE_BOXTEST, SCENE_WHITEFURNACE = 0, 1, 2, 3
+SCENE_SPONZA, SCENE_SUNTEMPLE, SCENE_BOXTEST, SCENE_WHITEFURNACE, SCENE_STRONGHOLD = 0, 1, 2, 3, 4
 
 
 class MeshVertex(C.Structure):
@@ -107,6 +107,11 @@ class HostTexture(C.Structure):
     _fields_ = [("width", u32), ("height", u32), ("fmt", u32), ("pad", u32), ("texels", C.c_void_p)]
 
 
+class ModelLoadSettings(C.Structure):
+    _fields_ = [("file_path", C.c_char_p), ("texture_dir", C.c_char_p), ("scene_scale", f32), ("force_srgb", u32),
+                ("merge_meshes", u32)]
+
+
 class HostScene(C.Structure):
     _fields_ = [("vertices", C.POINTER(MeshVertex)), ("num_vertices", u32), ("idx_bytes", u32),
                 ("indices", C.c_void_p), ("num_indices", u32), ("num_geometries", u32),
@@ -127,7 +132,7 @@ DXRPT_SYMBOLS = ("dxrpt_abi_version", "dxrpt_default_settings", "dxrpt_create", 
                  "dxrpt_set_scene", "dxrpt_add_texture", "dxrpt_set_sky", "dxrpt_build_bvh", "dxrpt_get_bvh_info",
                  "dxrpt_render", "dxrpt_get_stats", "dxrpt_trace_rays", "dxrpt_set_option", "dxrpt_reset_timing",
                  "dxrpt_post_process")
-DXRPT_HOST_SYMBOLS = ("dxrpt_host_scene_create", "dxrpt_host_scene_destroy", "dxrpt_host_last_error",
+DXRPT_HOST_SYMBOLS = ("dxrpt_host_scene_create", "dxrpt_host_scene_load", "dxrpt_host_scene_destroy", "dxrpt_host_last_error",
                       "dxrpt_host_inv_view_projection", "dxrpt_host_sky_create", "dxrpt_host_fill_constants",
                       "dxrpt_host_float_to_half", "dxrpt_host_half_to_float", "dxrpt_host_hosek_load",
                       "dxrpt_host_hosek_destroy", "dxrpt_host_hosek_last_error", "dxrpt_host_sky_create_hosek",
@@ -183,6 +188,7 @@ def host() -> C.CDLL:
         H = _load("libdxrpt_host.so")
         P = C.c_void_p
         H.dxrpt_host_scene_create.argtypes = [u32, C.c_uint64, u32, C.POINTER(C.POINTER(HostScene))]
+        H.dxrpt_host_scene_load.argtypes = [u32, C.POINTER(ModelLoadSettings), C.POINTER(C.POINTER(HostScene))]
         H.dxrpt_host_scene_destroy.argtypes = [C.POINTER(HostScene)]
         H.dxrpt_host_scene_destroy.restype = None
         H.dxrpt_host_last_error.restype = C.c_char_p

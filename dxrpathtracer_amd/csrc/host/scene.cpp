@@ -279,6 +279,59 @@ void SceneBuilder::cloth(V3 top_left, V3 axis, float width, float height, int nu
 
 }  // namespace dxrpt_host
 
+namespace dxrpt_host {
+size_t load_fbx_scene(const std::string& path, const std::string& texture_dir, float scene_scale, bool force_srgb,
+                      SceneBuilder& B);
+namespace {
+// SceneCameraPositions / Rotations / SunDirections, DXRPathTracer.cpp:96-98 (index = Scenes enum)
+const float kCamPos[DXRPT_SCENE_COUNT][3] = {{-11.5f, 1.85f, -0.45f}, {-1.0f, 5.5f, 12.0f}, {0.0f, 2.5f, -10.0f},
+                                             {0.0f, 0.0f, -3.0f}, {0.0f, 0.0f, -30.0f}};
+const float kCamRot[DXRPT_SCENE_COUNT][2] = {{0.0f, 1.544f}, {0.2f, 3.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};
+const float kSunDir[DXRPT_SCENE_COUNT][3] = {{0.26f, 0.987f, -0.16f}, {-0.133022308f, 0.642787635f, 0.75440651f},
+                                             {0.26f, 0.987f, -0.16f}, {0.0f, 1.0f, 0.0f}, {-0.218f, 0.5f, -0.839f}};
+
+// Fills the public view of a built scene.
+void publish(SceneStore& St, uint32_t scene_id, uint64_t seed, bool idx16) {
+    SceneBuilder& B = St.B;
+    dxrpt_host_scene& P = St.pub;
+    P.scene_id = scene_id;
+    P.seed = seed;
+    std::memcpy(P.camera_position, kCamPos[scene_id], sizeof(P.camera_position));
+    std::memcpy(P.camera_rotation, kCamRot[scene_id], sizeof(P.camera_rotation));
+    std::memcpy(P.sun_direction, kSunDir[scene_id], sizeof(P.sun_direction));
+    P.white_furnace = scene_id == DXRPT_SCENE_WHITEFURNACE ? 1u : 0u;  // DXRPathTracer.cpp:935
+    P.vertices = B.vertices.data();
+    P.num_vertices = uint32_t(B.vertices.size());
+    if (idx16) {
+        St.idx16.assign(B.indices.begin(), B.indices.end());
+        P.idx_bytes = 2;
+        P.indices = St.idx16.data();
+    } else {
+        P.idx_bytes = 4;
+        P.indices = B.indices.data();
+    }
+    P.num_indices = uint32_t(B.indices.size());
+    P.geometries = B.geos.data();
+    P.num_geometries = uint32_t(B.geos.size());
+    P.materials = B.mats.data();
+    P.num_materials = uint32_t(B.mats.size());
+    St.views.resize(B.textures.size());
+    for (size_t i = 0; i < B.textures.size(); ++i) {
+        St.views[i].width = B.textures[i].w;
+        St.views[i].height = B.textures[i].h;
+        St.views[i].fmt = B.textures[i].fmt;
+        St.views[i].texels = B.textures[i].data.data();
+    }
+    P.textures = St.views.data();
+    P.num_textures = uint32_t(St.views.size());
+    P.spot_lights = B.lights.empty() ? nullptr : B.lights.data();
+    P.num_spot_lights = uint32_t(B.lights.size());
+    P.num_triangles = B.indices.size() / 3;
+    P.internal = &St;
+}
+}  // namespace
+}  // namespace dxrpt_host
+
 using namespace dxrpt_host;
 
 extern "C" {
@@ -291,14 +344,6 @@ int dxrpt_host_scene_create(uint32_t scene_id, uint64_t seed, uint32_t detail, d
     try {
         std::unique_ptr<SceneStore> S(new SceneStore());
         SceneBuilder& B = S->B;
-        dxrpt_host_scene& P = S->pub;
-        P.scene_id = scene_id;
-        P.seed = seed;
-        // SceneCameraPositions / Rotations / SunDirections, DXRPathTracer.cpp:96-98
-        static const float cam_pos[4][3] = {{-11.5f, 1.85f, -0.45f}, {-1.0f, 5.5f, 12.0f}, {0.0f, 2.5f, -10.0f}, {0.0f, 0.0f, -3.0f}};
-        static const float cam_rot[4][2] = {{0.0f, 1.544f}, {0.2f, 3.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};
-        static const float sun_dir[4][3] = {{0.26f, 0.987f, -0.16f}, {-0.133022308f, 0.642787635f, 0.75440651f},
-                                            {0.26f, 0.987f, -0.16f}, {0.0f, 1.0f, 0.0f}};
         switch (scene_id) {
             case DXRPT_SCENE_SPONZA: build_sponza_proxy(B, seed, detail); break;
             case DXRPT_SCENE_SUNTEMPLE: build_suntemple_proxy(B, seed, detail); break;
@@ -306,43 +351,46 @@ int dxrpt_host_scene_create(uint32_t scene_id, uint64_t seed, uint32_t detail, d
             case DXRPT_SCENE_WHITEFURNACE: build_whitefurnace_proxy(B); break;
             default: g_last_error = "dxrpt_host_scene_create: unknown scene id"; return DXRPT_E_INVALID_ARG;
         }
-        std::memcpy(P.camera_position, cam_pos[scene_id], sizeof(P.camera_position));
-        std::memcpy(P.camera_rotation, cam_rot[scene_id], sizeof(P.camera_rotation));
-        std::memcpy(P.sun_direction, sun_dir[scene_id], sizeof(P.sun_direction));
-        P.white_furnace = scene_id == DXRPT_SCENE_WHITEFURNACE ? 1u : 0u;
-        P.vertices = B.vertices.data();
-        P.num_vertices = uint32_t(B.vertices.size());
-        if (scene_id == DXRPT_SCENE_BOXTEST) {  // IndexType::Index16Bit (Model.cpp:770)
-            S->idx16.assign(B.indices.begin(), B.indices.end());
-            P.idx_bytes = 2;
-            P.indices = S->idx16.data();
-        } else {
-            P.idx_bytes = 4;
-            P.indices = B.indices.data();
-        }
-        P.num_indices = uint32_t(B.indices.size());
-        P.geometries = B.geos.data();
-        P.num_geometries = uint32_t(B.geos.size());
-        P.materials = B.mats.data();
-        P.num_materials = uint32_t(B.mats.size());
-        S->views.resize(B.textures.size());
-        for (size_t i = 0; i < B.textures.size(); ++i) {
-            S->views[i].width = B.textures[i].w;
-            S->views[i].height = B.textures[i].h;
-            S->views[i].fmt = B.textures[i].fmt;
-            S->views[i].texels = B.textures[i].data.data();
-        }
-        P.textures = S->views.data();
-        P.num_textures = uint32_t(S->views.size());
-        P.spot_lights = B.lights.empty() ? nullptr : B.lights.data();
-        P.num_spot_lights = uint32_t(B.lights.size());
-        P.num_triangles = B.indices.size() / 3;
-        P.internal = S.get();
+        // IndexType::Index16Bit for BoxTest (Model.cpp:770)
+        publish(*S, scene_id, seed, scene_id == DXRPT_SCENE_BOXTEST);
         *out = &S.release()->pub;
         return DXRPT_OK;
     } catch (const std::exception& e) {
         g_last_error = e.what();
         return DXRPT_E_OOM;
+    }
+}
+
+int dxrpt_host_scene_load(uint32_t scene_id, const dxrpt_host_model_settings* settings, dxrpt_host_scene** out) {
+    if (!out || !settings || !settings->file_path) return DXRPT_E_INVALID_ARG;
+    *out = nullptr;
+    try {
+        if (scene_id >= DXRPT_SCENE_COUNT) {
+            g_last_error = "dxrpt_host_scene_load: unknown scene id";
+            return DXRPT_E_INVALID_ARG;
+        }
+        if (settings->merge_meshes) {
+            g_last_error = "dxrpt_host_scene_load: MergeMeshes (PreTransformVertices) is not supported";
+            return DXRPT_E_INVALID_ARG;
+        }
+        std::unique_ptr<SceneStore> S(new SceneStore());
+        // ModelLoadSettings::TextureDir is relative to the model file's directory (Model.cpp:551)
+        std::string path = settings->file_path;
+        const size_t slash = path.find_last_of('/');
+        std::string dir = slash == std::string::npos ? std::string() : path.substr(0, slash + 1);
+        std::string tdir = dir;
+        if (settings->texture_dir && settings->texture_dir[0]) {
+            tdir = dir + settings->texture_dir;
+            if (tdir.back() != '/') tdir += '/';
+        }
+        const size_t max_indices =
+            load_fbx_scene(path, tdir, settings->scene_scale, settings->force_srgb != 0, S->B);
+        publish(*S, scene_id, 0, max_indices <= 0xFFFF);  // Model.cpp:561-573
+        *out = &S.release()->pub;
+        return DXRPT_OK;
+    } catch (const std::exception& e) {
+        g_last_error = e.what();
+        return DXRPT_E_INVALID_ARG;
     }
 }
 

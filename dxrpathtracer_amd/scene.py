@@ -16,7 +16,16 @@ from . import _abi as A
 
 SPONZA_SEED = 0x53504F4E5A41  # "SPONZA" 
 SCENE_NAMES = {"sponza": A.SCENE_SPONZA, "suntemple": A.SCENE_SUNTEMPLE, "boxtest": A.SCENE_BOXTEST,
-               "whitefurnace": A.SCENE_WHITEFURNACE}
+               "whitefurnace": A.SCENE_WHITEFURNACE, "stronghold": A.SCENE_STRONGHOLD}
+# The reference's asset table (DXRPathTracer.cpp:83-95): model path (relative to the reference checkout's
+# Content/Models), texture dir (relative to the model), scene scale.  Sponza / SunTemple are absent from
+# the snapshot (procedural proxies); Stronghold is theInn.fbx.
+SCENE_ASSETS = {
+    A.SCENE_SPONZA: ("Sponza/Sponza_NoSpotLight.fbx", None, 0.01),
+    A.SCENE_SUNTEMPLE: ("SunTemple/SunTemple.fbx", "Textures", 0.005),
+    A.SCENE_WHITEFURNACE: ("WhiteFurnace/WhiteFurnace.fbx", None, 1.0),
+    A.SCENE_STRONGHOLD: ("theInn/source/theInn.fbx", "../textures", 0.1),
+}
 
 # DXRPathTracer.cpp:265 camera.Initialize(aspect, Pi_4, 0.1f, 100.0f)
 CAMERA_FOV = math.pi / 4
@@ -31,13 +40,25 @@ SKY_RES = 128  # Skybox.cpp:164
 class Scene:
     """A host scene (vertices, indices, geometries, materials, textures, lights + camera/sun pose)."""
 
-    def __init__(self, scene: str | int = "boxtest", seed: int = SPONZA_SEED, detail: int = 0):
+    def __init__(self, scene: str | int = "boxtest", seed: int = SPONZA_SEED, detail: int = 0, model_path: str | None = None,
+                 texture_dir: str | None = None, scene_scale: float | None = None):
+        """A built-in scene (proxy / BoxTest), or with `model_path` a model file loaded like
+        Model::CreateWithAssimp (dxrpt_host_scene_load; texture_dir and scene_scale default to the
+        reference's table for the scene id)."""
         sid = SCENE_NAMES[scene] if isinstance(scene, str) else int(scene)
         H = A.host()
         p = C.POINTER(A.HostScene)()
-        rc = H.dxrpt_host_scene_create(sid, seed, detail, C.byref(p))
+        if model_path is None:
+            rc = H.dxrpt_host_scene_create(sid, seed, detail, C.byref(p))
+            what = f"dxrpt_host_scene_create({sid})"
+        else:
+            _, tdir, scale = SCENE_ASSETS.get(sid, (None, None, 1.0))
+            st = A.ModelLoadSettings(model_path.encode(), (texture_dir if texture_dir is not None else tdir or "").encode(),
+                                     scale if scene_scale is None else scene_scale, 1, 0)
+            rc = H.dxrpt_host_scene_load(sid, C.byref(st), C.byref(p))
+            what = f"dxrpt_host_scene_load({model_path})"
         if rc != 0:
-            raise RuntimeError(f"dxrpt_host_scene_create({sid}) failed: {H.dxrpt_host_last_error().decode()}")
+            raise RuntimeError(f"{what} failed: {H.dxrpt_host_last_error().decode()}")
         self._p = p
         s = p.contents
         self.scene_id = sid
@@ -62,6 +83,15 @@ class Scene:
         self.sun_direction = tuple(s.sun_direction)
         self.white_furnace = bool(s.white_furnace)
         self._host = s
+
+    @classmethod
+    def from_reference(cls, scene: str | int, reference_root: str | None = None) -> "Scene":
+        """The scene's model file from a reference checkout (Content/Models, DXRPathTracer.cpp:83-95)."""
+        import os
+        sid = SCENE_NAMES[scene] if isinstance(scene, str) else int(scene)
+        root = reference_root or os.environ.get("DXRPT_REFERENCE_ROOT", "/root/reference")
+        rel = SCENE_ASSETS[sid][0]
+        return cls(sid, model_path=os.path.join(root, "Content", "Models", rel))
 
     def close(self):
         if self._p:

@@ -11,6 +11,9 @@
  *   Model::CreateWithAssimp(Sponza/SunTemple .fbx)          dxrpt_host_scene_create(SPONZA/SUNTEMPLE):
  *     (Graphics/Model.cpp:435-722; the .fbx files are         seeded procedural proxies (the assets are
  *     absent, .MISSING_LARGE_BLOBS:1-4)                       not in the reference snapshot)
+ *   Model::CreateWithAssimp(ModelLoadSettings) for a        dxrpt_host_scene_load (binary FBX 7.x +
+ *     present asset (WhiteFurnace.fbx, theInn.fbx;            DDS textures, Assimp's post-processing
+ *     DXRPathTracer.cpp:83-95, 946-953)                       steps restated: host/fbx.cpp)
  *   scene tables (DXRPathTracer.cpp:83-98)                  camera pose / sun direction fields
  *   FirstPersonCamera + XMMatrixPerspectiveFovLH            dxrpt_host_inv_view_projection
  *     (Graphics/Camera.cpp:202-229, DXRPathTracer.cpp:265)
@@ -32,6 +35,8 @@ extern "C" {
 #define DXRPT_SCENE_SUNTEMPLE 1u
 #define DXRPT_SCENE_BOXTEST 2u
 #define DXRPT_SCENE_WHITEFURNACE 3u
+#define DXRPT_SCENE_STRONGHOLD 4u /* ScenePaths[4] = theInn.fbx (DXRPathTracer.cpp:90) */
+#define DXRPT_SCENE_COUNT 5u
 
 typedef struct dxrpt_host_texture {
     uint32_t width, height, fmt, pad; /* fmt = DXRPT_TEX_* */
@@ -64,6 +69,23 @@ typedef struct dxrpt_host_scene {
 
 /* detail: 0 = default (the BASELINE.json-sized proxy); >0 = tessellation multiplier for tests. */
 int dxrpt_host_scene_create(uint32_t scene_id, uint64_t seed, uint32_t detail, dxrpt_host_scene** out);
+
+/* ModelLoadSettings (Graphics/Model.h:243-250) as DXRPathTracer fills it (DXRPathTracer.cpp:946-953):
+ * FilePath = ScenePaths[i], TextureDir = SceneTextureDirs[i] (relative to the model's directory, or
+ * NULL), ForceSRGB = true, SceneScale = SceneScales[i], MergeMeshes = false. */
+typedef struct dxrpt_host_model_settings {
+    const char* file_path;
+    const char* texture_dir;
+    float scene_scale;
+    uint32_t force_srgb;
+    uint32_t merge_meshes; /* must be 0: PreTransformVertices is not supported (the reference passes false) */
+} dxrpt_host_model_settings;
+
+/* Model::CreateWithAssimp (Graphics/Model.cpp:435-606) for a binary FBX file; scene_id selects the
+ * camera pose / sun direction of the reference's scene tables (DXRPathTracer.cpp:96-98) and furnace
+ * mode for DXRPT_SCENE_WHITEFURNACE.  Errors (missing file, unsupported texture format, malformed FBX):
+ * DXRPT_E_INVALID_ARG with dxrpt_host_last_error, as the reference throws Exception. */
+int dxrpt_host_scene_load(uint32_t scene_id, const dxrpt_host_model_settings* settings, dxrpt_host_scene** out);
 void dxrpt_host_scene_destroy(dxrpt_host_scene* scene);
 const char* dxrpt_host_last_error(void);
 
