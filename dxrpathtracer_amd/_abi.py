@@ -72,12 +72,12 @@ class Tile(C.Structure):
                 ("accum_pitch", u32), ("pad", u32)]
 
 
-K_RAYGEN, K_TRACE, K_SHADE, K_SHADOW, K_ACCUMULATE, K_RESOLVE, K_COUNT = range(7)
-KERNEL_NAMES = ("k_raygen", "k_trace", "k_shade", "k_shadow", "k_accumulate", "k_resolve")
+K_RAYGEN, K_TRACE, K_SHADE, K_SHADOW, K_ACCUMULATE, K_RESOLVE, K_PATH, K_COUNT = range(8)
+KERNEL_NAMES = ("k_raygen", "k_trace", "k_shade", "k_shadow", "k_accumulate", "k_resolve", "k_path")
 (OPT_COUNT_TRAVERSAL, OPT_KERNEL_TIMING, OPT_BVH_WIDTH, OPT_TRAVERSAL_MODE, OPT_REFILL_LANES, OPT_CHUNKS_PER_WAVE,
  OPT_POSTPONE_TRIS, OPT_TRACE_BLOCK, OPT_OCCUPANCY, OPT_SHADE_BLOCK, OPT_SHADE_OCCUPANCY, OPT_SPATIAL_SPLITS,
  OPT_LEAF_COST, OPT_SHADOW_OCCUPANCY, OPT_SHADOW_GRID, OPT_CONCURRENCY, OPT_TRAVERSAL_PIPELINE, OPT_PACKET_TRAVERSAL, OPT_LDS_NODES,
- OPT_KERNEL_TIMING_MASK, OPT_XCD_MAPPING, OPT_PACKET_SWITCH) = range(1, 23)
+ OPT_KERNEL_TIMING_MASK, OPT_XCD_MAPPING, OPT_PACKET_SWITCH, OPT_MEGAKERNEL_PATHS, OPT_MEGAKERNEL_OCCUPANCY) = range(1, 25)
 # context defaults of the traversal options (dxrpt_api.hip)
 DEFAULT_TRAVERSAL_PIPELINE = 0
 POST_FLOAT4, POST_RGBA8 = 0, 1  # dxrpt_post_process output formats
@@ -85,6 +85,7 @@ DEFAULT_PACKET_TRAVERSAL = 1
 DEFAULT_LDS_NODES = 0
 DEFAULT_XCD_MAPPING = 0
 DEFAULT_PACKET_SWITCH = 0
+DEFAULT_MEGAKERNEL_PATHS = 1100000
 
 
 class Stats(C.Structure):

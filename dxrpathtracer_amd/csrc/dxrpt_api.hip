@@ -112,6 +112,8 @@ struct dxrpt_ctx {
     uint32_t opt_shade_occ = 0;     // DXRPT_OPT_SHADE_OCCUPANCY
     uint32_t opt_xcd = 0;           // DXRPT_OPT_XCD_MAPPING
     uint32_t opt_packet_switch = 0; // DXRPT_OPT_PACKET_SWITCH
+    uint32_t opt_mega_paths = 1100000;  // DXRPT_OPT_MEGAKERNEL_PATHS (a GPU's share of a 1080p frame at >= 2 GPUs)
+    uint32_t opt_mega_occ = 0;          // DXRPT_OPT_MEGAKERNEL_OCCUPANCY (0 = by frame size)
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
     int built_width = 0;
     DevBuf d_trav;   // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
@@ -122,6 +124,7 @@ struct dxrpt_ctx {
         int L = 0;
         uint32_t mask = 0;  // kernel kinds whose events were recorded
         bool pending = false;
+        bool mega = false;  // megakernel frame: ev[0], ev[1] bracket its k_path launch
     };
     std::vector<FrameEvents> ring;
     size_t ring_head = 0;
@@ -273,12 +276,22 @@ void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
 // Adds one timed frame's event intervals to the per-kernel sums (blocks until the frame is done).
 void harvest(dxrpt_ctx* c, dxrpt_ctx::FrameEvents& f) {
     if (!f.pending) return;
-    HIP_CHECK(hipEventSynchronize(f.ev[frame_event_count(f.L) - 1]));
+    HIP_CHECK(hipEventSynchronize(f.ev[f.mega ? 1 : frame_event_count(f.L) - 1]));
     auto span = [&](int a, int b) {
         float ms = 0.f;
         HIP_CHECK(hipEventElapsedTime(&ms, f.ev[a], f.ev[b]));
         return double(ms);
     };
+    if (f.mega) {
+        if ((f.mask >> DXRPT_K_PATH) & 1u) {
+            c->kernel_ms[DXRPT_K_PATH] += span(0, 1);
+            c->kernel_launches[DXRPT_K_PATH]++;
+        }
+        c->frame_ms += span(0, 1);
+        c->timed_frames++;
+        f.pending = false;
+        return;
+    }
     auto slot = [&](int i) { return span(2 * i, 2 * i + 1); };
     auto add = [&](int kind, int i) {
         if (!((f.mask >> kind) & 1u)) return;
@@ -443,6 +456,13 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_PACKET_SWITCH) {
             require(value <= 100, "dxrpt_set_option: packet switch threshold must be 0..100 (percent)");
             ctx->opt_packet_switch = uint32_t(value);
+        } else if (option == DXRPT_OPT_MEGAKERNEL_PATHS) {
+            require(value <= 0xFFFFFFFFull, "dxrpt_set_option: megakernel path threshold too large");
+            ctx->opt_mega_paths = uint32_t(value);
+        } else if (option == DXRPT_OPT_MEGAKERNEL_OCCUPANCY) {
+            require(value == 0 || value == 1 || value == 4 || value == 6,
+                    "dxrpt_set_option: megakernel occupancy must be 0, 1, 4 or 6");
+            ctx->opt_mega_occ = uint32_t(value);
         } else if (option == DXRPT_OPT_BVH_WIDTH) {
             require(value == 2 || value == 8, "dxrpt_set_option: BVH width must be 2 or 8");
             ctx->opt_width = int(value);  // takes effect at the next dxrpt_build_bvh
@@ -713,6 +733,12 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.shade_occupancy = ctx->opt_shade_occ;
         fp.xcd_map = ctx->opt_xcd;
         fp.packet_switch = ctx->opt_packet_switch;
+        // megakernel for small frames (BVH8, no instrumentation, one thread per ray traversal)
+        fp.megakernel = (ctx->opt_mega_paths && paths <= ctx->opt_mega_paths && ctx->built_width == 8 && !ctx->opt_count &&
+                         ctx->opt_trav_mode == 0) ? 1u : 0u;
+        // register budget: the compiler's (3 waves/SIMD) while a frame's waves fit the GPU in about one
+        // round, 6 waves/SIMD above (measured: 1/8 and 1/4 of a 1080p frame vs 1/2)
+        fp.megakernel_occupancy = ctx->opt_mega_occ == 0 ? (paths <= 600000u ? 1u : 6u) : ctx->opt_mega_occ;
         hipStream_t s = static_cast<hipStream_t>(stream);
         if (ctx->opt_count) {
             fp.trav = ctx->d_trav.as<unsigned long long>();
@@ -734,6 +760,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             f.L = L;
             f.mask = ctx->opt_timing_mask;
             f.pending = true;
+            f.mega = fp.megakernel != 0;
             ev = f.ev.data();
         }
         const SceneDev sd = scene_dev(ctx, frame_traversal_threads(paths, ctx->fb.shadow_slots, fp.chunks_per_wave));

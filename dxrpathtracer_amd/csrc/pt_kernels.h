@@ -134,13 +134,16 @@ struct FrameParams {
                                      // some (0 = with their node visit)
     uint32_t xcd_map;                // 1: XCD-aware queue ranges and region shards (xcd_block / region_shard)
     uint32_t packet_switch;          // packet traversal: fall back to one ray per lane below this coherence (%)
+    uint32_t megakernel;             // 1: the whole frame runs in k_path (one thread per path, no passes)
+    uint32_t megakernel_occupancy;   // k_path register budget: 0 compiler default, 6 waves per SIMD
 };
 
 // Kernel sequence of one frame: raygen, then (trace, shade, shadow, resolve) per depth 1..L-1, then
 // accumulate.  With `aux` and 2 * kMaxDepthQueues `fork_ev` events, each depth's any-hit pass runs on
 // `aux` concurrently with the next depth's closest-hit pass.  When `ev` is non-null (per-kernel
 // timing), launch slot i = raygen, 1 + 4(d-1) + {trace, shade, shadow, resolve}, 1 + 4(L-1) =
-// accumulate is bracketed by events ev[2i], ev[2i+1] on the stream it runs on.
+// accumulate is bracketed by events ev[2i], ev[2i+1] on the stream it runs on.  A megakernel frame
+// (fp.megakernel) records ev[0], ev[1] around its single k_path launch.
 inline int frame_event_count(int L) { return 2 * (2 + 4 * (L - 1)); }
 hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream,
                         hipEvent_t* ev, hipStream_t aux = nullptr, hipEvent_t* fork_ev = nullptr);

@@ -833,33 +833,15 @@ PT_DEV bool xcd_item(bool xcd, uint32_t n, uint32_t& i, uint32_t& lw) {
     return true;
 }
 
-// RaygenShader, RayTrace.hlsl:92-126 (+ SamplePoint 85-90).  Path slot p goes to the queue-1 position
-// a wave-ordered append of its wave w = p / 64 would have produced (shard region_shard(w), waves of
-// one shard in order); the shard counts are analytic.
-__global__ __launch_bounds__(kBlock) void k_raygen(KArgs A) {
-    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t P = A.P.num_paths;
-    const bool xcd = A.P.xcd_map != 0u;
-    const uint32_t nw = (P + 63u) / 64u;
-    if (p == 0) {
-        uint32_t* cnt = A.F.counters + 1u * kQueueShards;
-        for (uint32_t s = 0; s < kQueueShards; ++s) {
-            uint32_t waves = 0;
-            if (!xcd) {
-                waves = s < nw ? (nw - 1u - s) / kQueueShards + 1u : 0u;
-            } else {  // waves of region r = s / 8 are [ceil(r nw / 8), ceil((r + 1) nw / 8)), those = s mod 8
-                const uint32_t r = s / 8u, sub = s % 8u;
-                const uint32_t b = uint32_t((uint64_t(r) * nw + kXcds - 1u) / kXcds);
-                const uint32_t e = uint32_t((uint64_t(r + 1u) * nw + kXcds - 1u) / kXcds);
-                const uint32_t f = b + ((sub + 8u - b % 8u) % 8u);
-                waves = f < e ? (e - 1u - f) / 8u + 1u : 0u;
-            }
-            uint32_t items = waves * 64u;
-            if (nw > 0u && region_shard(xcd, nw - 1u, nw) == s) items -= nw * 64u - P;
-            cnt[s] = items;
-        }
-    }
-    if (p >= P) return;
+// RaygenShader's ray (RayTrace.hlsl:92-126, SamplePoint 85-90) for path slot p: the tile and pixel of
+// the slot, CMJ set-0 jitter, near/far-plane unprojection.
+struct PrimaryRay {
+    f3 start, dir;
+    float length;
+    uint32_t pixelIdx, accumIdx;
+};
+
+PT_DEV PrimaryRay primary_ray(const KArgs& A, uint32_t p) {
     // path slot -> tile (binary search over the prefix table) -> pixel
     uint32_t lo = 0, hi = A.P.num_tiles;
     while (hi - lo > 1u) {
@@ -902,6 +884,40 @@ __global__ __launch_bounds__(kBlock) void k_raygen(KArgs A) {
     const f3 diff = sub(end, start);
     const f3 dir = normalize3(diff);
     const float rayLength = len3(diff);
+    return PrimaryRay{start, dir, rayLength, pixelIdx, accumIdx};
+}
+
+// RaygenShader, RayTrace.hlsl:92-126 (+ SamplePoint 85-90).  Path slot p goes to the queue-1 position
+// a wave-ordered append of its wave w = p / 64 would have produced (shard region_shard(w), waves of
+// one shard in order); the shard counts are analytic.
+__global__ __launch_bounds__(kBlock) void k_raygen(KArgs A) {
+    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t P = A.P.num_paths;
+    const bool xcd = A.P.xcd_map != 0u;
+    const uint32_t nw = (P + 63u) / 64u;
+    if (p == 0) {
+        uint32_t* cnt = A.F.counters + 1u * kQueueShards;
+        for (uint32_t s = 0; s < kQueueShards; ++s) {
+            uint32_t waves = 0;
+            if (!xcd) {
+                waves = s < nw ? (nw - 1u - s) / kQueueShards + 1u : 0u;
+            } else {  // waves of region r = s / 8 are [ceil(r nw / 8), ceil((r + 1) nw / 8)), those = s mod 8
+                const uint32_t r = s / 8u, sub = s % 8u;
+                const uint32_t b = uint32_t((uint64_t(r) * nw + kXcds - 1u) / kXcds);
+                const uint32_t e = uint32_t((uint64_t(r + 1u) * nw + kXcds - 1u) / kXcds);
+                const uint32_t f = b + ((sub + 8u - b % 8u) % 8u);
+                waves = f < e ? (e - 1u - f) / 8u + 1u : 0u;
+            }
+            uint32_t items = waves * 64u;
+            if (nw > 0u && region_shard(xcd, nw - 1u, nw) == s) items -= nw * 64u - P;
+            cnt[s] = items;
+        }
+    }
+    if (p >= P) return;
+    const PrimaryRay pr = primary_ray(A, p);
+    const f3 start = pr.start, dir = pr.dir;
+    const float rayLength = pr.length;
+    const uint32_t pixelIdx = pr.pixelIdx, accumIdx = pr.accumIdx;
     const uint32_t w = p >> 6;
     uint32_t widx;  // index of wave w among the waves of its shard
     if (!xcd) {
@@ -966,51 +982,49 @@ PT_DEV void emit_shadow(const KArgs& A, uint32_t pos, uint32_t& n, f3 o, f3 d, f
 
 PT_DEV bool nonzero3(f3 c) { return !(c.x == 0.0f && c.y == 0.0f && c.z == 0.0f); }
 
-// MissShader (RayTrace.hlsl:509-530) and ClosestHitShader -> PathTrace (151-441).
-// kOcc > 0: register budget for kOcc waves per SIMD; workgroups of FrameParams::shade_block threads.
-template <int kOcc>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
-void k_shade(KArgs A, int depth) {
-    const uint32_t* cnt = radiance_counts(A.F, depth);
-    const uint32_t nq = queue_total(cnt);
-    const bool xcd = A.P.xcd_map != 0u;
-    uint32_t i, lw;
-    if (!xcd_item(xcd, nq, i, lw) || i >= nq) return;
-    // the wave's shard in the queues it produces (all lanes of a wave share lw)
-    const uint32_t shard = region_shard(xcd, lw, (nq + 63u) / 64u);
-    const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
-    const dxrpt_app_settings& set = A.P.set;
-    const dxrpt_ray_trace_constants& rtc = A.P.rtc;
-    const RayQueue& Q = A.F.q[depth & 1];
-    const float4 o4 = Q.org[pos];
-    const float4 d4 = Q.dir[pos];
-    const uint32_t pathSlot = fbits(d4.w);
-    const float4 hit = A.F.hit[pos];
-    const float4 thr4 = Q.thr[pos];
-    float4 rad4 = Q.rad[pos];
-    const f3 pathThr = ld3(thr4);
-    const f3 inDir = ld3(d4);
-    const f3 inOrigin = ld3(o4);
-    const bool furnace = set.EnableWhiteFurnaceMode != 0;
-    uint32_t nsh = 0;
-    bool cont = false;
+// One path vertex: MissShader (RayTrace.hlsl:509-530) or ClosestHitShader -> PathTrace (151-441) for the
+// ray (inOrigin, inDir) of path depth `depth` with hit record `hit` (b1, b2, tri, geom).  Shadow rays
+// go to emit(origin, dir, tmin, tmax, pending contribution = pathThr * CalcLighting (or sky *
+// throughput), force_opaque) in the reference's order (sun, spot lights, final sky visibility); the
+// local radiance and the continuation come back in O.  Shared by k_shade (wavefront: emit queues the
+// shadow ray) and k_path (megakernel: emit traces it at once).
+struct VertexIn {
+    f3 inOrigin, inDir, pathThr;
+    float payloadRoughness;  // payload.Roughness (RayTrace.hlsl:70)
+    bool payloadIsDiffuse;   // payload.IsDiffuse (RayTrace.hlsl:69)
+    uint32_t pix;            // global pixel index (CMJ pattern)
+    float4 hit;
+};
+struct VertexOut {
     f3 local = f3{0.0f, 0.0f, 0.0f};
+    bool cont = false;
     f3 nextThr = f3{0.0f, 0.0f, 0.0f};
     f3 nextOrigin = f3{0.0f, 0.0f, 0.0f}, nextDir = f3{0.0f, 0.0f, 0.0f};
     float nextRoughness = 0.0f;
     bool nextIsDiffuse = false;
+};
+
+template <class Emit>
+PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emit, VertexOut& O) {
+    const dxrpt_app_settings& set = A.P.set;
+    const dxrpt_ray_trace_constants& rtc = A.P.rtc;
+    const float4 hit = V.hit;
+    const f3 pathThr = V.pathThr;
+    const f3 inDir = V.inDir;
+    const f3 inOrigin = V.inOrigin;
+    const bool furnace = set.EnableWhiteFurnaceMode != 0;
     const uint32_t tri = fbits(hit.z);
 
     if (tri == kMiss) {
         // MissShader
         if (furnace) {
-            local = f3{1.0f, 1.0f, 1.0f};
+            O.local = f3{1.0f, 1.0f, 1.0f};
         } else {
-            local = set.EnableSky ? sample_sky(A.S, inDir) : f3{0.0f, 0.0f, 0.0f};
+            O.local = set.EnableSky ? sample_sky(A.S, inDir) : f3{0.0f, 0.0f, 0.0f};
             if (depth == 1) {
                 float cosSunAngle = dot3(inDir, f3{rtc.SunDirectionWS[0], rtc.SunDirectionWS[1], rtc.SunDirectionWS[2]});
                 if (cosSunAngle >= rtc.CosSunAngularRadius)
-                    local = f3{rtc.SunRenderColor[0], rtc.SunRenderColor[1], rtc.SunRenderColor[2]};
+                    O.local = f3{rtc.SunRenderColor[0], rtc.SunRenderColor[1], rtc.SunRenderColor[2]};
             }
         }
     } else do {
@@ -1040,7 +1054,7 @@ void k_shade(KArgs A, int depth) {
         }
         const float metallic = saturate((furnace ? 1.0f : sample_tex(A.S, mat.Metallic, surf.u, surf.v).r) * set.MetallicScale);
         const bool enableDiffuse = (set.EnableDiffuse && metallic < 1.0f) || furnace;
-        const bool payloadIsDiffuse = (fbits(rad4.w) & 1u) != 0u;
+        const bool payloadIsDiffuse = V.payloadIsDiffuse;
         const bool enableSpecular =
             set.EnableSpecular && (set.EnableIndirectSpecular ? !(set.AvoidCausticPaths && payloadIsDiffuse) : (depth == 1));
         if (!enableDiffuse && !enableSpecular) break;
@@ -1049,7 +1063,7 @@ void k_shade(KArgs A, int depth) {
         const f3 diffuseAlbedo = scl(f3{lerpf(baseColor.x, 0.0f, metallic), lerpf(baseColor.y, 0.0f, metallic), lerpf(baseColor.z, 0.0f, metallic)}, dsel);
         const f3 specularAlbedo = scl(f3{lerpf(0.03f, baseColor.x, metallic), lerpf(0.03f, baseColor.y, metallic), lerpf(0.03f, baseColor.z, metallic)}, ssel);
         float roughness = sqrtRoughness * sqrtRoughness;
-        if (set.ClampRoughness) roughness = fmaxf(roughness, thr4.w);
+        if (set.ClampRoughness) roughness = fmaxf(roughness, V.payloadRoughness);
         f3 msEC = f3{1.0f, 1.0f, 1.0f};
         if (set.ApplyMultiscatteringEnergyCompensation) {
             const float Ess = ggx_env_brdf_scale(saturate(dot3(normalWS, neg(inDir))), sqrtRoughness);
@@ -1058,7 +1072,7 @@ void k_shade(KArgs A, int depth) {
         }
         if (!furnace) {
             Texel4 em = sample_tex(A.S, mat.Emissive, surf.u, surf.v);
-            local = f3{em.r, em.g, em.b};
+            O.local = f3{em.r, em.g, em.b};
         }
         const bool directZero = (depth == 1 && !set.EnableDirect);  // RayTrace.hlsl:385-386
         const bool shadowOpaque = depth > set.MaxAnyHitPathLength;
@@ -1077,7 +1091,7 @@ void k_shade(KArgs A, int depth) {
             const f3 c = calc_lighting(normalWS, sunDirection, f3{rtc.SunIrradiance[0], rtc.SunIrradiance[1], rtc.SunIrradiance[2]},
                                        diffuseAlbedo, specularAlbedo, roughness, positionWS, inOrigin, msEC);
             if (nonzero3(c))
-                emit_shadow(A, pos, nsh, positionWS, D, kRayTMin, kFP32Max, mul(pathThr, c), shadowOpaque);
+                emit(positionWS, D, kRayTMin, kFP32Max, mul(pathThr, c), shadowOpaque);
         }
         // Spot lights (RayTrace.hlsl:265-313)
         if (set.RenderLights && !furnace && !directZero) {
@@ -1098,16 +1112,16 @@ void k_shade(KArgs A, int depth) {
                     const f3 c = calc_lighting(normalWS, surfaceToLight, intensity, diffuseAlbedo, specularAlbedo, roughness,
                                                positionWS, inOrigin, msEC);
                     if (nonzero3(c))
-                        emit_shadow(A, pos, nsh, add(positionWS, scl(normalWS, 0.01f)), surfaceToLight, kSpotShadowNearClip,
+                        emit(add(positionWS, scl(normalWS, 0.01f)), surfaceToLight, kSpotShadowNearClip,
                                     distanceToLight - kSpotShadowNearClip, mul(pathThr, c), shadowOpaque);
                 }
             }
         }
-        if (directZero) local = f3{0.0f, 0.0f, 0.0f};
+        if (directZero) O.local = f3{0.0f, 0.0f, 0.0f};
         // BRDF importance sampling (RayTrace.hlsl:315-376); sample set = PathLength
         float bx, by;
         sample_cmj2d(rtc.CurrSampleIdx, uint32_t(set.SqrtNumSamples), uint32_t(set.SqrtNumSamples),
-                     uint32_t(depth) * rtc.TotalNumPixels + Q.pix[pos], &bx, &by);
+                     uint32_t(depth) * rtc.TotalNumPixels + V.pix, &bx, &by);
         f3 throughput, rayDirTS;
         float selector = bx;
         if (!enableSpecular) selector = 0.0f;
@@ -1137,22 +1151,62 @@ void k_shade(KArgs A, int depth) {
         const f3 rayDirWS = normalize3(add(add(scl(T, rayDirTS.x), scl(Bt, rayDirTS.y)), scl(Nrow, rayDirTS.z)));
         if (enableDiffuse && enableSpecular) throughput = scl(throughput, 2.0f);
         if (set.EnableIndirect && (depth + 1 < set.MaxPathLength) && !furnace) {
-            cont = true;
-            nextThr = mul(pathThr, throughput);
-            nextOrigin = positionWS;
-            nextDir = rayDirWS;
-            nextRoughness = roughness;
-            nextIsDiffuse = selector < 0.5f;
+            O.cont = true;
+            O.nextThr = mul(pathThr, throughput);
+            O.nextOrigin = positionWS;
+            O.nextDir = rayDirWS;
+            O.nextRoughness = roughness;
+            O.nextIsDiffuse = selector < 0.5f;
         } else if (furnace) {
-            local = throughput;  // RayTrace.hlsl:427-430 (visibility unused)
+            O.local = throughput;  // RayTrace.hlsl:427-430 (visibility unused)
         } else {
             const f3 sky = set.EnableSky ? sample_sky(A.S, rayDirWS) : f3{0.0f, 0.0f, 0.0f};
             const f3 c = mul(sky, throughput);
             if (nonzero3(c))
-                emit_shadow(A, pos, nsh, positionWS, rayDirWS, kRayTMin, kFP32Max, mul(pathThr, c),
+                emit(positionWS, rayDirWS, kRayTMin, kFP32Max, mul(pathThr, c),
                             depth + 1 > set.MaxAnyHitPathLength);
         }
     } while (false);
+}
+
+// MissShader (RayTrace.hlsl:509-530) and ClosestHitShader -> PathTrace (151-441).
+// kOcc > 0: register budget for kOcc waves per SIMD; workgroups of FrameParams::shade_block threads.
+template <int kOcc>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
+void k_shade(KArgs A, int depth) {
+    const uint32_t* cnt = radiance_counts(A.F, depth);
+    const uint32_t nq = queue_total(cnt);
+    const bool xcd = A.P.xcd_map != 0u;
+    uint32_t i, lw;
+    if (!xcd_item(xcd, nq, i, lw) || i >= nq) return;
+    // the wave's shard in the queues it produces (all lanes of a wave share lw)
+    const uint32_t shard = region_shard(xcd, lw, (nq + 63u) / 64u);
+    const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
+    const RayQueue& Q = A.F.q[depth & 1];
+    const float4 o4 = Q.org[pos];
+    const float4 d4 = Q.dir[pos];
+    const uint32_t pathSlot = fbits(d4.w);
+    const float4 thr4 = Q.thr[pos];
+    float4 rad4 = Q.rad[pos];
+    const f3 pathThr = ld3(thr4);
+    uint32_t nsh = 0;
+    VertexIn V;
+    V.inOrigin = ld3(o4);
+    V.inDir = ld3(d4);
+    V.pathThr = pathThr;
+    V.payloadRoughness = thr4.w;
+    V.payloadIsDiffuse = (fbits(rad4.w) & 1u) != 0u;
+    V.pix = Q.pix[pos];
+    V.hit = A.F.hit[pos];
+    VertexOut O;
+    path_vertex(A, depth, V, [&](f3 o, f3 d, float tmin, float tmax, f3 c, bool fo) {
+        emit_shadow(A, pos, nsh, o, d, tmin, tmax, c, fo);
+    }, O);
+    const f3 local = O.local;
+    const bool cont = O.cont;
+    const f3 nextThr = O.nextThr, nextOrigin = O.nextOrigin, nextDir = O.nextDir;
+    const float nextRoughness = O.nextRoughness;
+    const bool nextIsDiffuse = O.nextIsDiffuse;
 
     // Always add (also when zero): keeps NaN/inf propagation identical to the recursive form.
     rad4.x += pathThr.x * local.x;
@@ -1412,11 +1466,8 @@ __global__ __launch_bounds__(kBlock) void k_traverse8p(KArgs A, int depth) {
 }
 
 // RayTrace.hlsl:140-148
-__global__ __launch_bounds__(kBlock) void k_accumulate(KArgs A) {
-    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-    if (p >= A.P.num_paths) return;
-    const float4 r = A.F.px_rad[p];
-    const uint32_t a = A.F.ps_pix[p].y;
+// RaygenShader's clamp and progressive blend (RayTrace.hlsl:140-148) of path radiance r into accum[a].
+PT_DEV void accumulate_pixel(const KArgs& A, uint32_t a, float4 r) {
     const float rx = fminf(fmaxf(r.x, 0.0f), kFP16Max);
     const float ry = fminf(fmaxf(r.y, 0.0f), kFP16Max);
     const float rz = fminf(fmaxf(r.z, 0.0f), kFP16Max);
@@ -1424,6 +1475,96 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(KArgs A) {
     const float f = s / (s + 1.0f);
     const float4 cur = A.P.accum[a];
     A.P.accum[a] = make_float4(lerpf(rx, cur.x, f), lerpf(ry, cur.y, f), lerpf(rz, cur.z, f), 1.0f);
+}
+
+__global__ __launch_bounds__(kBlock) void k_accumulate(KArgs A) {
+    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= A.P.num_paths) return;
+    accumulate_pixel(A, A.F.ps_pix[p].y, A.F.px_rad[p]);
+}
+
+// ---- megakernel (small frames) --------------------------------------------------------------------
+// One thread per path runs the whole frame: raygen, then per depth the closest hit, path_vertex (the
+// same shading code as k_shade) and the vertex's shadow rays (any hit, in slot order), then the
+// accumulation.  There are no pass boundaries, so a frame costs its slowest WAVE's path instead of the
+// sum over passes of each pass's slowest wave -- what limits a GPU's share of a frame split over 8
+// GPUs (too few waves per pass to hide the dependent node-fetch chains).  The radiance of a path is
+// summed in the wavefront's order (local terms, then each vertex's shadow contributions in slot
+// order), so frames are bit-identical to the wavefront schedule.  Shadow rays go through the same
+// per-slot buffers (slot k * qsize + path), so any number of spot lights works.  Ray counts are
+// added to the queue counters (shard = wave % kQueueShards) for dxrpt_get_stats.
+PT_DEV void count_rays(uint32_t* counters, uint32_t n) {
+    const int lane = __lane_id();
+    const int leader = __ffsll(static_cast<long long>(__ballot(1))) - 1;
+    // wave sum of n (n <= 2 + lights): popcounts of the per-bit ballots
+    uint32_t total = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) total += uint32_t(__popcll(__ballot((n >> b) & 1u))) << b;
+    const uint32_t shard = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) % kQueueShards;
+    if (lane == leader && total) atomicAdd(&counters[shard], total);
+}
+
+template <int kOcc>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
+void k_path(KArgs A) {
+    extern __shared__ int stack[];
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= A.P.num_paths) return;
+    lds_int* stk = lane_stack(A.S, stack);
+    const dxrpt_app_settings& set = A.P.set;
+    const PrimaryRay pr = primary_ray(A, p);
+    f3 org = pr.start, dir = pr.dir;
+    float tmax = pr.length;
+    f3 thr = f3{1.0f, 1.0f, 1.0f};
+    float payloadRoughness = 0.0f;
+    bool payloadIsDiffuse = false;
+    float4 rad = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const int L = set.MaxPathLength < 2 ? 2 : set.MaxPathLength;
+    for (int d = 1; d <= L - 1; ++d) {
+        count_rays(A.F.counters + uint32_t(d) * kQueueShards, 1u);
+        HitRec h;
+        uint32_t nv = 0, nt = 0;
+        if (d == 1 && (A.P.packet & 1u))  // coherent primary rays: wave-coherent traversal (same results)
+            traverse8_packet<false>(A.S, org, dir, 0.0f, tmax, d <= set.MaxAnyHitPathLength, true, h);
+        else
+            traverse<8, false, false>(A.S, org, dir, d == 1 ? 0.0f : kRayTMin, tmax, d <= set.MaxAnyHitPathLength, stk, h, nv, nt);
+        VertexIn V;
+        V.inOrigin = org;
+        V.inDir = dir;
+        V.pathThr = thr;
+        V.payloadRoughness = payloadRoughness;
+        V.payloadIsDiffuse = payloadIsDiffuse;
+        V.pix = pr.pixelIdx;
+        V.hit = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
+        VertexOut O;
+        uint32_t nsh = 0;
+        path_vertex(A, d, V, [&](f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
+            emit_shadow(A, p, nsh, o, dd, tmn, tmx, c, fo);
+        }, O);
+        count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, nsh);
+        rad.x += thr.x * O.local.x;
+        rad.y += thr.y * O.local.y;
+        rad.z += thr.z * O.local.z;
+        for (uint32_t k = 0; k < nsh; ++k) {  // ShadowHit/Miss/AnyHit: contribution * visibility
+            const size_t slot = size_t(k) * A.F.qsize + p;
+            const float4 o4 = A.F.sh_org[slot];
+            const float4 d4 = A.F.sh_dir[slot];
+            const float4 c4 = A.F.sh_con[slot];
+            HitRec hs;
+            const bool occluded = traverse<8, true, false>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stk, hs, nv, nt);
+            rad.x += occluded ? c4.x * 0.0f : c4.x;
+            rad.y += occluded ? c4.y * 0.0f : c4.y;
+            rad.z += occluded ? c4.z * 0.0f : c4.z;
+        }
+        if (!O.cont) break;
+        org = O.nextOrigin;
+        dir = O.nextDir;
+        tmax = kFP32Max;
+        thr = O.nextThr;
+        payloadRoughness = O.nextRoughness;
+        payloadIsDiffuse = O.nextIsDiffuse;
+    }
+    accumulate_pixel(A, pr.accumIdx, rad);
 }
 
 // Arbitrary ray queries (dxrpt_trace_rays): flags bit0 = any-hit (shadow) semantics,
@@ -1490,6 +1631,17 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
     auto slot_of = [](int d, int kind) { return 1 + 4 * (d - 1) + kind; };  // kind 0 trace 1 shade 2 shadow 3 resolve
     hipError_t e = hipMemsetAsync(fb.counters, 0, 2 * kMaxDepthQueues * kQueueShards * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
+    if (fp.megakernel) {  // whole frame in k_path (timing: ev[0], ev[1] bracket the k_path launch)
+        const uint32_t tb = fp.trace_block;
+        const size_t ldsm = size_t(scene.stack_ints) * tb * sizeof(int);
+        const uint32_t gm = (fp.num_paths + tb - 1u) / tb;
+        if (ev) (void)hipEventRecord(ev[0], stream);
+        if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_path<6>), dim3(gm), dim3(tb), ldsm, stream, A);
+        else if (fp.megakernel_occupancy == 4) hipLaunchKernelGGL((k_path<4>), dim3(gm), dim3(tb), ldsm, stream, A);
+        else hipLaunchKernelGGL((k_path<0>), dim3(gm), dim3(tb), ldsm, stream, A);  // 1: the compiler's budget
+        if (ev) (void)hipEventRecord(ev[1], stream);
+        return hipGetLastError();
+    }
     start(0, stream);
     hipLaunchKernelGGL(k_raygen, dim3(g), dim3(kBlock), 0, stream, A);
     stop(0, stream);

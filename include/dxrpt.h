@@ -191,7 +191,8 @@ typedef struct dxrpt_tile {
 #define DXRPT_K_SHADOW 3      /* any-hit traversal of shadow rays (all depths) */
 #define DXRPT_K_ACCUMULATE 4
 #define DXRPT_K_RESOLVE 5     /* adds visibility-weighted shadow contributions to path radiance */
-#define DXRPT_K_COUNT 6
+#define DXRPT_K_PATH 6        /* megakernel frames (DXRPT_OPT_MEGAKERNEL_PATHS): the whole frame in one launch */
+#define DXRPT_K_COUNT 7
 
 /* Counters of the last dxrpt_render call (read back with a stream sync in dxrpt_get_stats), plus
  * per-kernel HIP-event timings accumulated since dxrpt_reset_timing (DXRPT_OPT_KERNEL_TIMING). */
@@ -303,6 +304,13 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 #define DXRPT_OPT_PACKET_SWITCH 22u /* packet traversal: a wave whose share of live lanes entering the visited
                                          nodes falls below this percentage continues one ray per lane
                                          (0 = never).  Identical results. */
+#define DXRPT_OPT_MEGAKERNEL_PATHS 23u /* frames of at most this many paths (default 1,100,000: a GPU's share of a
+                                            1080p frame at >= 2 GPUs) run as ONE kernel, one thread per path:
+                                            raygen, every depth's traversals and shading, accumulation; no
+                                            passes, no queues.  0 = never.  Identical results. */
+#define DXRPT_OPT_MEGAKERNEL_OCCUPANCY 24u /* megakernel register budget: 0 = by frame size (default: the
+                                              compiler's up to 600,000 paths, 6 waves/SIMD above), 1 = the
+                                              compiler's, 4 or 6 waves/SIMD */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

@@ -18,9 +18,9 @@ sys.path.insert(0, REPO)
 
 KEYS = {"w": "width", "m": "mode", "r": "refill", "k": "chunks", "p": "postpone", "b": "block", "o": "occ",
         "s": "sblock", "q": "socc", "x": "spatial", "c": "leafcost", "h": "hocc", "g": "sgrid",
-        "j": "conc", "t": "pipe", "a": "packet", "n": "ldsnodes", "z": "xcd", "u": "pswitch"}
+        "j": "conc", "t": "pipe", "a": "packet", "n": "ldsnodes", "z": "xcd", "u": "pswitch", "e": "mega", "v": "megaocc"}
 DEFAULTS = {"width": 8, "mode": 0, "refill": 16, "chunks": 4, "postpone": 0, "block": 64, "occ": 7, "sblock": 256,
-            "socc": 0, "spatial": 150, "leafcost": 150, "hocc": 8, "sgrid": 0, "conc": 1, "pipe": 0, "packet": 1, "ldsnodes": 0, "xcd": 0, "pswitch": 0}
+            "socc": 0, "spatial": 150, "leafcost": 150, "hocc": 8, "sgrid": 0, "conc": 1, "pipe": 0, "packet": 1, "ldsnodes": 0, "xcd": 0, "pswitch": 0, "mega": 0, "megaocc": 0}
 BUILD_KEYS = ("width", "spatial", "leafcost")  # a separate context (BVH) per combination
 
 
@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--L", type=int, default=3)
     ap.add_argument("--scene", default="sponza")
+    ap.add_argument("--share", type=int, default=1, help="render rank 0's band share of an N-GPU frame")
     args = ap.parse_args()
     import torch
     import dxrpathtracer_amd as D
@@ -70,6 +71,10 @@ def main():
         print(f"bvh {bk}: {info.num_nodes} nodes depth {info.max_depth} build {info.build_ms:.0f} ms", flush=True)
         tracers[bk] = t
     accum = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+    tiles = None
+    if args.share > 1:
+        from dxrpathtracer_amd.distributed import band_layout
+        tiles = band_layout(W, H, args.share).rank_tiles(0)
     consts = [D.make_constants(sc, st, sky, W, H, s) for s in range(16)]
     lights = D.make_lights(sc)
     sh = torch.cuda.current_stream().cuda_stream
@@ -92,28 +97,30 @@ def main():
             t.set_option(A.OPT_LDS_NODES, o["ldsnodes"])
             t.set_option(A.OPT_XCD_MAPPING, o["xcd"])
             t.set_option(A.OPT_PACKET_SWITCH, o["pswitch"])
+            t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30 if o["mega"] else 0)
+            t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, o["megaocc"])
             t.set_option(A.OPT_SHADE_BLOCK, o["sblock"])
             t.set_option(A.OPT_SHADE_OCCUPANCY, o["socc"])
             for f in range(3):
-                t.render_raw(consts[f], st, accum.data_ptr(), W, H, stream=sh, lights=lights)
+                t.render_raw(consts[f], st, accum.data_ptr(), W, H, tiles=tiles, stream=sh, lights=lights)
             torch.cuda.synchronize()
             # wall-clock pass without per-kernel timing (which serialises the concurrent passes)
             t0 = time.perf_counter()
             for f in range(args.frames):
-                t.render_raw(consts[f % 16], st, accum.data_ptr(), W, H, stream=sh, lights=lights)
+                t.render_raw(consts[f % 16], st, accum.data_ptr(), W, H, tiles=tiles, stream=sh, lights=lights)
             torch.cuda.synchronize()
             wall = (time.perf_counter() - t0) / args.frames * 1e3
             # per-kernel breakdown pass
             t.set_option(A.OPT_KERNEL_TIMING, 1)
             t.reset_timing()
             for f in range(args.frames):
-                t.render_raw(consts[f % 16], st, accum.data_ptr(), W, H, stream=sh, lights=lights)
+                t.render_raw(consts[f % 16], st, accum.data_ptr(), W, H, tiles=tiles, stream=sh, lights=lights)
             torch.cuda.synchronize()
             s = t.stats()
             t.set_option(A.OPT_KERNEL_TIMING, 0)
             n = max(1, s.timed_frames)
             res[v].append((wall, [s.kernel_ms[k] / n for k in range(A.K_COUNT)]))
-    print(f"{args.scene} {W}x{H} L={args.L}: median of {args.rounds} rounds x {args.frames} frames (ms/frame)")
+    print(f"{args.scene} {W}x{H} L={args.L} share 1/{args.share}: median of {args.rounds} rounds x {args.frames} frames (ms/frame)")
     print(f"{'variant':12s} {'wall':>8s} " + " ".join(f"{k:>12s}" for k in A.KERNEL_NAMES))
     for v, rows in res.items():
         wall = statistics.median(r[0] for r in rows)

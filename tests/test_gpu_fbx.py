@@ -16,7 +16,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("max_any_hit", [1, 3])
-def test_fbx_scene_matches_oracle(torch_cuda, tmp_path, max_any_hit):
+@pytest.mark.parametrize("mega", [0, A.DEFAULT_MEGAKERNEL_PATHS])  # wavefront passes / one-kernel frame
+def test_fbx_scene_matches_oracle(torch_cuda, tmp_path, max_any_hit, mega):
     torch = torch_cuda
     sc = D.Scene(A.SCENE_BOXTEST, model_path=F.box_room_fbx(str(tmp_path)))
     assert sc.materials[0][4] != 0xFFFFFFFF  # opacity map present: alpha-tested geometry
@@ -24,6 +25,7 @@ def test_fbx_scene_matches_oracle(torch_cuda, tmp_path, max_any_hit):
     sky = D.make_sky(st)
     W, H = 160, 96
     t = DXRPathTracer(0)
+    t.set_option(A.OPT_MEGAKERNEL_PATHS, mega)
     try:
         t.initialize_scene(sc, sky)
         t.build_rt_acceleration_structure()

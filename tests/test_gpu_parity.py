@@ -29,6 +29,9 @@ def tracer(name, width=8):
         sc, sky = scene_bundle(name)
         t = DXRPathTracer(0)
         t.set_option(A.OPT_BVH_WIDTH, width)
+        # the wavefront schedule for every test here; the megakernel (default for small frames) is
+        # checked against it bit for bit in test_megakernel_is_bit_identical
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
         t.initialize_scene(sc, sky)
         info = t.build_rt_acceleration_structure()
         assert info.width == width
@@ -310,6 +313,78 @@ def test_xcd_mapping_is_bit_identical(torch_cuda, packet, shadow_grid):
         np.testing.assert_array_equal(got, ref)
 
 
+def _boxtest_lights(sc, sky, st, W, H, sample):
+    rtc = D.make_constants(sc, st, sky, W, H, sample)
+    lights = D.make_lights(sc)
+    for i, (p, d) in enumerate([((1.5, 4.0, -2.0), (0.3, 1.0, -0.4)), ((-2.5, 1.5, -1.5), (-0.8, 0.2, -0.5)),
+                                ((0.5, 3.0, 2.0), (0.0, 1.0, 0.2))]):
+        L = lights.Lights[i]
+        L.Position[:] = p
+        L.Direction[:] = d
+        L.Intensity[:] = (50.0, 45.0, 37.5)
+        L.AngularAttenuationX, L.AngularAttenuationY, L.Range = 0.99, 0.95, 7.5
+    rtc.NumLights = 3
+    return rtc, lights
+
+
+@pytest.mark.parametrize("name,L,any_hit,occ,packet", [("sponza", 3, 1, 1, 1), ("sponza", 8, 1, 6, 0),
+                                                       ("suntemple", 4, 3, 0, 1), ("boxtest", 5, 1, 1, 0),
+                                                       ("whitefurnace", 3, 1, 6, 1)])
+def test_megakernel_is_bit_identical(torch_cuda, name, L, any_hit, occ, packet):
+    # DXRPT_OPT_MEGAKERNEL_PATHS: the whole frame as one kernel (one thread per path) must equal the
+    # wavefront frame bit for bit -- same shading code, same per-path summation order -- and count the
+    # same rays per depth; on full frames, on band tiles (a GPU's share) and with 3 spot lights
+    torch = torch_cuda
+    sc, sky = scene_bundle(name)
+    st = sc.settings(MaxPathLength=L, MaxAnyHitPathLength=any_hit)
+    W, H = 352, 200
+    t = tracer(name)
+    rtc, lights = (_boxtest_lights(sc, sky, st, W, H, 2) if name == "boxtest"
+                   else (D.make_constants(sc, st, sky, W, H, 2), D.make_lights(sc)))
+    lay = band_layout(W, H, 3)
+    try:
+        for tiles, n in ((None, W * H), (lay.rank_tiles(1), lay.counts[1])):
+            acc0 = torch.full((n, 4), 0.25, dtype=torch.float32, device="cuda")
+            t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
+            t.set_option(A.OPT_PACKET_TRAVERSAL, 0)
+            ref = gpu_render(torch, name, W, H, st, 2, tiles=tiles, n_out=n, accum=acc0.clone(), rtc=rtc,
+                             lights=lights).cpu().numpy()
+            s_ref = t.stats()
+            t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30)
+            t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, occ)
+            t.set_option(A.OPT_PACKET_TRAVERSAL, packet)
+            got = gpu_render(torch, name, W, H, st, 2, tiles=tiles, n_out=n, accum=acc0.clone(), rtc=rtc,
+                             lights=lights).cpu().numpy()
+            s_got = t.stats()
+            np.testing.assert_array_equal(got, ref)
+            assert list(s_got.radiance_rays_per_depth) == list(s_ref.radiance_rays_per_depth)
+            assert list(s_got.shadow_rays_per_depth) == list(s_ref.shadow_rays_per_depth)
+    finally:
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
+        t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, 0)
+        t.set_option(A.OPT_PACKET_TRAVERSAL, A.DEFAULT_PACKET_TRAVERSAL)
+
+
+def test_megakernel_timing(torch_cuda):
+    torch = torch_cuda
+    t = tracer("boxtest")
+    sc, _ = scene_bundle("boxtest")
+    st = sc.settings(MaxPathLength=3)
+    t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30)
+    t.set_option(A.OPT_KERNEL_TIMING, 1)
+    t.reset_timing()
+    try:
+        for s in range(3):
+            gpu_render(torch, "boxtest", 96, 64, st, s)
+        stt = t.stats()
+    finally:
+        t.set_option(A.OPT_KERNEL_TIMING, 0)
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
+    assert stt.timed_frames == 3 and stt.kernel_launches[A.K_PATH] == 3 and stt.kernel_ms[A.K_PATH] > 0
+    assert all(stt.kernel_launches[k] == 0 for k in range(A.K_COUNT) if k != A.K_PATH)
+    assert stt.frame_ms >= stt.kernel_ms[A.K_PATH] * 0.99
+
+
 def _random_rays(rng, n, lo, hi):
     o = rng.uniform(lo, hi, size=(n, 3)).astype(np.float32)
     d = rng.standard_normal((n, 3)).astype(np.float32)
@@ -386,8 +461,9 @@ def test_kernel_timing_option(torch_cuda, concurrency):
         t.set_option(A.OPT_CONCURRENCY, 1)
     assert stt.timed_frames == 5
     assert stt.kernel_launches[A.K_TRACE] == 10 and stt.kernel_launches[A.K_RAYGEN] == 5
-    assert all(stt.kernel_ms[k] > 0 for k in range(A.K_COUNT))
-    busy = sum(stt.kernel_ms[k] for k in range(A.K_COUNT))
+    wavefront = [k for k in range(A.K_COUNT) if k != A.K_PATH]
+    assert all(stt.kernel_ms[k] > 0 for k in wavefront) and stt.kernel_launches[A.K_PATH] == 0
+    busy = sum(stt.kernel_ms[k] for k in wavefront)
     if concurrency == 0:  # one stream: the frame spans every kernel
         assert stt.frame_ms >= busy * 0.99
     else:  # the any-hit passes overlap the next closest-hit passes
