@@ -33,8 +33,10 @@ METRIC = "Mrays/sec + ms/frame, Sponza 1920x1080 path-length 3 at 1/2/4/8 GPU"
 #   k_trace  (closest hit): 32 B ray in (2 x float4) + 16 B hit out
 #   k_shadow (any hit):     4 B queue entry + 48 B shadow slot in (origin, direction, contribution);
 #                           the 16-B contribution write of occluded rays is not counted (lower bound)
+#   k_path   (megakernel, one launch per frame): all of the above + 32 B accumulation RMW per pixel
 RAY_IN_BYTES, HIT_OUT_BYTES = 32, 16
 SHADOW_IN_BYTES = 52
+ACCUM_BYTES = 32
 
 
 def log(*a):
@@ -167,8 +169,8 @@ def main():
     breakdown = tracer.stats()
     kms = {A.KERNEL_NAMES[k]: breakdown.kernel_ms[k] for k in range(A.K_COUNT)}
     dominant = max(kms, key=kms.get)
-    roof_kernel = dominant if dominant in ("k_trace", "k_shadow") else "k_trace"
-    K_ROOF = A.K_TRACE if roof_kernel == "k_trace" else A.K_SHADOW
+    roof_kernel = dominant if dominant in ("k_trace", "k_shadow", "k_path") else "k_trace"
+    K_ROOF = {"k_trace": A.K_TRACE, "k_shadow": A.K_SHADOW, "k_path": A.K_PATH}[roof_kernel]
 
     # ---- timed region: production schedule (any-hit / closest-hit stream overlap), events on the
     # launching streams around the roofline kernel's launches only
@@ -207,11 +209,15 @@ def main():
                          + census.node_visits_radiance * bvh.node_bytes + census.tri_tests_radiance * bvh.tri_bytes)
     shadow_bytes_frame = (census.shadow_rays * SHADOW_IN_BYTES
                           + census.node_visits_shadow * bvh.node_bytes + census.tri_tests_shadow * bvh.tri_bytes)
-    roof_bytes = (trace_bytes_frame if roof_kernel == "k_trace" else shadow_bytes_frame) / launches_per_frame
+    # k_path (the whole frame in one launch): every ray's traversal bytes + the accumulation RMW; the
+    # shading gathers are not counted, so it is a lower bound
+    path_bytes_frame = trace_bytes_frame + shadow_bytes_frame + ACCUM_BYTES * n_local
+    roof_bytes = {"k_trace": trace_bytes_frame / launches_per_frame, "k_shadow": shadow_bytes_frame / launches_per_frame,
+                  "k_path": path_bytes_frame}[roof_kernel]
     achieved = roof_bytes / (roof_ms_avg * 1e-3) / 1e9
     pmc, traffic_src = pmc_traffic(roof_kernel)
     traffic = pmc.get("hbm_bytes_per_launch")
-    # the other traversal kernel, from the breakdown pass (for the record)
+    # the other traversal kernel, from the breakdown pass (for the record; wavefront schedule only)
     other = "k_shadow" if roof_kernel == "k_trace" else "k_trace"
     K_OTHER = A.K_SHADOW if other == "k_shadow" else A.K_TRACE
     other_ms = breakdown.kernel_ms[K_OTHER] / max(1, breakdown.kernel_launches[K_OTHER])
@@ -257,7 +263,8 @@ def main():
                                    "avg_launch_ms": round(other_ms, 4),
                                    "achieved_GBs": round(other_bytes / (other_ms * 1e-3) / 1e9, 1),
                                    "traffic": other_pmc.get("hbm_bytes_per_launch"),
-                                   "l2_hit_rate": other_pmc.get("l2_hit_rate")},
+                                   "l2_hit_rate": other_pmc.get("l2_hit_rate")} if other_ms > 0 else None,
+                "schedule": "megakernel (k_path)" if kms.get("k_path", 0) > 0 else "wavefront passes",
                 "gpu_frame_ms_events": round(gpu_frame_ms, 4),
                 "kernel_breakdown_note": "kernel_ms_per_frame from a separate all-kernel event pass before the timed region",
                 "frame_ms": {"mean": round(float(frame_ms.mean()), 4), "median": round(float(np.median(frame_ms)), 4),

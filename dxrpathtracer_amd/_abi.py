@@ -85,7 +85,8 @@ DEFAULT_PACKET_TRAVERSAL = 1
 DEFAULT_LDS_NODES = 0
 DEFAULT_XCD_MAPPING = 0
 DEFAULT_PACKET_SWITCH = 0
-DEFAULT_MEGAKERNEL_PATHS = 1100000
+DEFAULT_MEGAKERNEL_PATHS = 0xFFFFFFFF
+DEFAULT_MEGAKERNEL_OCCUPANCY = 4
 
 
 class Stats(C.Structure):

@@ -112,8 +112,8 @@ struct dxrpt_ctx {
     uint32_t opt_shade_occ = 0;     // DXRPT_OPT_SHADE_OCCUPANCY
     uint32_t opt_xcd = 0;           // DXRPT_OPT_XCD_MAPPING
     uint32_t opt_packet_switch = 0; // DXRPT_OPT_PACKET_SWITCH
-    uint32_t opt_mega_paths = 1100000;  // DXRPT_OPT_MEGAKERNEL_PATHS (a GPU's share of a 1080p frame at >= 2 GPUs)
-    uint32_t opt_mega_occ = 0;          // DXRPT_OPT_MEGAKERNEL_OCCUPANCY (0 = by frame size)
+    uint32_t opt_mega_paths = 0xFFFFFFFFu;  // DXRPT_OPT_MEGAKERNEL_PATHS (default: every frame)
+    uint32_t opt_mega_occ = 4;              // DXRPT_OPT_MEGAKERNEL_OCCUPANCY
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
     int built_width = 0;
     DevBuf d_trav;   // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
@@ -457,11 +457,9 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
             require(value <= 100, "dxrpt_set_option: packet switch threshold must be 0..100 (percent)");
             ctx->opt_packet_switch = uint32_t(value);
         } else if (option == DXRPT_OPT_MEGAKERNEL_PATHS) {
-            require(value <= 0xFFFFFFFFull, "dxrpt_set_option: megakernel path threshold too large");
-            ctx->opt_mega_paths = uint32_t(value);
+            ctx->opt_mega_paths = value > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(value);
         } else if (option == DXRPT_OPT_MEGAKERNEL_OCCUPANCY) {
-            require(value == 0 || value == 1 || value == 4 || value == 6,
-                    "dxrpt_set_option: megakernel occupancy must be 0, 1, 4 or 6");
+            require(value == 0 || value == 4 || value == 6, "dxrpt_set_option: megakernel occupancy must be 0, 4 or 6");
             ctx->opt_mega_occ = uint32_t(value);
         } else if (option == DXRPT_OPT_BVH_WIDTH) {
             require(value == 2 || value == 8, "dxrpt_set_option: BVH width must be 2 or 8");
@@ -736,9 +734,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // megakernel for small frames (BVH8, no instrumentation, one thread per ray traversal)
         fp.megakernel = (ctx->opt_mega_paths && paths <= ctx->opt_mega_paths && ctx->built_width == 8 && !ctx->opt_count &&
                          ctx->opt_trav_mode == 0) ? 1u : 0u;
-        // register budget: the compiler's (3 waves/SIMD) while a frame's waves fit the GPU in about one
-        // round, 6 waves/SIMD above (measured: 1/8 and 1/4 of a 1080p frame vs 1/2)
-        fp.megakernel_occupancy = ctx->opt_mega_occ == 0 ? (paths <= 600000u ? 1u : 6u) : ctx->opt_mega_occ;
+        fp.megakernel_occupancy = ctx->opt_mega_occ;
         hipStream_t s = static_cast<hipStream_t>(stream);
         if (ctx->opt_count) {
             fp.trav = ctx->d_trav.as<unsigned long long>();

@@ -304,13 +304,12 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 #define DXRPT_OPT_PACKET_SWITCH 22u /* packet traversal: a wave whose share of live lanes entering the visited
                                          nodes falls below this percentage continues one ray per lane
                                          (0 = never).  Identical results. */
-#define DXRPT_OPT_MEGAKERNEL_PATHS 23u /* frames of at most this many paths (default 1,100,000: a GPU's share of a
-                                            1080p frame at >= 2 GPUs) run as ONE kernel, one thread per path:
-                                            raygen, every depth's traversals and shading, accumulation; no
-                                            passes, no queues.  0 = never.  Identical results. */
-#define DXRPT_OPT_MEGAKERNEL_OCCUPANCY 24u /* megakernel register budget: 0 = by frame size (default: the
-                                              compiler's up to 600,000 paths, 6 waves/SIMD above), 1 = the
-                                              compiler's, 4 or 6 waves/SIMD */
+#define DXRPT_OPT_MEGAKERNEL_PATHS 23u /* frames of at most this many paths (default: all) run as ONE kernel, one
+                                            thread per path: raygen, every depth's traversals and shading,
+                                            accumulation -- no passes, no queues; larger frames run the
+                                            wavefront passes.  0 = always the wavefront.  Identical results. */
+#define DXRPT_OPT_MEGAKERNEL_OCCUPANCY 24u /* megakernel register budget in waves/SIMD: 4 (default, 128 VGPRs, no
+                                              spills), 6, or 0 = the compiler's (3) */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

@@ -65,8 +65,10 @@ def main(prof, rnd):
     # the timed kinds (DXRPT_K_TRACE / DXRPT_K_SHADOW): the uninstrumented instantiations of the frame
     # (packet and per-lane variants), launch-weighted
     for kind, prefixes in (("k_trace", ("k_trace<false", "k_trace_packet")),
-                           ("k_shadow", ("k_shadow<false", "k_shadow_packet"))):
+                           ("k_shadow", ("k_shadow<false", "k_shadow_packet")), ("k_path", ("k_path<",))):
         cands = [k for k in out["kernels"] if k.startswith(prefixes)]
+        if not cands:
+            continue
         calls = sum(out["kernels"][k].get("calls", 0) for k in cands)
 
         def wavg(key):

@@ -327,9 +327,9 @@ def _boxtest_lights(sc, sky, st, W, H, sample):
     return rtc, lights
 
 
-@pytest.mark.parametrize("name,L,any_hit,occ,packet", [("sponza", 3, 1, 1, 1), ("sponza", 8, 1, 6, 0),
-                                                       ("suntemple", 4, 3, 0, 1), ("boxtest", 5, 1, 1, 0),
-                                                       ("whitefurnace", 3, 1, 6, 1)])
+@pytest.mark.parametrize("name,L,any_hit,occ,packet", [("sponza", 3, 1, 4, 1), ("sponza", 8, 1, 6, 0),
+                                                       ("suntemple", 4, 3, 0, 1), ("boxtest", 5, 1, 4, 0),
+                                                       ("whitefurnace", 3, 1, 6, 1), ("suntemple", 3, 1, 4, 1)])
 def test_megakernel_is_bit_identical(torch_cuda, name, L, any_hit, occ, packet):
     # DXRPT_OPT_MEGAKERNEL_PATHS: the whole frame as one kernel (one thread per path) must equal the
     # wavefront frame bit for bit -- same shading code, same per-path summation order -- and count the
@@ -361,7 +361,7 @@ def test_megakernel_is_bit_identical(torch_cuda, name, L, any_hit, occ, packet):
             assert list(s_got.shadow_rays_per_depth) == list(s_ref.shadow_rays_per_depth)
     finally:
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
-        t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, 0)
+        t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, A.DEFAULT_MEGAKERNEL_OCCUPANCY)
         t.set_option(A.OPT_PACKET_TRAVERSAL, A.DEFAULT_PACKET_TRAVERSAL)
 
 
