@@ -86,7 +86,7 @@ DEFAULT_LDS_NODES = 0
 DEFAULT_XCD_MAPPING = 0
 DEFAULT_PACKET_SWITCH = 0
 DEFAULT_MEGAKERNEL_PATHS = 0xFFFFFFFF
-DEFAULT_MEGAKERNEL_OCCUPANCY = 4
+DEFAULT_MEGAKERNEL_OCCUPANCY = 0
 
 
 class Stats(C.Structure):

@@ -113,7 +113,7 @@ struct dxrpt_ctx {
     uint32_t opt_xcd = 0;           // DXRPT_OPT_XCD_MAPPING
     uint32_t opt_packet_switch = 0; // DXRPT_OPT_PACKET_SWITCH
     uint32_t opt_mega_paths = 0xFFFFFFFFu;  // DXRPT_OPT_MEGAKERNEL_PATHS (default: every frame)
-    uint32_t opt_mega_occ = 4;              // DXRPT_OPT_MEGAKERNEL_OCCUPANCY
+    uint32_t opt_mega_occ = 0;              // DXRPT_OPT_MEGAKERNEL_OCCUPANCY (0 = by frame size)
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
     int built_width = 0;
     DevBuf d_trav;   // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
@@ -459,7 +459,7 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_MEGAKERNEL_PATHS) {
             ctx->opt_mega_paths = value > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(value);
         } else if (option == DXRPT_OPT_MEGAKERNEL_OCCUPANCY) {
-            require(value == 0 || value == 4 || value == 6, "dxrpt_set_option: megakernel occupancy must be 0, 4 or 6");
+            require(value == 0 || (value >= 3 && value <= 6), "dxrpt_set_option: megakernel occupancy must be 0 or 3..6");
             ctx->opt_mega_occ = uint32_t(value);
         } else if (option == DXRPT_OPT_BVH_WIDTH) {
             require(value == 2 || value == 8, "dxrpt_set_option: BVH width must be 2 or 8");
@@ -734,7 +734,9 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // megakernel for small frames (BVH8, no instrumentation, one thread per ray traversal)
         fp.megakernel = (ctx->opt_mega_paths && paths <= ctx->opt_mega_paths && ctx->built_width == 8 && !ctx->opt_count &&
                          ctx->opt_trav_mode == 0) ? 1u : 0u;
-        fp.megakernel_occupancy = ctx->opt_mega_occ;
+        // register budget by frame size (measured, 1080p L=3 Sponza proxy): 5 waves/SIMD (96 VGPRs, some
+        // spills) once a frame has waves for several rounds, 4 (128 VGPRs, no spills) for a GPU's 1/8 share
+        fp.megakernel_occupancy = ctx->opt_mega_occ ? ctx->opt_mega_occ : (paths > 300000u ? 5u : 4u);
         hipStream_t s = static_cast<hipStream_t>(stream);
         if (ctx->opt_count) {
             fp.trav = ctx->d_trav.as<unsigned long long>();

@@ -1638,7 +1638,8 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
         if (ev) (void)hipEventRecord(ev[0], stream);
         if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_path<6>), dim3(gm), dim3(tb), ldsm, stream, A);
         else if (fp.megakernel_occupancy == 4) hipLaunchKernelGGL((k_path<4>), dim3(gm), dim3(tb), ldsm, stream, A);
-        else hipLaunchKernelGGL((k_path<0>), dim3(gm), dim3(tb), ldsm, stream, A);  // the compiler's budget
+        else if (fp.megakernel_occupancy == 5) hipLaunchKernelGGL((k_path<5>), dim3(gm), dim3(tb), ldsm, stream, A);
+        else hipLaunchKernelGGL((k_path<0>), dim3(gm), dim3(tb), ldsm, stream, A);  // 3: the compiler's budget
         if (ev) (void)hipEventRecord(ev[1], stream);
         return hipGetLastError();
     }

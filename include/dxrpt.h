@@ -308,8 +308,9 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                             thread per path: raygen, every depth's traversals and shading,
                                             accumulation -- no passes, no queues; larger frames run the
                                             wavefront passes.  0 = always the wavefront.  Identical results. */
-#define DXRPT_OPT_MEGAKERNEL_OCCUPANCY 24u /* megakernel register budget in waves/SIMD: 4 (default, 128 VGPRs, no
-                                              spills), 6, or 0 = the compiler's (3) */
+#define DXRPT_OPT_MEGAKERNEL_OCCUPANCY 24u /* megakernel register budget in waves/SIMD: 0 = by frame size
+                                              (default: 5 above 300,000 paths, else 4), 4 (128 VGPRs, no
+                                              spills), 5, 6, or 3 = the compiler's */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);
