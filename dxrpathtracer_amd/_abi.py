@@ -81,7 +81,7 @@ KERNEL_NAMES = ("k_raygen", "k_trace", "k_shade", "k_shadow", "k_accumulate", "k
 # context defaults of the traversal options (dxrpt_api.hip)
 DEFAULT_TRAVERSAL_PIPELINE = 0
 POST_FLOAT4, POST_RGBA8 = 0, 1  # dxrpt_post_process output formats
-DEFAULT_PACKET_TRAVERSAL = 1
+DEFAULT_PACKET_TRAVERSAL = 3
 DEFAULT_LDS_NODES = 0
 DEFAULT_XCD_MAPPING = 0
 DEFAULT_PACKET_SWITCH = 0

@@ -103,7 +103,7 @@ struct dxrpt_ctx {
     uint32_t opt_shadow_occ = 8;    // DXRPT_OPT_SHADOW_OCCUPANCY
     uint32_t opt_shadow_grid = 0;   // DXRPT_OPT_SHADOW_GRID
     uint32_t opt_pipeline = 0;      // DXRPT_OPT_TRAVERSAL_PIPELINE
-    uint32_t opt_packet = 1;        // DXRPT_OPT_PACKET_TRAVERSAL
+    uint32_t opt_packet = 3;        // DXRPT_OPT_PACKET_TRAVERSAL
     uint32_t opt_lds_nodes = 0;     // DXRPT_OPT_LDS_NODES
     uint32_t opt_concurrency = 1;   // DXRPT_OPT_CONCURRENCY
     hipStream_t aux = nullptr;      // any-hit pass stream (created on first use)

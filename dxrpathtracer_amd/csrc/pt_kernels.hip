@@ -1545,16 +1545,29 @@ void k_path(KArgs A) {
         rad.x += thr.x * O.local.x;
         rad.y += thr.y * O.local.y;
         rad.z += thr.z * O.local.z;
-        for (uint32_t k = 0; k < nsh; ++k) {  // ShadowHit/Miss/AnyHit: contribution * visibility
+        // ShadowHit/Miss/AnyHit: contribution * visibility, slot by slot.  The wave walks the slots
+        // together; at depth 1 (packet bit 1) slot 0 -- the sun shadow rays of an 8x8 pixel block's
+        // primary hits: one direction, nearby origins -- takes the wave-coherent traversal.
+        for (uint32_t k = 0; __ballot(k < nsh) != 0ull; ++k) {
+            const bool live = k < nsh;
             const size_t slot = size_t(k) * A.F.qsize + p;
-            const float4 o4 = A.F.sh_org[slot];
-            const float4 d4 = A.F.sh_dir[slot];
-            const float4 c4 = A.F.sh_con[slot];
+            float4 o4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d4 = make_float4(0.0f, 0.0f, 1.0f, 0.0f), c4 = o4;
+            if (live) {
+                o4 = A.F.sh_org[slot];
+                d4 = A.F.sh_dir[slot];
+                c4 = A.F.sh_con[slot];
+            }
             HitRec hs;
-            const bool occluded = traverse<8, true, false>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stk, hs, nv, nt);
-            rad.x += occluded ? c4.x * 0.0f : c4.x;
-            rad.y += occluded ? c4.y * 0.0f : c4.y;
-            rad.z += occluded ? c4.z * 0.0f : c4.z;
+            bool occluded = false;
+            if (d == 1 && k == 0 && (A.P.packet & 2u))
+                occluded = traverse8_packet<true>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live, hs);
+            else if (live)
+                occluded = traverse<8, true, false>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stk, hs, nv, nt);
+            if (live) {
+                rad.x += occluded ? c4.x * 0.0f : c4.x;
+                rad.y += occluded ? c4.y * 0.0f : c4.y;
+                rad.z += occluded ? c4.z * 0.0f : c4.z;
+            }
         }
         if (!O.cont) break;
         org = O.nextOrigin;

@@ -287,8 +287,10 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                             tests (default 0).  Results are identical for every value. */
 #define DXRPT_OPT_PACKET_TRAVERSAL 18u /* BVH8 wave-coherent traversal (the 64 rays of a wave share one node
                                           sequence fetched with scalar loads) per pass, bit mask: 1 = closest
-                                          hit at depth 1 (primary rays), 2 = any hit at depth 1, 4 = closest
-                                          hit at depth >= 2, 8 = any hit at depth >= 2.  Identical results. */
+                                          hit at depth 1 (primary rays), 2 = any hit at depth 1 (megakernel:
+                                          the sun shadow rays of the primary hits), 4 = closest hit at depth
+                                          >= 2, 8 = any hit at depth >= 2 (wavefront only); default 3.
+                                          Identical results. */
 #define DXRPT_OPT_LDS_NODES 19u       /* BVH8 per-lane traversal: each workgroup copies the top this-many nodes
                                          (breadth-first prefix of the tree, 80 B each) into LDS and visits them
                                          there (0..1024, default 0; when set, it replaces

@@ -20,7 +20,7 @@ KEYS = {"w": "width", "m": "mode", "r": "refill", "k": "chunks", "p": "postpone"
         "s": "sblock", "q": "socc", "x": "spatial", "c": "leafcost", "h": "hocc", "g": "sgrid",
         "j": "conc", "t": "pipe", "a": "packet", "n": "ldsnodes", "z": "xcd", "u": "pswitch", "e": "mega", "v": "megaocc"}
 DEFAULTS = {"width": 8, "mode": 0, "refill": 16, "chunks": 4, "postpone": 0, "block": 64, "occ": 7, "sblock": 256,
-            "socc": 0, "spatial": 150, "leafcost": 150, "hocc": 8, "sgrid": 0, "conc": 1, "pipe": 0, "packet": 1, "ldsnodes": 0, "xcd": 0, "pswitch": 0, "mega": 1, "megaocc": 0}
+            "socc": 0, "spatial": 150, "leafcost": 150, "hocc": 8, "sgrid": 0, "conc": 1, "pipe": 0, "packet": 3, "ldsnodes": 0, "xcd": 0, "pswitch": 0, "mega": 1, "megaocc": 0}
 BUILD_KEYS = ("width", "spatial", "leafcost")  # a separate context (BVH) per combination
 
 
