@@ -734,9 +734,11 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // megakernel for small frames (BVH8, no instrumentation, one thread per ray traversal)
         fp.megakernel = (ctx->opt_mega_paths && paths <= ctx->opt_mega_paths && ctx->built_width == 8 && !ctx->opt_count &&
                          ctx->opt_trav_mode == 0) ? 1u : 0u;
-        // register budget by frame size (measured, 1080p L=3 Sponza proxy): 5 waves/SIMD (96 VGPRs, some
-        // spills) once a frame has waves for several rounds, 4 (128 VGPRs, no spills) for a GPU's 1/8 share
-        fp.megakernel_occupancy = ctx->opt_mega_occ ? ctx->opt_mega_occ : (paths > 300000u ? 5u : 4u);
+        // register budget by frame size (measured, Sponza proxy 1080p L=3 and its 1/2, 1/4, 1/8 shares):
+        // more resident waves hide more latency once a frame has waves for several rounds; a GPU's 1/8
+        // share (~4k waves) fits in one round at 4 waves/SIMD without spills
+        fp.megakernel_occupancy = ctx->opt_mega_occ ? ctx->opt_mega_occ
+                                                    : (paths > 1500000u ? 6u : (paths > 300000u ? 5u : 4u));
         hipStream_t s = static_cast<hipStream_t>(stream);
         if (ctx->opt_count) {
             fp.trav = ctx->d_trav.as<unsigned long long>();

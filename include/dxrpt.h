@@ -311,8 +311,8 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                             accumulation -- no passes, no queues; larger frames run the
                                             wavefront passes.  0 = always the wavefront.  Identical results. */
 #define DXRPT_OPT_MEGAKERNEL_OCCUPANCY 24u /* megakernel register budget in waves/SIMD: 0 = by frame size
-                                              (default: 5 above 300,000 paths, else 4), 4 (128 VGPRs, no
-                                              spills), 5, 6, or 3 = the compiler's */
+                                              (default: 6 above 1,500,000 paths, 5 above 300,000, else 4),
+                                              4 (no spills), 5, 6, or 3 = the compiler's */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);
