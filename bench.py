@@ -8,7 +8,8 @@ MaxPathLength 3, one sample per pixel per frame with progressive accumulation.
 A step is one frame (DispatchRays(1920,1080,1) equivalent, DXRPathTracer.cpp:2024-2090) over the whole
 image.  With N ranks the image is split into 16-row bands (band b -> rank b % N) and every frame ends
 with an RCCL gather of the band slabs to rank 0 plus the un-permute: total work per
-frame is fixed, so scaling is "strong".  value = nominal Mrays/s of the whole job (W*H*(1+2(L-1))
+frame is fixed, so scaling is "strong".  The gather of frame f runs on RCCL's stream while frame f+1
+renders (distributed.PipelinedGather); the last frame's gather is inside the timed region.  value = nominal Mrays/s of the whole job (W*H*(1+2(L-1))
 rays per frame, the reference's HUD formula DXRPathTracer.cpp:2171) over the max-over-ranks time.
 Rank 0 prints one JSON line.
 """
@@ -107,7 +108,7 @@ def main():
     import torch.distributed as dist
     import dxrpathtracer_amd as D
     import dxrpathtracer_amd._abi as A
-    from dxrpathtracer_amd.distributed import band_layout, gather_frame, source_index
+    from dxrpathtracer_amd.distributed import PipelinedGather, band_layout, source_index
     from dxrpathtracer_amd.tracer import DXRPathTracer
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -141,20 +142,29 @@ def main():
         idx = torch.tensor(source_index(lay), dtype=torch.long, device="cuda")
     consts = [D.make_constants(scene, settings, sky, WIDTH, HEIGHT, s) for s in range(16)]
 
+    # frame-end gather of the band slabs to rank 0 (RCCL), overlapped with the next frame's render
+    pg = PipelinedGather(lay, rank, full, idx) if world > 1 else None
+
     def frame(f):
         tracer.render_raw(consts[f % 16], settings, accum.data_ptr(), WIDTH, HEIGHT, tiles=tiles, stream=sh,
                           lights=lights)
-        if world > 1:
-            gather_frame(accum, lay, rank, full, idx)
+        if pg is not None:
+            pg.submit(accum)
+
+    def flush():
+        if pg is not None:
+            pg.flush()
 
     # ---- traversal work census (instrumented kernels, untimed): nodes / triangles per ray
     tracer.set_option(A.OPT_COUNT_TRAVERSAL, 1)
     frame(0)
+    flush()
     census = tracer.stats()
     tracer.set_option(A.OPT_COUNT_TRAVERSAL, 0)
 
     for f in range(args.warmup):
         frame(f)
+    flush()
     torch.cuda.synchronize()
 
     # ---- per-kernel breakdown (all kinds, untimed pass before the timed region): picks the dominant
@@ -165,6 +175,7 @@ def main():
     tracer.reset_timing()
     for f in range(min(args.steps, 16)):
         frame(f)
+    flush()
     torch.cuda.synchronize()
     breakdown = tracer.stats()
     kms = {A.KERNEL_NAMES[k]: breakdown.kernel_ms[k] for k in range(A.K_COUNT)}
@@ -185,6 +196,7 @@ def main():
         ev[f][0].record(stream)
         frame(args.warmup + f)
         ev[f][1].record(stream)
+    flush()  # the last frame's gather + un-permute are inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -69,3 +69,54 @@ def gather_frame(local, layout: BandLayout, rank: int, full=None, src_index=None
         allbuf = torch.cat(gather_list, dim=0)
         torch.index_select(allbuf, 0, src_index, out=full)
     return full
+
+
+class PipelinedGather:
+    """The frame-end gather overlapped with the next frame's render.
+
+    submit(local) snapshots the rank's slab into one of two staging buffers (a device copy ordered
+    after the frame's kernels on the current stream) and starts the gather of that snapshot as an
+    asynchronous collective (RCCL runs it on its own stream), then completes the PREVIOUS frame's
+    gather: its wait orders the un-permute into `full` on the current stream.  The collective of frame
+    f therefore runs while frame f+1 renders, instead of between them (the render of f+1 only needs the
+    accumulation buffer, which the snapshot freed).  flush() completes the last frame.  Rank 0's
+    `full` holds frame f's image once submit(f+1) or flush() has returned to the stream."""
+
+    def __init__(self, layout: BandLayout, rank: int, full=None, src_index=None, group=None):
+        self.layout, self.rank, self.full, self.src_index, self.group = layout, rank, full, src_index, group
+        self.staging = None
+        self.recv = None
+        self.pending = None
+        self.count = 0
+
+    def submit(self, local):
+        import torch
+        import torch.distributed as dist
+        if self.layout.world == 1:
+            if self.full is not None:
+                self.full.copy_(local[: self.layout.width * self.layout.height])
+            return
+        if self.staging is None:
+            self.staging = [torch.empty_like(local) for _ in range(2)]
+            if self.rank == 0:
+                self.recv = [[torch.empty_like(local) for _ in range(self.layout.world)] for _ in range(2)]
+        k = self.count % 2
+        self.count += 1
+        self.staging[k].copy_(local)
+        work = dist.gather(self.staging[k], self.recv[k] if self.rank == 0 else None, dst=0, group=self.group,
+                           async_op=True)
+        prev, self.pending = self.pending, (work, k)
+        if prev is not None:
+            self._finish(prev)
+
+    def flush(self):
+        if self.pending is not None:
+            self._finish(self.pending)
+            self.pending = None
+
+    def _finish(self, pend):
+        import torch
+        work, k = pend
+        work.wait()
+        if self.rank == 0:
+            torch.index_select(torch.cat(self.recv[k], dim=0), 0, self.src_index, out=self.full)

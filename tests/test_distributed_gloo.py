@@ -64,3 +64,55 @@ def test_band_gather_reproduces_single_rank_frame(world):
         p.join(timeout=300)
         assert p.exitcode == 0
     assert q.get(timeout=10) is True
+
+
+def _worker_pipelined(rank, world, port, W, H, q):
+    # PipelinedGather over 3 frames with different slab contents: after submit(f+1) rank 0's frame
+    # buffer holds frame f exactly; after flush() the last frame
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dxrpathtracer_amd.distributed import PipelinedGather, band_layout, source_index
+        lay = band_layout(W, H, world)
+        full = torch.zeros((W * H, 4), dtype=torch.float32) if rank == 0 else None
+        idx = torch.tensor(source_index(lay), dtype=torch.long) if rank == 0 else None
+        pg = PipelinedGather(lay, rank, full, idx)
+
+        def frame_image(f):  # the full frame every rank "renders" its bands of, frame f
+            return (np.arange(W * H * 4, dtype=np.float32).reshape(H, W, 4) + 1000.0 * f)
+
+        local = torch.zeros((lay.max_count, 4), dtype=torch.float32)
+        ok = True
+        for f in range(3):
+            img = frame_image(f)
+            for t in lay.rank_tiles(rank):
+                local[t.accum_offset:t.accum_offset + t.w * t.h] = torch.from_numpy(
+                    img[t.y0:t.y0 + t.h, t.x0:t.x0 + t.w].reshape(-1, 4))
+            pg.submit(local)
+            local.fill_(-1.0)  # the next frame overwrites the accumulation buffer: the snapshot must hold
+            if rank == 0 and f > 0:
+                ok &= bool(np.array_equal(full.numpy().reshape(H, W, 4), frame_image(f - 1)))
+        pg.flush()
+        if rank == 0:
+            ok &= bool(np.array_equal(full.numpy().reshape(H, W, 4), frame_image(2)))
+            q.put(ok)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pipelined_gather_delivers_every_frame(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    W, H = 40, 56
+    procs = [ctx.Process(target=_worker_pipelined, args=(r, world, port, W, H, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) is True
