@@ -27,6 +27,11 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 WIDTH, HEIGHT, PATH_LENGTH = 1920, 1080, 3
+SCENE = "sponza"
+# BASELINE.json configs, selectable with --config (the default is the metric's; the others are the
+# parity configs, timed the same way for the record): name -> (scene, width, height, path length)
+CONFIGS = {"metric": ("sponza", 1920, 1080, 3), "c2": ("sponza", 1280, 720, 3), "c3": ("sponza", 1920, 1080, 8),
+           "c4": ("suntemple", 1920, 1080, 3), "c5": ("sponza", 3840, 2160, 6)}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "Mrays/sec + ms/frame, Sponza 1920x1080 path-length 3 at 1/2/4/8 GPU"
 # Algorithmic bytes, per ray, plus the BVH nodes (80 B) and triangle records (48 B) it
@@ -90,7 +95,7 @@ def pmc_traffic(kernel):
             d = json.load(open(p))
         except Exception:
             continue
-        if d.get("config") == f"sponza-proxy {WIDTH}x{HEIGHT} L={PATH_LENGTH}":
+        if d.get("config") == f"{SCENE}-proxy {WIDTH}x{HEIGHT} L={PATH_LENGTH}":
             return d, os.path.basename(p)
     return {}, None
 
@@ -102,7 +107,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
     args = ap.parse_args()
+    global SCENE, WIDTH, HEIGHT, PATH_LENGTH
+    SCENE, WIDTH, HEIGHT, PATH_LENGTH = CONFIGS[args.config]
+    metric = METRIC if args.config == "metric" else \
+        f"Mrays/sec + ms/frame, {SCENE.capitalize()} {WIDTH}x{HEIGHT} path-length {PATH_LENGTH} (BASELINE config {args.config})"
 
     import torch
     import torch.distributed as dist
@@ -124,7 +134,7 @@ def main():
 
     # ---- scene + acceleration structure (untimed, like the reference's InitializeScene + AS build)
     t0 = time.perf_counter()
-    scene = D.Scene("sponza")
+    scene = D.Scene(SCENE)
     settings = scene.settings(MaxPathLength=PATH_LENGTH)
     sky = D.make_sky(settings)
     tracer = DXRPathTracer(local_rank)
@@ -243,7 +253,7 @@ def main():
             cpu = cpu_baseline(scene, sky, settings, args.cpu_threads)
         frames = breakdown.timed_frames or 1
         result = {
-            "metric": METRIC,
+            "metric": metric,
             "value": round(value, 2),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -254,8 +264,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: seeded procedural Sponza proxy (Sponza.fbx absent from the reference snapshot)",
-            "config": {"workload": f"sponza-proxy {WIDTH}x{HEIGHT} L={PATH_LENGTH} 1spp/frame progressive",
+            "data": f"synthetic: seeded procedural {SCENE.capitalize()} proxy ({'Sponza.fbx' if SCENE == 'sponza' else 'SunTemple.fbx'} "
+                    "absent from the reference snapshot)",
+            "config": {"workload": f"{SCENE}-proxy {WIDTH}x{HEIGHT} L={PATH_LENGTH} 1spp/frame progressive",
                        "width": WIDTH, "height": HEIGHT, "max_path_length": PATH_LENGTH,
                        "sqrt_num_samples": 4, "triangles": scene.num_triangles,
                        "parallelism": f"screen bands x{world}" + (" + RCCL gather" if world > 1 else "")},

@@ -112,7 +112,7 @@ struct dxrpt_ctx {
     uint32_t opt_shade_occ = 0;     // DXRPT_OPT_SHADE_OCCUPANCY
     uint32_t opt_xcd = 0;           // DXRPT_OPT_XCD_MAPPING
     uint32_t opt_packet_switch = 0; // DXRPT_OPT_PACKET_SWITCH
-    uint32_t opt_mega_paths = 0xFFFFFFFFu;  // DXRPT_OPT_MEGAKERNEL_PATHS (default: every frame)
+    uint32_t opt_mega_paths = 10000000u;    // DXRPT_OPT_MEGAKERNEL_PATHS (path vertices)
     uint32_t opt_mega_occ = 0;              // DXRPT_OPT_MEGAKERNEL_OCCUPANCY (0 = by frame size)
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
     int built_width = 0;
@@ -732,7 +732,10 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.xcd_map = ctx->opt_xcd;
         fp.packet_switch = ctx->opt_packet_switch;
         // megakernel for small frames (BVH8, no instrumentation, one thread per ray traversal)
-        fp.megakernel = (ctx->opt_mega_paths && paths <= ctx->opt_mega_paths && ctx->built_width == 8 && !ctx->opt_count &&
+        // (path vertices = paths x (L-1); measured crossover ~10M: the megakernel wins on 1080p L=3 and on
+        // every GPU's share of an 8-GPU frame, the wavefront on 4K L=6 and 1080p L=8 full frames)
+        const uint64_t vertices = uint64_t(paths) * uint64_t((settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength) - 1);
+        fp.megakernel = (vertices <= ctx->opt_mega_paths && ctx->built_width == 8 && !ctx->opt_count &&
                          ctx->opt_trav_mode == 0) ? 1u : 0u;
         // register budget by frame size (measured, Sponza proxy 1080p L=3 and its 1/2, 1/4, 1/8 shares):
         // more resident waves hide more latency once a frame has waves for several rounds; a GPU's 1/8

@@ -306,10 +306,12 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 #define DXRPT_OPT_PACKET_SWITCH 22u /* packet traversal: a wave whose share of live lanes entering the visited
                                          nodes falls below this percentage continues one ray per lane
                                          (0 = never).  Identical results. */
-#define DXRPT_OPT_MEGAKERNEL_PATHS 23u /* frames of at most this many paths (default: all) run as ONE kernel, one
-                                            thread per path: raygen, every depth's traversals and shading,
-                                            accumulation -- no passes, no queues; larger frames run the
-                                            wavefront passes.  0 = always the wavefront.  Identical results. */
+#define DXRPT_OPT_MEGAKERNEL_PATHS 23u /* frames of at most this many path vertices (paths x (MaxPathLength-1);
+                                            default 10,000,000) run as ONE kernel, one thread per path:
+                                            raygen, every depth's traversals and shading, accumulation -- no
+                                            passes, no queues; larger frames run the wavefront passes (whose
+                                            compaction wins for long paths on big frames).  0 = always the
+                                            wavefront.  Identical results. */
 #define DXRPT_OPT_MEGAKERNEL_OCCUPANCY 24u /* megakernel register budget in waves/SIMD: 0 = by frame size
                                               (default: 6 above 1,500,000 paths, 5 above 300,000, else 4),
                                               4 (no spills), 5, 6, or 3 = the compiler's */
