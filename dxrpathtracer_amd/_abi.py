@@ -77,7 +77,8 @@ KERNEL_NAMES = ("k_raygen", "k_trace", "k_shade", "k_shadow", "k_accumulate", "k
 (OPT_COUNT_TRAVERSAL, OPT_KERNEL_TIMING, OPT_BVH_WIDTH, OPT_TRAVERSAL_MODE, OPT_REFILL_LANES, OPT_CHUNKS_PER_WAVE,
  OPT_POSTPONE_TRIS, OPT_TRACE_BLOCK, OPT_OCCUPANCY, OPT_SHADE_BLOCK, OPT_SHADE_OCCUPANCY, OPT_SPATIAL_SPLITS,
  OPT_LEAF_COST, OPT_SHADOW_OCCUPANCY, OPT_SHADOW_GRID, OPT_CONCURRENCY, OPT_TRAVERSAL_PIPELINE, OPT_PACKET_TRAVERSAL, OPT_LDS_NODES,
- OPT_KERNEL_TIMING_MASK, OPT_XCD_MAPPING, OPT_PACKET_SWITCH, OPT_MEGAKERNEL_PATHS, OPT_MEGAKERNEL_OCCUPANCY) = range(1, 25)
+ OPT_KERNEL_TIMING_MASK, OPT_XCD_MAPPING, OPT_PACKET_SWITCH, OPT_MEGAKERNEL_PATHS, OPT_MEGAKERNEL_OCCUPANCY,
+ OPT_BAKE_CHUNK) = range(1, 26)
 # context defaults of the traversal options (dxrpt_api.hip)
 DEFAULT_TRAVERSAL_PIPELINE = 0
 POST_FLOAT4, POST_RGBA8 = 0, 1  # dxrpt_post_process output formats
@@ -87,6 +88,7 @@ DEFAULT_XCD_MAPPING = 0
 DEFAULT_PACKET_SWITCH = 0
 DEFAULT_MEGAKERNEL_PATHS = 10000000
 DEFAULT_MEGAKERNEL_OCCUPANCY = 0
+DEFAULT_BAKE_CHUNK = 1 << 21
 
 
 class Stats(C.Structure):
@@ -133,13 +135,14 @@ for _t, _n in ((MeshVertex, 64), (GeometryInfo, 16), (Material, 24), (SpotLight,
 DXRPT_SYMBOLS = ("dxrpt_abi_version", "dxrpt_default_settings", "dxrpt_create", "dxrpt_destroy", "dxrpt_last_error",
                  "dxrpt_set_scene", "dxrpt_add_texture", "dxrpt_set_sky", "dxrpt_build_bvh", "dxrpt_get_bvh_info",
                  "dxrpt_render", "dxrpt_get_stats", "dxrpt_trace_rays", "dxrpt_set_option", "dxrpt_reset_timing",
-                 "dxrpt_post_process")
+                 "dxrpt_post_process", "dxrpt_bake_lightmap", "dxrpt_denoise_median")
 DXRPT_HOST_SYMBOLS = ("dxrpt_host_scene_create", "dxrpt_host_scene_load", "dxrpt_host_scene_destroy", "dxrpt_host_last_error",
                       "dxrpt_host_inv_view_projection", "dxrpt_host_sky_create", "dxrpt_host_fill_constants",
                       "dxrpt_host_float_to_half", "dxrpt_host_half_to_float", "dxrpt_host_hosek_load",
                       "dxrpt_host_hosek_destroy", "dxrpt_host_hosek_last_error", "dxrpt_host_sky_create_hosek",
                       "dxrpt_host_hosek_rgb_radiance", "dxrpt_host_hosek_solar_radiance", "dxrpt_host_spectrum_to_rgb",
-                      "dxrpt_host_spectrum_from_rgb_reflectance")
+                      "dxrpt_host_spectrum_from_rgb_reflectance", "dxrpt_host_lightmap_charts",
+                      "dxrpt_host_surface_map")
 
 _lib = None
 _host = None
@@ -178,6 +181,9 @@ def lib() -> C.CDLL:
         L.dxrpt_trace_rays.argtypes = [P, P, u32, u32, P, P]
         L.dxrpt_post_process.argtypes = [P, C.POINTER(AppSettings), P, u32, u32, P, u32, P]
         L.dxrpt_set_option.argtypes = [P, u32, C.c_uint64]
+        L.dxrpt_bake_lightmap.argtypes = [P, C.POINTER(RayTraceConstants), C.POINTER(AppSettings),
+                                          C.POINTER(LightConstants), P, P, P, P, u32, u32, P]
+        L.dxrpt_denoise_median.argtypes = [P, P, P, u32, u32, P]
         L.dxrpt_reset_timing.argtypes = [P]
         _lib = L
     return _lib
@@ -221,6 +227,8 @@ def host() -> C.CDLL:
         H.dxrpt_host_spectrum_to_rgb.restype = None
         H.dxrpt_host_spectrum_from_rgb_reflectance.argtypes = [P, C.POINTER(f32), C.POINTER(f32)]
         H.dxrpt_host_spectrum_from_rgb_reflectance.restype = None
+        H.dxrpt_host_lightmap_charts.argtypes = [C.POINTER(HostScene), u32, C.POINTER(MeshVertex), P]
+        H.dxrpt_host_surface_map.argtypes = [C.POINTER(MeshVertex), u32, P, u32, u32, u32, P, P]
         _host = H
     return _host
 

@@ -114,10 +114,12 @@ struct dxrpt_ctx {
     uint32_t opt_packet_switch = 0; // DXRPT_OPT_PACKET_SWITCH
     uint32_t opt_mega_paths = 10000000u;    // DXRPT_OPT_MEGAKERNEL_PATHS (path vertices)
     uint32_t opt_mega_occ = 0;              // DXRPT_OPT_MEGAKERNEL_OCCUPANCY (0 = by frame size)
+    uint32_t opt_bake_chunk = 1u << 21;     // DXRPT_OPT_BAKE_CHUNK (texels per bake launch)
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
     int built_width = 0;
     DevBuf d_trav;   // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
     DevBuf d_spill;  // BVH8 traversal stack entries beyond the LDS part (deep trees only)
+    DevBuf d_bake_list;  // live lightmap texels of the last bake pass + their count
     // kernel timing: a ring of per-frame event sets, harvested lazily
     struct FrameEvents {
         std::vector<hipEvent_t> ev;
@@ -142,6 +144,7 @@ struct dxrpt_ctx {
             for (DevBuf& b : qb) b.release();
         d_trav.release();
         d_spill.release();
+        d_bake_list.release();
         for (auto& f : ring)
             for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
         if (aux) {
@@ -461,6 +464,9 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_MEGAKERNEL_OCCUPANCY) {
             require(value == 0 || (value >= 3 && value <= 6), "dxrpt_set_option: megakernel occupancy must be 0 or 3..6");
             ctx->opt_mega_occ = uint32_t(value);
+        } else if (option == DXRPT_OPT_BAKE_CHUNK) {
+            require(value >= 64 && value <= (1u << 26), "dxrpt_set_option: bake chunk must be 64..2^26 texels");
+            ctx->opt_bake_chunk = uint32_t(value);
         } else if (option == DXRPT_OPT_BVH_WIDTH) {
             require(value == 2 || value == 8, "dxrpt_set_option: BVH width must be 2 or 8");
             ctx->opt_width = int(value);  // takes effect at the next dxrpt_build_bvh
@@ -863,6 +869,89 @@ int dxrpt_post_process(dxrpt_ctx* ctx, const dxrpt_app_settings* settings, const
         p.bloom_exp2 = float(std::exp2(double(settings->BloomExposure)));
         p.exposure_scale = float(std::exp2(double(settings->Exposure)) / 0.0009765625);
         HIP_CHECK(launch_post_process(p, static_cast<hipStream_t>(stream)));
+    });
+}
+
+// DXRPathTracer::RenderBakingPass_Progressive (DXRPathTracer.cpp:1895-1991): one DispatchRays(W, H) of
+// BakeRayGen over the surface map.  The dispatch is cut into chunks of texels so the per-texel shadow
+// slots stay bounded; every texel is independent, so the chunking changes nothing in the results.
+int dxrpt_bake_lightmap(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxrpt_app_settings* settings,
+                        const dxrpt_light_constants* lights, const float* surface_pos, const float* surface_normal,
+                        float* accum, float* lightmap, uint32_t width, uint32_t height, void* stream) {
+    if (!ctx) return DXRPT_E_INVALID_ARG;
+    return guarded(ctx, [&] {
+        require(ctx->bvh_built, "dxrpt_bake_lightmap: acceleration structure not built", DXRPT_E_STATE);
+        require(ctx->sky_set, "dxrpt_bake_lightmap: sky cubemap not set", DXRPT_E_STATE);
+        require(rtc && settings && surface_pos && surface_normal && accum && lightmap, "dxrpt_bake_lightmap: null argument");
+        require(width > 0 && height > 0, "dxrpt_bake_lightmap: empty lightmap");
+        require(uint64_t(width) * height < 0x7FFFFFFFull, "dxrpt_bake_lightmap: lightmap too large");
+        require(uint64_t(width) * height == rtc->TotalNumPixels, "dxrpt_bake_lightmap: TotalNumPixels != width*height");
+        require(settings->SqrtNumSamples >= 1, "dxrpt_bake_lightmap: SqrtNumSamples must be >= 1");
+        require(settings->MaxPathLength >= 1 && settings->MaxPathLength <= int(DXRPT_MAX_PATH_LENGTH),
+                "dxrpt_bake_lightmap: MaxPathLength must be in [1, 8]");
+        const bool useLights = settings->RenderLights && rtc->NumLights > 0;
+        require(!useLights || (lights && rtc->NumLights <= DXRPT_MAX_SPOT_LIGHTS), "dxrpt_bake_lightmap: bad lights");
+        upload_textures(ctx);
+        const uint32_t nl = useLights ? rtc->NumLights : 0u;
+        if (nl) {
+            std::vector<dxrpt_spot_light> L(lights->Lights, lights->Lights + nl);
+            if (L.size() != ctx->lights_cache.size() || std::memcmp(L.data(), ctx->lights_cache.data(), nl * sizeof(dxrpt_spot_light)) != 0) {
+                ctx->d_lights.upload(L.data(), nl * sizeof(dxrpt_spot_light));
+                ctx->lights_cache = L;
+            }
+        }
+        const uint32_t total = width * height;
+        const uint32_t chunk = std::min<uint32_t>(total, ctx->opt_bake_chunk);
+        ensure_frame(ctx, chunk, 2u + nl);
+        FrameParams fp;
+        fp.rtc = *rtc;
+        fp.rtc.NumLights = nl;
+        fp.set = *settings;
+        fp.lights = nl ? ctx->d_lights.as<dxrpt_spot_light>() : nullptr;
+        fp.num_paths = chunk;
+        // register budget as for the megakernel frames (same per-thread path loop)
+        fp.megakernel_occupancy = ctx->opt_mega_occ ? ctx->opt_mega_occ : (chunk > 1500000u ? 6u : (chunk > 300000u ? 5u : 4u));
+        fp.width = width;
+        fp.height = height;
+        const SceneDev sd = scene_dev(ctx, frame_traversal_threads(chunk, ctx->fb.shadow_slots, 0));
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        BakeArgs b;
+        b.pos = reinterpret_cast<const float4*>(surface_pos);
+        b.nrm = reinterpret_cast<const float4*>(surface_normal);
+        b.accum = reinterpret_cast<float4*>(accum);
+        b.lightmap = reinterpret_cast<float4*>(lightmap);
+        b.width = width;
+        b.height = height;
+        ctx->d_bake_list.ensure(size_t(total) * sizeof(uint32_t) + 64);
+        b.list = ctx->d_bake_list.as<uint32_t>();
+        b.count = b.list + total;  // the entry count lives after the list
+        HIP_CHECK(launch_bake_compact(b.pos, total, const_cast<uint32_t*>(b.list), const_cast<uint32_t*>(b.count), s));
+        HIP_CHECK(hipMemsetAsync(ctx->fb.counters, 0, 2 * kMaxDepthQueues * kQueueShards * sizeof(uint32_t), s));
+        // the live count stays on the device (no host sync): launches cover every texel, and chunks
+        // past the live count exit at once
+        for (uint32_t first = 0; first < total; first += chunk) {
+            b.first = first;
+            b.span = std::min(chunk, total - first);
+            HIP_CHECK(launch_bake(sd, ctx->fb, fp, b, s));
+        }
+        // dxrpt_get_stats then reports this pass: texels and the rays its paths traced
+        ctx->last_stream = s;
+        ctx->last_L = settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength;
+        std::memset(&ctx->last, 0, sizeof(ctx->last));
+        ctx->last.pixels = total;
+        ctx->rendered = true;
+    });
+}
+
+// DXRPathTracer::RenderLightmapMedianPass (DXRPathTracer.cpp:2092-2125): DenoiseCS with FilterRadius 1.
+int dxrpt_denoise_median(dxrpt_ctx* ctx, const float* in, float* out, uint32_t width, uint32_t height, void* stream) {
+    if (!ctx) return DXRPT_E_INVALID_ARG;
+    return guarded(ctx, [&] {
+        require(in && out, "dxrpt_denoise_median: null argument");
+        require(in != out, "dxrpt_denoise_median: in and out must not alias");
+        require(width > 0 && height > 0 && uint64_t(width) * height < 0x7FFFFFFFull, "dxrpt_denoise_median: bad size");
+        HIP_CHECK(launch_median3x3(reinterpret_cast<const float4*>(in), reinterpret_cast<float4*>(out), width, height,
+                                   static_cast<hipStream_t>(stream)));
     });
 }
 

@@ -26,4 +26,7 @@ struct PostParams {
 
 hipError_t launch_post_process(const PostParams& p, hipStream_t stream);
 
+// DenoiseMedian.hlsl (FilterRadius 1): luminance-median of each texel's clamped 3x3 neighbourhood.
+hipError_t launch_median3x3(const float4* in, float4* out, uint32_t w, uint32_t h, hipStream_t stream);
+
 }  // namespace dxrpt

@@ -129,6 +129,47 @@ uint32_t blocks(uint64_t n) { return uint32_t((n + kPostBlock - 1) / kPostBlock)
 
 }  // namespace
 
+// DenoiseCS (DenoiseMedian.hlsl:49-102): the 3x3 neighbourhood (coordinates clamped to the image) sorted
+// by luminance with the shader's insertion sort, the middle element (index 4) written with alpha 1.
+// The insertion sort is unrolled into compare-and-swap steps with static indices (the array stays in
+// registers): inserting element a walks j = a-1 .. 0 and swaps while the element before is brighter;
+// the `moving` flag stops the walk exactly where the shader's while loop stops (NaN keys included).
+__global__ __launch_bounds__(kPostBlock) void k_median3x3(const float4* __restrict__ in, float4* __restrict__ out,
+                                                          uint32_t w, uint32_t h) {
+    const uint32_t i = blockIdx.x * kPostBlock + threadIdx.x;
+    if (i >= w * h) return;
+    const int x = int(i % w), y = int(i / w);
+    float3 nb[9];
+    float lum[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        const int cx = min(max(x + (k % 3) - 1, 0), int(w) - 1), cy = min(max(y + (k / 3) - 1, 0), int(h) - 1);
+        const float4 v = in[size_t(cy) * w + cx];
+        nb[k] = make_float3(v.x, v.y, v.z);
+        lum[k] = (v.x * 0.299f + v.y * 0.587f) + v.z * 0.114f;
+    }
+#pragma unroll
+    for (int a = 1; a < 9; ++a) {
+        bool moving = true;
+#pragma unroll
+        for (int j = a - 1; j >= 0; --j) {
+            moving = moving && (lum[j] > lum[j + 1]);
+            const float3 lo = nb[j], hi = nb[j + 1];
+            const float ll = lum[j], lh = lum[j + 1];
+            nb[j] = moving ? hi : lo;
+            nb[j + 1] = moving ? lo : hi;
+            lum[j] = moving ? lh : ll;
+            lum[j + 1] = moving ? ll : lh;
+        }
+    }
+    out[i] = make_float4(nb[4].x, nb[4].y, nb[4].z, 1.0f);
+}
+
+hipError_t launch_median3x3(const float4* in, float4* out, uint32_t w, uint32_t h, hipStream_t stream) {
+    hipLaunchKernelGGL(k_median3x3, dim3(blocks(uint64_t(w) * h)), dim3(kPostBlock), 0, stream, in, out, w, h);
+    return hipGetLastError();
+}
+
 hipError_t launch_post_process(const PostParams& p, hipStream_t stream) {
     const uint32_t bw = p.width / 2, bh = p.height / 2;
     if (bw > 0 && bh > 0) {

@@ -148,6 +148,26 @@ inline int frame_event_count(int L) { return 2 * (2 + 4 * (L - 1)); }
 hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream,
                         hipEvent_t* ev, hipStream_t aux = nullptr, hipEvent_t* fork_ev = nullptr);
 
+// Lightmap baking (BakeRayGen) over a width x height lightmap.  launch_bake_compact lists the texels
+// inside a UV island (pos.w != 0; the others are skipped by BakeRayGen) into list[0, *count), so the
+// bake waves carry only live texels; launch_bake then traces list entries [first, first + span)
+// (threads past *count exit), shadow slots indexed by entry - first (FrameBuffers sized for >= span
+// paths).  Ray counts are added to fb.counters (the caller zeroes them once per bake pass).  fp
+// carries the constants (rtc.TotalNumPixels = width * height, rtc.CurrSampleIdx = the bake sample
+// index), settings, lights.
+struct BakeArgs {
+    const float4* pos;   // surface map: world position, w = 1 inside a UV island (0 outside)
+    const float4* nrm;   // surface map: world normal
+    float4* accum;       // rgb sum of valid samples, w = valid sample count (in/out)
+    float4* lightmap;    // rgb average, w = 1
+    const uint32_t* list;   // live texel indices (launch_bake_compact)
+    const uint32_t* count;  // number of list entries (device)
+    uint32_t width, height, first, span;
+};
+hipError_t launch_bake_compact(const float4* pos, uint32_t texels, uint32_t* list, uint32_t* count, hipStream_t stream);
+hipError_t launch_bake(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, const BakeArgs& b,
+                       hipStream_t stream);
+
 // Closest-hit / any-hit queries on arbitrary rays (dxrpt_trace_rays): rays are (o.xyz, tmin),
 // (d.xyz, tmax) pairs; hits are (t, b1, b2, bits(global tri)) with t = -1 and tri = ~0 on miss.
 hipError_t launch_trace_rays(const SceneDev& scene, const float4* rays, uint32_t n, uint32_t flags, float4* hits,

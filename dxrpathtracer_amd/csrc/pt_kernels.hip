@@ -1504,42 +1504,43 @@ PT_DEV void count_rays(uint32_t* counters, uint32_t n) {
     if (lane == leader && total) atomicAdd(&counters[shard], total);
 }
 
-template <int kOcc>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
-void k_path(KArgs A) {
-    extern __shared__ int stack[];
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= A.P.num_paths) return;
-    lds_int* stk = lane_stack(A.S, stack);
+// One path from its first ray (PathLength 1) to its end: per depth the closest hit, path_vertex and
+// the vertex's shadow rays in slot order -- the megakernel's per-thread loop, shared by k_path (camera
+// paths) and k_bake (lightmap texels).  `slot_p` (< F.qsize) indexes the per-slot shadow buffers, `pix`
+// is the CMJ pattern index; `packet` bit 0 / bit 1: wave-coherent traversal for the depth-1 closest hit
+// / the depth-1 sun shadow rays (all lanes must be active at depth 1 then).  Returns the radiance.
+// kBake: the first ray is BakeRayGen's (TMin 0.0001, IsDiffuse, no packets) instead of RaygenShader's.
+template <bool kBake>
+PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, f3 dir, float tmax, lds_int* stk) {
     const dxrpt_app_settings& set = A.P.set;
-    const PrimaryRay pr = primary_ray(A, p);
-    f3 org = pr.start, dir = pr.dir;
-    float tmax = pr.length;
+    const float tmin1 = kBake ? 0.0001f : 0.0f;
+    const bool isDiffuse1 = kBake;
+    const uint32_t packet = kBake ? 0u : A.P.packet;
     f3 thr = f3{1.0f, 1.0f, 1.0f};
     float payloadRoughness = 0.0f;
-    bool payloadIsDiffuse = false;
+    bool payloadIsDiffuse = isDiffuse1;
     float4 rad = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const int L = set.MaxPathLength < 2 ? 2 : set.MaxPathLength;
     for (int d = 1; d <= L - 1; ++d) {
         count_rays(A.F.counters + uint32_t(d) * kQueueShards, 1u);
         HitRec h;
         uint32_t nv = 0, nt = 0;
-        if (d == 1 && (A.P.packet & 1u))  // coherent primary rays: wave-coherent traversal (same results)
-            traverse8_packet<false>(A.S, org, dir, 0.0f, tmax, d <= set.MaxAnyHitPathLength, true, h);
+        if (d == 1 && (packet & 1u))  // coherent primary rays: wave-coherent traversal (same results)
+            traverse8_packet<false>(A.S, org, dir, tmin1, tmax, d <= set.MaxAnyHitPathLength, true, h);
         else
-            traverse<8, false, false>(A.S, org, dir, d == 1 ? 0.0f : kRayTMin, tmax, d <= set.MaxAnyHitPathLength, stk, h, nv, nt);
+            traverse<8, false, false>(A.S, org, dir, d == 1 ? tmin1 : kRayTMin, tmax, d <= set.MaxAnyHitPathLength, stk, h, nv, nt);
         VertexIn V;
         V.inOrigin = org;
         V.inDir = dir;
         V.pathThr = thr;
         V.payloadRoughness = payloadRoughness;
         V.payloadIsDiffuse = payloadIsDiffuse;
-        V.pix = pr.pixelIdx;
+        V.pix = pix;
         V.hit = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
         VertexOut O;
         uint32_t nsh = 0;
         path_vertex(A, d, V, [&](f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
-            emit_shadow(A, p, nsh, o, dd, tmn, tmx, c, fo);
+            emit_shadow(A, slot_p, nsh, o, dd, tmn, tmx, c, fo);
         }, O);
         count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, nsh);
         rad.x += thr.x * O.local.x;
@@ -1550,7 +1551,7 @@ void k_path(KArgs A) {
         // primary hits: one direction, nearby origins -- takes the wave-coherent traversal.
         for (uint32_t k = 0; __ballot(k < nsh) != 0ull; ++k) {
             const bool live = k < nsh;
-            const size_t slot = size_t(k) * A.F.qsize + p;
+            const size_t slot = size_t(k) * A.F.qsize + slot_p;
             float4 o4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d4 = make_float4(0.0f, 0.0f, 1.0f, 0.0f), c4 = o4;
             if (live) {
                 o4 = A.F.sh_org[slot];
@@ -1559,7 +1560,7 @@ void k_path(KArgs A) {
             }
             HitRec hs;
             bool occluded = false;
-            if (d == 1 && k == 0 && (A.P.packet & 2u))
+            if (d == 1 && k == 0 && (packet & 2u))
                 occluded = traverse8_packet<true>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live, hs);
             else if (live)
                 occluded = traverse<8, true, false>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stk, hs, nv, nt);
@@ -1577,7 +1578,88 @@ void k_path(KArgs A) {
         payloadRoughness = O.nextRoughness;
         payloadIsDiffuse = O.nextIsDiffuse;
     }
+    return rad;
+}
+
+template <int kOcc>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
+void k_path(KArgs A) {
+    extern __shared__ int stack[];
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= A.P.num_paths) return;
+    lds_int* stk = lane_stack(A.S, stack);
+    const PrimaryRay pr = primary_ray(A, p);
+    const float4 rad = trace_path<false>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk);
     accumulate_pixel(A, pr.accumIdx, rad);
+}
+
+// ---- lightmap baking (Baking.hlsl:336-465, BakeRayGen) -------------------------------------------
+// One thread per lightmap texel of the chunk [first, first + count): the surface map's world position
+// and normal (SurfaceMap.hlsl raster), a tangent frame from the normal, CMJ set 0 at the texel index
+// (TotalNumPixels = the lightmap's texel count, DXRPathTracer.cpp:1934-1935), a cosine-hemisphere ray
+// traced as a PathLength-1 diffuse path (the same trace_path as the camera paths), the firefly clamp
+// against the running average and the valid-sample accumulation (rgb sum, count), then the average
+// into the lightmap.  Bad inputs write the reference's marker colours.
+PT_DEV float luma(float3 c) { return (c.x * 0.299f + c.y * 0.587f) + c.z * 0.114f; }
+
+template <int kOcc>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
+void k_bake(KArgs A, BakeArgs B) {
+    extern __shared__ int stack[];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B.span || B.first + i >= *B.count) return;
+    const uint32_t texel = B.list[B.first + i];
+    const float4 pos4 = B.pos[texel];  // w != 0: inside a UV island (Baking.hlsl:351-354 in the compaction)
+    const f3 worldPos = f3{pos4.x, pos4.y, pos4.z};
+    if (isinf(worldPos.x) || isinf(worldPos.y) || isinf(worldPos.z)) {
+        B.lightmap[texel] = make_float4(0.0f, 0.0f, 1.0f, 1.0f);
+        return;
+    }
+    const float4 n4 = B.nrm[texel];
+    const f3 nv = f3{n4.x, n4.y, n4.z};
+    if (dot3(nv, nv) < 0.0001f) {
+        B.lightmap[texel] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+        return;
+    }
+    const f3 N = normalize3(nv);
+    const f3 up = fabsf(N.z) < 0.999f ? f3{0.0f, 0.0f, 1.0f} : f3{1.0f, 0.0f, 0.0f};
+    const f3 T = normalize3(cross3(up, N));
+    const f3 Bt = cross3(N, T);
+    float sx, sy;
+    const uint32_t nS = uint32_t(A.P.set.SqrtNumSamples);
+    sample_cmj2d(A.P.rtc.CurrSampleIdx, nS, nS, 0u * A.P.rtc.TotalNumPixels + texel, &sx, &sy);
+    const f3 dTS = sample_cosine_hemisphere(sx, sy);
+    const f3 dir = add(add(scl(T, dTS.x), scl(Bt, dTS.y)), scl(N, dTS.z));  // mul(dirTS, float3x3(T, B, N))
+    const f3 origin = add(worldPos, scl(dir, 0.00001f));
+    const bool badO = isinf(origin.x) || isinf(origin.y) || isinf(origin.z) || isnan(origin.x) || isnan(origin.y) || isnan(origin.z);
+    const bool badD = isinf(dir.x) || isinf(dir.y) || isinf(dir.z) || isnan(dir.x) || isnan(dir.y) || isnan(dir.z) ||
+                      len3(dir) < 0.001f;
+    if (badO || badD) {
+        B.lightmap[texel] = make_float4(1.0f, 0.0f, 1.0f, 1.0f);
+        return;
+    }
+    const float4 r = trace_path<true>(A, i, texel, origin, dir, kFP32Max, lane_stack(A.S, stack));
+    float3 c = make_float3(r.x, r.y, r.z);
+    const float4 prev = B.accum[texel];
+    float3 sum = make_float3(prev.x, prev.y, prev.z);
+    float n = prev.w;
+    if (n >= 1.0f) {  // firefly clamp against the running average (x10 its luminance)
+        const float3 avg = make_float3(sum.x / n, sum.y / n, sum.z / n);
+        const float avgL = luma(avg) + 0.001f;
+        const float sL = luma(c);
+        if (sL > avgL * 10.0f) {
+            const float k = avgL * 10.0f / sL;
+            c = make_float3(c.x * k, c.y * k, c.z * k);
+        }
+    }
+    const bool valid = !(isnan(c.x) || isnan(c.y) || isnan(c.z)) && !(luma(c) < 0.0001f);
+    if (valid) {
+        sum = make_float3(sum.x + c.x, sum.y + c.y, sum.z + c.z);
+        n += 1.0f;
+    }
+    B.accum[texel] = make_float4(sum.x, sum.y, sum.z, n);
+    const float3 avg = n > 0.0f ? make_float3(sum.x / n, sum.y / n, sum.z / n) : make_float3(0.0f, 0.0f, 0.0f);
+    B.lightmap[texel] = make_float4(avg.x, avg.y, avg.z, 1.0f);
 }
 
 // Arbitrary ray queries (dxrpt_trace_rays): flags bit0 = any-hit (shadow) semantics,
@@ -1770,6 +1852,42 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
     start(slot_of(L, 0), stream);
     hipLaunchKernelGGL(k_accumulate, dim3(g), dim3(kBlock), 0, stream, A);
     stop(slot_of(L, 0), stream);
+    return hipGetLastError();
+}
+
+// Live-texel list: one ballot + one atomic per wave; the order of the waves' segments does not matter
+// (every texel is independent and keeps its own CMJ pattern index).
+__global__ __launch_bounds__(256) void k_bake_compact(const float4* __restrict__ pos, uint32_t texels,
+                                                      uint32_t* __restrict__ list, uint32_t* __restrict__ count) {
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    const bool live = t < texels && pos[t].w != 0.0f;
+    const uint64_t m = __ballot(live);
+    if (m == 0ull) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t leader = uint32_t(__ffsll((unsigned long long)m) - 1);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, uint32_t(__popcll(m)));
+    base = __shfl(base, int(leader));
+    if (live) list[base + uint32_t(__popcll(m & ((1ull << lane) - 1ull)))] = t;
+}
+
+hipError_t launch_bake_compact(const float4* pos, uint32_t texels, uint32_t* list, uint32_t* count, hipStream_t stream) {
+    hipError_t e = hipMemsetAsync(count, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_bake_compact, dim3((texels + 255u) / 256u), dim3(256), 0, stream, pos, texels, list, count);
+    return hipGetLastError();
+}
+
+hipError_t launch_bake(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, const BakeArgs& b,
+                       hipStream_t stream) {
+    if (b.span == 0) return hipSuccess;
+    KArgs A{scene, fb, fp};
+    const uint32_t tb = 64;
+    const size_t lds = size_t(scene.stack_ints) * tb * sizeof(int);
+    const dim3 g((b.span + tb - 1u) / tb);
+    if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_bake<6>), g, dim3(tb), lds, stream, A, b);
+    else if (fp.megakernel_occupancy == 5) hipLaunchKernelGGL((k_bake<5>), g, dim3(tb), lds, stream, A, b);
+    else hipLaunchKernelGGL((k_bake<4>), g, dim3(tb), lds, stream, A, b);
     return hipGetLastError();
 }
 

@@ -256,3 +256,31 @@ def make_lights(scene: Scene) -> A.LightConstants:
 def nominal_rays(width: int, height: int, max_path_length: int) -> int:
     """HUD ray count, DXRPathTracer.cpp:2171."""
     return width * height * (1 + (max_path_length - 1) * 2)
+
+
+# ---- lightmap bake inputs ----------------------------------------------------------------------------
+def lightmap_charts(scene: Scene, resolution: int) -> tuple[np.ndarray, np.ndarray]:
+    """The lightmapped mesh (dxrpt_host_lightmap_charts; the reference uses xatlas, Model.cpp:608-715):
+    (vertices (3T, 16) float32 in the MeshVertex layout with LightmapUV set, indices (3T,) uint32)."""
+    n = (int(scene._host.num_indices) // 3) * 3
+    verts = np.zeros((n, 16), dtype=np.float32)
+    idx = np.zeros(n, dtype=np.uint32)
+    rc = A.host().dxrpt_host_lightmap_charts(scene._p, resolution,
+                                             verts.ctypes.data_as(C.POINTER(A.MeshVertex)), idx.ctypes.data)
+    if rc != 0:
+        raise ValueError(f"dxrpt_host_lightmap_charts: {n // 3} charts do not fit a {resolution}^2 lightmap")
+    return verts, idx
+
+
+def surface_map(vertices: np.ndarray, indices: np.ndarray, width: int, height: int) -> tuple[np.ndarray, np.ndarray]:
+    """RenderSurfaceMap (dxrpt_host_surface_map): (position (H, W, 4), normal (H, W, 4)) float32."""
+    vertices = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1, 16)
+    indices = np.ascontiguousarray(indices, dtype=np.uint32)
+    pos = np.empty((height, width, 4), dtype=np.float32)
+    nrm = np.empty((height, width, 4), dtype=np.float32)
+    rc = A.host().dxrpt_host_surface_map(vertices.ctypes.data_as(C.POINTER(A.MeshVertex)), vertices.shape[0],
+                                         indices.ctypes.data, indices.size, width, height, pos.ctypes.data,
+                                         nrm.ctypes.data)
+    if rc != 0:
+        raise ValueError("dxrpt_host_surface_map: bad arguments (index out of range or size)")
+    return pos, nrm

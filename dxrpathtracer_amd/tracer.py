@@ -132,6 +132,25 @@ class DXRPathTracer:
         self._check(self._L.dxrpt_trace_rays(self._ctx, C.c_void_p(rays_ptr), n, flags, C.c_void_p(hits_ptr),
                                              C.c_void_p(stream)), "dxrpt_trace_rays")
 
+    # ---- lightmap baking (DXRPathTracer.cpp:1993-2022, 1895-1991, 2092-2125) --------------------------
+    def bake_lightmap(self, settings: A.AppSettings, surface_pos_ptr: int, surface_normal_ptr: int, accum_ptr: int,
+                      lightmap_ptr: int, width: int, height: int, sample_idx: int, stream: int = 0,
+                      lights: A.LightConstants | None = None):
+        """RenderBakingPass_Progressive: one BakeRayGen pass (sample `sample_idx`) over a width x height
+        lightmap; all pointers are device float4 arrays.  The caller clears accum/lightmap before sample 0
+        and advances sample_idx (bakingSampleIndex++, DXRPathTracer.cpp:2020)."""
+        rtc = make_constants(self.scene, settings, self.sky, width, height, sample_idx)
+        lc = lights if lights is not None else make_lights(self.scene)
+        self._check(self._L.dxrpt_bake_lightmap(self._ctx, C.byref(rtc), C.byref(settings), C.byref(lc),
+                                                C.c_void_p(surface_pos_ptr), C.c_void_p(surface_normal_ptr),
+                                                C.c_void_p(accum_ptr), C.c_void_p(lightmap_ptr), width, height,
+                                                C.c_void_p(stream)), "dxrpt_bake_lightmap")
+
+    def denoise_median(self, in_ptr: int, out_ptr: int, width: int, height: int, stream: int = 0):
+        """RenderLightmapMedianPass: DenoiseCS (3x3 luminance median) from `in` into `out` (device float4)."""
+        self._check(self._L.dxrpt_denoise_median(self._ctx, C.c_void_p(in_ptr), C.c_void_p(out_ptr), width, height,
+                                                 C.c_void_p(stream)), "dxrpt_denoise_median")
+
 
 def row_band_tiles(width: int, height: int, rank: int, world: int, band: int = 16):
     """Screen-space sharding: bands of `band` full rows, band b -> rank b % world,

@@ -315,6 +315,8 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 #define DXRPT_OPT_MEGAKERNEL_OCCUPANCY 24u /* megakernel register budget in waves/SIMD: 0 = by frame size
                                               (default: 6 above 1,500,000 paths, 5 above 300,000, else 4),
                                               4 (no spills), 5, 6, or 3 = the compiler's */
+#define DXRPT_OPT_BAKE_CHUNK 25u /* texels per dxrpt_bake_lightmap launch (default 2^21; bounds the
+                                    per-texel shadow-slot buffers).  Identical results. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);
@@ -354,6 +356,28 @@ int dxrpt_get_stats(dxrpt_ctx* ctx, dxrpt_stats* out);
 #define DXRPT_TRACE_ALPHA 2u
 int dxrpt_trace_rays(dxrpt_ctx* ctx, const float* rays, uint32_t num_rays, uint32_t flags, float* hits,
                      void* stream);
+
+/* ---- lightmap baking (the second consumer of PathTrace) ----------------------------------------
+ * One progressive bake pass: BakeRayGen (DXRPathTracer/Baking.hlsl:336-465) as dispatched by
+ * DXRPathTracer::RenderBakingPass_Progressive (DXRPathTracer.cpp:1895-1991), one thread per texel of
+ * a width x height lightmap (all device float4, row-major):
+ *   surface_pos    world position, w != 0 inside a UV island (SurfaceMap.hlsl SV_Target0; w = 0 skips)
+ *   surface_normal world normal (SV_Target1)
+ *   accum          in/out: rgb = sum of the valid samples, w = their count (g_AccumulationBuffer)
+ *   lightmap       out: rgb = accum average, w = 1 (g_BakedLightMap); marker colours for bad texels
+ * A cosine-hemisphere ray around the normal (CMJ set 0 at the texel index, sample rtc->CurrSampleIdx)
+ * is traced as the first ray of a diffuse path (PathTrace with the scene's lights and sky), clamped
+ * against the running average (x10 luminance) and accumulated if valid.  rtc->TotalNumPixels must be
+ * width*height (DXRPathTracer.cpp:1934-1935).  Clear accum and lightmap to 0 before sample 0.
+ * Stream-ordered like dxrpt_render; dxrpt_get_stats afterwards reports the pass (pixels = texels,
+ * the radiance/shadow rays its paths traced). */
+int dxrpt_bake_lightmap(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxrpt_app_settings* settings,
+                        const dxrpt_light_constants* lights, const float* surface_pos, const float* surface_normal,
+                        float* accum, float* lightmap, uint32_t width, uint32_t height, void* stream);
+/* DenoiseCS (DenoiseMedian.hlsl:52-102, FilterRadius 1 as bound by DXRPathTracer.cpp:2106): each
+ * texel's clamped 3x3 neighbourhood of `in` (device float4 W*H) sorted by luminance
+ * (0.299, 0.587, 0.114) with a stable insertion sort; the 5th (median) rgb, alpha 1, into `out`. */
+int dxrpt_denoise_median(dxrpt_ctx* ctx, const float* in, float* out, uint32_t width, uint32_t height, void* stream);
 
 #ifdef __cplusplus
 }

@@ -133,6 +133,21 @@ void dxrpt_host_fill_constants(const float inv_view_projection[16], const float 
                                const float sun_render_color[3], uint32_t curr_sample_idx, uint32_t width,
                                uint32_t height, uint32_t num_lights, dxrpt_ray_trace_constants* out);
 
+/* ---- lightmap bake inputs (dxrpt_bake_lightmap) ------------------------------------------------
+ * The "lightmapped" mesh the reference gets from xatlas (Graphics/Model.cpp:608-715; xatlas is not in
+ * this image): every triangle of `scene` (in geometry order) becomes its own chart, two triangles per
+ * cell of a square grid over a resolution x resolution lightmap with 1-2 texels of gutter.  Writes
+ * 3 * (num_indices / 3) vertices (all attributes copied, LightmapUV set) and as many 32-bit indices
+ * (0, 1, 2, ...).  DXRPT_E_INVALID_ARG if the cells would be under 4 texels. */
+int dxrpt_host_lightmap_charts(const dxrpt_host_scene* scene, uint32_t resolution, dxrpt_mesh_vertex* out_vertices,
+                               uint32_t* out_indices);
+/* RenderSurfaceMap (DXRPathTracer.cpp:1845-1893, SurfaceMap.hlsl): rasterises the lightmapped mesh at
+ * LightmapUV into width x height float4 maps, cleared to 0: position (xyz, 1) and normalised normal
+ * (xyz, 1).  D3D rules (1/256 snapping, pixel-centre sampling, top-left fill), no culling, no depth
+ * test: the last triangle drawn over a texel wins. */
+int dxrpt_host_surface_map(const dxrpt_mesh_vertex* vertices, uint32_t num_vertices, const uint32_t* indices,
+                           uint32_t num_indices, uint32_t width, uint32_t height, float* out_pos, float* out_normal);
+
 /* IEEE binary16 <-> binary32 (round to nearest even), used for the cube texels. */
 uint16_t dxrpt_host_float_to_half(float f);
 float dxrpt_host_half_to_float(uint16_t h);

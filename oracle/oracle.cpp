@@ -850,6 +850,66 @@ F3 Raygen(const Ctx& C, uint32_t x, uint32_t y, uint32_t W, uint32_t H) {
               std::fmin(std::fmax(payload.Radiance.z, 0.0f), kFP16Max)};
 }
 
+// BakeRayGen, DXRPathTracer/Baking.hlsl:336-465 (its PathTrace/miss/hit shaders, Baking.hlsl:96-330,
+// are RayTrace.hlsl's; the shared PathTrace/TraceRadiance above serve both).  Updates texel i of
+// accum/lightmap (float4 each); a texel outside every UV island (pos.w == 0) is left untouched.
+inline float Luminance(F3 c) { return dot(c, F3{0.299f, 0.587f, 0.114f}); }
+
+void BakeTexel(const Ctx& C, uint32_t i, const float* pos, const float* nrm, float* accum, float* lightmap) {
+    const float* P4 = pos + size_t(i) * 4;
+    float* out = lightmap + size_t(i) * 4;
+    if (P4[3] == 0.0f) return;  // 351-354
+    const F3 worldPos = F3{P4[0], P4[1], P4[2]};
+    auto put = [&](float r, float g, float b) { out[0] = r; out[1] = g; out[2] = b; out[3] = 1.0f; };
+    if (std::isinf(worldPos.x) || std::isinf(worldPos.y) || std::isinf(worldPos.z)) return put(0, 0, 1);  // 357-361
+    const F3 worldNormalVec = F3{nrm[size_t(i) * 4], nrm[size_t(i) * 4 + 1], nrm[size_t(i) * 4 + 2]};
+    if (dot(worldNormalVec, worldNormalVec) < 0.0001f) return put(0, 0, 0);  // 363-369
+    const F3 worldNormal = normalize(worldNormalVec);
+    uint32_t sampleSetIdx = 0;
+    // 376-379: tangentToWorld rows (tangent, bitangent, normal)
+    const F3 up = std::fabs(worldNormal.z) < 0.999f ? F3{0, 0, 1} : F3{1, 0, 0};
+    const F3 tangent = normalize(cross(up, worldNormal));
+    const F3 bitangent = cross(worldNormal, tangent);
+    float hs[2];
+    SamplePoint(C, i, sampleSetIdx, hs);  // 382 (pixelIdx = y * W + x = i)
+    const F3 rayDirTS = SampleDirectionCosineHemisphere(hs[0], hs[1]);
+    const F3 rayDir = (tangent * rayDirTS.x + bitangent * rayDirTS.y) + worldNormal * rayDirTS.z;  // 386
+    const F3 origin = worldPos + rayDir * 0.00001f;                                                    // 390
+    auto bad = [](F3 v) {
+        return std::isinf(v.x) || std::isinf(v.y) || std::isinf(v.z) || std::isnan(v.x) || std::isnan(v.y) || std::isnan(v.z);
+    };
+    if (bad(origin) || bad(rayDir) || length(rayDir) < 0.001f) return put(1, 0, 1);  // 395-396, 415-419
+    PrimaryPayload payload;
+    payload.Radiance = F3{0, 0, 0};
+    payload.Roughness = 0.0f;
+    payload.PathLength = 1;
+    payload.PixelIdx = i;
+    payload.SampleSetIdx = sampleSetIdx;
+    payload.IsDiffuse = true;
+    TraceRadiance(C, origin, rayDir, 0.0001f, kFP32Max, payload.PathLength > uint32_t(C.set.MaxAnyHitPathLength), payload);
+    F3 newSampleColor = payload.Radiance;
+    float* acc = accum + size_t(i) * 4;
+    F3 colorSum = F3{acc[0], acc[1], acc[2]};
+    float validSampleCount = acc[3];
+    if (validSampleCount >= 1.0f) {  // 431-447: firefly clamp at 10x the running average's luminance
+        const F3 averageColor = F3{colorSum.x / validSampleCount, colorSum.y / validSampleCount, colorSum.z / validSampleCount};
+        const float averageLuminance = Luminance(averageColor) + 0.001f;
+        const float sampleLuminance = Luminance(newSampleColor);
+        if (sampleLuminance > averageLuminance * 10.0f) newSampleColor = newSampleColor * (averageLuminance * 10.0f / sampleLuminance);
+    }
+    const bool isNan = std::isnan(newSampleColor.x) || std::isnan(newSampleColor.y) || std::isnan(newSampleColor.z);
+    const bool isTooDark = Luminance(newSampleColor) < 0.0001f;
+    if (!isNan && !isTooDark) {  // 454-458
+        colorSum = colorSum + newSampleColor;
+        validSampleCount += 1.0f;
+    }
+    acc[0] = colorSum.x; acc[1] = colorSum.y; acc[2] = colorSum.z; acc[3] = validSampleCount;
+    F3 averageColor = F3{0, 0, 0};
+    if (validSampleCount > 0.0f)
+        averageColor = F3{colorSum.x / validSampleCount, colorSum.y / validSampleCount, colorSum.z / validSampleCount};
+    put(averageColor.x, averageColor.y, averageColor.z);  // 465
+}
+
 struct OracleScene {
     Scene S;
     double build_ms = 0;
@@ -959,6 +1019,67 @@ int oracle_render(const oracle_scene* scene, const oracle_ray_trace_constants* r
         }
     }
     return 0;
+}
+
+int oracle_bake(const oracle_scene* scene, const oracle_ray_trace_constants* rtc, const oracle_app_settings* settings,
+                const oracle_spot_light* lights, const float* pos, const float* nrm, uint32_t width, uint32_t height,
+                uint32_t first, uint32_t count, float* accum, float* lightmap, uint32_t threads, oracle_stats* out_stats) {
+    const Scene& S = reinterpret_cast<const OracleScene*>(scene)->S;
+    if (uint64_t(first) + count > uint64_t(width) * height) return -1;
+    if (threads == 0) threads = std::max(1u, std::thread::hardware_concurrency());
+    const uint32_t nl = (settings->RenderLights && lights) ? std::min(rtc->NumLights, 32u) : 0u;
+    std::atomic<uint32_t> next{0};
+    std::vector<Stats> stats(threads);
+    auto worker = [&](uint32_t tid) {
+        Ctx C{S, *rtc, *settings, lights, nl, stats[tid]};
+        for (;;) {
+            const uint32_t b = next.fetch_add(256);
+            if (b >= count) break;
+            for (uint32_t k = b; k < std::min(count, b + 256u); ++k) BakeTexel(C, first + k, pos, nrm, accum, lightmap);
+        }
+    };
+    std::vector<std::thread> pool;
+    for (uint32_t t = 1; t < threads; ++t) pool.emplace_back(worker, t);
+    worker(0);
+    for (auto& t : pool) t.join();
+    if (out_stats) {
+        std::memset(out_stats, 0, sizeof(*out_stats));
+        for (const Stats& st : stats) {
+            out_stats->radiance_rays += st.radiance_rays;
+            out_stats->shadow_rays += st.shadow_rays;
+            out_stats->node_visits += st.node_visits;
+            out_stats->tri_tests += st.tri_tests;
+        }
+    }
+    return 0;
+}
+
+// DenoiseCS, DXRPathTracer/DenoiseMedian.hlsl:52-102 with FilterRadius 1 (DXRPathTracer.cpp:2106).
+void oracle_median3x3(const float* in, float* out, uint32_t width, uint32_t height) {
+    for (uint32_t y = 0; y < height; ++y)
+        for (uint32_t x = 0; x < width; ++x) {
+            F3 nb[9];
+            int index = 0;
+            for (int dy = -1; dy <= 1; ++dy)
+                for (int dx = -1; dx <= 1; ++dx) {
+                    const int cx = std::min(std::max(int(x) + dx, 0), int(width) - 1);
+                    const int cy = std::min(std::max(int(y) + dy, 0), int(height) - 1);
+                    const float* v = in + (size_t(cy) * width + cx) * 4;
+                    nb[index++] = F3{v[0], v[1], v[2]};
+                }
+            for (int i = 1; i < 9; ++i) {  // 83-95
+                const F3 key = nb[i];
+                const float keyLuminance = Luminance(key);
+                int j = i - 1;
+                while (j >= 0 && Luminance(nb[j]) > keyLuminance) {
+                    nb[j + 1] = nb[j];
+                    j = j - 1;
+                }
+                nb[j + 1] = key;
+            }
+            float* o = out + (size_t(y) * width + x) * 4;
+            o[0] = nb[4].x; o[1] = nb[4].y; o[2] = nb[4].z; o[3] = 1.0f;
+        }
 }
 
 int oracle_trace_rays(const oracle_scene* scene, const float* rays, uint32_t n, uint32_t flags, float* hits) {

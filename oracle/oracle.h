@@ -56,6 +56,13 @@ double oracle_scene_build_ms(const oracle_scene* scene);
 int oracle_render(const oracle_scene* scene, const oracle_ray_trace_constants* rtc, const oracle_app_settings* settings,
                   const oracle_spot_light* lights, uint32_t width, uint32_t height, uint32_t x0, uint32_t y0, uint32_t w,
                   uint32_t h, float* accum, uint32_t threads, oracle_stats* out_stats);
+/* One bake pass (Baking.hlsl BakeRayGen) over texels [first, first + count) of a width x height
+ * lightmap: pos/nrm/accum/lightmap are W*H float4 (same meaning as dxrpt_bake_lightmap). */
+int oracle_bake(const oracle_scene* scene, const oracle_ray_trace_constants* rtc, const oracle_app_settings* settings,
+                const oracle_spot_light* lights, const float* pos, const float* nrm, uint32_t width, uint32_t height,
+                uint32_t first, uint32_t count, float* accum, float* lightmap, uint32_t threads, oracle_stats* out_stats);
+/* DenoiseMedian.hlsl DenoiseCS, FilterRadius 1: in/out W*H float4. */
+void oracle_median3x3(const float* in, float* out, uint32_t width, uint32_t height);
 /* rays: n x 8 floats (o.xyz, tmin, d.xyz, tmax); hits: n x 4 (same encoding as dxrpt_trace_rays). */
 int oracle_trace_rays(const oracle_scene* scene, const float* rays, uint32_t n, uint32_t flags, float* hits);
 

@@ -50,6 +50,9 @@ def lib() -> C.CDLL:
         L.oracle_scene_build_ms.restype = C.c_double
         L.oracle_render.argtypes = [P, P, P, P] + [C.c_uint32] * 6 + [P, C.c_uint32, C.POINTER(OracleStats)]
         L.oracle_trace_rays.argtypes = [P, P, C.c_uint32, C.c_uint32, P]
+        L.oracle_bake.argtypes = [P, P, P, P, P, P] + [C.c_uint32] * 4 + [P, P, C.c_uint32, C.POINTER(OracleStats)]
+        L.oracle_median3x3.argtypes = [P, P, C.c_uint32, C.c_uint32]
+        L.oracle_median3x3.restype = None
         _lib = L
     return _lib
 
@@ -112,3 +115,25 @@ class OracleScene:
         hits = np.zeros((rays.shape[0], 4), dtype=np.float32)
         lib().oracle_trace_rays(self.ptr, rays.ctypes.data, rays.shape[0], flags, hits.ctypes.data)
         return hits
+
+    def bake(self, rtc, settings, lights, pos, nrm, accum, lightmap, first=0, count=None, threads=0):
+        """One BakeRayGen pass over texels [first, first + count); updates accum / lightmap (H, W, 4) in place."""
+        h, w = pos.shape[:2]
+        for a in (pos, nrm, accum, lightmap):
+            assert a.dtype == np.float32 and a.flags.c_contiguous and a.shape == (h, w, 4)
+        count = w * h - first if count is None else count
+        st = OracleStats()
+        rc = lib().oracle_bake(self.ptr, C.addressof(rtc), C.addressof(settings),
+                               C.addressof(lights) if lights is not None else None, pos.ctypes.data, nrm.ctypes.data,
+                               w, h, first, count, accum.ctypes.data, lightmap.ctypes.data, threads, C.byref(st))
+        if rc != 0:
+            raise RuntimeError("oracle_bake failed")
+        return st
+
+
+def median3x3(img: np.ndarray) -> np.ndarray:
+    """DenoiseCS (FilterRadius 1) of an (H, W, 4) float32 image."""
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    out = np.empty_like(img)
+    lib().oracle_median3x3(img.ctypes.data, out.ctypes.data, img.shape[1], img.shape[0])
+    return out
