@@ -115,6 +115,7 @@ struct dxrpt_ctx {
     uint32_t opt_mega_paths = 10000000u;    // DXRPT_OPT_MEGAKERNEL_PATHS (path vertices)
     uint32_t opt_mega_occ = 0;              // DXRPT_OPT_MEGAKERNEL_OCCUPANCY (0 = by frame size)
     uint32_t opt_bake_chunk = 1u << 21;     // DXRPT_OPT_BAKE_CHUNK (texels per bake launch)
+    uint32_t opt_mega_persistent = 0;       // DXRPT_OPT_MEGAKERNEL_PERSISTENT (waves per CU, 0 = off)
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
     int built_width = 0;
     DevBuf d_trav;   // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
@@ -259,7 +260,7 @@ void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
     c->f_shorg.ensure(qsize * sl * 16);
     c->f_shdir.ensure(qsize * sl * 16);
     c->f_shcon.ensure(qsize * sl * 16);
-    c->f_counters.ensure(2 * kMaxDepthQueues * kQueueShards * sizeof(uint32_t));
+    c->f_counters.ensure((2 * kMaxDepthQueues * kQueueShards + 16) * sizeof(uint32_t));  // + the k_path work counter
     f.ps_pix = c->f_pix.as<uint2>();
     f.px_rad = c->f_pxrad.as<float4>();
     f.hit = c->f_hit.as<float4>();
@@ -462,8 +463,11 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_MEGAKERNEL_PATHS) {
             ctx->opt_mega_paths = value > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(value);
         } else if (option == DXRPT_OPT_MEGAKERNEL_OCCUPANCY) {
-            require(value == 0 || (value >= 3 && value <= 6), "dxrpt_set_option: megakernel occupancy must be 0 or 3..6");
+            require(value == 0 || (value >= 3 && value <= 8), "dxrpt_set_option: megakernel occupancy must be 0 or 3..8");
             ctx->opt_mega_occ = uint32_t(value);
+        } else if (option == DXRPT_OPT_MEGAKERNEL_PERSISTENT) {
+            require(value <= 64, "dxrpt_set_option: persistent megakernel waves per CU must be 0..64");
+            ctx->opt_mega_persistent = uint32_t(value);
         } else if (option == DXRPT_OPT_BAKE_CHUNK) {
             require(value >= 64 && value <= (1u << 26), "dxrpt_set_option: bake chunk must be 64..2^26 texels");
             ctx->opt_bake_chunk = uint32_t(value);
@@ -747,7 +751,9 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // more resident waves hide more latency once a frame has waves for several rounds; a GPU's 1/8
         // share (~4k waves) fits in one round at 4 waves/SIMD without spills
         fp.megakernel_occupancy = ctx->opt_mega_occ ? ctx->opt_mega_occ
-                                                    : (paths > 1500000u ? 6u : (paths > 300000u ? 5u : 4u));
+                                                    : (paths > 1500000u ? 7u : (paths > 300000u ? 5u : 4u));
+        fp.mega_persistent = ctx->opt_mega_persistent;
+        fp.num_cus = ctx->num_cus;
         hipStream_t s = static_cast<hipStream_t>(stream);
         if (ctx->opt_count) {
             fp.trav = ctx->d_trav.as<unsigned long long>();
@@ -910,7 +916,7 @@ int dxrpt_bake_lightmap(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, co
         fp.lights = nl ? ctx->d_lights.as<dxrpt_spot_light>() : nullptr;
         fp.num_paths = chunk;
         // register budget as for the megakernel frames (same per-thread path loop)
-        fp.megakernel_occupancy = ctx->opt_mega_occ ? ctx->opt_mega_occ : (chunk > 1500000u ? 6u : (chunk > 300000u ? 5u : 4u));
+        fp.megakernel_occupancy = ctx->opt_mega_occ ? ctx->opt_mega_occ : (chunk > 1500000u ? 7u : (chunk > 300000u ? 5u : 4u));
         fp.width = width;
         fp.height = height;
         const SceneDev sd = scene_dev(ctx, frame_traversal_threads(chunk, ctx->fb.shadow_slots, 0));

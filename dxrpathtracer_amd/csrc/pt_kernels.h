@@ -136,6 +136,9 @@ struct FrameParams {
     uint32_t packet_switch;          // packet traversal: fall back to one ray per lane below this coherence (%)
     uint32_t megakernel;             // 1: the whole frame runs in k_path (one thread per path, no passes)
     uint32_t megakernel_occupancy;   // k_path register budget: 0 compiler default, 6 waves per SIMD
+    uint32_t mega_persistent;        // >0: k_path as a persistent grid of this many waves per CU, each wave
+                                     // fetching 64-path chunks from a counter after fb.counters' shards
+    uint32_t num_cus;
 };
 
 // Kernel sequence of one frame: raygen, then (trace, shade, shadow, resolve) per depth 1..L-1, then

@@ -1581,16 +1581,34 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
     return rad;
 }
 
-template <int kOcc>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
-void k_path(KArgs A) {
-    extern __shared__ int stack[];
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= A.P.num_paths) return;
-    lds_int* stk = lane_stack(A.S, stack);
+PT_DEV void camera_path(const KArgs& A, uint32_t p, lds_int* stk) {
     const PrimaryRay pr = primary_ray(A, p);
     const float4 rad = trace_path<false>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk);
     accumulate_pixel(A, pr.accumIdx, rad);
+}
+
+// kPersistent: a grid sized to the resident waves; each wave takes the next 64 paths (one 8x8 pixel
+// block) from a frame counter until the frame is done, so no wave idles while a long one finishes.
+template <int kOcc, bool kPersistent>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
+void k_path(KArgs A) {
+    extern __shared__ int stack[];
+    lds_int* stk = lane_stack(A.S, stack);
+    if (!kPersistent) {
+        const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+        if (p >= A.P.num_paths) return;
+        camera_path(A, p, stk);
+        return;
+    }
+    uint32_t* work = A.F.counters + 2 * kMaxDepthQueues * kQueueShards;
+    const uint32_t lane = threadIdx.x & 63u;
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(work, 64u);
+        base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
+        if (base >= A.P.num_paths) break;  // uniform: every wave reaches it once the counter passes the frame
+        if (base + lane < A.P.num_paths) camera_path(A, base + lane, stk);
+    }
 }
 
 // ---- lightmap baking (Baking.hlsl:336-465, BakeRayGen) -------------------------------------------
@@ -1724,17 +1742,25 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
         if (ev && (slot == last_slot || timed(slot))) (void)hipEventRecord(ev[2 * slot + 1], st);
     };
     auto slot_of = [](int d, int kind) { return 1 + 4 * (d - 1) + kind; };  // kind 0 trace 1 shade 2 shadow 3 resolve
-    hipError_t e = hipMemsetAsync(fb.counters, 0, 2 * kMaxDepthQueues * kQueueShards * sizeof(uint32_t), stream);
+    hipError_t e = hipMemsetAsync(fb.counters, 0, (2 * kMaxDepthQueues * kQueueShards + 1) * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     if (fp.megakernel) {  // whole frame in k_path (timing: ev[0], ev[1] bracket the k_path launch)
         const uint32_t tb = fp.trace_block;
         const size_t ldsm = size_t(scene.stack_ints) * tb * sizeof(int);
         const uint32_t gm = (fp.num_paths + tb - 1u) / tb;
         if (ev) (void)hipEventRecord(ev[0], stream);
-        if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_path<6>), dim3(gm), dim3(tb), ldsm, stream, A);
-        else if (fp.megakernel_occupancy == 4) hipLaunchKernelGGL((k_path<4>), dim3(gm), dim3(tb), ldsm, stream, A);
-        else if (fp.megakernel_occupancy == 5) hipLaunchKernelGGL((k_path<5>), dim3(gm), dim3(tb), ldsm, stream, A);
-        else hipLaunchKernelGGL((k_path<0>), dim3(gm), dim3(tb), ldsm, stream, A);  // 3: the compiler's budget
+        if (fp.mega_persistent && tb == 64u) {
+            const uint32_t gp = std::min(gm, fp.mega_persistent * fp.num_cus);
+            if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_path<6, true>), dim3(gp), dim3(tb), ldsm, stream, A);
+            else if (fp.megakernel_occupancy == 4) hipLaunchKernelGGL((k_path<4, true>), dim3(gp), dim3(tb), ldsm, stream, A);
+            else hipLaunchKernelGGL((k_path<5, true>), dim3(gp), dim3(tb), ldsm, stream, A);
+        }
+        else if (fp.megakernel_occupancy == 8) hipLaunchKernelGGL((k_path<8, false>), dim3(gm), dim3(tb), ldsm, stream, A);
+        else if (fp.megakernel_occupancy == 7) hipLaunchKernelGGL((k_path<7, false>), dim3(gm), dim3(tb), ldsm, stream, A);
+        else if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_path<6, false>), dim3(gm), dim3(tb), ldsm, stream, A);
+        else if (fp.megakernel_occupancy == 4) hipLaunchKernelGGL((k_path<4, false>), dim3(gm), dim3(tb), ldsm, stream, A);
+        else if (fp.megakernel_occupancy == 5) hipLaunchKernelGGL((k_path<5, false>), dim3(gm), dim3(tb), ldsm, stream, A);
+        else hipLaunchKernelGGL((k_path<0, false>), dim3(gm), dim3(tb), ldsm, stream, A);  // 3: the compiler's budget
         if (ev) (void)hipEventRecord(ev[1], stream);
         return hipGetLastError();
     }
@@ -1885,7 +1911,8 @@ hipError_t launch_bake(const SceneDev& scene, const FrameBuffers& fb, const Fram
     const uint32_t tb = 64;
     const size_t lds = size_t(scene.stack_ints) * tb * sizeof(int);
     const dim3 g((b.span + tb - 1u) / tb);
-    if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_bake<6>), g, dim3(tb), lds, stream, A, b);
+    if (fp.megakernel_occupancy >= 7) hipLaunchKernelGGL((k_bake<7>), g, dim3(tb), lds, stream, A, b);
+    else if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_bake<6>), g, dim3(tb), lds, stream, A, b);
     else if (fp.megakernel_occupancy == 5) hipLaunchKernelGGL((k_bake<5>), g, dim3(tb), lds, stream, A, b);
     else hipLaunchKernelGGL((k_bake<4>), g, dim3(tb), lds, stream, A, b);
     return hipGetLastError();

@@ -313,8 +313,11 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                             compaction wins for long paths on big frames).  0 = always the
                                             wavefront.  Identical results. */
 #define DXRPT_OPT_MEGAKERNEL_OCCUPANCY 24u /* megakernel register budget in waves/SIMD: 0 = by frame size
-                                              (default: 6 above 1,500,000 paths, 5 above 300,000, else 4),
-                                              4 (no spills), 5, 6, or 3 = the compiler's */
+                                              (default: 7 above 1,500,000 paths, 5 above 300,000, else 4),
+                                              4 (no spills), 5, 6, 7, 8, or 3 = the compiler's */
+#define DXRPT_OPT_MEGAKERNEL_PERSISTENT 26u /* > 0: the megakernel as a persistent grid of this many
+                                               waves per CU pulling 64-path chunks (0 = one wave per
+                                               64 paths, default).  Identical results. */
 #define DXRPT_OPT_BAKE_CHUNK 25u /* texels per dxrpt_bake_lightmap launch (default 2^21; bounds the
                                     per-texel shadow-slot buffers).  Identical results. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);

@@ -327,10 +327,12 @@ def _boxtest_lights(sc, sky, st, W, H, sample):
     return rtc, lights
 
 
-@pytest.mark.parametrize("name,L,any_hit,occ,packet", [("sponza", 3, 1, 4, 3), ("sponza", 8, 1, 6, 0),
-                                                       ("suntemple", 4, 3, 3, 1), ("boxtest", 5, 1, 5, 2),
-                                                       ("whitefurnace", 3, 1, 6, 3), ("suntemple", 3, 1, 5, 3)])
-def test_megakernel_is_bit_identical(torch_cuda, name, L, any_hit, occ, packet):
+@pytest.mark.parametrize("name,L,any_hit,occ,packet,persist", [
+    ("sponza", 3, 1, 4, 3, 0), ("sponza", 8, 1, 6, 0, 0), ("suntemple", 4, 3, 3, 1, 0), ("boxtest", 5, 1, 5, 2, 0),
+    ("whitefurnace", 3, 1, 6, 3, 0), ("suntemple", 3, 1, 5, 3, 0), ("sponza", 4, 1, 7, 3, 0), ("boxtest", 3, 1, 8, 1, 0),
+    # persistent grid (DXRPT_OPT_MEGAKERNEL_PERSISTENT): few waves per CU so every wave loops
+    ("sponza", 3, 1, 6, 3, 1), ("boxtest", 5, 1, 5, 3, 2), ("suntemple", 3, 1, 4, 3, 24)])
+def test_megakernel_is_bit_identical(torch_cuda, name, L, any_hit, occ, packet, persist):
     # DXRPT_OPT_MEGAKERNEL_PATHS: the whole frame as one kernel (one thread per path) must equal the
     # wavefront frame bit for bit -- same shading code, same per-path summation order -- and count the
     # same rays per depth; on full frames, on band tiles (a GPU's share) and with 3 spot lights
@@ -353,6 +355,7 @@ def test_megakernel_is_bit_identical(torch_cuda, name, L, any_hit, occ, packet):
             t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30)
             t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, occ)
             t.set_option(A.OPT_PACKET_TRAVERSAL, packet)
+            t.set_option(A.OPT_MEGAKERNEL_PERSISTENT, persist)
             got = gpu_render(torch, name, W, H, st, 2, tiles=tiles, n_out=n, accum=acc0.clone(), rtc=rtc,
                              lights=lights).cpu().numpy()
             s_got = t.stats()
@@ -361,6 +364,7 @@ def test_megakernel_is_bit_identical(torch_cuda, name, L, any_hit, occ, packet):
             assert list(s_got.shadow_rays_per_depth) == list(s_ref.shadow_rays_per_depth)
     finally:
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
+        t.set_option(A.OPT_MEGAKERNEL_PERSISTENT, 0)
         t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, A.DEFAULT_MEGAKERNEL_OCCUPANCY)
         t.set_option(A.OPT_PACKET_TRAVERSAL, A.DEFAULT_PACKET_TRAVERSAL)
 
