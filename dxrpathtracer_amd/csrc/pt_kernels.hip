@@ -1510,8 +1510,10 @@ PT_DEV void count_rays(uint32_t* counters, uint32_t n) {
 // is the CMJ pattern index; `packet` bit 0 / bit 1: wave-coherent traversal for the depth-1 closest hit
 // / the depth-1 sun shadow rays (all lanes must be active at depth 1 then).  Returns the radiance.
 // kBake: the first ray is BakeRayGen's (TMin 0.0001, IsDiffuse, no packets) instead of RaygenShader's.
+// nc: the workgroup's LDS copy of the top BVH8 nodes for the per-lane traversals (n = 0: none).
 template <bool kBake>
-PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, f3 dir, float tmax, lds_int* stk) {
+PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, f3 dir, float tmax, lds_int* stk,
+                         const NodeCache& nc = NodeCache{nullptr, 0u}) {
     const dxrpt_app_settings& set = A.P.set;
     const float tmin1 = kBake ? 0.0001f : 0.0f;
     const bool isDiffuse1 = kBake;
@@ -1528,7 +1530,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
         if (d == 1 && (packet & 1u))  // coherent primary rays: wave-coherent traversal (same results)
             traverse8_packet<false>(A.S, org, dir, tmin1, tmax, d <= set.MaxAnyHitPathLength, true, h);
         else
-            traverse<8, false, false>(A.S, org, dir, d == 1 ? tmin1 : kRayTMin, tmax, d <= set.MaxAnyHitPathLength, stk, h, nv, nt);
+            traverse<8, false, false>(A.S, org, dir, d == 1 ? tmin1 : kRayTMin, tmax, d <= set.MaxAnyHitPathLength, stk, h, nv, nt, nc);
         VertexIn V;
         V.inOrigin = org;
         V.inDir = dir;
@@ -1563,7 +1565,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
             if (d == 1 && k == 0 && (packet & 2u))
                 occluded = traverse8_packet<true>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live, hs);
             else if (live)
-                occluded = traverse<8, true, false>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stk, hs, nv, nt);
+                occluded = traverse<8, true, false>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stk, hs, nv, nt, nc);
             if (live) {
                 rad.x += occluded ? c4.x * 0.0f : c4.x;
                 rad.y += occluded ? c4.y * 0.0f : c4.y;
@@ -1581,21 +1583,29 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
     return rad;
 }
 
-PT_DEV void camera_path(const KArgs& A, uint32_t p, lds_int* stk) {
+PT_DEV void camera_path(const KArgs& A, uint32_t p, lds_int* stk, const NodeCache& nc = NodeCache{nullptr, 0u}) {
     const PrimaryRay pr = primary_ray(A, p);
-    const float4 rad = trace_path<false>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk);
+    const float4 rad = trace_path<false>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, nc);
     accumulate_pixel(A, pr.accumIdx, rad);
 }
 
 // kPersistent: a grid sized to the resident waves; each wave takes the next 64 paths (one 8x8 pixel
 // block) from a frame counter until the frame is done, so no wave idles while a long one finishes.
-template <int kOcc, bool kPersistent>
+// kLds: the workgroup first copies the top A.P.lds_nodes BVH8 nodes (breadth-first, so the levels
+// every ray visits) behind the stacks; the per-lane traversals read those from LDS.
+template <int kOcc, bool kPersistent, bool kLds = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
 void k_path(KArgs A) {
     extern __shared__ int stack[];
     lds_int* stk = lane_stack(A.S, stack);
     if (!kPersistent) {
         const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+        if (kLds) {
+            const NodeCache nc = node_cache_fill(A.S, reinterpret_cast<uint4*>(stack + A.S.stack_ints * blockDim.x),
+                                                 A.P.lds_nodes);
+            if (p < A.P.num_paths) camera_path(A, p, stk, nc);
+            return;
+        }
         if (p >= A.P.num_paths) return;
         camera_path(A, p, stk);
         return;
@@ -1754,6 +1764,13 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
             if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_path<6, true>), dim3(gp), dim3(tb), ldsm, stream, A);
             else if (fp.megakernel_occupancy == 4) hipLaunchKernelGGL((k_path<4, true>), dim3(gp), dim3(tb), ldsm, stream, A);
             else hipLaunchKernelGGL((k_path<5, true>), dim3(gp), dim3(tb), ldsm, stream, A);
+        }
+        else if (A.P.lds_nodes) {
+            const size_t ldsn = ldsm + size_t(A.P.lds_nodes) * 80u;
+            if (fp.megakernel_occupancy >= 7) hipLaunchKernelGGL((k_path<7, false, true>), dim3(gm), dim3(tb), ldsn, stream, A);
+            else if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_path<6, false, true>), dim3(gm), dim3(tb), ldsn, stream, A);
+            else if (fp.megakernel_occupancy == 5) hipLaunchKernelGGL((k_path<5, false, true>), dim3(gm), dim3(tb), ldsn, stream, A);
+            else hipLaunchKernelGGL((k_path<4, false, true>), dim3(gm), dim3(tb), ldsn, stream, A);
         }
         else if (fp.megakernel_occupancy == 8) hipLaunchKernelGGL((k_path<8, false>), dim3(gm), dim3(tb), ldsm, stream, A);
         else if (fp.megakernel_occupancy == 7) hipLaunchKernelGGL((k_path<7, false>), dim3(gm), dim3(tb), ldsm, stream, A);

@@ -517,3 +517,24 @@ def test_errors_are_reported_not_raised(torch_cuda):
                      tiles=[A.Tile(60, 0, 8, 8, 0, 8, 0)])
     torch.cuda.synchronize()
     assert float(buf.abs().sum()) == 0.0  # nothing was launched
+
+
+@pytest.mark.parametrize("name,block,nodes", [("sponza", 64, 9), ("sponza", 256, 73), ("suntemple", 128, 200)])
+def test_megakernel_lds_node_cache_is_bit_identical(torch_cuda, name, block, nodes):
+    # DXRPT_OPT_LDS_NODES in the megakernel: the top BVH8 nodes read from the workgroup's LDS copy
+    torch = torch_cuda
+    sc, sky = scene_bundle(name)
+    st = sc.settings(MaxPathLength=4)
+    W, H = 320, 180
+    t = tracer(name)
+    try:
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30)
+        ref = gpu_render(torch, name, W, H, st, 1).cpu().numpy()
+        t.set_option(A.OPT_TRACE_BLOCK, block)
+        t.set_option(A.OPT_LDS_NODES, nodes)
+        got = gpu_render(torch, name, W, H, st, 1).cpu().numpy()
+        np.testing.assert_array_equal(got, ref)
+    finally:
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
+        t.set_option(A.OPT_TRACE_BLOCK, 64)
+        t.set_option(A.OPT_LDS_NODES, A.DEFAULT_LDS_NODES)
