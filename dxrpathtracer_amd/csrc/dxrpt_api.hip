@@ -116,6 +116,7 @@ struct dxrpt_ctx {
     uint32_t opt_mega_occ = 0;              // DXRPT_OPT_MEGAKERNEL_OCCUPANCY (0 = by frame size)
     uint32_t opt_bake_chunk = 1u << 21;     // DXRPT_OPT_BAKE_CHUNK (texels per bake launch)
     uint32_t opt_mega_persistent = 0;       // DXRPT_OPT_MEGAKERNEL_PERSISTENT (waves per CU, 0 = off)
+    uint32_t opt_mega_lanes = 64;           // DXRPT_OPT_MEGAKERNEL_LANES (paths per megakernel wave)
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
     int built_width = 0;
     DevBuf d_trav;   // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
@@ -468,6 +469,9 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_MEGAKERNEL_PERSISTENT) {
             require(value <= 64, "dxrpt_set_option: persistent megakernel waves per CU must be 0..64");
             ctx->opt_mega_persistent = uint32_t(value);
+        } else if (option == DXRPT_OPT_MEGAKERNEL_LANES) {
+            require(value == 16 || value == 32 || value == 64, "dxrpt_set_option: megakernel lanes must be 16, 32 or 64");
+            ctx->opt_mega_lanes = uint32_t(value);
         } else if (option == DXRPT_OPT_BAKE_CHUNK) {
             require(value >= 64 && value <= (1u << 26), "dxrpt_set_option: bake chunk must be 64..2^26 texels");
             ctx->opt_bake_chunk = uint32_t(value);
@@ -753,6 +757,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.megakernel_occupancy = ctx->opt_mega_occ ? ctx->opt_mega_occ
                                                     : (paths > 1500000u ? 7u : (paths > 300000u ? 5u : 4u));
         fp.mega_persistent = ctx->opt_mega_persistent;
+        fp.mega_lanes = ctx->opt_mega_lanes;
         fp.num_cus = ctx->num_cus;
         hipStream_t s = static_cast<hipStream_t>(stream);
         if (ctx->opt_count) {

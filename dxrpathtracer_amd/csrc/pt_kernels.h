@@ -138,6 +138,8 @@ struct FrameParams {
     uint32_t megakernel_occupancy;   // k_path register budget: 0 compiler default, 6 waves per SIMD
     uint32_t mega_persistent;        // >0: k_path as a persistent grid of this many waves per CU, each wave
                                      // fetching 64-path chunks from a counter after fb.counters' shards
+    uint32_t mega_lanes;             // k_path: paths per 64-lane wave (64, 32, 16); lanes >= mega_lanes
+                                     // re-trace lane (l mod mega_lanes)'s path and write nothing
     uint32_t num_cus;
 };
 

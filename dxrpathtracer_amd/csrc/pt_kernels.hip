@@ -1511,20 +1511,24 @@ PT_DEV void count_rays(uint32_t* counters, uint32_t n) {
 // / the depth-1 sun shadow rays (all lanes must be active at depth 1 then).  Returns the radiance.
 // kBake: the first ray is BakeRayGen's (TMin 0.0001, IsDiffuse, no packets) instead of RaygenShader's.
 // nc: the workgroup's LDS copy of the top BVH8 nodes for the per-lane traversals (n = 0: none).
+// quiet: a twin lane (DXRPT_OPT_MEGAKERNEL_LANES) -- same path as its partner lane, so it writes the
+// same shadow slots with the same values, and adds nothing to the ray counters.
 template <bool kBake>
 PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, f3 dir, float tmax, lds_int* stk,
-                         const NodeCache& nc = NodeCache{nullptr, 0u}) {
+                         const NodeCache& nc = NodeCache{nullptr, 0u}, bool quiet = false) {
     const dxrpt_app_settings& set = A.P.set;
     const float tmin1 = kBake ? 0.0001f : 0.0f;
     const bool isDiffuse1 = kBake;
-    const uint32_t packet = kBake ? 0u : A.P.packet;
+    // packets need every lane of the wave (the packet stack lives one entry per lane): a frame's last,
+    // partial wave traverses one ray per lane instead (same results)
+    const uint32_t packet = (kBake || __ballot(1) != ~0ull) ? 0u : A.P.packet;
     f3 thr = f3{1.0f, 1.0f, 1.0f};
     float payloadRoughness = 0.0f;
     bool payloadIsDiffuse = isDiffuse1;
     float4 rad = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const int L = set.MaxPathLength < 2 ? 2 : set.MaxPathLength;
     for (int d = 1; d <= L - 1; ++d) {
-        count_rays(A.F.counters + uint32_t(d) * kQueueShards, 1u);
+        count_rays(A.F.counters + uint32_t(d) * kQueueShards, quiet ? 0u : 1u);
         HitRec h;
         uint32_t nv = 0, nt = 0;
         if (d == 1 && (packet & 1u))  // coherent primary rays: wave-coherent traversal (same results)
@@ -1544,7 +1548,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
         path_vertex(A, d, V, [&](f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
             emit_shadow(A, slot_p, nsh, o, dd, tmn, tmx, c, fo);
         }, O);
-        count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, nsh);
+        count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, quiet ? 0u : nsh);
         rad.x += thr.x * O.local.x;
         rad.y += thr.y * O.local.y;
         rad.z += thr.z * O.local.z;
@@ -1583,10 +1587,159 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
     return rad;
 }
 
-PT_DEV void camera_path(const KArgs& A, uint32_t p, lds_int* stk, const NodeCache& nc = NodeCache{nullptr, 0u}) {
+// Per-lane BVH8 traversal whose kind is a lane value (closest hit, or any hit when `any`): the
+// path-group schedule below runs a continuation ray and shadow rays in one loop.  Same node order and
+// triangle tests as traverse<8, any, false>, so the same hit / visibility.
+PT_DEV bool traverse8_rt(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, bool any, lds_int* stk,
+                         HitRec& h) {
+    h.t = tmax;
+    h.tri = kMiss;
+    h.b1 = h.b2 = 0.0f;
+    h.geom = 0;
+    Ray8 R;
+    ray8_init(R, o, d, tmin, tmax, alpha, h);
+    uint32_t node = 0, nv = 0;
+    int sp = 0;
+    uint2 tos = make_uint2(0u, 0u);
+    while (true) {
+        uint32_t tbase = 0, tbits = 0;
+        const bool more = trav8_node<false>(S, R, node, sp, stk, tos, h, tbase, tbits, nv);
+        bool done = false;
+        while (tbits) {
+            const uint32_t b = uint32_t(__builtin_ctz(tbits));
+            tbits &= tbits - 1u;
+            const TriRec r = load_tri(S, tbase + b);
+            if (any ? test_tri_rec<true>(S, r, R.o, R.d, R.tmin, R.tmax, R.alpha, h)
+                    : test_tri_rec<false>(S, r, R.o, R.d, R.tmin, R.tmax, R.alpha, h)) {
+                done = true;
+                break;
+            }
+        }
+        if (done || !more) break;
+    }
+    return h.tri != kMiss;
+}
+
+// Path-group schedule (DXRPT_OPT_MEGAKERNEL_LANES g < 64): each path is carried by 64/g lanes of its
+// wave (lanes l, l+g, ...) that all run its shading (identical values, so identical control flow);
+// after a vertex, its continuation ray and its shadow rays are independent traversals, handed out to
+// the group's lanes round by round (item 0 = continuation, then the shadow slots), so a path's chain of
+// dependent traversals shortens (L=3 with the sun: R1 | R2+S1 | S2+V2 = 3 rounds instead of 5).  The
+// results are gathered back over the group with lane shuffles and summed in the reference's slot
+// order, so the frame equals trace_path's bit for bit.  Only member 0 counts rays (and, in
+// camera_path, writes the pixel).
+PT_DEV float4 trace_path_group(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, f3 dir, float tmax, lds_int* stk,
+                               uint32_t g) {
+    const dxrpt_app_settings& set = A.P.set;
+    const uint32_t lane = uint32_t(__lane_id());
+    const uint32_t member = lane / g, gsize = 64u / g, leader = lane & (g - 1u);
+    const bool quiet = member != 0u;
+    const uint32_t packet = __ballot(1) != ~0ull ? 0u : (A.P.packet & 1u);
+    f3 thr = f3{1.0f, 1.0f, 1.0f};
+    float payloadRoughness = 0.0f;
+    bool payloadIsDiffuse = false;
+    float4 rad = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const int L = set.MaxPathLength < 2 ? 2 : set.MaxPathLength;
+    HitRec h;
+    uint32_t nv = 0, nt = 0;
+    for (int d = 1; d <= L - 1; ++d) {
+        count_rays(A.F.counters + uint32_t(d) * kQueueShards, quiet ? 0u : 1u);
+        if (d == 1) {  // the primary ray: every member traces it (packets while the wave is full)
+            if (packet)
+                traverse8_packet<false>(A.S, org, dir, 0.0f, tmax, d <= set.MaxAnyHitPathLength, true, h);
+            else
+                traverse<8, false, false>(A.S, org, dir, 0.0f, tmax, d <= set.MaxAnyHitPathLength, stk, h, nv, nt);
+        }
+        VertexIn V;
+        V.inOrigin = org;
+        V.inDir = dir;
+        V.pathThr = thr;
+        V.payloadRoughness = payloadRoughness;
+        V.payloadIsDiffuse = payloadIsDiffuse;
+        V.pix = pix;
+        V.hit = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
+        VertexOut O;
+        uint32_t nsh = 0;
+        path_vertex(A, d, V, [&](f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
+            emit_shadow(A, slot_p, nsh, o, dd, tmn, tmx, c, fo);
+        }, O);
+        count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, quiet ? 0u : nsh);
+        rad.x += thr.x * O.local.x;
+        rad.y += thr.y * O.local.y;
+        rad.z += thr.z * O.local.z;
+        const uint32_t first = O.cont ? 1u : 0u, items = first + nsh;
+        uint32_t occ_lo = 0, occ_hi = 0;  // occlusion bit per shadow slot (<= 2 + 32 lights)
+        HitRec hn;
+        hn.t = 0.0f;
+        hn.b1 = hn.b2 = 0.0f;
+        hn.tri = kMiss;
+        hn.geom = 0;
+        for (uint32_t r = 0; __ballot(r * gsize < items) != 0ull; ++r) {
+            const uint32_t item = r * gsize + member;
+            if (item < items) {
+                f3 o, dd;
+                float tmn, tmx;
+                bool alpha, any;
+                if (item < first) {  // the continuation ray (PathLength d + 1)
+                    o = O.nextOrigin;
+                    dd = O.nextDir;
+                    tmn = kRayTMin;
+                    tmx = kFP32Max;
+                    alpha = d + 1 <= set.MaxAnyHitPathLength;
+                    any = false;
+                } else {
+                    const size_t slot = size_t(item - first) * A.F.qsize + slot_p;
+                    const float4 o4 = A.F.sh_org[slot], d4 = A.F.sh_dir[slot];
+                    o = ld3(o4);
+                    dd = ld3(d4);
+                    tmn = d4.w;
+                    tmx = o4.w;
+                    alpha = fbits(A.F.sh_con[slot].w) == 0u;
+                    any = true;
+                }
+                HitRec ht;
+                const bool hit = traverse8_rt(A.S, o, dd, tmn, tmx, alpha, any, stk, ht);
+                if (item < first) {
+                    hn = ht;
+                } else if (hit) {
+                    const uint32_t k = item - first;
+                    if (k < 32u) occ_lo |= 1u << k; else occ_hi |= 1u << (k - 32u);
+                }
+            }
+        }
+        // gather over the group: occlusion bits (OR over members), the continuation hit (member 0)
+        for (uint32_t off = g; off < 64u; off <<= 1) {
+            occ_lo |= uint32_t(__shfl_xor(int(occ_lo), int(off)));
+            occ_hi |= uint32_t(__shfl_xor(int(occ_hi), int(off)));
+        }
+        h.b1 = __shfl(hn.b1, int(leader));
+        h.b2 = __shfl(hn.b2, int(leader));
+        h.tri = uint32_t(__shfl(int(hn.tri), int(leader)));
+        h.geom = uint32_t(__shfl(int(hn.geom), int(leader)));
+        for (uint32_t k = 0; k < nsh; ++k) {  // ShadowHit/Miss: contribution * visibility, in slot order
+            const float4 c4 = A.F.sh_con[size_t(k) * A.F.qsize + slot_p];
+            const bool occluded = ((k < 32u ? occ_lo >> k : occ_hi >> (k - 32u)) & 1u) != 0u;
+            rad.x += occluded ? c4.x * 0.0f : c4.x;
+            rad.y += occluded ? c4.y * 0.0f : c4.y;
+            rad.z += occluded ? c4.z * 0.0f : c4.z;
+        }
+        if (!O.cont) break;
+        org = O.nextOrigin;
+        dir = O.nextDir;
+        thr = O.nextThr;
+        payloadRoughness = O.nextRoughness;
+        payloadIsDiffuse = O.nextIsDiffuse;
+    }
+    (void)gsize;
+    return rad;
+}
+
+PT_DEV void camera_path(const KArgs& A, uint32_t p, lds_int* stk, const NodeCache& nc = NodeCache{nullptr, 0u},
+                        bool twin = false) {
     const PrimaryRay pr = primary_ray(A, p);
-    const float4 rad = trace_path<false>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, nc);
-    accumulate_pixel(A, pr.accumIdx, rad);
+    const float4 rad = A.P.mega_lanes < 64u ? trace_path_group(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, A.P.mega_lanes)
+                                            : trace_path<false>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, nc);
+    if (!twin) accumulate_pixel(A, pr.accumIdx, rad);
 }
 
 // kPersistent: a grid sized to the resident waves; each wave takes the next 64 paths (one 8x8 pixel
@@ -1604,6 +1757,13 @@ void k_path(KArgs A) {
             const NodeCache nc = node_cache_fill(A.S, reinterpret_cast<uint4*>(stack + A.S.stack_ints * blockDim.x),
                                                  A.P.lds_nodes);
             if (p < A.P.num_paths) camera_path(A, p, stk, nc);
+            return;
+        }
+        if (A.P.mega_lanes < 64u) {  // wave-uniform: mega_lanes paths per wave, each traced by 64/mega_lanes lanes
+            const uint32_t lane = threadIdx.x & 63u;
+            const uint32_t q = (p >> 6) * A.P.mega_lanes + (lane & (A.P.mega_lanes - 1u));
+            if (q >= A.P.num_paths) return;
+            camera_path(A, q, stk, NodeCache{nullptr, 0u}, lane >= A.P.mega_lanes);
             return;
         }
         if (p >= A.P.num_paths) return;
@@ -1757,7 +1917,10 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
     if (fp.megakernel) {  // whole frame in k_path (timing: ev[0], ev[1] bracket the k_path launch)
         const uint32_t tb = fp.trace_block;
         const size_t ldsm = size_t(scene.stack_ints) * tb * sizeof(int);
-        const uint32_t gm = (fp.num_paths + tb - 1u) / tb;
+        // mega_lanes < 64 (per-lane path, no persistent grid / LDS nodes): 64 threads per mega_lanes paths
+        const bool twins = fp.mega_lanes < 64u && !fp.mega_persistent && !A.P.lds_nodes;
+        const uint64_t threads = twins ? (uint64_t(fp.num_paths) + fp.mega_lanes - 1u) / fp.mega_lanes * 64u : fp.num_paths;
+        const uint32_t gm = uint32_t((threads + tb - 1u) / tb);
         if (ev) (void)hipEventRecord(ev[0], stream);
         if (fp.mega_persistent && tb == 64u) {
             const uint32_t gp = std::min(gm, fp.mega_persistent * fp.num_cus);

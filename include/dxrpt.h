@@ -318,6 +318,10 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 #define DXRPT_OPT_MEGAKERNEL_PERSISTENT 26u /* > 0: the megakernel as a persistent grid of this many
                                                waves per CU pulling 64-path chunks (0 = one wave per
                                                64 paths, default).  Identical results. */
+#define DXRPT_OPT_MEGAKERNEL_LANES 27u /* paths per 64-lane megakernel wave: 64 (default), 32 or 16; each path
+                                          is then carried by 64/value lanes that shade it together and
+                                          trace its continuation and shadow rays concurrently (shorter
+                                          dependent-traversal chains on small frames).  Identical results. */
 #define DXRPT_OPT_BAKE_CHUNK 25u /* texels per dxrpt_bake_lightmap launch (default 2^21; bounds the
                                     per-texel shadow-slot buffers).  Identical results. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);

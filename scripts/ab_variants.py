@@ -18,9 +18,9 @@ sys.path.insert(0, REPO)
 
 KEYS = {"w": "width", "m": "mode", "r": "refill", "k": "chunks", "p": "postpone", "b": "block", "o": "occ",
         "s": "sblock", "q": "socc", "x": "spatial", "c": "leafcost", "h": "hocc", "g": "sgrid",
-        "j": "conc", "t": "pipe", "a": "packet", "n": "ldsnodes", "z": "xcd", "u": "pswitch", "e": "mega", "v": "megaocc", "y": "persist"}
+        "j": "conc", "t": "pipe", "a": "packet", "n": "ldsnodes", "z": "xcd", "u": "pswitch", "e": "mega", "v": "megaocc", "y": "persist", "l": "lanes"}
 DEFAULTS = {"width": 8, "mode": 0, "refill": 16, "chunks": 4, "postpone": 0, "block": 64, "occ": 7, "sblock": 256,
-            "socc": 0, "spatial": 150, "leafcost": 150, "hocc": 8, "sgrid": 0, "conc": 1, "pipe": 0, "packet": 3, "ldsnodes": 0, "xcd": 0, "pswitch": 0, "mega": 1, "megaocc": 0, "persist": 0}
+            "socc": 0, "spatial": 150, "leafcost": 150, "hocc": 8, "sgrid": 0, "conc": 1, "pipe": 0, "packet": 3, "ldsnodes": 0, "xcd": 0, "pswitch": 0, "mega": 1, "megaocc": 0, "persist": 0, "lanes": 64}
 BUILD_KEYS = ("width", "spatial", "leafcost")  # a separate context (BVH) per combination
 
 
@@ -100,6 +100,7 @@ def main():
             t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30 if o["mega"] else 0)
             t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, o["megaocc"])
             t.set_option(A.OPT_MEGAKERNEL_PERSISTENT, o["persist"])
+            t.set_option(A.OPT_MEGAKERNEL_LANES, o["lanes"])
             t.set_option(A.OPT_SHADE_BLOCK, o["sblock"])
             t.set_option(A.OPT_SHADE_OCCUPANCY, o["socc"])
             for f in range(3):

@@ -538,3 +538,40 @@ def test_megakernel_lds_node_cache_is_bit_identical(torch_cuda, name, block, nod
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
         t.set_option(A.OPT_TRACE_BLOCK, 64)
         t.set_option(A.OPT_LDS_NODES, A.DEFAULT_LDS_NODES)
+
+
+@pytest.mark.parametrize("name,L,lanes,W,H", [
+    ("sponza", 3, 32, 352, 200), ("sponza", 4, 16, 352, 200), ("suntemple", 3, 32, 320, 180),
+    # frames whose last wave is partial (5000 = 78 x 64 + 8 paths): packets off in that wave
+    ("sponza", 3, 64, 100, 50), ("suntemple", 3, 32, 100, 50), ("boxtest", 5, 16, 100, 50)])
+def test_megakernel_lanes_and_partial_waves_are_bit_identical(torch_cuda, name, L, lanes, W, H):
+    # DXRPT_OPT_MEGAKERNEL_LANES: `lanes` paths per wave, the other lanes re-trace a twin's path and
+    # write nothing -- the image and the ray counts must equal the wavefront frame's, on the full frame
+    # and on a band share
+    torch = torch_cuda
+    sc, sky = scene_bundle(name)
+    st = sc.settings(MaxPathLength=L)
+    t = tracer(name)
+    rtc, lights = D.make_constants(sc, st, sky, W, H, 3), D.make_lights(sc)
+    lay = band_layout(W, H, 2)
+    try:
+        for tiles, n in ((None, W * H), (lay.rank_tiles(1), lay.counts[1])):
+            acc0 = torch.full((n, 4), 0.5, dtype=torch.float32, device="cuda")
+            t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
+            t.set_option(A.OPT_PACKET_TRAVERSAL, 0)
+            ref = gpu_render(torch, name, W, H, st, 3, tiles=tiles, n_out=n, accum=acc0.clone(), rtc=rtc,
+                             lights=lights).cpu().numpy()
+            s_ref = t.stats()
+            t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30)
+            t.set_option(A.OPT_PACKET_TRAVERSAL, A.DEFAULT_PACKET_TRAVERSAL)
+            t.set_option(A.OPT_MEGAKERNEL_LANES, lanes)
+            got = gpu_render(torch, name, W, H, st, 3, tiles=tiles, n_out=n, accum=acc0.clone(), rtc=rtc,
+                             lights=lights).cpu().numpy()
+            s_got = t.stats()
+            np.testing.assert_array_equal(got, ref)
+            assert list(s_got.radiance_rays_per_depth) == list(s_ref.radiance_rays_per_depth)
+            assert list(s_got.shadow_rays_per_depth) == list(s_ref.shadow_rays_per_depth)
+    finally:
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
+        t.set_option(A.OPT_MEGAKERNEL_LANES, A.DEFAULT_MEGAKERNEL_LANES)
+        t.set_option(A.OPT_PACKET_TRAVERSAL, A.DEFAULT_PACKET_TRAVERSAL)
