@@ -1511,11 +1511,9 @@ PT_DEV void count_rays(uint32_t* counters, uint32_t n) {
 // / the depth-1 sun shadow rays (all lanes must be active at depth 1 then).  Returns the radiance.
 // kBake: the first ray is BakeRayGen's (TMin 0.0001, IsDiffuse, no packets) instead of RaygenShader's.
 // nc: the workgroup's LDS copy of the top BVH8 nodes for the per-lane traversals (n = 0: none).
-// quiet: a twin lane (DXRPT_OPT_MEGAKERNEL_LANES) -- same path as its partner lane, so it writes the
-// same shadow slots with the same values, and adds nothing to the ray counters.
 template <bool kBake>
 PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, f3 dir, float tmax, lds_int* stk,
-                         const NodeCache& nc = NodeCache{nullptr, 0u}, bool quiet = false) {
+                         const NodeCache& nc = NodeCache{nullptr, 0u}) {
     const dxrpt_app_settings& set = A.P.set;
     const float tmin1 = kBake ? 0.0001f : 0.0f;
     const bool isDiffuse1 = kBake;
@@ -1528,7 +1526,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
     float4 rad = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const int L = set.MaxPathLength < 2 ? 2 : set.MaxPathLength;
     for (int d = 1; d <= L - 1; ++d) {
-        count_rays(A.F.counters + uint32_t(d) * kQueueShards, quiet ? 0u : 1u);
+        count_rays(A.F.counters + uint32_t(d) * kQueueShards, 1u);
         HitRec h;
         uint32_t nv = 0, nt = 0;
         if (d == 1 && (packet & 1u))  // coherent primary rays: wave-coherent traversal (same results)
@@ -1548,7 +1546,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
         path_vertex(A, d, V, [&](f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
             emit_shadow(A, slot_p, nsh, o, dd, tmn, tmx, c, fo);
         }, O);
-        count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, quiet ? 0u : nsh);
+        count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, nsh);
         rad.x += thr.x * O.local.x;
         rad.y += thr.y * O.local.y;
         rad.z += thr.z * O.local.z;
@@ -1730,40 +1728,45 @@ PT_DEV float4 trace_path_group(const KArgs& A, uint32_t slot_p, uint32_t pix, f3
         payloadRoughness = O.nextRoughness;
         payloadIsDiffuse = O.nextIsDiffuse;
     }
-    (void)gsize;
     return rad;
 }
 
-PT_DEV void camera_path(const KArgs& A, uint32_t p, lds_int* stk, const NodeCache& nc = NodeCache{nullptr, 0u},
-                        bool twin = false) {
+PT_DEV void camera_path(const KArgs& A, uint32_t p, lds_int* stk, const NodeCache& nc = NodeCache{nullptr, 0u}) {
     const PrimaryRay pr = primary_ray(A, p);
-    const float4 rad = A.P.mega_lanes < 64u ? trace_path_group(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, A.P.mega_lanes)
-                                            : trace_path<false>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, nc);
-    if (!twin) accumulate_pixel(A, pr.accumIdx, rad);
+    const float4 rad = trace_path<false>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, nc);
+    accumulate_pixel(A, pr.accumIdx, rad);
+}
+
+// A path of a path group (DXRPT_OPT_MEGAKERNEL_LANES): only member 0 writes the pixel.
+PT_DEV void camera_path_group(const KArgs& A, uint32_t p, lds_int* stk, bool member0) {
+    const PrimaryRay pr = primary_ray(A, p);
+    const float4 rad = trace_path_group(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, A.P.mega_lanes);
+    if (member0) accumulate_pixel(A, pr.accumIdx, rad);
 }
 
 // kPersistent: a grid sized to the resident waves; each wave takes the next 64 paths (one 8x8 pixel
 // block) from a frame counter until the frame is done, so no wave idles while a long one finishes.
 // kLds: the workgroup first copies the top A.P.lds_nodes BVH8 nodes (breadth-first, so the levels
 // every ray visits) behind the stacks; the per-lane traversals read those from LDS.
-template <int kOcc, bool kPersistent, bool kLds = false>
+// kGroup: path groups of 64 / A.P.mega_lanes lanes (its own instantiation, so the default kernel's
+// register allocation does not carry the group schedule).
+template <int kOcc, bool kPersistent, bool kLds = false, bool kGroup = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
 void k_path(KArgs A) {
     extern __shared__ int stack[];
     lds_int* stk = lane_stack(A.S, stack);
+    if (kGroup) {  // mega_lanes paths per wave, each traced by 64 / mega_lanes lanes
+        const uint32_t lane = threadIdx.x & 63u;
+        const uint32_t q = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * A.P.mega_lanes + (lane & (A.P.mega_lanes - 1u));
+        if (q < A.P.num_paths) camera_path_group(A, q, stk, lane < A.P.mega_lanes);
+        return;
+    }
     if (!kPersistent) {
         const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
         if (kLds) {
             const NodeCache nc = node_cache_fill(A.S, reinterpret_cast<uint4*>(stack + A.S.stack_ints * blockDim.x),
                                                  A.P.lds_nodes);
             if (p < A.P.num_paths) camera_path(A, p, stk, nc);
-            return;
-        }
-        if (A.P.mega_lanes < 64u) {  // wave-uniform: mega_lanes paths per wave, each traced by 64/mega_lanes lanes
-            const uint32_t lane = threadIdx.x & 63u;
-            const uint32_t q = (p >> 6) * A.P.mega_lanes + (lane & (A.P.mega_lanes - 1u));
-            if (q >= A.P.num_paths) return;
-            camera_path(A, q, stk, NodeCache{nullptr, 0u}, lane >= A.P.mega_lanes);
             return;
         }
         if (p >= A.P.num_paths) return;
@@ -1934,6 +1937,12 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
             else if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_path<6, false, true>), dim3(gm), dim3(tb), ldsn, stream, A);
             else if (fp.megakernel_occupancy == 5) hipLaunchKernelGGL((k_path<5, false, true>), dim3(gm), dim3(tb), ldsn, stream, A);
             else hipLaunchKernelGGL((k_path<4, false, true>), dim3(gm), dim3(tb), ldsn, stream, A);
+        }
+        else if (twins) {
+            if (fp.megakernel_occupancy >= 7) hipLaunchKernelGGL((k_path<7, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
+            else if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_path<6, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
+            else if (fp.megakernel_occupancy == 5) hipLaunchKernelGGL((k_path<5, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
+            else hipLaunchKernelGGL((k_path<4, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
         }
         else if (fp.megakernel_occupancy == 8) hipLaunchKernelGGL((k_path<8, false>), dim3(gm), dim3(tb), ldsm, stream, A);
         else if (fp.megakernel_occupancy == 7) hipLaunchKernelGGL((k_path<7, false>), dim3(gm), dim3(tb), ldsm, stream, A);
