@@ -1517,9 +1517,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
     const dxrpt_app_settings& set = A.P.set;
     const float tmin1 = kBake ? 0.0001f : 0.0f;
     const bool isDiffuse1 = kBake;
-    // packets need every lane of the wave (the packet stack lives one entry per lane): a frame's last,
-    // partial wave traverses one ray per lane instead (same results)
-    const uint32_t packet = (kBake || __ballot(1) != ~0ull) ? 0u : A.P.packet;
+    const uint32_t packet = kBake ? 0u : A.P.packet;
     f3 thr = f3{1.0f, 1.0f, 1.0f};
     float payloadRoughness = 0.0f;
     bool payloadIsDiffuse = isDiffuse1;
