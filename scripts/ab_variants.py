@@ -4,7 +4,7 @@ workload (Sponza proxy 1920x1080, L=3).  Prints per-kernel ms per frame from the
 
     python scripts/ab_variants.py [--frames 16] [--rounds 3] [--variants w8m0,w8m1r16,...]
 variant syntax: letter+number tokens, e.g. w8m0b64o7 (w width, m mode, r refill lanes, k chunks per
-wave, p postpone lanes, b trace block, o occupancy)
+wave, p postpone lanes, b trace block, o occupancy; see KEYS for the rest, e.g. l megakernel lanes)
 """
 import argparse
 import os
