@@ -6,7 +6,7 @@ MaxPathLength 3, one sample per pixel per frame with progressive accumulation.
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 A step is one frame (DispatchRays(1920,1080,1) equivalent, DXRPathTracer.cpp:2024-2090) over the whole
-image.  With N ranks the image is split into 16-row bands (band b -> rank b % N) and every frame ends
+image.  With N ranks the image is split into 8-row bands (band b -> rank b % N) and every frame ends
 with an RCCL gather of the band slabs to rank 0 plus the un-permute: total work per
 frame is fixed, so scaling is "strong".  The gather of frame f runs on RCCL's stream while frame f+1
 renders (distributed.PipelinedGather); the last frame's gather is inside the timed region.  value = nominal Mrays/s of the whole job (W*H*(1+2(L-1))
