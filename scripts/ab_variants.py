@@ -49,7 +49,9 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--L", type=int, default=3)
     ap.add_argument("--scene", default="sponza")
-    ap.add_argument("--share", type=int, default=1, help="render rank 0's band share of an N-GPU frame")
+    ap.add_argument("--share", type=int, default=1, help="render one rank's band share of an N-GPU frame")
+    ap.add_argument("--rank", type=int, default=0, help="which rank's share (--share > 1)")
+    ap.add_argument("--band", type=int, default=0, help="band rows of the partition (0: distributed.BAND_ROWS)")
     args = ap.parse_args()
     import torch
     import dxrpathtracer_amd as D
@@ -74,7 +76,7 @@ def main():
     tiles = None
     if args.share > 1:
         from dxrpathtracer_amd.distributed import band_layout
-        tiles = band_layout(W, H, args.share).rank_tiles(0)
+        tiles = band_layout(W, H, args.share, **({'band': args.band} if args.band else {})).rank_tiles(args.rank)
     consts = [D.make_constants(sc, st, sky, W, H, s) for s in range(16)]
     lights = D.make_lights(sc)
     sh = torch.cuda.current_stream().cuda_stream
@@ -122,7 +124,7 @@ def main():
             t.set_option(A.OPT_KERNEL_TIMING, 0)
             n = max(1, s.timed_frames)
             res[v].append((wall, [s.kernel_ms[k] / n for k in range(A.K_COUNT)]))
-    print(f"{args.scene} {W}x{H} L={args.L} share 1/{args.share}: median of {args.rounds} rounds x {args.frames} frames (ms/frame)")
+    print(f"{args.scene} {W}x{H} L={args.L} share 1/{args.share} rank {args.rank}: median of {args.rounds} rounds x {args.frames} frames (ms/frame)")
     print(f"{'variant':12s} {'wall':>8s} " + " ".join(f"{k:>12s}" for k in A.KERNEL_NAMES))
     for v, rows in res.items():
         wall = statistics.median(r[0] for r in rows)
