@@ -141,6 +141,7 @@ DXRPT_SYMBOLS = ("dxrpt_abi_version", "dxrpt_default_settings", "dxrpt_create", 
 DXRPT_HOST_SYMBOLS = ("dxrpt_host_scene_create", "dxrpt_host_scene_load", "dxrpt_host_scene_destroy", "dxrpt_host_last_error",
                       "dxrpt_host_inv_view_projection", "dxrpt_host_sky_create", "dxrpt_host_fill_constants",
                       "dxrpt_host_float_to_half", "dxrpt_host_half_to_float", "dxrpt_host_hosek_load",
+                      "dxrpt_host_hosek_load_tables",
                       "dxrpt_host_hosek_destroy", "dxrpt_host_hosek_last_error", "dxrpt_host_sky_create_hosek",
                       "dxrpt_host_hosek_rgb_radiance", "dxrpt_host_hosek_solar_radiance", "dxrpt_host_spectrum_to_rgb",
                       "dxrpt_host_spectrum_from_rgb_reflectance", "dxrpt_host_lightmap_charts",
@@ -215,6 +216,7 @@ def host() -> C.CDLL:
         H.dxrpt_host_half_to_float.argtypes = [C.c_uint16]
         H.dxrpt_host_half_to_float.restype = f32
         H.dxrpt_host_hosek_load.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(P)]
+        H.dxrpt_host_hosek_load_tables.argtypes = [C.c_char_p, C.POINTER(P)]
         H.dxrpt_host_hosek_destroy.argtypes = [P]
         H.dxrpt_host_hosek_destroy.restype = None
         H.dxrpt_host_hosek_last_error.restype = C.c_char_p

@@ -394,53 +394,143 @@ extern "C" {
 
 const char* dxrpt_host_hosek_last_error(void) { return g_hosek_err.c_str(); }
 
-int dxrpt_host_hosek_load(const char* hosek_dir, const char* spectrum_source, dxrpt_host_hosek** out) {
-    if (!hosek_dir || !spectrum_source || !out) {
-        g_hosek_err = "dxrpt_host_hosek_load: null argument";
-        return -1;
-    }
-    *out = nullptr;
-    auto* H = new dxrpt_host_hosek();
-    std::string rgb, spec, sp;
-    const std::string dir(hosek_dir);
-    if (!read_file(dir + "/ArHosekSkyModelData_RGB.h", rgb) || !read_file(dir + "/ArHosekSkyModelData_Spectral.h", spec) ||
-        !read_file(spectrum_source, sp)) {
-        g_hosek_err = "dxrpt_host_hosek_load: cannot read the dataset sources under " + dir + " / " + spectrum_source;
-        delete H;
-        return -1;
-    }
-    auto need = [&](const std::string& src, const std::string& name, std::vector<double>& v, size_t n) {
-        if (!named_array(src, name, v) || v.size() != n) {
-            g_hosek_err = "dxrpt_host_hosek_load: array " + name + " missing or of unexpected size";
+}  // extern "C"
+
+namespace {
+
+// Fills every table of `H` through `get(name, values)` (false: missing).  Model tables are doubles,
+// the Spectrum.cpp tables are float literals.
+template <class Get>
+bool fill_tables(dxrpt_host_hosek& H, Get get, const char* who) {
+    auto need = [&](const std::string& name, std::vector<double>& v, size_t n) {
+        if (!get(name, v) || v.size() != n) {
+            g_hosek_err = std::string(who) + ": array " + name + " missing or of unexpected size";
             return false;
         }
         return true;
     };
     auto needf = [&](const std::string& name, std::vector<float>& v, size_t n) {
         std::vector<double> d;
-        if (!need(sp, name, d, n)) return false;
-        v.assign(d.begin(), d.end());  // the tables are float literals
+        if (!need(name, d, n)) return false;
+        v.assign(d.begin(), d.end());
         return true;
     };
     bool ok = true;
     for (int c = 0; c < 3 && ok; ++c)
-        ok = need(rgb, "datasetRGB" + std::to_string(c + 1), H->rgb[c], 1080) &&
-             need(rgb, "datasetRGBRad" + std::to_string(c + 1), H->rgbRad[c], 120);
+        ok = need("datasetRGB" + std::to_string(c + 1), H.rgb[c], 1080) &&
+             need("datasetRGBRad" + std::to_string(c + 1), H.rgbRad[c], 120);
     for (int w = 0; w < 11 && ok; ++w) {
         const std::string wl = std::to_string(320 + 40 * w);
-        ok = need(spec, "dataset" + wl, H->spec[w], 1080) && need(spec, "datasetRad" + wl, H->specRad[w], 120) &&
-             need(spec, "solarDataset" + wl, H->solar[w], 1800) && need(spec, "limbDarkeningDataset" + wl, H->limb[w], 6);
+        ok = need("dataset" + wl, H.spec[w], 1080) && need("datasetRad" + wl, H.specRad[w], 120) &&
+             need("solarDataset" + wl, H.solar[w], 1800) && need("limbDarkeningDataset" + wl, H.limb[w], 6);
     }
     static const char* refl[7] = {"RGBRefl2SpectWhite", "RGBRefl2SpectCyan", "RGBRefl2SpectMagenta", "RGBRefl2SpectYellow",
                                   "RGBRefl2SpectRed",   "RGBRefl2SpectGreen", "RGBRefl2SpectBlue"};
-    ok = ok && needf("CIE_lambda", H->cieLambda, 471) && needf("CIE_X", H->cieX, 471) && needf("CIE_Y", H->cieY, 471) &&
-         needf("CIE_Z", H->cieZ, 471) && needf("RGB2SpectLambda", H->rgbLambda, 32);
-    for (int k = 0; k < 7 && ok; ++k) ok = needf(refl[k], H->refl[k], 32);
-    if (!ok) {
+    ok = ok && needf("CIE_lambda", H.cieLambda, 471) && needf("CIE_X", H.cieX, 471) && needf("CIE_Y", H.cieY, 471) &&
+         needf("CIE_Z", H.cieZ, 471) && needf("RGB2SpectLambda", H.rgbLambda, 32);
+    for (int k = 0; k < 7 && ok; ++k) ok = needf(refl[k], H.refl[k], 32);
+    if (ok) spectrum_init(H);
+    return ok;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dxrpt_host_hosek_load(const char* hosek_dir, const char* spectrum_source, dxrpt_host_hosek** out) {
+    if (!hosek_dir || !spectrum_source || !out) {
+        g_hosek_err = "dxrpt_host_hosek_load: null argument";
+        return -1;
+    }
+    *out = nullptr;
+    std::string rgb, spec, sp;
+    const std::string dir(hosek_dir);
+    if (!read_file(dir + "/ArHosekSkyModelData_RGB.h", rgb) || !read_file(dir + "/ArHosekSkyModelData_Spectral.h", spec) ||
+        !read_file(spectrum_source, sp)) {
+        g_hosek_err = "dxrpt_host_hosek_load: cannot read the dataset sources under " + dir + " / " + spectrum_source;
+        return -1;
+    }
+    auto get = [&](const std::string& name, std::vector<double>& v) {
+        const std::string& src = name.rfind("dataset", 0) == 0 && name.find("RGB") != std::string::npos ? rgb
+                                 : (name.rfind("dataset", 0) == 0 || name.rfind("solar", 0) == 0 || name.rfind("limb", 0) == 0)
+                                     ? spec
+                                     : sp;
+        return named_array(src, name, v);
+    };
+    auto* H = new dxrpt_host_hosek();
+    if (!fill_tables(*H, get, "dxrpt_host_hosek_load")) {
         delete H;
         return -1;
     }
-    spectrum_init(*H);
+    *out = H;
+    return 0;
+}
+
+// The packaged tables (dxrpathtracer_amd/data/hosek_tables.bin, scripts/make_hosek_tables.py):
+// "DXRPTHK1", u32 count, then {u32 name length, name, u32 type (0 f64 / 1 f32), u32 count, data}.
+int dxrpt_host_hosek_load_tables(const char* path, dxrpt_host_hosek** out) {
+    if (!path || !out) {
+        g_hosek_err = "dxrpt_host_hosek_load_tables: null argument";
+        return -1;
+    }
+    *out = nullptr;
+    std::string blob;
+    if (!read_file(path, blob)) {
+        g_hosek_err = std::string("dxrpt_host_hosek_load_tables: cannot read ") + path;
+        return -1;
+    }
+    std::vector<std::pair<std::string, std::vector<double>>> tables;
+    size_t p = 0;
+    auto u32 = [&](uint32_t& v) {
+        if (p + 4 > blob.size()) return false;
+        std::memcpy(&v, blob.data() + p, 4);
+        p += 4;
+        return true;
+    };
+    uint32_t count = 0;
+    bool ok = blob.size() >= 12 && blob.compare(0, 8, "DXRPTHK1") == 0;
+    p = 8;
+    ok = ok && u32(count);
+    for (uint32_t i = 0; ok && i < count; ++i) {
+        uint32_t nlen = 0, type = 0, n = 0;
+        ok = u32(nlen) && p + nlen <= blob.size();
+        if (!ok) break;
+        std::string name = blob.substr(p, nlen);
+        p += nlen;
+        ok = u32(type) && u32(n) && type <= 1;
+        const size_t esz = type == 0 ? 8 : 4;
+        ok = ok && p + size_t(n) * esz <= blob.size();
+        if (!ok) break;
+        std::vector<double> v(n);
+        for (uint32_t k = 0; k < n; ++k) {
+            if (type == 0) {
+                std::memcpy(&v[k], blob.data() + p + size_t(k) * 8, 8);
+            } else {
+                float f;
+                std::memcpy(&f, blob.data() + p + size_t(k) * 4, 4);
+                v[k] = f;
+            }
+        }
+        p += size_t(n) * esz;
+        tables.emplace_back(std::move(name), std::move(v));
+    }
+    if (!ok || p != blob.size()) {
+        g_hosek_err = std::string("dxrpt_host_hosek_load_tables: malformed table file ") + path;
+        return -1;
+    }
+    auto get = [&](const std::string& name, std::vector<double>& v) {
+        for (auto& t : tables)
+            if (t.first == name) {
+                v = t.second;
+                return true;
+            }
+        return false;
+    };
+    auto* H = new dxrpt_host_hosek();
+    if (!fill_tables(*H, get, "dxrpt_host_hosek_load_tables")) {
+        delete H;
+        return -1;
+    }
     *out = H;
     return 0;
 }

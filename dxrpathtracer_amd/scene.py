@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -141,13 +142,19 @@ class Sky:
 
 
 class HosekData:
-    """The Hosek-Wilkie datasets (dxrpt_host_hosek_load): `hosek_dir` holds the reference's
-    ArHosekSkyModelData_RGB.h / _Spectral.h, `spectrum_source` is its Graphics/Spectrum.cpp."""
+    """The Hosek-Wilkie tables.  Default: the packaged table file (dxrpt_host_hosek_load_tables,
+    data/hosek_tables.bin, generated by scripts/make_hosek_tables.py).  With `hosek_dir` +
+    `spectrum_source`: parsed out of the reference's ArHosekSkyModelData_RGB.h / _Spectral.h and
+    Graphics/Spectrum.cpp (dxrpt_host_hosek_load; tests use it to check the packaged file)."""
 
-    def __init__(self, hosek_dir: str, spectrum_source: str):
+    def __init__(self, table_file: str | None = None, hosek_dir: str | None = None, spectrum_source: str | None = None):
         H = A.host()
         self._p = C.c_void_p()
-        if H.dxrpt_host_hosek_load(hosek_dir.encode(), spectrum_source.encode(), C.byref(self._p)) != 0:
+        if hosek_dir is not None:
+            rc = H.dxrpt_host_hosek_load(hosek_dir.encode(), spectrum_source.encode(), C.byref(self._p))
+        else:
+            rc = H.dxrpt_host_hosek_load_tables((table_file or HOSEK_TABLES).encode(), C.byref(self._p))
+        if rc != 0:
             raise RuntimeError(H.dxrpt_host_hosek_last_error().decode())
 
     @property
@@ -178,55 +185,47 @@ class HosekData:
             self._p = None
 
 
-def hosek_dataset_paths():
-    """Where the Hosek-Wilkie datasets are: $DXRPT_HOSEK_DIR / $DXRPT_SPECTRUM_SOURCE, else the
-    reference checkout's SampleFramework12/v1.02 ($DXRPT_REFERENCE_ROOT, default /root/reference).
-    None when they are not readable (then make_sky falls back to the analytic sky)."""
-    import os
+HOSEK_TABLES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "hosek_tables.bin")
+
+
+def reference_hosek_sources():
+    """The reference checkout's dataset sources ($DXRPT_REFERENCE_ROOT, default /root/reference), or None.
+    Only tests use them, to check the packaged tables; the product never reads the reference."""
     root = os.path.join(os.environ.get("DXRPT_REFERENCE_ROOT", "/root/reference"), "SampleFramework12", "v1.02")
-    hd = os.environ.get("DXRPT_HOSEK_DIR", os.path.join(root, "HosekSky"))
-    sp = os.environ.get("DXRPT_SPECTRUM_SOURCE", os.path.join(root, "Graphics", "Spectrum.cpp"))
+    hd, sp = os.path.join(root, "HosekSky"), os.path.join(root, "Graphics", "Spectrum.cpp")
     ok = all(os.path.isfile(p) for p in (os.path.join(hd, "ArHosekSkyModelData_RGB.h"),
                                           os.path.join(hd, "ArHosekSkyModelData_Spectral.h"), sp))
     return (hd, sp) if ok else None
 
 
-_HOSEK = {}
+_HOSEK = []
 
 
-def load_hosek():
-    """The process-wide HosekData, or None when the datasets are not available."""
-    paths = hosek_dataset_paths()
-    if paths is None:
-        return None
-    if paths not in _HOSEK:
-        _HOSEK[paths] = HosekData(*paths)
-    return _HOSEK[paths]
+def load_hosek() -> HosekData:
+    """The process-wide HosekData from the packaged tables (raises if the file is missing)."""
+    if not _HOSEK:
+        _HOSEK.append(HosekData())
+    return _HOSEK[0]
 
 
 def make_sky(settings: A.AppSettings, turbidity: float = DEFAULT_TURBIDITY,
-             ground_albedo=DEFAULT_GROUND_ALBEDO, res: int = SKY_RES, model: str = "auto") -> Sky:
-    """SkyCache::Init.  model: "hosek" (the reference's Hosek-Wilkie sky, needs the datasets),
-    "analytic" (Preetham proxy), "auto" (hosek when the datasets are available)."""
+             ground_albedo=DEFAULT_GROUND_ALBEDO, res: int = SKY_RES, model: str = "hosek") -> Sky:
+    """SkyCache::Init.  model: "hosek" (the reference's Hosek-Wilkie sky from the packaged tables, the
+    default) or "analytic" (a Preetham proxy, kept for A/B and for turbidity above the solar fit)."""
     cube = np.zeros(6 * res * res * 4, dtype=np.uint16)
     irr = (C.c_float * 3)()
     ren = (C.c_float * 3)()
     sun = (C.c_float * 3)(*settings.SunDirection)
     alb = (C.c_float * 3)(*ground_albedo)
-    data = None
-    if model in ("auto", "hosek"):
-        data = load_hosek()
-        if data is None and model == "hosek":
-            raise RuntimeError("Hosek-Wilkie datasets not found (set DXRPT_HOSEK_DIR / DXRPT_SPECTRUM_SOURCE)")
-    elif model != "analytic":
-        raise ValueError(f"unknown sky model {model!r}")
     H = A.host()
-    if data is not None:
-        rc = H.dxrpt_host_sky_create_hosek(data.handle, sun, settings.SunSize, turbidity, alb, res, cube.ctypes.data,
-                                           irr, ren)
+    if model == "hosek":
+        rc = H.dxrpt_host_sky_create_hosek(load_hosek().handle, sun, settings.SunSize, turbidity, alb, res,
+                                           cube.ctypes.data, irr, ren)
         if rc != 0:
             raise RuntimeError(H.dxrpt_host_hosek_last_error().decode())
         return Sky(cube, res, tuple(irr), tuple(ren), "hosek")
+    if model != "analytic":
+        raise ValueError(f"unknown sky model {model!r}")
     rc = H.dxrpt_host_sky_create(sun, settings.SunSize, turbidity, alb, res, cube.ctypes.data, irr, ren)
     if rc != 0:
         raise RuntimeError("dxrpt_host_sky_create failed")

@@ -95,9 +95,9 @@ void dxrpt_host_inv_view_projection(const float position[3], float xrot, float y
                                     float nearz, float farz, float out_inv_view_projection[16]);
 
 /* SkyCache::Init: a res x res x 6 RGBA16F sky cube (sun excluded) + sun irradiance/render colour,
- * all pre-scaled by FP16Scale = 2^-10.  Sky model: Preetham-Shirley-Smits analytic sky, the fallback
- * when the Hosek-Wilkie datasets are not available (dxrpt_host_sky_create_hosek is the reference's
- * model).  out_cube holds res*res*6*4 halfs. */
+ * all pre-scaled by FP16Scale = 2^-10.  Sky model: Preetham-Shirley-Smits analytic sky, an explicit
+ * alternative (dxrpt_host_sky_create_hosek is the reference's model and the default).  out_cube holds
+ * res*res*6*4 halfs. */
 int dxrpt_host_sky_create(const float sun_direction[3], float sun_size_deg, float turbidity,
                           const float ground_albedo[3], uint32_t res, uint16_t* out_cube,
                           float out_sun_irradiance[3], float out_sun_render_color[3]);
@@ -106,10 +106,13 @@ int dxrpt_host_sky_create(const float sun_direction[3], float sun_size_deg, floa
  * SkyCache::Init (Graphics/Skybox.cpp:48-215, Sample 252-270) with the Hosek-Wilkie RGB sky
  * (HosekSky/ArHosekSkyModel.cpp:604-652) and the spectral solar disc (:310-345, 521-566, 658-818)
  * converted to RGB through the pbrt SampledSpectrum helpers (Graphics/Spectrum.{h,cpp}).  The model
- * coefficient tables and the CIE / RGB-to-spectrum tables are data, read at run time from the
- * reference's dataset sources: `hosek_dir` holds ArHosekSkyModelData_RGB.h and
- * ArHosekSkyModelData_Spectral.h, `spectrum_source` is Graphics/Spectrum.cpp. */
+ * coefficient tables and the CIE / RGB-to-spectrum tables are data.  dxrpt_host_hosek_load_tables
+ * reads them from the packaged table file (dxrpathtracer_amd/data/hosek_tables.bin, generated once by
+ * scripts/make_hosek_tables.py); dxrpt_host_hosek_load parses them out of the reference's dataset
+ * sources (`hosek_dir` holds ArHosekSkyModelData_RGB.h and ArHosekSkyModelData_Spectral.h,
+ * `spectrum_source` is Graphics/Spectrum.cpp), used to check the packaged file. */
 typedef struct dxrpt_host_hosek dxrpt_host_hosek;
+int dxrpt_host_hosek_load_tables(const char* table_file, dxrpt_host_hosek** out);
 int dxrpt_host_hosek_load(const char* hosek_dir, const char* spectrum_source, dxrpt_host_hosek** out);
 void dxrpt_host_hosek_destroy(dxrpt_host_hosek* data);
 const char* dxrpt_host_hosek_last_error(void);

@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """Regression vectors for the Hosek-Wilkie sky (dxrpt_host_sky_create_hosek), written by OUR
-restatement (host/hosek.cpp) from the reference's dataset sources.  These pin the implementation
+restatement (host/hosek.cpp) from the packaged tables (data/hosek_tables.bin).  These pin the implementation
 against drift; the pin against the reference itself is the zenith probe of SURVEY.md 8(c) (3.04945,
 computed there from the reference's ArHosekSkyModel.cpp), asserted in tests/test_hosek_sky.py.
 
-    python tests/golden/make_hosek_golden.py   (needs the datasets, see scene.hosek_dataset_paths)
+    python tests/golden/make_hosek_golden.py
 """
 import json
 import os
@@ -20,7 +20,6 @@ PROBE_TEXELS = [(s, y, x) for s in range(6) for (y, x) in ((0, 0), (31, 97), (64
 
 
 def main():
-    assert D.scene.load_hosek() is not None, "Hosek datasets not found"
     out = {"generator": "tests/golden/make_hosek_golden.py (host/hosek.cpp restatement)", "scenes": {}}
     for name in ("sponza", "suntemple", "boxtest"):
         st = D.Scene(name).settings()

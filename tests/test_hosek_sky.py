@@ -4,7 +4,9 @@ Pins: the zenith probe of SURVEY.md 8(c) (Sponza sun, turbidity 2, ground albedo
 x 683 x 2^-10 = 3.04945, computed from the reference's ArHosekSkyModel.cpp) and regression vectors of
 this restatement (tests/golden/hosek_sky.json, tests/golden/make_hosek_golden.py).  The rest of the
 model (the spectral sun disc, DirectXMath float details) is parity-unpinned: no reference output of
-it exists here.  Skipped where the reference's dataset sources are not readable (the GPU box).
+it exists here.  The tables come from the packaged file (data/hosek_tables.bin), so these tests run
+without the reference checkout; where the checkout is present, the packaged file is checked against
+the reference's dataset sources table by table and cube by cube.
 """
 import json
 import math
@@ -17,7 +19,6 @@ import dxrpathtracer_amd as D
 import dxrpathtracer_amd._abi as A
 
 HOSEK = D.scene.load_hosek()
-pytestmark = pytest.mark.skipif(HOSEK is None, reason="Hosek-Wilkie dataset sources not available")
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "hosek_sky.json")
 
 
@@ -104,6 +105,36 @@ def test_missing_dataset_is_an_error_not_a_crash(tmp_path):
     rc = A.host().dxrpt_host_hosek_load(str(tmp_path).encode(), str(tmp_path / "none.cpp").encode(), C.byref(p))
     assert rc != 0 and not p.value
     assert b"cannot read" in A.host().dxrpt_host_hosek_last_error()
+    rc = A.host().dxrpt_host_hosek_load_tables(str(tmp_path / "none.bin").encode(), C.byref(p))
+    assert rc != 0 and not p.value
+    assert b"cannot read" in A.host().dxrpt_host_hosek_last_error()
+
+
+def test_truncated_table_file_is_rejected(tmp_path):
+    import ctypes as C
+    blob = open(D.scene.HOSEK_TABLES, "rb").read()
+    for cut in (4, 12, len(blob) // 2, len(blob) - 1):
+        f = tmp_path / f"cut{cut}.bin"
+        f.write_bytes(blob[:cut])
+        p = C.c_void_p()
+        assert A.host().dxrpt_host_hosek_load_tables(str(f).encode(), C.byref(p)) != 0 and not p.value
+        assert b"malformed" in A.host().dxrpt_host_hosek_last_error()
+
+
+def test_default_sky_is_hosek():
+    assert D.make_sky(D.Scene("sponza").settings(), res=8).model == "hosek"
+
+
+@pytest.mark.skipif(D.scene.reference_hosek_sources() is None, reason="reference checkout not present")
+def test_packaged_tables_match_reference_sources():
+    """The packaged table file and the reference's dataset sources give the same model, bit for bit."""
+    src = D.scene.HosekData(None, *D.scene.reference_hosek_sources())
+    for args in ((2.0, 0.25, 0.9, 0.3, 0.7, 0), (7.5, 0.6, 0.1, 1.2, 0.05, 2), (1.0, 0.0, 1.5, 0.0, 1.5, 1)):
+        assert HOSEK.rgb_radiance(*args) == src.rgb_radiance(*args)
+    for wl in (400.0, 455.0, 550.0, 699.0):
+        assert HOSEK.solar_radiance(0.8, 3.3, 0.4, 0.7, 0.001, wl) == src.solar_radiance(0.8, 3.3, 0.4, 0.7, 0.001, wl)
+    assert HOSEK.spectrum_from_rgb((0.2, 0.5, 0.9)) == src.spectrum_from_rgb((0.2, 0.5, 0.9))
+    assert HOSEK.spectrum_to_rgb([float(i) for i in range(60)]) == src.spectrum_to_rgb([float(i) for i in range(60)])
 
 
 def test_turbidity_above_fit_range_is_rejected():
