@@ -758,9 +758,6 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
                                                     : (paths > 1500000u ? 7u : (paths > 300000u ? 5u : 4u));
         fp.mega_persistent = ctx->opt_mega_persistent;
         fp.mega_lanes = ctx->opt_mega_lanes;
-        // megakernel packets need every lane of a wave (the packet stack lives one entry per lane): a
-        // frame whose last wave is partial traverses one ray per lane (same results)
-        if (fp.megakernel && paths % 64u != 0u) fp.packet = 0u;
         fp.num_cus = ctx->num_cus;
         hipStream_t s = static_cast<hipStream_t>(stream);
         if (ctx->opt_count) {

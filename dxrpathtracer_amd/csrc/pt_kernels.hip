@@ -1513,11 +1513,11 @@ PT_DEV void count_rays(uint32_t* counters, uint32_t n) {
 // nc: the workgroup's LDS copy of the top BVH8 nodes for the per-lane traversals (n = 0: none).
 template <bool kBake>
 PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, f3 dir, float tmax, lds_int* stk,
-                         const NodeCache& nc = NodeCache{nullptr, 0u}) {
+                         uint32_t packet_mask, const NodeCache& nc = NodeCache{nullptr, 0u}) {
     const dxrpt_app_settings& set = A.P.set;
     const float tmin1 = kBake ? 0.0001f : 0.0f;
     const bool isDiffuse1 = kBake;
-    const uint32_t packet = kBake ? 0u : A.P.packet;
+    const uint32_t packet = kBake ? 0u : packet_mask;
     f3 thr = f3{1.0f, 1.0f, 1.0f};
     float payloadRoughness = 0.0f;
     bool payloadIsDiffuse = isDiffuse1;
@@ -1729,9 +1729,13 @@ PT_DEV float4 trace_path_group(const KArgs& A, uint32_t slot_p, uint32_t pix, f3
     return rad;
 }
 
+// Path p of a wave whose paths are 64-aligned (p & ~63 .. p | 63).  Packets need every lane of the wave
+// (the packet stack lives one entry per lane): a partial last wave (num_paths % 64 != 0) traverses one
+// ray per lane -- a wave-uniform scalar test, the other waves keep their packets (same results).
 PT_DEV void camera_path(const KArgs& A, uint32_t p, lds_int* stk, const NodeCache& nc = NodeCache{nullptr, 0u}) {
     const PrimaryRay pr = primary_ray(A, p);
-    const float4 rad = trace_path<false>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, nc);
+    const uint32_t packet = (p | 63u) < A.P.num_paths ? A.P.packet : 0u;
+    const float4 rad = trace_path<false>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, packet, nc);
     accumulate_pixel(A, pr.accumIdx, rad);
 }
 
@@ -1827,7 +1831,7 @@ void k_bake(KArgs A, BakeArgs B) {
         B.lightmap[texel] = make_float4(1.0f, 0.0f, 1.0f, 1.0f);
         return;
     }
-    const float4 r = trace_path<true>(A, i, texel, origin, dir, kFP32Max, lane_stack(A.S, stack));
+    const float4 r = trace_path<true>(A, i, texel, origin, dir, kFP32Max, lane_stack(A.S, stack), 0u);
     float3 c = make_float3(r.x, r.y, r.z);
     const float4 prev = B.accum[texel];
     float3 sum = make_float3(prev.x, prev.y, prev.z);
@@ -1925,7 +1929,9 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
         if (ev) (void)hipEventRecord(ev[0], stream);
         if (fp.mega_persistent && tb == 64u) {
             const uint32_t gp = std::min(gm, fp.mega_persistent * fp.num_cus);
-            if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_path<6, true>), dim3(gp), dim3(tb), ldsm, stream, A);
+            // the same register budgets as the non-persistent kernel (A/B at equal occupancy)
+            if (fp.megakernel_occupancy >= 7) hipLaunchKernelGGL((k_path<7, true>), dim3(gp), dim3(tb), ldsm, stream, A);
+            else if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_path<6, true>), dim3(gp), dim3(tb), ldsm, stream, A);
             else if (fp.megakernel_occupancy == 4) hipLaunchKernelGGL((k_path<4, true>), dim3(gp), dim3(tb), ldsm, stream, A);
             else hipLaunchKernelGGL((k_path<5, true>), dim3(gp), dim3(tb), ldsm, stream, A);
         }

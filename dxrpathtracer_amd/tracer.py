@@ -9,8 +9,6 @@ from __future__ import annotations
 
 import ctypes as C
 
-import numpy as np
-
 from . import _abi as A
 from .scene import Scene, Sky, make_constants, make_lights
 
@@ -151,29 +149,3 @@ class DXRPathTracer:
         self._check(self._L.dxrpt_denoise_median(self._ctx, C.c_void_p(in_ptr), C.c_void_p(out_ptr), width, height,
                                                  C.c_void_p(stream)), "dxrpt_denoise_median")
 
-
-def row_band_tiles(width: int, height: int, rank: int, world: int, band: int = 16):
-    """Screen-space sharding: bands of `band` full rows, band b -> rank b % world,
-    written compactly (band after band) into the rank's local buffer."""
-    tiles = []
-    off = 0
-    for b, y0 in enumerate(range(0, height, band)):
-        if b % world != rank:
-            continue
-        h = min(band, height - y0)
-        tiles.append(A.Tile(0, y0, width, h, off, width, 0))
-        off += width * h
-    return tiles, off
-
-
-def unpermute_bands(parts, width: int, height: int, world: int, band: int = 16) -> np.ndarray:
-    """Host reference of the gather's un-permute: parts[r] is rank r's compact (n_r, 4) buffer."""
-    out = np.zeros((height * width, 4), dtype=np.float32)
-    offs = [0] * world
-    for b, y0 in enumerate(range(0, height, band)):
-        r = b % world
-        h = min(band, height - y0)
-        n = width * h
-        out[y0 * width:(y0 + h) * width] = parts[r][offs[r]:offs[r] + n]
-        offs[r] += n
-    return out.reshape(height, width, 4)

@@ -317,7 +317,8 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                               4 (no spills), 5, 6, 7, 8, or 3 = the compiler's */
 #define DXRPT_OPT_MEGAKERNEL_PERSISTENT 26u /* > 0: the megakernel as a persistent grid of this many
                                                waves per CU pulling 64-path chunks (0 = one wave per
-                                               64 paths, default).  Identical results. */
+                                               64 paths, default); occupancy 8 runs at the 7-wave budget.
+                                               Identical results. */
 #define DXRPT_OPT_MEGAKERNEL_LANES 27u /* paths per 64-lane megakernel wave: 64 (default), 32 or 16; each path
                                           is then carried by 64/value lanes that shade it together and
                                           trace its continuation and shadow rays concurrently (shorter

@@ -9,8 +9,12 @@ import dxrpathtracer_amd as D
 from oracle import pyoracle as O
 
 # Parity gate (BASELINE.json north_star): per-pixel RGB within 1e-4 relative at matched CMJ indices.
+# The relative error's denominator is floored at ATOL / RTOL = 1e-4 (radiance is in 2^-10-scaled units,
+# sky texels ~1..5), so the gate is relative for every pixel brighter than 1e-4 and 1e-8 absolute below.
 RTOL = 1e-4
-ATOL = 1e-6  # absolute floor for pixels whose true value is ~0
+ATOL = 1e-8
+# max relative error seen per parity check in this session (reported by conftest's terminal summary)
+PARITY_LOG: list = []
 
 
 @functools.lru_cache(maxsize=None)
@@ -35,6 +39,7 @@ def assert_parity(gpu: np.ndarray, ref: np.ndarray, what: str):
     assert gpu.shape == ref.shape, (gpu.shape, ref.shape)
     assert np.isfinite(gpu).all(), f"{what}: non-finite GPU pixels"
     e = rel_err(gpu[..., :3], ref[..., :3])
+    PARITY_LOG.append((what, float(e.max()) if e.size else 0.0, int(e.shape[0] * e.shape[1])))
     bad = e > RTOL
     if bad.any():
         idx = np.argwhere(bad)[:5]

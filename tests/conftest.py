@@ -38,3 +38,17 @@ def torch_cuda():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch
+
+
+def pytest_terminal_summary(terminalreporter):
+    """Max relative error of every GPU-vs-oracle parity check run in this session."""
+    try:
+        from tests._common import PARITY_LOG
+    except Exception:
+        return
+    if not PARITY_LOG:
+        return
+    terminalreporter.section("parity: max relative error per check (gate 1e-4)")
+    for what, err, n in PARITY_LOG:
+        terminalreporter.write_line(f"{err:.3e}  {n:8d} px  {what}")
+    terminalreporter.write_line(f"overall max {max(e for _, e, _ in PARITY_LOG):.3e} over {len(PARITY_LOG)} checks")

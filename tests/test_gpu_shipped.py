@@ -1,0 +1,153 @@
+"""GPU parity of the SHIPPED configuration: full frames through dxrpt_render with no option overrides.
+
+The other parity tests pin the wavefront schedule (tests/test_gpu_parity.py) and reach the megakernel
+only through bit-identity.  Here every context is fresh and untouched, so each frame runs exactly what
+bench.py times: the megakernel k_path (packet primaries and depth-1 sun shadows, the occupancy picked
+by frame size) up to 10M path vertices, the wavefront above; frame buffers sized for the whole frame.
+Each full frame (RaygenShader over DispatchRays(W, H, 1), RayTrace.hlsl:92-149) is compared with the
+oracle on >= 6 crops: the four corners, the last rows, a sky region, the centre, and -- for sizes that
+are not a multiple of 64 paths -- the partial last wave.  Gate: tests/_common.py (1e-4 relative).
+"""
+import numpy as np
+import pytest
+
+import dxrpathtracer_amd as D
+import dxrpathtracer_amd._abi as A
+from dxrpathtracer_amd.distributed import band_layout
+from dxrpathtracer_amd.tracer import DXRPathTracer
+from tests._common import assert_parity, oracle_scene, scene_bundle
+
+pytestmark = pytest.mark.gpu
+
+_CTX = {}
+
+
+def shipped(name):
+    """A context with every option at its default (one per scene)."""
+    if name not in _CTX:
+        sc, sky = scene_bundle(name)
+        t = DXRPathTracer(0)
+        t.initialize_scene(sc, sky)
+        t.build_rt_acceleration_structure()
+        _CTX[name] = t
+    return _CTX[name]
+
+
+def frame_crops(W, H, extra=()):
+    c = 64
+    crops = [(0, 0, c, c), (W - c, 0, c, c), (0, H - c, c, c), (W - c, H - c, c, c),  # corners
+             (0, H - 2, W, 2),                                                       # the last rows
+             (W // 2 - 48, H // 2 - 32, 96, 64)]                                     # centre
+    n = W * H
+    if n % 64:  # the partial last wave: its paths are the last n % 64 of the frame (row-major tail)
+        k = n % 64
+        crops.append((W - k, H - 1, k, 1) if k <= W else (0, H - 1, W, 1))
+    return crops + list(extra)
+
+
+# a block of primary-ray misses (the proxy atrium's open roof at the reference pose: MissShader with
+# the sky cube and the sun disc test; found with the oracle's trace_rays).  SunTemple's hall shows no sky.
+SKY = {"sponza": (992, 0, 160, 24)}
+
+
+def render_shipped(torch, name, W, H, L, sample, prefill=0.0, tiles=None, n_out=None, check_kernel=None):
+    sc, sky = scene_bundle(name)
+    st = sc.settings(MaxPathLength=L)
+    rtc = D.make_constants(sc, st, sky, W, H, sample)
+    t = shipped(name)
+    n = W * H if n_out is None else n_out
+    init = torch.full((n, 4), prefill, dtype=torch.float32, device="cuda")
+    acc = init.clone()
+    stream = torch.cuda.current_stream().cuda_stream
+    t.render_raw(rtc, st, acc.data_ptr(), W, H, tiles=tiles, stream=stream, lights=D.make_lights(sc))
+    torch.cuda.synchronize()
+    out = acc.cpu().numpy()
+    if check_kernel is not None:
+        # which schedule ran: kernel timing only brackets launches (the frame must come out identical)
+        acc2 = init.clone()
+        t.set_option(A.OPT_KERNEL_TIMING, 1)
+        t.reset_timing()
+        try:
+            t.render_raw(rtc, st, acc2.data_ptr(), W, H, tiles=tiles, stream=stream, lights=D.make_lights(sc))
+            torch.cuda.synchronize()
+            s = t.stats()
+        finally:
+            t.set_option(A.OPT_KERNEL_TIMING, 0)
+        assert (s.kernel_launches[A.K_PATH] == 1) == (check_kernel == "megakernel"), \
+            f"expected the {check_kernel} schedule, k_path launches {s.kernel_launches[A.K_PATH]}"
+        np.testing.assert_array_equal(acc2.cpu().numpy(), out)
+    return out, st, rtc
+
+
+def compare_crops(name, W, H, out, st, rtc, crops, prefill, what, origin=None):
+    """origin(x, y) -> row of `out` holding pixel (x, y) (default: the full frame, row-major)."""
+    sc, _ = scene_bundle(name)
+    for (x0, y0, w, h) in crops:
+        old = np.full((h, w, 4), prefill, dtype=np.float32)
+        ref, _ = oracle_scene(name).render(rtc, st, D.make_lights(sc), W, H, crop=(x0, y0, w, h), accum=old)
+        if origin is None:
+            got = out.reshape(H, W, 4)[y0:y0 + h, x0:x0 + w]
+        else:
+            rows = np.array([[origin(x, y) for x in range(x0, x0 + w)] for y in range(y0, y0 + h)])
+            got = out[rows]
+        assert_parity(got, ref, f"{what} crop {(x0, y0, w, h)}")
+
+
+@pytest.mark.parametrize("sample,prefill", [(0, 0.0), (7, 0.375)])
+def test_metric_frame_1080p_L3(torch_cuda, sample, prefill):
+    # BASELINE.json metric: Sponza(-proxy) 1920x1080 MaxPathLength 3, the bench's kernel configuration
+    W, H = 1920, 1080
+    out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 3, sample, prefill, check_kernel="megakernel")
+    assert np.isfinite(out).all() and (out[:, 3] == 1.0).all()
+    compare_crops("sponza", W, H, out, st, rtc, frame_crops(W, H, [SKY["sponza"]]), prefill, f"metric s{sample}")
+
+
+def test_suntemple_1080p_L3(torch_cuda):
+    # BASELINE.json configs[3]: alpha-tested foliage through the megakernel's any-hit paths
+    W, H = 1920, 1080
+    out, st, rtc = render_shipped(torch_cuda, "suntemple", W, H, 3, 1, check_kernel="megakernel")
+    compare_crops("suntemple", W, H, out, st, rtc, frame_crops(W, H, [(800, 400, 96, 96), (1200, 600, 96, 64)]), 0.0,
+                  "C4")
+
+
+def test_sponza_720p_L3(torch_cuda):
+    # BASELINE.json configs[1]
+    W, H = 1280, 720
+    out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 3, 3, check_kernel="megakernel")
+    compare_crops("sponza", W, H, out, st, rtc, frame_crops(W, H), 0.0, "C2")
+
+
+def test_sponza_1080p_L8_wavefront(torch_cuda):
+    # BASELINE.json configs[2]: 2.07M paths x 7 vertices > 10M -> the default wavefront schedule
+    W, H = 1920, 1080
+    out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 8, 15, 0.125, check_kernel="wavefront")
+    compare_crops("sponza", W, H, out, st, rtc, frame_crops(W, H), 0.125, "C3 s15")
+
+
+def test_partial_last_wave_frame(torch_cuda):
+    # 1366 x 767 = 1,047,722 paths = 16,370 full waves + 42 paths: the last wave is partial
+    W, H = 1366, 767
+    assert (W * H) % 64 == 42
+    out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 3, 5, check_kernel="megakernel")
+    compare_crops("sponza", W, H, out, st, rtc, frame_crops(W, H), 0.0, "1366x767")
+
+
+@pytest.mark.parametrize("world,rank", [(8, 7), (2, 1)])
+def test_gpu_share_of_metric_frame(torch_cuda, world, rank):
+    # one rank's band share of the metric frame (what each GPU renders in bench.py --gpus N)
+    W, H = 1920, 1080
+    lay = band_layout(W, H, world)
+    tiles = lay.rank_tiles(rank)
+    out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 3, 2, tiles=tiles, n_out=lay.counts[rank],
+                                  check_kernel="megakernel")
+    where = {}
+    for t in tiles:
+        for yy in range(t.h):
+            where[t.y0 + yy] = (t.x0, t.accum_offset + yy * t.accum_pitch)
+    rows = sorted(where)
+    # crops inside the rank's rows: first band's corners, a middle band, the last band
+    mid = rows[len(rows) // 2]
+    crops = [(0, rows[0], 64, 1), (W - 64, rows[0], 64, 1), (W // 2, mid, 128, 1), (0, rows[-1], W, 1),
+             (1000, rows[-8], 64, 1), (300, rows[3], 200, 1)]
+    compare_crops("sponza", W, H, out, st, rtc, crops, 0.0, f"share {rank}/{world}",
+                  origin=lambda x, y: where[y][1] + (x - where[y][0]))
