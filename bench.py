@@ -59,12 +59,35 @@ def cpu_model():
     return None
 
 
+def usable_cpus():
+    """(threads to use, detail): the CPUs this process may run on -- its affinity mask, capped by a
+    cgroup v2 CPU quota (cpu.max) when one is set (a GPU box grants a job a share of the host)."""
+    host = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = host
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    n = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    return n, {"host_cpus": host, "affinity_cpus": aff, "cgroup_cpu_quota": quota}
+
+
 def cpu_baseline(scene, sky, settings, threads):
     """The CPU oracle (scalar C++ restatement, own BVH) on a bounded sample: one full 1920x1080 L=3
-    frame at CurrSampleIdx 0 on `threads` host threads, plus a single-thread figure on a 1920x68 band
-    of the same frame."""
+    frame at CurrSampleIdx 0 on `threads` host threads (default: every CPU the process may use, one
+    worker per core as SURVEY.md 8(d) asks), plus a single-thread figure on a 1920x68 band of the
+    same frame."""
     import dxrpathtracer_amd as D
     from oracle import pyoracle as O
+    cpus = usable_cpus()
+    if threads <= 0:
+        threads = cpus[0]
     orc = O.OracleScene(scene, sky)
     rtc = D.make_constants(scene, settings, sky, WIDTH, HEIGHT, 0)
     lights = D.make_lights(scene)
@@ -83,7 +106,7 @@ def cpu_baseline(scene, sky, settings, threads):
             "frame_s": round(dt, 3),
             "single_thread_Mrays_s": round(band[2] * band[3] * per_px / dt1 / 1e6, 3),
             "single_thread_sample": f"{band[2]}x{band[3]} band at rows {band[1]}..{band[1] + band[3] - 1}, {dt1:.2f} s",
-            "cpu_model": cpu_model(), "host_cpus": os.cpu_count()}
+            "cpu_model": cpu_model(), **cpus[1]}
 
 
 def pmc_traffic(kernel):
@@ -106,7 +129,7 @@ def main():
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: every usable CPU)")
     ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
     args = ap.parse_args()
     global SCENE, WIDTH, HEIGHT, PATH_LENGTH
@@ -231,9 +254,12 @@ def main():
                          + census.node_visits_radiance * bvh.node_bytes + census.tri_tests_radiance * bvh.tri_bytes)
     shadow_bytes_frame = (census.shadow_rays * SHADOW_IN_BYTES
                           + census.node_visits_shadow * bvh.node_bytes + census.tri_tests_shadow * bvh.tri_bytes)
-    # k_path (the whole frame in one launch): every ray's traversal bytes + the accumulation RMW; the
-    # shading gathers are not counted, so it is a lower bound
-    path_bytes_frame = trace_bytes_frame + shadow_bytes_frame + ACCUM_BYTES * n_local
+    # k_path (the whole frame in one launch, rays and path state in registers): the node and triangle
+    # FETCHES its census counted (per lane in the per-lane traversals, once per wave in the packet
+    # traversals) + the accumulation RMW; the shading gathers are not counted, so it is a lower bound
+    fetch_bytes_frame = ((census.node_visits_radiance + census.node_visits_shadow) * bvh.node_bytes
+                         + (census.tri_tests_radiance + census.tri_tests_shadow) * bvh.tri_bytes)
+    path_bytes_frame = fetch_bytes_frame + ACCUM_BYTES * n_local
     roof_bytes = {"k_trace": trace_bytes_frame / launches_per_frame, "k_shadow": shadow_bytes_frame / launches_per_frame,
                   "k_path": path_bytes_frame}[roof_kernel]
     achieved = roof_bytes / (roof_ms_avg * 1e-3) / 1e9
@@ -268,7 +294,7 @@ def main():
                     "absent from the reference snapshot)",
             "config": {"workload": f"{SCENE}-proxy {WIDTH}x{HEIGHT} L={PATH_LENGTH} 1spp/frame progressive",
                        "width": WIDTH, "height": HEIGHT, "max_path_length": PATH_LENGTH,
-                       "sqrt_num_samples": 4, "triangles": scene.num_triangles,
+                       "sqrt_num_samples": 4, "triangles": scene.num_triangles, "sky": sky.model,
                        "parallelism": f"screen bands x{world}" + (" + RCCL gather" if world > 1 else "")},
             "roofline": {"bound": "hbm", "kernel": roof_kernel, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -276,10 +302,13 @@ def main():
                          "avg_launch_ms": round(roof_ms_avg, 4), "traffic_source": traffic_src,
                          "traffic_kernel": pmc.get("kernel"), "l2_hit_rate": pmc.get("l2_hit_rate")},
             "cpu_baseline": cpu,
+            # the headline counts the reference's HUD rays (W*H*(1+2(L-1)) per frame); the kernels skip
+            # shadow rays whose pending contribution is exactly 0 (identical image), so fewer are traced:
+            "nominal_rays_per_frame": nominal_per_frame,
+            "counted_rays_per_frame": int(stats.radiance_rays + stats.shadow_rays),
+            "counted_Mrays_s": round((stats.radiance_rays + stats.shadow_rays) * args.steps / elapsed / 1e6, 2)
+            if world == 1 else None,
             "detail": {
-                "counted_rays_per_frame": int(stats.radiance_rays + stats.shadow_rays),
-                "counted_Mrays_s": round((stats.radiance_rays + stats.shadow_rays) * world * args.steps / elapsed / 1e6, 2)
-                if world == 1 else None,
                 "kernel_ms_per_frame": {k: round(v / frames, 4) for k, v in kms.items()},
                 "dominant_kernel": dominant,
                 "roofline_other": {"kernel": other, "bytes_per_launch": int(other_bytes),
@@ -292,10 +321,18 @@ def main():
                 "kernel_breakdown_note": "kernel_ms_per_frame from a separate all-kernel event pass before the timed region",
                 "frame_ms": {"mean": round(float(frame_ms.mean()), 4), "median": round(float(np.median(frame_ms)), 4),
                              "max": round(float(frame_ms.max()), 4)},
-                "nodes_per_radiance_ray": round(census.node_visits_radiance / max(1, census.radiance_rays), 2),
-                "tris_per_radiance_ray": round(census.tri_tests_radiance / max(1, census.radiance_rays), 2),
-                "tris_per_shadow_ray": round(census.tri_tests_shadow / max(1, census.shadow_rays), 2),
-                "nodes_per_shadow_ray": round(census.node_visits_shadow / max(1, census.shadow_rays), 2),
+                "census": {"what": "node / triangle-record fetches of the timed schedule (per lane in per-lane "
+                                   "traversals, per wave in packet traversals), one instrumented frame",
+                           "node_fetches_radiance": int(census.node_visits_radiance),
+                           "tri_fetches_radiance": int(census.tri_tests_radiance),
+                           "node_fetches_shadow": int(census.node_visits_shadow),
+                           "tri_fetches_shadow": int(census.tri_tests_shadow),
+                           "node_bytes": int(bvh.node_bytes), "tri_bytes": int(bvh.tri_bytes),
+                           "accum_bytes_per_pixel": ACCUM_BYTES, "pixels": int(n_local)},
+                "node_fetches_per_radiance_ray": round(census.node_visits_radiance / max(1, census.radiance_rays), 2),
+                "tri_fetches_per_radiance_ray": round(census.tri_tests_radiance / max(1, census.radiance_rays), 2),
+                "node_fetches_per_shadow_ray": round(census.node_visits_shadow / max(1, census.shadow_rays), 2),
+                "tri_fetches_per_shadow_ray": round(census.tri_tests_shadow / max(1, census.shadow_rays), 2),
                 "bvh": {"nodes": bvh.num_nodes, "max_depth": bvh.max_depth, "build_ms": round(bvh.build_ms, 1),
                         "sah": round(bvh.sah_cost, 2)},
                 "setup_s": round(setup_s, 2),

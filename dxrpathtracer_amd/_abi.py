@@ -10,6 +10,9 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "lib")
+# libdxrpt.so from another directory (A/B of kernel builds, scripts/ab_builds.sh); the host library
+# always comes from LIB_DIR
+KERNEL_LIB_DIR = os.environ.get("DXRPT_KERNEL_LIB_DIR") or LIB_DIR
 
 u32 = C.c_uint32
 i32 = C.c_int32
@@ -151,8 +154,8 @@ _lib = None
 _host = None
 
 
-def _load(name: str) -> C.CDLL:
-    path = os.path.join(LIB_DIR, name)
+def _load(name: str, where: str = LIB_DIR) -> C.CDLL:
+    path = os.path.join(where, name)
     if not os.path.exists(path):
         raise ImportError(f"{path} is missing: build it with `make -C dxrpathtracer_amd/csrc` "
                           f"(or __graft_entry__.build()); there is no fallback implementation")
@@ -163,7 +166,7 @@ def lib() -> C.CDLL:
     """libdxrpt.so: the HIP path tracer (fails loudly if not built)."""
     global _lib
     if _lib is None:
-        L = _load("libdxrpt.so")
+        L = _load("libdxrpt.so", KERNEL_LIB_DIR)
         P = C.c_void_p
         L.dxrpt_abi_version.restype = C.c_int
         L.dxrpt_default_settings.argtypes = [C.POINTER(AppSettings)]

@@ -749,8 +749,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // (path vertices = paths x (L-1); measured crossover ~10M: the megakernel wins on 1080p L=3 and on
         // every GPU's share of an 8-GPU frame, the wavefront on 4K L=6 and 1080p L=8 full frames)
         const uint64_t vertices = uint64_t(paths) * uint64_t((settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength) - 1);
-        fp.megakernel = (vertices <= ctx->opt_mega_paths && ctx->built_width == 8 && !ctx->opt_count &&
-                         ctx->opt_trav_mode == 0) ? 1u : 0u;
+        fp.megakernel = (vertices <= ctx->opt_mega_paths && ctx->built_width == 8 && ctx->opt_trav_mode == 0) ? 1u : 0u;
         // register budget by frame size (measured, Sponza proxy 1080p L=3 and its 1/2, 1/4, 1/8 shares):
         // more resident waves hide more latency once a frame has waves for several rounds; a GPU's 1/8
         // share (~4k waves) fits in one round at 4 waves/SIMD without spills

@@ -65,6 +65,31 @@ struct Texel4 {
     float r, g, b, a;
 };
 
+// DXRPT_LDS_LUT: the 512-entry decode table (unorm, sRGB) is copied to the workgroup's LDS at kernel
+// start (lut_fill), so a texel's decode is an LDS read instead of a dependent global-memory gather.
+// Every kernel that samples textures (shading, alpha-tested traversal) calls lut_fill first.
+#ifndef DXRPT_LDS_LUT
+#define DXRPT_LDS_LUT 1
+#endif
+#if DXRPT_LDS_LUT
+__shared__ float g_lut[512];
+#endif
+
+PT_DEV void lut_fill(const SceneDev& S) {
+#if DXRPT_LDS_LUT
+    for (uint32_t i = threadIdx.x; i < 512u; i += blockDim.x) g_lut[i] = S.lut[i];
+    __syncthreads();
+#endif
+}
+
+PT_DEV float lut_at(const SceneDev& S, uint32_t i) {
+#if DXRPT_LDS_LUT
+    return g_lut[i];
+#else
+    return S.lut[i];
+#endif
+}
+
 PT_DEV Texel4 fetch_texel(const SceneDev& S, const TexDesc& td, int x, int y) {
     const bool r8 = td.fmt == DXRPT_TEX_R8_UNORM;
     const uint32_t tiles_x = (td.width + (r8 ? kTexTileW8 : kTexTileW32) - 1u) / (r8 ? kTexTileW8 : kTexTileW32);
@@ -72,15 +97,15 @@ PT_DEV Texel4 fetch_texel(const SceneDev& S, const TexDesc& td, int x, int y) {
     Texel4 t;
     if (r8) {
         uint32_t w = S.texels[td.offset + word];
-        float v = S.lut[(w >> ((uint32_t(x) & 3u) * 8u)) & 0xFFu];
+        float v = lut_at(S, (w >> ((uint32_t(x) & 3u) * 8u)) & 0xFFu);
         t.r = v; t.g = v; t.b = v; t.a = 1.0f;
     } else {
         uint32_t w = S.texels[td.offset + word];
-        const float* l = S.lut + (td.fmt == DXRPT_TEX_RGBA8_SRGB ? 256 : 0);
-        t.r = l[w & 0xFFu];
-        t.g = l[(w >> 8) & 0xFFu];
-        t.b = l[(w >> 16) & 0xFFu];
-        t.a = S.lut[w >> 24];
+        const uint32_t l = td.fmt == DXRPT_TEX_RGBA8_SRGB ? 256u : 0u;
+        t.r = lut_at(S, l + (w & 0xFFu));
+        t.g = lut_at(S, l + ((w >> 8) & 0xFFu));
+        t.b = lut_at(S, l + ((w >> 16) & 0xFFu));
+        t.a = lut_at(S, w >> 24);
     }
     return t;
 }
@@ -220,16 +245,33 @@ struct TriRec {
     float4 p0, p1, p2;
 };
 
-PT_DEV TriRec load_tri(const SceneDev& S, uint32_t rec) {
-    const float4* T = reinterpret_cast<const float4*>(S.tris);
-    return TriRec{T[rec * 3 + 0], T[rec * 3 + 1], T[rec * 3 + 2]};
-}
-
 // Keeps a loaded record in registers at this point: the compiler otherwise sinks the v0 load behind
 // the det != 0 branch, which costs a second dependent round trip per triangle.
 PT_DEV void pin_tri(const TriRec& r) {
     asm volatile("" ::"v"(r.p0.x), "v"(r.p0.y), "v"(r.p0.z), "v"(r.p0.w), "v"(r.p1.x), "v"(r.p1.y), "v"(r.p1.z),
                  "v"(r.p1.w), "v"(r.p2.x), "v"(r.p2.y), "v"(r.p2.z), "v"(r.p2.w));
+}
+
+// DXRPT_PIN_LOADS: a record's words come from one 64-bit base address (immediate offsets) and are
+// all in registers before the first test uses them -- one memory round trip per record.
+#ifndef DXRPT_PIN_LOADS
+#define DXRPT_PIN_LOADS 1
+#endif
+
+PT_DEV TriRec load_tri_raw(const SceneDev& S, uint32_t rec) {
+    const float4* T = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(S.tris) + size_t(rec) * 48u);
+    return TriRec{T[0], T[1], T[2]};
+}
+
+PT_DEV TriRec load_tri(const SceneDev& S, uint32_t rec) {
+#if DXRPT_PIN_LOADS
+    const TriRec r = load_tri_raw(S, rec);
+    pin_tri(r);
+    return r;
+#else
+    const float4* T = reinterpret_cast<const float4*>(S.tris);
+    return TriRec{T[rec * 3 + 0], T[rec * 3 + 1], T[rec * 3 + 2]};
+#endif
 }
 
 template <bool kAnyHit>
@@ -385,8 +427,18 @@ struct NodeCache {
 };
 
 PT_DEV Node8Words load_node8(const SceneDev& S, uint32_t node) {
+#if DXRPT_PIN_LOADS
+    const uint4* N = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(S.nodes8) + size_t(node) * 80u);
+    const Node8Words w{N[0], N[1], N[2], N[3], N[4]};
+    // the leaf metadata (w1.zw) is otherwise loaded behind the leaf-hit branch: a second round trip
+    asm volatile("" ::"v"(w.w0.x), "v"(w.w0.y), "v"(w.w0.z), "v"(w.w0.w), "v"(w.w1.x), "v"(w.w1.y), "v"(w.w1.z),
+                 "v"(w.w1.w), "v"(w.w2.x), "v"(w.w2.y), "v"(w.w2.z), "v"(w.w2.w), "v"(w.w3.x), "v"(w.w3.y),
+                 "v"(w.w3.z), "v"(w.w3.w), "v"(w.w4.x), "v"(w.w4.y), "v"(w.w4.z), "v"(w.w4.w));
+    return w;
+#else
     const uint4* N = reinterpret_cast<const uint4*>(S.nodes8);
     return Node8Words{N[node * 5 + 0], N[node * 5 + 1], N[node * 5 + 2], N[node * 5 + 3], N[node * 5 + 4]};
+#endif
 }
 
 PT_DEV Node8Words load_node8(const SceneDev& S, const NodeCache& nc, uint32_t node) {
@@ -518,8 +570,8 @@ PT_DEV bool trav8_tris2(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32
         const bool two = tbits != 0u;
         const uint32_t b1 = two ? uint32_t(__builtin_ctz(tbits)) : b0;
         tbits &= tbits - 1u;
-        const TriRec ra = load_tri(S, tbase + b0);
-        const TriRec rb = load_tri(S, tbase + b1);
+        const TriRec ra = load_tri_raw(S, tbase + b0);
+        const TriRec rb = load_tri_raw(S, tbase + b1);
         pin_tri(ra);
         pin_tri(rb);
         if (kCount) ntest += two ? 2u : 1u;
@@ -607,9 +659,11 @@ constexpr uint32_t kSwitchMinVisits = 4;
 template <bool kAnyHit>
 PT_DEV bool traverse8_from(const SceneDev& S, const Ray8& R, lds_int* stk, HitRec& h);
 
-template <bool kAnyHit>
+// kCount: node / triangle FETCHES are counted in *cnt (cnt[0] nodes, cnt[1] triangles) by the wave's
+// first live lane -- a packet fetches each node and triangle once per wave (scalar loads).
+template <bool kAnyHit, bool kCount = false>
 PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, bool live, HitRec& h,
-                             uint32_t switch_pct = 0u, lds_int* stk = nullptr) {
+                             uint32_t switch_pct = 0u, lds_int* stk = nullptr, uint32_t* cnt = nullptr) {
     Ray8 R;
     ray8_init(R, o, d, tmin, tmax, alpha, h);
     unsigned long long lv = __ballot(live);
@@ -618,11 +672,13 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
     // key order of the first live lane's octant for the whole wave (any order gives the same results)
     const uint32_t oct = uint32_t(__builtin_amdgcn_readlane(int(R.oct), __ffsll(static_cast<long long>(lv)) - 1));
     const uint32_t lane = uint32_t(__lane_id());
+    const bool counter = kCount && lane == uint32_t(__ffsll(static_cast<long long>(lv)) - 1);
     uint32_t sbase = 0, sword = 0;  // stack entry j in lane j
     uint32_t sp = 0;
     uint32_t node = 0;
     while (true) {
         const Node8Words W = load_node8_uniform(S, node);
+        if (counter) ++cnt[0];
         const uint32_t hm = live ? box8_hits(R, W, h.t) : 0u;
         const uint32_t um = wave_or8(hm);
         if (switch_pct) {
@@ -650,6 +706,7 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
             const uint32_t b = uint32_t(__builtin_ctz(tbits));
             tbits &= tbits - 1u;
             const TriRec r = load_tri_uniform(S, tbase + b);
+            if (counter) ++cnt[1];
             if (live && test_tri_rec<kAnyHit>(S, r, R.o, R.d, R.tmin, R.tmax, R.alpha, h)) live = false;  // occluded
         }
         if (kAnyHit && __ballot(live) == 0ull) break;
@@ -942,6 +999,7 @@ __global__ __launch_bounds__(kBlock) void k_raygen(KArgs A) {
 template <bool kCount, int W, int kOcc, int kPipe = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
 void k_trace(KArgs A, int depth) {
+    lut_fill(A.S);
     extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved, then the node cache
     NodeCache nc{nullptr, 0u};
     if (W == 8 && !kCount && (kPipe & 4))  // LDS node cache: a separate instantiation, so that the
@@ -982,9 +1040,12 @@ PT_DEV void emit_shadow(const KArgs& A, uint32_t pos, uint32_t& n, f3 o, f3 d, f
 
 PT_DEV bool nonzero3(f3 c) { return !(c.x == 0.0f && c.y == 0.0f && c.z == 0.0f); }
 
+// Shadow ray kinds, in the order a vertex emits them (RayTrace.hlsl:224-262, 265-313, 415-425).
+constexpr int kShadowSun = 0, kShadowSpot = 1, kShadowSky = 2;
+
 // One path vertex: MissShader (RayTrace.hlsl:509-530) or ClosestHitShader -> PathTrace (151-441) for the
 // ray (inOrigin, inDir) of path depth `depth` with hit record `hit` (b1, b2, tri, geom).  Shadow rays
-// go to emit(origin, dir, tmin, tmax, pending contribution = pathThr * CalcLighting (or sky *
+// go to emit(kind, origin, dir, tmin, tmax, pending contribution = pathThr * CalcLighting (or sky *
 // throughput), force_opaque) in the reference's order (sun, spot lights, final sky visibility); the
 // local radiance and the continuation come back in O.  Shared by k_shade (wavefront: emit queues the
 // shadow ray) and k_path (megakernel: emit traces it at once).
@@ -1091,7 +1152,7 @@ PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emi
             const f3 c = calc_lighting(normalWS, sunDirection, f3{rtc.SunIrradiance[0], rtc.SunIrradiance[1], rtc.SunIrradiance[2]},
                                        diffuseAlbedo, specularAlbedo, roughness, positionWS, inOrigin, msEC);
             if (nonzero3(c))
-                emit(positionWS, D, kRayTMin, kFP32Max, mul(pathThr, c), shadowOpaque);
+                emit(kShadowSun, positionWS, D, kRayTMin, kFP32Max, mul(pathThr, c), shadowOpaque);
         }
         // Spot lights (RayTrace.hlsl:265-313)
         if (set.RenderLights && !furnace && !directZero) {
@@ -1112,7 +1173,7 @@ PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emi
                     const f3 c = calc_lighting(normalWS, surfaceToLight, intensity, diffuseAlbedo, specularAlbedo, roughness,
                                                positionWS, inOrigin, msEC);
                     if (nonzero3(c))
-                        emit(add(positionWS, scl(normalWS, 0.01f)), surfaceToLight, kSpotShadowNearClip,
+                        emit(kShadowSpot, add(positionWS, scl(normalWS, 0.01f)), surfaceToLight, kSpotShadowNearClip,
                                     distanceToLight - kSpotShadowNearClip, mul(pathThr, c), shadowOpaque);
                 }
             }
@@ -1163,7 +1224,7 @@ PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emi
             const f3 sky = set.EnableSky ? sample_sky(A.S, rayDirWS) : f3{0.0f, 0.0f, 0.0f};
             const f3 c = mul(sky, throughput);
             if (nonzero3(c))
-                emit(positionWS, rayDirWS, kRayTMin, kFP32Max, mul(pathThr, c),
+                emit(kShadowSky, positionWS, rayDirWS, kRayTMin, kFP32Max, mul(pathThr, c),
                             depth + 1 > set.MaxAnyHitPathLength);
         }
     } while (false);
@@ -1174,6 +1235,7 @@ PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emi
 template <int kOcc>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
 void k_shade(KArgs A, int depth) {
+    lut_fill(A.S);
     const uint32_t* cnt = radiance_counts(A.F, depth);
     const uint32_t nq = queue_total(cnt);
     const bool xcd = A.P.xcd_map != 0u;
@@ -1199,7 +1261,7 @@ void k_shade(KArgs A, int depth) {
     V.pix = Q.pix[pos];
     V.hit = A.F.hit[pos];
     VertexOut O;
-    path_vertex(A, depth, V, [&](f3 o, f3 d, float tmin, float tmax, f3 c, bool fo) {
+    path_vertex(A, depth, V, [&](int, f3 o, f3 d, float tmin, float tmax, f3 c, bool fo) {
         emit_shadow(A, pos, nsh, o, d, tmin, tmax, c, fo);
     }, O);
     const f3 local = O.local;
@@ -1259,6 +1321,7 @@ void k_shade(KArgs A, int depth) {
 template <bool kCount, int W, int kOcc, int kPipe = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
 void k_shadow(KArgs A, int depth) {
+    lut_fill(A.S);
     extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved, then the node cache
     NodeCache nc{nullptr, 0u};
     if (W == 8 && !kCount && (kPipe & 4))  // LDS node cache: a separate instantiation, so that the
@@ -1292,6 +1355,7 @@ void k_shadow(KArgs A, int depth) {
 template <int kOcc>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
 void k_trace_packet(KArgs A, int depth) {
+    lut_fill(A.S);
     const uint32_t* cnt = radiance_counts(A.F, depth);
     const uint32_t n = queue_total(cnt);
     uint32_t i, lw;
@@ -1314,6 +1378,7 @@ void k_trace_packet(KArgs A, int depth) {
 template <int kOcc>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
 void k_shadow_packet(KArgs A, int depth) {
+    lut_fill(A.S);
     const uint32_t* cnt = shadow_counts(A.F, depth);
     const uint32_t n = queue_total(cnt);
     uint32_t i, lw;
@@ -1363,6 +1428,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(KArgs A, int depth) {
 // grid covers the queue; the dispatcher balances waves across CUs.  No atomics.
 template <bool kCount, bool kShadow>
 __global__ __launch_bounds__(kBlock) void k_traverse8p(KArgs A, int depth) {
+    lut_fill(A.S);
     extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved (launch_lds_bytes)
     lds_int* stk = lane_stack(A.S, stack);
     const uint32_t* cnt = kShadow ? shadow_counts(A.F, depth) : radiance_counts(A.F, depth);
@@ -1504,6 +1570,12 @@ PT_DEV void count_rays(uint32_t* counters, uint32_t n) {
     if (lane == leader && total) atomicAdd(&counters[shard], total);
 }
 
+// DXRPT_SHADOW_MODE 0: every shadow ray of a vertex goes through the per-slot buffers (global memory)
+// and the wave walks the slots; 1: the sun and sky-visibility rays stay in registers.
+#ifndef DXRPT_SHADOW_MODE
+#define DXRPT_SHADOW_MODE 0
+#endif
+
 // One path from its first ray (PathLength 1) to its end: per depth the closest hit, path_vertex and
 // the vertex's shadow rays in slot order -- the megakernel's per-thread loop, shared by k_path (camera
 // paths) and k_bake (lightmap texels).  `slot_p` (< F.qsize) indexes the per-slot shadow buffers, `pix`
@@ -1511,13 +1583,17 @@ PT_DEV void count_rays(uint32_t* counters, uint32_t n) {
 // / the depth-1 sun shadow rays (all lanes must be active at depth 1 then).  Returns the radiance.
 // kBake: the first ray is BakeRayGen's (TMin 0.0001, IsDiffuse, no packets) instead of RaygenShader's.
 // nc: the workgroup's LDS copy of the top BVH8 nodes for the per-lane traversals (n = 0: none).
-template <bool kBake>
+// kCount: census of the traversal work (cnt[0..1] closest-hit node / triangle fetches, cnt[2..3] any
+// hit; per-lane traversals fetch per lane, packet traversals once per wave).
+template <bool kBake, bool kCount = false>
 PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, f3 dir, float tmax, lds_int* stk,
-                         uint32_t packet_mask, const NodeCache& nc = NodeCache{nullptr, 0u}) {
+                         uint32_t packet_mask, const NodeCache& nc = NodeCache{nullptr, 0u}, uint32_t* cnt = nullptr) {
     const dxrpt_app_settings& set = A.P.set;
     const float tmin1 = kBake ? 0.0001f : 0.0f;
     const bool isDiffuse1 = kBake;
     const uint32_t packet = kBake ? 0u : packet_mask;
+    uint32_t unused[4] = {0u, 0u, 0u, 0u};
+    if (!kCount) cnt = unused;
     f3 thr = f3{1.0f, 1.0f, 1.0f};
     float payloadRoughness = 0.0f;
     bool payloadIsDiffuse = isDiffuse1;
@@ -1526,11 +1602,11 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
     for (int d = 1; d <= L - 1; ++d) {
         count_rays(A.F.counters + uint32_t(d) * kQueueShards, 1u);
         HitRec h;
-        uint32_t nv = 0, nt = 0;
         if (d == 1 && (packet & 1u))  // coherent primary rays: wave-coherent traversal (same results)
-            traverse8_packet<false>(A.S, org, dir, tmin1, tmax, d <= set.MaxAnyHitPathLength, true, h);
+            traverse8_packet<false, kCount>(A.S, org, dir, tmin1, tmax, d <= set.MaxAnyHitPathLength, true, h, 0u, nullptr, cnt);
         else
-            traverse<8, false, false>(A.S, org, dir, d == 1 ? tmin1 : kRayTMin, tmax, d <= set.MaxAnyHitPathLength, stk, h, nv, nt, nc);
+            traverse<8, false, kCount>(A.S, org, dir, d == 1 ? tmin1 : kRayTMin, tmax, d <= set.MaxAnyHitPathLength, stk, h,
+                                       cnt[0], cnt[1], nc);
         VertexIn V;
         V.inOrigin = org;
         V.inDir = dir;
@@ -1539,9 +1615,10 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
         V.payloadIsDiffuse = payloadIsDiffuse;
         V.pix = pix;
         V.hit = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
+#if DXRPT_SHADOW_MODE == 0
         VertexOut O;
         uint32_t nsh = 0;
-        path_vertex(A, d, V, [&](f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
+        path_vertex(A, d, V, [&](int, f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
             emit_shadow(A, slot_p, nsh, o, dd, tmn, tmx, c, fo);
         }, O);
         count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, nsh);
@@ -1563,15 +1640,81 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
             HitRec hs;
             bool occluded = false;
             if (d == 1 && k == 0 && (packet & 2u))
-                occluded = traverse8_packet<true>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live, hs);
+                occluded = traverse8_packet<true, kCount>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live, hs, 0u, nullptr, cnt + 2);
             else if (live)
-                occluded = traverse<8, true, false>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stk, hs, nv, nt, nc);
+                occluded = traverse<8, true, kCount>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stk, hs, cnt[2], cnt[3], nc);
             if (live) {
                 rad.x += occluded ? c4.x * 0.0f : c4.x;
                 rad.y += occluded ? c4.y * 0.0f : c4.y;
                 rad.z += occluded ? c4.z * 0.0f : c4.z;
             }
         }
+#else
+        VertexOut O;
+        // The vertex's sun and sky-visibility rays stay in registers: both start at the hit position
+        // with TMin 1e-5 / TMax FP32Max (RayTrace.hlsl:241-244, 415-425), the sun's direction is the
+        // wave-uniform SunDirectionWS, so a ray is its pending contribution (+ the sky direction).
+        // Spot-light rays (any number) go through the per-slot buffers.
+        uint32_t nsh = 0, nspot = 0;
+        bool hasSun = false, hasSky = false;
+        f3 cSun = f3{0.0f, 0.0f, 0.0f}, cSky = cSun, shOrg = cSun, skyDir = cSun;
+        path_vertex(A, d, V, [&](int kind, f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
+            ++nsh;
+            if (kind == kShadowSun) {
+                hasSun = true;
+                cSun = c;
+                shOrg = o;
+            } else if (kind == kShadowSky) {
+                hasSky = true;
+                cSky = c;
+                shOrg = o;
+                skyDir = dd;
+            } else {
+                emit_shadow(A, slot_p, nspot, o, dd, tmn, tmx, c, fo);
+            }
+        }, O);
+        count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, nsh);
+        rad.x += thr.x * O.local.x;
+        rad.y += thr.y * O.local.y;
+        rad.z += thr.z * O.local.z;
+        // ShadowHit/Miss/AnyHit: contribution * visibility, in the emission order (sun, spots, sky).
+        // At depth 1 (packet bit 1) the sun shadow rays of an 8x8 pixel block's primary hits -- one
+        // direction, nearby origins -- take the wave-coherent traversal.
+        const f3 sunD = f3{A.P.rtc.SunDirectionWS[0], A.P.rtc.SunDirectionWS[1], A.P.rtc.SunDirectionWS[2]};
+        const bool sunAlpha = !(d > set.MaxAnyHitPathLength), skyAlpha = !(d + 1 > set.MaxAnyHitPathLength);
+        if (__ballot(hasSun) != 0ull) {
+            HitRec hs;
+            bool occluded = false;
+            if (d == 1 && (packet & 2u))
+                occluded = traverse8_packet<true, kCount>(A.S, shOrg, sunD, kRayTMin, kFP32Max, sunAlpha, hasSun, hs, 0u, nullptr, cnt + 2);
+            else if (hasSun)
+                occluded = traverse<8, true, kCount>(A.S, shOrg, sunD, kRayTMin, kFP32Max, sunAlpha, stk, hs, cnt[2], cnt[3], nc);
+            if (hasSun) {
+                rad.x += occluded ? cSun.x * 0.0f : cSun.x;
+                rad.y += occluded ? cSun.y * 0.0f : cSun.y;
+                rad.z += occluded ? cSun.z * 0.0f : cSun.z;
+            }
+        }
+        for (uint32_t k = 0; __ballot(k < nspot) != 0ull; ++k) {
+            if (k < nspot) {
+                const size_t slot = size_t(k) * A.F.qsize + slot_p;
+                const float4 o4 = A.F.sh_org[slot], d4 = A.F.sh_dir[slot], c4 = A.F.sh_con[slot];
+                HitRec hs;
+                const bool occluded =
+                    traverse<8, true, kCount>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stk, hs, cnt[2], cnt[3], nc);
+                rad.x += occluded ? c4.x * 0.0f : c4.x;
+                rad.y += occluded ? c4.y * 0.0f : c4.y;
+                rad.z += occluded ? c4.z * 0.0f : c4.z;
+            }
+        }
+        if (hasSky) {
+            HitRec hs;
+            const bool occluded = traverse<8, true, kCount>(A.S, shOrg, skyDir, kRayTMin, kFP32Max, skyAlpha, stk, hs, cnt[2], cnt[3], nc);
+            rad.x += occluded ? cSky.x * 0.0f : cSky.x;
+            rad.y += occluded ? cSky.y * 0.0f : cSky.y;
+            rad.z += occluded ? cSky.z * 0.0f : cSky.z;
+        }
+#endif
         if (!O.cont) break;
         org = O.nextOrigin;
         dir = O.nextDir;
@@ -1656,7 +1799,7 @@ PT_DEV float4 trace_path_group(const KArgs& A, uint32_t slot_p, uint32_t pix, f3
         V.hit = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
         VertexOut O;
         uint32_t nsh = 0;
-        path_vertex(A, d, V, [&](f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
+        path_vertex(A, d, V, [&](int, f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
             emit_shadow(A, slot_p, nsh, o, dd, tmn, tmx, c, fo);
         }, O);
         count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, quiet ? 0u : nsh);
@@ -1732,10 +1875,12 @@ PT_DEV float4 trace_path_group(const KArgs& A, uint32_t slot_p, uint32_t pix, f3
 // Path p of a wave whose paths are 64-aligned (p & ~63 .. p | 63).  Packets need every lane of the wave
 // (the packet stack lives one entry per lane): a partial last wave (num_paths % 64 != 0) traverses one
 // ray per lane -- a wave-uniform scalar test, the other waves keep their packets (same results).
-PT_DEV void camera_path(const KArgs& A, uint32_t p, lds_int* stk, const NodeCache& nc = NodeCache{nullptr, 0u}) {
+template <bool kCount = false>
+PT_DEV void camera_path(const KArgs& A, uint32_t p, lds_int* stk, const NodeCache& nc = NodeCache{nullptr, 0u},
+                        uint32_t* cnt = nullptr) {
     const PrimaryRay pr = primary_ray(A, p);
     const uint32_t packet = (p | 63u) < A.P.num_paths ? A.P.packet : 0u;
-    const float4 rad = trace_path<false>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, packet, nc);
+    const float4 rad = trace_path<false, kCount>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, packet, nc, cnt);
     accumulate_pixel(A, pr.accumIdx, rad);
 }
 
@@ -1752,9 +1897,10 @@ PT_DEV void camera_path_group(const KArgs& A, uint32_t p, lds_int* stk, bool mem
 // every ray visits) behind the stacks; the per-lane traversals read those from LDS.
 // kGroup: path groups of 64 / A.P.mega_lanes lanes (its own instantiation, so the default kernel's
 // register allocation does not carry the group schedule).
-template <int kOcc, bool kPersistent, bool kLds = false, bool kGroup = false>
+template <int kOcc, bool kPersistent, bool kLds = false, bool kGroup = false, bool kCount = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
 void k_path(KArgs A) {
+    lut_fill(A.S);
     extern __shared__ int stack[];
     lds_int* stk = lane_stack(A.S, stack);
     if (kGroup) {  // mega_lanes paths per wave, each traced by 64 / mega_lanes lanes
@@ -1769,6 +1915,17 @@ void k_path(KArgs A) {
             const NodeCache nc = node_cache_fill(A.S, reinterpret_cast<uint4*>(stack + A.S.stack_ints * blockDim.x),
                                                  A.P.lds_nodes);
             if (p < A.P.num_paths) camera_path(A, p, stk, nc);
+            return;
+        }
+        if (kCount) {  // census (DXRPT_OPT_COUNT_TRAVERSAL): wave sums, one 64-bit atomic per counter per wave
+            uint32_t cnt[4] = {0u, 0u, 0u, 0u};
+            if (p < A.P.num_paths) camera_path<true>(A, p, stk, NodeCache{nullptr, 0u}, cnt);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint32_t v = cnt[k];
+                for (int off = 32; off > 0; off >>= 1) v += uint32_t(__shfl_xor(int(v), off));
+                if ((threadIdx.x & 63u) == 0u) atomicAdd(&A.P.trav[k], (unsigned long long)v);
+            }
             return;
         }
         if (p >= A.P.num_paths) return;
@@ -1798,6 +1955,7 @@ PT_DEV float luma(float3 c) { return (c.x * 0.299f + c.y * 0.587f) + c.z * 0.114
 template <int kOcc>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
 void k_bake(KArgs A, BakeArgs B) {
+    lut_fill(A.S);
     extern __shared__ int stack[];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= B.span || B.first + i >= *B.count) return;
@@ -1859,6 +2017,7 @@ void k_bake(KArgs A, BakeArgs B) {
 // bit1 = alpha test enabled (not FORCE_OPAQUE).
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_trace_rays(SceneDev S, const float4* rays, uint32_t n, uint32_t flags, float4* hits) {
+    lut_fill(S);
     extern __shared__ int stack[];  // S.stack_ints per lane, lane-interleaved (launch_lds_bytes)
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
@@ -1927,7 +2086,10 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
         const uint64_t threads = twins ? (uint64_t(fp.num_paths) + fp.mega_lanes - 1u) / fp.mega_lanes * 64u : fp.num_paths;
         const uint32_t gm = uint32_t((threads + tb - 1u) / tb);
         if (ev) (void)hipEventRecord(ev[0], stream);
-        if (fp.mega_persistent && tb == 64u) {
+        if (A.P.trav) {  // census frame (DXRPT_OPT_COUNT_TRAVERSAL): same schedule, counting instantiation
+            hipLaunchKernelGGL((k_path<7, false, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
+        }
+        else if (fp.mega_persistent && tb == 64u) {
             const uint32_t gp = std::min(gm, fp.mega_persistent * fp.num_cus);
             // the same register budgets as the non-persistent kernel (A/B at equal occupancy)
             if (fp.megakernel_occupancy >= 7) hipLaunchKernelGGL((k_path<7, true>), dim3(gp), dim3(tb), ldsm, stream, A);

@@ -203,7 +203,9 @@ typedef struct dxrpt_stats {
     uint64_t nominal_rays;             /* W*H*(1+2(L-1)) of the rendered pixels, DXRPathTracer.cpp:2171 */
     uint64_t radiance_rays_per_depth[DXRPT_MAX_PATH_LENGTH];
     uint64_t shadow_rays_per_depth[DXRPT_MAX_PATH_LENGTH];
-    /* DXRPT_OPT_COUNT_TRAVERSAL only (last render): BVH nodes visited / triangles tested */
+    /* DXRPT_OPT_COUNT_TRAVERSAL only (last render): BVH node and triangle-record FETCHES of the schedule
+       that ran -- one per lane per visit in per-lane traversals, one per wave per visit in the
+       wave-coherent packet traversals (scalar loads) */
     uint64_t node_visits_radiance, tri_tests_radiance, node_visits_shadow, tri_tests_shadow;
     /* DXRPT_OPT_KERNEL_TIMING only: summed kernel durations (ms) and launches since the last reset */
     double kernel_ms[DXRPT_K_COUNT];
@@ -259,7 +261,8 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx);
 int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 
 /* ---- options ---------------------------------------------------------------------------------- */
-#define DXRPT_OPT_COUNT_TRAVERSAL 1u  /* 1: instrumented kernels count node visits / triangle tests (slower) */
+#define DXRPT_OPT_COUNT_TRAVERSAL 1u  /* 1: instrumented kernels of the same schedule count node / triangle
+                                         fetches (slower; images identical) */
 #define DXRPT_OPT_KERNEL_TIMING 2u    /* 1: record a hipEvent after every launch of dxrpt_render */
 #define DXRPT_OPT_BVH_WIDTH 3u        /* 2 or 8 (default): layout built by the next dxrpt_build_bvh */
 #define DXRPT_OPT_TRAVERSAL_MODE 4u   /* BVH8: 0 = one thread per ray (default), 1 = wave pools with lane refill */

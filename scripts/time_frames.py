@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""ms/frame of the default (shipped) schedule on a BASELINE config, for A/B of kernel builds
+(DXRPT_KERNEL_LIB_DIR picks the libdxrpt.so).  Prints one line: label, median and mean ms/frame of
+`--rounds` x `--frames` frames (HIP events on the render stream), counted rays per frame.
+
+    python scripts/time_frames.py [--label x] [--config metric|c2|c3|c4|c5] [--share N --rank r]
+"""
+import argparse
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+CONFIGS = {"metric": ("sponza", 1920, 1080, 3), "c2": ("sponza", 1280, 720, 3), "c3": ("sponza", 1920, 1080, 8),
+           "c4": ("suntemple", 1920, 1080, 3), "c5": ("sponza", 3840, 2160, 6)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--label", default=os.environ.get("DXRPT_KERNEL_LIB_DIR", "default"))
+    ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
+    ap.add_argument("--frames", type=int, default=32)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--share", type=int, default=1)
+    ap.add_argument("--rank", type=int, default=0)
+    args = ap.parse_args()
+    import torch
+    import dxrpathtracer_amd as D
+    from dxrpathtracer_amd.distributed import band_layout
+    from dxrpathtracer_amd.tracer import DXRPathTracer
+
+    name, W, H, L = CONFIGS[args.config]
+    sc = D.Scene(name)
+    st = sc.settings(MaxPathLength=L)
+    sky = D.make_sky(st)
+    t = DXRPathTracer(0)
+    t.initialize_scene(sc, sky)
+    t.build_rt_acceleration_structure()
+    tiles, n = None, W * H
+    if args.share > 1:
+        lay = band_layout(W, H, args.share)
+        tiles, n = lay.rank_tiles(args.rank), lay.counts[args.rank]
+    acc = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
+    consts = [D.make_constants(sc, st, sky, W, H, s) for s in range(16)]
+    lights = D.make_lights(sc)
+    stream = torch.cuda.current_stream()
+    for f in range(5):
+        t.render_raw(consts[f % 16], st, acc.data_ptr(), W, H, tiles=tiles, stream=stream.cuda_stream, lights=lights)
+    torch.cuda.synchronize()
+    rounds = []
+    for r in range(args.rounds):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for f in range(args.frames):
+            t.render_raw(consts[f % 16], st, acc.data_ptr(), W, H, tiles=tiles, stream=stream.cuda_stream, lights=lights)
+        b.record(stream)
+        torch.cuda.synchronize()
+        rounds.append(a.elapsed_time(b) / args.frames)
+    s = t.stats()
+    print(f"{args.label:24s} {args.config} share 1/{args.share} r{args.rank}: median {statistics.median(rounds):.4f} "
+          f"mean {statistics.mean(rounds):.4f} min {min(rounds):.4f} ms/frame  rays {s.radiance_rays + s.shadow_rays}",
+          flush=True)
+    t.close()
+
+
+if __name__ == "__main__":
+    main()
