@@ -71,10 +71,10 @@ struct dxrpt_ctx {
     std::vector<dxrpt_material> mats;
     std::vector<TexDesc> texdesc;
     std::vector<uint32_t> texels;
-    bool scene_set = false, bvh_built = false, sky_set = false, tex_dirty = true;
+    bool scene_set = false, bvh_built = false, sky_set = false, tex_dirty = true, geoshade_dirty = true;
     uint32_t sky_res = 0;
     // device copies
-    DevBuf d_vertices, d_indices, d_geos, d_mats, d_texdesc, d_texels, d_sky, d_lut, d_nodes, d_nodes8, d_tris;
+    DevBuf d_vertices, d_indices, d_geos, d_mats, d_texdesc, d_texels, d_sky, d_lut, d_nodes, d_nodes8, d_tris, d_geoshade;
     DevBuf d_lights, d_tiles, d_tile_prefix;
     DevBuf p_bloom0, p_bloom1;  // post-processing scratch (RGBA16F half-res)
     DevBuf d_tri_verts;  // per global triangle: its 3 MeshVertex records (3 x 64 B), built with the BVH
@@ -138,7 +138,7 @@ struct dxrpt_ctx {
     double frame_ms = 0.0;
 
     ~dxrpt_ctx() {
-        DevBuf* all[] = {&d_vertices, &d_indices, &d_geos, &d_mats, &d_texdesc, &d_texels, &d_sky, &d_lut, &d_nodes,
+        DevBuf* all[] = {&d_vertices, &d_indices, &d_geos, &d_mats, &d_texdesc, &d_texels, &d_sky, &d_lut, &d_geoshade, &d_nodes,
                          &d_nodes8, &d_tris, &d_tri_verts, &d_lights, &d_tiles, &d_tile_prefix, &f_pix, &f_pxrad, &f_hit, &f_fwd,
                          &f_shn, &f_shq, &f_shorg, &f_shdir, &f_shcon, &f_counters, &p_bloom0, &p_bloom1};
         for (DevBuf* b : all) b->release();
@@ -220,6 +220,7 @@ SceneDev scene_dev(dxrpt_ctx* c, uint32_t traversal_threads) {
     s.geoinfo = c->d_geos.as<dxrpt_geometry_info>();
     s.materials = c->d_mats.as<dxrpt_material>();
     s.texdesc = c->d_texdesc.as<TexDesc>();
+    s.geoshade = c->d_geoshade.as<GeoShade>();
     s.texels = c->d_texels.as<uint32_t>();
     s.sky = c->d_sky.as<uint16_t>();
     s.lut = c->d_lut.as<float>();
@@ -228,11 +229,34 @@ SceneDev scene_dev(dxrpt_ctx* c, uint32_t traversal_threads) {
     return s;
 }
 
+// Uploads added textures and (re)builds the per-geometry shading records (pt_layout.h GeoShade):
+// GeometryInfo.MaterialIdx -> Material -> the texture descriptors, resolved once on the host.  A
+// material index that names no added texture resolves to "none" (the render path rejects such
+// materials before it launches; an opacity of DXRPT_INVALID_INDEX is the reference's "opaque").
 void upload_textures(dxrpt_ctx* c) {
-    if (!c->tex_dirty) return;
-    c->d_texdesc.upload(c->texdesc.data(), c->texdesc.size() * sizeof(TexDesc));
-    c->d_texels.upload(c->texels.data(), c->texels.size() * sizeof(uint32_t));
-    c->tex_dirty = false;
+    if (c->tex_dirty) {
+        c->d_texdesc.upload(c->texdesc.data(), c->texdesc.size() * sizeof(TexDesc));
+        c->d_texels.upload(c->texels.data(), c->texels.size() * sizeof(uint32_t));
+        c->tex_dirty = false;
+        c->geoshade_dirty = true;
+    }
+    if (!c->geoshade_dirty || c->geos.empty()) return;
+    auto ref = [&](uint32_t t) {
+        GeoTex g{0u, 0u};
+        if (t < c->texdesc.size()) {
+            const TexDesc& d = c->texdesc[t];
+            g.offset = d.offset;
+            g.whf = d.width | (d.height << 15) | (d.fmt << 30);
+        }
+        return g;
+    };
+    std::vector<GeoShade> gs(c->geos.size());
+    for (size_t g = 0; g < c->geos.size(); ++g) {
+        const dxrpt_material& m = c->mats[c->geos[g].MaterialIdx];
+        gs[g] = GeoShade{ref(m.Albedo), ref(m.Normal), ref(m.Roughness), ref(m.Metallic), ref(m.Emissive), ref(m.Opacity)};
+    }
+    c->d_geoshade.upload(gs.data(), gs.size() * sizeof(GeoShade));
+    c->geoshade_dirty = false;
 }
 
 void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
@@ -525,6 +549,7 @@ int dxrpt_set_scene(dxrpt_ctx* ctx, const dxrpt_mesh_vertex* vertices, uint32_t 
         ctx->d_indices.upload(ctx->indices.data(), ctx->indices.size() * 4);
         ctx->d_geos.upload(ctx->geos.data(), ctx->geos.size() * sizeof(dxrpt_geometry_info));
         ctx->d_mats.upload(ctx->mats.data(), ctx->mats.size() * sizeof(dxrpt_material));
+        ctx->geoshade_dirty = true;
         ctx->scene_set = true;
         ctx->bvh_built = false;
     });

@@ -91,6 +91,7 @@ struct SceneDev {
     const dxrpt_geometry_info* geoinfo = nullptr;
     const dxrpt_material* materials = nullptr;
     const TexDesc* texdesc = nullptr;
+    const GeoShade* geoshade = nullptr;  // per geometry: its material's textures, resolved
     const uint32_t* texels = nullptr;
     const uint16_t* sky = nullptr;
     const float* lut = nullptr;  // [0..255] unorm, [256..511] sRGB->linear

@@ -110,8 +110,22 @@ PT_DEV Texel4 fetch_texel(const SceneDev& S, const TexDesc& td, int x, int y) {
     return t;
 }
 
+PT_DEV Texel4 sample_tex_desc(const SceneDev& S, const TexDesc td, float u, float v);
+
 PT_DEV Texel4 sample_tex(const SceneDev& S, uint32_t texIdx, float u, float v) {
-    const TexDesc td = S.texdesc[texIdx];
+    return sample_tex_desc(S, S.texdesc[texIdx], u, v);
+}
+
+PT_DEV TexDesc tex_desc(GeoTex g) {
+    TexDesc td;
+    td.offset = g.offset;
+    td.width = g.whf & 0x7FFFu;
+    td.height = (g.whf >> 15) & 0x7FFFu;
+    td.fmt = g.whf >> 30;
+    return td;
+}
+
+PT_DEV Texel4 sample_tex_desc(const SceneDev& S, const TexDesc td, float u, float v) {
     float x = u * float(td.width) - 0.5f;
     float y = v * float(td.height) - 0.5f;
     float x0 = floorf(x), y0 = floorf(y);
@@ -198,9 +212,8 @@ PT_DEV Surface get_hit_surface(const SceneDev& S, uint32_t gtri, float b1, float
 
 // AnyHitShader / ShadowAnyHitShader (RayTrace.hlsl:485-507): opacity.x < 0.35 -> IgnoreHit.
 PT_DEV bool alpha_accepts(const SceneDev& S, uint32_t geom, uint32_t gtri, float b1, float b2) {
-    const dxrpt_geometry_info gi = S.geoinfo[geom];
-    const uint32_t opacity = S.materials[gi.MaterialIdx].Opacity;
-    if (opacity == DXRPT_INVALID_INDEX) return true;
+    const GeoTex opacity = S.geoshade[geom].opacity;
+    if (opacity.whf == 0u) return true;
     const float w0 = (1.0f - b1) - b2;
     const float2* V = reinterpret_cast<const float2*>(S.tri_verts + size_t(gtri) * 12u);
     float2 uv[3];
@@ -208,7 +221,7 @@ PT_DEV bool alpha_accepts(const SceneDev& S, uint32_t geom, uint32_t gtri, float
     for (int k = 0; k < 3; ++k) uv[k] = V[k * 8 + 3];  // float2 #3 of MeshVertex k = UV
     float u = bary_lerp(uv[0].x, uv[1].x, uv[2].x, w0, b1, b2);
     float v = bary_lerp(uv[0].y, uv[1].y, uv[2].y, w0, b1, b2);
-    return !(sample_tex(S, opacity, u, v).r < 0.35f);
+    return !(sample_tex_desc(S, tex_desc(opacity), u, v).r < 0.35f);
 }
 
 // ---- traversal ------------------------------------------------------------------------------------
@@ -1094,13 +1107,13 @@ PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emi
         if (depth > 1 && !set.EnableIndirect) break;
         const uint32_t geom = fbits(hit.w);
         const Surface surf = get_hit_surface(A.S, tri, hit.x, hit.y);
-        const dxrpt_material mat = A.S.materials[A.S.geoinfo[geom].MaterialIdx];
+        const GeoShade mat = A.S.geoshade[geom];  // GetGeometryMaterial (RayTrace.hlsl:467-474), resolved
         const f3 T = surf.t, Bt = surf.b;
         f3 Nrow = surf.n;
         const f3 positionWS = surf.pos;
         f3 normalWS = surf.n;
         if (set.EnableNormalMaps) {
-            Texel4 nm = sample_tex(A.S, mat.Normal, surf.u, surf.v);
+            Texel4 nm = sample_tex_desc(A.S, tex_desc(mat.normal), surf.u, surf.v);
             f3 nts;
             nts.x = nm.r * 2.0f - 1.0f;
             nts.y = nm.g * 2.0f - 1.0f;
@@ -1110,16 +1123,16 @@ PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emi
         }
         f3 baseColor = f3{1.0f, 1.0f, 1.0f};
         if (set.EnableAlbedoMaps && !furnace) {
-            Texel4 a = sample_tex(A.S, mat.Albedo, surf.u, surf.v);
+            Texel4 a = sample_tex_desc(A.S, tex_desc(mat.albedo), surf.u, surf.v);
             baseColor = f3{a.r, a.g, a.b};
         }
-        const float metallic = saturate((furnace ? 1.0f : sample_tex(A.S, mat.Metallic, surf.u, surf.v).r) * set.MetallicScale);
+        const float metallic = saturate((furnace ? 1.0f : sample_tex_desc(A.S, tex_desc(mat.metallic), surf.u, surf.v).r) * set.MetallicScale);
         const bool enableDiffuse = (set.EnableDiffuse && metallic < 1.0f) || furnace;
         const bool payloadIsDiffuse = V.payloadIsDiffuse;
         const bool enableSpecular =
             set.EnableSpecular && (set.EnableIndirectSpecular ? !(set.AvoidCausticPaths && payloadIsDiffuse) : (depth == 1));
         if (!enableDiffuse && !enableSpecular) break;
-        const float sqrtRoughness = saturate((furnace ? 1.0f : sample_tex(A.S, mat.Roughness, surf.u, surf.v).r) * set.RoughnessScale);
+        const float sqrtRoughness = saturate((furnace ? 1.0f : sample_tex_desc(A.S, tex_desc(mat.roughness), surf.u, surf.v).r) * set.RoughnessScale);
         const float dsel = enableDiffuse ? 1.0f : 0.0f, ssel = enableSpecular ? 1.0f : 0.0f;
         const f3 diffuseAlbedo = scl(f3{lerpf(baseColor.x, 0.0f, metallic), lerpf(baseColor.y, 0.0f, metallic), lerpf(baseColor.z, 0.0f, metallic)}, dsel);
         const f3 specularAlbedo = scl(f3{lerpf(0.03f, baseColor.x, metallic), lerpf(0.03f, baseColor.y, metallic), lerpf(0.03f, baseColor.z, metallic)}, ssel);
@@ -1132,7 +1145,7 @@ PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emi
             msEC = f3{1.0f + specularAlbedo.x * k, 1.0f + specularAlbedo.y * k, 1.0f + specularAlbedo.z * k};
         }
         if (!furnace) {
-            Texel4 em = sample_tex(A.S, mat.Emissive, surf.u, surf.v);
+            Texel4 em = sample_tex_desc(A.S, tex_desc(mat.emissive), surf.u, surf.v);
             O.local = f3{em.r, em.g, em.b};
         }
         const bool directZero = (depth == 1 && !set.EnableDirect);  // RayTrace.hlsl:385-386

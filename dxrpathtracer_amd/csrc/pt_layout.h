@@ -91,6 +91,21 @@ struct TexDesc {
     uint32_t fmt;
 };
 
+// A texture reference packed into 8 B: `offset` as in TexDesc, whf = width | height << 15 | fmt << 30
+// (width, height <= 32767); whf == 0: no texture.
+struct GeoTex {
+    uint32_t offset;
+    uint32_t whf;
+};
+
+// Per-geometry shading record, 48 B (three 16-B words): the geometry's material textures resolved
+// (GeometryInfo.MaterialIdx -> Material -> texture descriptors, RayTrace.hlsl:467-474, 497), so a hit
+// reaches its texels in two dependent loads (this record, then the texels) instead of four.
+struct GeoShade {
+    GeoTex albedo, normal, roughness, metallic, emissive, opacity;  // opacity.whf == 0: opaque
+};
+static_assert(sizeof(GeoShade) == 48, "GeoShade must be 48 B");
+
 constexpr uint32_t kTexTileWords = 32;  // 128 B
 constexpr uint32_t kTexTileW32 = 8, kTexTileH32 = 4;
 constexpr uint32_t kTexTileW8 = 16, kTexTileH8 = 8;
