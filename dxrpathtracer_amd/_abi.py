@@ -144,7 +144,8 @@ DXRPT_SYMBOLS = ("dxrpt_abi_version", "dxrpt_default_settings", "dxrpt_create", 
 DXRPT_HOST_SYMBOLS = ("dxrpt_host_scene_create", "dxrpt_host_scene_load", "dxrpt_host_scene_destroy", "dxrpt_host_last_error",
                       "dxrpt_host_inv_view_projection", "dxrpt_host_sky_create", "dxrpt_host_fill_constants",
                       "dxrpt_host_float_to_half", "dxrpt_host_half_to_float", "dxrpt_host_hosek_load",
-                      "dxrpt_host_hosek_load_tables",
+                      "dxrpt_host_hosek_load_tables", "dxrpt_host_texture_load", "dxrpt_host_texture_free",
+                      "dxrpt_host_set_asset_dir",
                       "dxrpt_host_hosek_destroy", "dxrpt_host_hosek_last_error", "dxrpt_host_sky_create_hosek",
                       "dxrpt_host_hosek_rgb_radiance", "dxrpt_host_hosek_solar_radiance", "dxrpt_host_spectrum_to_rgb",
                       "dxrpt_host_spectrum_from_rgb_reflectance", "dxrpt_host_lightmap_charts",
@@ -220,6 +221,10 @@ def host() -> C.CDLL:
         H.dxrpt_host_half_to_float.restype = f32
         H.dxrpt_host_hosek_load.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(P)]
         H.dxrpt_host_hosek_load_tables.argtypes = [C.c_char_p, C.POINTER(P)]
+        H.dxrpt_host_texture_load.argtypes = [C.c_char_p, u32, C.POINTER(HostTexture)]
+        H.dxrpt_host_texture_free.argtypes = [C.POINTER(HostTexture)]
+        H.dxrpt_host_texture_free.restype = None
+        H.dxrpt_host_set_asset_dir.argtypes = [C.c_char_p]
         H.dxrpt_host_hosek_destroy.argtypes = [P]
         H.dxrpt_host_hosek_destroy.restype = None
         H.dxrpt_host_hosek_last_error.restype = C.c_char_p

@@ -45,8 +45,6 @@
 
 namespace dxrpt_host {
 
-bool load_dds(const std::string& path, bool srgb, Texture& tex, std::string& err);
-
 namespace fbx {
 
 struct Error : std::runtime_error {
@@ -658,11 +656,7 @@ size_t load_fbx_scene(const std::string& path, const std::string& texture_dir, f
             }
             Texture t;
             std::string err;
-            std::string lower = file;
-            std::transform(lower.begin(), lower.end(), lower.begin(), [](unsigned char c) { return char(std::tolower(c)); });
-            if (lower.size() < 4 || lower.compare(lower.size() - 4, 4, ".dds") != 0)
-                throw Error("texture " + file + ": only DDS files are supported (the reference decodes other formats through WIC)");
-            if (!load_dds(file, srgb, t, err)) throw Error(err);
+            if (!load_image(file, srgb, t, err)) throw Error(err);  // DDS / PNG / JPEG (WIC in the reference)
             idx[s] = B.add_texture(std::move(t));
             tex_by_path[key] = idx[s];
         }

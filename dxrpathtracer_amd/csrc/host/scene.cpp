@@ -1,6 +1,7 @@
 // scene.cpp — host scene inputs: BoxTest (exact), WhiteFurnace/Sponza/SunTemple proxies, primitives.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -12,6 +13,7 @@ namespace dxrpt_host {
 
 namespace {
 thread_local std::string g_last_error;
+std::string g_asset_dir;
 
 struct SceneStore {
     dxrpt_host_scene pub{};
@@ -330,6 +332,9 @@ void publish(SceneStore& St, uint32_t scene_id, uint64_t seed, bool idx16) {
     P.internal = &St;
 }
 }  // namespace
+
+const std::string& asset_dir() { return g_asset_dir; }
+
 }  // namespace dxrpt_host
 
 using namespace dxrpt_host;
@@ -337,6 +342,40 @@ using namespace dxrpt_host;
 extern "C" {
 
 const char* dxrpt_host_last_error(void) { return g_last_error.c_str(); }
+
+int dxrpt_host_set_asset_dir(const char* dir) {
+    if (!dir) return DXRPT_E_INVALID_ARG;
+    g_asset_dir = dir;
+    return DXRPT_OK;
+}
+
+int dxrpt_host_texture_load(const char* path, uint32_t force_srgb, dxrpt_host_texture* out) {
+    if (!path || !out) return DXRPT_E_INVALID_ARG;
+    std::memset(out, 0, sizeof(*out));
+    Texture t;
+    std::string err;
+    if (!load_image(path, force_srgb != 0, t, err)) {
+        g_last_error = err;
+        return DXRPT_E_INVALID_ARG;
+    }
+    void* px = std::malloc(t.data.size());
+    if (!px) {
+        g_last_error = "dxrpt_host_texture_load: out of memory";
+        return DXRPT_E_INVALID_ARG;
+    }
+    std::memcpy(px, t.data.data(), t.data.size());
+    out->width = t.w;
+    out->height = t.h;
+    out->fmt = t.fmt;
+    out->texels = px;
+    return DXRPT_OK;
+}
+
+void dxrpt_host_texture_free(dxrpt_host_texture* tex) {
+    if (!tex) return;
+    std::free(const_cast<void*>(tex->texels));
+    tex->texels = nullptr;
+}
 
 int dxrpt_host_scene_create(uint32_t scene_id, uint64_t seed, uint32_t detail, dxrpt_host_scene** out) {
     if (!out) return DXRPT_E_INVALID_ARG;

@@ -133,4 +133,15 @@ MaterialTextures make_material_textures(Pattern p, uint64_t seed, uint32_t size,
 void build_sponza_proxy(SceneBuilder& B, uint64_t seed, uint32_t detail);
 void build_suntemple_proxy(SceneBuilder& B, uint64_t seed, uint32_t detail);
 
+// Texture files (dds.cpp, image.cpp): LoadTexture's decoders (Graphics/Textures.cpp:38-172).
+bool load_dds(const std::string& path, bool srgb, Texture& tex, std::string& err);
+bool load_png(const std::string& path, bool srgb, Texture& tex, std::string& err);
+bool load_jpeg(const std::string& path, bool srgb, Texture& tex, std::string& err);
+bool load_image(const std::string& path, bool srgb, Texture& tex, std::string& err);  // by file signature
+
+// Packaged assets (dxrpt_host_set_asset_dir): the directory holding suntemple/*.r8z.
+const std::string& asset_dir();
+// An R8 image stored as "DXR8", u32 width, u32 height, zlib stream of width*height bytes.
+bool load_r8z(const std::string& path, Texture& tex, std::string& err);
+
 }  // namespace dxrpt_host

@@ -151,6 +151,19 @@ int dxrpt_host_lightmap_charts(const dxrpt_host_scene* scene, uint32_t resolutio
 int dxrpt_host_surface_map(const dxrpt_mesh_vertex* vertices, uint32_t num_vertices, const uint32_t* indices,
                            uint32_t num_indices, uint32_t width, uint32_t height, float* out_pos, float* out_normal);
 
+/* LoadTexture (Graphics/Textures.cpp:38-172) for one file, chosen by its signature: DDS (uncompressed,
+ * BC1/BC3/BC4/BC5), PNG (all colour types and bit depths, Adam7) or baseline/extended sequential JPEG
+ * -- the formats the reference decodes with DirectXTex / WIC.  Mip 0 only: RGBA8
+ * (DXRPT_TEX_RGBA8_SRGB when force_srgb, else _UNORM) or R8 (BC4).  The texels are malloc'd; release
+ * them with dxrpt_host_texture_free.  DXRPT_E_INVALID_ARG + dxrpt_host_last_error on failure. */
+int dxrpt_host_texture_load(const char* path, uint32_t force_srgb, dxrpt_host_texture* out);
+void dxrpt_host_texture_free(dxrpt_host_texture* tex);
+
+/* Directory of the packaged assets (dxrpathtracer_amd/data): the SunTemple proxy's foliage opacity
+ * maps (suntemple/NAME.r8z, decoded from the reference's BC4 files by scripts/make_suntemple_opacity.py).
+ * dxrpathtracer_amd.scene sets it on import. */
+int dxrpt_host_set_asset_dir(const char* dir);
+
 /* IEEE binary16 <-> binary32 (round to nearest even), used for the cube texels. */
 uint16_t dxrpt_host_float_to_half(float f);
 float dxrpt_host_half_to_float(uint16_t h);

@@ -178,10 +178,12 @@ def bc4_decode_block(b):
     return [pal[(bits >> (3 * i)) & 7] for i in range(16)]
 
 
-def box_room_fbx(directory):
+def box_room_fbx(directory, images="dds"):
     """A synthetic scene for the GPU ingest test: floor, back and side walls, a box and an alpha-tested
-    card (TransparentColor -> opacity, BC4), albedo from a BC1 DDS.  Geometry is given in the
-    renderer's (left-handed) frame and written with z mirrored, as an FBX exporter would store it."""
+    card (TransparentColor -> opacity), albedo and opacity from BC1 / BC4 DDS files (images="dds") or
+    from a PNG albedo and a greyscale JPEG opacity (images="png", the WIC formats; needs PIL for the
+    JPEG).  Geometry is given in the renderer's (left-handed) frame and written with z mirrored, as an
+    FBX exporter would store it."""
     import os
     quads = []  # (4 corners, normal)
 
@@ -217,7 +219,17 @@ def box_room_fbx(directory):
         v = 255 if bx % 2 == 0 else 0
         op.append(bytes([v, v, 0, 0, 0, 0, 0, 0]))
     write_dds(os.path.join(directory, "opacity.dds"), 8, 8, fourcc=b"BC4U", data=b"".join(op))
+    slots = {"DiffuseColor": "albedo.dds", "TransparentColor": "opacity.dds"}
+    if images == "png":
+        import numpy as np
+        from PIL import Image
+        from tests.image_util import write_png
+        yy, xx = np.mgrid[0:16, 0:16]
+        rgb = np.stack([(xx * 16) % 256, (yy * 16) % 256, ((xx ^ yy) * 32) % 256], -1)
+        write_png(os.path.join(directory, "albedo.png"), rgb, 2, 8, interlace=True)
+        mask = np.where((xx // 4 + yy // 4) % 2 == 0, 255, 0).astype(np.uint8)
+        Image.fromarray(mask, "L").save(os.path.join(directory, "opacity.jpg"), quality=90)
+        slots = {"DiffuseColor": "albedo.png", "TransparentColor": "opacity.jpg"}
     path = os.path.join(directory, "room.fbx")
-    mesh_fbx(path, pos, polys, normals, uvs, uv_index,
-             material_slots={"DiffuseColor": "albedo.dds", "TransparentColor": "opacity.dds"})
+    mesh_fbx(path, pos, polys, normals, uvs, uv_index, material_slots=slots)
     return path

@@ -1,5 +1,5 @@
 """Real-asset ingest: dxrpt_host_scene_load = Model::CreateWithAssimp restated for
-binary FBX + DDS (host/fbx.cpp, host/dds.cpp).
+binary FBX + DDS / PNG / JPEG (host/fbx.cpp, host/dds.cpp, host/image.cpp).
 
 Assimp 4.1.0 is not vendored (prebuilt lib only), so its post-processing is parity-unpinned; these
 tests pin what the reference's call site fixes (Graphics/Model.cpp:435-606, DXRPathTracer.cpp:83-95,
@@ -118,9 +118,12 @@ def test_bc_block_decode(tmp_path):
 
 
 def test_unsupported_texture_format_fails_loudly(tmp_path):
-    (tmp_path / "albedo.png").write_bytes(b"\x89PNG\r\n\x1a\n")
-    with pytest.raises(RuntimeError, match="only DDS"):
-        D.Scene(A.SCENE_BOXTEST, model_path=_synthetic(tmp_path, material_tex="albedo.png"))
+    (tmp_path / "albedo.tga").write_bytes(b"\x00\x00\x02" + bytes(40))
+    with pytest.raises(RuntimeError, match="unsupported image format"):
+        D.Scene(A.SCENE_BOXTEST, model_path=_synthetic(tmp_path, material_tex="albedo.tga"))
+    (tmp_path / "broken.png").write_bytes(b"\x89PNG\r\n\x1a\n")
+    with pytest.raises(RuntimeError, match="PNG"):
+        D.Scene(A.SCENE_BOXTEST, model_path=_synthetic(tmp_path, material_tex="broken.png"))
     with pytest.raises(RuntimeError, match="does not exist"):
         D.Scene(A.SCENE_BOXTEST, model_path=str(tmp_path / "nope.fbx"))
 
@@ -174,3 +177,20 @@ def test_white_furnace_fbx_known_answer():
     centre = rgb[H // 2 - 2:H // 2 + 2, W // 2 - 2:W // 2 + 2].mean()
     expected = (1.0 - math.log(2.0)) / _ess(0.0, 1.0)
     assert abs(centre - expected) < 0.03, (centre, expected)
+
+
+def test_png_and_jpeg_textures_through_materials(tmp_path):
+    # DiffuseColor -> albedo slot from a PNG (sRGB, ForceSRGB), TransparentColor -> opacity from a JPEG
+    pytest.importorskip("PIL.Image")
+    sc = D.Scene(A.SCENE_BOXTEST, model_path=F.box_room_fbx(str(tmp_path), images="png"))
+    m = sc.materials[0]
+    w, h, fmt, data = sc.textures[m[0]]
+    assert (w, h, fmt) == (16, 16, A.TEX_RGBA8_SRGB)
+    img = data.reshape(16, 16, 4)
+    yy, xx = np.mgrid[0:16, 0:16]
+    assert (img[..., 0] == (xx * 16) % 256).all() and (img[..., 2] == ((xx ^ yy) * 32) % 256).all()
+    w, h, fmt, data = sc.textures[m[4]]
+    assert (w, h, fmt) == (16, 16, A.TEX_RGBA8_UNORM)
+    r = data.reshape(16, 16, 4)[..., 0].astype(int)
+    want = np.where((xx // 4 + yy // 4) % 2 == 0, 255, 0)
+    assert np.abs(r - want).max() < 40 and ((r > 128) == (want > 128)).all()

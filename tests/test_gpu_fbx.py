@@ -1,6 +1,6 @@
-"""GPU parity on a scene ingested through dxrpt_host_scene_load (FBX + BC1/BC4 DDS textures, alpha
-tested through the TransparentColor -> opacity slot): the HIP path against the CPU oracle on the same
-loaded inputs.  The scene is a synthetic FBX written by the test (the reference's assets do not travel
+"""GPU parity on a scene ingested through dxrpt_host_scene_load (FBX + BC1/BC4 DDS textures, or a PNG
+albedo and a JPEG opacity -- the WIC formats -- alpha tested through the TransparentColor -> opacity
+slot): the HIP path against the CPU oracle on the same loaded inputs.  The scene is a synthetic FBX written by the test (the reference's assets do not travel
 to the GPU box)."""
 import numpy as np
 import pytest
@@ -15,11 +15,14 @@ from tests._common import assert_parity
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("images", ["dds", "png"])
 @pytest.mark.parametrize("max_any_hit", [1, 3])
 @pytest.mark.parametrize("mega", [0, A.DEFAULT_MEGAKERNEL_PATHS])  # wavefront passes / one-kernel frame
-def test_fbx_scene_matches_oracle(torch_cuda, tmp_path, max_any_hit, mega):
+def test_fbx_scene_matches_oracle(torch_cuda, tmp_path, max_any_hit, mega, images):
     torch = torch_cuda
-    sc = D.Scene(A.SCENE_BOXTEST, model_path=F.box_room_fbx(str(tmp_path)))
+    if images == "png":
+        pytest.importorskip("PIL.Image")
+    sc = D.Scene(A.SCENE_BOXTEST, model_path=F.box_room_fbx(str(tmp_path), images=images))
     assert sc.materials[0][4] != 0xFFFFFFFF  # opacity map present: alpha-tested geometry
     st = sc.settings(MaxPathLength=4, MaxAnyHitPathLength=max_any_hit)
     sky = D.make_sky(st)
