@@ -9,6 +9,8 @@
 // splitmix64 seeded with `seed` (default 0x53504F4E5A41, "SPONZA").
 #include <algorithm>
 #include <cmath>
+#include <stdexcept>
+#include <string>
 
 #include "scene_builder.h"
 
@@ -28,6 +30,24 @@ uint32_t add_pbr(SceneBuilder& B, Pattern p, uint64_t seed, uint32_t size, float
     uint32_t ir = B.add_texture(std::move(t.roughness));
     uint32_t im = B.add_texture(std::move(t.metallic));
     uint32_t io = alpha ? B.add_texture(std::move(t.opacity)) : DXRPT_INVALID_INDEX;
+    return B.add_material(ia, in, ir, im, io, black);
+}
+
+// A PBR material whose opacity map is a packaged asset (asset_dir()/<file>, an .r8z R8 image).
+uint32_t add_pbr_asset_opacity(SceneBuilder& B, Pattern p, uint64_t seed, uint32_t size, float r, float g, float b,
+                               float rough, float metal, const char* file, uint32_t black) {
+    MaterialTextures t = make_material_textures(p, seed, size, r, g, b, rough, metal, false);
+    Texture op;
+    std::string err;
+    const std::string path = asset_dir() + "/suntemple/" + file;
+    if (asset_dir().empty() || !load_r8z(path, op, err))
+        throw std::runtime_error("SunTemple proxy: cannot load the packaged opacity map " + path +
+                                 " (dxrpt_host_set_asset_dir -> dxrpathtracer_amd/data): " + err);
+    uint32_t ia = B.add_texture(std::move(t.albedo));
+    uint32_t in = B.add_texture(std::move(t.normal));
+    uint32_t ir = B.add_texture(std::move(t.roughness));
+    uint32_t im = B.add_texture(std::move(t.metallic));
+    uint32_t io = B.add_texture(std::move(op));
     return B.add_material(ia, in, ir, im, io, black);
 }
 
@@ -230,8 +250,12 @@ void build_suntemple_proxy(SceneBuilder& B, uint64_t seed, uint32_t detail) {
     const uint32_t mPillar = add_pbr(B, Pattern::Marble, rng.next(), TS, 0.80f, 0.74f, 0.62f, 0.4f, 0.0f, false, black);
     const uint32_t mRoof = add_pbr(B, Pattern::Wood, rng.next(), TS, 0.35f, 0.25f, 0.18f, 0.7f, 0.0f, false, black);
     const uint32_t mGold = add_pbr(B, Pattern::Metal, rng.next(), 256, 0.95f, 0.75f, 0.30f, 0.3f, 1.0f, false, black);
-    const uint32_t mLeafA = add_pbr(B, Pattern::Leaves, rng.next(), TS, 0.25f, 0.40f, 0.10f, 0.7f, 0.0f, true, black);
-    const uint32_t mLeafB = add_pbr(B, Pattern::Leaves, rng.next(), TS, 0.45f, 0.35f, 0.10f, 0.7f, 0.0f, true, black);
+    // foliage: procedural albedo / normal / roughness, the reference's own BC4 opacity maps (SURVEY.md
+    // 8(d): Content/Models/SunTemple/Textures, packaged by scripts/make_suntemple_opacity.py)
+    const uint32_t mLeafA = add_pbr_asset_opacity(B, Pattern::Leaves, rng.next(), TS, 0.25f, 0.40f, 0.10f, 0.7f, 0.0f,
+                                                  "T_M_Tree_Branches_0_A.r8z", black);
+    const uint32_t mLeafB = add_pbr_asset_opacity(B, Pattern::Leaves, rng.next(), TS, 0.45f, 0.35f, 0.10f, 0.7f, 0.0f,
+                                                  "T_Soul_Tree011M_Inst_0_A.r8z", black);
     const uint32_t mBark = add_pbr(B, Pattern::Wood, rng.next(), TS, 0.30f, 0.22f, 0.15f, 0.9f, 0.0f, false, black);
     const float X = 9.0f, Z0 = -24.0f, Z1 = 16.0f, H = 11.0f;
     B.begin_mesh(mFloor);

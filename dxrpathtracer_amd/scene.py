@@ -38,6 +38,18 @@ DEFAULT_GROUND_ALBEDO = (0.25, 0.25, 0.25)
 SKY_RES = 128  # Skybox.cpp:164
 
 
+DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+
+
+def _host():
+    """libdxrpt_host.so with the packaged asset directory set (the SunTemple proxy's opacity maps)."""
+    H = A.host()
+    if not getattr(H, "_asset_dir_set", False):
+        H.dxrpt_host_set_asset_dir(DATA_DIR.encode())
+        H._asset_dir_set = True
+    return H
+
+
 class Scene:
     """A host scene (vertices, indices, geometries, materials, textures, lights + camera/sun pose)."""
 
@@ -47,7 +59,7 @@ class Scene:
         Model::CreateWithAssimp (dxrpt_host_scene_load; texture_dir and scene_scale default to the
         reference's table for the scene id)."""
         sid = SCENE_NAMES[scene] if isinstance(scene, str) else int(scene)
-        H = A.host()
+        H = _host()
         p = C.POINTER(A.HostScene)()
         if model_path is None:
             rc = H.dxrpt_host_scene_create(sid, seed, detail, C.byref(p))
