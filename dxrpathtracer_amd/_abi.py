@@ -81,7 +81,7 @@ KERNEL_NAMES = ("k_raygen", "k_trace", "k_shade", "k_shadow", "k_accumulate", "k
  OPT_POSTPONE_TRIS, OPT_TRACE_BLOCK, OPT_OCCUPANCY, OPT_SHADE_BLOCK, OPT_SHADE_OCCUPANCY, OPT_SPATIAL_SPLITS,
  OPT_LEAF_COST, OPT_SHADOW_OCCUPANCY, OPT_SHADOW_GRID, OPT_CONCURRENCY, OPT_TRAVERSAL_PIPELINE, OPT_PACKET_TRAVERSAL, OPT_LDS_NODES,
  OPT_KERNEL_TIMING_MASK, OPT_XCD_MAPPING, OPT_PACKET_SWITCH, OPT_MEGAKERNEL_PATHS, OPT_MEGAKERNEL_OCCUPANCY,
- OPT_BAKE_CHUNK, OPT_MEGAKERNEL_PERSISTENT, OPT_MEGAKERNEL_LANES) = range(1, 28)
+ OPT_BAKE_CHUNK, OPT_MEGAKERNEL_PERSISTENT, OPT_MEGAKERNEL_LANES, OPT_WAVE_CLOCKS) = range(1, 29)
 # context defaults of the traversal options (dxrpt_api.hip)
 DEFAULT_TRAVERSAL_PIPELINE = 0
 POST_FLOAT4, POST_RGBA8 = 0, 1  # dxrpt_post_process output formats
@@ -140,7 +140,7 @@ for _t, _n in ((MeshVertex, 64), (GeometryInfo, 16), (Material, 24), (SpotLight,
 DXRPT_SYMBOLS = ("dxrpt_abi_version", "dxrpt_default_settings", "dxrpt_create", "dxrpt_destroy", "dxrpt_last_error",
                  "dxrpt_set_scene", "dxrpt_add_texture", "dxrpt_set_sky", "dxrpt_build_bvh", "dxrpt_get_bvh_info",
                  "dxrpt_render", "dxrpt_get_stats", "dxrpt_trace_rays", "dxrpt_set_option", "dxrpt_reset_timing",
-                 "dxrpt_post_process", "dxrpt_bake_lightmap", "dxrpt_denoise_median")
+                 "dxrpt_post_process", "dxrpt_bake_lightmap", "dxrpt_denoise_median", "dxrpt_get_wave_clocks")
 DXRPT_HOST_SYMBOLS = ("dxrpt_host_scene_create", "dxrpt_host_scene_load", "dxrpt_host_scene_destroy", "dxrpt_host_last_error",
                       "dxrpt_host_inv_view_projection", "dxrpt_host_sky_create", "dxrpt_host_fill_constants",
                       "dxrpt_host_float_to_half", "dxrpt_host_half_to_float", "dxrpt_host_hosek_load",
@@ -185,6 +185,7 @@ def lib() -> C.CDLL:
         L.dxrpt_render.argtypes = [P, C.POINTER(RayTraceConstants), C.POINTER(AppSettings),
                                    C.POINTER(LightConstants), P, u32, u32, C.POINTER(Tile), u32, P]
         L.dxrpt_get_stats.argtypes = [P, C.POINTER(Stats)]
+        L.dxrpt_get_wave_clocks.argtypes = [P, C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint32)]
         L.dxrpt_trace_rays.argtypes = [P, P, u32, u32, P, P]
         L.dxrpt_post_process.argtypes = [P, C.POINTER(AppSettings), P, u32, u32, P, u32, P]
         L.dxrpt_set_option.argtypes = [P, u32, C.c_uint64]

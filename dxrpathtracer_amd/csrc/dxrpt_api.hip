@@ -120,6 +120,9 @@ struct dxrpt_ctx {
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
     int built_width = 0;
     DevBuf d_trav;   // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
+    DevBuf d_wclock;  // 2 x u64 per wave (DXRPT_OPT_WAVE_CLOCKS)
+    bool opt_wave_clocks = false;
+    uint32_t wclock_waves = 0;
     DevBuf d_spill;  // BVH8 traversal stack entries beyond the LDS part (deep trees only)
     DevBuf d_bake_list;  // live lightmap texels of the last bake pass + their count
     // kernel timing: a ring of per-frame event sets, harvested lazily
@@ -140,7 +143,7 @@ struct dxrpt_ctx {
     ~dxrpt_ctx() {
         DevBuf* all[] = {&d_vertices, &d_indices, &d_geos, &d_mats, &d_texdesc, &d_texels, &d_sky, &d_lut, &d_geoshade, &d_nodes,
                          &d_nodes8, &d_tris, &d_tri_verts, &d_lights, &d_tiles, &d_tile_prefix, &f_pix, &f_pxrad, &f_hit, &f_fwd,
-                         &f_shn, &f_shq, &f_shorg, &f_shdir, &f_shcon, &f_counters, &p_bloom0, &p_bloom1};
+                         &f_shn, &f_shq, &f_shorg, &f_shdir, &f_shcon, &f_counters, &p_bloom0, &p_bloom1, &d_wclock};
         for (DevBuf* b : all) b->release();
         for (auto& qb : f_q)
             for (DevBuf& b : qb) b.release();
@@ -485,6 +488,8 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_PACKET_SWITCH) {
             require(value <= 100, "dxrpt_set_option: packet switch threshold must be 0..100 (percent)");
             ctx->opt_packet_switch = uint32_t(value);
+        } else if (option == DXRPT_OPT_WAVE_CLOCKS) {
+            ctx->opt_wave_clocks = value != 0;
         } else if (option == DXRPT_OPT_MEGAKERNEL_PATHS) {
             ctx->opt_mega_paths = value > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(value);
         } else if (option == DXRPT_OPT_MEGAKERNEL_OCCUPANCY) {
@@ -754,6 +759,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.width = width;
         fp.height = height;
         fp.trav = nullptr;
+        fp.wave_clock = nullptr;
         // 32 KiB of LDS per 256-thread workgroup -> 5 resident workgroups per CU (160 KiB)
         fp.chunks_per_wave = ctx->opt_trav_mode == 1 ? ctx->opt_chunks : 0u;
         fp.refill_lanes = ctx->opt_refill;
@@ -787,6 +793,12 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         if (ctx->opt_count) {
             fp.trav = ctx->d_trav.as<unsigned long long>();
             HIP_CHECK(hipMemsetAsync(fp.trav, 0, 4 * sizeof(unsigned long long), s));
+            ctx->wclock_waves = 0;
+            if (ctx->opt_wave_clocks && fp.megakernel) {
+                ctx->wclock_waves = (paths + 63u) / 64u;
+                ctx->d_wclock.ensure(size_t(ctx->wclock_waves) * 2 * sizeof(unsigned long long));
+                fp.wave_clock = ctx->d_wclock.as<unsigned long long>();
+            }
         }
         const int L = settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength;
         hipEvent_t* ev = nullptr;
@@ -860,6 +872,17 @@ int dxrpt_get_stats(dxrpt_ctx* ctx, dxrpt_stats* out) {
         s.timed_frames = ctx->timed_frames;
         s.frame_ms = ctx->frame_ms;
         *out = s;
+    });
+}
+
+int dxrpt_get_wave_clocks(dxrpt_ctx* ctx, uint64_t* out, uint32_t max_waves, uint32_t* num_waves) {
+    if (!ctx || !num_waves) return DXRPT_E_INVALID_ARG;
+    return guarded(ctx, [&] {
+        require(ctx->rendered, "dxrpt_get_wave_clocks: nothing rendered yet", DXRPT_E_STATE);
+        HIP_CHECK(hipStreamSynchronize(ctx->last_stream));
+        *num_waves = ctx->wclock_waves;
+        const uint32_t n = std::min(max_waves, ctx->wclock_waves);
+        if (n && out) HIP_CHECK(hipMemcpy(out, ctx->d_wclock.p, size_t(n) * 2 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     });
 }
 

@@ -119,6 +119,7 @@ struct FrameParams {
     uint32_t num_paths;
     uint32_t width, height;
     unsigned long long* trav;        // non-null: count traversal work ([0..1] closest node/tri, [2..3] shadow)
+    unsigned long long* wave_clock;  // census frames, non-null: per-wave (start, end) s_memrealtime stamps
     uint32_t chunks_per_wave;        // BVH8 wave-pool traversal: 64-ray chunks per wave; 0 = one thread per ray
     uint32_t refill_lanes;           // wave-pool kernels: refill once this many lanes of a wave are idle
     uint32_t trace_block;            // workgroup size of the one-thread-per-ray traversal kernels (64..256)

@@ -1931,8 +1931,14 @@ void k_path(KArgs A) {
             return;
         }
         if (kCount) {  // census (DXRPT_OPT_COUNT_TRAVERSAL): wave sums, one 64-bit atomic per counter per wave
+            const unsigned long long t0 = A.P.wave_clock ? __builtin_amdgcn_s_memrealtime() : 0ull;
             uint32_t cnt[4] = {0u, 0u, 0u, 0u};
             if (p < A.P.num_paths) camera_path<true>(A, p, stk, NodeCache{nullptr, 0u}, cnt);
+            if (A.P.wave_clock && (threadIdx.x & 63u) == 0u) {  // vector stores from lane 0 of the wave
+                const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+                A.P.wave_clock[2 * (p >> 6)] = t0;
+                A.P.wave_clock[2 * (p >> 6) + 1] = t1;
+            }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 uint32_t v = cnt[k];

@@ -119,6 +119,18 @@ class DXRPathTracer:
         self._check(self._L.dxrpt_get_stats(self._ctx, C.byref(st)), "dxrpt_get_stats")
         return st
 
+    def wave_clocks(self):
+        """Per-wave (start, end) s_memrealtime stamps (100 MHz ticks) of the last census frame rendered
+        with OPT_COUNT_TRAVERSAL + OPT_WAVE_CLOCKS (megakernel), as a (waves, 2) uint64 array."""
+        import numpy as np
+        n = C.c_uint32()
+        self._check(self._L.dxrpt_get_wave_clocks(self._ctx, None, 0, C.byref(n)), "dxrpt_get_wave_clocks")
+        out = np.zeros((n.value, 2), dtype=np.uint64)
+        if n.value:
+            self._check(self._L.dxrpt_get_wave_clocks(self._ctx, out.ctypes.data_as(C.POINTER(C.c_uint64)), n.value,
+                                                      C.byref(n)), "dxrpt_get_wave_clocks")
+        return out
+
     def post_process(self, settings: A.AppSettings, accum_ptr: int, width: int, height: int, out_ptr: int,
                      out_format: int = A.POST_FLOAT4, stream: int = 0):
         """PostProcessor::Render (PostProcessor.cpp:43-92): bloom + exposure + filmic tone map of the

@@ -328,6 +328,10 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                           dependent-traversal chains on small frames).  Identical results. */
 #define DXRPT_OPT_BAKE_CHUNK 25u /* texels per dxrpt_bake_lightmap launch (default 2^21; bounds the
                                     per-texel shadow-slot buffers).  Identical results. */
+#define DXRPT_OPT_WAVE_CLOCKS 28u /* 1: with DXRPT_OPT_COUNT_TRAVERSAL, the megakernel census frame also
+                                     records each wave's start and end time (s_memrealtime, 100 MHz),
+                                     read with dxrpt_get_wave_clocks (diagnostic: where a frame's tail
+                                     comes from).  Images identical. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);
@@ -355,6 +359,10 @@ int dxrpt_post_process(dxrpt_ctx* ctx, const dxrpt_app_settings* settings, const
                        uint32_t height, void* out, uint32_t out_format, void* stream);
 /* Synchronises the context's last stream and returns the counters of the last dxrpt_render. */
 int dxrpt_get_stats(dxrpt_ctx* ctx, dxrpt_stats* out);
+/* Diagnostic (DXRPT_OPT_WAVE_CLOCKS + DXRPT_OPT_COUNT_TRAVERSAL, megakernel frames): the last render's
+ * per-wave (start, end) s_memrealtime stamps, wave w = paths [64 w, 64 w + 64) in path-slot order;
+ * copies min(max_waves, waves) pairs into out[2 w], out[2 w + 1] and the wave count into *num_waves. */
+int dxrpt_get_wave_clocks(dxrpt_ctx* ctx, uint64_t* out, uint32_t max_waves, uint32_t* num_waves);
 
 /* TraceRay on arbitrary rays against the built acceleration structure (the DXR TraceRay call sites
  * RayTrace.hlsl:138,258,305,407,425 without the shading).  `rays` (device) holds num_rays pairs of

@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--share", type=int, default=1)
     ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--any-hit", type=int, default=None, help="MaxAnyHitPathLength override")
+    ap.add_argument("--packet", type=int, default=None, help="DXRPT_OPT_PACKET_TRAVERSAL override")
+    ap.add_argument("--occ", type=int, default=None, help="DXRPT_OPT_MEGAKERNEL_OCCUPANCY override")
     args = ap.parse_args()
     import torch
     import dxrpathtracer_amd as D
@@ -32,9 +35,14 @@ def main():
 
     name, W, H, L = CONFIGS[args.config]
     sc = D.Scene(name)
-    st = sc.settings(MaxPathLength=L)
+    st = sc.settings(MaxPathLength=L, **({} if args.any_hit is None else {"MaxAnyHitPathLength": args.any_hit}))
     sky = D.make_sky(st)
     t = DXRPathTracer(0)
+    import dxrpathtracer_amd._abi as A
+    if args.packet is not None:
+        t.set_option(A.OPT_PACKET_TRAVERSAL, args.packet)
+    if args.occ is not None:
+        t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, args.occ)
     t.initialize_scene(sc, sky)
     t.build_rt_acceleration_structure()
     tiles, n = None, W * H
