@@ -6,8 +6,9 @@ MaxPathLength 3, one sample per pixel per frame with progressive accumulation.
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 A step is one frame (DispatchRays(1920,1080,1) equivalent, DXRPathTracer.cpp:2024-2090) over the whole
-image.  With N ranks the image is split into 8-row bands (band b -> rank b % N) and every frame ends
-with an RCCL gather of the band slabs to rank 0 plus the un-permute: total work per
+image.  With N ranks the image is split into 8-row bands, band b -> rank b % N (distributed.band_layout;
+--layout blocks: 8x8-pixel blocks dealt in a seeded random order) and every frame ends
+with an RCCL gather of the rank slabs to rank 0 plus the un-permute: total work per
 frame is fixed, so scaling is "strong".  The gather of frame f runs on RCCL's stream while frame f+1
 renders (distributed.PipelinedGather); the last frame's gather is inside the timed region.  value = nominal Mrays/s of the whole job (W*H*(1+2(L-1))
 rays per frame, the reference's HUD formula DXRPathTracer.cpp:2171) over the max-over-ranks time.
@@ -131,6 +132,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: every usable CPU)")
     ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
+    ap.add_argument("--layout", default="bands", choices=["bands", "blocks"],
+                    help="N-GPU screen partition: round-robin 8-row bands (default) or a seeded 8x8-block deal")
     args = ap.parse_args()
     global SCENE, WIDTH, HEIGHT, PATH_LENGTH
     SCENE, WIDTH, HEIGHT, PATH_LENGTH = CONFIGS[args.config]
@@ -141,7 +144,7 @@ def main():
     import torch.distributed as dist
     import dxrpathtracer_amd as D
     import dxrpathtracer_amd._abi as A
-    from dxrpathtracer_amd.distributed import PipelinedGather, band_layout, source_index
+    from dxrpathtracer_amd.distributed import PipelinedGather, screen_layout, source_index
     from dxrpathtracer_amd.tracer import DXRPathTracer
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -165,7 +168,7 @@ def main():
     bvh = tracer.build_rt_acceleration_structure()
     setup_s = time.perf_counter() - t0
     lights = D.make_lights(scene)
-    lay = band_layout(WIDTH, HEIGHT, world)
+    lay = screen_layout(WIDTH, HEIGHT, world, args.layout)
     tiles = lay.rank_tiles(rank) if world > 1 else None
     n_local = lay.counts[rank] if world > 1 else WIDTH * HEIGHT
     accum = torch.zeros((max(lay.max_count, n_local), 4), dtype=torch.float32, device="cuda")
@@ -295,7 +298,7 @@ def main():
             "config": {"workload": f"{SCENE}-proxy {WIDTH}x{HEIGHT} L={PATH_LENGTH} 1spp/frame progressive",
                        "width": WIDTH, "height": HEIGHT, "max_path_length": PATH_LENGTH,
                        "sqrt_num_samples": 4, "triangles": scene.num_triangles, "sky": sky.model,
-                       "parallelism": f"screen bands x{world}" + (" + RCCL gather" if world > 1 else "")},
+                       "parallelism": (f"screen {args.layout} x{world} + RCCL gather" if world > 1 else "single GPU")},
             "roofline": {"bound": "hbm", "kernel": roof_kernel, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "bytes_per_launch": int(roof_bytes),

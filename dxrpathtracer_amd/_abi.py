@@ -93,7 +93,7 @@ DEFAULT_MEGAKERNEL_PATHS = 10000000
 DEFAULT_MEGAKERNEL_OCCUPANCY = 0
 DEFAULT_BAKE_CHUNK = 1 << 21
 DEFAULT_MEGAKERNEL_PERSISTENT = 0
-DEFAULT_MEGAKERNEL_LANES = 64
+DEFAULT_MEGAKERNEL_LANES = 0  # by frame size
 
 
 class Stats(C.Structure):

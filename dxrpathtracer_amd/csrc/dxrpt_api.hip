@@ -116,7 +116,7 @@ struct dxrpt_ctx {
     uint32_t opt_mega_occ = 0;              // DXRPT_OPT_MEGAKERNEL_OCCUPANCY (0 = by frame size)
     uint32_t opt_bake_chunk = 1u << 21;     // DXRPT_OPT_BAKE_CHUNK (texels per bake launch)
     uint32_t opt_mega_persistent = 0;       // DXRPT_OPT_MEGAKERNEL_PERSISTENT (waves per CU, 0 = off)
-    uint32_t opt_mega_lanes = 64;           // DXRPT_OPT_MEGAKERNEL_LANES (paths per megakernel wave)
+    uint32_t opt_mega_lanes = 0;            // DXRPT_OPT_MEGAKERNEL_LANES (paths per megakernel wave, 0 = by size)
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
     int built_width = 0;
     DevBuf d_trav;   // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
@@ -499,7 +499,8 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
             require(value <= 64, "dxrpt_set_option: persistent megakernel waves per CU must be 0..64");
             ctx->opt_mega_persistent = uint32_t(value);
         } else if (option == DXRPT_OPT_MEGAKERNEL_LANES) {
-            require(value == 16 || value == 32 || value == 64, "dxrpt_set_option: megakernel lanes must be 16, 32 or 64");
+            require(value == 0 || value == 16 || value == 32 || value == 64,
+                    "dxrpt_set_option: megakernel lanes must be 0 (by frame size), 16, 32 or 64");
             ctx->opt_mega_lanes = uint32_t(value);
         } else if (option == DXRPT_OPT_BAKE_CHUNK) {
             require(value >= 64 && value <= (1u << 26), "dxrpt_set_option: bake chunk must be 64..2^26 texels");
@@ -784,10 +785,17 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // register budget by frame size (measured, Sponza proxy 1080p L=3 and its 1/2, 1/4, 1/8 shares):
         // more resident waves hide more latency once a frame has waves for several rounds; a GPU's 1/8
         // share (~4k waves) fits in one round at 4 waves/SIMD without spills
+        // Small frames (a GPU's 1/8 share of 1080p and below) end with their slowest waves' paths
+        // (alpha-tested foliage, scripts/wave_clocks.py): two lanes per path trace a vertex's
+        // continuation and shadow rays concurrently, shortening those chains (1/8 share 0.72-0.76 ->
+        // 0.68-0.69 ms at 6 waves/SIMD, profiles/r02_ab_path_groups_shares.txt); from the 1/4 share up
+        // the doubled waves cost more than the shorter chains save.
+        const uint32_t lanes = ctx->opt_mega_lanes ? ctx->opt_mega_lanes : (paths <= 400000u ? 32u : 64u);
         fp.megakernel_occupancy = ctx->opt_mega_occ ? ctx->opt_mega_occ
-                                                    : (paths > 1500000u ? 7u : (paths > 300000u ? 5u : 4u));
+                                : lanes < 64u ? 6u
+                                : (paths > 1500000u ? 7u : (paths > 300000u ? 5u : 4u));
         fp.mega_persistent = ctx->opt_mega_persistent;
-        fp.mega_lanes = ctx->opt_mega_lanes;
+        fp.mega_lanes = lanes;
         fp.num_cus = ctx->num_cus;
         hipStream_t s = static_cast<hipStream_t>(stream);
         if (ctx->opt_count) {

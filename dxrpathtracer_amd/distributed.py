@@ -2,9 +2,11 @@
 
 The reference is single-GPU; every pixel's path is independent and the CMJ pattern uses only the
 GLOBAL pixel index (RayTrace.hlsl:85-96), so any partition of the image renders bit-identical pixels.
-Rank r path-traces bands b = r, r+N, r+2N, ... of `band` full rows into a compact local buffer
-(dxrpt_tile accum_offset/pitch), and rank 0 gathers the slabs (torch.distributed: RCCL over xGMI on
-the GPU node, gloo in the CPU tests) and un-permutes them into the full RGBA32F frame.
+Rank r path-traces its share of the image -- bands b = r, r+N, r+2N, ... of `band` full rows
+(band_layout, the default), or 8x8 pixel blocks dealt in a seeded random order (block_layout) -- into a
+compact local buffer (dxrpt_tile accum_offset/pitch), and rank 0 gathers the slabs
+(torch.distributed: RCCL over xGMI on the GPU node, gloo in the CPU tests) and un-permutes them into
+the full RGBA32F frame.
 """
 from __future__ import annotations
 
@@ -41,6 +43,49 @@ def band_layout(width: int, height: int, world: int, band: int = BAND_ROWS) -> B
         tiles[r].append(A.Tile(0, y0, width, h, counts[r], width, 0))
         counts[r] += width * h
     return BandLayout(width, height, world, band, tiles, counts, max(counts))
+
+
+def _mix64(x: int) -> int:
+    """splitmix64 finaliser: the partition's only source of pseudo-randomness (deterministic)."""
+    x = (x + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return x ^ (x >> 31)
+
+
+def block_layout(width: int, height: int, world: int, block: int = 8, seed: int = 0x5EED) -> BandLayout:
+    """Cost-spreading partition: the image's block x block pixel blocks (one megakernel wave each) are
+    dealt to the ranks in a seeded pseudo-random order, round robin, so every rank receives an equal
+    number of blocks drawn from the whole image.  The expensive blocks of a frame -- measured with
+    scripts/wave_clocks.py: alpha-tested foliage, clustered in a few block rows -- land on all ranks
+    instead of on the one that owns those rows, which is what an N-GPU frame waits for.  Each rank
+    renders its blocks in raster order (tiles of block x block pixels, compact in its slab); pixels,
+    CMJ seeds and results are those of the full frame (global pixel indices)."""
+    nbx, nby = (width + block - 1) // block, (height + block - 1) // block
+    order = sorted(range(nbx * nby), key=lambda b: (_mix64(b ^ (seed << 32)), b))
+    owner = [0] * (nbx * nby)
+    for k, b in enumerate(order):
+        owner[b] = k % world
+    tiles = [[] for _ in range(world)]
+    counts = [0] * world
+    for b in range(nbx * nby):
+        r = owner[b]
+        x0, y0 = (b % nbx) * block, (b // nbx) * block
+        w, h = min(block, width - x0), min(block, height - y0)
+        tiles[r].append(A.Tile(x0, y0, w, h, counts[r], w, 0))
+        counts[r] += w * h
+    return BandLayout(width, height, world, block, tiles, counts, max(counts))
+
+
+def screen_layout(width: int, height: int, world: int, kind: str = "bands") -> BandLayout:
+    """The multi-GPU screen partition: "bands" (band_layout, default) or "blocks" (block_layout).  Measured
+    per-rank times of a 1080p frame's 1/8 shares (profiles/r02_shares_path_groups_default.txt): bands
+    0.62-0.69 ms, blocks 0.66-0.70 -- a share ends with its slowest waves, not with its pixel count."""
+    if kind == "bands":
+        return band_layout(width, height, world)
+    if kind == "blocks":
+        return block_layout(width, height, world)
+    raise ValueError(f"unknown screen layout {kind!r}")
 
 
 def source_index(layout: BandLayout):

@@ -316,16 +316,19 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                             compaction wins for long paths on big frames).  0 = always the
                                             wavefront.  Identical results. */
 #define DXRPT_OPT_MEGAKERNEL_OCCUPANCY 24u /* megakernel register budget in waves/SIMD: 0 = by frame size
-                                              (default: 7 above 1,500,000 paths, 5 above 300,000, else 4),
+                                              (default: 6 with path groups, else 7 above 1,500,000 paths,
+                                              5 above 300,000, else 4),
                                               4 (no spills), 5, 6, 7, 8, or 3 = the compiler's */
 #define DXRPT_OPT_MEGAKERNEL_PERSISTENT 26u /* > 0: the megakernel as a persistent grid of this many
                                                waves per CU pulling 64-path chunks (0 = one wave per
                                                64 paths, default); occupancy 8 runs at the 7-wave budget.
                                                Identical results. */
-#define DXRPT_OPT_MEGAKERNEL_LANES 27u /* paths per 64-lane megakernel wave: 64 (default), 32 or 16; each path
-                                          is then carried by 64/value lanes that shade it together and
-                                          trace its continuation and shadow rays concurrently (shorter
-                                          dependent-traversal chains on small frames).  Identical results. */
+#define DXRPT_OPT_MEGAKERNEL_LANES 27u /* paths per 64-lane megakernel wave: 0 = by frame size (default:
+                                          32 up to 400,000 paths -- a GPU's share of an 8-GPU 1080p frame --
+                                          else 64), 64, 32 or 16; each path is then carried by 64/value
+                                          lanes that shade it together and trace its continuation and
+                                          shadow rays concurrently (shorter dependent-traversal chains on
+                                          small frames).  Identical results. */
 #define DXRPT_OPT_BAKE_CHUNK 25u /* texels per dxrpt_bake_lightmap launch (default 2^21; bounds the
                                     per-texel shadow-slot buffers).  Identical results. */
 #define DXRPT_OPT_WAVE_CLOCKS 28u /* 1: with DXRPT_OPT_COUNT_TRAVERSAL, the megakernel census frame also

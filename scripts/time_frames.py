@@ -24,13 +24,15 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--share", type=int, default=1)
     ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--layout", default="bands", choices=["blocks", "bands", "blocks-raster"],
+                    help="screen partition of --share (blocks-raster: 8x8 tiles in raster order, block k -> rank k %% N)")
     ap.add_argument("--any-hit", type=int, default=None, help="MaxAnyHitPathLength override")
     ap.add_argument("--packet", type=int, default=None, help="DXRPT_OPT_PACKET_TRAVERSAL override")
     ap.add_argument("--occ", type=int, default=None, help="DXRPT_OPT_MEGAKERNEL_OCCUPANCY override")
     args = ap.parse_args()
     import torch
     import dxrpathtracer_amd as D
-    from dxrpathtracer_amd.distributed import band_layout
+    from dxrpathtracer_amd.distributed import screen_layout
     from dxrpathtracer_amd.tracer import DXRPathTracer
 
     name, W, H, L = CONFIGS[args.config]
@@ -46,8 +48,15 @@ def main():
     t.initialize_scene(sc, sky)
     t.build_rt_acceleration_structure()
     tiles, n = None, W * H
-    if args.share > 1:
-        lay = band_layout(W, H, args.share)
+    if args.layout == "blocks-raster":  # the whole frame as 8x8 block tiles in raster order (tile-count A/B)
+        from dxrpathtracer_amd import _abi as AA
+        tiles = [AA.Tile(x, y, 8, 8, (y // 8 * (W // 8) + x // 8) * 64, 8, 0) for y in range(0, H, 8) for x in range(0, W, 8)]
+        if args.share > 1:
+            tiles = tiles[args.rank::args.share]
+            tiles = [AA.Tile(t.x0, t.y0, 8, 8, 64 * k, 8, 0) for k, t in enumerate(tiles)]
+        n = 64 * len(tiles)
+    elif args.share > 1:
+        lay = screen_layout(W, H, args.share, args.layout)
         tiles, n = lay.rank_tiles(args.rank), lay.counts[args.rank]
     acc = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
     consts = [D.make_constants(sc, st, sky, W, H, s) for s in range(16)]
@@ -66,7 +75,7 @@ def main():
         torch.cuda.synchronize()
         rounds.append(a.elapsed_time(b) / args.frames)
     s = t.stats()
-    print(f"{args.label:24s} {args.config} share 1/{args.share} r{args.rank}: median {statistics.median(rounds):.4f} "
+    print(f"{args.label:24s} {args.config} share 1/{args.share} r{args.rank} {args.layout if args.share > 1 else ''}: median {statistics.median(rounds):.4f} "
           f"mean {statistics.mean(rounds):.4f} min {min(rounds):.4f} ms/frame  rays {s.radiance_rays + s.shadow_rays}",
           flush=True)
     t.close()

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
     ap.add_argument("--share", type=int, default=1)
     ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--layout", default="bands", choices=["blocks", "bands"])
     ap.add_argument("--frames", type=int, default=3, help="census frames (the last one is reported)")
     ap.add_argument("--json", default=None)
     ap.add_argument("--occ", type=int, default=0, help="megakernel occupancy (0: default by size)")
@@ -30,7 +31,7 @@ def main():
     import torch
     import dxrpathtracer_amd as D
     import dxrpathtracer_amd._abi as A
-    from dxrpathtracer_amd.distributed import band_layout
+    from dxrpathtracer_amd.distributed import screen_layout
     from dxrpathtracer_amd.tracer import DXRPathTracer
 
     name, W, H, L = CONFIGS[args.config]
@@ -42,7 +43,7 @@ def main():
     t.build_rt_acceleration_structure()
     tiles, n = None, W * H
     if args.share > 1:
-        lay = band_layout(W, H, args.share)
+        lay = screen_layout(W, H, args.share, args.layout)
         tiles, n = lay.rank_tiles(args.rank), lay.counts[args.rank]
     acc = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
@@ -69,7 +70,7 @@ def main():
         bw, bh = (tt.w + 7) // 8, (tt.h + 7) // 8
         for b in range(bw * bh):
             blocks.append((tt.x0 + (b % bw) * 8, tt.y0 + (b // bw) * 8))
-    res = {"config": args.config, "share": args.share, "rank": args.rank, "waves": int(len(wc)),
+    res = {"config": args.config, "share": args.share, "rank": args.rank, "layout": args.layout, "waves": int(len(wc)),
            "span_us": float(end.max()), "last_start_us": float(start.max()),
            "dur_us": {q: float(np.percentile(dur, p)) for q, p in (("min", 0), ("p50", 50), ("p90", 90), ("p99", 99),
                                                                       ("max", 100))},

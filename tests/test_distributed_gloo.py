@@ -22,7 +22,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, W, H, q):
+def _worker(rank, world, port, W, H, q, kind="bands"):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -30,12 +30,12 @@ def _worker(rank, world, port, W, H, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import dxrpathtracer_amd as D
-        from dxrpathtracer_amd.distributed import band_layout, gather_frame, source_index
+        from dxrpathtracer_amd.distributed import gather_frame, screen_layout, source_index
         from tests._common import oracle_scene, scene_bundle
         sc, sky = scene_bundle("boxtest")
         st = sc.settings(MaxPathLength=3)
         rtc = D.make_constants(sc, st, sky, W, H, 1)
-        lay = band_layout(W, H, world)
+        lay = screen_layout(W, H, world, kind)
         local = np.zeros((lay.max_count, 4), dtype=np.float32)
         orc = oracle_scene("boxtest")
         for t in lay.rank_tiles(rank):
@@ -51,13 +51,13 @@ def _worker(rank, world, port, W, H, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_band_gather_reproduces_single_rank_frame(world):
+@pytest.mark.parametrize("world,kind", [(2, "bands"), (2, "blocks"), (3, "blocks")])
+def test_band_gather_reproduces_single_rank_frame(world, kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    W, H = 48, 76  # 10 bands of 8 rows (last one partial)
-    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, q)) for r in range(world)]
+    W, H = 52, 76  # 10 bands of 8 rows / 7 x 10 blocks of 8 x 8, the last row and column partial
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, q, kind)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -75,8 +75,8 @@ def _worker_pipelined(rank, world, port, W, H, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from dxrpathtracer_amd.distributed import PipelinedGather, band_layout, source_index
-        lay = band_layout(W, H, world)
+        from dxrpathtracer_amd.distributed import PipelinedGather, screen_layout, source_index
+        lay = screen_layout(W, H, world, "blocks")
         full = torch.zeros((W * H, 4), dtype=torch.float32) if rank == 0 else None
         idx = torch.tensor(source_index(lay), dtype=torch.long) if rank == 0 else None
         pg = PipelinedGather(lay, rank, full, idx)
@@ -119,11 +119,29 @@ def test_pipelined_gather_delivers_every_frame(world):
 
 
 def test_band_partition_is_balanced():
-    # the busiest rank decides the frame time: at the metric's 1920x1080 the 8-row bands keep every
-    # rank within 1 % of the mean pixel count at 2, 4 and 8 ranks
+    # 8-row bands at the metric's 1920x1080: every rank within 1 % of the mean pixel count at 2, 4, 8 ranks
     from dxrpathtracer_amd.distributed import band_layout
     for world in (2, 4, 8):
         lay = band_layout(1920, 1080, world)
         assert sum(lay.counts) == 1920 * 1080
         assert max(lay.counts) <= 1.01 * (1920 * 1080 / world), (world, lay.counts)
         assert all(t.h % 8 == 0 for r in range(world) for t in lay.rank_tiles(r))
+
+
+def test_block_partition_covers_image_and_spreads_rows():
+    # the default partition: every pixel exactly once, equal block counts, each rank's blocks drawn
+    # from (nearly) every block row, so clustered expensive rows (foliage) are shared by all ranks
+    from dxrpathtracer_amd.distributed import block_layout, source_index
+    for W, H, world in ((1920, 1080, 8), (1920, 1080, 2), (1366, 767, 3), (64, 8, 8)):
+        lay = block_layout(W, H, world)
+        idx = source_index(lay)
+        assert sorted(idx) == sorted(set(idx)) and len(idx) == W * H
+        nblocks = [len(lay.rank_tiles(r)) for r in range(world)]
+        assert max(nblocks) - min(nblocks) <= 1
+        again = block_layout(W, H, world)  # deterministic
+        key = lambda L: [[(t.x0, t.y0, t.w, t.h, t.accum_offset) for t in L.rank_tiles(r)] for r in range(world)]
+        assert key(lay) == key(again)
+    lay = block_layout(1920, 1080, 8)
+    for r in range(8):
+        rows = {t.y0 // 8 for t in lay.rank_tiles(r)}
+        assert len(rows) >= 0.95 * 135

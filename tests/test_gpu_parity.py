@@ -15,7 +15,7 @@ import pytest
 import dxrpathtracer_amd as D
 import dxrpathtracer_amd._abi as A
 from dxrpathtracer_amd.tracer import DXRPathTracer
-from dxrpathtracer_amd.distributed import band_layout
+from dxrpathtracer_amd.distributed import band_layout, block_layout
 from tests._common import assert_parity, oracle_scene, scene_bundle
 
 pytestmark = pytest.mark.gpu
@@ -176,8 +176,8 @@ def test_tiling_is_bit_identical(torch_cuda):
     sc, _ = scene_bundle("sponza")
     st = sc.settings(MaxPathLength=3)
     full = gpu_render(torch, "sponza", W, H, st, 3).cpu().numpy().reshape(H, W, 4)
-    for world in (2, 3, 8):
-        lay = band_layout(W, H, world)
+    for world, lay_of in ((2, band_layout), (3, band_layout), (8, band_layout), (3, block_layout), (8, block_layout)):
+        lay = lay_of(W, H, world)
         for r in range(world):
             part = gpu_render(torch, "sponza", W, H, st, 3, tiles=lay.rank_tiles(r), n_out=lay.counts[r]).cpu().numpy()
             for t in lay.rank_tiles(r):

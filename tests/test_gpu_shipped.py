@@ -13,7 +13,7 @@ import pytest
 
 import dxrpathtracer_amd as D
 import dxrpathtracer_amd._abi as A
-from dxrpathtracer_amd.distributed import band_layout
+from dxrpathtracer_amd.distributed import screen_layout
 from dxrpathtracer_amd.tracer import DXRPathTracer
 from tests._common import assert_parity, oracle_scene, scene_bundle
 
@@ -132,22 +132,23 @@ def test_partial_last_wave_frame(torch_cuda):
     compare_crops("sponza", W, H, out, st, rtc, frame_crops(W, H), 0.0, "1366x767")
 
 
-@pytest.mark.parametrize("world,rank", [(8, 7), (2, 1)])
-def test_gpu_share_of_metric_frame(torch_cuda, world, rank):
-    # one rank's band share of the metric frame (what each GPU renders in bench.py --gpus N)
+@pytest.mark.parametrize("world,rank,kind", [(8, 7, "blocks"), (2, 1, "blocks"), (8, 2, "bands")])
+def test_gpu_share_of_metric_frame(torch_cuda, world, rank, kind):
+    # one rank's share of the metric frame (what each GPU renders in bench.py --gpus N)
     W, H = 1920, 1080
-    lay = band_layout(W, H, world)
+    lay = screen_layout(W, H, world, kind)
     tiles = lay.rank_tiles(rank)
     out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 3, 2, tiles=tiles, n_out=lay.counts[rank],
                                   check_kernel="megakernel")
-    where = {}
+    where = {}  # pixel -> row of the rank's slab
     for t in tiles:
         for yy in range(t.h):
-            where[t.y0 + yy] = (t.x0, t.accum_offset + yy * t.accum_pitch)
-    rows = sorted(where)
-    # crops inside the rank's rows: first band's corners, a middle band, the last band
-    mid = rows[len(rows) // 2]
-    crops = [(0, rows[0], 64, 1), (W - 64, rows[0], 64, 1), (W // 2, mid, 128, 1), (0, rows[-1], W, 1),
-             (1000, rows[-8], 64, 1), (300, rows[3], 200, 1)]
-    compare_crops("sponza", W, H, out, st, rtc, crops, 0.0, f"share {rank}/{world}",
-                  origin=lambda x, y: where[y][1] + (x - where[y][0]))
+            for xx in range(t.w):
+                where[(t.x0 + xx, t.y0 + yy)] = t.accum_offset + yy * t.accum_pitch + xx
+    # the rank's first, middle and last tiles, and a few more spread over its list (whole tiles)
+    picks = sorted({0, len(tiles) // 3, len(tiles) // 2, (2 * len(tiles)) // 3, len(tiles) - 2, len(tiles) - 1})
+    crops = [(tiles[i].x0, tiles[i].y0, tiles[i].w, tiles[i].h) for i in picks]
+    if kind == "bands":  # bands are whole rows: compare a 128-px window of each instead
+        crops = [(x0 + (k * 300) % (W - 128), y0, 128, h) for k, (x0, y0, w, h) in enumerate(crops)]
+    compare_crops("sponza", W, H, out, st, rtc, crops, 0.0, f"share {rank}/{world} {kind}",
+                  origin=lambda x, y: where[(x, y)])
