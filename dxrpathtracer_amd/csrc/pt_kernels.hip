@@ -211,6 +211,44 @@ PT_DEV Surface get_hit_surface(const SceneDev& S, uint32_t gtri, float b1, float
 }
 
 // AnyHitShader / ShadowAnyHitShader (RayTrace.hlsl:485-507): opacity.x < 0.35 -> IgnoreHit.
+// The opacity tap of AnyHitShader split in two, so several candidates' texel loads are in flight
+// together (traverse8_packet's two-triangle steps): issue computes the bilinear footprint and loads its
+// four texel words, finish decodes and filters channel r exactly as sample_tex_desc(...).r does.
+struct OpacityTap {
+    uint32_t w00, w10, w01, w11;  // texel words
+    uint32_t s0, s1;              // byte shift of column ix0 / ix1 (R8: x & 3; RGBA8: 0)
+    uint32_t lut;                 // decode table base (0 unorm, 256 sRGB)
+    float fx, fy;
+};
+
+PT_DEV OpacityTap opacity_issue(const SceneDev& S, const TexDesc td, float u, float v) {
+    float x = u * float(td.width) - 0.5f;
+    float y = v * float(td.height) - 0.5f;
+    float x0 = floorf(x), y0 = floorf(y);
+    OpacityTap t;
+    t.fx = x - x0;
+    t.fy = y - y0;
+    const int ix0 = wrap_coord(int(x0), td.width), ix1 = wrap_coord(int(x0) + 1, td.width);
+    const int iy0 = wrap_coord(int(y0), td.height), iy1 = wrap_coord(int(y0) + 1, td.height);
+    const bool r8 = td.fmt == DXRPT_TEX_R8_UNORM;
+    const uint32_t tiles_x = (td.width + (r8 ? kTexTileW8 : kTexTileW32) - 1u) / (r8 ? kTexTileW8 : kTexTileW32);
+    const uint32_t* T = S.texels + td.offset;
+    t.w00 = T[tex_tile_word(uint32_t(ix0), uint32_t(iy0), tiles_x, r8)];
+    t.w10 = T[tex_tile_word(uint32_t(ix1), uint32_t(iy0), tiles_x, r8)];
+    t.w01 = T[tex_tile_word(uint32_t(ix0), uint32_t(iy1), tiles_x, r8)];
+    t.w11 = T[tex_tile_word(uint32_t(ix1), uint32_t(iy1), tiles_x, r8)];
+    t.s0 = r8 ? (uint32_t(ix0) & 3u) * 8u : 0u;
+    t.s1 = r8 ? (uint32_t(ix1) & 3u) * 8u : 0u;
+    t.lut = td.fmt == DXRPT_TEX_RGBA8_SRGB ? 256u : 0u;
+    return t;
+}
+
+PT_DEV float opacity_finish(const SceneDev& S, const OpacityTap& t) {
+    const float a = lut_at(S, t.lut + ((t.w00 >> t.s0) & 0xFFu)), b = lut_at(S, t.lut + ((t.w10 >> t.s1) & 0xFFu));
+    const float c = lut_at(S, t.lut + ((t.w01 >> t.s0) & 0xFFu)), d = lut_at(S, t.lut + ((t.w11 >> t.s1) & 0xFFu));
+    return lerpf(lerpf(a, b, t.fx), lerpf(c, d, t.fx), t.fy);
+}
+
 PT_DEV bool alpha_accepts(const SceneDev& S, uint32_t geom, uint32_t gtri, float b1, float b2) {
     const GeoTex opacity = S.geoshade[geom].opacity;
     if (opacity.whf == 0u) return true;
@@ -307,6 +345,18 @@ PT_DEV bool test_tri_rec(const SceneDev& S, const TriRec& r, f3 o, f3 d, float t
     h.b2 = v;
     h.geom = geom;
     return kAnyHit;
+}
+
+// The geometric part of test_tri_rec: the triangle is a candidate if the ray hits it inside
+// [tmin, tmax] (any hit) or ahead of the current best (closest hit); alpha and acceptance follow.
+template <bool kAnyHit>
+PT_DEV bool tri_candidate(const TriRec& r, f3 o, f3 d, float tmin, float tmax, const HitRec& h, float& t, float& u,
+                          float& v) {
+    if (!intersect_triangle(o, d, ld3(r.p0), ld3(r.p1), ld3(r.p2), &t, &u, &v)) return false;
+    if (!(t >= tmin)) return false;
+    if (kAnyHit) return t <= tmax;
+    const uint32_t gtri = fbits(r.p0.w);
+    return t < h.t || (t == h.t && gtri < h.tri);
 }
 
 template <bool kAnyHit>
@@ -653,6 +703,30 @@ PT_DEV TriRec load_tri_uniform(const SceneDev& S, uint32_t rec) {
     return TriRec{f4(T[b + 0]), f4(T[b + 1]), f4(T[b + 2])};
 }
 
+// A triangle's opacity map and vertex UVs when the triangle is wave-uniform (packet traversal):
+// scalar loads of GeoShade::opacity and the three MeshVertex::UV of its vertex record.
+struct AlphaInputs {
+    GeoTex op;
+    float2 uv0, uv1, uv2;
+    PT_DEV float u(float b1, float b2) const { return bary_lerp(uv0.x, uv1.x, uv2.x, (1.0f - b1) - b2, b1, b2); }
+    PT_DEV float v(float b1, float b2) const { return bary_lerp(uv0.y, uv1.y, uv2.y, (1.0f - b1) - b2, b1, b2); }
+};
+typedef unsigned int U32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(4))) const U32x2 ConstU2;
+
+PT_DEV AlphaInputs alpha_inputs_uniform(const SceneDev& S, uint32_t geom, uint32_t gtri) {
+    ConstU2* G = (ConstU2*)(S.geoshade);   // NOLINT: 6 GeoTex per geometry, opacity last
+    ConstU2* V = (ConstU2*)(S.tri_verts);  // NOLINT: 3 x 64-B MeshVertex per triangle, UV = 8-B word 3
+    const U32x2 op = G[geom * 6u + 5u];
+    const U32x2 a = V[gtri * 24u + 3u], b = V[gtri * 24u + 11u], c = V[gtri * 24u + 19u];
+    AlphaInputs ai;
+    ai.op = GeoTex{op.x, op.y};
+    ai.uv0 = make_float2(__uint_as_float(a.x), __uint_as_float(a.y));
+    ai.uv1 = make_float2(__uint_as_float(b.x), __uint_as_float(b.y));
+    ai.uv2 = make_float2(__uint_as_float(c.x), __uint_as_float(c.y));
+    return ai;
+}
+
 PT_DEV uint32_t wave_or8(uint32_t m) {
     uint32_t u = 0;
 #pragma unroll
@@ -674,7 +748,11 @@ PT_DEV bool traverse8_from(const SceneDev& S, const Ray8& R, lds_int* stk, HitRe
 
 // kCount: node / triangle FETCHES are counted in *cnt (cnt[0] nodes, cnt[1] triangles) by the wave's
 // first live lane -- a packet fetches each node and triangle once per wave (scalar loads).
-template <bool kAnyHit, bool kCount = false>
+// kPair: leaf triangles two at a time (both records, both geometric tests against the bound at the
+// step's start -- a superset of the sequential candidates --, both opacity taps in flight, acceptance in
+// order with the live bound: the hits of testing them one after the other, with one alpha round trip
+// per pair).  Used by the path-group kernel, whose small frames end with alpha-tested foliage waves.
+template <bool kAnyHit, bool kCount = false, bool kPair = false>
 PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, bool live, HitRec& h,
                              uint32_t switch_pct = 0u, lds_int* stk = nullptr, uint32_t* cnt = nullptr) {
     Ray8 R;
@@ -715,7 +793,56 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
             tbits |= ((1u << (m >> 5)) - 1u) << (m & 31u);
         }
         const uint32_t tbase = W.w1.y;
-        while (tbits) {
+        while (kPair && tbits) {
+            const uint32_t b0 = uint32_t(__builtin_ctz(tbits));
+            tbits &= tbits - 1u;
+            const bool two = tbits != 0u;
+            const uint32_t b1 = two ? uint32_t(__builtin_ctz(tbits)) : b0;
+            if (two) tbits &= tbits - 1u;
+            const TriRec r0 = load_tri_uniform(S, tbase + b0), r1 = load_tri_uniform(S, tbase + b1);
+            if (counter) cnt[1] += two ? 2u : 1u;
+            float t0 = 0.0f, u0 = 0.0f, v0 = 0.0f, t1 = 0.0f, u1 = 0.0f, v1 = 0.0f;
+            const bool c0 = live && tri_candidate<kAnyHit>(r0, R.o, R.d, R.tmin, R.tmax, h, t0, u0, v0);
+            const bool c1 = two && live && tri_candidate<kAnyHit>(r1, R.o, R.d, R.tmin, R.tmax, h, t1, u1, v1);
+            // AnyHitShader (RayTrace.hlsl:485-507) for candidates on alpha-tested geometry
+            const bool n0 = c0 && R.alpha && !(fbits(r0.p2.w) & kTriOpaque);
+            const bool n1 = c1 && R.alpha && !(fbits(r1.p2.w) & kTriOpaque);
+            float o0 = 1.0f, o1 = 1.0f;
+            const bool any0 = __ballot(n0) != 0ull, any1 = __ballot(n1) != 0ull;
+            if (any0 || any1) {
+                OpacityTap q0{}, q1{};
+                bool m0 = false, m1 = false;
+                if (any0) {
+                    const AlphaInputs ai = alpha_inputs_uniform(S, fbits(r0.p1.w), fbits(r0.p0.w));
+                    m0 = n0 && ai.op.whf != 0u;
+                    if (m0) q0 = opacity_issue(S, tex_desc(ai.op), ai.u(u0, v0), ai.v(u0, v0));
+                }
+                if (any1) {
+                    const AlphaInputs ai = alpha_inputs_uniform(S, fbits(r1.p1.w), fbits(r1.p0.w));
+                    m1 = n1 && ai.op.whf != 0u;
+                    if (m1) q1 = opacity_issue(S, tex_desc(ai.op), ai.u(u1, v1), ai.v(u1, v1));
+                }
+                if (m0) o0 = opacity_finish(S, q0);
+                if (m1) o1 = opacity_finish(S, q1);
+            }
+            if (c0 && !(o0 < 0.35f) && (kAnyHit || t0 < h.t || (t0 == h.t && fbits(r0.p0.w) < h.tri))) {
+                h.t = t0;
+                h.tri = fbits(r0.p0.w);
+                h.b1 = u0;
+                h.b2 = v0;
+                h.geom = fbits(r0.p1.w);
+                if (kAnyHit) live = false;  // occluded
+            }
+            if (c1 && live && !(o1 < 0.35f) && (kAnyHit || t1 < h.t || (t1 == h.t && fbits(r1.p0.w) < h.tri))) {
+                h.t = t1;
+                h.tri = fbits(r1.p0.w);
+                h.b1 = u1;
+                h.b2 = v1;
+                h.geom = fbits(r1.p1.w);
+                if (kAnyHit) live = false;
+            }
+        }
+        while (!kPair && tbits) {
             const uint32_t b = uint32_t(__builtin_ctz(tbits));
             tbits &= tbits - 1u;
             const TriRec r = load_tri_uniform(S, tbase + b);
@@ -1798,7 +1925,7 @@ PT_DEV float4 trace_path_group(const KArgs& A, uint32_t slot_p, uint32_t pix, f3
         count_rays(A.F.counters + uint32_t(d) * kQueueShards, quiet ? 0u : 1u);
         if (d == 1) {  // the primary ray: every member traces it (packets while the wave is full)
             if (packet)
-                traverse8_packet<false>(A.S, org, dir, 0.0f, tmax, d <= set.MaxAnyHitPathLength, true, h);
+                traverse8_packet<false, false, true>(A.S, org, dir, 0.0f, tmax, d <= set.MaxAnyHitPathLength, true, h);
             else
                 traverse<8, false, false>(A.S, org, dir, 0.0f, tmax, d <= set.MaxAnyHitPathLength, stk, h, nv, nt);
         }
