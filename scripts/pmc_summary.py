@@ -56,6 +56,11 @@ def main(prof, rnd):
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             e["hbm_read_bytes_raw"] = c["FETCH_SIZE"] * 1024
             e["hbm_bytes_per_launch"] = c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024
+        if "WRITE_SIZE" in c:
+            e["hbm_write_bytes"] = c["WRITE_SIZE"] * 1024
+        if c.get("SQ_WAVE_CYCLES"):
+            e["wait_any_frac"] = c.get("SQ_WAIT_ANY", 0.0) / c["SQ_WAVE_CYCLES"]
+            e["issue_frac"] = c.get("SQ_ACTIVE_INST_ANY", 0.0) / c["SQ_WAVE_CYCLES"]
         if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c and c["TCC_HIT_sum"] + c["TCC_MISS_sum"] > 0:
             e["l2_hit_rate"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
         out["kernels"][k] = e
@@ -66,7 +71,9 @@ def main(prof, rnd):
     # (packet and per-lane variants), launch-weighted
     for kind, prefixes in (("k_trace", ("k_trace<false", "k_trace_packet")),
                            ("k_shadow", ("k_shadow<false", "k_shadow_packet")), ("k_path", ("k_path<",))):
-        cands = [k for k in out["kernels"] if k.startswith(prefixes)]
+        # k_path<..., true> is the bench's one instrumented census frame (kCount), not a timed launch
+        cands = [k for k in out["kernels"] if k.startswith(prefixes)
+                 and not (kind == "k_path" and k.endswith(", true>"))]
         if not cands:
             continue
         calls = sum(out["kernels"][k].get("calls", 0) for k in cands)
@@ -76,12 +83,23 @@ def main(prof, rnd):
             if not calls or any(v is None for _, v in vals):
                 return None
             return sum(c * v for c, v in vals) / calls
+
+        def wavg_pmc(counter):
+            vals = [(out["kernels"][k].get("calls", 0), out["kernels"][k]["pmc"].get(counter)) for k in cands]
+            if not calls or any(v is None for _, v in vals):
+                return None
+            return sum(c * v for c, v in vals) / calls
         with open(f"profiles/{rnd}_pmc_{kind}.json", "w") as f:
             json.dump({"config": CONFIG, "kernel": " + ".join(sorted(cands)), "calls": calls,
                        "avg_ms": (sum(out["kernels"][k].get("total_ms", 0.0) for k in cands) / calls) if calls else None,
                        "per_kernel_avg_ms": {k: out["kernels"][k].get("avg_ms") for k in cands},
                        "hbm_bytes_per_launch": wavg("hbm_bytes_per_launch"),
                        "hbm_read_bytes_raw": wavg("hbm_read_bytes_raw"), "l2_hit_rate": wavg("l2_hit_rate"),
+                       "hbm_write_bytes_per_launch": wavg("hbm_write_bytes"),
+                       "wait_any_per_wave_cycle": wavg("wait_any_frac"),
+                       "active_inst_any_per_wave_cycle": wavg("issue_frac"),
+                       "counters_per_launch": ({c: wavg_pmc(c) for c in sorted(out["kernels"][cands[0]]["pmc"])}
+                                               if cands else {}),
                        "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 16-B/lane read correction) + WRITE_SIZE KiB x1024"},
                       f, indent=2)
     for src in ("kt/run_kernel_stats.csv",):

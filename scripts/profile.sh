@@ -9,7 +9,8 @@ B="python3 bench.py --no-cpu-baseline"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- $B --steps 32 --warmup 5 \
     > $OUT/kt_bench.json 2> $OUT/kt.err || exit $?
 echo "kernel trace ok"; cat $OUT/kt_bench.json
-for pmc in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM" "SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE"; do
+for pmc in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM" "SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE" \
+           "SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_FLAT SQ_WAIT_INST_LDS"; do
   tag=$(echo $pmc | tr ' ' '_')
   timeout -k 10 600 rocprofv3 --pmc $pmc -d $OUT/pmc_$tag -o run --output-format csv -- $B --steps 8 --warmup 2 \
       > $OUT/pmc_$tag.json 2> $OUT/pmc_$tag.err || { echo "pmc $pmc failed rc=$?"; tail -5 $OUT/pmc_$tag.err; exit 1; }

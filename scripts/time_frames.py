@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--any-hit", type=int, default=None, help="MaxAnyHitPathLength override")
     ap.add_argument("--packet", type=int, default=None, help="DXRPT_OPT_PACKET_TRAVERSAL override")
     ap.add_argument("--occ", type=int, default=None, help="DXRPT_OPT_MEGAKERNEL_OCCUPANCY override")
+    ap.add_argument("--max-path", type=int, default=None, help="MaxPathLength override (a cost breakdown by depth)")
     args = ap.parse_args()
     import torch
     import dxrpathtracer_amd as D
@@ -36,6 +37,7 @@ def main():
     from dxrpathtracer_amd.tracer import DXRPathTracer
 
     name, W, H, L = CONFIGS[args.config]
+    L = L if args.max_path is None else args.max_path
     sc = D.Scene(name)
     st = sc.settings(MaxPathLength=L, **({} if args.any_hit is None else {"MaxAnyHitPathLength": args.any_hit}))
     sky = D.make_sky(st)
@@ -75,7 +77,7 @@ def main():
         torch.cuda.synchronize()
         rounds.append(a.elapsed_time(b) / args.frames)
     s = t.stats()
-    print(f"{args.label:24s} {args.config} share 1/{args.share} r{args.rank} {args.layout if args.share > 1 else ''}: median {statistics.median(rounds):.4f} "
+    print(f"{args.label:24s} {args.config}{'' if args.max_path is None else f' L={L}'} share 1/{args.share} r{args.rank} {args.layout if args.share > 1 else ''}: median {statistics.median(rounds):.4f} "
           f"mean {statistics.mean(rounds):.4f} min {min(rounds):.4f} ms/frame  rays {s.radiance_rays + s.shadow_rays}",
           flush=True)
     t.close()
