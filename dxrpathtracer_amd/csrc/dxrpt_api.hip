@@ -653,7 +653,14 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
             std::memcpy(&r.p2[3], &flags, 4);
         }
         if (ctx->opt_width == 8) {
-            ctx->d_nodes8.upload(res.nodes8.data(), res.nodes8.size() * sizeof(Bvh8Node));
+            if (kNode8Stride == sizeof(Bvh8Node)) {
+                ctx->d_nodes8.upload(res.nodes8.data(), res.nodes8.size() * sizeof(Bvh8Node));
+            } else {  // padded device layout (pt_layout.h kNode8Stride)
+                std::vector<uint8_t> padded(res.nodes8.size() * size_t(kNode8Stride), 0u);
+                for (size_t i = 0; i < res.nodes8.size(); ++i)
+                    std::memcpy(padded.data() + i * kNode8Stride, &res.nodes8[i], sizeof(Bvh8Node));
+                ctx->d_nodes8.upload(padded.data(), padded.size());
+            }
         } else {
             ctx->d_nodes.upload(res.nodes.data(), res.nodes.size() * sizeof(BvhNode));
         }

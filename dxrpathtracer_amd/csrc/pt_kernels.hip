@@ -491,7 +491,7 @@ struct NodeCache {
 
 PT_DEV Node8Words load_node8(const SceneDev& S, uint32_t node) {
 #if DXRPT_PIN_LOADS
-    const uint4* N = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(S.nodes8) + size_t(node) * 80u);
+    const uint4* N = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(S.nodes8) + size_t(node) * kNode8Stride);
     const Node8Words w{N[0], N[1], N[2], N[3], N[4]};
     // the leaf metadata (w1.zw) is otherwise loaded behind the leaf-hit branch: a second round trip
     asm volatile("" ::"v"(w.w0.x), "v"(w.w0.y), "v"(w.w0.z), "v"(w.w0.w), "v"(w.w1.x), "v"(w.w1.y), "v"(w.w1.z),
@@ -500,14 +500,14 @@ PT_DEV Node8Words load_node8(const SceneDev& S, uint32_t node) {
     return w;
 #else
     const uint4* N = reinterpret_cast<const uint4*>(S.nodes8);
-    return Node8Words{N[node * 5 + 0], N[node * 5 + 1], N[node * 5 + 2], N[node * 5 + 3], N[node * 5 + 4]};
+    return Node8Words{N[node * kNode8Words + 0], N[node * kNode8Words + 1], N[node * kNode8Words + 2], N[node * kNode8Words + 3], N[node * kNode8Words + 4]};
 #endif
 }
 
 PT_DEV Node8Words load_node8(const SceneDev& S, const NodeCache& nc, uint32_t node) {
     if (node < nc.n) {
         const uint4* L = nc.lds;
-        return Node8Words{L[node * 5 + 0], L[node * 5 + 1], L[node * 5 + 2], L[node * 5 + 3], L[node * 5 + 4]};
+        return Node8Words{L[node * kNode8Words + 0], L[node * kNode8Words + 1], L[node * kNode8Words + 2], L[node * kNode8Words + 3], L[node * kNode8Words + 4]};
     }
     return load_node8(S, node);
 }
@@ -515,7 +515,7 @@ PT_DEV Node8Words load_node8(const SceneDev& S, const NodeCache& nc, uint32_t no
 // Copies the top `n` nodes into `lds` (all threads of the workgroup; ends with a barrier).
 PT_DEV NodeCache node_cache_fill(const SceneDev& S, uint4* lds, uint32_t n) {
     const uint4* N = reinterpret_cast<const uint4*>(S.nodes8);
-    for (uint32_t j = threadIdx.x; j < n * 5u; j += blockDim.x) lds[j] = N[j];
+    for (uint32_t j = threadIdx.x; j < n * kNode8Words; j += blockDim.x) lds[j] = N[j];
     __syncthreads();
     return NodeCache{lds, n};
 }
@@ -693,7 +693,7 @@ PT_DEV float4 f4(U32x4 v) {
 
 PT_DEV Node8Words load_node8_uniform(const SceneDev& S, uint32_t node) {
     ConstU4* N = (ConstU4*)(S.nodes8);  // NOLINT: generic -> constant address space
-    const uint32_t b = node * 5u;
+    const uint32_t b = node * kNode8Words;
     return Node8Words{u4(N[b + 0]), u4(N[b + 1]), u4(N[b + 2]), u4(N[b + 3]), u4(N[b + 4])};
 }
 
@@ -1715,6 +1715,18 @@ PT_DEV void count_rays(uint32_t* counters, uint32_t n) {
 #ifndef DXRPT_SHADOW_MODE
 #define DXRPT_SHADOW_MODE 0
 #endif
+// Memory-overlap mode of the megakernel's per-lane traversals (traverse8_pipe kPipe bits: 1 triangle
+// pairs, 2 next node loaded before the current node's triangles); closest hit / any hit.
+// 1: the depth-1 packet shadow traversal takes only sun rays (0: slot 0 whatever its kind, the r01-r02 rule).
+#ifndef DXRPT_SUN0_CHECK
+#define DXRPT_SUN0_CHECK 1
+#endif
+#ifndef DXRPT_MEGA_PIPE_CH
+#define DXRPT_MEGA_PIPE_CH 0
+#endif
+#ifndef DXRPT_MEGA_PIPE_AH
+#define DXRPT_MEGA_PIPE_AH 0
+#endif
 
 // One path from its first ray (PathLength 1) to its end: per depth the closest hit, path_vertex and
 // the vertex's shadow rays in slot order -- the megakernel's per-thread loop, shared by k_path (camera
@@ -1745,7 +1757,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
         if (d == 1 && (packet & 1u))  // coherent primary rays: wave-coherent traversal (same results)
             traverse8_packet<false, kCount>(A.S, org, dir, tmin1, tmax, d <= set.MaxAnyHitPathLength, true, h, 0u, nullptr, cnt);
         else
-            traverse<8, false, kCount>(A.S, org, dir, d == 1 ? tmin1 : kRayTMin, tmax, d <= set.MaxAnyHitPathLength, stk, h,
+            traverse<8, false, kCount, DXRPT_MEGA_PIPE_CH>(A.S, org, dir, d == 1 ? tmin1 : kRayTMin, tmax, d <= set.MaxAnyHitPathLength, stk, h,
                                        cnt[0], cnt[1], nc);
         VertexIn V;
         V.inOrigin = org;
@@ -1758,7 +1770,9 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
 #if DXRPT_SHADOW_MODE == 0
         VertexOut O;
         uint32_t nsh = 0;
-        path_vertex(A, d, V, [&](int, f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
+        bool sun0 = false;  // slot 0 holds the sun's shadow ray (the sun is emitted first when at all)
+        path_vertex(A, d, V, [&](int kind, f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
+            sun0 |= kind == kShadowSun || !DXRPT_SUN0_CHECK;
             emit_shadow(A, slot_p, nsh, o, dd, tmn, tmx, c, fo);
         }, O);
         count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, nsh);
@@ -1766,8 +1780,10 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
         rad.y += thr.y * O.local.y;
         rad.z += thr.z * O.local.z;
         // ShadowHit/Miss/AnyHit: contribution * visibility, slot by slot.  The wave walks the slots
-        // together; at depth 1 (packet bit 1) slot 0 -- the sun shadow rays of an 8x8 pixel block's
-        // primary hits: one direction, nearby origins -- takes the wave-coherent traversal.
+        // together; at depth 1 (packet bit 1) the sun shadow rays of an 8x8 pixel block's primary hits
+        // -- one direction, nearby origins -- take the wave-coherent traversal.  A lane whose sun term
+        // is zero has another kind of ray in slot 0 (a spot light's, or at MaxPathLength 2 the sky
+        // visibility ray, random directions): it traces per lane, after the packet.
         for (uint32_t k = 0; __ballot(k < nsh) != 0ull; ++k) {
             const bool live = k < nsh;
             const size_t slot = size_t(k) * A.F.qsize + slot_p;
@@ -1779,10 +1795,12 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
             }
             HitRec hs;
             bool occluded = false;
-            if (d == 1 && k == 0 && (packet & 2u))
-                occluded = traverse8_packet<true, kCount>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live, hs, 0u, nullptr, cnt + 2);
-            else if (live)
-                occluded = traverse<8, true, kCount>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stk, hs, cnt[2], cnt[3], nc);
+            const bool pk = d == 1 && k == 0 && (packet & 2u);
+            if (pk)
+                occluded = traverse8_packet<true, kCount>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live && sun0, hs,
+                                                          0u, nullptr, cnt + 2);
+            if (live && !(pk && sun0))
+                occluded = traverse<8, true, kCount, DXRPT_MEGA_PIPE_AH>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stk, hs, cnt[2], cnt[3], nc);
             if (live) {
                 rad.x += occluded ? c4.x * 0.0f : c4.x;
                 rad.y += occluded ? c4.y * 0.0f : c4.y;
@@ -1828,7 +1846,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
             if (d == 1 && (packet & 2u))
                 occluded = traverse8_packet<true, kCount>(A.S, shOrg, sunD, kRayTMin, kFP32Max, sunAlpha, hasSun, hs, 0u, nullptr, cnt + 2);
             else if (hasSun)
-                occluded = traverse<8, true, kCount>(A.S, shOrg, sunD, kRayTMin, kFP32Max, sunAlpha, stk, hs, cnt[2], cnt[3], nc);
+                occluded = traverse<8, true, kCount, DXRPT_MEGA_PIPE_AH>(A.S, shOrg, sunD, kRayTMin, kFP32Max, sunAlpha, stk, hs, cnt[2], cnt[3], nc);
             if (hasSun) {
                 rad.x += occluded ? cSun.x * 0.0f : cSun.x;
                 rad.y += occluded ? cSun.y * 0.0f : cSun.y;
@@ -1841,7 +1859,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
                 const float4 o4 = A.F.sh_org[slot], d4 = A.F.sh_dir[slot], c4 = A.F.sh_con[slot];
                 HitRec hs;
                 const bool occluded =
-                    traverse<8, true, kCount>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stk, hs, cnt[2], cnt[3], nc);
+                    traverse<8, true, kCount, DXRPT_MEGA_PIPE_AH>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stk, hs, cnt[2], cnt[3], nc);
                 rad.x += occluded ? c4.x * 0.0f : c4.x;
                 rad.y += occluded ? c4.y * 0.0f : c4.y;
                 rad.z += occluded ? c4.z * 0.0f : c4.z;
@@ -1849,7 +1867,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
         }
         if (hasSky) {
             HitRec hs;
-            const bool occluded = traverse<8, true, kCount>(A.S, shOrg, skyDir, kRayTMin, kFP32Max, skyAlpha, stk, hs, cnt[2], cnt[3], nc);
+            const bool occluded = traverse<8, true, kCount, DXRPT_MEGA_PIPE_AH>(A.S, shOrg, skyDir, kRayTMin, kFP32Max, skyAlpha, stk, hs, cnt[2], cnt[3], nc);
             rad.x += occluded ? cSky.x * 0.0f : cSky.x;
             rad.y += occluded ? cSky.y * 0.0f : cSky.y;
             rad.z += occluded ? cSky.z * 0.0f : cSky.z;
@@ -2244,7 +2262,7 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
             else hipLaunchKernelGGL((k_path<5, true>), dim3(gp), dim3(tb), ldsm, stream, A);
         }
         else if (A.P.lds_nodes) {
-            const size_t ldsn = ldsm + size_t(A.P.lds_nodes) * 80u;
+            const size_t ldsn = ldsm + size_t(A.P.lds_nodes) * kNode8Stride;
             if (fp.megakernel_occupancy >= 7) hipLaunchKernelGGL((k_path<7, false, true>), dim3(gm), dim3(tb), ldsn, stream, A);
             else if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_path<6, false, true>), dim3(gm), dim3(tb), ldsn, stream, A);
             else if (fp.megakernel_occupancy == 5) hipLaunchKernelGGL((k_path<5, false, true>), dim3(gm), dim3(tb), ldsn, stream, A);
@@ -2276,7 +2294,7 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
     const uint32_t gst_full = (fp.num_paths * fb.shadow_slots + tb - 1u) / tb;
     const uint32_t gst = fp.shadow_grid ? std::min<uint32_t>(gst_full, fp.shadow_grid * (kBlock / tb)) : gst_full;
     const size_t ldst = size_t(scene.stack_ints) * tb * sizeof(int);
-    const size_t ldsc = ldst + size_t(A.P.lds_nodes) * 80u;  // + the node cache (uncounted BVH8 kernels)
+    const size_t ldsc = ldst + size_t(A.P.lds_nodes) * kNode8Stride;  // + the node cache (uncounted BVH8 kernels)
     const bool w8 = scene.width == 8;
     const bool pers = w8 && fp.chunks_per_wave > 0;
     const uint32_t gp = pers ? pool_grid(fp.num_paths, fp.chunks_per_wave) : 0u;

@@ -59,6 +59,14 @@ struct Bvh8Node {
     uint8_t qhi[3][8];
 };
 static_assert(sizeof(Bvh8Node) == 80, "Bvh8Node must be 80 B");
+// Device stride of a node: 80 (packed) or 128 (one node per 128-B cache line, 48 B of padding; the
+// A/B of DESIGN.md §7).  The builder's array is always packed; the upload pads.
+#ifndef DXRPT_NODE_STRIDE
+#define DXRPT_NODE_STRIDE 80
+#endif
+constexpr uint32_t kNode8Stride = DXRPT_NODE_STRIDE;
+constexpr uint32_t kNode8Words = kNode8Stride / 16u;  // 16-B words
+static_assert(kNode8Stride == 80u || kNode8Stride == 128u, "node stride 80 or 128");
 
 constexpr int kMaxLeafTris8 = 3;
 constexpr int kTraversalStack8 = 16;  // group-stack entries per lane; the builder caps BVH8 depth to fit.
