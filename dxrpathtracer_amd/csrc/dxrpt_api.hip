@@ -123,6 +123,13 @@ struct dxrpt_ctx {
     DevBuf d_wclock;  // 2 x u64 per wave (DXRPT_OPT_WAVE_CLOCKS)
     bool opt_wave_clocks = false;
     uint32_t wclock_waves = 0;
+    // DXRPT_OPT_WAVE_ORDER: per wave slot, the last frame's duration and the order built from it
+    uint32_t opt_wave_order = 2;  // 0 off, 1 on, 2 by frame size (see render)
+    DevBuf d_wave_cost, d_wave_order, d_wave_hist;  // hist: 2 frames x (histogram, cursor) x kWaveClasses
+    uint32_t order_parity = 0;
+    uint64_t order_key = 0;     // (waves, lanes, tiles generation) the order was built for
+    bool order_ready = false;   // d_wave_order holds an order for order_key
+    uint64_t tiles_gen = 0;     // bumped whenever the tile list changes
     DevBuf d_spill;  // BVH8 traversal stack entries beyond the LDS part (deep trees only)
     DevBuf d_bake_list;  // live lightmap texels of the last bake pass + their count
     // kernel timing: a ring of per-frame event sets, harvested lazily
@@ -490,6 +497,10 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
             ctx->opt_packet_switch = uint32_t(value);
         } else if (option == DXRPT_OPT_WAVE_CLOCKS) {
             ctx->opt_wave_clocks = value != 0;
+        } else if (option == DXRPT_OPT_WAVE_ORDER) {
+            require(value <= 2, "dxrpt_set_option: wave order must be 0, 1 or 2");
+            ctx->opt_wave_order = uint32_t(value);
+            ctx->order_ready = false;
         } else if (option == DXRPT_OPT_MEGAKERNEL_PATHS) {
             ctx->opt_mega_paths = value > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(value);
         } else if (option == DXRPT_OPT_MEGAKERNEL_OCCUPANCY) {
@@ -744,6 +755,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             ctx->d_tiles.upload(tl.data(), tl.size() * sizeof(dxrpt_tile));
             ctx->d_tile_prefix.upload(prefix.data(), prefix.size() * sizeof(uint32_t));
             ctx->tiles_cache = tl;
+            ++ctx->tiles_gen;
         }
         uint32_t nl = useLights ? rtc->NumLights : 0u;
         if (nl) {
@@ -768,6 +780,9 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.height = height;
         fp.trav = nullptr;
         fp.wave_clock = nullptr;
+        fp.wave_order = nullptr;
+        fp.wave_cost = nullptr;
+        fp.wave_hist = nullptr;
         // 32 KiB of LDS per 256-thread workgroup -> 5 resident workgroups per CU (160 KiB)
         fp.chunks_per_wave = ctx->opt_trav_mode == 1 ? ctx->opt_chunks : 0u;
         fp.refill_lanes = ctx->opt_refill;
@@ -815,6 +830,32 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
                 fp.wave_clock = ctx->d_wclock.as<unsigned long long>();
             }
         }
+        // cost-ordered waves (default megakernel schedules only: not the census, persistent or LDS-node ones)
+        // By frame size (2): frames of at most 3 rounds of resident waves, whose end is a large part of
+        // their time (a GPU's share of a multi-GPU frame, 720p: -10..-14 %); a full 1080p frame (4.5
+        // rounds) keeps path order, where concurrent neighbouring blocks share more cache than the
+        // shorter tail saves (profiles/r02_ab_wave_order.txt).
+        uint32_t order_waves = 0;
+        const uint32_t waves = lanes < 64u ? (paths + lanes - 1u) / lanes : (paths + 63u) / 64u;
+        const uint64_t slots = uint64_t(ctx->num_cus) * 4u * fp.megakernel_occupancy;
+        const bool order_on = ctx->opt_wave_order == 1 || (ctx->opt_wave_order == 2 && waves <= 3u * slots);
+        const bool order_kernel = lanes < 64u || (fp.megakernel_occupancy >= 4u && fp.megakernel_occupancy <= 7u);
+        if (order_on && order_kernel && fp.megakernel && !ctx->opt_count && !fp.mega_persistent && !ctx->opt_lds_nodes) {
+            order_waves = waves;
+            const uint64_t key = (uint64_t(order_waves) << 32) ^ (uint64_t(lanes) << 24) ^ ctx->tiles_gen;
+            ctx->d_wave_cost.ensure(size_t(order_waves) * sizeof(uint32_t));
+            ctx->d_wave_order.ensure(size_t(order_waves) * sizeof(uint32_t));
+            ctx->d_wave_hist.ensure(4 * kWaveClasses * sizeof(uint32_t));
+            if (key != ctx->order_key || !ctx->order_ready) {  // (re)start: path order, zeroed histograms
+                ctx->order_key = key;
+                ctx->order_ready = false;
+                ctx->order_parity = 0;
+                HIP_CHECK(hipMemsetAsync(ctx->d_wave_hist.p, 0, 4 * kWaveClasses * sizeof(uint32_t), static_cast<hipStream_t>(stream)));
+            }
+            fp.wave_cost = ctx->d_wave_cost.as<uint32_t>();
+            fp.wave_hist = ctx->d_wave_hist.as<uint32_t>() + ctx->order_parity * 2 * kWaveClasses;
+            fp.wave_order = ctx->order_ready ? ctx->d_wave_order.as<uint32_t>() : nullptr;
+        }
         const int L = settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength;
         hipEvent_t* ev = nullptr;
         if (ctx->opt_timing) {
@@ -845,6 +886,15 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             aux = ctx->aux;
         }
         HIP_CHECK(launch_frame(sd, ctx->fb, fp, s, ev, aux, aux ? ctx->fork_ev.data() : nullptr));
+        if (order_waves) {  // the next frame's order from this frame's wave classes (after the frame events)
+            uint32_t* h = ctx->d_wave_hist.as<uint32_t>();
+            uint32_t* cur = h + ctx->order_parity * 2 * kWaveClasses;
+            uint32_t* nxt = h + (1u - ctx->order_parity) * 2 * kWaveClasses;
+            HIP_CHECK(launch_wave_order(fp.wave_cost, cur, cur + kWaveClasses, nxt, nxt + kWaveClasses,
+                                        ctx->d_wave_order.as<uint32_t>(), order_waves, s));
+            ctx->order_ready = true;
+            ctx->order_parity ^= 1u;
+        }
         ctx->last_stream = s;
         ctx->last_L = settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength;
         std::memset(&ctx->last, 0, sizeof(ctx->last));

@@ -143,7 +143,17 @@ struct FrameParams {
     uint32_t mega_lanes;             // k_path: paths per 64-lane wave (64, 32, 16); lanes >= mega_lanes
                                      // re-trace lane (l mod mega_lanes)'s path and write nothing
     uint32_t num_cus;
+    // DXRPT_OPT_WAVE_ORDER (default megakernel schedules): wave w of the launch traces the paths of wave
+    // slot wave_order[w] (a permutation, costliest first, built from the previous frame; null:
+    // identity).  Non-null wave_cost: each wave slot's duration class (kWaveClasses log-scale classes
+    // of its s_memrealtime span, 0 = costliest) goes to wave_cost[slot] and is counted in
+    // wave_hist[class].
+    const uint32_t* wave_order;
+    uint32_t* wave_cost;
+    uint32_t* wave_hist;
 };
+
+constexpr uint32_t kWaveClasses = 256;
 
 // Kernel sequence of one frame: raygen, then (trace, shade, shadow, resolve) per depth 1..L-1, then
 // accumulate.  With `aux` and 2 * kMaxDepthQueues `fork_ev` events, each depth's any-hit pass runs on
@@ -152,6 +162,12 @@ struct FrameParams {
 // accumulate is bracketed by events ev[2i], ev[2i+1] on the stream it runs on.  A megakernel frame
 // (fp.megakernel) records ev[0], ev[1] around its single k_path launch.
 inline int frame_event_count(int L) { return 2 * (2 + 4 * (L - 1)); }
+// Builds `order` (n wave slots, costliest first) from the classes in `cls` and their histogram `hist`
+// (kWaveClasses counts) with `cursor` (kWaveClasses zeros) as scratch, and zeroes `hist_next` and
+// `cursor_next` (the next frame's).  Order within a class is unspecified: it only schedules.
+hipError_t launch_wave_order(const uint32_t* cls, const uint32_t* hist, uint32_t* cursor, uint32_t* hist_next,
+                             uint32_t* cursor_next, uint32_t* order, uint32_t n, hipStream_t stream);
+
 hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream,
                         hipEvent_t* ev, hipStream_t aux = nullptr, hipEvent_t* fork_ev = nullptr);
 

@@ -1717,6 +1717,11 @@ PT_DEV void count_rays(uint32_t* counters, uint32_t n) {
 #endif
 // Memory-overlap mode of the megakernel's per-lane traversals (traverse8_pipe kPipe bits: 1 triangle
 // pairs, 2 next node loaded before the current node's triangles); closest hit / any hit.
+// Diagnostic builds only (never shipped; they change the image): 1 = shadow rays are not traced
+// (every shadow ray unoccluded), to price their share of a frame.
+#ifndef DXRPT_DIAG_NO_SHADOW
+#define DXRPT_DIAG_NO_SHADOW 0
+#endif
 // 1: the depth-1 packet shadow traversal takes only sun rays (0: slot 0 whatever its kind, the r01-r02 rule).
 #ifndef DXRPT_SUN0_CHECK
 #define DXRPT_SUN0_CHECK 1
@@ -1727,6 +1732,46 @@ PT_DEV void count_rays(uint32_t* counters, uint32_t n) {
 #ifndef DXRPT_MEGA_PIPE_AH
 #define DXRPT_MEGA_PIPE_AH 0
 #endif
+
+// DXRPT_CHAIN_SHADOWS: a lane's per-lane shadow rays (slots k0 .. n-1) are traced back to back in ONE
+// loop -- a lane that finishes ray k starts ray k+1 at its next step, instead of idling until the
+// wave's slowest ray k is done (nested per-lane loops re-converge after every ray).  Each ray is
+// exactly traverse<8, true>'s (ray8_init, then trav8_step until done), taken and added to the
+// radiance in slot order, so the result is the slot loop's.
+#ifndef DXRPT_CHAIN_SHADOWS
+#define DXRPT_CHAIN_SHADOWS 0
+#endif
+
+template <bool kCount>
+PT_DEV void shadow_rays_chained(const KArgs& A, uint32_t slot_p, uint32_t k0, uint32_t n, lds_int* stk, float4& rad,
+                                uint32_t* cnt, const NodeCache& nc) {
+    uint32_t k = k0;
+    Ray8 R;
+    HitRec h;
+    uint32_t node = 0;
+    int sp = 0;
+    uint2 tos = make_uint2(0u, 0u);
+    f3 c = f3{0.0f, 0.0f, 0.0f};
+    auto start = [&](uint32_t kk) {
+        const size_t slot = size_t(kk) * A.F.qsize + slot_p;
+        const float4 o4 = A.F.sh_org[slot], d4 = A.F.sh_dir[slot], c4 = A.F.sh_con[slot];
+        ray8_init(R, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, h);
+        c = ld3(c4);
+        node = 0;
+        sp = 0;
+        tos = make_uint2(0u, 0u);
+    };
+    if (k < n) start(k);
+    while (k < n) {
+        if (trav8_step<true, kCount>(A.S, R, node, sp, stk, tos, h, cnt[2], cnt[3], nc)) {
+            const bool occluded = h.tri != kMiss;
+            rad.x += occluded ? c.x * 0.0f : c.x;
+            rad.y += occluded ? c.y * 0.0f : c.y;
+            rad.z += occluded ? c.z * 0.0f : c.z;
+            if (++k < n) start(k);
+        }
+    }
+}
 
 // One path from its first ray (PathLength 1) to its end: per depth the closest hit, path_vertex and
 // the vertex's shadow rays in slot order -- the megakernel's per-thread loop, shared by k_path (camera
@@ -1784,7 +1829,30 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
         // -- one direction, nearby origins -- take the wave-coherent traversal.  A lane whose sun term
         // is zero has another kind of ray in slot 0 (a spot light's, or at MaxPathLength 2 the sky
         // visibility ray, random directions): it traces per lane, after the packet.
-        for (uint32_t k = 0; __ballot(k < nsh) != 0ull; ++k) {
+#if DXRPT_CHAIN_SHADOWS
+        uint32_t k0 = 0;
+        if (d == 1 && (packet & 2u) && !DXRPT_DIAG_NO_SHADOW) {  // slot 0 of the sun lanes: one packet
+            const bool live = nsh > 0u && sun0;
+            const size_t slot = slot_p;
+            float4 o4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d4 = make_float4(0.0f, 0.0f, 1.0f, 0.0f), c4 = o4;
+            if (live) {
+                o4 = A.F.sh_org[slot];
+                d4 = A.F.sh_dir[slot];
+                c4 = A.F.sh_con[slot];
+            }
+            HitRec hs;
+            const bool occluded = traverse8_packet<true, kCount>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live,
+                                                                 hs, 0u, nullptr, cnt + 2);
+            if (live) {
+                rad.x += occluded ? c4.x * 0.0f : c4.x;
+                rad.y += occluded ? c4.y * 0.0f : c4.y;
+                rad.z += occluded ? c4.z * 0.0f : c4.z;
+                k0 = 1u;
+            }
+        }
+        if (!DXRPT_DIAG_NO_SHADOW) shadow_rays_chained<kCount>(A, slot_p, k0, nsh, stk, rad, cnt, nc);
+#else
+        for (uint32_t k = 0; !DXRPT_DIAG_NO_SHADOW && __ballot(k < nsh) != 0ull; ++k) {
             const bool live = k < nsh;
             const size_t slot = size_t(k) * A.F.qsize + slot_p;
             float4 o4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d4 = make_float4(0.0f, 0.0f, 1.0f, 0.0f), c4 = o4;
@@ -1807,6 +1875,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
                 rad.z += occluded ? c4.z * 0.0f : c4.z;
             }
         }
+#endif
 #else
         VertexOut O;
         // The vertex's sun and sky-visibility rays stay in registers: both start at the hit position
@@ -2049,13 +2118,89 @@ PT_DEV void camera_path_group(const KArgs& A, uint32_t p, lds_int* stk, bool mem
     if (member0) accumulate_pixel(A, pr.accumIdx, rad);
 }
 
+// Cost-ordered dispatch (FrameParams::wave_order / wave_cost): the hardware starts waves in launch order,
+// so a frame ends with the waves started last; running the costliest wave slots (last frame's
+// durations: the image changes little between progressive frames) first leaves short ones for the
+// end and shortens the tail in which resident slots run dry (scripts/wave_clocks.py busy_frac).
+// Which lanes trace which paths is unchanged -- only the order of whole waves -- so images are equal.
+struct WaveSlot {
+    uint32_t slot;
+    unsigned long long t0;
+};
+
+PT_DEV WaveSlot wave_slot(const KArgs& A) {
+    WaveSlot ws;
+    ws.slot = uint32_t(__builtin_amdgcn_readfirstlane(int((blockIdx.x * blockDim.x + threadIdx.x) >> 6)));
+    if (A.P.wave_order) ws.slot = A.P.wave_order[ws.slot];
+    ws.t0 = A.P.wave_cost ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    return ws;
+}
+
+PT_DEV void wave_slot_done(const KArgs& A, const WaveSlot& ws) {
+    if (!A.P.wave_cost) return;
+    const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - ws.t0;
+    // class: 16 octaves (2^4 .. 2^19 ticks of 10 ns) x 16 steps within an octave, costliest = 0
+    const uint32_t d = dt > 0xFFFFFull ? 0xFFFFFu : uint32_t(dt) | 16u;
+    const uint32_t lg = 31u - uint32_t(__builtin_clz(d));
+    const uint32_t key = (lg - 4u) * 16u + ((d << (31u - lg)) >> 27 & 15u);
+    if ((threadIdx.x & 63u) == 0u) {  // vector store and atomic from lane 0
+        A.P.wave_cost[ws.slot] = kWaveClasses - 1u - key;
+        atomicAdd(&A.P.wave_hist[kWaveClasses - 1u - key], 1u);
+    }
+}
+
+// One thread per wave slot, kWaveClasses threads per workgroup: the class offsets (exclusive scan of
+// the histogram, per workgroup), ranks within the workgroup (LDS atomics), one global reservation per
+// (workgroup, class).
+__global__ __launch_bounds__(kWaveClasses) void k_wave_order(const uint32_t* cls, const uint32_t* hist, uint32_t* cursor,
+                                                             uint32_t* hist_next, uint32_t* cursor_next, uint32_t* order,
+                                                             uint32_t n) {
+    __shared__ uint32_t scan[kWaveClasses], lcount[kWaveClasses], lbase[kWaveClasses];
+    const uint32_t t = threadIdx.x;
+    uint32_t v = hist[t];
+    const uint32_t own = v;
+    scan[t] = v;
+    lcount[t] = 0u;
+    for (uint32_t off = 1; off < kWaveClasses; off <<= 1) {
+        __syncthreads();
+        const uint32_t add = t >= off ? scan[t - off] : 0u;
+        __syncthreads();
+        scan[t] = v = v + add;
+    }
+    __syncthreads();
+    scan[t] = v - own;
+    const uint32_t i = blockIdx.x * kWaveClasses + t;
+    uint32_t c = 0, r = 0;
+    if (i < n) {
+        c = cls[i];
+        r = atomicAdd(&lcount[c], 1u);
+    }
+    __syncthreads();
+    if (lcount[t]) lbase[t] = atomicAdd(&cursor[t], lcount[t]);
+    __syncthreads();
+    if (i < n) order[scan[c] + lbase[c] + r] = i;
+    if (blockIdx.x == 0u) {
+        hist_next[t] = 0u;
+        cursor_next[t] = 0u;
+    }
+}
+
+hipError_t launch_wave_order(const uint32_t* cls, const uint32_t* hist, uint32_t* cursor, uint32_t* hist_next,
+                             uint32_t* cursor_next, uint32_t* order, uint32_t n, hipStream_t stream) {
+    hipLaunchKernelGGL(k_wave_order, dim3((n + kWaveClasses - 1u) / kWaveClasses), dim3(kWaveClasses), 0, stream, cls,
+                       hist, cursor, hist_next, cursor_next, order, n);
+    return hipGetLastError();
+}
+
 // kPersistent: a grid sized to the resident waves; each wave takes the next 64 paths (one 8x8 pixel
 // block) from a frame counter until the frame is done, so no wave idles while a long one finishes.
 // kLds: the workgroup first copies the top A.P.lds_nodes BVH8 nodes (breadth-first, so the levels
 // every ray visits) behind the stacks; the per-lane traversals read those from LDS.
 // kGroup: path groups of 64 / A.P.mega_lanes lanes (its own instantiation, so the default kernel's
 // register allocation does not carry the group schedule).
-template <int kOcc, bool kPersistent, bool kLds = false, bool kGroup = false, bool kCount = false>
+// kOrder: the cost-ordered dispatch (wave_slot); its own instantiation, so that the path-ordered
+// kernel of large frames keeps its code (the indirection costs it ~2 %).
+template <int kOcc, bool kPersistent, bool kLds = false, bool kGroup = false, bool kCount = false, bool kOrder = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
 void k_path(KArgs A) {
     lut_fill(A.S);
@@ -2063,8 +2208,17 @@ void k_path(KArgs A) {
     lds_int* stk = lane_stack(A.S, stack);
     if (kGroup) {  // mega_lanes paths per wave, each traced by 64 / mega_lanes lanes
         const uint32_t lane = threadIdx.x & 63u;
-        const uint32_t q = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * A.P.mega_lanes + (lane & (A.P.mega_lanes - 1u));
+        const WaveSlot ws = wave_slot(A);
+        const uint32_t q = ws.slot * A.P.mega_lanes + (lane & (A.P.mega_lanes - 1u));
         if (q < A.P.num_paths) camera_path_group(A, q, stk, lane < A.P.mega_lanes);
+        wave_slot_done(A, ws);
+        return;
+    }
+    if (!kPersistent && !kLds && !kCount && kOrder) {
+        const WaveSlot ws = wave_slot(A);
+        const uint32_t p = (ws.slot << 6) | (threadIdx.x & 63u);
+        if (p < A.P.num_paths) camera_path(A, p, stk);
+        wave_slot_done(A, ws);
         return;
     }
     if (!kPersistent) {
@@ -2268,11 +2422,17 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
             else if (fp.megakernel_occupancy == 5) hipLaunchKernelGGL((k_path<5, false, true>), dim3(gm), dim3(tb), ldsn, stream, A);
             else hipLaunchKernelGGL((k_path<4, false, true>), dim3(gm), dim3(tb), ldsn, stream, A);
         }
-        else if (twins) {
+        else if (twins) {  // (cost ordering by FrameParams::wave_order / wave_cost, null: off)
             if (fp.megakernel_occupancy >= 7) hipLaunchKernelGGL((k_path<7, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
             else if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_path<6, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
             else if (fp.megakernel_occupancy == 5) hipLaunchKernelGGL((k_path<5, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
             else hipLaunchKernelGGL((k_path<4, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
+        }
+        else if (fp.wave_cost && fp.megakernel_occupancy >= 4 && fp.megakernel_occupancy <= 7) {  // cost-ordered waves
+            if (fp.megakernel_occupancy == 7) hipLaunchKernelGGL((k_path<7, false, false, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
+            else if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_path<6, false, false, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
+            else if (fp.megakernel_occupancy == 5) hipLaunchKernelGGL((k_path<5, false, false, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
+            else hipLaunchKernelGGL((k_path<4, false, false, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
         }
         else if (fp.megakernel_occupancy == 8) hipLaunchKernelGGL((k_path<8, false>), dim3(gm), dim3(tb), ldsm, stream, A);
         else if (fp.megakernel_occupancy == 7) hipLaunchKernelGGL((k_path<7, false>), dim3(gm), dim3(tb), ldsm, stream, A);

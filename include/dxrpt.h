@@ -335,6 +335,14 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                      records each wave's start and end time (s_memrealtime, 100 MHz),
                                      read with dxrpt_get_wave_clocks (diagnostic: where a frame's tail
                                      comes from).  Images identical. */
+#define DXRPT_OPT_WAVE_ORDER 29u     /* 1: megakernel frames start their costliest waves first -- each
+                                     wave's duration class is recorded every frame and a small pass
+                                     orders the next frame's waves by it (progressive frames cost alike),
+                                     so the frame does not end on long waves started last.  The order
+                                     resets when the frame's tiles or path count change.  0: waves in
+                                     path order.  2 (default): 1 for frames of at most 3 rounds of
+                                     resident waves (a GPU's share of a multi-GPU frame), else 0.
+                                     Images identical in every mode. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

@@ -24,11 +24,12 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--share", type=int, default=1)
     ap.add_argument("--rank", type=int, default=0)
-    ap.add_argument("--layout", default="bands", choices=["blocks", "bands", "blocks-raster"],
+    ap.add_argument("--layout", default="bands", choices=["blocks", "bands", "blocks-raster", "blocks-lpt"],
                     help="screen partition of --share (blocks-raster: 8x8 tiles in raster order, block k -> rank k %% N)")
     ap.add_argument("--any-hit", type=int, default=None, help="MaxAnyHitPathLength override")
     ap.add_argument("--packet", type=int, default=None, help="DXRPT_OPT_PACKET_TRAVERSAL override")
     ap.add_argument("--occ", type=int, default=None, help="DXRPT_OPT_MEGAKERNEL_OCCUPANCY override")
+    ap.add_argument("--wave-order", type=int, default=None, help="DXRPT_OPT_WAVE_ORDER override")
     ap.add_argument("--max-path", type=int, default=None, help="MaxPathLength override (a cost breakdown by depth)")
     args = ap.parse_args()
     import torch
@@ -47,10 +48,28 @@ def main():
         t.set_option(A.OPT_PACKET_TRAVERSAL, args.packet)
     if args.occ is not None:
         t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, args.occ)
+    if args.wave_order is not None:
+        t.set_option(A.OPT_WAVE_ORDER, args.wave_order)
     t.initialize_scene(sc, sky)
     t.build_rt_acceleration_structure()
     tiles, n = None, W * H
-    if args.layout == "blocks-raster":  # the whole frame as 8x8 block tiles in raster order (tile-count A/B)
+    if args.layout == "blocks-lpt":  # 8x8 block tiles, costliest first (one census frame's wave clocks)
+        from dxrpathtracer_amd import _abi as AA
+        import numpy as np
+        acc0 = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+        t.set_option(A.OPT_COUNT_TRAVERSAL, 1)
+        t.set_option(A.OPT_WAVE_CLOCKS, 1)
+        t.render_raw(D.make_constants(sc, st, sky, W, H, 0), st, acc0.data_ptr(), W, H,
+                     stream=torch.cuda.current_stream().cuda_stream, lights=D.make_lights(sc))
+        torch.cuda.synchronize()
+        wc = t.wave_clocks().astype(np.int64)
+        t.set_option(A.OPT_WAVE_CLOCKS, 0)
+        t.set_option(A.OPT_COUNT_TRAVERSAL, 0)
+        bw = (W + 7) // 8
+        order = np.argsort(-(wc[:, 1] - wc[:, 0]), kind="stable")  # wave w of the full frame = block w
+        tiles = [AA.Tile(int(b % bw) * 8, int(b // bw) * 8, 8, 8, 64 * k, 8, 0) for k, b in enumerate(order)]
+        n = 64 * len(tiles)
+    elif args.layout == "blocks-raster":  # the whole frame as 8x8 block tiles in raster order (tile-count A/B)
         from dxrpathtracer_amd import _abi as AA
         tiles = [AA.Tile(x, y, 8, 8, (y // 8 * (W // 8) + x // 8) * 64, 8, 0) for y in range(0, H, 8) for x in range(0, W, 8)]
         if args.share > 1:
@@ -77,7 +96,7 @@ def main():
         torch.cuda.synchronize()
         rounds.append(a.elapsed_time(b) / args.frames)
     s = t.stats()
-    print(f"{args.label:24s} {args.config}{'' if args.max_path is None else f' L={L}'} share 1/{args.share} r{args.rank} {args.layout if args.share > 1 else ''}: median {statistics.median(rounds):.4f} "
+    print(f"{args.label:24s} {args.config}{'' if args.max_path is None else f' L={L}'}{'' if args.wave_order is None else f' order={args.wave_order}'} share 1/{args.share} r{args.rank} {args.layout if args.share > 1 else ''}: median {statistics.median(rounds):.4f} "
           f"mean {statistics.mean(rounds):.4f} min {min(rounds):.4f} ms/frame  rays {s.radiance_rays + s.shadow_rays}",
           flush=True)
     t.close()

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--frames", type=int, default=3, help="census frames (the last one is reported)")
     ap.add_argument("--json", default=None)
     ap.add_argument("--occ", type=int, default=0, help="megakernel occupancy (0: default by size)")
+    ap.add_argument("--slots", type=int, default=256 * 4 * 7, help="resident wave slots (CUs x SIMDs x waves/SIMD)")
     args = ap.parse_args()
     import torch
     import dxrpathtracer_amd as D
@@ -77,6 +78,10 @@ def main():
            "mean_us": float(dur.mean()),
            "slowest": [{"wave": int(w), "block_xy": blocks[w] if w < len(blocks) else None,
                         "start_us": round(float(start[w]), 1), "dur_us": round(float(dur[w]), 1)} for w in order[:12]],
+           # resident-slot utilisation: wave time / (slots x span), and waves alive at fractions of the span
+           "slots": int(args.slots), "busy_frac": float(dur.sum() / (args.slots * end.max())),
+           "alive_at": {f"{q}%": int(((start <= end.max() * q / 100) & (end > end.max() * q / 100)).sum())
+                        for q in (25, 50, 75, 85, 90, 95, 98)},
            "nodes_per_path": round((s.node_visits_radiance + s.node_visits_shadow) / max(1, n), 2)}
     print(json.dumps(res))
     if args.json:

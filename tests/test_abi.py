@@ -71,3 +71,13 @@ def test_oracle_is_not_linked_by_the_product():
     for lib in ("libdxrpt.so", "libdxrpt_host.so"):
         data = open(os.path.join(A.LIB_DIR, lib), "rb").read()
         assert b"oracle_" not in data, lib
+
+
+def test_option_ids_match_header():
+    # every DXRPT_OPT_* id of include/dxrpt.h has the same value in the Python binding
+    import re
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "dxrpt.h")).read()
+    ids = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define DXRPT_OPT_(\w+)\s+(\d+)u", hdr)}
+    assert len(ids) >= 29
+    for name, v in ids.items():
+        assert getattr(A, "OPT_" + name) == v, name

@@ -575,3 +575,43 @@ def test_megakernel_lanes_and_partial_waves_are_bit_identical(torch_cuda, name, 
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
         t.set_option(A.OPT_MEGAKERNEL_LANES, A.DEFAULT_MEGAKERNEL_LANES)
         t.set_option(A.OPT_PACKET_TRAVERSAL, A.DEFAULT_PACKET_TRAVERSAL)
+
+
+@pytest.mark.parametrize("name,lanes,W,H", [("sponza", 64, 352, 200), ("suntemple", 32, 320, 180),
+                                            ("sponza", 64, 100, 50)])
+def test_wave_order_is_bit_identical(torch_cuda, name, lanes, W, H):
+    # DXRPT_OPT_WAVE_ORDER: from the second frame on, waves start costliest first (the order is built
+    # on the device from the previous frame's wave durations); every frame -- a progressive sequence
+    # into one accumulation buffer, then a switch to a band share (the order resets) and back -- must
+    # equal the path-ordered frames bit for bit
+    torch = torch_cuda
+    sc, sky = scene_bundle(name)
+    st = sc.settings(MaxPathLength=3)
+    t = tracer(name)
+    lights = D.make_lights(sc)
+    lay = band_layout(W, H, 2)
+    runs = []
+    try:
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30)
+        t.set_option(A.OPT_MEGAKERNEL_LANES, lanes)
+        for order in (0, 1):
+            t.set_option(A.OPT_WAVE_ORDER, order)
+            acc = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+            share = torch.zeros((lay.counts[1], 4), dtype=torch.float32, device="cuda")
+            frames = []
+            for f, part in enumerate(("full", "full", "full", "share", "share", "full")):
+                rtc = D.make_constants(sc, st, sky, W, H, f)
+                if part == "full":
+                    gpu_render(torch, name, W, H, st, f, accum=acc, rtc=rtc, lights=lights)
+                    frames.append(acc.cpu().numpy().copy())
+                else:
+                    gpu_render(torch, name, W, H, st, f, tiles=lay.rank_tiles(1), n_out=lay.counts[1], accum=share,
+                               rtc=rtc, lights=lights)
+                    frames.append(share.cpu().numpy().copy())
+            runs.append(frames)
+        for a, b in zip(*runs):
+            np.testing.assert_array_equal(b, a)
+    finally:
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
+        t.set_option(A.OPT_MEGAKERNEL_LANES, A.DEFAULT_MEGAKERNEL_LANES)
+        t.set_option(A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)
