@@ -45,8 +45,18 @@ PT_DEV float bitsf(uint32_t u) { return __uint_as_float(u); }
 // the spill path (global) never merges with it into flat accesses.
 typedef __attribute__((address_space(3))) int lds_int;
 constexpr int kStkStride = 64;
+#ifndef DXRPT_STACK_REMAT
+#define DXRPT_STACK_REMAT 0
+#endif
 PT_DEV lds_int* lane_stack(const SceneDev& S, int* stack) {
+#if DXRPT_STACK_REMAT
+    // the wave's part scalar, the lane's from mbcnt: cheap to recompute, so the compiler need not keep
+    // (or spill) a per-lane base across the path
+    const uint32_t wave = uint32_t(__builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)));
+    return (lds_int*)(stack) + wave * S.stack_ints * 64u + uint32_t(__lane_id());
+#else
     return (lds_int*)(stack) + (threadIdx.x >> 6) * S.stack_ints * 64u + (threadIdx.x & 63u);
+#endif
 }
 
 // ---- texture sampling ---------------------------------------------------------------------------
@@ -249,14 +259,23 @@ PT_DEV float opacity_finish(const SceneDev& S, const OpacityTap& t) {
     return lerpf(lerpf(a, b, t.fx), lerpf(c, d, t.fx), t.fy);
 }
 
+#ifndef DXRPT_ALPHA_ONE_TRIP
+#define DXRPT_ALPHA_ONE_TRIP 1
+#endif
 PT_DEV bool alpha_accepts(const SceneDev& S, uint32_t geom, uint32_t gtri, float b1, float b2) {
     const GeoTex opacity = S.geoshade[geom].opacity;
-    if (opacity.whf == 0u) return true;
-    const float w0 = (1.0f - b1) - b2;
     const float2* V = reinterpret_cast<const float2*>(S.tri_verts + size_t(gtri) * 12u);
     float2 uv[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) uv[k] = V[k * 8 + 3];  // float2 #3 of MeshVertex k = UV
+#if DXRPT_ALPHA_ONE_TRIP
+    // the opacity descriptor and the UVs in one memory round trip (a triangle that reaches here is
+    // alpha tested, so its geometry has an opacity map; otherwise the UVs are simply unused)
+    asm volatile("" ::"v"(opacity.offset), "v"(opacity.whf), "v"(uv[0].x), "v"(uv[0].y), "v"(uv[1].x), "v"(uv[1].y),
+                 "v"(uv[2].x), "v"(uv[2].y));
+#endif
+    if (opacity.whf == 0u) return true;
+    const float w0 = (1.0f - b1) - b2;
     float u = bary_lerp(uv[0].x, uv[1].x, uv[2].x, w0, b1, b2);
     float v = bary_lerp(uv[0].y, uv[1].y, uv[2].y, w0, b1, b2);
     return !(sample_tex_desc(S, tex_desc(opacity), u, v).r < 0.35f);
