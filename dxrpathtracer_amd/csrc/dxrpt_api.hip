@@ -813,9 +813,11 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // 0.68-0.69 ms at 6 waves/SIMD, profiles/r02_ab_path_groups_shares.txt); from the 1/4 share up
         // the doubled waves cost more than the shorter chains save.
         const uint32_t lanes = ctx->opt_mega_lanes ? ctx->opt_mega_lanes : (paths <= 400000u ? 32u : 64u);
+        // (with cost-ordered waves, r02: path groups 5 waves/SIMD, 1/8 share 0.574 -> 0.562 ms; 600k-1.5M
+        // paths 6, 720p 1.111 -> 1.095 and the 1/2 share 1.20 -> 1.165 ms; profiles/r02_ab_occ_mid_frames.txt)
         fp.megakernel_occupancy = ctx->opt_mega_occ ? ctx->opt_mega_occ
-                                : lanes < 64u ? 6u
-                                : (paths > 1500000u ? 7u : (paths > 300000u ? 5u : 4u));
+                                : lanes < 64u ? 5u
+                                : (paths > 1500000u ? 7u : (paths > 600000u ? 6u : (paths > 300000u ? 5u : 4u)));
         fp.mega_persistent = ctx->opt_mega_persistent;
         fp.mega_lanes = lanes;
         fp.num_cus = ctx->num_cus;
@@ -855,6 +857,11 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             fp.wave_cost = ctx->d_wave_cost.as<uint32_t>();
             fp.wave_hist = ctx->d_wave_hist.as<uint32_t>() + ctx->order_parity * 2 * kWaveClasses;
             fp.wave_order = ctx->order_ready ? ctx->d_wave_order.as<uint32_t>() : nullptr;
+            if (ctx->opt_wave_clocks) {  // per-slot stamps of an ordered frame (diagnostic)
+                ctx->wclock_waves = order_waves;
+                ctx->d_wclock.ensure(size_t(order_waves) * 2 * sizeof(unsigned long long));
+                fp.wave_clock = ctx->d_wclock.as<unsigned long long>();
+            }
         }
         const int L = settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength;
         hipEvent_t* ev = nullptr;

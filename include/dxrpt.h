@@ -316,8 +316,8 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                             compaction wins for long paths on big frames).  0 = always the
                                             wavefront.  Identical results. */
 #define DXRPT_OPT_MEGAKERNEL_OCCUPANCY 24u /* megakernel register budget in waves/SIMD: 0 = by frame size
-                                              (default: 6 with path groups, else 7 above 1,500,000 paths,
-                                              5 above 300,000, else 4),
+                                              (default: 5 with path groups, else 7 above 1,500,000 paths,
+                                              6 above 600,000, 5 above 300,000, else 4),
                                               4 (no spills), 5, 6, 7, 8, or 3 = the compiler's */
 #define DXRPT_OPT_MEGAKERNEL_PERSISTENT 26u /* > 0: the megakernel as a persistent grid of this many
                                                waves per CU pulling 64-path chunks (0 = one wave per
@@ -334,7 +334,8 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 #define DXRPT_OPT_WAVE_CLOCKS 28u /* 1: with DXRPT_OPT_COUNT_TRAVERSAL, the megakernel census frame also
                                      records each wave's start and end time (s_memrealtime, 100 MHz),
                                      read with dxrpt_get_wave_clocks (diagnostic: where a frame's tail
-                                     comes from).  Images identical. */
+                                     comes from); without it, a cost-ordered frame (DXRPT_OPT_WAVE_ORDER)
+                                     records each wave slot's stamps.  Images identical. */
 #define DXRPT_OPT_WAVE_ORDER 29u     /* 1: megakernel frames start their costliest waves first -- each
                                      wave's duration class is recorded every frame and a small pass
                                      orders the next frame's waves by it (progressive frames cost alike),

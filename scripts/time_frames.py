@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--any-hit", type=int, default=None, help="MaxAnyHitPathLength override")
     ap.add_argument("--packet", type=int, default=None, help="DXRPT_OPT_PACKET_TRAVERSAL override")
     ap.add_argument("--occ", type=int, default=None, help="DXRPT_OPT_MEGAKERNEL_OCCUPANCY override")
+    ap.add_argument("--band", type=int, default=None, help="band height of --layout bands (default BAND_ROWS)")
+    ap.add_argument("--lanes", type=int, default=None, help="DXRPT_OPT_MEGAKERNEL_LANES override")
     ap.add_argument("--wave-order", type=int, default=None, help="DXRPT_OPT_WAVE_ORDER override")
     ap.add_argument("--max-path", type=int, default=None, help="MaxPathLength override (a cost breakdown by depth)")
     args = ap.parse_args()
@@ -50,6 +52,8 @@ def main():
         t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, args.occ)
     if args.wave_order is not None:
         t.set_option(A.OPT_WAVE_ORDER, args.wave_order)
+    if args.lanes is not None:
+        t.set_option(A.OPT_MEGAKERNEL_LANES, args.lanes)
     t.initialize_scene(sc, sky)
     t.build_rt_acceleration_structure()
     tiles, n = None, W * H
@@ -77,7 +81,9 @@ def main():
             tiles = [AA.Tile(t.x0, t.y0, 8, 8, 64 * k, 8, 0) for k, t in enumerate(tiles)]
         n = 64 * len(tiles)
     elif args.share > 1:
-        lay = screen_layout(W, H, args.share, args.layout)
+        from dxrpathtracer_amd.distributed import band_layout
+        lay = (band_layout(W, H, args.share, args.band) if args.layout == "bands" and args.band
+               else screen_layout(W, H, args.share, args.layout))
         tiles, n = lay.rank_tiles(args.rank), lay.counts[args.rank]
     acc = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
     consts = [D.make_constants(sc, st, sky, W, H, s) for s in range(16)]
@@ -96,7 +102,7 @@ def main():
         torch.cuda.synchronize()
         rounds.append(a.elapsed_time(b) / args.frames)
     s = t.stats()
-    print(f"{args.label:24s} {args.config}{'' if args.max_path is None else f' L={L}'}{'' if args.wave_order is None else f' order={args.wave_order}'} share 1/{args.share} r{args.rank} {args.layout if args.share > 1 else ''}: median {statistics.median(rounds):.4f} "
+    print(f"{args.label:24s} {args.config}{'' if args.max_path is None else f' L={L}'}{'' if args.wave_order is None else f' order={args.wave_order}'} share 1/{args.share} r{args.rank} {args.layout if args.share > 1 else ''}{args.band or ''}: median {statistics.median(rounds):.4f} "
           f"mean {statistics.mean(rounds):.4f} min {min(rounds):.4f} ms/frame  rays {s.radiance_rays + s.shadow_rays}",
           flush=True)
     t.close()

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--frames", type=int, default=3, help="census frames (the last one is reported)")
     ap.add_argument("--json", default=None)
     ap.add_argument("--occ", type=int, default=0, help="megakernel occupancy (0: default by size)")
+    ap.add_argument("--ordered", action="store_true", help="time the default (cost-ordered) frames, not a census")
     ap.add_argument("--slots", type=int, default=256 * 4 * 7, help="resident wave slots (CUs x SIMDs x waves/SIMD)")
     args = ap.parse_args()
     import torch
@@ -48,7 +49,8 @@ def main():
         tiles, n = lay.rank_tiles(args.rank), lay.counts[args.rank]
     acc = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
-    t.set_option(A.OPT_COUNT_TRAVERSAL, 1)
+    if not args.ordered:  # census frame (path order); --ordered: the shipped cost-ordered frames
+        t.set_option(A.OPT_COUNT_TRAVERSAL, 1)
     t.set_option(A.OPT_WAVE_CLOCKS, 1)
     if args.occ:
         t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, args.occ)
@@ -64,19 +66,20 @@ def main():
     dur = end - start
     order = np.argsort(-dur)
     # block position of wave w: the tiles are walked in order, 64 paths per wave (8x8 blocks when the
-    # tile is a multiple of 8 in both sizes)
+    # tile is a multiple of 8 in both sizes; path-group frames: 2 waves per block)
     tl = tiles if tiles else [A.Tile(0, 0, W, H, 0, W, 0)]
     blocks = []
     for tt in tl:
         bw, bh = (tt.w + 7) // 8, (tt.h + 7) // 8
         for b in range(bw * bh):
             blocks.append((tt.x0 + (b % bw) * 8, tt.y0 + (b // bw) * 8))
-    res = {"config": args.config, "share": args.share, "rank": args.rank, "layout": args.layout, "waves": int(len(wc)),
+    per = max(1, round(n / len(wc)))  # paths per wave
+    res = {"config": args.config, "ordered": bool(args.ordered), "paths_per_wave": per, "share": args.share, "rank": args.rank, "layout": args.layout, "waves": int(len(wc)),
            "span_us": float(end.max()), "last_start_us": float(start.max()),
            "dur_us": {q: float(np.percentile(dur, p)) for q, p in (("min", 0), ("p50", 50), ("p90", 90), ("p99", 99),
                                                                       ("max", 100))},
            "mean_us": float(dur.mean()),
-           "slowest": [{"wave": int(w), "block_xy": blocks[w] if w < len(blocks) else None,
+           "slowest": [{"wave": int(w), "block_xy": blocks[w * per // 64] if w * per // 64 < len(blocks) else None,
                         "start_us": round(float(start[w]), 1), "dur_us": round(float(dur[w]), 1)} for w in order[:12]],
            # resident-slot utilisation: wave time / (slots x span), and waves alive at fractions of the span
            "slots": int(args.slots), "busy_frac": float(dur.sum() / (args.slots * end.max())),
