@@ -2149,8 +2149,9 @@ struct WaveSlot {
 
 PT_DEV WaveSlot wave_slot(const KArgs& A) {
     WaveSlot ws;
-    ws.slot = uint32_t(__builtin_amdgcn_readfirstlane(int((blockIdx.x * blockDim.x + threadIdx.x) >> 6)));
-    if (A.P.wave_order) ws.slot = A.P.wave_order[ws.slot];
+    const uint32_t w = uint32_t(__builtin_amdgcn_readfirstlane(int((blockIdx.x * blockDim.x + threadIdx.x) >> 6)));
+    ws.slot = w;
+    if (A.P.wave_order) ws.slot = A.P.wave_order[w];
     ws.t0 = A.P.wave_cost ? __builtin_amdgcn_s_memrealtime() : 0ull;
     return ws;
 }
@@ -2165,6 +2166,10 @@ PT_DEV void wave_slot_done(const KArgs& A, const WaveSlot& ws) {
     if ((threadIdx.x & 63u) == 0u) {  // vector store and atomic from lane 0
         A.P.wave_cost[ws.slot] = kWaveClasses - 1u - key;
         atomicAdd(&A.P.wave_hist[kWaveClasses - 1u - key], 1u);
+        if (A.P.wave_clock) {  // DXRPT_OPT_WAVE_CLOCKS on an ordered frame: the slot's start and end
+            A.P.wave_clock[2 * ws.slot] = ws.t0;
+            A.P.wave_clock[2 * ws.slot + 1] = ws.t0 + dt;
+        }
     }
 }
 

@@ -15,8 +15,9 @@ from dataclasses import dataclass
 from . import _abi as A
 
 # 8-row bands (one 8x8-pixel-block row per band, the megakernel's wave footprint): 1080 rows over 8
-# ranks = 135 bands, 17 or 16 per rank (136 rows max against a 135 mean, 0.7 % over); 16-row bands
-# left 144 rows on the busiest of 8 ranks (6.7 % over), which bounded the 8-GPU frame.
+# ranks = 135 bands, 17 or 16 per rank.  Chosen by the SLOWEST rank's share, which is what an N-GPU
+# frame waits for: all 8 ranks' 1/8 shares with the shipped schedule take at most 0.557 ms with 8-row,
+# 0.575 with 16-row and 0.595 with 32-row bands (profiles/r02_ab_band_height_all_ranks.txt).
 BAND_ROWS = 8
 
 
@@ -79,8 +80,10 @@ def block_layout(width: int, height: int, world: int, block: int = 8, seed: int 
 
 def screen_layout(width: int, height: int, world: int, kind: str = "bands") -> BandLayout:
     """The multi-GPU screen partition: "bands" (band_layout, default) or "blocks" (block_layout).  Measured
-    per-rank times of a 1080p frame's 1/8 shares (profiles/r02_shares_path_groups_default.txt): bands
-    0.62-0.69 ms, blocks 0.66-0.70 -- a share ends with its slowest waves, not with its pixel count."""
+    per-rank times of a 1080p frame's 1/8 shares before cost-ordered waves
+    (profiles/r02_shares_path_groups_default.txt): bands 0.62-0.69 ms, blocks 0.66-0.70 -- a share ends
+    with its slowest waves, not with its pixel count; with cost-ordered waves every rank's band share
+    takes 0.53-0.56 ms (profiles/r02_shares_all_ranks_default.txt)."""
     if kind == "bands":
         return band_layout(width, height, world)
     if kind == "blocks":

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--any-hit", type=int, default=None, help="MaxAnyHitPathLength override")
     ap.add_argument("--packet", type=int, default=None, help="DXRPT_OPT_PACKET_TRAVERSAL override")
     ap.add_argument("--occ", type=int, default=None, help="DXRPT_OPT_MEGAKERNEL_OCCUPANCY override")
+    ap.add_argument("--tile", default=None, help="x,y,w,h: render only this rectangle (one tile)")
     ap.add_argument("--band", type=int, default=None, help="band height of --layout bands (default BAND_ROWS)")
     ap.add_argument("--lanes", type=int, default=None, help="DXRPT_OPT_MEGAKERNEL_LANES override")
     ap.add_argument("--wave-order", type=int, default=None, help="DXRPT_OPT_WAVE_ORDER override")
@@ -57,7 +58,11 @@ def main():
     t.initialize_scene(sc, sky)
     t.build_rt_acceleration_structure()
     tiles, n = None, W * H
-    if args.layout == "blocks-lpt":  # 8x8 block tiles, costliest first (one census frame's wave clocks)
+    if args.tile:
+        from dxrpathtracer_amd import _abi as AA
+        x, y, w, h = (int(v) for v in args.tile.split(","))
+        tiles, n = [AA.Tile(x, y, w, h, 0, w, 0)], w * h
+    elif args.layout == "blocks-lpt":  # 8x8 block tiles, costliest first (one census frame's wave clocks)
         from dxrpathtracer_amd import _abi as AA
         import numpy as np
         acc0 = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
@@ -102,7 +107,7 @@ def main():
         torch.cuda.synchronize()
         rounds.append(a.elapsed_time(b) / args.frames)
     s = t.stats()
-    print(f"{args.label:24s} {args.config}{'' if args.max_path is None else f' L={L}'}{'' if args.wave_order is None else f' order={args.wave_order}'} share 1/{args.share} r{args.rank} {args.layout if args.share > 1 else ''}{args.band or ''}: median {statistics.median(rounds):.4f} "
+    print(f"{args.label:24s} {args.config}{'' if args.max_path is None else f' L={L}'}{'' if args.wave_order is None else f' order={args.wave_order}'} share 1/{args.share} r{args.rank} {args.layout if args.share > 1 else ''}{args.band or ''}{' tile ' + args.tile if args.tile else ''}: median {statistics.median(rounds):.4f} "
           f"mean {statistics.mean(rounds):.4f} min {min(rounds):.4f} ms/frame  rays {s.radiance_rays + s.shadow_rays}",
           flush=True)
     t.close()

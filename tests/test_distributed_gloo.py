@@ -120,6 +120,8 @@ def test_pipelined_gather_delivers_every_frame(world):
 
 def test_band_partition_is_balanced():
     # 8-row bands at the metric's 1920x1080: every rank within 1 % of the mean pixel count at 2, 4, 8 ranks
+    # (pixel balance only: the band height itself is chosen by the slowest rank's measured share time,
+    # distributed.BAND_ROWS)
     from dxrpathtracer_amd.distributed import band_layout
     for world in (2, 4, 8):
         lay = band_layout(1920, 1080, world)
