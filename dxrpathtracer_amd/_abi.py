@@ -142,7 +142,8 @@ for _t, _n in ((MeshVertex, 64), (GeometryInfo, 16), (Material, 24), (SpotLight,
 DXRPT_SYMBOLS = ("dxrpt_abi_version", "dxrpt_default_settings", "dxrpt_create", "dxrpt_destroy", "dxrpt_last_error",
                  "dxrpt_set_scene", "dxrpt_add_texture", "dxrpt_set_sky", "dxrpt_build_bvh", "dxrpt_get_bvh_info",
                  "dxrpt_render", "dxrpt_get_stats", "dxrpt_trace_rays", "dxrpt_set_option", "dxrpt_reset_timing",
-                 "dxrpt_post_process", "dxrpt_bake_lightmap", "dxrpt_denoise_median", "dxrpt_get_wave_clocks")
+                 "dxrpt_post_process", "dxrpt_bake_lightmap", "dxrpt_denoise_median", "dxrpt_get_wave_clocks",
+                 "dxrpt_get_phase_clocks")
 DXRPT_HOST_SYMBOLS = ("dxrpt_host_scene_create", "dxrpt_host_scene_load", "dxrpt_host_scene_destroy", "dxrpt_host_last_error",
                       "dxrpt_host_inv_view_projection", "dxrpt_host_sky_create", "dxrpt_host_fill_constants",
                       "dxrpt_host_float_to_half", "dxrpt_host_half_to_float", "dxrpt_host_hosek_load",
@@ -188,6 +189,7 @@ def lib() -> C.CDLL:
                                    C.POINTER(LightConstants), P, u32, u32, C.POINTER(Tile), u32, P]
         L.dxrpt_get_stats.argtypes = [P, C.POINTER(Stats)]
         L.dxrpt_get_wave_clocks.argtypes = [P, C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint32)]
+        L.dxrpt_get_phase_clocks.argtypes = [P, C.POINTER(C.c_uint64)]
         L.dxrpt_trace_rays.argtypes = [P, P, u32, u32, P, P]
         L.dxrpt_post_process.argtypes = [P, C.POINTER(AppSettings), P, u32, u32, P, u32, P]
         L.dxrpt_set_option.argtypes = [P, u32, C.c_uint64]

@@ -958,6 +958,15 @@ int dxrpt_get_wave_clocks(dxrpt_ctx* ctx, uint64_t* out, uint32_t max_waves, uin
     });
 }
 
+int dxrpt_get_phase_clocks(dxrpt_ctx* ctx, uint64_t out[8]) {
+    if (!ctx || !out) return DXRPT_E_INVALID_ARG;
+    return guarded(ctx, [&] {
+        unsigned long long t[8];
+        HIP_CHECK(read_phase_ticks(t));
+        for (int k = 0; k < 8; ++k) out[k] = t[k];
+    });
+}
+
 int dxrpt_trace_rays(dxrpt_ctx* ctx, const float* rays, uint32_t num_rays, uint32_t flags, float* hits, void* stream) {
     if (!ctx) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {

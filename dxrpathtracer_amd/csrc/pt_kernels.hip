@@ -1761,6 +1761,38 @@ PT_DEV void count_rays(uint32_t* counters, uint32_t n) {
 #define DXRPT_CHAIN_SHADOWS 0
 #endif
 
+// DXRPT_DIAG_PHASES (diagnostic builds only; dxrpt_get_phase_clocks): each lane of the full-frame
+// megakernel sums the s_memrealtime ticks it spends in each phase of its path (the clock is wave-wide, so
+// a lane masked off while others finish a loop is charged to the phase that loop belongs to, and a lane
+// whose path ended waits in phase 7); wave sums go to g_phase_ticks with one atomic per phase per wave.
+#ifndef DXRPT_DIAG_PHASES
+#define DXRPT_DIAG_PHASES 0
+#endif
+struct PhaseAcc {
+    uint32_t a[8];
+    uint32_t t;
+};
+__device__ unsigned long long g_phase_ticks[8];
+PT_DEV void phase_mark(PhaseAcc* pa, int k) {
+#if DXRPT_DIAG_PHASES
+    if (pa) {
+        const uint32_t now = uint32_t(__builtin_amdgcn_s_memrealtime());
+        pa->a[k] += now - pa->t;
+        pa->t = now;
+    }
+#endif
+}
+PT_DEV void phase_flush(PhaseAcc* pa) {
+#if DXRPT_DIAG_PHASES
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        uint32_t v = pa->a[k];
+        for (int off = 32; off > 0; off >>= 1) v += uint32_t(__shfl_xor(int(v), off));
+        if ((threadIdx.x & 63u) == 0u) atomicAdd(&g_phase_ticks[k], (unsigned long long)v);
+    }
+#endif
+}
+
 template <bool kCount>
 PT_DEV void shadow_rays_chained(const KArgs& A, uint32_t slot_p, uint32_t k0, uint32_t n, lds_int* stk, float4& rad,
                                 uint32_t* cnt, const NodeCache& nc) {
@@ -1803,7 +1835,8 @@ PT_DEV void shadow_rays_chained(const KArgs& A, uint32_t slot_p, uint32_t k0, ui
 // hit; per-lane traversals fetch per lane, packet traversals once per wave).
 template <bool kBake, bool kCount = false>
 PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, f3 dir, float tmax, lds_int* stk,
-                         uint32_t packet_mask, const NodeCache& nc = NodeCache{nullptr, 0u}, uint32_t* cnt = nullptr) {
+                         uint32_t packet_mask, const NodeCache& nc = NodeCache{nullptr, 0u}, uint32_t* cnt = nullptr,
+                         PhaseAcc* pa = nullptr) {
     const dxrpt_app_settings& set = A.P.set;
     const float tmin1 = kBake ? 0.0001f : 0.0f;
     const bool isDiffuse1 = kBake;
@@ -1823,6 +1856,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
         else
             traverse<8, false, kCount, DXRPT_MEGA_PIPE_CH>(A.S, org, dir, d == 1 ? tmin1 : kRayTMin, tmax, d <= set.MaxAnyHitPathLength, stk, h,
                                        cnt[0], cnt[1], nc);
+        phase_mark(pa, d == 1 ? 0 : d == 2 ? 3 : 6);
         VertexIn V;
         V.inOrigin = org;
         V.inDir = dir;
@@ -1840,6 +1874,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
             emit_shadow(A, slot_p, nsh, o, dd, tmn, tmx, c, fo);
         }, O);
         count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, nsh);
+        phase_mark(pa, d == 1 ? 1 : d == 2 ? 4 : 6);
         rad.x += thr.x * O.local.x;
         rad.y += thr.y * O.local.y;
         rad.z += thr.z * O.local.z;
@@ -1961,6 +1996,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
             rad.z += occluded ? cSky.z * 0.0f : cSky.z;
         }
 #endif
+        phase_mark(pa, d == 1 ? 2 : d == 2 ? 5 : 6);
         if (!O.cont) break;
         org = O.nextOrigin;
         dir = O.nextDir;
@@ -2123,10 +2159,10 @@ PT_DEV float4 trace_path_group(const KArgs& A, uint32_t slot_p, uint32_t pix, f3
 // ray per lane -- a wave-uniform scalar test, the other waves keep their packets (same results).
 template <bool kCount = false>
 PT_DEV void camera_path(const KArgs& A, uint32_t p, lds_int* stk, const NodeCache& nc = NodeCache{nullptr, 0u},
-                        uint32_t* cnt = nullptr) {
+                        uint32_t* cnt = nullptr, PhaseAcc* pa = nullptr) {
     const PrimaryRay pr = primary_ray(A, p);
     const uint32_t packet = (p | 63u) < A.P.num_paths ? A.P.packet : 0u;
-    const float4 rad = trace_path<false, kCount>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, packet, nc, cnt);
+    const float4 rad = trace_path<false, kCount>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, packet, nc, cnt, pa);
     accumulate_pixel(A, pr.accumIdx, rad);
 }
 
@@ -2270,6 +2306,13 @@ void k_path(KArgs A) {
             }
             return;
         }
+#if DXRPT_DIAG_PHASES
+        PhaseAcc pa = {{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, uint32_t(__builtin_amdgcn_s_memrealtime())};
+        if (p < A.P.num_paths) camera_path(A, p, stk, NodeCache{nullptr, 0u}, nullptr, &pa);
+        phase_mark(&pa, 7);
+        phase_flush(&pa);
+        return;
+#endif
         if (p >= A.P.num_paths) return;
         camera_path(A, p, stk);
         return;
@@ -2630,6 +2673,14 @@ hipError_t launch_trace_rays(const SceneDev& scene, const float4* rays, uint32_t
     else
         hipLaunchKernelGGL((k_trace_rays<2>), dim3(grid_for(n)), dim3(kBlock), lds, stream, scene, rays, n, flags, hits);
     return hipGetLastError();
+}
+
+hipError_t read_phase_ticks(unsigned long long out[8]) {
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return e;
+    if ((e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_ticks), 8 * sizeof(unsigned long long))) != hipSuccess) return e;
+    const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_phase_ticks), zero, sizeof(zero));
 }
 
 }  // namespace dxrpt

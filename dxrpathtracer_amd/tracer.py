@@ -136,6 +136,13 @@ class DXRPathTracer:
                                                       C.byref(n)), "dxrpt_get_wave_clocks")
         return out
 
+    def phase_clocks(self):
+        """Lane ticks per camera-path phase since the last call (kernel builds with -DDXRPT_DIAG_PHASES=1;
+        zeros otherwise), see dxrpt_get_phase_clocks."""
+        out = (C.c_uint64 * 8)()
+        self._check(self._L.dxrpt_get_phase_clocks(self._ctx, out), "dxrpt_get_phase_clocks")
+        return [int(v) for v in out]
+
     def post_process(self, settings: A.AppSettings, accum_ptr: int, width: int, height: int, out_ptr: int,
                      out_format: int = A.POST_FLOAT4, stream: int = 0):
         """PostProcessor::Render (PostProcessor.cpp:43-92): bloom + exposure + filmic tone map of the

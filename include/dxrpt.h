@@ -375,6 +375,12 @@ int dxrpt_get_stats(dxrpt_ctx* ctx, dxrpt_stats* out);
  * per-wave (start, end) s_memrealtime stamps, wave w = paths [64 w, 64 w + 64) in path-slot order;
  * copies min(max_waves, waves) pairs into out[2 w], out[2 w + 1] and the wave count into *num_waves. */
 int dxrpt_get_wave_clocks(dxrpt_ctx* ctx, uint64_t* out, uint32_t max_waves, uint32_t* num_waves);
+/* Diagnostic of kernel builds made with -DDXRPT_DIAG_PHASES=1 (zeros in the shipped build): lane time,
+ * in s_memrealtime ticks (100 MHz) summed over every lane of the full-frame megakernel, spent in each
+ * phase of a camera path since the last call -- 0 raygen + depth-1 closest hit, 1 depth-1 shading,
+ * 2 depth-1 shadow rays, 3/4/5 the same at depth 2, 6 depths >= 3, 7 accumulation and waiting for the
+ * wave's other lanes after the path ended.  Synchronises the device; reads and zeroes the sums. */
+int dxrpt_get_phase_clocks(dxrpt_ctx* ctx, uint64_t out[8]);
 
 /* TraceRay on arbitrary rays against the built acceleration structure (the DXR TraceRay call sites
  * RayTrace.hlsl:138,258,305,407,425 without the shading).  `rays` (device) holds num_rays pairs of

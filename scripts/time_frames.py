@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--lanes", type=int, default=None, help="DXRPT_OPT_MEGAKERNEL_LANES override")
     ap.add_argument("--wave-order", type=int, default=None, help="DXRPT_OPT_WAVE_ORDER override")
     ap.add_argument("--max-path", type=int, default=None, help="MaxPathLength override (a cost breakdown by depth)")
+    ap.add_argument("--phases", action="store_true",
+                    help="print the per-phase lane-time split of the timed frames (kernel builds with -DDXRPT_DIAG_PHASES=1)")
     args = ap.parse_args()
     import torch
     import dxrpathtracer_amd as D
@@ -97,6 +99,8 @@ def main():
     for f in range(5):
         t.render_raw(consts[f % 16], st, acc.data_ptr(), W, H, tiles=tiles, stream=stream.cuda_stream, lights=lights)
     torch.cuda.synchronize()
+    if args.phases:
+        t.phase_clocks()  # zero the sums of the warm-up frames
     rounds = []
     for r in range(args.rounds):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -110,6 +114,11 @@ def main():
     print(f"{args.label:24s} {args.config}{'' if args.max_path is None else f' L={L}'}{'' if args.wave_order is None else f' order={args.wave_order}'} share 1/{args.share} r{args.rank} {args.layout if args.share > 1 else ''}{args.band or ''}{' tile ' + args.tile if args.tile else ''}: median {statistics.median(rounds):.4f} "
           f"mean {statistics.mean(rounds):.4f} min {min(rounds):.4f} ms/frame  rays {s.radiance_rays + s.shadow_rays}",
           flush=True)
+    if args.phases:
+        ph = t.phase_clocks()
+        tot = float(sum(ph)) or 1.0
+        names = ("d1 trace", "d1 shade", "d1 shadow", "d2 trace", "d2 shade", "d2 shadow", "d>=3", "end/idle")
+        print("  phases (share of lane time): " + ", ".join(f"{nm} {v / tot:.3f}" for nm, v in zip(names, ph)), flush=True)
     t.close()
 
 
