@@ -48,6 +48,9 @@ constexpr int kStkStride = 64;
 #ifndef DXRPT_STACK_REMAT
 #define DXRPT_STACK_REMAT 0
 #endif
+#ifndef DXRPT_STACK_TID
+#define DXRPT_STACK_TID 1
+#endif
 PT_DEV lds_int* lane_stack(const SceneDev& S, int* stack) {
 #if DXRPT_STACK_REMAT
     // the wave's part scalar, the lane's from mbcnt: cheap to recompute, so the compiler need not keep
@@ -482,8 +485,24 @@ PT_DEV void ray8_init(Ray8& R, f3 o, f3 d, float tmin, float tmax, bool alpha, H
 // Group stack: `sp` entries; the top one lives in registers (`tos`), entries 0 .. sp-2 in LDS
 // (first kStackLds8) and in the thread's global spill slab (deeper), so a pop hands over the next
 // group at once and the LDS refill of `tos` overlaps the next node fetch.
+// DXRPT_STACK_TID (the megakernel's 64-thread workgroups, stk == nullptr): the lane's stack base is
+// recomputed at every access from the lane id (volatile asm: never kept live across the path, so it is
+// never spilled and reloaded from scratch on a push or pop).
+PT_DEV lds_int* stack_base(lds_int* stk) {
+#if DXRPT_STACK_TID
+    if (stk == nullptr) {
+        extern __shared__ int stack[];
+        uint32_t lane;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+        return (lds_int*)(stack) + lane;
+    }
+#endif
+    return stk;
+}
+
 PT_DEV void stack8_store(const SceneDev& S, lds_int* stk, int j, uint2 e) {
     if (j < kStackLds8) {
+        stk = stack_base(stk);
         stk[(2 * j) * kStkStride] = int(e.x);
         stk[(2 * j + 1) * kStkStride] = int(e.y);
     } else {  // rare: deep entries spill to this thread's global slab
@@ -492,7 +511,10 @@ PT_DEV void stack8_store(const SceneDev& S, lds_int* stk, int j, uint2 e) {
 }
 
 PT_DEV uint2 stack8_load(const SceneDev& S, const lds_int* stk, int j) {
-    if (j < kStackLds8) return make_uint2(uint32_t(stk[(2 * j) * kStkStride]), uint32_t(stk[(2 * j + 1) * kStkStride]));
+    if (j < kStackLds8) {
+        stk = const_cast<lds_int*>(stack_base(const_cast<lds_int*>(stk)));
+        return make_uint2(uint32_t(stk[(2 * j) * kStkStride]), uint32_t(stk[(2 * j + 1) * kStkStride]));
+    }
     return S.spill8[size_t(j - kStackLds8) * S.spill_stride + blockIdx.x * blockDim.x + threadIdx.x];
 }
 
@@ -2265,7 +2287,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0
 void k_path(KArgs A) {
     lut_fill(A.S);
     extern __shared__ int stack[];
+#if DXRPT_STACK_TID
+    lds_int* stk = nullptr;  // 64-thread workgroups: the base is the lane's, recomputed per access (stack_base)
+#else
     lds_int* stk = lane_stack(A.S, stack);
+#endif
     if (kGroup) {  // mega_lanes paths per wave, each traced by 64 / mega_lanes lanes
         const uint32_t lane = threadIdx.x & 63u;
         const WaveSlot ws = wave_slot(A);
@@ -2374,7 +2400,11 @@ void k_bake(KArgs A, BakeArgs B) {
         B.lightmap[texel] = make_float4(1.0f, 0.0f, 1.0f, 1.0f);
         return;
     }
+#if DXRPT_STACK_TID
+    const float4 r = trace_path<true>(A, i, texel, origin, dir, kFP32Max, nullptr, 0u);  // 64-thread workgroups
+#else
     const float4 r = trace_path<true>(A, i, texel, origin, dir, kFP32Max, lane_stack(A.S, stack), 0u);
+#endif
     float3 c = make_float3(r.x, r.y, r.z);
     const float4 prev = B.accum[texel];
     float3 sum = make_float3(prev.x, prev.y, prev.z);
@@ -2464,7 +2494,8 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
     hipError_t e = hipMemsetAsync(fb.counters, 0, (2 * kMaxDepthQueues * kQueueShards + 1) * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     if (fp.megakernel) {  // whole frame in k_path (timing: ev[0], ev[1] bracket the k_path launch)
-        const uint32_t tb = fp.trace_block;
+        // one wave per workgroup: the per-lane stack base is the lane's (DXRPT_STACK_TID, stack_base)
+        const uint32_t tb = 64u;
         const size_t ldsm = size_t(scene.stack_ints) * tb * sizeof(int);
         // mega_lanes < 64 (per-lane path, no persistent grid / LDS nodes): 64 threads per mega_lanes paths
         const bool twins = fp.mega_lanes < 64u && !fp.mega_persistent && !A.P.lds_nodes;

@@ -270,7 +270,9 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 #define DXRPT_OPT_CHUNKS_PER_WAVE 6u  /* wave-pool mode: 64-ray chunks owned by each wave (1..64, default 4) */
 #define DXRPT_OPT_POSTPONE_TRIS 7u    /* wave-pool mode: batch triangle tests until this many lanes have some
                                          (0 = test with the node visit, default) */
-#define DXRPT_OPT_TRACE_BLOCK 8u      /* workgroup size of the one-thread-per-ray traversal kernels: 64 (default), 128, 256 */
+#define DXRPT_OPT_TRACE_BLOCK 8u      /* workgroup size of the one-thread-per-ray traversal kernels of the
+                                        wavefront schedule: 64 (default), 128, 256 (the megakernel always
+                                        runs one wave per workgroup) */
 #define DXRPT_OPT_OCCUPANCY 9u        /* BVH8 closest-hit register budget: 0 = compiler default, 7 (default) or 8 waves/SIMD */
 #define DXRPT_OPT_SHADE_BLOCK 10u     /* workgroup size of the shading kernel: 64, 128, 256 (default) */
 #define DXRPT_OPT_SHADE_OCCUPANCY 11u /* shading kernel register budget: 0 = compiler default, 6, 7 or 8 waves/SIMD */
