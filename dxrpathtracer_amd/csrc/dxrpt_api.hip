@@ -125,6 +125,7 @@ struct dxrpt_ctx {
     uint32_t wclock_waves = 0;
     // DXRPT_OPT_WAVE_ORDER: per wave slot, the last frame's duration and the order built from it
     uint32_t opt_wave_order = 2;  // 0 off, 1 on, 2 by frame size (see render)
+    uint32_t opt_split_permille = 0;  // DXRPT_OPT_SPLIT_UNITS
     DevBuf d_wave_cost, d_wave_order, d_wave_hist;  // hist: 2 frames x (histogram, cursor) x kWaveClasses
     uint32_t order_parity = 0;
     uint64_t order_key = 0;     // (waves, lanes, tiles generation) the order was built for
@@ -501,6 +502,9 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
             require(value <= 2, "dxrpt_set_option: wave order must be 0, 1 or 2");
             ctx->opt_wave_order = uint32_t(value);
             ctx->order_ready = false;
+        } else if (option == DXRPT_OPT_SPLIT_UNITS) {
+            require(value <= 1000, "dxrpt_set_option: split units must be 0..1000 (per mille of the waves)");
+            ctx->opt_split_permille = uint32_t(value);
         } else if (option == DXRPT_OPT_MEGAKERNEL_PATHS) {
             ctx->opt_mega_paths = value > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(value);
         } else if (option == DXRPT_OPT_MEGAKERNEL_OCCUPANCY) {
@@ -783,6 +787,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.wave_order = nullptr;
         fp.wave_cost = nullptr;
         fp.wave_hist = nullptr;
+        fp.split_units = 0;
         // 32 KiB of LDS per 256-thread workgroup -> 5 resident workgroups per CU (160 KiB)
         fp.chunks_per_wave = ctx->opt_trav_mode == 1 ? ctx->opt_chunks : 0u;
         fp.refill_lanes = ctx->opt_refill;
@@ -857,6 +862,9 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             fp.wave_cost = ctx->d_wave_cost.as<uint32_t>();
             fp.wave_hist = ctx->d_wave_hist.as<uint32_t>() + ctx->order_parity * 2 * kWaveClasses;
             fp.wave_order = ctx->order_ready ? ctx->d_wave_order.as<uint32_t>() : nullptr;
+            // the costliest slots of the order split in two (path groups, once an order exists)
+            if (lanes < 64u && ctx->order_ready && ctx->opt_split_permille)
+                fp.split_units = std::min<uint32_t>(order_waves, uint32_t((uint64_t(order_waves) * ctx->opt_split_permille + 999u) / 1000u));
             if (ctx->opt_wave_clocks) {  // per-slot stamps of an ordered frame (diagnostic)
                 ctx->wclock_waves = order_waves;
                 ctx->d_wclock.ensure(size_t(order_waves) * 2 * sizeof(unsigned long long));

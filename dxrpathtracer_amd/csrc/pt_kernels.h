@@ -151,6 +151,11 @@ struct FrameParams {
     const uint32_t* wave_order;
     uint32_t* wave_cost;
     uint32_t* wave_hist;
+    // Path-group frames with an order (DXRPT_OPT_SPLIT_UNITS): the first split_units slots of the order
+    // (the costliest) each run as TWO waves of mega_lanes / 2 paths (twice the lanes per path), launch
+    // waves 0 .. 2 split_units - 1; the other slots follow one wave each.  A split slot keeps the
+    // class it was measured with unsplit.
+    uint32_t split_units;
 };
 
 constexpr uint32_t kWaveClasses = 256;

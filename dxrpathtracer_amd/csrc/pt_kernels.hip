@@ -2188,10 +2188,10 @@ PT_DEV void camera_path(const KArgs& A, uint32_t p, lds_int* stk, const NodeCach
     accumulate_pixel(A, pr.accumIdx, rad);
 }
 
-// A path of a path group (DXRPT_OPT_MEGAKERNEL_LANES): only member 0 writes the pixel.
-PT_DEV void camera_path_group(const KArgs& A, uint32_t p, lds_int* stk, bool member0) {
+// A path of a path group (DXRPT_OPT_MEGAKERNEL_LANES; g paths per wave): only member 0 writes the pixel.
+PT_DEV void camera_path_group(const KArgs& A, uint32_t p, lds_int* stk, bool member0, uint32_t g) {
     const PrimaryRay pr = primary_ray(A, p);
-    const float4 rad = trace_path_group(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, A.P.mega_lanes);
+    const float4 rad = trace_path_group(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, g);
     if (member0) accumulate_pixel(A, pr.accumIdx, rad);
 }
 
@@ -2205,13 +2205,29 @@ struct WaveSlot {
     unsigned long long t0;
 };
 
-PT_DEV WaveSlot wave_slot(const KArgs& A) {
+PT_DEV WaveSlot wave_slot(const KArgs& A, uint32_t* half = nullptr) {
     WaveSlot ws;
-    const uint32_t w = uint32_t(__builtin_amdgcn_readfirstlane(int((blockIdx.x * blockDim.x + threadIdx.x) >> 6)));
+    uint32_t w = uint32_t(__builtin_amdgcn_readfirstlane(int((blockIdx.x * blockDim.x + threadIdx.x) >> 6)));
+    if (half) {  // path groups: the costliest split_units slots run as two half waves each (half 1, 2)
+        const uint32_t k = A.P.split_units;
+        *half = w < 2u * k ? 1u + (w & 1u) : 0u;
+        w = w < 2u * k ? w >> 1 : w - k;
+    }
     ws.slot = w;
     if (A.P.wave_order) ws.slot = A.P.wave_order[w];
     ws.t0 = A.P.wave_cost ? __builtin_amdgcn_s_memrealtime() : 0ull;
     return ws;
+}
+
+// A split slot (half 1 / 2) keeps its unsplit class: half 1 counts it again in the histogram, so the
+// next order holds it among the costliest (its clock stamps are half 1's).
+PT_DEV void wave_slot_split_done(const KArgs& A, const WaveSlot& ws, uint32_t half) {
+    if (!A.P.wave_cost || half != 1u || (threadIdx.x & 63u) != 0u) return;
+    atomicAdd(&A.P.wave_hist[A.P.wave_cost[ws.slot]], 1u);
+    if (A.P.wave_clock) {
+        A.P.wave_clock[2 * ws.slot] = ws.t0;
+        A.P.wave_clock[2 * ws.slot + 1] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 PT_DEV void wave_slot_done(const KArgs& A, const WaveSlot& ws) {
@@ -2294,10 +2310,14 @@ void k_path(KArgs A) {
 #endif
     if (kGroup) {  // mega_lanes paths per wave, each traced by 64 / mega_lanes lanes
         const uint32_t lane = threadIdx.x & 63u;
-        const WaveSlot ws = wave_slot(A);
-        const uint32_t q = ws.slot * A.P.mega_lanes + (lane & (A.P.mega_lanes - 1u));
-        if (q < A.P.num_paths) camera_path_group(A, q, stk, lane < A.P.mega_lanes);
-        wave_slot_done(A, ws);
+        uint32_t half = 0;
+        const WaveSlot ws = wave_slot(A, &half);
+        // a split slot's half h traces paths [(h - 1) g, h g) of the slot with g = mega_lanes / 2
+        const uint32_t g = half ? A.P.mega_lanes >> 1 : A.P.mega_lanes;
+        const uint32_t q = ws.slot * A.P.mega_lanes + (half ? (half - 1u) * g : 0u) + (lane & (g - 1u));
+        if (q < A.P.num_paths) camera_path_group(A, q, stk, lane < g, g);
+        if (half) wave_slot_split_done(A, ws, half);
+        else wave_slot_done(A, ws);
         return;
     }
     if (!kPersistent && !kLds && !kCount && kOrder) {
@@ -2499,7 +2519,8 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
         const size_t ldsm = size_t(scene.stack_ints) * tb * sizeof(int);
         // mega_lanes < 64 (per-lane path, no persistent grid / LDS nodes): 64 threads per mega_lanes paths
         const bool twins = fp.mega_lanes < 64u && !fp.mega_persistent && !A.P.lds_nodes;
-        const uint64_t threads = twins ? (uint64_t(fp.num_paths) + fp.mega_lanes - 1u) / fp.mega_lanes * 64u : fp.num_paths;
+        const uint64_t threads = twins ? ((uint64_t(fp.num_paths) + fp.mega_lanes - 1u) / fp.mega_lanes + fp.split_units) * 64u
+                                       : fp.num_paths;
         const uint32_t gm = uint32_t((threads + tb - 1u) / tb);
         if (ev) (void)hipEventRecord(ev[0], stream);
         if (A.P.trav) {  // census frame (DXRPT_OPT_COUNT_TRAVERSAL): same schedule, counting instantiation

@@ -346,6 +346,11 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                      path order.  2 (default): 1 for frames of at most 3 rounds of
                                      resident waves (a GPU's share of a multi-GPU frame), else 0.
                                      Images identical in every mode. */
+#define DXRPT_OPT_SPLIT_UNITS 30u    /* path-group frames with a wave order: the costliest this-many
+                                        per mille of the frame's waves (at least one when > 0) each run
+                                        as two waves of half the paths, twice the lanes per path -- the
+                                        slowest waves set a small frame's time.  Default 0.  Identical
+                                        results. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

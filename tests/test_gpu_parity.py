@@ -578,12 +578,13 @@ def test_megakernel_lanes_and_partial_waves_are_bit_identical(torch_cuda, name, 
 
 
 @pytest.mark.parametrize("name,lanes,W,H", [("sponza", 64, 352, 200), ("suntemple", 32, 320, 180),
-                                            ("sponza", 64, 100, 50)])
+                                            ("sponza", 64, 100, 50), ("sponza", 32, 100, 50)])
 def test_wave_order_is_bit_identical(torch_cuda, name, lanes, W, H):
     # DXRPT_OPT_WAVE_ORDER: from the second frame on, waves start costliest first (the order is built
     # on the device from the previous frame's wave durations); every frame -- a progressive sequence
     # into one accumulation buffer, then a switch to a band share (the order resets) and back -- must
-    # equal the path-ordered frames bit for bit
+    # equal the path-ordered frames bit for bit.  Path-group frames also split their costliest slots
+    # (DXRPT_OPT_SPLIT_UNITS: 5 % of the slots, and every slot) into two half waves.
     torch = torch_cuda
     sc, sky = scene_bundle(name)
     st = sc.settings(MaxPathLength=3)
@@ -594,8 +595,9 @@ def test_wave_order_is_bit_identical(torch_cuda, name, lanes, W, H):
     try:
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30)
         t.set_option(A.OPT_MEGAKERNEL_LANES, lanes)
-        for order in (0, 1):
+        for order, split in ((0, 0), (1, 0)) + (((1, 50), (1, 1000)) if lanes < 64 else ()):
             t.set_option(A.OPT_WAVE_ORDER, order)
+            t.set_option(A.OPT_SPLIT_UNITS, split)
             acc = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
             share = torch.zeros((lay.counts[1], 4), dtype=torch.float32, device="cuda")
             frames = []
@@ -609,9 +611,11 @@ def test_wave_order_is_bit_identical(torch_cuda, name, lanes, W, H):
                                rtc=rtc, lights=lights)
                     frames.append(share.cpu().numpy().copy())
             runs.append(frames)
-        for a, b in zip(*runs):
-            np.testing.assert_array_equal(b, a)
+        for run in runs[1:]:
+            for a, b in zip(runs[0], run):
+                np.testing.assert_array_equal(b, a)
     finally:
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
         t.set_option(A.OPT_MEGAKERNEL_LANES, A.DEFAULT_MEGAKERNEL_LANES)
         t.set_option(A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)
+        t.set_option(A.OPT_SPLIT_UNITS, A.DEFAULT_SPLIT_UNITS)
