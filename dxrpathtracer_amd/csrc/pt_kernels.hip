@@ -2030,6 +2030,92 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
     return rad;
 }
 
+// DXRPT_GROUP_PAIRS: the path-group traversal tests a leaf's triangles two at a time -- both records in
+// one memory round trip, both geometric tests against the bound at the pair's start (a superset of the
+// sequential candidates), both candidates' alpha inputs (opacity descriptor + UVs) and then both
+// opacity taps in flight together, acceptance in order with the live bound: the hits of testing them one
+// after the other, in half the dependent round trips (the slowest waves of a small frame are
+// alpha-tested shadow rays through foliage).
+#ifndef DXRPT_GROUP_PAIRS
+#define DXRPT_GROUP_PAIRS 1
+#endif
+
+// The alpha inputs of triangle `gtri` on geometry `geom` for a per-lane candidate (issued, not waited on).
+struct LaneAlpha {
+    GeoTex op;
+    float2 uv0, uv1, uv2;
+};
+PT_DEV LaneAlpha lane_alpha_issue(const SceneDev& S, uint32_t geom, uint32_t gtri) {
+    LaneAlpha a;
+    a.op = S.geoshade[geom].opacity;
+    const float2* V = reinterpret_cast<const float2*>(S.tri_verts + size_t(gtri) * 12u);
+    a.uv0 = V[3];
+    a.uv1 = V[11];
+    a.uv2 = V[19];
+    return a;
+}
+
+// Opacity of a per-lane candidate at barycentrics (b1, b2): AnyHitShader's tap (alpha_accepts), split
+// so two candidates' taps can be in flight together.
+PT_DEV OpacityTap lane_alpha_tap(const SceneDev& S, const LaneAlpha& a, float b1, float b2) {
+    const float w0 = (1.0f - b1) - b2;
+    const float u = bary_lerp(a.uv0.x, a.uv1.x, a.uv2.x, w0, b1, b2);
+    const float v = bary_lerp(a.uv0.y, a.uv1.y, a.uv2.y, w0, b1, b2);
+    return opacity_issue(S, tex_desc(a.op), u, v);
+}
+
+PT_DEV bool trav8_tris_pairs(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32_t tbits, HitRec& h, bool any) {
+    while (tbits) {
+        const uint32_t b0 = uint32_t(__builtin_ctz(tbits));
+        tbits &= tbits - 1u;
+        const bool two = tbits != 0u;
+        const uint32_t b1 = two ? uint32_t(__builtin_ctz(tbits)) : b0;
+        if (two) tbits &= tbits - 1u;
+        const TriRec r0 = load_tri_raw(S, tbase + b0), r1 = load_tri_raw(S, tbase + b1);
+        pin_tri(r0);
+        pin_tri(r1);
+        float t0 = 0.0f, u0 = 0.0f, v0 = 0.0f, t1 = 0.0f, u1 = 0.0f, v1 = 0.0f;
+        const bool c0 = any ? tri_candidate<true>(r0, R.o, R.d, R.tmin, R.tmax, h, t0, u0, v0)
+                            : tri_candidate<false>(r0, R.o, R.d, R.tmin, R.tmax, h, t0, u0, v0);
+        const bool c1 = two && (any ? tri_candidate<true>(r1, R.o, R.d, R.tmin, R.tmax, h, t1, u1, v1)
+                                    : tri_candidate<false>(r1, R.o, R.d, R.tmin, R.tmax, h, t1, u1, v1));
+        if (!c0 && !c1) continue;
+        const bool n0 = c0 && R.alpha && !(fbits(r0.p2.w) & kTriOpaque);
+        const bool n1 = c1 && R.alpha && !(fbits(r1.p2.w) & kTriOpaque);
+        float o0 = 1.0f, o1 = 1.0f;
+        if (n0 || n1) {  // AnyHitShader (RayTrace.hlsl:485-507) for the candidates on alpha-tested geometry
+            const LaneAlpha a0 = lane_alpha_issue(S, fbits(r0.p1.w), fbits(r0.p0.w));
+            const LaneAlpha a1 = lane_alpha_issue(S, fbits(r1.p1.w), fbits(r1.p0.w));
+            asm volatile("" ::"v"(a0.op.offset), "v"(a0.op.whf), "v"(a0.uv0.x), "v"(a0.uv0.y), "v"(a0.uv1.x), "v"(a0.uv1.y),
+                         "v"(a0.uv2.x), "v"(a0.uv2.y), "v"(a1.op.offset), "v"(a1.op.whf), "v"(a1.uv0.x), "v"(a1.uv0.y),
+                         "v"(a1.uv1.x), "v"(a1.uv1.y), "v"(a1.uv2.x), "v"(a1.uv2.y));
+            const bool m0 = n0 && a0.op.whf != 0u, m1 = n1 && a1.op.whf != 0u;
+            OpacityTap q0{}, q1{};
+            if (m0) q0 = lane_alpha_tap(S, a0, u0, v0);
+            if (m1) q1 = lane_alpha_tap(S, a1, u1, v1);
+            if (m0) o0 = opacity_finish(S, q0);
+            if (m1) o1 = opacity_finish(S, q1);
+        }
+        if (c0 && !(o0 < 0.35f) && (any || t0 < h.t || (t0 == h.t && fbits(r0.p0.w) < h.tri))) {
+            h.t = t0;
+            h.tri = fbits(r0.p0.w);
+            h.b1 = u0;
+            h.b2 = v0;
+            h.geom = fbits(r0.p1.w);
+            if (any) return true;
+        }
+        if (c1 && !(o1 < 0.35f) && (any || t1 < h.t || (t1 == h.t && fbits(r1.p0.w) < h.tri))) {
+            h.t = t1;
+            h.tri = fbits(r1.p0.w);
+            h.b1 = u1;
+            h.b2 = v1;
+            h.geom = fbits(r1.p1.w);
+            if (any) return true;
+        }
+    }
+    return false;
+}
+
 // Per-lane BVH8 traversal whose kind is a lane value (closest hit, or any hit when `any`): the
 // path-group schedule below runs a continuation ray and shadow rays in one loop.  Same node order and
 // triangle tests as traverse<8, any, false>, so the same hit / visibility.
@@ -2048,7 +2134,8 @@ PT_DEV bool traverse8_rt(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, 
         uint32_t tbase = 0, tbits = 0;
         const bool more = trav8_node<false>(S, R, node, sp, stk, tos, h, tbase, tbits, nv);
         bool done = false;
-        while (tbits) {
+        if (DXRPT_GROUP_PAIRS && tbits) done = trav8_tris_pairs(S, R, tbase, tbits, h, any);
+        while (!DXRPT_GROUP_PAIRS && tbits) {
             const uint32_t b = uint32_t(__builtin_ctz(tbits));
             tbits &= tbits - 1u;
             const TriRec r = load_tri(S, tbase + b);
