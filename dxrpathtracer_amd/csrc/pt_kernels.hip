@@ -784,6 +784,12 @@ PT_DEV uint32_t wave_or8(uint32_t m) {
 // traversal would, so the result is still that of traverse8).
 constexpr uint32_t kSwitchMinVisits = 4;
 
+// DXRPT_PACKET_PREFETCH: the packet traversal selects its next node right after the box test and loads
+// it while the current node's leaf triangles are tested (same visit order and bounds, same results).
+#ifndef DXRPT_PACKET_PREFETCH
+#define DXRPT_PACKET_PREFETCH 0
+#endif
+
 template <bool kAnyHit>
 PT_DEV bool traverse8_from(const SceneDev& S, const Ray8& R, lds_int* stk, HitRec& h);
 
@@ -808,8 +814,13 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
     uint32_t sbase = 0, sword = 0;  // stack entry j in lane j
     uint32_t sp = 0;
     uint32_t node = 0;
+#if DXRPT_PACKET_PREFETCH
+    Node8Words W = load_node8_uniform(S, 0u);
+#endif
     while (true) {
+#if !DXRPT_PACKET_PREFETCH
         const Node8Words W = load_node8_uniform(S, node);
+#endif
         if (counter) ++cnt[0];
         const uint32_t hm = live ? box8_hits(R, W, h.t) : 0u;
         const uint32_t um = wave_or8(hm);
@@ -834,6 +845,40 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
             tbits |= ((1u << (m >> 5)) - 1u) << (m & 31u);
         }
         const uint32_t tbase = W.w1.y;
+#if DXRPT_PACKET_PREFETCH
+        uint32_t ihits = um & imask;
+        if (oct & 1u) ihits = ((ihits & 0x55u) << 1) | ((ihits >> 1) & 0x55u);
+        if (oct & 2u) ihits = ((ihits & 0x33u) << 2) | ((ihits >> 2) & 0x33u);
+        if (oct & 4u) ihits = ((ihits & 0x0Fu) << 4) | ((ihits >> 4) & 0x0Fu);
+        uint32_t gbase = W.w1.x;
+        uint32_t gword = (ihits << 24) | imask;
+        bool found = false;
+        while (true) {
+            if (gword >> 24) {
+                const uint32_t k = 31u - uint32_t(__builtin_clz(gword));
+                gword &= ~(1u << k);
+                const uint32_t slot = (k - 24u) ^ oct;
+                node = gbase + uint32_t(__builtin_popcount(gword & 0xFFu & ((1u << slot) - 1u)));
+                if (gword >> 24) {  // push the rest of the group
+                    if (lane == sp) {
+                        sbase = gbase;
+                        sword = gword;
+                    }
+                    ++sp;
+                }
+                found = true;
+                break;
+            }
+            if (sp == 0u) break;
+            --sp;
+            gbase = uint32_t(__builtin_amdgcn_readlane(int(sbase), int(sp)));
+            gword = uint32_t(__builtin_amdgcn_readlane(int(sword), int(sp)));
+        }
+        // the next node is known before this node's triangles are tested (their hits only tighten the
+        // bound its box test will use): its words are in flight while they are
+        Node8Words Wn = W;
+        if (found) Wn = load_node8_uniform(S, node);
+#endif
         while (kPair && tbits) {
             const uint32_t b0 = uint32_t(__builtin_ctz(tbits));
             tbits &= tbits - 1u;
@@ -890,6 +935,11 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
             if (counter) ++cnt[1];
             if (live && test_tri_rec<kAnyHit>(S, r, R.o, R.d, R.tmin, R.tmax, R.alpha, h)) live = false;  // occluded
         }
+#if DXRPT_PACKET_PREFETCH
+        if (kAnyHit && __ballot(live) == 0ull) break;
+        if (!found) break;
+        W = Wn;
+#else
         if (kAnyHit && __ballot(live) == 0ull) break;
         uint32_t ihits = um & imask;
         if (oct & 1u) ihits = ((ihits & 0x55u) << 1) | ((ihits >> 1) & 0x55u);
@@ -920,6 +970,7 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
             gword = uint32_t(__builtin_amdgcn_readlane(int(sword), int(sp)));
         }
         if (!found) break;
+#endif
     }
     return h.tri != kMiss;
 }
