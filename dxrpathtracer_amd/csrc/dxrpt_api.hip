@@ -126,6 +126,7 @@ struct dxrpt_ctx {
     // DXRPT_OPT_WAVE_ORDER: per wave slot, the last frame's duration and the order built from it
     uint32_t opt_wave_order = 2;  // 0 off, 1 on, 2 by frame size (see render)
     uint32_t opt_split_permille = 0;  // DXRPT_OPT_SPLIT_UNITS
+    uint32_t opt_xcd_chunk = 8;       // DXRPT_OPT_XCD_CHUNK (r02: 1080p 2.100 -> 2.075 ms, C4 2.276 -> 2.252)
     DevBuf d_wave_cost, d_wave_order, d_wave_hist;  // hist: 2 frames x (histogram, cursor) x kWaveClasses
     uint32_t order_parity = 0;
     uint64_t order_key = 0;     // (waves, lanes, tiles generation) the order was built for
@@ -502,6 +503,9 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
             require(value <= 2, "dxrpt_set_option: wave order must be 0, 1 or 2");
             ctx->opt_wave_order = uint32_t(value);
             ctx->order_ready = false;
+        } else if (option == DXRPT_OPT_XCD_CHUNK) {
+            require(value <= 4096, "dxrpt_set_option: XCD chunk must be 0..4096 blocks");
+            ctx->opt_xcd_chunk = uint32_t(value);
         } else if (option == DXRPT_OPT_SPLIT_UNITS) {
             require(value <= 1000, "dxrpt_set_option: split units must be 0..1000 (per mille of the waves)");
             ctx->opt_split_permille = uint32_t(value);
@@ -788,6 +792,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.wave_cost = nullptr;
         fp.wave_hist = nullptr;
         fp.split_units = 0;
+        fp.xcd_chunk = ctx->opt_xcd_chunk;
         // 32 KiB of LDS per 256-thread workgroup -> 5 resident workgroups per CU (160 KiB)
         fp.chunks_per_wave = ctx->opt_trav_mode == 1 ? ctx->opt_chunks : 0u;
         fp.refill_lanes = ctx->opt_refill;

@@ -156,6 +156,10 @@ struct FrameParams {
     // waves 0 .. 2 split_units - 1; the other slots follow one wave each.  A split slot keeps the
     // class it was measured with unsplit.
     uint32_t split_units;
+    // Megakernel, path-ordered frames (DXRPT_OPT_XCD_CHUNK): workgroup i runs on XCD i mod 8, so the
+    // kernel maps it to pixel block (8 t + (i mod 8 + t) mod 8) C + (i / 8) mod C, t = (i / 8) / C: each
+    // XCD (own L2) takes runs of C consecutive 8x8 blocks, runs dealt to the XCDs in rotation.  0: block i.
+    uint32_t xcd_chunk;
 };
 
 constexpr uint32_t kWaveClasses = 256;

@@ -2497,6 +2497,16 @@ void k_path(KArgs A) {
         phase_flush(&pa);
         return;
 #endif
+        if (A.P.xcd_chunk) {  // XCD-local runs of blocks (FrameParams::xcd_chunk); the tail stays in order
+            // run t of XCD x is chunk 8 t + (x + t) mod 8: the XCDs' chunks rotate from run to run, so no
+            // XCD keeps the same screen columns (a fixed deal makes stripes of unequal cost)
+            const uint32_t C = A.P.xcd_chunk, i = blockIdx.x, full = gridDim.x / (8u * C) * (8u * C);
+            const uint32_t k = i >> 3, t = k / C;
+            const uint32_t b = i < full ? (t * 8u + (((i & 7u) + t) & 7u)) * C + k % C : i;
+            const uint32_t q = b * blockDim.x + threadIdx.x;
+            if (q < A.P.num_paths) camera_path(A, q, stk);
+            return;
+        }
         if (p >= A.P.num_paths) return;
         camera_path(A, p, stk);
         return;

@@ -351,6 +351,10 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                         as two waves of half the paths, twice the lanes per path -- the
                                         slowest waves set a small frame's time.  Default 0.  Identical
                                         results. */
+#define DXRPT_OPT_XCD_CHUNK 31u      /* path-ordered megakernel frames: each XCD (its own L2) takes runs of
+                                        this many consecutive 8x8 pixel blocks, runs dealt to the 8 XCDs
+                                        in rotation (default 8; 0: block i on workgroup i, i.e.
+                                        neighbouring blocks on different XCDs).  Identical results. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

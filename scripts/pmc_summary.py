@@ -71,9 +71,10 @@ def main(prof, rnd):
     # (packet and per-lane variants), launch-weighted
     for kind, prefixes in (("k_trace", ("k_trace<false", "k_trace_packet")),
                            ("k_shadow", ("k_shadow<false", "k_shadow_packet")), ("k_path", ("k_path<",))):
-        # k_path<..., true> is the bench's one instrumented census frame (kCount), not a timed launch
+        # k_path<occ, persistent, lds, group, kCount = true, order> is the bench's one instrumented census
+        # frame, not a timed launch
         cands = [k for k in out["kernels"] if k.startswith(prefixes)
-                 and not (kind == "k_path" and k.endswith(", true>"))]
+                 and not (kind == "k_path" and k[k.index("<") + 1:-1].split(", ")[4:5] == ["true"])]
         if not cands:
             continue
         calls = sum(out["kernels"][k].get("calls", 0) for k in cands)

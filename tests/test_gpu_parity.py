@@ -619,3 +619,29 @@ def test_wave_order_is_bit_identical(torch_cuda, name, lanes, W, H):
         t.set_option(A.OPT_MEGAKERNEL_LANES, A.DEFAULT_MEGAKERNEL_LANES)
         t.set_option(A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)
         t.set_option(A.OPT_SPLIT_UNITS, A.DEFAULT_SPLIT_UNITS)
+
+
+@pytest.mark.parametrize("name,W,H", [("sponza", 352, 200), ("suntemple", 100, 50)])
+def test_xcd_chunk_mapping_is_bit_identical(torch_cuda, name, W, H):
+    # DXRPT_OPT_XCD_CHUNK: path-ordered megakernel frames deal runs of C blocks to the XCDs in rotation;
+    # which workgroup traces which block changes, nothing else (C = 3: a partial group of runs and a
+    # partial last wave at 100 x 50)
+    torch = torch_cuda
+    sc, sky = scene_bundle(name)
+    st = sc.settings(MaxPathLength=3)
+    t = tracer(name)
+    try:
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30)
+        t.set_option(A.OPT_MEGAKERNEL_LANES, 64)
+        t.set_option(A.OPT_WAVE_ORDER, 0)
+        imgs = []
+        for c in (0, 8, 3):
+            t.set_option(A.OPT_XCD_CHUNK, c)
+            imgs.append(gpu_render(torch, name, W, H, st, 1).cpu().numpy())
+        for img in imgs[1:]:
+            np.testing.assert_array_equal(img, imgs[0])
+    finally:
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
+        t.set_option(A.OPT_MEGAKERNEL_LANES, A.DEFAULT_MEGAKERNEL_LANES)
+        t.set_option(A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)
+        t.set_option(A.OPT_XCD_CHUNK, A.DEFAULT_XCD_CHUNK)
