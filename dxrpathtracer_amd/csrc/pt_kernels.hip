@@ -786,6 +786,10 @@ constexpr uint32_t kSwitchMinVisits = 4;
 
 // DXRPT_PACKET_PREFETCH: the packet traversal selects its next node right after the box test and loads
 // it while the current node's leaf triangles are tested (same visit order and bounds, same results).
+// DXRPT_ORDER_XCD: cost-ordered frames also deal runs of xcd_chunk consecutive order positions to the XCDs.
+#ifndef DXRPT_ORDER_XCD
+#define DXRPT_ORDER_XCD 0
+#endif
 #ifndef DXRPT_PACKET_PREFETCH
 #define DXRPT_PACKET_PREFETCH 0
 #endif
@@ -2343,6 +2347,15 @@ struct WaveSlot {
     unsigned long long t0;
 };
 
+// FrameParams::xcd_chunk: position of launch index i (of n, one wave per workgroup, workgroup i on XCD
+// i mod 8) when each XCD takes runs of C consecutive positions, the runs dealt in rotation: run t of
+// XCD x is run 8 t + (x + t) mod 8.  A bijection on [0, n) (the last partial group stays in order).
+PT_DEV uint32_t xcd_position(uint32_t i, uint32_t n, uint32_t C) {
+    const uint32_t full = n / (8u * C) * (8u * C);
+    const uint32_t k = i >> 3, t = k / C;
+    return i < full ? (t * 8u + (((i & 7u) + t) & 7u)) * C + k % C : i;
+}
+
 PT_DEV WaveSlot wave_slot(const KArgs& A, uint32_t* half = nullptr) {
     WaveSlot ws;
     uint32_t w = uint32_t(__builtin_amdgcn_readfirstlane(int((blockIdx.x * blockDim.x + threadIdx.x) >> 6)));
@@ -2352,7 +2365,13 @@ PT_DEV WaveSlot wave_slot(const KArgs& A, uint32_t* half = nullptr) {
         w = w < 2u * k ? w >> 1 : w - k;
     }
     ws.slot = w;
-    if (A.P.wave_order) ws.slot = A.P.wave_order[w];
+    if (A.P.wave_order) {
+#if DXRPT_ORDER_XCD
+        // the cost order's neighbours (same class, path order within it) on one XCD
+        if (A.P.xcd_chunk && !(half && A.P.split_units)) w = xcd_position(w, gridDim.x * (blockDim.x >> 6), A.P.xcd_chunk);
+#endif
+        ws.slot = A.P.wave_order[w];
+    }
     ws.t0 = A.P.wave_cost ? __builtin_amdgcn_s_memrealtime() : 0ull;
     return ws;
 }
@@ -2500,10 +2519,7 @@ void k_path(KArgs A) {
         if (A.P.xcd_chunk) {  // XCD-local runs of blocks (FrameParams::xcd_chunk); the tail stays in order
             // run t of XCD x is chunk 8 t + (x + t) mod 8: the XCDs' chunks rotate from run to run, so no
             // XCD keeps the same screen columns (a fixed deal makes stripes of unequal cost)
-            const uint32_t C = A.P.xcd_chunk, i = blockIdx.x, full = gridDim.x / (8u * C) * (8u * C);
-            const uint32_t k = i >> 3, t = k / C;
-            const uint32_t b = i < full ? (t * 8u + (((i & 7u) + t) & 7u)) * C + k % C : i;
-            const uint32_t q = b * blockDim.x + threadIdx.x;
+            const uint32_t q = xcd_position(blockIdx.x, gridDim.x, A.P.xcd_chunk) * blockDim.x + threadIdx.x;
             if (q < A.P.num_paths) camera_path(A, q, stk);
             return;
         }
