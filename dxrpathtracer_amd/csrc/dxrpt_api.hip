@@ -683,6 +683,7 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
         } else {
             ctx->d_nodes.upload(res.nodes.data(), res.nodes.size() * sizeof(BvhNode));
         }
+        tris.resize(size_t(nrefs) + 6u, TriRecord{});  // padding: packet chunk loads read up to 256 B past a record
         ctx->d_tris.upload(tris.data(), tris.size() * sizeof(TriRecord));
         {   // shading-side copy of each triangle's vertices: one contiguous 192-B record per gtri, so a
             // hit gathers 2 cache lines in one round trip instead of 3 indices then 3 vertices

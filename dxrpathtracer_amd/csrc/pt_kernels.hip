@@ -786,6 +786,12 @@ constexpr uint32_t kSwitchMinVisits = 4;
 
 // DXRPT_PACKET_PREFETCH: the packet traversal selects its next node right after the box test and loads
 // it while the current node's leaf triangles are tested (same visit order and bounds, same results).
+// DXRPT_PACKET_VCHUNK: the packet traversal loads a node's pending triangle records as 64-dword vector
+// chunks (lane j: dword j) and reads them with readlane, instead of scalar loads of one record or pair
+// per round trip (the tris buffer is padded by six records so a chunk never reads past it).
+#ifndef DXRPT_PACKET_VCHUNK
+#define DXRPT_PACKET_VCHUNK 0
+#endif
 // DXRPT_ORDER_XCD: cost-ordered frames also deal runs of xcd_chunk consecutive order positions to the XCDs.
 #ifndef DXRPT_ORDER_XCD
 #define DXRPT_ORDER_XCD 0
@@ -818,6 +824,7 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
     uint32_t sbase = 0, sword = 0;  // stack entry j in lane j
     uint32_t sp = 0;
     uint32_t node = 0;
+    const bool full = DXRPT_PACKET_VCHUNK && __ballot(1) == ~0ull;  // every lane loads its chunk dword
 #if DXRPT_PACKET_PREFETCH
     Node8Words W = load_node8_uniform(S, 0u);
 #endif
@@ -849,6 +856,34 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
             tbits |= ((1u << (m >> 5)) - 1u) << (m & 31u);
         }
         const uint32_t tbase = W.w1.y;
+#if DXRPT_PACKET_VCHUNK
+        if (full && tbits) {
+            // the pending records (contiguous from tbase) in 64-dword chunks, one vector load per chunk:
+            // lane j holds dword j; each record is then read lane by lane (readlane) -- one memory round
+            // trip for up to five records instead of one per scalar-loaded pair
+            const uint32_t* TD = reinterpret_cast<const uint32_t*>(S.tris);
+            uint32_t lo = tbase + uint32_t(__builtin_ctz(tbits));
+            uint32_t chunk = TD[size_t(lo) * 12u + lane];
+            while (tbits) {
+                const uint32_t b = uint32_t(__builtin_ctz(tbits));
+                tbits &= tbits - 1u;
+                const uint32_t rec = tbase + b;
+                uint32_t off = (rec - lo) * 12u;
+                if (off + 12u > 64u) {
+                    lo = rec;
+                    chunk = TD[size_t(lo) * 12u + lane];
+                    off = 0u;
+                }
+                auto rl = [&](uint32_t k) { return __uint_as_float(uint32_t(__builtin_amdgcn_readlane(int(chunk), int(off + k)))); };
+                TriRec r;
+                r.p0 = make_float4(rl(0), rl(1), rl(2), rl(3));
+                r.p1 = make_float4(rl(4), rl(5), rl(6), rl(7));
+                r.p2 = make_float4(rl(8), rl(9), rl(10), rl(11));
+                if (counter) ++cnt[1];
+                if (live && test_tri_rec<kAnyHit>(S, r, R.o, R.d, R.tmin, R.tmax, R.alpha, h)) live = false;  // occluded
+            }
+        }
+#endif
 #if DXRPT_PACKET_PREFETCH
         uint32_t ihits = um & imask;
         if (oct & 1u) ihits = ((ihits & 0x55u) << 1) | ((ihits >> 1) & 0x55u);
