@@ -90,7 +90,7 @@ DEFAULT_PACKET_TRAVERSAL = 3
 DEFAULT_LDS_NODES = 0
 DEFAULT_XCD_MAPPING = 0
 DEFAULT_PACKET_SWITCH = 0
-DEFAULT_MEGAKERNEL_PATHS = 10000000
+DEFAULT_MEGAKERNEL_PATHS = 0xFFFFFFFF
 DEFAULT_MEGAKERNEL_OCCUPANCY = 0
 DEFAULT_BAKE_CHUNK = 1 << 21
 DEFAULT_SPLIT_UNITS = 0

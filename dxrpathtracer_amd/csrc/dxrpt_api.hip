@@ -112,7 +112,7 @@ struct dxrpt_ctx {
     uint32_t opt_shade_occ = 0;     // DXRPT_OPT_SHADE_OCCUPANCY
     uint32_t opt_xcd = 0;           // DXRPT_OPT_XCD_MAPPING
     uint32_t opt_packet_switch = 0; // DXRPT_OPT_PACKET_SWITCH
-    uint32_t opt_mega_paths = 10000000u;    // DXRPT_OPT_MEGAKERNEL_PATHS (path vertices)
+    uint32_t opt_mega_paths = 0xFFFFFFFFu;  // DXRPT_OPT_MEGAKERNEL_PATHS (path vertices; r02: every config)
     uint32_t opt_mega_occ = 0;              // DXRPT_OPT_MEGAKERNEL_OCCUPANCY (0 = by frame size)
     uint32_t opt_bake_chunk = 1u << 21;     // DXRPT_OPT_BAKE_CHUNK (texels per bake launch)
     uint32_t opt_mega_persistent = 0;       // DXRPT_OPT_MEGAKERNEL_PERSISTENT (waves per CU, 0 = off)

@@ -312,11 +312,11 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                          nodes falls below this percentage continues one ray per lane
                                          (0 = never).  Identical results. */
 #define DXRPT_OPT_MEGAKERNEL_PATHS 23u /* frames of at most this many path vertices (paths x (MaxPathLength-1);
-                                            default 10,000,000) run as ONE kernel, one thread per path:
-                                            raygen, every depth's traversals and shading, accumulation -- no
-                                            passes, no queues; larger frames run the wavefront passes (whose
-                                            compaction wins for long paths on big frames).  0 = always the
-                                            wavefront.  Identical results. */
+                                            default 0xFFFFFFFF: every frame) run as ONE kernel, one thread
+                                            per path: raygen, every depth's traversals and shading,
+                                            accumulation -- no passes, no queues; larger frames run the
+                                            wavefront passes (compacted queues between depths).  0 = always
+                                            the wavefront.  Identical results. */
 #define DXRPT_OPT_MEGAKERNEL_OCCUPANCY 24u /* megakernel register budget in waves/SIMD: 0 = by frame size
                                               (default: 5 with path groups, else 7 above 1,500,000 paths,
                                               6 above 600,000, 5 above 300,000, else 4),

@@ -3,7 +3,8 @@
 The other parity tests pin the wavefront schedule (tests/test_gpu_parity.py) and reach the megakernel
 only through bit-identity.  Here every context is fresh and untouched, so each frame runs exactly what
 bench.py times: the megakernel k_path (packet primaries and depth-1 sun shadows, the occupancy picked
-by frame size) up to 10M path vertices, the wavefront above; frame buffers sized for the whole frame.
+by frame size) for every BASELINE config; frame buffers sized for the whole frame.  One test also runs
+the wavefront passes at full size (DXRPT_OPT_MEGAKERNEL_PATHS 0, the only option it sets).
 Each full frame (RaygenShader over DispatchRays(W, H, 1), RayTrace.hlsl:92-149) is compared with the
 oracle on >= 6 crops: the four corners, the last rows, a sky region, the centre, and -- for sizes that
 are not a multiple of 64 paths -- the partial last wave.  Gate: tests/_common.py (1e-4 relative).
@@ -50,11 +51,21 @@ def frame_crops(W, H, extra=()):
 SKY = {"sponza": (992, 0, 160, 24)}
 
 
-def render_shipped(torch, name, W, H, L, sample, prefill=0.0, tiles=None, n_out=None, check_kernel=None):
+def render_shipped(torch, name, W, H, L, sample, prefill=0.0, tiles=None, n_out=None, check_kernel=None,
+                   mega_paths=None):
     sc, sky = scene_bundle(name)
     st = sc.settings(MaxPathLength=L)
     rtc = D.make_constants(sc, st, sky, W, H, sample)
     t = shipped(name)
+    if mega_paths is not None:
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, mega_paths)
+    try:
+        return _render_shipped(torch, t, sc, st, rtc, W, H, prefill, tiles, n_out, check_kernel)
+    finally:
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, A.DEFAULT_MEGAKERNEL_PATHS)
+
+
+def _render_shipped(torch, t, sc, st, rtc, W, H, prefill, tiles, n_out, check_kernel):
     n = W * H if n_out is None else n_out
     init = torch.full((n, 4), prefill, dtype=torch.float32, device="cuda")
     acc = init.clone()
@@ -117,11 +128,18 @@ def test_sponza_720p_L3(torch_cuda):
     compare_crops("sponza", W, H, out, st, rtc, frame_crops(W, H), 0.0, "C2")
 
 
-def test_sponza_1080p_L8_wavefront(torch_cuda):
-    # BASELINE.json configs[2]: 2.07M paths x 7 vertices > 10M -> the default wavefront schedule
+def test_sponza_1080p_L8(torch_cuda):
+    # BASELINE.json configs[2]: 2.07M paths x 7 vertices, the default megakernel schedule
     W, H = 1920, 1080
-    out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 8, 15, 0.125, check_kernel="wavefront")
+    out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 8, 15, 0.125, check_kernel="megakernel")
     compare_crops("sponza", W, H, out, st, rtc, frame_crops(W, H), 0.125, "C3 s15")
+
+
+def test_sponza_1080p_L8_wavefront(torch_cuda):
+    # the same frame through the wavefront passes (compacted queues over 2.07M paths, 7 depths)
+    W, H = 1920, 1080
+    out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 8, 15, 0.125, check_kernel="wavefront", mega_paths=0)
+    compare_crops("sponza", W, H, out, st, rtc, frame_crops(W, H), 0.125, "C3 s15 wavefront")
 
 
 def test_partial_last_wave_frame(torch_cuda):
