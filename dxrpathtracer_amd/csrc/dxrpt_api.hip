@@ -827,10 +827,11 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // (with cost-ordered waves, r02: path groups 5 waves/SIMD, 1/8 share 0.574 -> 0.562 ms; 600k-1.5M
         // paths 6, 720p 1.111 -> 1.095 and the 1/2 share 1.20 -> 1.165 ms; profiles/r02_ab_occ_mid_frames.txt)
         // (r02, late: a GPU's 1/4 share, 518k paths, 4 waves/SIMD instead of 5: slowest rank 0.742 -> 0.729 ms,
-        // profiles/r02_ab_occ_quarter_share.txt)
+        // profiles/r02_ab_occ_quarter_share.txt; 600k-1.5M paths 7 instead of 6: 720p 1.098 -> 1.090, the 1/2
+        // share 1.174 -> 1.164, profiles/r02_ab_occ_mid_frames_head.txt)
         fp.megakernel_occupancy = ctx->opt_mega_occ ? ctx->opt_mega_occ
                                 : lanes < 64u ? 5u
-                                : (paths > 1500000u ? 7u : (paths > 600000u ? 6u : 4u));
+                                : (paths > 600000u ? 7u : 4u);
         fp.mega_persistent = ctx->opt_mega_persistent;
         fp.mega_lanes = lanes;
         fp.num_cus = ctx->num_cus;

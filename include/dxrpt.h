@@ -318,8 +318,8 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                             wavefront passes (compacted queues between depths).  0 = always
                                             the wavefront.  Identical results. */
 #define DXRPT_OPT_MEGAKERNEL_OCCUPANCY 24u /* megakernel register budget in waves/SIMD: 0 = by frame size
-                                              (default: 5 with path groups, else 7 above 1,500,000 paths,
-                                              6 above 600,000, 5 above 300,000, else 4),
+                                              (default: 5 with path groups, else 7 above 600,000 paths,
+                                              else 4),
                                               4 (no spills), 5, 6, 7, 8, or 3 = the compiler's */
 #define DXRPT_OPT_MEGAKERNEL_PERSISTENT 26u /* > 0: the megakernel as a persistent grid of this many
                                                waves per CU pulling 64-path chunks (0 = one wave per
