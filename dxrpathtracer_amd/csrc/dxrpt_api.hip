@@ -120,6 +120,8 @@ struct dxrpt_ctx {
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
     int built_width = 0;
     DevBuf d_trav;   // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
+    uint32_t ctr_set = 0;                 // counter set of the next frame (f_counters holds two)
+    bool ctr_clean[2] = {false, false};   // set known to be zero (zeroed by the previous megakernel frame)
     DevBuf d_wclock;  // 2 x u64 per wave (DXRPT_OPT_WAVE_CLOCKS)
     bool opt_wave_clocks = false;
     uint32_t wclock_waves = 0;
@@ -297,7 +299,10 @@ void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
     c->f_shorg.ensure(qsize * sl * 16);
     c->f_shdir.ensure(qsize * sl * 16);
     c->f_shcon.ensure(qsize * sl * 16);
-    c->f_counters.ensure((2 * kMaxDepthQueues * kQueueShards + 16) * sizeof(uint32_t));  // + the k_path work counter
+    if (!c->f_counters.p) {  // two counter sets (ping-pong across megakernel frames), both dirty at first
+        c->f_counters.ensure(2 * kCounterWords * sizeof(uint32_t));
+        c->ctr_clean[0] = c->ctr_clean[1] = false;
+    }
     f.ps_pix = c->f_pix.as<uint2>();
     f.px_rad = c->f_pxrad.as<float4>();
     f.hit = c->f_hit.as<float4>();
@@ -307,7 +312,7 @@ void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
     f.sh_org = c->f_shorg.as<float4>();
     f.sh_dir = c->f_shdir.as<float4>();
     f.sh_con = c->f_shcon.as<float4>();
-    f.counters = c->f_counters.as<uint32_t>();
+    f.counters = c->f_counters.as<uint32_t>() + c->ctr_set * kCounterWords;
     f.capacity = cap;
     f.cap_r = cap_r;
     f.qsize = uint32_t(qsize);
@@ -909,7 +914,22 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             }
             aux = ctx->aux;
         }
-        HIP_CHECK(launch_frame(sd, ctx->fb, fp, s, ev, aux, aux ? ctx->fork_ev.data() : nullptr));
+        {   // counter sets: this frame's is fb.counters (read by dxrpt_get_stats); a megakernel frame zeroes
+            // the other one in-kernel, so the next frame skips the fill launch
+            uint32_t* base = ctx->f_counters.as<uint32_t>();
+            const uint32_t cur = ctx->ctr_set;
+            ctx->fb.counters = base + cur * kCounterWords;
+            ctx->fb.counters_clean = ctx->ctr_clean[cur];
+            ctx->fb.counters_next = fp.megakernel ? base + (1u - cur) * kCounterWords : nullptr;
+            HIP_CHECK(launch_frame(sd, ctx->fb, fp, s, ev, aux, aux ? ctx->fork_ev.data() : nullptr));
+            ctx->ctr_clean[cur] = false;
+            if (fp.megakernel) {
+                ctx->ctr_clean[1u - cur] = true;
+                ctx->ctr_set = 1u - cur;
+            }
+            ctx->fb.counters_next = nullptr;
+            ctx->fb.counters_clean = false;
+        }
         if (order_waves) {  // the next frame's order from this frame's wave classes (after the frame events)
             uint32_t* h = ctx->d_wave_hist.as<uint32_t>();
             uint32_t* cur = h + ctx->order_parity * 2 * kWaveClasses;
@@ -1082,7 +1102,10 @@ int dxrpt_bake_lightmap(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, co
         b.list = ctx->d_bake_list.as<uint32_t>();
         b.count = b.list + total;  // the entry count lives after the list
         HIP_CHECK(launch_bake_compact(b.pos, total, const_cast<uint32_t*>(b.list), const_cast<uint32_t*>(b.count), s));
-        HIP_CHECK(hipMemsetAsync(ctx->fb.counters, 0, 2 * kMaxDepthQueues * kQueueShards * sizeof(uint32_t), s));
+        ctx->fb.counters = ctx->f_counters.as<uint32_t>() + ctx->ctr_set * kCounterWords;
+        ctx->fb.counters_next = nullptr;
+        HIP_CHECK(hipMemsetAsync(ctx->fb.counters, 0, kCounterWords * sizeof(uint32_t), s));
+        ctx->ctr_clean[ctx->ctr_set] = false;
         // the live count stays on the device (no host sync): launches cover every texel, and chunks
         // past the live count exit at once
         for (uint32_t first = 0; first < total; first += chunk) {

@@ -63,7 +63,11 @@ struct FrameBuffers {
     float4* sh_org = nullptr;
     float4* sh_dir = nullptr;
     float4* sh_con = nullptr;
-    uint32_t* counters = nullptr;  // [queue][shard]: 2 * kMaxDepthQueues * kQueueShards
+    uint32_t* counters = nullptr;  // [queue][shard]: 2 * kMaxDepthQueues * kQueueShards (+ the k_path work counter)
+    // megakernel frames: the other counter set of the ping-pong pair (the next frame's), zeroed by k_path's
+    // workgroup 0 -- so the next frame needs no fill launch (null: nothing to zero)
+    uint32_t* counters_next = nullptr;
+    bool counters_clean = false;   // counters already zero: launch_frame skips its fill
     uint32_t capacity = 0;         // paths
     uint32_t cap_r = 0;            // radiance queue shard capacity (multiple of 64)
     uint32_t qsize = 0;            // kQueueShards * cap_r >= capacity
@@ -163,6 +167,8 @@ struct FrameParams {
 };
 
 constexpr uint32_t kWaveClasses = 256;
+// words of one counter set: the sharded queue counters, the k_path work counter, padding to 16 B
+constexpr uint32_t kCounterWords = 2 * 16 * 64 + 16;
 
 // Kernel sequence of one frame: raygen, then (trace, shade, shadow, resolve) per depth 1..L-1, then
 // accumulate.  With `aux` and 2 * kMaxDepthQueues `fork_ev` events, each depth's any-hit pass runs on

@@ -2493,6 +2493,8 @@ hipError_t launch_wave_order(const uint32_t* cls, const uint32_t* hist, uint32_t
 template <int kOcc, bool kPersistent, bool kLds = false, bool kGroup = false, bool kCount = false, bool kOrder = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
 void k_path(KArgs A) {
+    if (A.F.counters_next && blockIdx.x == 0u)  // the next frame's counter set (this stream's previous frame's)
+        for (uint32_t i = threadIdx.x; i < kCounterWords; i += blockDim.x) A.F.counters_next[i] = 0u;
     lut_fill(A.S);
     extern __shared__ int stack[];
 #if DXRPT_STACK_TID
@@ -2710,7 +2712,8 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
         if (ev && (slot == last_slot || timed(slot))) (void)hipEventRecord(ev[2 * slot + 1], st);
     };
     auto slot_of = [](int d, int kind) { return 1 + 4 * (d - 1) + kind; };  // kind 0 trace 1 shade 2 shadow 3 resolve
-    hipError_t e = hipMemsetAsync(fb.counters, 0, (2 * kMaxDepthQueues * kQueueShards + 1) * sizeof(uint32_t), stream);
+    static_assert(kCounterWords >= 2 * kMaxDepthQueues * kQueueShards + 1 && kCounterWords % 4 == 0, "counter set");
+    hipError_t e = fb.counters_clean ? hipSuccess : hipMemsetAsync(fb.counters, 0, kCounterWords * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     if (fp.megakernel) {  // whole frame in k_path (timing: ev[0], ev[1] bracket the k_path launch)
         // one wave per workgroup: the per-lane stack base is the lane's (DXRPT_STACK_TID, stack_base)
