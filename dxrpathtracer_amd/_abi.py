@@ -82,7 +82,7 @@ KERNEL_NAMES = ("k_raygen", "k_trace", "k_shade", "k_shadow", "k_accumulate", "k
  OPT_LEAF_COST, OPT_SHADOW_OCCUPANCY, OPT_SHADOW_GRID, OPT_CONCURRENCY, OPT_TRAVERSAL_PIPELINE, OPT_PACKET_TRAVERSAL, OPT_LDS_NODES,
  OPT_KERNEL_TIMING_MASK, OPT_XCD_MAPPING, OPT_PACKET_SWITCH, OPT_MEGAKERNEL_PATHS, OPT_MEGAKERNEL_OCCUPANCY,
  OPT_BAKE_CHUNK, OPT_MEGAKERNEL_PERSISTENT, OPT_MEGAKERNEL_LANES, OPT_WAVE_CLOCKS,
- OPT_WAVE_ORDER, OPT_SPLIT_UNITS, OPT_XCD_CHUNK) = range(1, 32)
+ OPT_WAVE_ORDER, OPT_SPLIT_UNITS, OPT_XCD_CHUNK, OPT_WAVE_ORDER_PERIOD) = range(1, 33)
 # context defaults of the traversal options (dxrpt_api.hip)
 DEFAULT_TRAVERSAL_PIPELINE = 0
 POST_FLOAT4, POST_RGBA8 = 0, 1  # dxrpt_post_process output formats
@@ -95,6 +95,7 @@ DEFAULT_MEGAKERNEL_OCCUPANCY = 0
 DEFAULT_BAKE_CHUNK = 1 << 21
 DEFAULT_SPLIT_UNITS = 0
 DEFAULT_XCD_CHUNK = 8
+DEFAULT_WAVE_ORDER_PERIOD = 16
 DEFAULT_MEGAKERNEL_PERSISTENT = 0
 DEFAULT_MEGAKERNEL_LANES = 0  # by frame size
 DEFAULT_WAVE_ORDER = 2  # by frame size

@@ -133,6 +133,8 @@ struct dxrpt_ctx {
     uint32_t order_parity = 0;
     uint64_t order_key = 0;     // (waves, lanes, tiles generation) the order was built for
     bool order_ready = false;   // d_wave_order holds an order for order_key
+    uint32_t order_frame = 0;   // ordered frames since the order (re)started
+    uint32_t opt_order_period = 16;  // DXRPT_OPT_WAVE_ORDER_PERIOD (r02: 1/8 share 0.549 -> 0.534 ms)
     uint64_t tiles_gen = 0;     // bumped whenever the tile list changes
     DevBuf d_spill;  // BVH8 traversal stack entries beyond the LDS part (deep trees only)
     DevBuf d_bake_list;  // live lightmap texels of the last bake pass + their count
@@ -511,6 +513,9 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_XCD_CHUNK) {
             require(value <= 4096, "dxrpt_set_option: XCD chunk must be 0..4096 blocks");
             ctx->opt_xcd_chunk = uint32_t(value);
+        } else if (option == DXRPT_OPT_WAVE_ORDER_PERIOD) {
+            require(value >= 1 && value <= 1024, "dxrpt_set_option: wave order period must be 1..1024 frames");
+            ctx->opt_order_period = uint32_t(value);
         } else if (option == DXRPT_OPT_SPLIT_UNITS) {
             require(value <= 1000, "dxrpt_set_option: split units must be 0..1000 (per mille of the waves)");
             ctx->opt_split_permille = uint32_t(value);
@@ -857,6 +862,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // rounds) keeps path order, where concurrent neighbouring blocks share more cache than the
         // shorter tail saves (profiles/r02_ab_wave_order.txt).
         uint32_t order_waves = 0;
+        bool order_pass = false;
         const uint32_t waves = lanes < 64u ? (paths + lanes - 1u) / lanes : (paths + 63u) / 64u;
         const uint64_t slots = uint64_t(ctx->num_cus) * 4u * fp.megakernel_occupancy;
         const bool order_on = ctx->opt_wave_order == 1 || (ctx->opt_wave_order == 2 && waves <= 3u * slots);
@@ -871,10 +877,15 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
                 ctx->order_key = key;
                 ctx->order_ready = false;
                 ctx->order_parity = 0;
+                ctx->order_frame = 0;
                 HIP_CHECK(hipMemsetAsync(ctx->d_wave_hist.p, 0, 4 * kWaveClasses * sizeof(uint32_t), static_cast<hipStream_t>(stream)));
             }
-            fp.wave_cost = ctx->d_wave_cost.as<uint32_t>();
-            fp.wave_hist = ctx->d_wave_hist.as<uint32_t>() + ctx->order_parity * 2 * kWaveClasses;
+            // every opt_order_period-th ordered frame records its wave classes and rebuilds the order
+            // (progressive frames cost alike); the frames between reuse it -- no recording atomics, no
+            // order pass
+            order_pass = ctx->opt_wave_clocks || ctx->order_frame % ctx->opt_order_period == 0u;
+            fp.wave_cost = order_pass ? ctx->d_wave_cost.as<uint32_t>() : nullptr;
+            fp.wave_hist = order_pass ? ctx->d_wave_hist.as<uint32_t>() + ctx->order_parity * 2 * kWaveClasses : nullptr;
             fp.wave_order = ctx->order_ready ? ctx->d_wave_order.as<uint32_t>() : nullptr;
             // the costliest slots of the order split in two (path groups, once an order exists)
             if (lanes < 64u && ctx->order_ready && ctx->opt_split_permille)
@@ -930,7 +941,8 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             ctx->fb.counters_next = nullptr;
             ctx->fb.counters_clean = false;
         }
-        if (order_waves) {  // the next frame's order from this frame's wave classes (after the frame events)
+        if (order_waves) ++ctx->order_frame;
+        if (order_waves && order_pass) {  // the next frames' order from this frame's wave classes (after the frame events)
             uint32_t* h = ctx->d_wave_hist.as<uint32_t>();
             uint32_t* cur = h + ctx->order_parity * 2 * kWaveClasses;
             uint32_t* nxt = h + (1u - ctx->order_parity) * 2 * kWaveClasses;

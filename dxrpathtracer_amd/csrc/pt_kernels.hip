@@ -2749,7 +2749,7 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
             else if (fp.megakernel_occupancy == 5) hipLaunchKernelGGL((k_path<5, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
             else hipLaunchKernelGGL((k_path<4, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
         }
-        else if (fp.wave_cost && fp.megakernel_occupancy >= 4 && fp.megakernel_occupancy <= 7) {  // cost-ordered waves
+        else if ((fp.wave_cost || fp.wave_order) && fp.megakernel_occupancy >= 4 && fp.megakernel_occupancy <= 7) {  // cost-ordered waves
             if (fp.megakernel_occupancy == 7) hipLaunchKernelGGL((k_path<7, false, false, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
             else if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_path<6, false, false, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
             else if (fp.megakernel_occupancy == 5) hipLaunchKernelGGL((k_path<5, false, false, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);

@@ -355,6 +355,10 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                         this many consecutive 8x8 pixel blocks, runs dealt to the 8 XCDs
                                         in rotation (default 8; 0: block i on workgroup i, i.e.
                                         neighbouring blocks on different XCDs).  Identical results. */
+#define DXRPT_OPT_WAVE_ORDER_PERIOD 32u /* cost-ordered frames: every this-many-th frame records its waves'
+                                           durations and rebuilds the order, the frames between reuse it
+                                           (default 16, one SqrtNumSamples^2 = 16 cycle of progressive
+                                           frames; 1 = every frame).  Identical results. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

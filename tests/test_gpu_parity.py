@@ -595,9 +595,10 @@ def test_wave_order_is_bit_identical(torch_cuda, name, lanes, W, H):
     try:
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30)
         t.set_option(A.OPT_MEGAKERNEL_LANES, lanes)
-        for order, split in ((0, 0), (1, 0)) + (((1, 50), (1, 1000)) if lanes < 64 else ()):
+        for order, split, period in ((0, 0, 1), (1, 0, 1), (1, 0, 2)) + (((1, 50, 1), (1, 1000, 3)) if lanes < 64 else ()):
             t.set_option(A.OPT_WAVE_ORDER, order)
             t.set_option(A.OPT_SPLIT_UNITS, split)
+            t.set_option(A.OPT_WAVE_ORDER_PERIOD, period)
             acc = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
             share = torch.zeros((lay.counts[1], 4), dtype=torch.float32, device="cuda")
             frames = []
@@ -619,6 +620,7 @@ def test_wave_order_is_bit_identical(torch_cuda, name, lanes, W, H):
         t.set_option(A.OPT_MEGAKERNEL_LANES, A.DEFAULT_MEGAKERNEL_LANES)
         t.set_option(A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)
         t.set_option(A.OPT_SPLIT_UNITS, A.DEFAULT_SPLIT_UNITS)
+        t.set_option(A.OPT_WAVE_ORDER_PERIOD, A.DEFAULT_WAVE_ORDER_PERIOD)
 
 
 @pytest.mark.parametrize("name,W,H", [("sponza", 352, 200), ("suntemple", 100, 50)])
