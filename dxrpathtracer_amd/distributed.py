@@ -114,10 +114,10 @@ def gather_frame(local, layout: BandLayout, rank: int, full=None, src_index=None
         if full is not None:
             full.copy_(local[: layout.width * layout.height])
         return full
-    gather_list = [torch.empty_like(local) for _ in range(layout.world)] if rank == 0 else None
-    dist.gather(local, gather_list, dst=0, group=group)
+    # rank 0 receives the slabs straight into one (world * max_count, 4) buffer (contiguous row blocks)
+    allbuf = torch.empty((layout.world * local.shape[0], 4), dtype=local.dtype, device=local.device) if rank == 0 else None
+    dist.gather(local, list(allbuf.chunk(layout.world)) if rank == 0 else None, dst=0, group=group)
     if rank == 0:
-        allbuf = torch.cat(gather_list, dim=0)
         torch.index_select(allbuf, 0, src_index, out=full)
     return full
 
@@ -149,13 +149,15 @@ class PipelinedGather:
             return
         if self.staging is None:
             self.staging = [torch.empty_like(local) for _ in range(2)]
-            if self.rank == 0:
-                self.recv = [[torch.empty_like(local) for _ in range(self.layout.world)] for _ in range(2)]
+            if self.rank == 0:  # each frame's slabs land in one contiguous buffer: no concatenation copy
+                w = self.layout.world
+                self.recv = [torch.empty((w * local.shape[0], 4), dtype=local.dtype, device=local.device)
+                             for _ in range(2)]
         k = self.count % 2
         self.count += 1
         self.staging[k].copy_(local)
-        work = dist.gather(self.staging[k], self.recv[k] if self.rank == 0 else None, dst=0, group=self.group,
-                           async_op=True)
+        work = dist.gather(self.staging[k], list(self.recv[k].chunk(self.layout.world)) if self.rank == 0 else None,
+                           dst=0, group=self.group, async_op=True)
         prev, self.pending = self.pending, (work, k)
         if prev is not None:
             self._finish(prev)
@@ -170,4 +172,4 @@ class PipelinedGather:
         work, k = pend
         work.wait()
         if self.rank == 0:
-            torch.index_select(torch.cat(self.recv[k], dim=0), 0, self.src_index, out=self.full)
+            torch.index_select(self.recv[k], 0, self.src_index, out=self.full)
