@@ -792,6 +792,10 @@ constexpr uint32_t kSwitchMinVisits = 4;
 #ifndef DXRPT_PACKET_VCHUNK
 #define DXRPT_PACKET_VCHUNK 0
 #endif
+// DXRPT_TRAV_PRIO: wave priority (s_setprio) while a wave runs a per-lane traversal (0: off).
+#ifndef DXRPT_TRAV_PRIO
+#define DXRPT_TRAV_PRIO 0
+#endif
 // DXRPT_ORDER_XCD: cost-ordered frames also deal runs of xcd_chunk consecutive order positions to the XCDs.
 #ifndef DXRPT_ORDER_XCD
 #define DXRPT_ORDER_XCD 0
@@ -1033,8 +1037,14 @@ PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
     uint32_t node = 0;
     int sp = 0;
     uint2 tos = make_uint2(0u, 0u);
+#if DXRPT_TRAV_PRIO
+    __builtin_amdgcn_s_setprio(DXRPT_TRAV_PRIO);  // traversing waves issue their next fetch first
+#endif
     while (!trav8_step<kAnyHit, kCount>(S, R, node, sp, stk, tos, h, nvisit, ntest, nc)) {
     }
+#if DXRPT_TRAV_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     return h.tri != kMiss;
 }
 
