@@ -82,7 +82,8 @@ KERNEL_NAMES = ("k_raygen", "k_trace", "k_shade", "k_shadow", "k_accumulate", "k
  OPT_LEAF_COST, OPT_SHADOW_OCCUPANCY, OPT_SHADOW_GRID, OPT_CONCURRENCY, OPT_TRAVERSAL_PIPELINE, OPT_PACKET_TRAVERSAL, OPT_LDS_NODES,
  OPT_KERNEL_TIMING_MASK, OPT_XCD_MAPPING, OPT_PACKET_SWITCH, OPT_MEGAKERNEL_PATHS, OPT_MEGAKERNEL_OCCUPANCY,
  OPT_BAKE_CHUNK, OPT_MEGAKERNEL_PERSISTENT, OPT_MEGAKERNEL_LANES, OPT_WAVE_CLOCKS,
- OPT_WAVE_ORDER, OPT_SPLIT_UNITS, OPT_XCD_CHUNK, OPT_WAVE_ORDER_PERIOD) = range(1, 33)
+ OPT_WAVE_ORDER, OPT_SPLIT_UNITS, OPT_XCD_CHUNK, OPT_WAVE_ORDER_PERIOD, OPT_MEGAKERNEL_SPLIT,
+ OPT_TAIL_OCCUPANCY) = range(1, 35)
 # context defaults of the traversal options (dxrpt_api.hip)
 DEFAULT_TRAVERSAL_PIPELINE = 0
 POST_FLOAT4, POST_RGBA8 = 0, 1  # dxrpt_post_process output formats
@@ -99,6 +100,8 @@ DEFAULT_WAVE_ORDER_PERIOD = 16
 DEFAULT_MEGAKERNEL_PERSISTENT = 0
 DEFAULT_MEGAKERNEL_LANES = 0  # by frame size
 DEFAULT_WAVE_ORDER = 2  # by frame size
+DEFAULT_MEGAKERNEL_SPLIT = 0
+DEFAULT_TAIL_OCCUPANCY = 0
 
 
 class Stats(C.Structure):
@@ -108,7 +111,12 @@ class Stats(C.Structure):
                 ("node_visits_radiance", C.c_uint64), ("tri_tests_radiance", C.c_uint64),
                 ("node_visits_shadow", C.c_uint64), ("tri_tests_shadow", C.c_uint64),
                 ("kernel_ms", C.c_double * K_COUNT), ("kernel_launches", C.c_uint64 * K_COUNT),
-                ("timed_frames", C.c_uint64), ("frame_ms", C.c_double)]
+                ("timed_frames", C.c_uint64), ("frame_ms", C.c_double), ("schedule", u32), ("paths_per_wave", u32),
+                ("occupancy", u32), ("pad", u32)]
+
+
+# dxrpt_stats.schedule bits
+SCHED_MEGAKERNEL, SCHED_PATH_GROUPS, SCHED_ORDER_KERNEL, SCHED_COST_ORDERED, SCHED_CENSUS, SCHED_SPLIT = 1, 2, 4, 8, 16, 32
 
 
 class BvhInfo(C.Structure):

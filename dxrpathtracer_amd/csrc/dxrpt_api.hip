@@ -117,6 +117,8 @@ struct dxrpt_ctx {
     uint32_t opt_bake_chunk = 1u << 21;     // DXRPT_OPT_BAKE_CHUNK (texels per bake launch)
     uint32_t opt_mega_persistent = 0;       // DXRPT_OPT_MEGAKERNEL_PERSISTENT (waves per CU, 0 = off)
     uint32_t opt_mega_lanes = 0;            // DXRPT_OPT_MEGAKERNEL_LANES (paths per megakernel wave, 0 = by size)
+    uint32_t opt_split = 0;                 // DXRPT_OPT_MEGAKERNEL_SPLIT (0 off, 1 on, 2 by frame size)
+    uint32_t opt_tail_occ = 0;              // DXRPT_OPT_TAIL_OCCUPANCY (0 = the head's budget)
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
     int built_width = 0;
     DevBuf d_trav;   // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
@@ -534,6 +536,12 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_BAKE_CHUNK) {
             require(value >= 64 && value <= (1u << 26), "dxrpt_set_option: bake chunk must be 64..2^26 texels");
             ctx->opt_bake_chunk = uint32_t(value);
+        } else if (option == DXRPT_OPT_MEGAKERNEL_SPLIT) {
+            require(value <= 2, "dxrpt_set_option: megakernel split must be 0 (off), 1 (on) or 2 (by frame size)");
+            ctx->opt_split = uint32_t(value);
+        } else if (option == DXRPT_OPT_TAIL_OCCUPANCY) {
+            require(value == 0 || (value >= 4 && value <= 8), "dxrpt_set_option: tail occupancy must be 0 (by frame) or 4..8");
+            ctx->opt_tail_occ = uint32_t(value);
         } else if (option == DXRPT_OPT_BVH_WIDTH) {
             require(value == 2 || value == 8, "dxrpt_set_option: BVH width must be 2 or 8");
             ctx->opt_width = int(value);  // takes effect at the next dxrpt_build_bvh
@@ -844,13 +852,16 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
                                 : (paths > 600000u ? 7u : 4u);
         fp.mega_persistent = ctx->opt_mega_persistent;
         fp.mega_lanes = lanes;
+        // depth-split schedule (k_path_head + compacting k_path_tail): 64-lane path-ordered frames only
+        fp.split = ctx->opt_split == 1u ? 1u : 0u;
+        fp.tail_occupancy = ctx->opt_tail_occ ? ctx->opt_tail_occ : fp.megakernel_occupancy;
         fp.num_cus = ctx->num_cus;
         hipStream_t s = static_cast<hipStream_t>(stream);
+        ctx->wclock_waves = 0;  // set again below only by a frame that records stamps
         if (ctx->opt_count) {
             fp.trav = ctx->d_trav.as<unsigned long long>();
             HIP_CHECK(hipMemsetAsync(fp.trav, 0, 4 * sizeof(unsigned long long), s));
-            ctx->wclock_waves = 0;
-            if (ctx->opt_wave_clocks && fp.megakernel) {
+            if (ctx->opt_wave_clocks && fp.megakernel) {  // census: the 64-lane kernel, one slot per 64 paths
                 ctx->wclock_waves = (paths + 63u) / 64u;
                 ctx->d_wclock.ensure(size_t(ctx->wclock_waves) * 2 * sizeof(unsigned long long));
                 fp.wave_clock = ctx->d_wclock.as<unsigned long long>();
@@ -925,6 +936,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             }
             aux = ctx->aux;
         }
+        uint32_t sched = 0;
         {   // counter sets: this frame's is fb.counters (read by dxrpt_get_stats); a megakernel frame zeroes
             // the other one in-kernel, so the next frame skips the fill launch
             uint32_t* base = ctx->f_counters.as<uint32_t>();
@@ -932,7 +944,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             ctx->fb.counters = base + cur * kCounterWords;
             ctx->fb.counters_clean = ctx->ctr_clean[cur];
             ctx->fb.counters_next = fp.megakernel ? base + (1u - cur) * kCounterWords : nullptr;
-            HIP_CHECK(launch_frame(sd, ctx->fb, fp, s, ev, aux, aux ? ctx->fork_ev.data() : nullptr));
+            HIP_CHECK(launch_frame(sd, ctx->fb, fp, s, ev, aux, aux ? ctx->fork_ev.data() : nullptr, &sched));
             ctx->ctr_clean[cur] = false;
             if (fp.megakernel) {
                 ctx->ctr_clean[1u - cur] = true;
@@ -956,6 +968,9 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         std::memset(&ctx->last, 0, sizeof(ctx->last));
         ctx->last.pixels = paths;
         ctx->last.nominal_rays = uint64_t(paths) * uint64_t(1 + (ctx->last_L - 1) * 2);
+        ctx->last.schedule = sched;
+        ctx->last.paths_per_wave = fp.megakernel ? ((sched & DXRPT_SCHED_PATH_GROUPS) ? lanes : 64u) : 0u;
+        ctx->last.occupancy = fp.megakernel ? fp.megakernel_occupancy : 0u;
         ctx->rendered = true;
     });
 }

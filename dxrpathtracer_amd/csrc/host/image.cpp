@@ -319,7 +319,9 @@ bool load_jpeg_mem(const std::vector<uint8_t>& d, const std::string& path, Textu
         const uint32_t n = len - 2;
         if (m == 0xDB) {  // DQT
             for (uint32_t q = 0; q < n;) {
-                const uint32_t pq = s[q] >> 4, tq = s[q] & 3u;
+                const uint32_t pq = s[q] >> 4, tq = s[q] & 15u;
+                if (pq > 1 || tq > 3) return fail("bad quantisation table id / precision");
+                if (q + 1 + 64 * (pq + 1) > n) return fail("truncated quantisation table");
                 ++q;
                 for (int k = 0; k < 64; ++k) {
                     qt[tq][kZigzag[k]] = pq ? be16(s + q + 2 * k) : s[q + k];
@@ -328,7 +330,8 @@ bool load_jpeg_mem(const std::vector<uint8_t>& d, const std::string& path, Textu
             }
         } else if (m == 0xC4) {  // DHT
             for (uint32_t q = 0; q + 17 <= n;) {
-                const uint32_t tc = s[q] >> 4, th = s[q] & 3u;
+                const uint32_t tc = s[q] >> 4, th = s[q] & 15u;
+                if (tc > 1 || th > 3) return fail("bad Huffman table class / id");
                 Huffman& H = tc ? hac[th] : hdc[th];
                 uint32_t total = 0;
                 for (int L = 1; L <= 16; ++L) total += s[q + L];
@@ -348,20 +351,24 @@ bool load_jpeg_mem(const std::vector<uint8_t>& d, const std::string& path, Textu
                 q += 17 + total;
             }
         } else if (m == 0xDD) {  // DRI
+            if (n < 2) return fail("truncated restart interval");
             restart = be16(s);
         } else if (m == 0xC0 || m == 0xC1) {  // SOF0 / SOF1
+            if (n < 6) return fail("truncated frame header");
             if (s[0] != 8) return fail("only 8-bit JPEG samples are supported");
             height = be16(s + 1);
             width = be16(s + 3);
             const uint32_t nc = s[5];
             if ((nc != 1 && nc != 3) || width == 0 || height == 0 || width > 16384 || height > 16384)
                 return fail("unsupported JPEG frame (components / size)");
+            if (n < 6 + 3 * nc) return fail("truncated frame header");
             comps.resize(nc);
             for (uint32_t c = 0; c < nc; ++c) {
                 comps[c].id = s[6 + 3 * c];
                 comps[c].h = s[7 + 3 * c] >> 4;
                 comps[c].v = s[7 + 3 * c] & 15u;
-                comps[c].tq = s[8 + 3 * c] & 3u;
+                comps[c].tq = s[8 + 3 * c];
+                if (comps[c].tq > 3) return fail("bad quantisation table id");
                 if (comps[c].h < 1 || comps[c].h > 4 || comps[c].v < 1 || comps[c].v > 4) return fail("bad sampling factors");
             }
             frame = true;
@@ -369,14 +376,17 @@ bool load_jpeg_mem(const std::vector<uint8_t>& d, const std::string& path, Textu
             return fail("progressive / lossless / arithmetic JPEG is not supported");
         } else if (m == 0xDA) {  // SOS: one interleaved scan with every component (baseline)
             if (!frame) return fail("scan before frame header");
+            if (n < 1) return fail("truncated scan header");
             const uint32_t ns = s[0];
             if (ns != comps.size()) return fail("non-interleaved sequential scans are not supported");
+            if (n < 1 + 2 * ns + 3) return fail("truncated scan header");
             for (uint32_t k = 0; k < ns; ++k) {
                 const uint32_t cid = s[1 + 2 * k];
                 auto it = std::find_if(comps.begin(), comps.end(), [&](const Component& c) { return c.id == cid; });
                 if (it == comps.end()) return fail("scan names an unknown component");
                 it->td = s[2 + 2 * k] >> 4;
-                it->ta = s[2 + 2 * k] & 3u;
+                it->ta = s[2 + 2 * k] & 15u;
+                if (it->td > 3 || it->ta > 3) return fail("bad Huffman table id in scan");
                 if (!hdc[it->td].defined || !hac[it->ta].defined) return fail("scan uses an undefined Huffman table");
             }
             uint32_t hmax = 1, vmax = 1;

@@ -164,6 +164,11 @@ struct FrameParams {
     // kernel maps it to pixel block (8 t + (i mod 8 + t) mod 8) C + (i / 8) mod C, t = (i / 8) / C: each
     // XCD (own L2) takes runs of C consecutive 8x8 blocks, runs dealt to the XCDs in rotation.  0: block i.
     uint32_t xcd_chunk;
+    // Depth-split megakernel (DXRPT_OPT_MEGAKERNEL_SPLIT; 64-lane path-ordered frames): 1 = k_path_head
+    // (depth 1) then one compacting k_path_tail per further depth; 0 = the single k_path.
+    // tail_occupancy: the tails' register budget (waves/SIMD).
+    uint32_t split;
+    uint32_t tail_occupancy;
 };
 
 constexpr uint32_t kWaveClasses = 256;
@@ -183,8 +188,10 @@ inline int frame_event_count(int L) { return 2 * (2 + 4 * (L - 1)); }
 hipError_t launch_wave_order(const uint32_t* cls, const uint32_t* hist, uint32_t* cursor, uint32_t* hist_next,
                              uint32_t* cursor_next, uint32_t* order, uint32_t n, hipStream_t stream);
 
+// *sched_out (if non-null) receives the DXRPT_SCHED_* bits of the schedule launched.
 hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream,
-                        hipEvent_t* ev, hipStream_t aux = nullptr, hipEvent_t* fork_ev = nullptr);
+                        hipEvent_t* ev, hipStream_t aux = nullptr, hipEvent_t* fork_ev = nullptr,
+                        uint32_t* sched_out = nullptr);
 
 // Lightmap baking (BakeRayGen) over a width x height lightmap.  launch_bake_compact lists the texels
 // inside a UV island (pos.w != 0; the others are skipped by BakeRayGen) into list[0, *count), so the

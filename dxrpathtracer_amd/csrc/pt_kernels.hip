@@ -2543,7 +2543,7 @@ void k_path(KArgs A) {
             const unsigned long long t0 = A.P.wave_clock ? __builtin_amdgcn_s_memrealtime() : 0ull;
             uint32_t cnt[4] = {0u, 0u, 0u, 0u};
             if (p < A.P.num_paths) camera_path<true>(A, p, stk, NodeCache{nullptr, 0u}, cnt);
-            if (A.P.wave_clock && (threadIdx.x & 63u) == 0u) {  // vector stores from lane 0 of the wave
+            if (A.P.wave_clock && (threadIdx.x & 63u) == 0u && p < A.P.num_paths) {  // vector stores from lane 0
                 const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
                 A.P.wave_clock[2 * (p >> 6)] = t0;
                 A.P.wave_clock[2 * (p >> 6) + 1] = t1;
@@ -2583,6 +2583,173 @@ void k_path(KArgs A) {
         if (base >= A.P.num_paths) break;  // uniform: every wave reaches it once the counter passes the frame
         if (base + lane < A.P.num_paths) camera_path(A, base + lane, stk);
     }
+}
+
+// ---- depth-split megakernel (FrameParams::split) ---------------------------------------------
+// The frame as one megakernel launch per path depth: k_path_head runs every camera path from raygen
+// through its first vertex (packet primaries and depth-1 sun shadows: the coherent part); k_path_tail(d)
+// runs depth d of the paths still alive.  Between depths the surviving paths are compacted -- wave64
+// ballot + popcount, one atomic per wave on a sharded counter -- into a queue whose entries carry the
+// whole path state, so every tail wave is full of live paths (the single k_path keeps a lane per path
+// for all L - 1 depths, idle once its path ended), and the path state lives in the queue rather than in
+// registers across the traversals: a tail keeps only the queue position and the ray across its
+// closest-hit traversal and re-reads the rest afterwards, and every kernel queues the continuation
+// BEFORE tracing the vertex's shadow rays, so only the radiance sum is live across them.  Each kernel
+// has its own register budget (FrameParams::megakernel_occupancy / tail_occupancy).  A path's radiance
+// is k_path's sum, continued term by term from the queued partial sum, so frames are bit-identical.
+// Queue of depth d (RayQueue q[d & 1], counters d, shard = producer wave mod kQueueShards):
+//   org (origin xyz, FP32Max)   dir (direction xyz, bits(accumulation index))
+//   thr (throughput rgb, payload Roughness)   rad (radiance so far, bits(payload IsDiffuse))   pix (CMJ pattern)
+// The queued count of depth d is that depth's radiance-ray count (dxrpt_get_stats).
+
+// A vertex's shadow rays (ShadowHit/Miss/AnyHit, RayTrace.hlsl:497-507, 532-542) walked slot by slot by
+// the wave, contribution * visibility added to rad in slot order -- trace_path's walk (the depth-1 sun
+// rays of a full wave through the packet traversal, packet bit 1).
+PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh, bool sun0, uint32_t packet,
+                           float4& rad) {
+    uint32_t nv = 0, nt = 0;
+    for (uint32_t k = 0; __ballot(k < nsh) != 0ull; ++k) {
+        const bool live = k < nsh;
+        const size_t slot = size_t(k) * A.F.qsize + slot_p;
+        float4 o4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d4 = make_float4(0.0f, 0.0f, 1.0f, 0.0f), c4 = o4;
+        if (live) {
+            o4 = A.F.sh_org[slot];
+            d4 = A.F.sh_dir[slot];
+            c4 = A.F.sh_con[slot];
+        }
+        HitRec hs;
+        bool occluded = false;
+        const bool pk = d == 1 && k == 0 && (packet & 2u);
+        if (pk)
+            occluded = traverse8_packet<true, false>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live && sun0, hs);
+        if (live && !(pk && sun0))
+            occluded = traverse<8, true, false>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, nullptr, hs, nv, nt);
+        if (live) {
+            rad.x += occluded ? c4.x * 0.0f : c4.x;
+            rad.y += occluded ? c4.y * 0.0f : c4.y;
+            rad.z += occluded ? c4.z * 0.0f : c4.z;
+        }
+    }
+}
+
+// Queues the continuation of a vertex (all active lanes must call; `cont` selects) into queue d + 1;
+// returns its position.  The radiance word is written later (split_finish), after the shadow rays.
+PT_DEV uint32_t split_push(const KArgs& A, int d, bool cont, const VertexOut& O, uint32_t pix, uint32_t accumIdx) {
+    const uint32_t shard = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) % kQueueShards;
+    const uint32_t pos = queue_append(A.F.counters + uint32_t(d + 1) * kQueueShards, A.F.cap_r, cont, shard);
+    if (cont) {
+        const RayQueue& Q = A.F.q[(d + 1) & 1];
+        Q.org[pos] = make_float4(O.nextOrigin.x, O.nextOrigin.y, O.nextOrigin.z, kFP32Max);
+        Q.dir[pos] = make_float4(O.nextDir.x, O.nextDir.y, O.nextDir.z, bitsf(accumIdx));
+        Q.thr[pos] = make_float4(O.nextThr.x, O.nextThr.y, O.nextThr.z, O.nextRoughness);
+        Q.pix[pos] = pix;
+    }
+    return pos;
+}
+
+// The vertex's radiance sum: into its queued continuation, or the pixel if the path ended here.
+PT_DEV void split_finish(const KArgs& A, int d, bool cont, uint32_t qpos, bool nextDiffuse, uint32_t accumIdx,
+                         const float4& rad) {
+    if (cont)
+        A.F.q[(d + 1) & 1].rad[qpos] = make_float4(rad.x, rad.y, rad.z, bitsf(nextDiffuse ? 1u : 0u));
+    else
+        accumulate_pixel(A, accumIdx, rad);
+}
+
+// Raygen + depth 1 of every camera path (one 64-path 8x8 block per wave, XCD runs as k_path).
+template <int kOcc>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
+void k_path_head(KArgs A) {
+    if (A.F.counters_next && blockIdx.x == 0u)  // the next frame's counter set (see k_path)
+        for (uint32_t i = threadIdx.x; i < kCounterWords; i += blockDim.x) A.F.counters_next[i] = 0u;
+    lut_fill(A.S);
+    const uint32_t p = (A.P.xcd_chunk ? xcd_position(blockIdx.x, gridDim.x, A.P.xcd_chunk) : blockIdx.x) * blockDim.x +
+                       threadIdx.x;
+    if (p >= A.P.num_paths) return;
+    const dxrpt_app_settings& set = A.P.set;
+    const PrimaryRay pr = primary_ray(A, p);
+    const uint32_t packet = (p | 63u) < A.P.num_paths ? A.P.packet : 0u;
+    count_rays(A.F.counters + 1u * kQueueShards, 1u);
+    HitRec h;
+    uint32_t nv = 0, nt = 0;
+    if (packet & 1u)  // coherent primary rays: wave-coherent traversal (same results)
+        traverse8_packet<false, false>(A.S, pr.start, pr.dir, 0.0f, pr.length, 1 <= set.MaxAnyHitPathLength, true, h);
+    else
+        traverse<8, false, false>(A.S, pr.start, pr.dir, 0.0f, pr.length, 1 <= set.MaxAnyHitPathLength, nullptr, h, nv, nt);
+    VertexIn V;
+    V.inOrigin = pr.start;
+    V.inDir = pr.dir;
+    V.pathThr = f3{1.0f, 1.0f, 1.0f};
+    V.payloadRoughness = 0.0f;
+    V.payloadIsDiffuse = false;
+    V.pix = pr.pixelIdx;
+    V.hit = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
+    VertexOut O;
+    uint32_t nsh = 0;
+    bool sun0 = false;
+    path_vertex(A, 1, V, [&](int kind, f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
+        sun0 |= kind == kShadowSun || !DXRPT_SUN0_CHECK;
+        emit_shadow(A, p, nsh, o, dd, tmn, tmx, c, fo);
+    }, O);
+    count_rays(A.F.counters + (kMaxDepthQueues + 1u) * kQueueShards, nsh);
+    const bool cont = O.cont;
+    const bool nextDiffuse = O.nextIsDiffuse;
+    const uint32_t qpos = split_push(A, 1, cont, O, pr.pixelIdx, pr.accumIdx);
+    float4 rad = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    rad.x += 1.0f * O.local.x;
+    rad.y += 1.0f * O.local.y;
+    rad.z += 1.0f * O.local.z;
+    vertex_shadows(A, 1, p, nsh, sun0, packet, rad);
+    split_finish(A, 1, cont, qpos, nextDiffuse, pr.accumIdx, rad);
+}
+
+// Depth d of the paths queued for it (one per lane); waves past the queued count exit at once (the grid
+// covers every path of the frame).
+template <int kOcc>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0 ? kOcc : 1)))
+void k_path_tail(KArgs A, int d) {
+    const uint32_t* cnt = A.F.counters + uint32_t(d) * kQueueShards;
+    const uint32_t n = queue_total(cnt);
+    if (blockIdx.x * blockDim.x >= n) return;  // the whole workgroup (one wave) is past the queue
+    lut_fill(A.S);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const dxrpt_app_settings& set = A.P.set;
+    const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
+    const RayQueue& Q = A.F.q[d & 1];
+    HitRec h;
+    {
+        const float4 o4 = Q.org[pos], d4 = Q.dir[pos];
+        uint32_t nv = 0, nt = 0;
+        traverse<8, false, false>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= set.MaxAnyHitPathLength, nullptr, h, nv, nt);
+    }
+    // the rest of the path state comes back from the queue after the traversal
+    const float4 o4 = Q.org[pos], d4 = Q.dir[pos], t4 = Q.thr[pos], r4 = Q.rad[pos];
+    const uint32_t accumIdx = fbits(d4.w);
+    VertexIn V;
+    V.inOrigin = ld3(o4);
+    V.inDir = ld3(d4);
+    V.pathThr = ld3(t4);
+    V.payloadRoughness = t4.w;
+    V.payloadIsDiffuse = (fbits(r4.w) & 1u) != 0u;
+    V.pix = Q.pix[pos];
+    V.hit = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
+    VertexOut O;
+    uint32_t nsh = 0;
+    path_vertex(A, d, V, [&](int, f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
+        emit_shadow(A, pos, nsh, o, dd, tmn, tmx, c, fo);
+    }, O);
+    count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, nsh);
+    const bool cont = O.cont;
+    const bool nextDiffuse = O.nextIsDiffuse;
+    const int L = set.MaxPathLength < 2 ? 2 : set.MaxPathLength;
+    const uint32_t qpos = d + 1 <= L - 1 ? split_push(A, d, cont, O, V.pix, accumIdx) : 0u;
+    float4 rad = make_float4(r4.x, r4.y, r4.z, 0.0f);
+    rad.x += V.pathThr.x * O.local.x;
+    rad.y += V.pathThr.y * O.local.y;
+    rad.z += V.pathThr.z * O.local.z;
+    vertex_shadows(A, d, pos, nsh, false, 0u, rad);
+    split_finish(A, d, cont, qpos, nextDiffuse, accumIdx, rad);
 }
 
 // ---- lightmap baking (Baking.hlsl:336-465, BakeRayGen) -------------------------------------------
@@ -2698,9 +2865,43 @@ uint32_t frame_traversal_threads(uint32_t num_paths, uint32_t shadow_slots, uint
 
 uint32_t trace_rays_threads(uint32_t n) { return grid_for(n) * kBlock; }
 
+template <int kOcc>
+static void launch_head(const KArgs& A, uint32_t g, size_t lds, hipStream_t s) {
+    hipLaunchKernelGGL((k_path_head<kOcc>), dim3(g), dim3(64), lds, s, A);
+}
+template <int kOcc>
+static void launch_tail(const KArgs& A, uint32_t g, size_t lds, hipStream_t s, int d) {
+    hipLaunchKernelGGL((k_path_tail<kOcc>), dim3(g), dim3(64), lds, s, A, d);
+}
+
+// The depth-split schedule (FrameParams::split): the head, then one tail launch per depth.
+static void launch_split(const KArgs& A, uint32_t gm, size_t lds, hipStream_t s) {
+    const FrameParams& fp = A.P;
+    const int L = fp.set.MaxPathLength < 2 ? 2 : fp.set.MaxPathLength;
+    switch (fp.megakernel_occupancy) {
+        case 8: launch_head<8>(A, gm, lds, s); break;
+        case 7: launch_head<7>(A, gm, lds, s); break;
+        case 6: launch_head<6>(A, gm, lds, s); break;
+        case 5: launch_head<5>(A, gm, lds, s); break;
+        default: launch_head<4>(A, gm, lds, s); break;
+    }
+    for (int d = 2; d <= L - 1; ++d) {
+        switch (fp.tail_occupancy) {
+            case 8: launch_tail<8>(A, gm, lds, s, d); break;
+            case 7: launch_tail<7>(A, gm, lds, s, d); break;
+            case 6: launch_tail<6>(A, gm, lds, s, d); break;
+            case 5: launch_tail<5>(A, gm, lds, s, d); break;
+            default: launch_tail<4>(A, gm, lds, s, d); break;
+        }
+    }
+}
+
 hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream,
-                        hipEvent_t* ev, hipStream_t aux, hipEvent_t* fork_ev) {
+                        hipEvent_t* ev, hipStream_t aux, hipEvent_t* fork_ev, uint32_t* sched_out) {
     KArgs A{scene, fb, fp};
+    uint32_t sched_local = 0;
+    uint32_t& sched = sched_out ? *sched_out : sched_local;
+    sched = 0;
     A.P.lds_nodes = scene.width == 8 ? std::min(fp.lds_nodes, scene.num_nodes) : 0u;
     const uint32_t g = grid_for(fp.num_paths);
     const size_t lds = size_t(scene.stack_ints) * kBlock * sizeof(int);
@@ -2729,14 +2930,22 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
         // one wave per workgroup: the per-lane stack base is the lane's (DXRPT_STACK_TID, stack_base)
         const uint32_t tb = 64u;
         const size_t ldsm = size_t(scene.stack_ints) * tb * sizeof(int);
-        // mega_lanes < 64 (per-lane path, no persistent grid / LDS nodes): 64 threads per mega_lanes paths
-        const bool twins = fp.mega_lanes < 64u && !fp.mega_persistent && !A.P.lds_nodes;
+        // mega_lanes < 64 (per-lane path, no persistent grid / LDS nodes): 64 threads per mega_lanes paths.
+        // A census frame always runs the 64-lane per-path kernel (one wave per 64 paths).
+        const bool twins = fp.mega_lanes < 64u && !fp.mega_persistent && !A.P.lds_nodes && !A.P.trav;
         const uint64_t threads = twins ? ((uint64_t(fp.num_paths) + fp.mega_lanes - 1u) / fp.mega_lanes + fp.split_units) * 64u
                                        : fp.num_paths;
         const uint32_t gm = uint32_t((threads + tb - 1u) / tb);
+        const bool ordered = (fp.wave_cost || fp.wave_order) && fp.megakernel_occupancy >= 4 && fp.megakernel_occupancy <= 7;
+        sched = DXRPT_SCHED_MEGAKERNEL;
         if (ev) (void)hipEventRecord(ev[0], stream);
         if (A.P.trav) {  // census frame (DXRPT_OPT_COUNT_TRAVERSAL): same schedule, counting instantiation
+            sched |= DXRPT_SCHED_CENSUS;
             hipLaunchKernelGGL((k_path<7, false, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
+        }
+        else if (fp.split && !fp.mega_persistent && !A.P.lds_nodes && !twins && !ordered) {
+            sched |= DXRPT_SCHED_SPLIT;
+            launch_split(A, gm, ldsm, stream);
         }
         else if (fp.mega_persistent && tb == 64u) {
             const uint32_t gp = std::min(gm, fp.mega_persistent * fp.num_cus);
@@ -2754,12 +2963,15 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
             else hipLaunchKernelGGL((k_path<4, false, true>), dim3(gm), dim3(tb), ldsn, stream, A);
         }
         else if (twins) {  // (cost ordering by FrameParams::wave_order / wave_cost, null: off)
+            sched |= DXRPT_SCHED_PATH_GROUPS | (fp.wave_cost || fp.wave_order ? DXRPT_SCHED_ORDER_KERNEL : 0u) |
+                     (fp.wave_order ? DXRPT_SCHED_COST_ORDERED : 0u);
             if (fp.megakernel_occupancy >= 7) hipLaunchKernelGGL((k_path<7, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
             else if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_path<6, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
             else if (fp.megakernel_occupancy == 5) hipLaunchKernelGGL((k_path<5, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
             else hipLaunchKernelGGL((k_path<4, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
         }
-        else if ((fp.wave_cost || fp.wave_order) && fp.megakernel_occupancy >= 4 && fp.megakernel_occupancy <= 7) {  // cost-ordered waves
+        else if (ordered) {  // cost-ordered waves
+            sched |= DXRPT_SCHED_ORDER_KERNEL | (fp.wave_order ? DXRPT_SCHED_COST_ORDERED : 0u);
             if (fp.megakernel_occupancy == 7) hipLaunchKernelGGL((k_path<7, false, false, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
             else if (fp.megakernel_occupancy == 6) hipLaunchKernelGGL((k_path<6, false, false, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);
             else if (fp.megakernel_occupancy == 5) hipLaunchKernelGGL((k_path<5, false, false, false, false, true>), dim3(gm), dim3(tb), ldsm, stream, A);

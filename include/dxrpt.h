@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define DXRPT_ABI_VERSION 1
+#define DXRPT_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------------------------------- */
 #define DXRPT_OK 0
@@ -212,7 +212,20 @@ typedef struct dxrpt_stats {
     uint64_t kernel_launches[DXRPT_K_COUNT];
     uint64_t timed_frames;
     double frame_ms;                   /* summed raygen-start -> accumulate-end time of the timed frames */
+    /* The schedule the last dxrpt_render ran (DXRPT_SCHED_* bits), the paths each 64-lane wave of its
+       megakernel carried (64, or 32 / 16 with path groups; 0 for the wavefront passes) and its register
+       budget in waves per SIMD. */
+    uint32_t schedule;
+    uint32_t paths_per_wave;
+    uint32_t occupancy;
+    uint32_t pad;
 } dxrpt_stats;
+#define DXRPT_SCHED_MEGAKERNEL 1u    /* k_path (or the split head/tail kernels): no wavefront passes */
+#define DXRPT_SCHED_PATH_GROUPS 2u   /* several lanes per path (paths_per_wave < 64) */
+#define DXRPT_SCHED_ORDER_KERNEL 4u  /* the cost-ordered instantiation ran (it records wave costs) */
+#define DXRPT_SCHED_COST_ORDERED 8u  /* ... and started the waves in a cost order built by earlier frames */
+#define DXRPT_SCHED_CENSUS 16u       /* the counting (DXRPT_OPT_COUNT_TRAVERSAL) instantiation */
+#define DXRPT_SCHED_SPLIT 32u        /* depth-split megakernel: k_path_head then compacted k_path_tail */
 
 /* BVH summary (dxrpt_get_bvh_info). */
 typedef struct dxrpt_bvh_info {
@@ -359,6 +372,15 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                            durations and rebuilds the order, the frames between reuse it
                                            (default 16, one SqrtNumSamples^2 = 16 cycle of progressive
                                            frames; 1 = every frame).  Identical results. */
+#define DXRPT_OPT_MEGAKERNEL_SPLIT 33u /* 1: 64-lane path-ordered megakernel frames run as one kernel per path
+                                          depth -- a head kernel runs raygen and depth 1 of every camera
+                                          path, then per further depth one kernel runs the surviving paths,
+                                          compacted into full waves (wave64 ballot, one atomic per wave),
+                                          with the path state in the queue instead of registers and its own
+                                          register budget.  0: the single k_path.  2: by frame size.
+                                          Identical results. */
+#define DXRPT_OPT_TAIL_OCCUPANCY 34u   /* register budget of the split schedule's tail kernels in waves/SIMD:
+                                          0 = the head's (default), 4..8 */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);
@@ -386,9 +408,12 @@ int dxrpt_post_process(dxrpt_ctx* ctx, const dxrpt_app_settings* settings, const
                        uint32_t height, void* out, uint32_t out_format, void* stream);
 /* Synchronises the context's last stream and returns the counters of the last dxrpt_render. */
 int dxrpt_get_stats(dxrpt_ctx* ctx, dxrpt_stats* out);
-/* Diagnostic (DXRPT_OPT_WAVE_CLOCKS + DXRPT_OPT_COUNT_TRAVERSAL, megakernel frames): the last render's
- * per-wave (start, end) s_memrealtime stamps, wave w = paths [64 w, 64 w + 64) in path-slot order;
- * copies min(max_waves, waves) pairs into out[2 w], out[2 w + 1] and the wave count into *num_waves. */
+/* Diagnostic (DXRPT_OPT_WAVE_CLOCKS, megakernel frames): the last render's per-slot (start, end)
+ * s_memrealtime stamps.  On a census frame (+ DXRPT_OPT_COUNT_TRAVERSAL, always the 64-lane per-path
+ * kernel) slot w = paths [64 w, 64 w + 64) in path-slot order; on a cost-ordered frame slot w = the
+ * paths [L w, L w + L) with L = the frame's paths per wave (64, or the path-group width).  A render that
+ * records no stamps leaves *num_waves = 0.  Copies min(max_waves, slots) pairs into out[2 w],
+ * out[2 w + 1] and the slot count into *num_waves. */
 int dxrpt_get_wave_clocks(dxrpt_ctx* ctx, uint64_t* out, uint32_t max_waves, uint32_t* num_waves);
 /* Diagnostic of kernel builds made with -DDXRPT_DIAG_PHASES=1 (zeros in the shipped build): lane time,
  * in s_memrealtime ticks (100 MHz) summed over every lane of the full-frame megakernel, spent in each

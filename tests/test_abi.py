@@ -34,7 +34,7 @@ def test_libdxrpt_host_exports_every_declared_function():
 
 def test_abi_version_and_defaults():
     L = A.lib()
-    assert L.dxrpt_abi_version() == 1
+    assert L.dxrpt_abi_version() == 2
     s = A.AppSettings()
     L.dxrpt_default_settings(C.byref(s))
     py = A.default_settings()

@@ -131,6 +131,57 @@ def test_unsupported_images_fail_loudly(tmp_path):
         I.decode(tmp_path / "missing.png")
 
 
+def _jpeg_segments(data):
+    """(marker, offset of the 0xFF, segment length) of every header segment before the entropy data."""
+    out, p = [], 2
+    while p + 4 <= len(data):
+        m = data[p + 1]
+        n = (data[p + 2] << 8) | data[p + 3]
+        out.append((m, p, n))
+        if m == 0xDA:
+            break
+        p += 2 + n
+    return out
+
+
+def _patched(data, at, value):
+    b = bytearray(data)
+    b[at] = value
+    return bytes(b)
+
+
+def test_malformed_jpeg_fails_loudly(tmp_path):
+    # table ids out of range and segments too short for their fixed fields must be rejected before
+    # any read past the segment (Huffman / quantisation tables are indexed 0..3)
+    buf = io.BytesIO()
+    PIL.fromarray(_smooth_image(24, 24, 3), "RGB").save(buf, "JPEG", quality=80)
+    good = buf.getvalue()
+    seg = {m: (p, n) for m, p, n in _jpeg_segments(good)}
+    sos_p, sos_n = seg[0xDA]
+    sof_p, sof_n = seg[0xC0]
+    dqt_p, _ = seg[0xDB]
+    dht_p, _ = seg[0xC4]
+    cases = {
+        "scan DC table id 15": _patched(good, sos_p + 4 + 2, 0xF0 | (good[sos_p + 4 + 2] & 0x0F)),
+        "scan AC table id 7": _patched(good, sos_p + 4 + 2, (good[sos_p + 4 + 2] & 0xF0) | 0x07),
+        "quant table id 9": _patched(good, dqt_p + 4, 0x09),
+        "quant precision 3": _patched(good, dqt_p + 4, 0x30),
+        "huffman class 2": _patched(good, dht_p + 4, 0x20 | (good[dht_p + 4] & 0x0F)),
+        "frame component quant id 5": _patched(good, sof_p + 4 + 8, 5),
+        # SOF claiming 3 components in a 5-byte segment, then end of file
+        "short frame header": good[:sof_p] + bytes([0xFF, 0xC0, 0x00, 0x07, 8, 0, 24, 0, 24]),
+        "short scan header": good[:sos_p] + bytes([0xFF, 0xDA, 0x00, 0x03, 3]),
+        "short restart interval": good[:sos_p] + bytes([0xFF, 0xDD, 0x00, 0x02]) + good[sos_p:],
+        "quant table past the segment": good[:dqt_p] + bytes([0xFF, 0xDB, 0x00, 0x06, 0x00, 1, 2, 3]) + good[dqt_p:],
+    }
+    for what, data in cases.items():
+        f = tmp_path / "bad.jpg"
+        f.write_bytes(data)
+        with pytest.raises(RuntimeError):
+            I.decode(f)
+        assert what
+
+
 @needs_ref
 def test_reference_png_assets_exact():
     # theInn's textures (Content/Models/theInn/textures): RGBA and RGB, 512..2048 px
