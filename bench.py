@@ -134,6 +134,9 @@ def main():
     ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
     ap.add_argument("--layout", default="bands", choices=["bands", "blocks"],
                     help="N-GPU screen partition: round-robin 8-row bands (default) or a seeded 8x8-block deal")
+    ap.add_argument("--gather", default="native", choices=["native", "torch"],
+                    help="N-GPU frame-end gather: the C ABI's RCCL send/recv + un-permute kernel (default) or "
+                         "torch.distributed.gather + index_select")
     args = ap.parse_args()
     global SCENE, WIDTH, HEIGHT, PATH_LENGTH
     SCENE, WIDTH, HEIGHT, PATH_LENGTH = CONFIGS[args.config]
@@ -144,7 +147,7 @@ def main():
     import torch.distributed as dist
     import dxrpathtracer_amd as D
     import dxrpathtracer_amd._abi as A
-    from dxrpathtracer_amd.distributed import PipelinedGather, screen_layout, source_index
+    from dxrpathtracer_amd.distributed import NativeGather, PipelinedGather, screen_layout, source_index
     from dxrpathtracer_amd.tracer import DXRPathTracer
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -175,11 +178,14 @@ def main():
     full = idx = None
     if world > 1 and rank == 0:
         full = torch.zeros((WIDTH * HEIGHT, 4), dtype=torch.float32, device="cuda")
-        idx = torch.tensor(source_index(lay), dtype=torch.long, device="cuda")
+        if args.gather == "torch":
+            idx = torch.tensor(source_index(lay), dtype=torch.long, device="cuda")
     consts = [D.make_constants(scene, settings, sky, WIDTH, HEIGHT, s) for s in range(16)]
 
     # frame-end gather of the band slabs to rank 0 (RCCL), overlapped with the next frame's render
-    pg = PipelinedGather(lay, rank, full, idx) if world > 1 else None
+    pg = None
+    if world > 1:
+        pg = NativeGather(lay, rank, local_rank, full) if args.gather == "native" else PipelinedGather(lay, rank, full, idx)
 
     def frame(f):
         tracer.render_raw(consts[f % 16], settings, accum.data_ptr(), WIDTH, HEIGHT, tiles=tiles, stream=sh,
@@ -298,7 +304,8 @@ def main():
             "config": {"workload": f"{SCENE}-proxy {WIDTH}x{HEIGHT} L={PATH_LENGTH} 1spp/frame progressive",
                        "width": WIDTH, "height": HEIGHT, "max_path_length": PATH_LENGTH,
                        "sqrt_num_samples": 4, "triangles": scene.num_triangles, "sky": sky.model,
-                       "parallelism": (f"screen {args.layout} x{world} + RCCL gather" if world > 1 else "single GPU")},
+                       "parallelism": (f"screen {args.layout} x{world} + RCCL gather ({args.gather})" if world > 1
+                                       else "single GPU")},
             "roofline": {"bound": "hbm", "kernel": roof_kernel, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "bytes_per_launch": int(roof_bytes),
@@ -343,6 +350,8 @@ def main():
         }
         print(json.dumps(result), flush=True)
     if world > 1:
+        if hasattr(pg, "close"):
+            pg.close()
         dist.barrier()
         dist.destroy_process_group()
     tracer.close()

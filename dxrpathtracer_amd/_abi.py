@@ -22,6 +22,7 @@ DXRPT_OK = 0
 DXRPT_INVALID_INDEX = 0xFFFFFFFF
 DXRPT_MAX_SPOT_LIGHTS = 32
 DXRPT_MAX_PATH_LENGTH = 8
+DXRPT_COMM_ID_BYTES = 128
 TEX_RGBA8_UNORM, TEX_RGBA8_SRGB, TEX_R8_UNORM = 0, 1, 2
 TRACE_ANY_HIT, TRACE_ALPHA = 1, 2
 SCENE_SPONZA, SCENE_SUNTEMPLE, SCENE_BOXTEST, SCENE_WHITEFURNACE, SCENE_STRONGHOLD = 0, 1, 2, 3, 4
@@ -154,7 +155,8 @@ DXRPT_SYMBOLS = ("dxrpt_abi_version", "dxrpt_default_settings", "dxrpt_create", 
                  "dxrpt_set_scene", "dxrpt_add_texture", "dxrpt_set_sky", "dxrpt_build_bvh", "dxrpt_get_bvh_info",
                  "dxrpt_render", "dxrpt_get_stats", "dxrpt_trace_rays", "dxrpt_set_option", "dxrpt_reset_timing",
                  "dxrpt_post_process", "dxrpt_bake_lightmap", "dxrpt_denoise_median", "dxrpt_get_wave_clocks",
-                 "dxrpt_get_phase_clocks")
+                 "dxrpt_get_phase_clocks", "dxrpt_sample_cmj", "dxrpt_comm_unique_id", "dxrpt_comm_create",
+                 "dxrpt_comm_destroy", "dxrpt_gather_slabs", "dxrpt_unpermute", "dxrpt_multi_last_error")
 DXRPT_HOST_SYMBOLS = ("dxrpt_host_scene_create", "dxrpt_host_scene_load", "dxrpt_host_scene_destroy", "dxrpt_host_last_error",
                       "dxrpt_host_inv_view_projection", "dxrpt_host_sky_create", "dxrpt_host_fill_constants",
                       "dxrpt_host_float_to_half", "dxrpt_host_half_to_float", "dxrpt_host_hosek_load",
@@ -208,6 +210,13 @@ def lib() -> C.CDLL:
                                           C.POINTER(LightConstants), P, P, P, P, u32, u32, P]
         L.dxrpt_denoise_median.argtypes = [P, P, P, u32, u32, P]
         L.dxrpt_reset_timing.argtypes = [P]
+        L.dxrpt_sample_cmj.argtypes = [P, P, u32, P, P]
+        L.dxrpt_comm_unique_id.argtypes = [P]
+        L.dxrpt_comm_create.argtypes = [C.c_int, C.c_int, C.c_int, P, C.POINTER(P)]
+        L.dxrpt_comm_destroy.argtypes = [P]
+        L.dxrpt_gather_slabs.argtypes = [P, P, C.POINTER(C.c_uint64), P, P]
+        L.dxrpt_unpermute.argtypes = [P, C.POINTER(Tile), u32, P, u32, u32, P]
+        L.dxrpt_multi_last_error.restype = C.c_char_p
         _lib = L
     return _lib
 

@@ -1042,6 +1042,15 @@ int dxrpt_trace_rays(dxrpt_ctx* ctx, const float* rays, uint32_t num_rays, uint3
     });
 }
 
+int dxrpt_sample_cmj(dxrpt_ctx* ctx, const uint32_t* cases, uint32_t num_cases, float* out, void* stream) {
+    if (!ctx) return DXRPT_E_INVALID_ARG;
+    return guarded(ctx, [&] {
+        require(num_cases == 0 || (cases && out), "dxrpt_sample_cmj: null argument");
+        HIP_CHECK(launch_sample_cmj(reinterpret_cast<const uint4*>(cases), num_cases, reinterpret_cast<float2*>(out),
+                                    static_cast<hipStream_t>(stream)));
+    });
+}
+
 // PostProcessor::Render (DXRPathTracer/PostProcessor.cpp:43-92): bloom + exposure + filmic tone map.
 int dxrpt_post_process(dxrpt_ctx* ctx, const dxrpt_app_settings* settings, const float* accum, uint32_t width,
                        uint32_t height, void* out, uint32_t out_format, void* stream) {

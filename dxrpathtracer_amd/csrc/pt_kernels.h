@@ -223,6 +223,9 @@ hipError_t launch_trace_rays(const SceneDev& scene, const float4* rays, uint32_t
 uint32_t frame_traversal_threads(uint32_t num_paths, uint32_t shadow_slots, uint32_t chunks_per_wave);
 uint32_t trace_rays_threads(uint32_t n);
 
+// SampleCMJ2D on device cases (x = sampleIdx, y = numSamplesX, z = numSamplesY, w = pattern) -> out.
+hipError_t launch_sample_cmj(const uint4* cases, uint32_t n, float2* out, hipStream_t stream);
+
 // DXRPT_DIAG_PHASES builds: the per-phase lane ticks since the last call (synchronises the device, zeroes them).
 hipError_t read_phase_ticks(unsigned long long out[8]);
 

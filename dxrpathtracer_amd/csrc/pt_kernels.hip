@@ -2634,8 +2634,13 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
 
 // Queues the continuation of a vertex (all active lanes must call; `cont` selects) into queue d + 1;
 // returns its position.  The radiance word is written later (split_finish), after the shadow rays.
-PT_DEV uint32_t split_push(const KArgs& A, int d, bool cont, const VertexOut& O, uint32_t pix, uint32_t accumIdx) {
-    const uint32_t shard = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) % kQueueShards;
+// Producer wave w of nw (in screen order) appends to shard w * 64 / nw: each shard holds a contiguous
+// run of screen blocks, so the next depth's waves, which take the queue in shard order, sweep the
+// image like the head's (neighbouring origins resident together share the BVH nodes and texels in
+// cache), while the waves running at any time still spread their atomics over several shards.
+PT_DEV uint32_t split_push(const KArgs& A, int d, bool cont, const VertexOut& O, uint32_t pix, uint32_t accumIdx,
+                           uint32_t w, uint32_t nw) {
+    const uint32_t shard = uint32_t((uint64_t(w) * kQueueShards) / nw);
     const uint32_t pos = queue_append(A.F.counters + uint32_t(d + 1) * kQueueShards, A.F.cap_r, cont, shard);
     if (cont) {
         const RayQueue& Q = A.F.q[(d + 1) & 1];
@@ -2663,8 +2668,8 @@ void k_path_head(KArgs A) {
     if (A.F.counters_next && blockIdx.x == 0u)  // the next frame's counter set (see k_path)
         for (uint32_t i = threadIdx.x; i < kCounterWords; i += blockDim.x) A.F.counters_next[i] = 0u;
     lut_fill(A.S);
-    const uint32_t p = (A.P.xcd_chunk ? xcd_position(blockIdx.x, gridDim.x, A.P.xcd_chunk) : blockIdx.x) * blockDim.x +
-                       threadIdx.x;
+    const uint32_t blk = A.P.xcd_chunk ? xcd_position(blockIdx.x, gridDim.x, A.P.xcd_chunk) : blockIdx.x;
+    const uint32_t p = blk * blockDim.x + threadIdx.x;
     if (p >= A.P.num_paths) return;
     const dxrpt_app_settings& set = A.P.set;
     const PrimaryRay pr = primary_ray(A, p);
@@ -2694,7 +2699,7 @@ void k_path_head(KArgs A) {
     count_rays(A.F.counters + (kMaxDepthQueues + 1u) * kQueueShards, nsh);
     const bool cont = O.cont;
     const bool nextDiffuse = O.nextIsDiffuse;
-    const uint32_t qpos = split_push(A, 1, cont, O, pr.pixelIdx, pr.accumIdx);
+    const uint32_t qpos = split_push(A, 1, cont, O, pr.pixelIdx, pr.accumIdx, blk, gridDim.x);
     float4 rad = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     rad.x += 1.0f * O.local.x;
     rad.y += 1.0f * O.local.y;
@@ -2710,9 +2715,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kOcc > 0
 void k_path_tail(KArgs A, int d) {
     const uint32_t* cnt = A.F.counters + uint32_t(d) * kQueueShards;
     const uint32_t n = queue_total(cnt);
-    if (blockIdx.x * blockDim.x >= n) return;  // the whole workgroup (one wave) is past the queue
+    const uint32_t nw = (n + 63u) / 64u;  // waves with work
+    // wave j of the queue: XCD runs of A.P.xcd_chunk consecutive queue chunks among the nw live waves
+    // (workgroup b runs on XCD b mod 8; the grid's surplus workgroups exit at once)
+    if (blockIdx.x >= nw) return;
+    const uint32_t j = A.P.xcd_chunk ? xcd_position(blockIdx.x, nw, A.P.xcd_chunk) : blockIdx.x;
     lut_fill(A.S);
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t i = j * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const dxrpt_app_settings& set = A.P.set;
     const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
@@ -2743,7 +2752,7 @@ void k_path_tail(KArgs A, int d) {
     const bool cont = O.cont;
     const bool nextDiffuse = O.nextIsDiffuse;
     const int L = set.MaxPathLength < 2 ? 2 : set.MaxPathLength;
-    const uint32_t qpos = d + 1 <= L - 1 ? split_push(A, d, cont, O, V.pix, accumIdx) : 0u;
+    const uint32_t qpos = d + 1 <= L - 1 ? split_push(A, d, cont, O, V.pix, accumIdx, j, nw) : 0u;
     float4 rad = make_float4(r4.x, r4.y, r4.z, 0.0f);
     rad.x += V.pathThr.x * O.local.x;
     rad.y += V.pathThr.y * O.local.y;
@@ -3148,6 +3157,22 @@ hipError_t launch_trace_rays(const SceneDev& scene, const float4* rays, uint32_t
         hipLaunchKernelGGL((k_trace_rays<8>), dim3(grid_for(n)), dim3(kBlock), lds, stream, scene, rays, n, flags, hits);
     else
         hipLaunchKernelGGL((k_trace_rays<2>), dim3(grid_for(n)), dim3(kBlock), lds, stream, scene, rays, n, flags, hits);
+    return hipGetLastError();
+}
+
+// SampleCMJ2D (Sampling.hlsl:322-331) on arbitrary (sampleIdx, numSamplesX, numSamplesY, pattern) cases.
+__global__ __launch_bounds__(kBlock) void k_sample_cmj(const uint4* cases, uint32_t n, float2* out) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint4 c = cases[i];
+    float x, y;
+    sample_cmj2d(c.x, c.y, c.z, c.w, &x, &y);
+    out[i] = make_float2(x, y);
+}
+
+hipError_t launch_sample_cmj(const uint4* cases, uint32_t n, float2* out, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sample_cmj, dim3(grid_for(n)), dim3(kBlock), 0, stream, cases, n, out);
     return hipGetLastError();
 }
 

@@ -173,3 +173,99 @@ class PipelinedGather:
         work.wait()
         if self.rank == 0:
             torch.index_select(self.recv[k], 0, self.src_index, out=self.full)
+
+
+def gathered_tiles(layout: BandLayout):
+    """Every rank's tiles with accum_offset moved to the rank's slab in the gathered buffer of
+    dxrpt_gather_slabs (rank r's slab at sum(counts[:r]) pixels): the tile list of dxrpt_unpermute."""
+    out, base = [], 0
+    for r in range(layout.world):
+        for t in layout.tiles[r]:
+            out.append(A.Tile(t.x0, t.y0, t.w, t.h, base + t.accum_offset, t.accum_pitch, 0))
+        base += layout.counts[r]
+    return out
+
+
+class NativeGather:
+    """The frame-end gather through the C ABI (libdxrpt.so): an RCCL communicator of the
+    job's ranks made by dxrpt_comm_create (rank 0's unique id broadcast over torch.distributed, the only
+    thing torch does here), grouped ncclSend / ncclRecv of every rank's slab into one contiguous buffer on
+    rank 0 (dxrpt_gather_slabs) and the un-permute kernel into the W x H frame (dxrpt_unpermute) -- the
+    sequence a C++ host runs.  Pipelined like PipelinedGather: frame f's slab is
+    snapshotted on the render stream, gathered on a side stream while frame f+1 renders, and un-permuted
+    on the render stream once frame f+1 is submitted (or at flush())."""
+
+    def __init__(self, layout: BandLayout, rank: int, device: int, full=None, group=None):
+        import ctypes as C
+        import torch
+        import torch.distributed as dist
+        self.layout, self.rank, self.full = layout, rank, full
+        self.L = A.lib()
+        uid = C.create_string_buffer(A.DXRPT_COMM_ID_BYTES)
+        if rank == 0:
+            self._check(self.L.dxrpt_comm_unique_id(uid), "dxrpt_comm_unique_id")
+        obj = [bytes(uid.raw) if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        uid = C.create_string_buffer(obj[0], A.DXRPT_COMM_ID_BYTES)
+        self.comm = C.c_void_p()
+        self._check(self.L.dxrpt_comm_create(device, layout.world, rank, uid, C.byref(self.comm)), "dxrpt_comm_create")
+        self.counts = (C.c_uint64 * layout.world)(*layout.counts)
+        self.tiles = gathered_tiles(layout)
+        self.tarr = (A.Tile * len(self.tiles))(*self.tiles)
+        self.total = sum(layout.counts)
+        self.side = torch.cuda.Stream()
+        self.staging = None
+        self.recv = None
+        self.pending = None
+        self.count = 0
+
+    def _check(self, rc, what):
+        if rc != A.DXRPT_OK:
+            msg = self.L.dxrpt_multi_last_error()
+            raise RuntimeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    def submit(self, local):
+        import ctypes as C
+        import torch
+        cur = torch.cuda.current_stream()
+        n = self.layout.counts[self.rank]
+        if self.staging is None:
+            self.staging = [torch.empty((n, 4), dtype=torch.float32, device=local.device) for _ in range(2)]
+            if self.rank == 0:
+                self.recv = [torch.empty((self.total, 4), dtype=torch.float32, device=local.device) for _ in range(2)]
+        k = self.count % 2
+        self.count += 1
+        self.staging[k].copy_(local[:n])
+        self.side.wait_stream(cur)
+        self._check(self.L.dxrpt_gather_slabs(self.comm, C.c_void_p(self.staging[k].data_ptr()), self.counts,
+                                              C.c_void_p(self.recv[k].data_ptr()) if self.rank == 0 else None,
+                                              C.c_void_p(self.side.cuda_stream)), "dxrpt_gather_slabs")
+        ev = torch.cuda.Event()
+        ev.record(self.side)
+        prev, self.pending = self.pending, (ev, k)
+        if prev is not None:
+            self._finish(prev)
+
+    def flush(self):
+        if self.pending is not None:
+            self._finish(self.pending)
+            self.pending = None
+
+    def _finish(self, pend):
+        import ctypes as C
+        import torch
+        ev, k = pend
+        cur = torch.cuda.current_stream()
+        cur.wait_event(ev)
+        if self.rank == 0:
+            self._check(self.L.dxrpt_unpermute(C.c_void_p(self.recv[k].data_ptr()), self.tarr, len(self.tiles),
+                                               C.c_void_p(self.full.data_ptr()), self.layout.width, self.layout.height,
+                                               C.c_void_p(cur.cuda_stream)), "dxrpt_unpermute")
+
+    def close(self):
+        if self.comm:
+            self.flush()
+            import torch
+            torch.cuda.synchronize()
+            self._check(self.L.dxrpt_comm_destroy(self.comm), "dxrpt_comm_destroy")
+            self.comm = None

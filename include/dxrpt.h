@@ -434,6 +434,38 @@ int dxrpt_get_phase_clocks(dxrpt_ctx* ctx, uint64_t out[8]);
 int dxrpt_trace_rays(dxrpt_ctx* ctx, const float* rays, uint32_t num_rays, uint32_t flags, float* hits,
                      void* stream);
 
+/* SampleCMJ2D (Shaders/Sampling.hlsl:322-331, the sampler of RayTrace.hlsl:85-90) evaluated by the GPU
+ * path's own code on num_cases device cases of 4 uint32 (sampleIdx, numSamplesX, numSamplesY, pattern);
+ * out (device) receives 2 floats per case.  Pins the kernels' sampler against the reference's vectors. */
+int dxrpt_sample_cmj(dxrpt_ctx* ctx, const uint32_t* cases, uint32_t num_cases, float* out, void* stream);
+
+/* ---- multi-GPU frame (no reference counterpart: the reference is single-GPU) -------
+ * The frame is split into screen tiles across the GPUs of a node, one process and context per GPU: rank
+ * r renders its tiles (dxrpt_render with its tile list; accum_offset/pitch address its compact slab),
+ * dxrpt_gather_slabs moves every slab to rank 0 over RCCL (grouped ncclSend / ncclRecv: each xGMI link
+ * carries one rank's slab, all at once), and rank 0 scatters the gathered slabs into the W x H frame
+ * with dxrpt_unpermute.  CMJ seeds use global pixel indices, so the result is the single-GPU frame. */
+#define DXRPT_COMM_ID_BYTES 128
+/* An RCCL unique id (ncclGetUniqueId) for dxrpt_comm_create; rank 0 makes it and sends the 128 bytes to
+ * the other ranks by any means (MPI, a file, torch.distributed in the Python driver). */
+int dxrpt_comm_unique_id(void* id);
+/* RCCL communicator of `nranks` ranks on HIP device `hip_device` (ncclCommInitRank; collective: every rank
+ * calls it with the same id).  *comm is an ncclComm_t, released with dxrpt_comm_destroy. */
+int dxrpt_comm_create(int hip_device, int nranks, int rank, const void* id, void** comm);
+int dxrpt_comm_destroy(void* comm);
+/* Collective frame-end gather: rank r sends counts[r] float4 pixels of its device `slab`; rank 0 receives
+ * all ranks' slabs back to back into its device `gathered` (rank r at sum(counts[0..r-1]) float4s; its
+ * own slab is copied on `stream`).  Every rank passes the same counts[nranks]; stream-ordered. */
+int dxrpt_gather_slabs(void* comm, const float* slab, const uint64_t* counts, float* gathered, void* stream);
+/* Un-permute: the pixels of `tiles` (host array; tile pixel (lx, ly) read at src[accum_offset + ly *
+ * accum_pitch + lx], float4 units) written to the row-major width x height device frame `dst` at
+ * (x0 + lx, y0 + ly).  For a gathered frame: every rank's tiles with accum_offset += the rank's slab
+ * offset in `gathered`.  The tile list is cached on the device while it is unchanged. */
+int dxrpt_unpermute(const float* src, const dxrpt_tile* tiles, uint32_t num_tiles, float* dst, uint32_t width,
+                    uint32_t height, void* stream);
+/* Message of the last failed dxrpt_comm_* / dxrpt_gather_slabs / dxrpt_unpermute call of this thread. */
+const char* dxrpt_multi_last_error(void);
+
 /* ---- lightmap baking (the second consumer of PathTrace) ----------------------------------------
  * One progressive bake pass: BakeRayGen (DXRPathTracer/Baking.hlsl:336-465) as dispatched by
  * DXRPathTracer::RenderBakingPass_Progressive (DXRPathTracer.cpp:1895-1991), one thread per texel of

@@ -691,3 +691,21 @@ def test_megakernel_split_is_bit_identical(torch_cuda, name, L, W, H, occ, tocc)
         t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, A.DEFAULT_MEGAKERNEL_OCCUPANCY)
         t.set_option(A.OPT_MEGAKERNEL_LANES, A.DEFAULT_MEGAKERNEL_LANES)
         t.set_option(A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)
+
+
+def test_gpu_cmj_matches_reference_vectors(torch_cuda):
+    # the kernels' SampleCMJ2D (pt_math.h, Sampling.hlsl:322-331) against the reference's own C++ CMJ
+    # (Graphics/Sampling.cpp:383-432, tests/golden/make_cmj_golden.py), bit for bit
+    import json
+    import os
+    torch = torch_cuda
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "cmj_reference.json")))
+    cases = np.array(g["cases"], dtype=np.uint64)
+    inp = torch.from_numpy(cases[:, :4].astype(np.uint32).view(np.int32).copy()).cuda()
+    out = torch.zeros((len(cases), 2), dtype=torch.float32, device="cuda")
+    t = tracer("boxtest")
+    rc = A.lib().dxrpt_sample_cmj(t._ctx, C.c_void_p(inp.data_ptr()), len(cases), C.c_void_p(out.data_ptr()),
+                                  C.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), cases[:, 4:6].astype(np.uint32))

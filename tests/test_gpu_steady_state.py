@@ -1,0 +1,125 @@
+"""GPU parity of the STEADY-STATE shipped schedule: consecutive progressive frames through one fresh,
+untouched context, as bench.py and every rank of an N-GPU run render them.
+
+A frame of at most 3 rounds of resident waves runs the cost-ordered megakernel instantiation: frame 0
+records its wave costs in path order, frames 1+ start their waves in the cost order built from them
+(DXRPT_OPT_WAVE_ORDER, default "by frame size").  Frames of at most 400,000 paths (a GPU's 1/8 share of
+the metric frame) run path groups.  Each test renders >= 3 consecutive frames (RaygenShader over
+DispatchRays(W, H, 1), RayTrace.hlsl:92-149) into ONE accumulation target, checks after every frame
+that the schedule it expects actually ran (dxrpt_stats.schedule / paths_per_wave), and compares the
+accumulated crops with the oracle accumulated the same way (the progressive rule, RayTrace.hlsl:140-148).
+Gate: tests/_common.py (1e-4 relative).
+"""
+import numpy as np
+import pytest
+
+import dxrpathtracer_amd as D
+import dxrpathtracer_amd._abi as A
+from dxrpathtracer_amd.distributed import band_layout
+from dxrpathtracer_amd.tracer import DXRPathTracer
+from tests._common import assert_parity, oracle_scene, scene_bundle
+
+pytestmark = pytest.mark.gpu
+
+
+def _fresh(name):
+    sc, sky = scene_bundle(name)
+    t = DXRPathTracer(0)
+    t.initialize_scene(sc, sky)
+    t.build_rt_acceleration_structure()
+    return t
+
+
+def _band_crops(lay, rank, n=4, w=128):
+    """(crop, slab offset of its first pixel, slab pitch) for n bands of the rank spread over its list."""
+    tiles = lay.rank_tiles(rank)
+    picks = sorted({0, len(tiles) // 3, (2 * len(tiles)) // 3, len(tiles) - 1})[:n]
+    out = []
+    for k, i in enumerate(picks):
+        t = tiles[i]
+        x0 = t.x0 + (k * 397) % (t.w - w)
+        out.append(((x0, t.y0, w, t.h), t.accum_offset + (x0 - t.x0), t.accum_pitch))
+    return out
+
+
+def _frame_crops(W, H):
+    c = 64
+    crops = [(0, 0, c, c), (W - c, H - c, c, c), (W // 2 - 48, H // 2 - 32, 96, 64), (W // 3, H - 40, 80, 40)]
+    return [(cr, cr[1] * W + cr[0], W) for cr in crops]
+
+
+def _steady_frames(torch, name, W, H, L, frames, crops, tiles=None, n_out=None, expect=None):
+    sc, sky = scene_bundle(name)
+    st = sc.settings(MaxPathLength=L)
+    lights = D.make_lights(sc)
+    t = _fresh(name)
+    n = W * H if n_out is None else n_out
+    acc = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
+    refs = [None] * len(crops)
+    stream = torch.cuda.current_stream().cuda_stream
+    scheds = []
+    try:
+        for f in range(frames):
+            rtc = D.make_constants(sc, st, sky, W, H, f)
+            t.render_raw(rtc, st, acc.data_ptr(), W, H, tiles=tiles, stream=stream, lights=lights)
+            torch.cuda.synchronize()
+            s = t.stats()
+            scheds.append((s.schedule, s.paths_per_wave))
+            if expect is not None:
+                expect(f, s)
+            out = acc.cpu().numpy()
+            for k, ((x0, y0, w, h), off, pitch) in enumerate(crops):
+                refs[k], _ = oracle_scene(name).render(rtc, st, lights, W, H, crop=(x0, y0, w, h), accum=refs[k])
+                rows = np.array([[off + yy * pitch + xx for xx in range(w)] for yy in range(h)])
+                assert_parity(out[rows], refs[k], f"{name} {W}x{H} L{L} frame {f} crop {(x0, y0, w, h)}")
+    finally:
+        t.close()
+    return scheds
+
+
+def _expect_ordered(lanes):
+    def check(f, s):
+        assert s.schedule & A.SCHED_MEGAKERNEL and not s.schedule & A.SCHED_CENSUS, s.schedule
+        assert s.schedule & A.SCHED_ORDER_KERNEL, f"frame {f}: the cost-ordered instantiation did not run ({s.schedule})"
+        # frame 0 builds the order from its own wave costs; frames 1+ start their waves in that order
+        assert bool(s.schedule & A.SCHED_COST_ORDERED) == (f > 0), f"frame {f}: schedule {s.schedule}"
+        assert s.paths_per_wave == lanes, (f, s.paths_per_wave)
+        assert bool(s.schedule & A.SCHED_PATH_GROUPS) == (lanes < 64)
+    return check
+
+
+def test_c2_720p_L3_consecutive_frames(torch_cuda):
+    # BASELINE.json configs[1]: 14,400 waves <= 3 rounds of resident waves -> cost-ordered k_path from frame 1
+    W, H = 1280, 720
+    _steady_frames(torch_cuda, "sponza", W, H, 3, 3, _frame_crops(W, H), expect=_expect_ordered(64))
+
+
+@pytest.mark.parametrize("world,rank,lanes", [(8, 5, 32), (8, 0, 32), (2, 1, 64)])
+def test_metric_band_share_consecutive_frames(torch_cuda, world, rank, lanes):
+    # one GPU's share of the metric frame (bench.py --gpus N): 1/8 = 259,200 paths in path groups of 32
+    # per wave, 1/2 = 1,036,800 paths 64 per wave; both cost-ordered from their second frame
+    W, H = 1920, 1080
+    lay = band_layout(W, H, world)
+    _steady_frames(torch_cuda, "sponza", W, H, 3, 3, _band_crops(lay, rank), tiles=lay.rank_tiles(rank),
+                   n_out=lay.counts[rank], expect=_expect_ordered(lanes))
+
+
+def test_c5_4k_L6_gpu_share_consecutive_frames(torch_cuda):
+    # BASELINE.json configs[4]: what each of the 8 GPUs renders -- a 1/8 band share of 3840x2160 at
+    # MaxPathLength 6 (1,036,800 paths) on the default schedule, three consecutive frames
+    W, H = 3840, 2160
+    lay = band_layout(W, H, 8)
+    _steady_frames(torch_cuda, "sponza", W, H, 6, 3, _band_crops(lay, 3, w=96), tiles=lay.rank_tiles(3),
+                   n_out=lay.counts[3], expect=_expect_ordered(64))
+
+
+def test_c3_1080p_L8_sixteen_samples(torch_cuda):
+    # BASELINE.json configs[2]: "16 spp" = SqrtNumSamples 4 -> CurrSampleIdx 0..15 accumulated into one
+    # target through the shipped context (DXRPathTracer.cpp:2027-2028, 2089), compared after every frame
+    W, H = 1920, 1080
+    crops = [((x0, y0, 48, 48), y0 * W + x0, W) for (x0, y0) in ((0, 0), (936, 516), (1500, 880), (300, 1032))]
+
+    def check(f, s):
+        assert s.schedule & A.SCHED_MEGAKERNEL and s.paths_per_wave == 64, (f, s.schedule, s.paths_per_wave)
+
+    _steady_frames(torch_cuda, "sponza", W, H, 8, 16, crops, expect=check)

@@ -29,6 +29,21 @@ def test_cmj_matches_reference_probes():
         np.testing.assert_allclose(got, p["value"], rtol=2e-8, atol=1e-9)
 
 
+def _cmj_cases():
+    g = json.load(open(os.path.join(GOLDEN, "cmj_reference.json")))
+    return np.array(g["cases"], dtype=np.uint64)
+
+
+def test_cmj_matches_reference_vectors_bit_exact():
+    # 6,032 outputs of the reference's own SampleCMJ2D (Graphics/Sampling.cpp:383-432, compiled from the
+    # checkout by tests/golden/make_cmj_golden.py): every sample of square and non-square grids, patterns
+    # of several frame sizes / pixels / path depths and arbitrary u32 patterns
+    cases = _cmj_cases()
+    assert len(cases) > 5000 and len({(int(r[1]), int(r[2])) for r in cases}) >= 10
+    got = np.array([O.cmj2d(int(s), int(nx), int(ny), int(p)) for s, nx, ny, p, _, _ in cases], dtype=np.float32)
+    np.testing.assert_array_equal(got.view(np.uint32), cases[:, 4:6].astype(np.uint32))
+
+
 def test_cmj_is_a_latin_hypercube_stratification():
     # Kensler CMJ: the 16 samples of one pattern fall in distinct x and y strata (Sampling.hlsl:322-331)
     for pattern in (0, 1, 12345, 0xDEADBEEF):
