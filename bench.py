@@ -124,6 +124,62 @@ def pmc_traffic(kernel):
     return {}, None
 
 
+def pmc_frame(config):
+    """Per-FRAME counters of the megakernel schedule (k_path, or the split schedule's head + tails) from
+    the newest committed summary for this config (profiles/<round>_pmc_frame_<config>.json, written by
+    scripts/pmc_summary.py over scripts/profile.sh's rocprofv3 passes)."""
+    import glob
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", f"*_pmc_frame_{config}.json")), reverse=True):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if d.get("config") == f"{SCENE}-proxy {WIDTH}x{HEIGHT} L={PATH_LENGTH}":
+            return d, os.path.basename(p)
+    return {}, None
+
+
+def full_formula_bytes(census, settings, bvh, pixels):
+    """SURVEY.md 8(d)'s algorithmic bytes of one frame, term by term as the survey writes them:
+      per ray: 32 B in (o, d, tmax, flags) + 16 B hit out (radiance) or 4 B visibility (shadow)
+               + N_node x S_node + N_tri x S_tri (the census' fetches of the timed schedule)
+      per radiance hit: 12 (3 indices) + 192 (3 vertices) + 16 (GeometryInfo) + 24 (Material)
+               + taps x 4 texels x 4 B (RGBA8: normal, albedo if enabled; metallic, roughness, emissive)
+               + 64 (path-state RMW) + 32 (next-ray write) + 32 (shadow-ray write)
+      per miss: 4 x 8 B (FP16 cube bilinear)
+      + 32 B accumulation RMW per pixel.
+    Alpha-test opacity taps of any-hit candidates are not counted (a lower bound for C4)."""
+    hits = int(census.radiance_hits)
+    misses = int(census.radiance_rays) - hits
+    taps = 3 + int(settings.EnableNormalMaps) + int(settings.EnableAlbedoMaps)
+    per_hit = 12 + 192 + 16 + 24 + taps * 16 + 64 + 32 + 32
+    terms = {
+        "radiance_ray_io": int(census.radiance_rays) * (32 + 16),
+        "shadow_ray_io": int(census.shadow_rays) * (32 + 4),
+        "bvh_node_fetches": int(census.node_visits_radiance + census.node_visits_shadow) * int(bvh.node_bytes),
+        "triangle_fetches": int(census.tri_tests_radiance + census.tri_tests_shadow) * int(bvh.tri_bytes),
+        "radiance_hit_shading": hits * per_hit,
+        "miss_sky_taps": misses * 32,
+        "accumulation": ACCUM_BYTES * int(pixels),
+    }
+    return sum(terms.values()), {"terms": terms, "radiance_hits": hits, "misses": misses,
+                                 "taps_per_hit": taps, "bytes_per_hit": per_hit}
+
+
+def schedule_name(bits, ppw, A):
+    if not bits & A.SCHED_MEGAKERNEL:
+        return "wavefront passes"
+    if bits & A.SCHED_SPLIT:
+        return "depth-split megakernel (k_path_head + k_path_tail per depth)" + (", two concurrent halves"
+                                                                                 if bits & A.SCHED_PARTS else "")
+    s = "megakernel (k_path)"
+    if bits & A.SCHED_PATH_GROUPS:
+        s += f", path groups ({ppw} paths per wave)"
+    if bits & A.SCHED_COST_ORDERED:
+        s += ", cost-ordered waves"
+    return s
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -268,12 +324,26 @@ def main():
     # traversals) + the accumulation RMW; the shading gathers are not counted, so it is a lower bound
     fetch_bytes_frame = ((census.node_visits_radiance + census.node_visits_shadow) * bvh.node_bytes
                          + (census.tri_tests_radiance + census.tri_tests_shadow) * bvh.tri_bytes)
-    path_bytes_frame = fetch_bytes_frame + ACCUM_BYTES * n_local
+    path_bytes_lower = fetch_bytes_frame + ACCUM_BYTES * n_local
+    path_bytes_full, full_detail = full_formula_bytes(census, settings, bvh, n_local)
+    # k_path: the survey's full formula (census of the timed schedule); the fetch-only figure stays beside it
     roof_bytes = {"k_trace": trace_bytes_frame / launches_per_frame, "k_shadow": shadow_bytes_frame / launches_per_frame,
-                  "k_path": path_bytes_frame}[roof_kernel]
+                  "k_path": path_bytes_full}[roof_kernel]
     achieved = roof_bytes / (roof_ms_avg * 1e-3) / 1e9
     pmc, traffic_src = pmc_traffic(roof_kernel)
     traffic = pmc.get("hbm_bytes_per_launch")
+    l2_hit = pmc.get("l2_hit_rate")
+    wait_frac = pmc.get("wait_any_per_wave_cycle")
+    write_bytes = pmc.get("hbm_write_bytes_per_launch")
+    if roof_kernel == "k_path":  # per-frame PMC summary of the megakernel schedule of this config
+        fr, src = pmc_frame(args.config)
+        if fr:
+            traffic, traffic_src = fr.get("hbm_bytes_per_frame"), src
+            l2_hit, wait_frac, write_bytes = fr.get("l2_hit_rate"), fr.get("wait_any_per_wave_cycle"), fr.get("hbm_write_bytes")
+            pmc = {"kernel": " + ".join(fr.get("kernels", []))}
+    # what limits the kernel, from its counters: waves parked on s_waitcnt for most of their cycles with
+    # HBM far from its peak = latency of dependent loads (the roofline below is still priced against HBM)
+    bound = "latency" if (wait_frac is not None and wait_frac > 0.3 and achieved < 0.6 * HBM_PEAK_GBS) else "hbm"
     # the other traversal kernel, from the breakdown pass (for the record; wavefront schedule only)
     other = "k_shadow" if roof_kernel == "k_trace" else "k_trace"
     K_OTHER = A.K_SHADOW if other == "k_shadow" else A.K_TRACE
@@ -306,11 +376,18 @@ def main():
                        "sqrt_num_samples": 4, "triangles": scene.num_triangles, "sky": sky.model,
                        "parallelism": (f"screen {args.layout} x{world} + RCCL gather ({args.gather})" if world > 1
                                        else "single GPU")},
-            "roofline": {"bound": "hbm", "kernel": roof_kernel, "achieved": round(achieved, 1),
+            "roofline": {"bound": bound, "roofline_kind": "hbm",
+                         "kernel": ("k_path_head + k_path_tail (one frame)" if roof_kernel == "k_path" and stats.schedule & A.SCHED_SPLIT
+                                    else roof_kernel), "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "bytes_per_launch": int(roof_bytes),
+                         "bytes_formula": "SURVEY.md 8(d) full formula" if roof_kernel == "k_path" else "per-ray I/O + fetches",
+                         "bytes_fetch_lower_bound": int(path_bytes_lower) if roof_kernel == "k_path" else None,
+                         "frac_fetch_lower_bound": round(path_bytes_lower / (roof_ms_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                         if roof_kernel == "k_path" else None,
                          "avg_launch_ms": round(roof_ms_avg, 4), "traffic_source": traffic_src,
-                         "traffic_kernel": pmc.get("kernel"), "l2_hit_rate": pmc.get("l2_hit_rate")},
+                         "traffic_kernel": pmc.get("kernel"), "l2_hit_rate": l2_hit,
+                         "hbm_write_bytes": write_bytes, "wait_any_per_wave_cycle": wait_frac},
             "cpu_baseline": cpu,
             # the headline counts the reference's HUD rays (W*H*(1+2(L-1)) per frame); the kernels skip
             # shadow rays whose pending contribution is exactly 0 (identical image), so fewer are traced:
@@ -326,7 +403,9 @@ def main():
                                    "achieved_GBs": round(other_bytes / (other_ms * 1e-3) / 1e9, 1),
                                    "traffic": other_pmc.get("hbm_bytes_per_launch"),
                                    "l2_hit_rate": other_pmc.get("l2_hit_rate")} if other_ms > 0 else None,
-                "schedule": "megakernel (k_path)" if kms.get("k_path", 0) > 0 else "wavefront passes",
+                "schedule": schedule_name(stats.schedule, stats.paths_per_wave, A),
+                "schedule_bits": int(stats.schedule),
+                "algorithmic_bytes": full_detail,
                 "gpu_frame_ms_events": round(gpu_frame_ms, 4),
                 "kernel_breakdown_note": "kernel_ms_per_frame from a separate all-kernel event pass before the timed region",
                 "frame_ms": {"mean": round(float(frame_ms.mean()), 4), "median": round(float(np.median(frame_ms)), 4),

@@ -84,7 +84,7 @@ KERNEL_NAMES = ("k_raygen", "k_trace", "k_shade", "k_shadow", "k_accumulate", "k
  OPT_KERNEL_TIMING_MASK, OPT_XCD_MAPPING, OPT_PACKET_SWITCH, OPT_MEGAKERNEL_PATHS, OPT_MEGAKERNEL_OCCUPANCY,
  OPT_BAKE_CHUNK, OPT_MEGAKERNEL_PERSISTENT, OPT_MEGAKERNEL_LANES, OPT_WAVE_CLOCKS,
  OPT_WAVE_ORDER, OPT_SPLIT_UNITS, OPT_XCD_CHUNK, OPT_WAVE_ORDER_PERIOD, OPT_MEGAKERNEL_SPLIT,
- OPT_TAIL_OCCUPANCY) = range(1, 35)
+ OPT_TAIL_OCCUPANCY, OPT_SPLIT_PARTS) = range(1, 36)
 # context defaults of the traversal options (dxrpt_api.hip)
 DEFAULT_TRAVERSAL_PIPELINE = 0
 POST_FLOAT4, POST_RGBA8 = 0, 1  # dxrpt_post_process output formats
@@ -101,7 +101,8 @@ DEFAULT_WAVE_ORDER_PERIOD = 16
 DEFAULT_MEGAKERNEL_PERSISTENT = 0
 DEFAULT_MEGAKERNEL_LANES = 0  # by frame size
 DEFAULT_WAVE_ORDER = 2  # by frame size
-DEFAULT_MEGAKERNEL_SPLIT = 0
+DEFAULT_MEGAKERNEL_SPLIT = 2  # by frame size
+DEFAULT_SPLIT_PARTS = 0  # by frame size
 DEFAULT_TAIL_OCCUPANCY = 0
 
 
@@ -113,11 +114,12 @@ class Stats(C.Structure):
                 ("node_visits_shadow", C.c_uint64), ("tri_tests_shadow", C.c_uint64),
                 ("kernel_ms", C.c_double * K_COUNT), ("kernel_launches", C.c_uint64 * K_COUNT),
                 ("timed_frames", C.c_uint64), ("frame_ms", C.c_double), ("schedule", u32), ("paths_per_wave", u32),
-                ("occupancy", u32), ("pad", u32)]
+                ("occupancy", u32), ("pad", u32), ("radiance_hits", C.c_uint64)]
 
 
 # dxrpt_stats.schedule bits
-SCHED_MEGAKERNEL, SCHED_PATH_GROUPS, SCHED_ORDER_KERNEL, SCHED_COST_ORDERED, SCHED_CENSUS, SCHED_SPLIT = 1, 2, 4, 8, 16, 32
+SCHED_MEGAKERNEL, SCHED_PATH_GROUPS, SCHED_ORDER_KERNEL, SCHED_COST_ORDERED, SCHED_CENSUS, SCHED_SPLIT, SCHED_PARTS = \
+    1, 2, 4, 8, 16, 32, 64
 
 
 class BvhInfo(C.Structure):

@@ -59,6 +59,11 @@ struct DevBuf {
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
+// Depth-split schedule by frame size (DXRPT_OPT_MEGAKERNEL_SPLIT 2): frames of at least this many path
+// vertices (paths x (L - 1)); two concurrent parts up to kSplitPartsMaxPaths paths (DXRPT_OPT_SPLIT_PARTS 0).
+constexpr uint64_t kSplitMinVertices = 8000000;
+constexpr uint32_t kSplitPartsMaxPaths = 4000000;
+
 }  // namespace
 
 struct dxrpt_ctx {
@@ -117,11 +122,24 @@ struct dxrpt_ctx {
     uint32_t opt_bake_chunk = 1u << 21;     // DXRPT_OPT_BAKE_CHUNK (texels per bake launch)
     uint32_t opt_mega_persistent = 0;       // DXRPT_OPT_MEGAKERNEL_PERSISTENT (waves per CU, 0 = off)
     uint32_t opt_mega_lanes = 0;            // DXRPT_OPT_MEGAKERNEL_LANES (paths per megakernel wave, 0 = by size)
-    uint32_t opt_split = 0;                 // DXRPT_OPT_MEGAKERNEL_SPLIT (0 off, 1 on, 2 by frame size)
+    uint32_t opt_split = 2;                 // DXRPT_OPT_MEGAKERNEL_SPLIT (0 off, 1 on, 2 by frame size)
+    uint32_t opt_split_parts = 0;           // DXRPT_OPT_SPLIT_PARTS (0 = by frame size, 1, 2)
+    // split-schedule frame parts beyond the first (own queues, shadow slots, counters, stream)
+    struct FramePart {
+        DevBuf q[2][5], shorg, shdir, shcon, counters;
+        FrameBuffers fb;
+        uint32_t ctr_set = 0;
+        bool ctr_clean[2] = {false, false};
+        hipStream_t stream = nullptr;
+        hipEvent_t done = nullptr;
+    };
+    FramePart part[2];
+    hipEvent_t part_fork = nullptr;
+    std::vector<const uint32_t*> stat_counters;  // counter sets of the last frame (several with parts)
     uint32_t opt_tail_occ = 0;              // DXRPT_OPT_TAIL_OCCUPANCY (0 = the head's budget)
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
     int built_width = 0;
-    DevBuf d_trav;   // 4 x u64 traversal counters (DXRPT_OPT_COUNT_TRAVERSAL)
+    DevBuf d_trav;   // 5 x u64 census counters (DXRPT_OPT_COUNT_TRAVERSAL): node / triangle fetches, radiance hits
     uint32_t ctr_set = 0;                 // counter set of the next frame (f_counters holds two)
     bool ctr_clean[2] = {false, false};   // set known to be zero (zeroed by the previous megakernel frame)
     DevBuf d_wclock;  // 2 x u64 per wave (DXRPT_OPT_WAVE_CLOCKS)
@@ -172,6 +190,20 @@ struct dxrpt_ctx {
             (void)hipStreamDestroy(aux);
         }
         for (hipEvent_t e : fork_ev) (void)hipEventDestroy(e);
+        for (FramePart& fp : part) {
+            for (auto& qb : fp.q)
+                for (DevBuf& b : qb) b.release();
+            fp.shorg.release();
+            fp.shdir.release();
+            fp.shcon.release();
+            fp.counters.release();
+            if (fp.stream) {
+                (void)hipStreamSynchronize(fp.stream);
+                (void)hipStreamDestroy(fp.stream);
+            }
+            if (fp.done) (void)hipEventDestroy(fp.done);
+        }
+        if (part_fork) (void)hipEventDestroy(part_fork);
     }
 };
 
@@ -214,7 +246,9 @@ std::vector<float> make_lut() {
 
 // Device view of the scene for launches of up to `traversal_threads` global threads (sizes the
 // BVH8 stack spill slab, allocated only when the tree is deeper than the LDS part of the stack).
-SceneDev scene_dev(dxrpt_ctx* c, uint32_t traversal_threads) {
+// `slabs` concurrent launches (split-schedule frame parts) each get their own BVH8 stack-spill slab;
+// this SceneDev uses slab `slab`.
+SceneDev scene_dev(dxrpt_ctx* c, uint32_t traversal_threads, uint32_t slabs = 1, uint32_t slab = 0) {
     SceneDev s;
     s.nodes = c->d_nodes.as<BvhNode>();
     s.nodes8 = c->d_nodes8.as<Bvh8Node>();
@@ -224,8 +258,9 @@ SceneDev scene_dev(dxrpt_ctx* c, uint32_t traversal_threads) {
         s.num_nodes = c->bvh.num_nodes;
         s.stack_ints = 2u * std::min<uint32_t>(entries, uint32_t(kStackLds8));
         if (entries > uint32_t(kStackLds8)) {
-            c->d_spill.ensure(size_t(kTraversalStack8 - kStackLds8) * traversal_threads * sizeof(uint2));
-            s.spill8 = c->d_spill.as<uint2>();
+            const size_t per = size_t(kTraversalStack8 - kStackLds8) * traversal_threads;
+            c->d_spill.ensure(per * slabs * sizeof(uint2));
+            s.spill8 = c->d_spill.as<uint2>() + per * slab;
             s.spill_stride = traversal_threads;
         }
     } else {
@@ -317,6 +352,46 @@ void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
     f.sh_dir = c->f_shdir.as<float4>();
     f.sh_con = c->f_shcon.as<float4>();
     f.counters = c->f_counters.as<uint32_t>() + c->ctr_set * kCounterWords;
+    f.capacity = cap;
+    f.cap_r = cap_r;
+    f.qsize = uint32_t(qsize);
+    f.shadow_slots = sl;
+}
+
+// Buffers of split-schedule frame part k (queues, shadow slots, counters) for `paths` paths.
+void ensure_part(dxrpt_ctx* c, int k, uint32_t paths, uint32_t slots) {
+    dxrpt_ctx::FramePart& P = c->part[k];
+    FrameBuffers& f = P.fb;
+    if (!P.stream) {
+        HIP_CHECK(hipStreamCreateWithFlags(&P.stream, hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&P.done, hipEventDisableTiming));
+    }
+    if (!c->part_fork) HIP_CHECK(hipEventCreateWithFlags(&c->part_fork, hipEventDisableTiming));
+    if (paths <= f.capacity && slots <= f.shadow_slots && f.counters) return;
+    const uint32_t cap = std::max(paths, f.capacity);
+    const uint32_t sl = std::max(slots, std::max(f.shadow_slots, 2u));
+    const uint32_t cap_r = queue_shard_capacity(cap);
+    const size_t qsize = size_t(kQueueShards) * cap_r;
+    require(qsize * sl < (size_t(1) << 32), "frame too large for 32-bit shadow slot ids", DXRPT_E_INVALID_ARG);
+    for (int b = 0; b < 2; ++b) {
+        for (int i = 0; i < 4; ++i) P.q[b][i].ensure(qsize * 16);
+        P.q[b][4].ensure(qsize * 4);
+        f.q[b].org = P.q[b][0].as<float4>();
+        f.q[b].dir = P.q[b][1].as<float4>();
+        f.q[b].thr = P.q[b][2].as<float4>();
+        f.q[b].rad = P.q[b][3].as<float4>();
+        f.q[b].pix = P.q[b][4].as<uint32_t>();
+    }
+    P.shorg.ensure(qsize * sl * 16);
+    P.shdir.ensure(qsize * sl * 16);
+    P.shcon.ensure(qsize * sl * 16);
+    if (!P.counters.p) {
+        P.counters.ensure(2 * kCounterWords * sizeof(uint32_t));
+        P.ctr_clean[0] = P.ctr_clean[1] = false;
+    }
+    f.sh_org = P.shorg.as<float4>();
+    f.sh_dir = P.shdir.as<float4>();
+    f.sh_con = P.shcon.as<float4>();
     f.capacity = cap;
     f.cap_r = cap_r;
     f.qsize = uint32_t(qsize);
@@ -448,7 +523,7 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
     return guarded(ctx, [&] {
         if (option == DXRPT_OPT_COUNT_TRAVERSAL) {
             ctx->opt_count = value != 0;
-            if (ctx->opt_count) ctx->d_trav.ensure(4 * sizeof(unsigned long long));
+            if (ctx->opt_count) ctx->d_trav.ensure(5 * sizeof(unsigned long long));
         } else if (option == DXRPT_OPT_KERNEL_TIMING) {
             ctx->opt_timing = value != 0;
         } else if (option == DXRPT_OPT_TRAVERSAL_MODE) {
@@ -539,6 +614,9 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_MEGAKERNEL_SPLIT) {
             require(value <= 2, "dxrpt_set_option: megakernel split must be 0 (off), 1 (on) or 2 (by frame size)");
             ctx->opt_split = uint32_t(value);
+        } else if (option == DXRPT_OPT_SPLIT_PARTS) {
+            require(value <= 2, "dxrpt_set_option: split parts must be 0 (by frame size), 1 or 2");
+            ctx->opt_split_parts = uint32_t(value);
         } else if (option == DXRPT_OPT_TAIL_OCCUPANCY) {
             require(value == 0 || (value >= 4 && value <= 8), "dxrpt_set_option: tail occupancy must be 0 (by frame) or 4..8");
             ctx->opt_tail_occ = uint32_t(value);
@@ -852,15 +930,22 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
                                 : (paths > 600000u ? 7u : 4u);
         fp.mega_persistent = ctx->opt_mega_persistent;
         fp.mega_lanes = lanes;
-        // depth-split schedule (k_path_head + compacting k_path_tail): 64-lane path-ordered frames only
-        fp.split = ctx->opt_split == 1u ? 1u : 0u;
-        fp.tail_occupancy = ctx->opt_tail_occ ? ctx->opt_tail_occ : fp.megakernel_occupancy;
+        // depth-split schedule (k_path_head + one compacting k_path_tail per depth): 64-lane path-ordered
+        // frames.  By frame size (r03 A/B, profiles/r03_ab_msplit*.txt): it wins where there are many path
+        // vertices per frame (1080p L=8 6.90 -> 6.52 ms, 4K L=6 18.50 -> 17.04) and loses on short paths
+        // (1080p L=3 2.07 -> 2.23, L=4 3.09 -> 3.18; L=5 even), where each kernel's drain is a larger
+        // part of its time.  Budgets: head 6 waves/SIMD (80 VGPRs), tails 7 (72).
+        const bool split_by_size = vertices >= kSplitMinVertices && lanes == 64u;
+        fp.split = (ctx->opt_split == 1u || (ctx->opt_split == 2u && split_by_size)) && lanes == 64u && fp.megakernel ? 1u : 0u;
+        if (fp.split && !ctx->opt_mega_occ) fp.megakernel_occupancy = 6u;
+        fp.tail_occupancy = ctx->opt_tail_occ ? ctx->opt_tail_occ : (ctx->opt_mega_occ ? fp.megakernel_occupancy : 7u);
+        fp.path_base = 0;
         fp.num_cus = ctx->num_cus;
         hipStream_t s = static_cast<hipStream_t>(stream);
         ctx->wclock_waves = 0;  // set again below only by a frame that records stamps
         if (ctx->opt_count) {
             fp.trav = ctx->d_trav.as<unsigned long long>();
-            HIP_CHECK(hipMemsetAsync(fp.trav, 0, 4 * sizeof(unsigned long long), s));
+            HIP_CHECK(hipMemsetAsync(fp.trav, 0, 5 * sizeof(unsigned long long), s));
             if (ctx->opt_wave_clocks && fp.megakernel) {  // census: the 64-lane kernel, one slot per 64 paths
                 ctx->wclock_waves = (paths + 63u) / 64u;
                 ctx->d_wclock.ensure(size_t(ctx->wclock_waves) * 2 * sizeof(unsigned long long));
@@ -876,7 +961,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         bool order_pass = false;
         const uint32_t waves = lanes < 64u ? (paths + lanes - 1u) / lanes : (paths + 63u) / 64u;
         const uint64_t slots = uint64_t(ctx->num_cus) * 4u * fp.megakernel_occupancy;
-        const bool order_on = ctx->opt_wave_order == 1 || (ctx->opt_wave_order == 2 && waves <= 3u * slots);
+        const bool order_on = !fp.split && (ctx->opt_wave_order == 1 || (ctx->opt_wave_order == 2 && waves <= 3u * slots));
         const bool order_kernel = lanes < 64u || (fp.megakernel_occupancy >= 4u && fp.megakernel_occupancy <= 7u);
         if (order_on && order_kernel && fp.megakernel && !ctx->opt_count && !fp.mega_persistent && !ctx->opt_lds_nodes) {
             order_waves = waves;
@@ -937,7 +1022,42 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             aux = ctx->aux;
         }
         uint32_t sched = 0;
-        {   // counter sets: this frame's is fb.counters (read by dxrpt_get_stats); a megakernel frame zeroes
+        // split frames of at most kSplitPartsMaxPaths paths run as two concurrent parts (the top and the
+        // bottom half of the path slots, each with its own queues and counters, on two internal streams):
+        // one part's per-depth kernels fill the other's drains (1080p L=8 6.52 -> 5.91 ms; a 4K frame
+        // keeps one part: its kernels are long enough, 17.04 -> 17.15 with two)
+        const uint32_t nparts = !(fp.split && !ctx->opt_count && !fp.mega_persistent && !ctx->opt_lds_nodes) ? 1u
+                              : ctx->opt_split_parts ? ctx->opt_split_parts : (paths <= kSplitPartsMaxPaths ? 2u : 1u);
+        if (nparts == 2u && paths >= 128u) {
+            const uint32_t half = ((paths / 64u) / 2u) * 64u;  // a multiple of 64: parts keep whole 8x8 blocks
+            const uint32_t cnt[2] = {half, paths - half}, base[2] = {0u, half};
+            const uint32_t threads = frame_traversal_threads(paths, 2u + nl, 0);
+            if (ev) HIP_CHECK(hipEventRecord(ev[0], s));
+            HIP_CHECK(hipEventRecord(ctx->part_fork, s));
+            ctx->stat_counters.clear();
+            for (int k = 0; k < 2; ++k) {
+                ensure_part(ctx, k, cnt[k], 2u + nl);
+                dxrpt_ctx::FramePart& P = ctx->part[k];
+                const uint32_t cur = P.ctr_set;
+                uint32_t* cb = P.counters.as<uint32_t>();
+                P.fb.counters = cb + cur * kCounterWords;
+                P.fb.counters_clean = P.ctr_clean[cur];
+                P.fb.counters_next = cb + (1u - cur) * kCounterWords;
+                FrameParams fk = fp;
+                fk.num_paths = cnt[k];
+                fk.path_base = base[k];
+                HIP_CHECK(hipStreamWaitEvent(P.stream, ctx->part_fork, 0));
+                HIP_CHECK(launch_split_part(scene_dev(ctx, threads, 2u, uint32_t(k)), P.fb, fk, P.stream));
+                HIP_CHECK(hipEventRecord(P.done, P.stream));
+                HIP_CHECK(hipStreamWaitEvent(s, P.done, 0));
+                P.ctr_clean[cur] = false;
+                P.ctr_clean[1u - cur] = true;
+                P.ctr_set = 1u - cur;
+                ctx->stat_counters.push_back(P.fb.counters);
+            }
+            if (ev) HIP_CHECK(hipEventRecord(ev[1], s));
+            sched = DXRPT_SCHED_MEGAKERNEL | DXRPT_SCHED_SPLIT | DXRPT_SCHED_PARTS;
+        } else {   // counter sets: this frame's is fb.counters (read by dxrpt_get_stats); a megakernel frame zeroes
             // the other one in-kernel, so the next frame skips the fill launch
             uint32_t* base = ctx->f_counters.as<uint32_t>();
             const uint32_t cur = ctx->ctr_set;
@@ -952,6 +1072,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             }
             ctx->fb.counters_next = nullptr;
             ctx->fb.counters_clean = false;
+            ctx->stat_counters.assign(1, ctx->fb.counters);
         }
         if (order_waves) ++ctx->order_frame;
         if (order_waves && order_pass) {  // the next frames' order from this frame's wave classes (after the frame events)
@@ -981,10 +1102,12 @@ int dxrpt_get_stats(dxrpt_ctx* ctx, dxrpt_stats* out) {
         require(ctx->rendered, "dxrpt_get_stats: nothing rendered yet", DXRPT_E_STATE);
         HIP_CHECK(hipStreamSynchronize(ctx->last_stream));
         uint32_t shards[2 * kMaxDepthQueues * kQueueShards];
-        HIP_CHECK(hipMemcpy(shards, ctx->fb.counters, sizeof(shards), hipMemcpyDeviceToHost));
         uint32_t cnt[2 * kMaxDepthQueues] = {};
-        for (uint32_t q = 0; q < 2 * kMaxDepthQueues; ++q)
-            for (uint32_t k = 0; k < kQueueShards; ++k) cnt[q] += shards[q * kQueueShards + k];
+        for (const uint32_t* set : ctx->stat_counters) {  // one counter set per frame part
+            HIP_CHECK(hipMemcpy(shards, set, sizeof(shards), hipMemcpyDeviceToHost));
+            for (uint32_t q = 0; q < 2 * kMaxDepthQueues; ++q)
+                for (uint32_t k = 0; k < kQueueShards; ++k) cnt[q] += shards[q * kQueueShards + k];
+        }
         dxrpt_stats s = ctx->last;
         for (int d = 1; d < ctx->last_L && d < int(DXRPT_MAX_PATH_LENGTH); ++d) {
             s.radiance_rays_per_depth[d] = cnt[d];
@@ -993,8 +1116,9 @@ int dxrpt_get_stats(dxrpt_ctx* ctx, dxrpt_stats* out) {
             s.shadow_rays += cnt[16 + d];
         }
         if (ctx->opt_count && ctx->d_trav.p) {
-            unsigned long long tr[4];
+            unsigned long long tr[5];
             HIP_CHECK(hipMemcpy(tr, ctx->d_trav.p, sizeof(tr), hipMemcpyDeviceToHost));
+            s.radiance_hits = (s.schedule & DXRPT_SCHED_CENSUS) ? tr[4] : 0u;  // the megakernel census counts hits
             s.node_visits_radiance = tr[0];
             s.tri_tests_radiance = tr[1];
             s.node_visits_shadow = tr[2];
@@ -1142,6 +1266,7 @@ int dxrpt_bake_lightmap(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, co
         ctx->fb.counters_next = nullptr;
         HIP_CHECK(hipMemsetAsync(ctx->fb.counters, 0, kCounterWords * sizeof(uint32_t), s));
         ctx->ctr_clean[ctx->ctr_set] = false;
+        ctx->stat_counters.assign(1, ctx->fb.counters);
         // the live count stays on the device (no host sync): launches cover every texel, and chunks
         // past the live count exit at once
         for (uint32_t first = 0; first < total; first += chunk) {

@@ -169,6 +169,9 @@ struct FrameParams {
     // tail_occupancy: the tails' register budget (waves/SIMD).
     uint32_t split;
     uint32_t tail_occupancy;
+    // Split-schedule frame parts (launch_split_part): this part traces the frame's path slots
+    // [path_base, path_base + num_paths) (path_base a multiple of 64); 0 otherwise.
+    uint32_t path_base;
 };
 
 constexpr uint32_t kWaveClasses = 256;
@@ -187,6 +190,12 @@ inline int frame_event_count(int L) { return 2 * (2 + 4 * (L - 1)); }
 // `cursor_next` (the next frame's).  Order within a class is unspecified: it only schedules.
 hipError_t launch_wave_order(const uint32_t* cls, const uint32_t* hist, uint32_t* cursor, uint32_t* hist_next,
                              uint32_t* cursor_next, uint32_t* order, uint32_t n, hipStream_t stream);
+
+// One part of a depth-split frame (FrameParams::path_base / num_paths) on its own stream: zeroes the
+// part's counters unless fb.counters_clean, then k_path_head and the k_path_tail launches.  Parts of
+// one frame run concurrently on separate streams with separate FrameBuffers (queues, shadow slots,
+// counters) and SceneDev::spill8 slabs.
+hipError_t launch_split_part(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream);
 
 // *sched_out (if non-null) receives the DXRPT_SCHED_* bits of the schedule launched.
 hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream,

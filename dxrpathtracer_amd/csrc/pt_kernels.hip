@@ -828,7 +828,9 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
     uint32_t sbase = 0, sword = 0;  // stack entry j in lane j
     uint32_t sp = 0;
     uint32_t node = 0;
-    const bool full = DXRPT_PACKET_VCHUNK && __ballot(1) == ~0ull;  // every lane loads its chunk dword
+#if DXRPT_PACKET_VCHUNK
+    const bool full = __ballot(1) == ~0ull;  // every lane loads its chunk dword
+#endif
 #if DXRPT_PACKET_PREFETCH
     Node8Words W = load_node8_uniform(S, 0u);
 #endif
@@ -1963,7 +1965,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
     const float tmin1 = kBake ? 0.0001f : 0.0f;
     const bool isDiffuse1 = kBake;
     const uint32_t packet = kBake ? 0u : packet_mask;
-    uint32_t unused[4] = {0u, 0u, 0u, 0u};
+    uint32_t unused[5] = {0u, 0u, 0u, 0u, 0u};
     if (!kCount) cnt = unused;
     f3 thr = f3{1.0f, 1.0f, 1.0f};
     float payloadRoughness = 0.0f;
@@ -1979,6 +1981,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
             traverse<8, false, kCount, DXRPT_MEGA_PIPE_CH>(A.S, org, dir, d == 1 ? tmin1 : kRayTMin, tmax, d <= set.MaxAnyHitPathLength, stk, h,
                                        cnt[0], cnt[1], nc);
         phase_mark(pa, d == 1 ? 0 : d == 2 ? 3 : 6);
+        if (kCount && h.tri != kMiss) ++cnt[4];  // radiance hits: the vertices PathTrace shades
         VertexIn V;
         V.inOrigin = org;
         V.inDir = dir;
@@ -2382,6 +2385,140 @@ PT_DEV void camera_path_group(const KArgs& A, uint32_t p, lds_int* stk, bool mem
     if (member0) accumulate_pixel(A, pr.accumIdx, rad);
 }
 
+// A vertex's shadow rays (ShadowHit/Miss/AnyHit, RayTrace.hlsl:497-507, 532-542) walked slot by slot by
+// the wave, contribution * visibility added to rad in slot order -- trace_path's walk (the depth-1 sun
+// rays of a full wave through the packet traversal, packet bit 1).
+PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh, bool sun0, uint32_t packet,
+                           float4& rad) {
+    uint32_t nv = 0, nt = 0;
+    for (uint32_t k = 0; __ballot(k < nsh) != 0ull; ++k) {
+        const bool live = k < nsh;
+        const size_t slot = size_t(k) * A.F.qsize + slot_p;
+        float4 o4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d4 = make_float4(0.0f, 0.0f, 1.0f, 0.0f), c4 = o4;
+        if (live) {
+            o4 = A.F.sh_org[slot];
+            d4 = A.F.sh_dir[slot];
+            c4 = A.F.sh_con[slot];
+        }
+        HitRec hs;
+        bool occluded = false;
+        const bool pk = d == 1 && k == 0 && (packet & 2u);
+        if (pk)
+            occluded = traverse8_packet<true, false>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live && sun0, hs);
+        if (live && !(pk && sun0))
+            occluded = traverse<8, true, false>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, nullptr, hs, nv, nt);
+        if (live) {
+            rad.x += occluded ? c4.x * 0.0f : c4.x;
+            rad.y += occluded ? c4.y * 0.0f : c4.y;
+            rad.z += occluded ? c4.z * 0.0f : c4.z;
+        }
+    }
+}
+
+// DXRPT_MEGA_STAGE: k_path's camera path with the path state kept in memory instead of registers across
+// the traversals -- the split schedule's staging inside the single kernel.  FrameBuffers::q[0] at the
+// path slot p (unused by megakernel frames) holds the continuation: org (origin, bits(accumulation
+// index)), dir (direction, bits(CMJ pattern)), thr (throughput, payload Roughness), rad (radiance so
+// far, bits(payload IsDiffuse)).  The continuation is stored before the vertex's shadow rays are
+// traced (only the radiance sum is live across them) and re-read after the next closest-hit traversal
+// (only the ray and p are live across it).  Same arithmetic in the same order as trace_path.
+#ifndef DXRPT_MEGA_STAGE
+#define DXRPT_MEGA_STAGE 0
+#endif
+PT_DEV void camera_path_staged(const KArgs& A, uint32_t p) {
+    const dxrpt_app_settings& set = A.P.set;
+    const RayQueue& Q = A.F.q[0];
+    const int L = set.MaxPathLength < 2 ? 2 : set.MaxPathLength;
+    bool cont;
+    bool nextDiffuse;
+    float4 rad;
+    {   // depth 1: RaygenShader's ray, packet traversals while the wave is full
+        const PrimaryRay pr = primary_ray(A, p);
+        const uint32_t packet = (p | 63u) < A.P.num_paths ? A.P.packet : 0u;
+        count_rays(A.F.counters + 1u * kQueueShards, 1u);
+        HitRec h;
+        uint32_t nv = 0, nt = 0;
+        if (packet & 1u)
+            traverse8_packet<false, false>(A.S, pr.start, pr.dir, 0.0f, pr.length, 1 <= set.MaxAnyHitPathLength, true, h);
+        else
+            traverse<8, false, false>(A.S, pr.start, pr.dir, 0.0f, pr.length, 1 <= set.MaxAnyHitPathLength, nullptr, h, nv, nt);
+        VertexIn V;
+        V.inOrigin = pr.start;
+        V.inDir = pr.dir;
+        V.pathThr = f3{1.0f, 1.0f, 1.0f};
+        V.payloadRoughness = 0.0f;
+        V.payloadIsDiffuse = false;
+        V.pix = pr.pixelIdx;
+        V.hit = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
+        VertexOut O;
+        uint32_t nsh = 0;
+        bool sun0 = false;
+        path_vertex(A, 1, V, [&](int kind, f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
+            sun0 |= kind == kShadowSun || !DXRPT_SUN0_CHECK;
+            emit_shadow(A, p, nsh, o, dd, tmn, tmx, c, fo);
+        }, O);
+        count_rays(A.F.counters + (kMaxDepthQueues + 1u) * kQueueShards, nsh);
+        cont = O.cont;
+        nextDiffuse = O.nextIsDiffuse;
+        if (cont) {
+            Q.org[p] = make_float4(O.nextOrigin.x, O.nextOrigin.y, O.nextOrigin.z, bitsf(pr.accumIdx));
+            Q.dir[p] = make_float4(O.nextDir.x, O.nextDir.y, O.nextDir.z, bitsf(pr.pixelIdx));
+            Q.thr[p] = make_float4(O.nextThr.x, O.nextThr.y, O.nextThr.z, O.nextRoughness);
+        }
+        rad = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        rad.x += 1.0f * O.local.x;
+        rad.y += 1.0f * O.local.y;
+        rad.z += 1.0f * O.local.z;
+        vertex_shadows(A, 1, p, nsh, sun0, packet, rad);
+        if (!cont) {
+            accumulate_pixel(A, pr.accumIdx, rad);
+            return;
+        }
+    }
+    for (int d = 2; d <= L - 1; ++d) {
+        Q.rad[p] = make_float4(rad.x, rad.y, rad.z, bitsf(nextDiffuse ? 1u : 0u));
+        count_rays(A.F.counters + uint32_t(d) * kQueueShards, 1u);
+        HitRec h;
+        {
+            const float4 o4 = Q.org[p], d4 = Q.dir[p];
+            uint32_t nv = 0, nt = 0;
+            traverse<8, false, false>(A.S, ld3(o4), ld3(d4), kRayTMin, kFP32Max, d <= set.MaxAnyHitPathLength, nullptr, h, nv, nt);
+        }
+        const float4 o4 = Q.org[p], d4 = Q.dir[p], t4 = Q.thr[p], r4 = Q.rad[p];
+        const uint32_t accumIdx = fbits(o4.w);
+        VertexIn V;
+        V.inOrigin = ld3(o4);
+        V.inDir = ld3(d4);
+        V.pathThr = ld3(t4);
+        V.payloadRoughness = t4.w;
+        V.payloadIsDiffuse = (fbits(r4.w) & 1u) != 0u;
+        V.pix = fbits(d4.w);
+        V.hit = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
+        VertexOut O;
+        uint32_t nsh = 0;
+        path_vertex(A, d, V, [&](int, f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
+            emit_shadow(A, p, nsh, o, dd, tmn, tmx, c, fo);
+        }, O);
+        count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, nsh);
+        cont = O.cont;
+        nextDiffuse = O.nextIsDiffuse;
+        if (cont) {
+            Q.org[p] = make_float4(O.nextOrigin.x, O.nextOrigin.y, O.nextOrigin.z, bitsf(accumIdx));
+            Q.dir[p] = make_float4(O.nextDir.x, O.nextDir.y, O.nextDir.z, d4.w);
+            Q.thr[p] = make_float4(O.nextThr.x, O.nextThr.y, O.nextThr.z, O.nextRoughness);
+        }
+        rad = make_float4(r4.x, r4.y, r4.z, 0.0f);
+        rad.x += V.pathThr.x * O.local.x;
+        rad.y += V.pathThr.y * O.local.y;
+        rad.z += V.pathThr.z * O.local.z;
+        vertex_shadows(A, d, p, nsh, false, 0u, rad);
+        if (!cont) {
+            accumulate_pixel(A, accumIdx, rad);
+            return;
+        }
+    }
+}
+
 // Cost-ordered dispatch (FrameParams::wave_order / wave_cost): the hardware starts waves in launch order,
 // so a frame ends with the waves started last; running the costliest wave slots (last frame's
 // durations: the image changes little between progressive frames) first leaves short ones for the
@@ -2527,7 +2664,10 @@ void k_path(KArgs A) {
     if (!kPersistent && !kLds && !kCount && kOrder) {
         const WaveSlot ws = wave_slot(A);
         const uint32_t p = (ws.slot << 6) | (threadIdx.x & 63u);
-        if (p < A.P.num_paths) camera_path(A, p, stk);
+        if (p < A.P.num_paths) {
+            if (DXRPT_MEGA_STAGE) camera_path_staged(A, p);
+            else camera_path(A, p, stk);
+        }
         wave_slot_done(A, ws);
         return;
     }
@@ -2541,7 +2681,7 @@ void k_path(KArgs A) {
         }
         if (kCount) {  // census (DXRPT_OPT_COUNT_TRAVERSAL): wave sums, one 64-bit atomic per counter per wave
             const unsigned long long t0 = A.P.wave_clock ? __builtin_amdgcn_s_memrealtime() : 0ull;
-            uint32_t cnt[4] = {0u, 0u, 0u, 0u};
+            uint32_t cnt[5] = {0u, 0u, 0u, 0u, 0u};
             if (p < A.P.num_paths) camera_path<true>(A, p, stk, NodeCache{nullptr, 0u}, cnt);
             if (A.P.wave_clock && (threadIdx.x & 63u) == 0u && p < A.P.num_paths) {  // vector stores from lane 0
                 const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
@@ -2549,7 +2689,7 @@ void k_path(KArgs A) {
                 A.P.wave_clock[2 * (p >> 6) + 1] = t1;
             }
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < 5; ++k) {
                 uint32_t v = cnt[k];
                 for (int off = 32; off > 0; off >>= 1) v += uint32_t(__shfl_xor(int(v), off));
                 if ((threadIdx.x & 63u) == 0u) atomicAdd(&A.P.trav[k], (unsigned long long)v);
@@ -2567,11 +2707,15 @@ void k_path(KArgs A) {
             // run t of XCD x is chunk 8 t + (x + t) mod 8: the XCDs' chunks rotate from run to run, so no
             // XCD keeps the same screen columns (a fixed deal makes stripes of unequal cost)
             const uint32_t q = xcd_position(blockIdx.x, gridDim.x, A.P.xcd_chunk) * blockDim.x + threadIdx.x;
-            if (q < A.P.num_paths) camera_path(A, q, stk);
+            if (q < A.P.num_paths) {
+                if (DXRPT_MEGA_STAGE) camera_path_staged(A, q);
+                else camera_path(A, q, stk);
+            }
             return;
         }
         if (p >= A.P.num_paths) return;
-        camera_path(A, p, stk);
+        if (DXRPT_MEGA_STAGE) camera_path_staged(A, p);
+        else camera_path(A, p, stk);
         return;
     }
     uint32_t* work = A.F.counters + 2 * kMaxDepthQueues * kQueueShards;
@@ -2601,36 +2745,6 @@ void k_path(KArgs A) {
 //   org (origin xyz, FP32Max)   dir (direction xyz, bits(accumulation index))
 //   thr (throughput rgb, payload Roughness)   rad (radiance so far, bits(payload IsDiffuse))   pix (CMJ pattern)
 // The queued count of depth d is that depth's radiance-ray count (dxrpt_get_stats).
-
-// A vertex's shadow rays (ShadowHit/Miss/AnyHit, RayTrace.hlsl:497-507, 532-542) walked slot by slot by
-// the wave, contribution * visibility added to rad in slot order -- trace_path's walk (the depth-1 sun
-// rays of a full wave through the packet traversal, packet bit 1).
-PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh, bool sun0, uint32_t packet,
-                           float4& rad) {
-    uint32_t nv = 0, nt = 0;
-    for (uint32_t k = 0; __ballot(k < nsh) != 0ull; ++k) {
-        const bool live = k < nsh;
-        const size_t slot = size_t(k) * A.F.qsize + slot_p;
-        float4 o4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d4 = make_float4(0.0f, 0.0f, 1.0f, 0.0f), c4 = o4;
-        if (live) {
-            o4 = A.F.sh_org[slot];
-            d4 = A.F.sh_dir[slot];
-            c4 = A.F.sh_con[slot];
-        }
-        HitRec hs;
-        bool occluded = false;
-        const bool pk = d == 1 && k == 0 && (packet & 2u);
-        if (pk)
-            occluded = traverse8_packet<true, false>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live && sun0, hs);
-        if (live && !(pk && sun0))
-            occluded = traverse<8, true, false>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, nullptr, hs, nv, nt);
-        if (live) {
-            rad.x += occluded ? c4.x * 0.0f : c4.x;
-            rad.y += occluded ? c4.y * 0.0f : c4.y;
-            rad.z += occluded ? c4.z * 0.0f : c4.z;
-        }
-    }
-}
 
 // Queues the continuation of a vertex (all active lanes must call; `cont` selects) into queue d + 1;
 // returns its position.  The radiance word is written later (split_finish), after the shadow rays.
@@ -2669,10 +2783,10 @@ void k_path_head(KArgs A) {
         for (uint32_t i = threadIdx.x; i < kCounterWords; i += blockDim.x) A.F.counters_next[i] = 0u;
     lut_fill(A.S);
     const uint32_t blk = A.P.xcd_chunk ? xcd_position(blockIdx.x, gridDim.x, A.P.xcd_chunk) : blockIdx.x;
-    const uint32_t p = blk * blockDim.x + threadIdx.x;
+    const uint32_t p = blk * blockDim.x + threadIdx.x;  // path slot within this launch (shadow-slot index)
     if (p >= A.P.num_paths) return;
     const dxrpt_app_settings& set = A.P.set;
-    const PrimaryRay pr = primary_ray(A, p);
+    const PrimaryRay pr = primary_ray(A, A.P.path_base + p);
     const uint32_t packet = (p | 63u) < A.P.num_paths ? A.P.packet : 0u;
     count_rays(A.F.counters + 1u * kQueueShards, 1u);
     HitRec h;
@@ -2903,6 +3017,18 @@ static void launch_split(const KArgs& A, uint32_t gm, size_t lds, hipStream_t s)
             default: launch_tail<4>(A, gm, lds, s, d); break;
         }
     }
+}
+
+hipError_t launch_split_part(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream) {
+    if (!fb.counters_clean) {
+        const hipError_t e = hipMemsetAsync(fb.counters, 0, kCounterWords * sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+    }
+    if (fp.num_paths == 0) return hipSuccess;
+    KArgs A{scene, fb, fp};
+    const size_t lds = size_t(scene.stack_ints) * 64u * sizeof(int);
+    launch_split(A, (fp.num_paths + 63u) / 64u, lds, stream);
+    return hipGetLastError();
 }
 
 hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream,

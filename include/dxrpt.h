@@ -219,6 +219,9 @@ typedef struct dxrpt_stats {
     uint32_t paths_per_wave;
     uint32_t occupancy;
     uint32_t pad;
+    /* DXRPT_OPT_COUNT_TRAVERSAL on a megakernel frame: radiance rays that hit a triangle (the vertices
+       PathTrace shades); the other radiance rays ran MissShader.  0 otherwise. */
+    uint64_t radiance_hits;
 } dxrpt_stats;
 #define DXRPT_SCHED_MEGAKERNEL 1u    /* k_path (or the split head/tail kernels): no wavefront passes */
 #define DXRPT_SCHED_PATH_GROUPS 2u   /* several lanes per path (paths_per_wave < 64) */
@@ -226,6 +229,7 @@ typedef struct dxrpt_stats {
 #define DXRPT_SCHED_COST_ORDERED 8u  /* ... and started the waves in a cost order built by earlier frames */
 #define DXRPT_SCHED_CENSUS 16u       /* the counting (DXRPT_OPT_COUNT_TRAVERSAL) instantiation */
 #define DXRPT_SCHED_SPLIT 32u        /* depth-split megakernel: k_path_head then compacted k_path_tail */
+#define DXRPT_SCHED_PARTS 64u        /* ... as two concurrent halves of the frame's paths */
 
 /* BVH summary (dxrpt_get_bvh_info). */
 typedef struct dxrpt_bvh_info {
@@ -377,10 +381,15 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                           path, then per further depth one kernel runs the surviving paths,
                                           compacted into full waves (wave64 ballot, one atomic per wave),
                                           with the path state in the queue instead of registers and its own
-                                          register budget.  0: the single k_path.  2: by frame size.
+                                          register budget.  0: the single k_path.  2 (default): by frame
+                                          size -- frames of >= 8M path vertices (paths x (L-1)).
                                           Identical results. */
+#define DXRPT_OPT_SPLIT_PARTS 35u      /* split frames as this many concurrent parts (halves of the path slots,
+                                          each with its own queues on an internal stream): 0 = by frame size
+                                          (default: 2 up to 4M paths, else 1), 1 or 2.  Identical results. */
 #define DXRPT_OPT_TAIL_OCCUPANCY 34u   /* register budget of the split schedule's tail kernels in waves/SIMD:
-                                          0 = the head's (default), 4..8 */
+                                          0 = by default 7 (the head's 6, or DXRPT_OPT_MEGAKERNEL_OCCUPANCY
+                                          when set), 4..8 */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

@@ -21,14 +21,23 @@ def main():
     ap.add_argument("--parts", default="1,2,3,4")
     ap.add_argument("--shards", default="", help="also time rank 0's band share of an N-way split, e.g. 2,4,8")
     ap.add_argument("--share-parts", default="2,4", help="rank 0's share split into k concurrent parts")
+    ap.add_argument("--config", default="metric", choices=["metric", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--msplit", type=int, default=None, help="DXRPT_OPT_MEGAKERNEL_SPLIT for every context")
+    ap.add_argument("--occ", type=int, default=None)
+    ap.add_argument("--tail-occ", type=int, default=None)
+    ap.add_argument("--wave-order", type=int, default=None)
+    ap.add_argument("--part-layout", default="bands", choices=["bands", "halves"],
+                    help="parts = interleaved 8-row bands, or contiguous row ranges")
     args = ap.parse_args()
     import torch
     import dxrpathtracer_amd as D
     from dxrpathtracer_amd.distributed import band_layout
     from dxrpathtracer_amd.tracer import DXRPathTracer
 
-    W, H, L = 1920, 1080, 3
-    sc = D.Scene("sponza")
+    import dxrpathtracer_amd._abi as A
+    name, W, H, L = {"metric": ("sponza", 1920, 1080, 3), "c2": ("sponza", 1280, 720, 3), "c3": ("sponza", 1920, 1080, 8),
+                     "c4": ("suntemple", 1920, 1080, 3), "c5": ("sponza", 3840, 2160, 6)}[args.config]
+    sc = D.Scene(name)
     st = sc.settings(MaxPathLength=L)
     sky = D.make_sky(st)
     lights = D.make_lights(sc)
@@ -37,6 +46,10 @@ def main():
     tracers = []
     for _ in range(kmax):
         t = DXRPathTracer(0)
+        for opt, v in ((A.OPT_MEGAKERNEL_SPLIT, args.msplit), (A.OPT_MEGAKERNEL_OCCUPANCY, args.occ),
+                       (A.OPT_TAIL_OCCUPANCY, args.tail_occ), (A.OPT_WAVE_ORDER, args.wave_order)):
+            if v is not None:
+                t.set_option(opt, v)
         t.initialize_scene(sc, sky)
         t.build_rt_acceleration_structure()
         tracers.append(t)
@@ -46,6 +59,10 @@ def main():
     for rnd in range(args.rounds):
         for k in (int(x) for x in args.parts.split(",")):
             lay = band_layout(W, H, k)
+            if args.part_layout == "halves" and k > 1:  # contiguous row ranges (multiples of 8 rows)
+                rows = [((H // 8) * r // k) * 8 for r in range(k)] + [H]
+                lay.tiles = [[A.Tile(0, rows[r], W, rows[r + 1] - rows[r], 0, W, 0)] for r in range(k)]
+                lay.counts = [W * (rows[r + 1] - rows[r]) for r in range(k)]
             accs = [torch.zeros((max(1, lay.counts[r]), 4), dtype=torch.float32, device="cuda") for r in range(k)]
 
             def frame(f):
@@ -69,7 +86,7 @@ def main():
             torch.cuda.synchronize()
             res.setdefault(k, []).append((time.perf_counter() - t0) / args.frames * 1e3)
     for k, v in res.items():
-        print(f"parts {k}: ms/frame " + " ".join(f"{x:.3f}" for x in v) + f"  min {min(v):.3f}")
+        print(f"{args.config} {args.part_layout} msplit={args.msplit} occ={args.occ}/{args.tail_occ} order={args.wave_order} parts {k}: ms/frame " + " ".join(f"{x:.3f}" for x in v) + f"  min {min(v):.3f}")
     # one rank's share of an N-GPU frame (what each GPU renders at N GPUs, before the gather)
     for n in (int(x) for x in args.shards.split(",") if x):
         lay = band_layout(W, H, n)

@@ -14,7 +14,7 @@ import os
 import sys
 from collections import defaultdict
 
-CONFIG = "sponza-proxy 1920x1080 L=3"
+CONFIG = os.environ.get("PMC_CONFIG", "sponza-proxy 1920x1080 L=3")
 
 
 def short(name):
@@ -103,8 +103,48 @@ def main(prof, rnd):
                                                if cands else {}),
                        "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 16-B/lane read correction) + WRITE_SIZE KiB x1024"},
                       f, indent=2)
+    # per FRAME of the megakernel schedule (k_path, or the split schedule's k_path_head + k_path_tail per
+    # depth): counters summed over every megakernel launch (the census frame's counting k_path excluded)
+    # and divided by the frames (launches of the frame's first kernel)
+    fam = [k for k in out["kernels"] if k.startswith(("k_path<", "k_path_head<", "k_path_tail<"))
+           and not (k.startswith("k_path<") and k[k.index("<") + 1:-1].split(", ")[4:5] == ["true"])]
+    firsts = [k for k in fam if k.startswith(("k_path<", "k_path_head<"))]
+    frames = sum(out["kernels"][k].get("calls", 0) for k in firsts)
+    if fam and frames:
+        tot = defaultdict(float)
+        ms = 0.0
+        for k in fam:
+            e = out["kernels"][k]
+            n = e.get("calls", 0)
+            ms += e.get("total_ms", 0.0)
+            for c, v in e["pmc"].items():
+                tot[c] += v * n
+        pf = {c: v / frames for c, v in tot.items()}
+        fr = {"config": CONFIG, "kernels": sorted(fam), "frames": frames, "ms_per_frame": ms / frames,
+              "per_kernel": {k: {"calls": out["kernels"][k].get("calls"), "avg_ms": out["kernels"][k].get("avg_ms")}
+                             for k in fam},
+              "counters_per_frame": pf,
+              "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 16-B/lane read correction) + WRITE_SIZE KiB x1024"}
+        if "FETCH_SIZE" in pf and "WRITE_SIZE" in pf:
+            fr["hbm_read_bytes_raw"] = pf["FETCH_SIZE"] * 1024
+            fr["hbm_write_bytes"] = pf["WRITE_SIZE"] * 1024
+            fr["hbm_bytes_per_frame"] = pf["FETCH_SIZE"] * 1024 * 2 + pf["WRITE_SIZE"] * 1024
+        if pf.get("SQ_WAVE_CYCLES"):
+            fr["wait_any_per_wave_cycle"] = pf.get("SQ_WAIT_ANY", 0.0) / pf["SQ_WAVE_CYCLES"]
+            fr["active_inst_any_per_wave_cycle"] = pf.get("SQ_ACTIVE_INST_ANY", 0.0) / pf["SQ_WAVE_CYCLES"]
+        if pf.get("SQ_ACTIVE_INST_VALU"):
+            fr["valu_lane_utilisation"] = pf.get("SQ_THREAD_CYCLES_VALU", 0.0) / (pf["SQ_ACTIVE_INST_VALU"] * 64.0)
+        if pf.get("TCC_HIT_sum", 0) + pf.get("TCC_MISS_sum", 0) > 0:
+            fr["l2_hit_rate"] = pf["TCC_HIT_sum"] / (pf["TCC_HIT_sum"] + pf["TCC_MISS_sum"])
+        tag = os.environ.get("PMC_CONFIG_TAG", "metric")
+        with open(f"profiles/{rnd}_pmc_frame_{tag}.json", "w") as f:
+            json.dump(fr, f, indent=2)
+        print(f"per frame ({tag}): {fr['ms_per_frame']:.4f} ms, HBM {fr.get('hbm_bytes_per_frame', 0) / 1e9:.3f} GB "
+              f"(writes {fr.get('hbm_write_bytes', 0) / 1e9:.3f}), L2 hit {fr.get('l2_hit_rate', 0):.3f}, "
+              f"wait {fr.get('wait_any_per_wave_cycle', 0):.3f}, lanes {fr.get('valu_lane_utilisation', 0):.3f}")
     for src in ("kt/run_kernel_stats.csv",):
-        with open(os.path.join(prof, src)) as f, open(f"profiles/{rnd}_kernel_stats.csv", "w") as g:
+        tag = os.environ.get("PMC_CONFIG_TAG", "metric")
+        with open(os.path.join(prof, src)) as f, open(f"profiles/{rnd}_kernel_stats{'' if tag == 'metric' else '_' + tag}.csv", "w") as g:
             g.write(f.read())
     for k, e in out["kernels"].items():
         print(f"{k:26s} calls {e.get('calls', 0):4d} avg {e.get('avg_ms', 0):8.4f} ms  "

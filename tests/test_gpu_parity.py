@@ -649,14 +649,16 @@ def test_xcd_chunk_mapping_is_bit_identical(torch_cuda, name, W, H):
         t.set_option(A.OPT_XCD_CHUNK, A.DEFAULT_XCD_CHUNK)
 
 
-@pytest.mark.parametrize("name,L,W,H,occ,tocc", [
-    ("sponza", 3, 352, 200, 7, 7), ("sponza", 8, 352, 200, 5, 6), ("suntemple", 3, 320, 180, 6, 5),
-    ("boxtest", 5, 100, 50, 4, 8), ("sponza", 6, 100, 50, 8, 4), ("whitefurnace", 3, 128, 128, 7, 7)])
-def test_megakernel_split_is_bit_identical(torch_cuda, name, L, W, H, occ, tocc):
+@pytest.mark.parametrize("name,L,W,H,occ,tocc,parts", [
+    ("sponza", 3, 352, 200, 7, 7, 1), ("sponza", 8, 352, 200, 5, 6, 2), ("suntemple", 3, 320, 180, 6, 5, 2),
+    ("boxtest", 5, 100, 50, 4, 8, 2), ("sponza", 6, 100, 50, 8, 4, 1), ("whitefurnace", 3, 128, 128, 7, 7, 2),
+    ("sponza", 8, 97, 61, 6, 7, 2)])
+def test_megakernel_split_is_bit_identical(torch_cuda, name, L, W, H, occ, tocc, parts):
     # DXRPT_OPT_MEGAKERNEL_SPLIT: one kernel per depth with the surviving paths compacted between depths
     # (wave64 ballot, one atomic per wave) and the path state carried in the queue -- the frame and the
     # ray counts per depth must equal the wavefront frame's, on full frames (partial last waves at 100 x
-    # 50), on a band share, with 3 spot lights (BoxTest) and alpha-tested any hit (SunTemple)
+    # 50 and 97 x 61), on a band share, with 3 spot lights (BoxTest) and alpha-tested any hit (SunTemple);
+    # DXRPT_OPT_SPLIT_PARTS 2: the frame's path slots as two concurrent halves on two internal streams
     torch = torch_cuda
     sc, sky = scene_bundle(name)
     st = sc.settings(MaxPathLength=L)
@@ -677,16 +679,19 @@ def test_megakernel_split_is_bit_identical(torch_cuda, name, L, W, H, occ, tocc)
             t.set_option(A.OPT_MEGAKERNEL_SPLIT, 1)
             t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, occ)
             t.set_option(A.OPT_TAIL_OCCUPANCY, tocc)
+            t.set_option(A.OPT_SPLIT_PARTS, parts)
             got = gpu_render(torch, name, W, H, st, 4, tiles=tiles, n_out=n, accum=acc0.clone(), rtc=rtc,
                              lights=lights).cpu().numpy()
             s_got = t.stats()
             assert s_got.schedule & A.SCHED_SPLIT, s_got.schedule
+            assert bool(s_got.schedule & A.SCHED_PARTS) == (parts == 2), s_got.schedule
             np.testing.assert_array_equal(got, ref)
             assert list(s_got.radiance_rays_per_depth) == list(s_ref.radiance_rays_per_depth)
             assert list(s_got.shadow_rays_per_depth) == list(s_ref.shadow_rays_per_depth)
     finally:
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
         t.set_option(A.OPT_MEGAKERNEL_SPLIT, A.DEFAULT_MEGAKERNEL_SPLIT)
+        t.set_option(A.OPT_SPLIT_PARTS, A.DEFAULT_SPLIT_PARTS)
         t.set_option(A.OPT_TAIL_OCCUPANCY, A.DEFAULT_TAIL_OCCUPANCY)
         t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, A.DEFAULT_MEGAKERNEL_OCCUPANCY)
         t.set_option(A.OPT_MEGAKERNEL_LANES, A.DEFAULT_MEGAKERNEL_LANES)

@@ -52,7 +52,7 @@ SKY = {"sponza": (992, 0, 160, 24)}
 
 
 def render_shipped(torch, name, W, H, L, sample, prefill=0.0, tiles=None, n_out=None, check_kernel=None,
-                   mega_paths=None):
+                   mega_paths=None, sched=None):
     sc, sky = scene_bundle(name)
     st = sc.settings(MaxPathLength=L)
     rtc = D.make_constants(sc, st, sky, W, H, sample)
@@ -60,12 +60,12 @@ def render_shipped(torch, name, W, H, L, sample, prefill=0.0, tiles=None, n_out=
     if mega_paths is not None:
         t.set_option(A.OPT_MEGAKERNEL_PATHS, mega_paths)
     try:
-        return _render_shipped(torch, t, sc, st, rtc, W, H, prefill, tiles, n_out, check_kernel)
+        return _render_shipped(torch, t, sc, st, rtc, W, H, prefill, tiles, n_out, check_kernel, sched)
     finally:
         t.set_option(A.OPT_MEGAKERNEL_PATHS, A.DEFAULT_MEGAKERNEL_PATHS)
 
 
-def _render_shipped(torch, t, sc, st, rtc, W, H, prefill, tiles, n_out, check_kernel):
+def _render_shipped(torch, t, sc, st, rtc, W, H, prefill, tiles, n_out, check_kernel, sched=None):
     n = W * H if n_out is None else n_out
     init = torch.full((n, 4), prefill, dtype=torch.float32, device="cuda")
     acc = init.clone()
@@ -73,6 +73,9 @@ def _render_shipped(torch, t, sc, st, rtc, W, H, prefill, tiles, n_out, check_ke
     t.render_raw(rtc, st, acc.data_ptr(), W, H, tiles=tiles, stream=stream, lights=D.make_lights(sc))
     torch.cuda.synchronize()
     out = acc.cpu().numpy()
+    if sched is not None:  # the DXRPT_SCHED_* bits the shipped defaults must pick for this frame
+        got = t.stats().schedule
+        assert got & sched == sched, f"schedule {got}, expected bits {sched}"
     if check_kernel is not None:
         # which schedule ran: kernel timing only brackets launches (the frame must come out identical)
         acc2 = init.clone()
@@ -108,7 +111,8 @@ def compare_crops(name, W, H, out, st, rtc, crops, prefill, what, origin=None):
 def test_metric_frame_1080p_L3(torch_cuda, sample, prefill):
     # BASELINE.json metric: Sponza(-proxy) 1920x1080 MaxPathLength 3, the bench's kernel configuration
     W, H = 1920, 1080
-    out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 3, sample, prefill, check_kernel="megakernel")
+    out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 3, sample, prefill, check_kernel="megakernel",
+                                  sched=A.SCHED_MEGAKERNEL)
     assert np.isfinite(out).all() and (out[:, 3] == 1.0).all()
     compare_crops("sponza", W, H, out, st, rtc, frame_crops(W, H, [SKY["sponza"]]), prefill, f"metric s{sample}")
 
@@ -129,10 +133,21 @@ def test_sponza_720p_L3(torch_cuda):
 
 
 def test_sponza_1080p_L8(torch_cuda):
-    # BASELINE.json configs[2]: 2.07M paths x 7 vertices, the default megakernel schedule
+    # BASELINE.json configs[2]: 2.07M paths x 7 vertices, the default schedule: the depth-split megakernel
+    # (head + one compacting tail per depth) as two concurrent halves of the frame
     W, H = 1920, 1080
-    out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 8, 15, 0.125, check_kernel="megakernel")
+    out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 8, 15, 0.125, check_kernel="megakernel",
+                                  sched=A.SCHED_MEGAKERNEL | A.SCHED_SPLIT | A.SCHED_PARTS)
     compare_crops("sponza", W, H, out, st, rtc, frame_crops(W, H), 0.125, "C3 s15")
+
+
+def test_sponza_4k_L6(torch_cuda):
+    # BASELINE.json configs[4] on one GPU: 8.3M paths x 5 vertices, the depth-split megakernel (one part)
+    W, H = 3840, 2160
+    out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 6, 2, 0.0, check_kernel="megakernel",
+                                  sched=A.SCHED_MEGAKERNEL | A.SCHED_SPLIT)
+    assert not (rtc is None)
+    compare_crops("sponza", W, H, out, st, rtc, frame_crops(W, H, [(1900, 1000, 64, 64)]), 0.0, "C5 4K L6")
 
 
 def test_sponza_1080p_L8_wavefront(torch_cuda):

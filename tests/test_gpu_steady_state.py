@@ -120,6 +120,8 @@ def test_c3_1080p_L8_sixteen_samples(torch_cuda):
     crops = [((x0, y0, 48, 48), y0 * W + x0, W) for (x0, y0) in ((0, 0), (936, 516), (1500, 880), (300, 1032))]
 
     def check(f, s):
+        # 2.07M paths x 7 vertices: the depth-split schedule as two concurrent halves (default by frame size)
         assert s.schedule & A.SCHED_MEGAKERNEL and s.paths_per_wave == 64, (f, s.schedule, s.paths_per_wave)
+        assert s.schedule & A.SCHED_SPLIT and s.schedule & A.SCHED_PARTS, (f, s.schedule)
 
     _steady_frames(torch_cuda, "sponza", W, H, 8, 16, crops, expect=check)
