@@ -228,7 +228,7 @@ def main():
     setup_s = time.perf_counter() - t0
     lights = D.make_lights(scene)
     lay = screen_layout(WIDTH, HEIGHT, world, args.layout)
-    tiles = lay.rank_tiles(rank) if world > 1 else None
+    tiles = lay.tile_array(rank) if world > 1 else None
     n_local = lay.counts[rank] if world > 1 else WIDTH * HEIGHT
     accum = torch.zeros((max(lay.max_count, n_local), 4), dtype=torch.float32, device="cuda")
     full = idx = None

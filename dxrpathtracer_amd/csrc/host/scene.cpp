@@ -3,6 +3,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <dlfcn.h>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -13,7 +14,21 @@ namespace dxrpt_host {
 
 namespace {
 thread_local std::string g_last_error;
+// Packaged-asset directory (dxrpt_host_set_asset_dir); unset, it defaults to ../data next to this
+// library (dxrpathtracer_amd/lib/libdxrpt_host.so -> dxrpathtracer_amd/data).
+std::mutex g_asset_mutex;
 std::string g_asset_dir;
+bool g_asset_dir_set = false;
+
+std::string default_asset_dir() {
+    Dl_info info{};
+    if (dladdr(reinterpret_cast<void*>(&dxrpt_host_set_asset_dir), &info) && info.dli_fname) {
+        std::string lib = info.dli_fname;
+        const size_t slash = lib.find_last_of('/');
+        return (slash == std::string::npos ? std::string(".") : lib.substr(0, slash)) + "/../data";
+    }
+    return std::string();
+}
 
 struct SceneStore {
     dxrpt_host_scene pub{};
@@ -333,7 +348,14 @@ void publish(SceneStore& St, uint32_t scene_id, uint64_t seed, bool idx16) {
 }
 }  // namespace
 
-const std::string& asset_dir() { return g_asset_dir; }
+std::string asset_dir() {
+    std::lock_guard<std::mutex> lock(g_asset_mutex);
+    if (!g_asset_dir_set) {
+        g_asset_dir = default_asset_dir();
+        g_asset_dir_set = true;
+    }
+    return g_asset_dir;
+}
 
 }  // namespace dxrpt_host
 
@@ -345,7 +367,9 @@ const char* dxrpt_host_last_error(void) { return g_last_error.c_str(); }
 
 int dxrpt_host_set_asset_dir(const char* dir) {
     if (!dir) return DXRPT_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lock(g_asset_mutex);
     g_asset_dir = dir;
+    g_asset_dir_set = true;
     return DXRPT_OK;
 }
 
@@ -394,9 +418,12 @@ int dxrpt_host_scene_create(uint32_t scene_id, uint64_t seed, uint32_t detail, d
         publish(*S, scene_id, seed, scene_id == DXRPT_SCENE_BOXTEST);
         *out = &S.release()->pub;
         return DXRPT_OK;
-    } catch (const std::exception& e) {
-        g_last_error = e.what();
+    } catch (const std::bad_alloc&) {
+        g_last_error = "dxrpt_host_scene_create: out of memory";
         return DXRPT_E_OOM;
+    } catch (const std::exception& e) {  // e.g. a packaged asset that cannot be read
+        g_last_error = e.what();
+        return DXRPT_E_INVALID_ARG;
     }
 }
 

@@ -140,7 +140,7 @@ bool load_jpeg(const std::string& path, bool srgb, Texture& tex, std::string& er
 bool load_image(const std::string& path, bool srgb, Texture& tex, std::string& err);  // by file signature
 
 // Packaged assets (dxrpt_host_set_asset_dir): the directory holding suntemple/*.r8z.
-const std::string& asset_dir();
+std::string asset_dir();
 // An R8 image stored as "DXR8", u32 width, u32 height, zlib stream of width*height bytes.
 bool load_r8z(const std::string& path, Texture& tex, std::string& err);
 

@@ -39,10 +39,11 @@ uint32_t add_pbr_asset_opacity(SceneBuilder& B, Pattern p, uint64_t seed, uint32
     MaterialTextures t = make_material_textures(p, seed, size, r, g, b, rough, metal, false);
     Texture op;
     std::string err;
-    const std::string path = asset_dir() + "/suntemple/" + file;
-    if (asset_dir().empty() || !load_r8z(path, op, err))
+    const std::string dir = asset_dir();
+    const std::string path = dir + "/suntemple/" + file;
+    if (dir.empty() || !load_r8z(path, op, err))
         throw std::runtime_error("SunTemple proxy: cannot load the packaged opacity map " + path +
-                                 " (dxrpt_host_set_asset_dir -> dxrpathtracer_amd/data): " + err);
+                                 " (default: ../data next to libdxrpt_host.so; dxrpt_host_set_asset_dir overrides): " + err);
     uint32_t ia = B.add_texture(std::move(t.albedo));
     uint32_t in = B.add_texture(std::move(t.normal));
     uint32_t ir = B.add_texture(std::move(t.roughness));

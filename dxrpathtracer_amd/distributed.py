@@ -34,6 +34,15 @@ class BandLayout:
     def rank_tiles(self, rank: int):
         return self.tiles[rank]
 
+    def tile_array(self, rank: int):
+        """Rank `rank`'s tiles as a ctypes Tile array, built once per layout and rank (DXRPathTracer.render_raw
+        passes it to dxrpt_render without re-marshalling).  Layouts are not edited after construction."""
+        cache = self.__dict__.setdefault("_arrays", {})
+        if rank not in cache:
+            t = self.tiles[rank]
+            cache[rank] = (A.Tile * len(t))(*t)
+        return cache[rank]
+
 
 def band_layout(width: int, height: int, world: int, band: int = BAND_ROWS) -> BandLayout:
     tiles = [[] for _ in range(world)]

@@ -99,16 +99,15 @@ class DXRPathTracer:
     def render_raw(self, rtc: A.RayTraceConstants, settings: A.AppSettings, accum_ptr: int, width: int,
                    height: int, tiles=None, stream: int = 0, lights: A.LightConstants | None = None):
         tarr, nt = None, 0
-        if tiles:
-            # the ctypes tile array is rebuilt only when a different tile list is passed (an N-GPU block
-            # partition has thousands of tiles; marshalling them every frame would starve the GPU)
-            key = (id(tiles), len(tiles))
-            if getattr(self, "_tiles_key", None) != key or getattr(self, "_tiles_ref", None) is not tiles:
-                arr = (A.Tile * len(tiles))()
-                for i, t in enumerate(tiles):
-                    arr[i] = t if isinstance(t, A.Tile) else A.Tile(*t)
-                self._tiles_key, self._tiles_ref, self._tiles_arr = key, tiles, arr
-            tarr, nt = self._tiles_arr, len(tiles)
+        if isinstance(tiles, C.Array):
+            # a ctypes Tile array built once by the caller (BandLayout.tile_array: an N-GPU block partition
+            # has thousands of tiles, marshalling them every frame would starve the GPU)
+            tarr, nt = tiles, len(tiles)
+        elif tiles:  # a list of Tile / tuples: marshalled on every call, so later edits to it are seen
+            tarr = (A.Tile * len(tiles))()
+            for i, t in enumerate(tiles):
+                tarr[i] = t if isinstance(t, A.Tile) else A.Tile(*t)
+            nt = len(tiles)
         lp = C.byref(lights) if lights is not None else None
         self._check(self._L.dxrpt_render(self._ctx, C.byref(rtc), C.byref(settings), lp, C.c_void_p(accum_ptr),
                                          width, height, tarr, nt, C.c_void_p(stream)), "dxrpt_render")

@@ -161,7 +161,9 @@ void dxrpt_host_texture_free(dxrpt_host_texture* tex);
 
 /* Directory of the packaged assets (dxrpathtracer_amd/data): the SunTemple proxy's foliage opacity
  * maps (suntemple/NAME.r8z, decoded from the reference's BC4 files by scripts/make_suntemple_opacity.py).
- * dxrpathtracer_amd.scene sets it on import. */
+ * Default: ../data next to libdxrpt_host.so (the package layout), so a C/C++ caller needs no call;
+ * dxrpathtracer_amd.scene sets it on import.  Thread-safe.  A scene that needs a missing asset fails
+ * dxrpt_host_scene_create with DXRPT_E_INVALID_ARG and the path in dxrpt_host_last_error. */
 int dxrpt_host_set_asset_dir(const char* dir);
 
 /* IEEE binary16 <-> binary32 (round to nearest even), used for the cube texels. */

@@ -98,6 +98,7 @@ def main():
         order = np.argsort(-(wc[:, 1] - wc[:, 0]), kind="stable")  # wave w of the full frame = block w
         tiles = [AA.Tile(int(b % bw) * 8, int(b // bw) * 8, 8, 8, 64 * k, 8, 0) for k, b in enumerate(order)]
         n = 64 * len(tiles)
+        tiles = (AA.Tile * len(tiles))(*tiles)
     elif args.layout == "blocks-raster":  # the whole frame as 8x8 block tiles in raster order (tile-count A/B)
         from dxrpathtracer_amd import _abi as AA
         tiles = [AA.Tile(x, y, 8, 8, (y // 8 * (W // 8) + x // 8) * 64, 8, 0) for y in range(0, H, 8) for x in range(0, W, 8)]
@@ -105,11 +106,12 @@ def main():
             tiles = tiles[args.rank::args.share]
             tiles = [AA.Tile(t.x0, t.y0, 8, 8, 64 * k, 8, 0) for k, t in enumerate(tiles)]
         n = 64 * len(tiles)
+        tiles = (AA.Tile * len(tiles))(*tiles)
     elif args.share > 1:
         from dxrpathtracer_amd.distributed import band_layout
         lay = (band_layout(W, H, args.share, args.band) if args.layout == "bands" and args.band
                else screen_layout(W, H, args.share, args.layout))
-        tiles, n = lay.rank_tiles(args.rank), lay.counts[args.rank]
+        tiles, n = lay.tile_array(args.rank), lay.counts[args.rank]
     acc = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
     consts = [D.make_constants(sc, st, sky, W, H, s) for s in range(16)]
     lights = D.make_lights(sc)

@@ -147,3 +147,21 @@ def test_block_partition_covers_image_and_spreads_rows():
     for r in range(8):
         rows = {t.y0 // 8 for t in lay.rank_tiles(r)}
         assert len(rows) >= 0.95 * 135
+
+
+def test_tile_array_matches_rank_tiles():
+    # BandLayout.tile_array: the ctypes array render_raw passes straight to dxrpt_render (built once)
+    from dxrpathtracer_amd.distributed import band_layout, block_layout, gathered_tiles
+    for lay in (band_layout(1920, 1080, 8), block_layout(333, 187, 3)):
+        for r in range(lay.world):
+            arr = lay.tile_array(r)
+            assert arr is lay.tile_array(r)
+            got = [(t.x0, t.y0, t.w, t.h, t.accum_offset, t.accum_pitch) for t in arr]
+            want = [(t.x0, t.y0, t.w, t.h, t.accum_offset, t.accum_pitch) for t in lay.rank_tiles(r)]
+            assert got == want
+        # dxrpt_unpermute's list: every rank's tiles, offsets moved to the rank's slab in the gathered buffer
+        gt = gathered_tiles(lay)
+        assert len(gt) == sum(len(lay.rank_tiles(r)) for r in range(lay.world))
+        assert sum(t.w * t.h for t in gt) == lay.width * lay.height
+        ends = sorted((t.accum_offset, t.accum_offset + t.h * t.accum_pitch) for t in gt)
+        assert ends[0][0] == 0 and all(a[1] <= b[0] for a, b in zip(ends, ends[1:]))

@@ -124,3 +124,26 @@ def test_band_layout_covers_every_pixel_once(world):
     for r in range(world):
         owned = sum(t.w * t.h for t in lay.tiles[r])
         assert owned == lay.counts[r]
+
+
+def test_asset_dir_defaults_next_to_the_library():
+    # a C caller that never calls dxrpt_host_set_asset_dir still finds the packaged SunTemple opacity
+    # maps (../data next to libdxrpt_host.so); a missing asset is an argument/IO error, not "out of memory"
+    import subprocess
+    import sys
+    code = r"""
+import ctypes as C, os, sys
+lib = C.CDLL(os.path.join(sys.argv[1], "libdxrpt_host.so"))
+lib.dxrpt_host_last_error.restype = C.c_char_p
+out = C.c_void_p()
+rc = lib.dxrpt_host_scene_create(1, C.c_uint64(0), 1, C.byref(out))   # DXRPT_SCENE_SUNTEMPLE, small detail
+assert rc == 0, (rc, lib.dxrpt_host_last_error())
+lib.dxrpt_host_scene_destroy(out)
+assert lib.dxrpt_host_set_asset_dir(b"/nonexistent") == 0
+rc = lib.dxrpt_host_scene_create(1, C.c_uint64(0), 1, C.byref(out))
+assert rc == -1 and b"opacity map" in lib.dxrpt_host_last_error(), (rc, lib.dxrpt_host_last_error())
+print("ok")
+"""
+    import dxrpathtracer_amd._abi as A
+    r = subprocess.run([sys.executable, "-c", code, A.LIB_DIR], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr
