@@ -157,7 +157,7 @@ DXRPT_SYMBOLS = ("dxrpt_abi_version", "dxrpt_default_settings", "dxrpt_create", 
                  "dxrpt_set_scene", "dxrpt_add_texture", "dxrpt_set_sky", "dxrpt_build_bvh", "dxrpt_get_bvh_info",
                  "dxrpt_render", "dxrpt_get_stats", "dxrpt_trace_rays", "dxrpt_set_option", "dxrpt_reset_timing",
                  "dxrpt_post_process", "dxrpt_bake_lightmap", "dxrpt_denoise_median", "dxrpt_get_wave_clocks",
-                 "dxrpt_get_phase_clocks", "dxrpt_sample_cmj", "dxrpt_comm_unique_id", "dxrpt_comm_create",
+                 "dxrpt_get_phase_clocks", "dxrpt_sample_cmj", "dxrpt_render_aov", "dxrpt_comm_unique_id", "dxrpt_comm_create",
                  "dxrpt_comm_destroy", "dxrpt_gather_slabs", "dxrpt_unpermute", "dxrpt_multi_last_error")
 DXRPT_HOST_SYMBOLS = ("dxrpt_host_scene_create", "dxrpt_host_scene_load", "dxrpt_host_scene_destroy", "dxrpt_host_last_error",
                       "dxrpt_host_inv_view_projection", "dxrpt_host_sky_create", "dxrpt_host_fill_constants",
@@ -213,6 +213,8 @@ def lib() -> C.CDLL:
         L.dxrpt_denoise_median.argtypes = [P, P, P, u32, u32, P]
         L.dxrpt_reset_timing.argtypes = [P]
         L.dxrpt_sample_cmj.argtypes = [P, P, u32, P, P]
+        L.dxrpt_render_aov.argtypes = [P, C.POINTER(RayTraceConstants), C.POINTER(AppSettings), P, u32, u32,
+                                       C.POINTER(Tile), u32, P]
         L.dxrpt_comm_unique_id.argtypes = [P]
         L.dxrpt_comm_create.argtypes = [C.c_int, C.c_int, C.c_int, P, C.POINTER(P)]
         L.dxrpt_comm_destroy.argtypes = [P]

@@ -811,6 +811,69 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info) {
     return DXRPT_OK;
 }
 
+// The call's tile list (NULL: the full frame) validated and uploaded with its pixel prefix sums (only when it
+// changed); returns the number of paths (pixels).
+uint32_t prepare_tiles(dxrpt_ctx* ctx, const dxrpt_tile* tiles, uint32_t num_tiles, uint32_t width, uint32_t height,
+                       const char* who) {
+    std::vector<dxrpt_tile> tl;
+    if (!tiles || num_tiles == 0) {
+        dxrpt_tile t{};
+        t.x0 = 0; t.y0 = 0; t.w = width; t.h = height; t.accum_offset = 0; t.accum_pitch = width;
+        tl.push_back(t);
+    } else {
+        tl.assign(tiles, tiles + num_tiles);
+    }
+    std::vector<uint32_t> prefix(tl.size() + 1, 0);
+    uint64_t total = 0;
+    for (size_t k = 0; k < tl.size(); ++k) {
+        const dxrpt_tile& t = tl[k];
+        require(t.w > 0 && t.h > 0 && uint64_t(t.x0) + t.w <= width && uint64_t(t.y0) + t.h <= height,
+                std::string(who) + ": tile " + std::to_string(k) + " outside the image");
+        require(t.accum_pitch >= t.w, std::string(who) + ": tile accum_pitch < width");
+        require(t.accum_offset + uint64_t(t.h - 1) * t.accum_pitch + t.w <= 0xFFFFFFFFull,
+                std::string(who) + ": accumulation index exceeds 32 bits");
+        prefix[k] = uint32_t(total);
+        total += uint64_t(t.w) * t.h;
+        require(total < 0x7FFFFFFFull, std::string(who) + ": too many pixels in one call");
+    }
+    prefix[tl.size()] = uint32_t(total);
+    if (tl.size() != ctx->tiles_cache.size() || std::memcmp(tl.data(), ctx->tiles_cache.data(), tl.size() * sizeof(dxrpt_tile)) != 0) {
+        ctx->d_tiles.upload(tl.data(), tl.size() * sizeof(dxrpt_tile));
+        ctx->d_tile_prefix.upload(prefix.data(), prefix.size() * sizeof(uint32_t));
+        ctx->tiles_cache = tl;
+        ++ctx->tiles_gen;
+    }
+    return uint32_t(total);
+}
+
+int dxrpt_render_aov(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxrpt_app_settings* settings, float* out,
+                     uint32_t width, uint32_t height, const dxrpt_tile* tiles, uint32_t num_tiles, void* stream) {
+    if (!ctx) return DXRPT_E_INVALID_ARG;
+    return guarded(ctx, [&] {
+        require(ctx->bvh_built, "dxrpt_render_aov: acceleration structure not built", DXRPT_E_STATE);
+        require(ctx->built_width == 8, "dxrpt_render_aov: needs the BVH8 layout", DXRPT_E_UNSUPPORTED);
+        require(rtc && settings && out, "dxrpt_render_aov: null argument");
+        require(width > 0 && height > 0, "dxrpt_render_aov: empty image");
+        require(uint64_t(width) * height == rtc->TotalNumPixels, "dxrpt_render_aov: TotalNumPixels != width*height");
+        require(settings->SqrtNumSamples >= 1, "dxrpt_render_aov: SqrtNumSamples must be >= 1");
+        upload_textures(ctx);
+        const uint32_t paths = prepare_tiles(ctx, tiles, num_tiles, width, height, "dxrpt_render_aov");
+        FrameParams fp{};
+        fp.rtc = *rtc;
+        fp.set = *settings;
+        fp.tiles = ctx->d_tiles.as<dxrpt_tile>();
+        fp.tile_prefix = ctx->d_tile_prefix.as<uint32_t>();
+        fp.accum = reinterpret_cast<float4*>(out);
+        fp.num_tiles = uint32_t(ctx->tiles_cache.size());
+        fp.num_paths = paths;
+        fp.width = width;
+        fp.height = height;
+        fp.packet = ctx->opt_packet;
+        HIP_CHECK(launch_primary_aov(scene_dev(ctx, ((paths + 255u) / 256u) * 256u), ctx->fb, fp,
+                                     static_cast<hipStream_t>(stream)));
+    });
+}
+
 int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxrpt_app_settings* settings,
                  const dxrpt_light_constants* lights, float* accum, uint32_t width, uint32_t height,
                  const dxrpt_tile* tiles, uint32_t num_tiles, void* stream) {
@@ -833,35 +896,8 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
                         (m.Opacity == DXRPT_INVALID_INDEX || m.Opacity < nt),
                     "dxrpt_render: material references a texture that was not added");
         }
-        std::vector<dxrpt_tile> tl;
-        if (!tiles || num_tiles == 0) {
-            dxrpt_tile t{};
-            t.x0 = 0; t.y0 = 0; t.w = width; t.h = height; t.accum_offset = 0; t.accum_pitch = width;
-            tl.push_back(t);
-        } else {
-            tl.assign(tiles, tiles + num_tiles);
-        }
-        std::vector<uint32_t> prefix(tl.size() + 1, 0);
-        uint64_t total = 0;
-        for (size_t k = 0; k < tl.size(); ++k) {
-            const dxrpt_tile& t = tl[k];
-            require(t.w > 0 && t.h > 0 && uint64_t(t.x0) + t.w <= width && uint64_t(t.y0) + t.h <= height,
-                    "dxrpt_render: tile " + std::to_string(k) + " outside the image");
-            require(t.accum_pitch >= t.w, "dxrpt_render: tile accum_pitch < width");
-            require(t.accum_offset + uint64_t(t.h - 1) * t.accum_pitch + t.w <= 0xFFFFFFFFull,
-                    "dxrpt_render: accumulation index exceeds 32 bits");
-            prefix[k] = uint32_t(total);
-            total += uint64_t(t.w) * t.h;
-            require(total < 0x7FFFFFFFull, "dxrpt_render: too many pixels in one call");
-        }
-        prefix[tl.size()] = uint32_t(total);
-        const uint32_t paths = uint32_t(total);
-        if (tl.size() != ctx->tiles_cache.size() || std::memcmp(tl.data(), ctx->tiles_cache.data(), tl.size() * sizeof(dxrpt_tile)) != 0) {
-            ctx->d_tiles.upload(tl.data(), tl.size() * sizeof(dxrpt_tile));
-            ctx->d_tile_prefix.upload(prefix.data(), prefix.size() * sizeof(uint32_t));
-            ctx->tiles_cache = tl;
-            ++ctx->tiles_gen;
-        }
+        const uint32_t paths = prepare_tiles(ctx, tiles, num_tiles, width, height, "dxrpt_render");
+        const std::vector<dxrpt_tile>& tl = ctx->tiles_cache;
         uint32_t nl = useLights ? rtc->NumLights : 0u;
         if (nl) {
             std::vector<dxrpt_spot_light> L(lights->Lights, lights->Lights + nl);
@@ -1032,11 +1068,11 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             const uint32_t half = ((paths / 64u) / 2u) * 64u;  // a multiple of 64: parts keep whole 8x8 blocks
             const uint32_t cnt[2] = {half, paths - half}, base[2] = {0u, half};
             const uint32_t threads = frame_traversal_threads(paths, 2u + nl, 0);
+            for (int k = 0; k < 2; ++k) ensure_part(ctx, k, cnt[k], 2u + nl);  // (creates the streams and events)
             if (ev) HIP_CHECK(hipEventRecord(ev[0], s));
             HIP_CHECK(hipEventRecord(ctx->part_fork, s));
             ctx->stat_counters.clear();
             for (int k = 0; k < 2; ++k) {
-                ensure_part(ctx, k, cnt[k], 2u + nl);
                 dxrpt_ctx::FramePart& P = ctx->part[k];
                 const uint32_t cur = P.ctr_set;
                 uint32_t* cb = P.counters.as<uint32_t>();

@@ -232,6 +232,9 @@ hipError_t launch_trace_rays(const SceneDev& scene, const float4* rays, uint32_t
 uint32_t frame_traversal_threads(uint32_t num_paths, uint32_t shadow_slots, uint32_t chunks_per_wave);
 uint32_t trace_rays_threads(uint32_t n);
 
+// Primary-only AOV of the frame's tiles into fp.accum (one float4 per path slot's accumulation index).
+hipError_t launch_primary_aov(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream);
+
 // SampleCMJ2D on device cases (x = sampleIdx, y = numSamplesX, z = numSamplesY, w = pattern) -> out.
 hipError_t launch_sample_cmj(const uint4* cases, uint32_t n, float2* out, hipStream_t stream);
 

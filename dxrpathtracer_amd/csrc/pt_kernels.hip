@@ -3286,6 +3286,46 @@ hipError_t launch_trace_rays(const SceneDev& scene, const float4* rays, uint32_t
     return hipGetLastError();
 }
 
+// Primary-only AOV (SURVEY.md 8(d), C1 plumbing): RaygenShader's ray for path slot p (the tiles of the
+// call), its closest hit (packet traversal on full waves, as k_path's depth 1), and the albedo tap
+// PathTrace takes at the hit (RayTrace.hlsl:180-183); out[accumIdx] = (albedo rgb, 1) on a hit, 0 on a
+// miss.  No shading, no accumulation: a debug view of the ray-generation / traversal / surface plumbing.
+__global__ __launch_bounds__(64) void k_primary_aov(KArgs A) {
+    lut_fill(A.S);
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= A.P.num_paths) return;
+    const PrimaryRay pr = primary_ray(A, p);
+    HitRec h;
+    uint32_t nv = 0, nt = 0;
+    const bool alpha = 1 <= A.P.set.MaxAnyHitPathLength;
+    if ((p | 63u) < A.P.num_paths && (A.P.packet & 1u))
+        traverse8_packet<false, false>(A.S, pr.start, pr.dir, 0.0f, pr.length, alpha, true, h);
+    else
+        traverse<8, false, false>(A.S, pr.start, pr.dir, 0.0f, pr.length, alpha, nullptr, h, nv, nt);
+    float4 out = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (h.tri != kMiss) {
+        out.w = 1.0f;
+        if (A.P.set.EnableAlbedoMaps && !A.P.set.EnableWhiteFurnaceMode) {
+            const Surface surf = get_hit_surface(A.S, h.tri, h.b1, h.b2);
+            const Texel4 a = sample_tex_desc(A.S, tex_desc(A.S.geoshade[h.geom].albedo), surf.u, surf.v);
+            out.x = a.r;
+            out.y = a.g;
+            out.z = a.b;
+        } else {
+            out.x = out.y = out.z = 1.0f;
+        }
+    }
+    A.P.accum[pr.accumIdx] = out;
+}
+
+hipError_t launch_primary_aov(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream) {
+    if (fp.num_paths == 0) return hipSuccess;
+    KArgs A{scene, fb, fp};
+    const size_t lds = size_t(scene.stack_ints) * 64u * sizeof(int);
+    hipLaunchKernelGGL(k_primary_aov, dim3((fp.num_paths + 63u) / 64u), dim3(64), lds, stream, A);
+    return hipGetLastError();
+}
+
 // SampleCMJ2D (Sampling.hlsl:322-331) on arbitrary (sampleIdx, numSamplesX, numSamplesY, pattern) cases.
 __global__ __launch_bounds__(kBlock) void k_sample_cmj(const uint4* cases, uint32_t n, float2* out) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;

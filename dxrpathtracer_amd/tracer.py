@@ -112,6 +112,16 @@ class DXRPathTracer:
         self._check(self._L.dxrpt_render(self._ctx, C.byref(rtc), C.byref(settings), lp, C.c_void_p(accum_ptr),
                                          width, height, tarr, nt, C.c_void_p(stream)), "dxrpt_render")
 
+    def render_aov(self, rtc: A.RayTraceConstants, settings: A.AppSettings, out_ptr: int, width: int, height: int,
+                   tiles=None, stream: int = 0):
+        """Primary-only AOV (dxrpt_render_aov): (albedo rgb, 1) at each pixel's primary hit, 0 on a miss."""
+        tarr, nt = None, 0
+        if tiles:
+            tarr = tiles if isinstance(tiles, C.Array) else (A.Tile * len(tiles))(*[t if isinstance(t, A.Tile) else A.Tile(*t) for t in tiles])
+            nt = len(tiles)
+        self._check(self._L.dxrpt_render_aov(self._ctx, C.byref(rtc), C.byref(settings), C.c_void_p(out_ptr), width,
+                                             height, tarr, nt, C.c_void_p(stream)), "dxrpt_render_aov")
+
     def set_option(self, option: int, value: int):
         self._check(self._L.dxrpt_set_option(self._ctx, option, value), "dxrpt_set_option")
 

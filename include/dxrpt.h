@@ -405,6 +405,13 @@ int dxrpt_render(dxrpt_ctx* ctx,
                  float* accum, uint32_t width, uint32_t height,
                  const dxrpt_tile* tiles, uint32_t num_tiles,
                  void* stream);
+/* Primary-only AOV (debug plumbing): for every pixel of `tiles` (NULL: the full frame;
+ * addressing as dxrpt_render), RaygenShader's primary ray (CMJ set 0 of rtc->CurrSampleIdx), its closest
+ * hit (alpha-tested iff MaxAnyHitPathLength >= 1) and the albedo PathTrace takes there
+ * (RayTrace.hlsl:180-183): out = (albedo rgb, 1) on a hit, (0, 0, 0, 0) on a miss.  Overwrites `out`
+ * (device float4), no accumulation.  Stream-ordered. */
+int dxrpt_render_aov(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxrpt_app_settings* settings, float* out,
+                     uint32_t width, uint32_t height, const dxrpt_tile* tiles, uint32_t num_tiles, void* stream);
 /* ---- post-processing (the consumer of the accumulation buffer) --------------------------------
  * PostProcessor::Render (DXRPathTracer/PostProcessor.cpp:43-92, PostProcessing.hlsl): half-res bloom
  * (2x2 gather, 2 x separable 14-tap Gaussian in RGBA16F), exposure 2^Exposure / FP16Scale and the

@@ -819,6 +819,46 @@ void TraceRadiance(const Ctx& C, F3 o, F3 d, float tmin, float tmax, bool forceO
     }
 }
 
+// The primary-only AOV of pixel (x, y) (SURVEY.md 8(d), C1 plumbing): RaygenShader's ray (92-126), its
+// closest hit, and the hit surface's albedo tap as PathTrace takes it (RayTrace.hlsl:180-183: the
+// albedo map when EnableAlbedoMaps and not furnace, else 1); out = (albedo rgb, 1) on a hit, 0 on a miss.
+void PrimaryAov(const Ctx& C, uint32_t x, uint32_t y, uint32_t W, uint32_t H, float out[4]) {
+    const uint32_t pixelIdx = y * W + x;
+    uint32_t sampleSetIdx = 0;
+    float s[2];
+    SamplePoint(C, pixelIdx, sampleSetIdx, s);
+    float rx = float(x) + s[0], ry = float(y) + s[1];
+    float ncx = rx / (float(W) * 0.5f) - 1.0f, ncy = ry / (float(H) * 0.5f) - 1.0f;
+    ncy *= -1.0f;
+    const float* M = C.rtc.InvViewProjection;
+    float a[4], b[4];
+    for (int j = 0; j < 4; ++j) {
+        a[j] = ((ncx * M[0 * 4 + j] + ncy * M[1 * 4 + j]) + 0.0f * M[2 * 4 + j]) + 1.0f * M[3 * 4 + j];
+        b[j] = ((ncx * M[0 * 4 + j] + ncy * M[1 * 4 + j]) + 1.0f * M[2 * 4 + j]) + 1.0f * M[3 * 4 + j];
+    }
+    F3 start = F3{a[0] / a[3], a[1] / a[3], a[2] / a[3]};
+    F3 end = F3{b[0] / b[3], b[1] / b[3], b[2] / b[3]};
+    F3 rayDir = normalize(end - start);
+    float rayLength = length(end - start);
+    Hit h;
+    C.st.radiance_rays++;
+    out[0] = out[1] = out[2] = out[3] = 0.0f;
+    if (TraceRay(C.S, start, rayDir, 0.0f, rayLength, false, !(1u > uint32_t(C.set.MaxAnyHitPathLength)), h, C.st)) {
+        const uint32_t geom = C.S.tgeom[h.tri];
+        const oracle_geometry_info& gi = C.S.geo[geom];
+        const Surf sf = GetHitSurface(C.S, geom, h.tri - gi.IdxOffset / 3, h.b1, h.b2);
+        F3 base = F3{1.0f, 1.0f, 1.0f};
+        if (C.set.EnableAlbedoMaps && !C.set.EnableWhiteFurnaceMode) {
+            T4 t = SampleTex(C.S, C.S.mat[gi.MaterialIdx].Albedo, sf.u, sf.v);
+            base = F3{t.r, t.g, t.b};
+        }
+        out[0] = base.x;
+        out[1] = base.y;
+        out[2] = base.z;
+        out[3] = 1.0f;
+    }
+}
+
 // RaygenShader, 92-149: returns the clamped radiance of pixel (x, y)
 F3 Raygen(const Ctx& C, uint32_t x, uint32_t y, uint32_t W, uint32_t H) {
     const uint32_t pixelIdx = y * W + x;
@@ -1018,6 +1058,17 @@ int oracle_render(const oracle_scene* scene, const oracle_ray_trace_constants* r
             out_stats->tri_tests += s.tri_tests;
         }
     }
+    return 0;
+}
+
+int oracle_render_aov(const oracle_scene* scene, const oracle_ray_trace_constants* rtc, const oracle_app_settings* settings,
+                      uint32_t width, uint32_t height, uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, float* out) {
+    const Scene& S = reinterpret_cast<const OracleScene*>(scene)->S;
+    if (x0 + w > width || y0 + h > height) return -1;
+    Stats st;
+    Ctx C{S, *rtc, *settings, nullptr, 0u, st};
+    for (uint32_t r = 0; r < h; ++r)
+        for (uint32_t c = 0; c < w; ++c) PrimaryAov(C, x0 + c, y0 + r, width, height, out + (size_t(r) * w + c) * 4);
     return 0;
 }
 

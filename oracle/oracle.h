@@ -56,6 +56,10 @@ double oracle_scene_build_ms(const oracle_scene* scene);
 int oracle_render(const oracle_scene* scene, const oracle_ray_trace_constants* rtc, const oracle_app_settings* settings,
                   const oracle_spot_light* lights, uint32_t width, uint32_t height, uint32_t x0, uint32_t y0, uint32_t w,
                   uint32_t h, float* accum, uint32_t threads, oracle_stats* out_stats);
+/* Primary-only AOV (C1 plumbing) of the crop: per pixel (albedo rgb, 1) at the primary ray's closest hit,
+ * (0, 0, 0, 0) on a miss; out is w*h float4, crop-local row-major. */
+int oracle_render_aov(const oracle_scene* scene, const oracle_ray_trace_constants* rtc, const oracle_app_settings* settings,
+                      uint32_t width, uint32_t height, uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, float* out);
 /* One bake pass (Baking.hlsl BakeRayGen) over texels [first, first + count) of a width x height
  * lightmap: pos/nrm/accum/lightmap are W*H float4 (same meaning as dxrpt_bake_lightmap). */
 int oracle_bake(const oracle_scene* scene, const oracle_ray_trace_constants* rtc, const oracle_app_settings* settings,

@@ -50,6 +50,7 @@ def lib() -> C.CDLL:
         L.oracle_scene_build_ms.restype = C.c_double
         L.oracle_render.argtypes = [P, P, P, P] + [C.c_uint32] * 6 + [P, C.c_uint32, C.POINTER(OracleStats)]
         L.oracle_trace_rays.argtypes = [P, P, C.c_uint32, C.c_uint32, P]
+        L.oracle_render_aov.argtypes = [P, P, P] + [C.c_uint32] * 6 + [P]
         L.oracle_bake.argtypes = [P, P, P, P, P, P] + [C.c_uint32] * 4 + [P, P, C.c_uint32, C.POINTER(OracleStats)]
         L.oracle_median3x3.argtypes = [P, P, C.c_uint32, C.c_uint32]
         L.oracle_median3x3.restype = None
@@ -109,6 +110,16 @@ class OracleScene:
         if rc != 0:
             raise RuntimeError("oracle_render failed")
         return accum, st
+
+    def render_aov(self, rtc, settings, width, height, crop=None):
+        """Primary-only AOV over `crop`: (h, w, 4) float32 = (albedo rgb, 1) on a hit, 0 on a miss."""
+        x0, y0, w, h = crop if crop is not None else (0, 0, width, height)
+        out = np.zeros((h, w, 4), dtype=np.float32)
+        rc = lib().oracle_render_aov(self.ptr, C.addressof(rtc), C.addressof(settings), width, height, x0, y0, w, h,
+                                     out.ctypes.data)
+        if rc != 0:
+            raise RuntimeError("oracle_render_aov failed")
+        return out
 
     def trace_rays(self, rays: np.ndarray, flags: int) -> np.ndarray:
         rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)

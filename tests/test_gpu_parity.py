@@ -714,3 +714,33 @@ def test_gpu_cmj_matches_reference_vectors(torch_cuda):
     assert rc == 0
     torch.cuda.synchronize()
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), cases[:, 4:6].astype(np.uint32))
+
+
+@pytest.mark.parametrize("name,W,H,crops", [("boxtest", 256, 256, None),
+                                            ("sponza", 1920, 1080, [(900, 480, 96, 96), (0, 0, 64, 64), (1700, 900, 80, 64)]),
+                                            ("suntemple", 1920, 1080, [(800, 400, 96, 96), (100, 200, 64, 64)])])
+def test_primary_aov_matches_oracle(torch_cuda, name, W, H, crops):
+    # dxrpt_render_aov (C1 plumbing: primary ray, closest hit with the alpha test, albedo tap) against the
+    # oracle's AOV, bit for bit: BoxTest 256x256 as BASELINE configs[0], crops of the 1080p scenes
+    torch = torch_cuda
+    sc, sky = scene_bundle(name)
+    st = sc.settings(MaxPathLength=3)
+    rtc = D.make_constants(sc, st, sky, W, H, 3)
+    t = tracer(name)
+    if crops is None:
+        out = torch.full((W * H, 4), 9.0, dtype=torch.float32, device="cuda")
+        t.render_aov(rtc, st, out.data_ptr(), W, H, stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        ref = oracle_scene(name).render_aov(rtc, st, W, H)
+        np.testing.assert_array_equal(out.cpu().numpy().reshape(H, W, 4), ref)
+        return
+    tiles, n = crop_tiles(crops, W)
+    out = torch.full((n, 4), 9.0, dtype=torch.float32, device="cuda")
+    t.render_aov(rtc, st, out.data_ptr(), W, H, tiles=tiles, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    off = 0
+    for (x0, y0, w, h) in crops:
+        ref = oracle_scene(name).render_aov(rtc, st, W, H, crop=(x0, y0, w, h))
+        np.testing.assert_array_equal(got[off:off + w * h].reshape(h, w, 4), ref)
+        off += w * h

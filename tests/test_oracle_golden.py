@@ -166,3 +166,21 @@ def test_feature_toggles_change_the_image(flag):
     b, _ = _render("boxtest", 48, 48, MaxPathLength=3, **{flag: 0})
     assert np.isfinite(b).all()
     assert not np.array_equal(a, b), flag
+
+
+def test_primary_aov_boxtest_known_answer():
+    # C1 plumbing: BoxTest 256x256 primary-only AOV.  Every BoxTest material is the
+    # default base colour 0xC0 (Model.cpp:74-82, 115-117; BoxTest albedo not sRGB-decoded, 768) = 192/255,
+    # so a hit pixel is exactly (192/255, 192/255, 192/255, 1) and a miss 0.
+    W = H = 256
+    sc, sky = scene_bundle("boxtest")
+    st = sc.settings(MaxPathLength=2)
+    rtc = D.make_constants(sc, st, sky, W, H, 0)
+    aov = oracle_scene("boxtest").render_aov(rtc, st, W, H)
+    hit = aov[..., 3] == 1.0
+    assert 0.2 < hit.mean() < 0.95
+    np.testing.assert_array_equal(aov[hit][:, :3], np.float32(192.0 / 255.0))
+    assert (aov[~hit] == 0.0).all()
+    # a crop of the AOV is the same pixels of the full-frame AOV (global pixel indices for the CMJ seeds)
+    part = oracle_scene("boxtest").render_aov(rtc, st, W, H, crop=(40, 100, 64, 32))
+    np.testing.assert_array_equal(part, aov[100:132, 40:104])
