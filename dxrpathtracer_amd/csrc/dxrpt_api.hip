@@ -942,9 +942,10 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.shade_occupancy = ctx->opt_shade_occ;
         fp.xcd_map = ctx->opt_xcd;
         fp.packet_switch = ctx->opt_packet_switch;
-        // megakernel for small frames (BVH8, no instrumentation, one thread per ray traversal)
-        // (path vertices = paths x (L-1); measured crossover ~10M: the megakernel wins on 1080p L=3 and on
-        // every GPU's share of an 8-GPU frame, the wavefront on 4K L=6 and 1080p L=8 full frames)
+        // megakernel schedule for every frame by default (BVH8, one thread per ray traversal):
+        // DXRPT_OPT_MEGAKERNEL_PATHS bounds it by path vertices = paths x (L-1); since r02 the megakernel
+        // (and, from 8M vertices, its depth-split form) beats the wavefront passes at every BASELINE size,
+        // which stay selectable (DXRPT_OPT_MEGAKERNEL_PATHS 0) and parity-tested at full size
         const uint64_t vertices = uint64_t(paths) * uint64_t((settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength) - 1);
         fp.megakernel = (vertices <= ctx->opt_mega_paths && ctx->built_width == 8 && ctx->opt_trav_mode == 0) ? 1u : 0u;
         // register budget by frame size (measured, Sponza proxy 1080p L=3 and its 1/2, 1/4, 1/8 shares):

@@ -15,9 +15,11 @@
 // FromRGB(Reflectance) Spectrum.cpp:113-185, XYZToRGB Spectrum.h:51-55).
 //
 // The model's coefficient tables (published with the model: RGB and spectral datasets, solar
-// radiance and limb darkening fits) and the CIE 1931 / Smits RGB-to-spectrum tables are DATA; they
-// are read at run time from the reference's own dataset sources (named C arrays in
-// HosekSky/ArHosekSkyModelData_{RGB,Spectral}.h and Graphics/Spectrum.cpp), like a scene asset.
+// radiance and limb darkening fits) and the CIE 1931 / Smits RGB-to-spectrum tables are DATA: they
+// ship with the package as dxrpathtracer_amd/data/hosek_tables.bin (written once by
+// scripts/make_hosek_tables.py from the reference's HosekSky/ArHosekSkyModelData_{RGB,Spectral}.h and
+// Graphics/Spectrum.cpp) and are read from that file at run time (dxrpt_host_hosek_load_tables), like
+// a scene asset; nothing reads the reference checkout at run time.
 //
 // Arithmetic follows the reference's types: doubles inside the model, floats in SkyCache::Init
 // (Float3 ops as DirectXMath's SSE2 paths: dot = (x*x + y*y) + z*z, normalize = v / sqrt(dot),

@@ -131,7 +131,7 @@ def test_band_partition_is_balanced():
 
 
 def test_block_partition_covers_image_and_spreads_rows():
-    # the default partition: every pixel exactly once, equal block counts, each rank's blocks drawn
+    # the block partition (--layout blocks; bands are the default): every pixel exactly once, equal block counts, each rank's blocks drawn
     # from (nearly) every block row, so clustered expensive rows (foliage) are shared by all ranks
     from dxrpathtracer_amd.distributed import block_layout, source_index
     for W, H, world in ((1920, 1080, 8), (1920, 1080, 2), (1366, 767, 3), (64, 8, 8)):
