@@ -65,7 +65,8 @@ def main(prof, rnd):
             e["l2_hit_rate"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
         out["kernels"][k] = e
     os.makedirs("profiles", exist_ok=True)
-    with open(f"profiles/{rnd}_kernels.json", "w") as f:
+    sfx = "" if os.environ.get("PMC_CONFIG_TAG", "metric") == "metric" else "_" + os.environ["PMC_CONFIG_TAG"]
+    with open(f"profiles/{rnd}_kernels{sfx}.json", "w") as f:
         json.dump(out, f, indent=2)
     # the timed kinds (DXRPT_K_TRACE / DXRPT_K_SHADOW): the uninstrumented instantiations of the frame
     # (packet and per-lane variants), launch-weighted
@@ -90,7 +91,7 @@ def main(prof, rnd):
             if not calls or any(v is None for _, v in vals):
                 return None
             return sum(c * v for c, v in vals) / calls
-        with open(f"profiles/{rnd}_pmc_{kind}.json", "w") as f:
+        with open(f"profiles/{rnd}_pmc_{kind}{sfx}.json", "w") as f:
             json.dump({"config": CONFIG, "kernel": " + ".join(sorted(cands)), "calls": calls,
                        "avg_ms": (sum(out["kernels"][k].get("total_ms", 0.0) for k in cands) / calls) if calls else None,
                        "per_kernel_avg_ms": {k: out["kernels"][k].get("avg_ms") for k in cands},
