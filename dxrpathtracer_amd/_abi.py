@@ -84,7 +84,7 @@ KERNEL_NAMES = ("k_raygen", "k_trace", "k_shade", "k_shadow", "k_accumulate", "k
  OPT_KERNEL_TIMING_MASK, OPT_XCD_MAPPING, OPT_PACKET_SWITCH, OPT_MEGAKERNEL_PATHS, OPT_MEGAKERNEL_OCCUPANCY,
  OPT_BAKE_CHUNK, OPT_MEGAKERNEL_PERSISTENT, OPT_MEGAKERNEL_LANES, OPT_WAVE_CLOCKS,
  OPT_WAVE_ORDER, OPT_SPLIT_UNITS, OPT_XCD_CHUNK, OPT_WAVE_ORDER_PERIOD, OPT_MEGAKERNEL_SPLIT,
- OPT_TAIL_OCCUPANCY, OPT_SPLIT_PARTS) = range(1, 36)
+ OPT_TAIL_OCCUPANCY, OPT_SPLIT_PARTS, OPT_OPACITY_MICROMAP, OPT_FRAME_OVERLAP) = range(1, 38)
 # context defaults of the traversal options (dxrpt_api.hip)
 DEFAULT_TRAVERSAL_PIPELINE = 0
 POST_FLOAT4, POST_RGBA8 = 0, 1  # dxrpt_post_process output formats
@@ -98,6 +98,12 @@ DEFAULT_BAKE_CHUNK = 1 << 21
 DEFAULT_SPLIT_UNITS = 0
 DEFAULT_XCD_CHUNK = 8
 DEFAULT_WAVE_ORDER_PERIOD = 16
+DEFAULT_OPACITY_MICROMAP = 1
+DEFAULT_FRAME_OVERLAP = 1
+# opacity micromap (pt_layout.h kOmm*): cells per barycentric axis, verdicts
+OMM_SPLIT = 32  # include/dxrpt.h DXRPT_OMM_SPLIT
+OMM_WORDS = 33  # DXRPT_OMM_WORDS
+OMM_UNKNOWN, OMM_OPAQUE, OMM_TRANSPARENT = 0, 1, 2
 DEFAULT_MEGAKERNEL_PERSISTENT = 0
 DEFAULT_MEGAKERNEL_LANES = 0  # by frame size
 DEFAULT_WAVE_ORDER = 2  # by frame size
@@ -118,8 +124,8 @@ class Stats(C.Structure):
 
 
 # dxrpt_stats.schedule bits
-SCHED_MEGAKERNEL, SCHED_PATH_GROUPS, SCHED_ORDER_KERNEL, SCHED_COST_ORDERED, SCHED_CENSUS, SCHED_SPLIT, SCHED_PARTS = \
-    1, 2, 4, 8, 16, 32, 64
+SCHED_MEGAKERNEL, SCHED_PATH_GROUPS, SCHED_ORDER_KERNEL, SCHED_COST_ORDERED, SCHED_CENSUS, SCHED_SPLIT, SCHED_PARTS, \
+    SCHED_OVERLAP = 1, 2, 4, 8, 16, 32, 64, 128
 
 
 class BvhInfo(C.Structure):
@@ -158,7 +164,8 @@ DXRPT_SYMBOLS = ("dxrpt_abi_version", "dxrpt_default_settings", "dxrpt_create", 
                  "dxrpt_render", "dxrpt_get_stats", "dxrpt_trace_rays", "dxrpt_set_option", "dxrpt_reset_timing",
                  "dxrpt_post_process", "dxrpt_bake_lightmap", "dxrpt_denoise_median", "dxrpt_get_wave_clocks",
                  "dxrpt_get_phase_clocks", "dxrpt_sample_cmj", "dxrpt_render_aov", "dxrpt_comm_unique_id", "dxrpt_comm_create",
-                 "dxrpt_comm_destroy", "dxrpt_gather_slabs", "dxrpt_unpermute", "dxrpt_multi_last_error")
+                 "dxrpt_comm_destroy", "dxrpt_gather_slabs", "dxrpt_unpermute", "dxrpt_multi_last_error",
+                 "dxrpt_opacity_micromap")
 DXRPT_HOST_SYMBOLS = ("dxrpt_host_scene_create", "dxrpt_host_scene_load", "dxrpt_host_scene_destroy", "dxrpt_host_last_error",
                       "dxrpt_host_inv_view_projection", "dxrpt_host_sky_create", "dxrpt_host_fill_constants",
                       "dxrpt_host_float_to_half", "dxrpt_host_half_to_float", "dxrpt_host_hosek_load",
@@ -221,6 +228,7 @@ def lib() -> C.CDLL:
         L.dxrpt_gather_slabs.argtypes = [P, P, C.POINTER(C.c_uint64), P, P]
         L.dxrpt_unpermute.argtypes = [P, C.POINTER(Tile), u32, P, u32, u32, P]
         L.dxrpt_multi_last_error.restype = C.c_char_p
+        L.dxrpt_opacity_micromap.argtypes = [P, u32, u32, u32, u32, P, P]
         _lib = L
     return _lib
 

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <stdexcept>
 #include <string>
@@ -16,6 +17,7 @@
 
 #include "../../include/dxrpt.h"
 #include "bvh_build.h"
+#include "omm.h"
 #include "pt_kernels.h"
 #include "pt_layout.h"
 #include "post_kernels.h"
@@ -137,6 +139,21 @@ struct dxrpt_ctx {
     hipEvent_t part_fork = nullptr;
     std::vector<const uint32_t*> stat_counters;  // counter sets of the last frame (several with parts)
     uint32_t opt_tail_occ = 0;              // DXRPT_OPT_TAIL_OCCUPANCY (0 = the head's budget)
+    uint32_t opt_omm = 1;                   // DXRPT_OPT_OPACITY_MICROMAP
+    // DXRPT_OPT_FRAME_OVERLAP: single-kernel megakernel frames alternate between the two FramePart
+    // streams/buffers (frame f on part f % 2) and stage their radiance (d_stage[f % 2]); the caller's
+    // stream blends the stage once the frame is done, so frame f+1's waves start while frame f drains
+    uint32_t opt_overlap = 1;
+    DevBuf d_stage[2];
+    hipEvent_t stage_free[2] = {nullptr, nullptr};  // caller stream: the part's last stage has been blended
+    bool stage_used[2] = {false, false};
+    hipEvent_t ovl_gate = nullptr;                   // the next overlapped frame waits for it (an order pass)
+    bool ovl_gate_set = false;
+    uint32_t ovl_parity = 0;
+    bool ovl_inflight = false;                       // overlapped frames may still run on the part streams
+    DevBuf d_omm;                           // kOmmWords per micromap slot (pt_layout.h kOmm*)
+    std::vector<uint32_t> omm_tris;         // slot -> global triangle (alpha-tested geometry), set by the BVH build
+    bool omm_dirty = true, omm_any = false; // any: some triangle has a verdict (else d_omm is not read)
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
     int built_width = 0;
     DevBuf d_trav;   // 5 x u64 census counters (DXRPT_OPT_COUNT_TRAVERSAL): node / triangle fetches, radiance hits
@@ -176,7 +193,7 @@ struct dxrpt_ctx {
     ~dxrpt_ctx() {
         DevBuf* all[] = {&d_vertices, &d_indices, &d_geos, &d_mats, &d_texdesc, &d_texels, &d_sky, &d_lut, &d_geoshade, &d_nodes,
                          &d_nodes8, &d_tris, &d_tri_verts, &d_lights, &d_tiles, &d_tile_prefix, &f_pix, &f_pxrad, &f_hit, &f_fwd,
-                         &f_shn, &f_shq, &f_shorg, &f_shdir, &f_shcon, &f_counters, &p_bloom0, &p_bloom1, &d_wclock};
+                         &f_shn, &f_shq, &f_shorg, &f_shdir, &f_shcon, &f_counters, &p_bloom0, &p_bloom1, &d_wclock, &d_omm};
         for (DevBuf* b : all) b->release();
         for (auto& qb : f_q)
             for (DevBuf& b : qb) b.release();
@@ -204,6 +221,11 @@ struct dxrpt_ctx {
             if (fp.done) (void)hipEventDestroy(fp.done);
         }
         if (part_fork) (void)hipEventDestroy(part_fork);
+        for (int k = 0; k < 2; ++k) {
+            d_stage[k].release();
+            if (stage_free[k]) (void)hipEventDestroy(stage_free[k]);
+        }
+        if (ovl_gate) (void)hipEventDestroy(ovl_gate);
     }
 };
 
@@ -235,14 +257,14 @@ void require(bool c, const std::string& msg, int code = DXRPT_E_INVALID_ARG) {
 // double and rounded once; oracle/oracle.cpp builds the same table the same way.
 std::vector<float> make_lut() {
     std::vector<float> l(512);
-    for (int i = 0; i < 256; ++i) {
-        l[i] = float(i) / 255.0f;
-        double c = double(i) / 255.0;
-        double lin = c <= 0.04045 ? c / 12.92 : std::pow((c + 0.055) / 1.055, 2.4);
-        l[256 + i] = float(lin);
+    for (uint32_t i = 0; i < 256; ++i) {
+        l[i] = omm_decode(0u, i);
+        l[256 + i] = omm_decode(256u, i);
     }
     return l;
 }
+
+void drain_overlap(dxrpt_ctx* c);
 
 // Device view of the scene for launches of up to `traversal_threads` global threads (sizes the
 // BVH8 stack spill slab, allocated only when the tree is deeper than the LDS part of the stack).
@@ -259,6 +281,7 @@ SceneDev scene_dev(dxrpt_ctx* c, uint32_t traversal_threads, uint32_t slabs = 1,
         s.stack_ints = 2u * std::min<uint32_t>(entries, uint32_t(kStackLds8));
         if (entries > uint32_t(kStackLds8)) {
             const size_t per = size_t(kTraversalStack8 - kStackLds8) * traversal_threads;
+            if (c->d_spill.bytes < per * slabs * sizeof(uint2)) drain_overlap(c);  // (re)allocation
             c->d_spill.ensure(per * slabs * sizeof(uint2));
             s.spill8 = c->d_spill.as<uint2>() + per * slab;
             s.spill_stride = traversal_threads;
@@ -279,6 +302,7 @@ SceneDev scene_dev(dxrpt_ctx* c, uint32_t traversal_threads, uint32_t slabs = 1,
     s.lut = c->d_lut.as<float>();
     s.sky_res = c->sky_res;
     s.num_textures = uint32_t(c->texdesc.size());
+    s.omm = c->opt_omm && c->omm_any ? c->d_omm.as<uint32_t>() : nullptr;
     return s;
 }
 
@@ -286,7 +310,70 @@ SceneDev scene_dev(dxrpt_ctx* c, uint32_t traversal_threads, uint32_t slabs = 1,
 // GeometryInfo.MaterialIdx -> Material -> the texture descriptors, resolved once on the host.  A
 // material index that names no added texture resolves to "none" (the render path rejects such
 // materials before it launches; an opacity of DXRPT_INVALID_INDEX is the reference's "opaque").
+// Waits for the overlapped frames still in flight (DXRPT_OPT_FRAME_OVERLAP) before anything they read is
+// replaced or freed: scene, texture, tile, light and buffer uploads, and calls that share their buffers.
+void drain_overlap(dxrpt_ctx* c) {
+    if (!c->ovl_inflight) return;
+    for (dxrpt_ctx::FramePart& P : c->part)
+        if (P.stream) HIP_CHECK(hipStreamSynchronize(P.stream));
+    if (c->last_stream) HIP_CHECK(hipStreamSynchronize(c->last_stream));  // the stage blends
+    c->ovl_inflight = false;
+}
+
+// The opacity micromap of every triangle on alpha-tested geometry (omm.cpp), one slot per triangle in
+// the order the BVH build numbered them (TriRecord flags >> 1), rebuilt when the texture set changes.
+// Triangles whose opacity map is missing or huge keep all-unknown words (always tapped).
+void build_omm(dxrpt_ctx* c) {
+    const uint32_t ntris = uint32_t(c->indices.size() / 3), ng = uint32_t(c->geos.size());
+    const size_t nslots = c->omm_tris.size();
+    std::vector<uint32_t> words(nslots * kOmmWords, 0u);
+    std::vector<std::unique_ptr<OpacityField>> fields(c->texdesc.size());
+    std::vector<uint32_t> tri_geom(ntris, 0u);
+    for (uint32_t g = 0; g < ng; ++g) {
+        const uint32_t end = g + 1 < ng ? c->geos[g + 1].IdxOffset / 3 : ntris;
+        for (uint32_t t = c->geos[g].IdxOffset / 3; t < end && t < ntris; ++t) tri_geom[t] = g;
+    }
+    bool any = false;
+    for (size_t slot = 0; slot < nslots; ++slot) {
+        const uint32_t t = c->omm_tris[slot], g = tri_geom[t];
+        const uint32_t op = c->mats[c->geos[g].MaterialIdx].Opacity;
+        if (op >= c->texdesc.size()) continue;  // no such texture (always accepts): never probed
+        const TexDesc& d = c->texdesc[op];
+        if (size_t(d.width) * d.height > (size_t(1) << 24)) continue;  // > 16 M texels: tapped as before
+        if (!fields[op]) {
+            const bool r8 = d.fmt == DXRPT_TEX_R8_UNORM;
+            const uint32_t lut = d.fmt == DXRPT_TEX_RGBA8_SRGB ? 256u : 0u;
+            const uint32_t tiles_x = (d.width + (r8 ? kTexTileW8 : kTexTileW32) - 1u) / (r8 ? kTexTileW8 : kTexTileW32);
+            float dec[256];
+            for (uint32_t b = 0; b < 256; ++b) dec[b] = omm_decode(lut, b);
+            std::vector<float> v(size_t(d.width) * d.height);
+            const uint32_t* T = c->texels.data() + d.offset;
+            for (uint32_t y = 0; y < d.height; ++y)
+                for (uint32_t x = 0; x < d.width; ++x) {
+                    const uint32_t w = T[tex_tile_word(x, y, tiles_x, r8)];
+                    v[size_t(y) * d.width + x] = dec[(r8 ? w >> (8u * (x & 3u)) : w) & 0xFFu];
+                }
+            fields[op] = std::make_unique<OpacityField>(d.width, d.height, std::move(v));
+        }
+        float uv[6];
+        for (int k = 0; k < 3; ++k) {  // indices were range-checked by the BVH build
+            const dxrpt_mesh_vertex& mv = c->vertices[size_t(c->indices[size_t(t) * 3 + k]) + c->geos[g].VtxOffset];
+            uv[2 * k] = mv.UV[0];
+            uv[2 * k + 1] = mv.UV[1];
+        }
+        uint32_t* w = &words[slot * kOmmWords];
+        omm_triangle(*fields[op], uv, w);
+        for (uint32_t k = 0; k < kOmmWords; ++k) any = any || w[k] != 0u;
+    }
+    if (any) c->d_omm.upload(words.data(), words.size() * sizeof(uint32_t));
+    c->omm_any = any;
+    c->omm_dirty = false;
+}
+
 void upload_textures(dxrpt_ctx* c) {
+    if ((c->omm_dirty && c->opt_omm && c->bvh_built) || c->tex_dirty || (c->geoshade_dirty && !c->geos.empty()))
+        drain_overlap(c);
+    if (c->omm_dirty && c->opt_omm && c->bvh_built) build_omm(c);
     if (c->tex_dirty) {
         c->d_texdesc.upload(c->texdesc.data(), c->texdesc.size() * sizeof(TexDesc));
         c->d_texels.upload(c->texels.data(), c->texels.size() * sizeof(uint32_t));
@@ -617,6 +704,12 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_SPLIT_PARTS) {
             require(value <= 2, "dxrpt_set_option: split parts must be 0 (by frame size), 1 or 2");
             ctx->opt_split_parts = uint32_t(value);
+        } else if (option == DXRPT_OPT_FRAME_OVERLAP) {
+            require(value <= 1, "dxrpt_set_option: frame overlap must be 0 (off) or 1 (on)");
+            ctx->opt_overlap = uint32_t(value);
+        } else if (option == DXRPT_OPT_OPACITY_MICROMAP) {
+            require(value <= 1, "dxrpt_set_option: opacity micromap must be 0 (off) or 1 (on)");
+            ctx->opt_omm = uint32_t(value);
         } else if (option == DXRPT_OPT_TAIL_OCCUPANCY) {
             require(value == 0 || (value >= 4 && value <= 8), "dxrpt_set_option: tail occupancy must be 0 (by frame) or 4..8");
             ctx->opt_tail_occ = uint32_t(value);
@@ -647,6 +740,7 @@ int dxrpt_set_scene(dxrpt_ctx* ctx, const dxrpt_mesh_vertex* vertices, uint32_t 
                     uint32_t num_geometries, const dxrpt_material* materials, uint32_t num_materials) {
     if (!ctx) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
+        drain_overlap(ctx);
         require(vertices && indices && geometries && materials, "dxrpt_set_scene: null array");
         require(idx_bytes == 2 || idx_bytes == 4, "dxrpt_set_scene: idx_bytes must be 2 or 4");
         require(num_indices % 3 == 0 && num_indices > 0, "dxrpt_set_scene: num_indices must be a positive multiple of 3");
@@ -671,6 +765,7 @@ int dxrpt_set_scene(dxrpt_ctx* ctx, const dxrpt_mesh_vertex* vertices, uint32_t 
         ctx->d_geos.upload(ctx->geos.data(), ctx->geos.size() * sizeof(dxrpt_geometry_info));
         ctx->d_mats.upload(ctx->mats.data(), ctx->mats.size() * sizeof(dxrpt_material));
         ctx->geoshade_dirty = true;
+        ctx->omm_dirty = true;
         ctx->scene_set = true;
         ctx->bvh_built = false;
     });
@@ -679,6 +774,7 @@ int dxrpt_set_scene(dxrpt_ctx* ctx, const dxrpt_mesh_vertex* vertices, uint32_t 
 int dxrpt_add_texture(dxrpt_ctx* ctx, uint32_t w, uint32_t h, uint32_t fmt, const void* texels, uint32_t* out_index) {
     if (!ctx) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
+        drain_overlap(ctx);
         require(texels && w > 0 && h > 0, "dxrpt_add_texture: empty texture");
         require(w <= 16384 && h <= 16384, "dxrpt_add_texture: texture larger than 16384");
         require(fmt <= DXRPT_TEX_R8_UNORM, "dxrpt_add_texture: unknown format");
@@ -708,12 +804,14 @@ int dxrpt_add_texture(dxrpt_ctx* ctx, uint32_t w, uint32_t h, uint32_t fmt, cons
         if (out_index) *out_index = uint32_t(ctx->texdesc.size());
         ctx->texdesc.push_back(d);
         ctx->tex_dirty = true;
+        ctx->omm_dirty = true;
     });
 }
 
 int dxrpt_set_sky(dxrpt_ctx* ctx, const uint16_t* cube, uint32_t res) {
     if (!ctx) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
+        drain_overlap(ctx);
         require(cube && res > 0 && res <= 4096, "dxrpt_set_sky: bad cube");
         ctx->d_sky.upload(cube, size_t(res) * res * 6 * 4 * sizeof(uint16_t));
         ctx->sky_res = res;
@@ -724,6 +822,7 @@ int dxrpt_set_sky(dxrpt_ctx* ctx, const uint16_t* cube, uint32_t res) {
 int dxrpt_build_bvh(dxrpt_ctx* ctx) {
     if (!ctx) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
+        drain_overlap(ctx);
         require(ctx->scene_set, "dxrpt_build_bvh: no scene (call dxrpt_set_scene first)", DXRPT_E_STATE);
         auto t0 = std::chrono::steady_clock::now();
         // Global triangle list: gtri = IdxOffset/3 + PrimitiveIndex for every geometry.
@@ -752,6 +851,14 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
             throw ApiError(DXRPT_E_INVALID_ARG, err);
         // one record per leaf reference (BVH8 spatial splits may reference a triangle more than once)
         const uint32_t nrefs = uint32_t(res.tri_order.size());
+        // opacity micromap slots: the triangles of alpha-tested geometry in global order
+        std::vector<uint32_t> slot_of(ntris, 0u);
+        ctx->omm_tris.clear();
+        for (uint32_t t = 0; t < ntris; ++t)
+            if (ctx->mats[ctx->geos[tri_geom[t]].MaterialIdx].Opacity != DXRPT_INVALID_INDEX) {
+                slot_of[t] = uint32_t(ctx->omm_tris.size());
+                ctx->omm_tris.push_back(t);
+            }
         std::vector<TriRecord> tris(nrefs);
         for (uint32_t i = 0; i < nrefs; ++i) {
             const uint32_t t = res.tri_order[i];
@@ -759,7 +866,7 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
             TriRecord& r = tris[i];
             const uint32_t g = tri_geom[t];
             const bool opaque = ctx->mats[ctx->geos[g].MaterialIdx].Opacity == DXRPT_INVALID_INDEX;
-            uint32_t flags = opaque ? kTriOpaque : 0u;
+            uint32_t flags = opaque ? kTriOpaque : slot_of[t] << 1;
             r.p0[0] = v[0]; r.p0[1] = v[1]; r.p0[2] = v[2];
             r.p1[0] = v[3] - v[0]; r.p1[1] = v[4] - v[1]; r.p1[2] = v[5] - v[2];
             r.p2[0] = v[6] - v[0]; r.p2[1] = v[7] - v[1]; r.p2[2] = v[8] - v[2];
@@ -801,6 +908,8 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
         ctx->bvh.sah_cost = res.sah_cost;
         ctx->built_width = ctx->opt_width;
         ctx->bvh_built = true;
+        ctx->omm_dirty = true;
+        ctx->omm_any = false;
     });
 }
 
@@ -838,6 +947,7 @@ uint32_t prepare_tiles(dxrpt_ctx* ctx, const dxrpt_tile* tiles, uint32_t num_til
     }
     prefix[tl.size()] = uint32_t(total);
     if (tl.size() != ctx->tiles_cache.size() || std::memcmp(tl.data(), ctx->tiles_cache.data(), tl.size() * sizeof(dxrpt_tile)) != 0) {
+        drain_overlap(ctx);
         ctx->d_tiles.upload(tl.data(), tl.size() * sizeof(dxrpt_tile));
         ctx->d_tile_prefix.upload(prefix.data(), prefix.size() * sizeof(uint32_t));
         ctx->tiles_cache = tl;
@@ -850,6 +960,7 @@ int dxrpt_render_aov(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const
                      uint32_t width, uint32_t height, const dxrpt_tile* tiles, uint32_t num_tiles, void* stream) {
     if (!ctx) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
+        drain_overlap(ctx);
         require(ctx->bvh_built, "dxrpt_render_aov: acceleration structure not built", DXRPT_E_STATE);
         require(ctx->built_width == 8, "dxrpt_render_aov: needs the BVH8 layout", DXRPT_E_UNSUPPORTED);
         require(rtc && settings && out, "dxrpt_render_aov: null argument");
@@ -902,6 +1013,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         if (nl) {
             std::vector<dxrpt_spot_light> L(lights->Lights, lights->Lights + nl);
             if (L.size() != ctx->lights_cache.size() || std::memcmp(L.data(), ctx->lights_cache.data(), nl * sizeof(dxrpt_spot_light)) != 0) {
+                drain_overlap(ctx);
                 ctx->d_lights.upload(L.data(), nl * sizeof(dxrpt_spot_light));
                 ctx->lights_cache = L;
             }
@@ -994,6 +1106,39 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // their time (a GPU's share of a multi-GPU frame, 720p: -10..-14 %); a full 1080p frame (4.5
         // rounds) keeps path order, where concurrent neighbouring blocks share more cache than the
         // shorter tail saves (profiles/r02_ab_wave_order.txt).
+        // Overlapped frames (DXRPT_OPT_FRAME_OVERLAP, single-kernel megakernel frames): this frame runs on
+        // part ov's stream with its buffers, counters and BVH8 stack-spill slab, stages its radiance, and
+        // the caller's stream blends the stage after it -- the next frame (the other part) may start as
+        // soon as it is launched, filling this frame's drain.  Its waits: the stage's previous blend, and
+        // the previous frame's order pass (a recording frame).  The first overlapped frame after other
+        // work waits for the caller's stream.
+        const bool overlap = ctx->opt_overlap && fp.megakernel && !fp.split && !ctx->opt_count && !ctx->opt_wave_clocks &&
+                             !fp.mega_persistent && !ctx->opt_lds_nodes && paths > 0;
+        const int ov = int(ctx->ovl_parity);
+        hipStream_t fs = s;
+        FrameParams fo{};
+        if (overlap) {
+            dxrpt_ctx::FramePart& P = ctx->part[ov];
+            if (!(paths <= P.fb.capacity && 2u + nl <= P.fb.shadow_slots && P.fb.counters) ||
+                ctx->d_stage[ov].bytes < size_t(paths) * 16u)
+                drain_overlap(ctx);  // buffers about to be (re)allocated
+            ensure_part(ctx, ov, paths, 2u + nl);
+            ctx->d_stage[ov].ensure(size_t(paths) * 16u);
+            if (!ctx->stage_free[ov]) HIP_CHECK(hipEventCreateWithFlags(&ctx->stage_free[ov], hipEventDisableTiming));
+            if (!ctx->ovl_gate) HIP_CHECK(hipEventCreateWithFlags(&ctx->ovl_gate, hipEventDisableTiming));
+            fs = P.stream;
+            if (!ctx->ovl_inflight) {  // after non-overlapped work: start behind the caller's stream
+                HIP_CHECK(hipEventRecord(ctx->part_fork, s));
+                HIP_CHECK(hipStreamWaitEvent(fs, ctx->part_fork, 0));
+                ctx->stage_used[0] = ctx->stage_used[1] = false;
+                ctx->ovl_gate_set = false;
+            }
+            if (ctx->stage_used[ov]) HIP_CHECK(hipStreamWaitEvent(fs, ctx->stage_free[ov], 0));
+            if (ctx->ovl_gate_set) {
+                HIP_CHECK(hipStreamWaitEvent(fs, ctx->ovl_gate, 0));
+                ctx->ovl_gate_set = false;
+            }
+        }
         uint32_t order_waves = 0;
         bool order_pass = false;
         const uint32_t waves = lanes < 64u ? (paths + lanes - 1u) / lanes : (paths + 63u) / 64u;
@@ -1003,6 +1148,8 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         if (order_on && order_kernel && fp.megakernel && !ctx->opt_count && !fp.mega_persistent && !ctx->opt_lds_nodes) {
             order_waves = waves;
             const uint64_t key = (uint64_t(order_waves) << 32) ^ (uint64_t(lanes) << 24) ^ ctx->tiles_gen;
+            if (key != ctx->order_key || !ctx->order_ready || ctx->d_wave_order.bytes < size_t(order_waves) * sizeof(uint32_t))
+                drain_overlap(ctx);  // the other part's frame may still read the order / record classes
             ctx->d_wave_cost.ensure(size_t(order_waves) * sizeof(uint32_t));
             ctx->d_wave_order.ensure(size_t(order_waves) * sizeof(uint32_t));
             ctx->d_wave_hist.ensure(4 * kWaveClasses * sizeof(uint32_t));
@@ -1011,7 +1158,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
                 ctx->order_ready = false;
                 ctx->order_parity = 0;
                 ctx->order_frame = 0;
-                HIP_CHECK(hipMemsetAsync(ctx->d_wave_hist.p, 0, 4 * kWaveClasses * sizeof(uint32_t), static_cast<hipStream_t>(stream)));
+                HIP_CHECK(hipMemsetAsync(ctx->d_wave_hist.p, 0, 4 * kWaveClasses * sizeof(uint32_t), fs));
             }
             // every opt_order_period-th ordered frame records its wave classes and rebuilds the order
             // (progressive frames cost alike); the frames between reuse it -- no recording atomics, no
@@ -1048,7 +1195,6 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             f.mega = fp.megakernel != 0;
             ev = f.ev.data();
         }
-        const SceneDev sd = scene_dev(ctx, frame_traversal_threads(paths, ctx->fb.shadow_slots, fp.chunks_per_wave));
         hipStream_t aux = nullptr;
         if (ctx->opt_concurrency) {
             if (!ctx->aux) {
@@ -1094,7 +1240,26 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             }
             if (ev) HIP_CHECK(hipEventRecord(ev[1], s));
             sched = DXRPT_SCHED_MEGAKERNEL | DXRPT_SCHED_SPLIT | DXRPT_SCHED_PARTS;
-        } else {   // counter sets: this frame's is fb.counters (read by dxrpt_get_stats); a megakernel frame zeroes
+        } else if (overlap) {
+            dxrpt_ctx::FramePart& P = ctx->part[ov];
+            const uint32_t cur = P.ctr_set;
+            uint32_t* cb = P.counters.as<uint32_t>();
+            P.fb.counters = cb + cur * kCounterWords;
+            P.fb.counters_clean = P.ctr_clean[cur];
+            P.fb.counters_next = cb + (1u - cur) * kCounterWords;  // zeroed in-kernel for this part's next frame
+            fo = fp;
+            fo.stage = ctx->d_stage[ov].as<float4>();
+            const SceneDev so = scene_dev(ctx, frame_traversal_threads(paths, 2u + nl, 0), 2u, uint32_t(ov));
+            HIP_CHECK(launch_frame(so, P.fb, fo, fs, ev, nullptr, nullptr, &sched));
+            P.ctr_clean[cur] = false;
+            P.ctr_clean[1u - cur] = true;
+            P.ctr_set = 1u - cur;
+            P.fb.counters_next = nullptr;
+            P.fb.counters_clean = false;
+            ctx->stat_counters.assign(1, P.fb.counters);
+            sched |= DXRPT_SCHED_OVERLAP;
+        } else {
+            const SceneDev sd = scene_dev(ctx, frame_traversal_threads(paths, ctx->fb.shadow_slots, fp.chunks_per_wave));   // counter sets: this frame's is fb.counters (read by dxrpt_get_stats); a megakernel frame zeroes
             // the other one in-kernel, so the next frame skips the fill launch
             uint32_t* base = ctx->f_counters.as<uint32_t>();
             const uint32_t cur = ctx->ctr_set;
@@ -1116,10 +1281,26 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             uint32_t* h = ctx->d_wave_hist.as<uint32_t>();
             uint32_t* cur = h + ctx->order_parity * 2 * kWaveClasses;
             uint32_t* nxt = h + (1u - ctx->order_parity) * 2 * kWaveClasses;
+            // overlapped: the previous frame (the other part) may still read the order being rewritten
+            if (overlap && ctx->ovl_inflight) HIP_CHECK(hipStreamWaitEvent(fs, ctx->part[1 - ov].done, 0));
             HIP_CHECK(launch_wave_order(fp.wave_cost, cur, cur + kWaveClasses, nxt, nxt + kWaveClasses,
-                                        ctx->d_wave_order.as<uint32_t>(), order_waves, s));
+                                        ctx->d_wave_order.as<uint32_t>(), order_waves, fs));
             ctx->order_ready = true;
             ctx->order_parity ^= 1u;
+            if (overlap) {  // and the next frame reads the new order
+                HIP_CHECK(hipEventRecord(ctx->ovl_gate, fs));
+                ctx->ovl_gate_set = true;
+            }
+        }
+        if (overlap) {  // the caller's stream blends the stage once the frame is done
+            dxrpt_ctx::FramePart& P = ctx->part[ov];
+            HIP_CHECK(hipEventRecord(P.done, fs));
+            HIP_CHECK(hipStreamWaitEvent(s, P.done, 0));
+            HIP_CHECK(launch_accum_stage(fo, s));
+            HIP_CHECK(hipEventRecord(ctx->stage_free[ov], s));
+            ctx->stage_used[ov] = true;
+            ctx->ovl_parity ^= 1u;
+            ctx->ovl_inflight = true;
         }
         ctx->last_stream = s;
         ctx->last_L = settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength;
@@ -1195,12 +1376,34 @@ int dxrpt_get_phase_clocks(dxrpt_ctx* ctx, uint64_t out[8]) {
 int dxrpt_trace_rays(dxrpt_ctx* ctx, const float* rays, uint32_t num_rays, uint32_t flags, float* hits, void* stream) {
     if (!ctx) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
+        drain_overlap(ctx);
         require(ctx->bvh_built, "dxrpt_trace_rays: acceleration structure not built", DXRPT_E_STATE);
         require(num_rays == 0 || (rays && hits), "dxrpt_trace_rays: null argument");
         upload_textures(ctx);
         HIP_CHECK(launch_trace_rays(scene_dev(ctx, trace_rays_threads(num_rays)), reinterpret_cast<const float4*>(rays), num_rays, flags,
                                     reinterpret_cast<float4*>(hits), static_cast<hipStream_t>(stream)));
     });
+}
+
+int dxrpt_opacity_micromap(const float* uvs, uint32_t num_tris, uint32_t w, uint32_t h, uint32_t fmt, const void* texels,
+                           uint32_t* words) {
+    static_assert(kOmmWords == DXRPT_OMM_WORDS && kOmmSplit == DXRPT_OMM_SPLIT, "include/dxrpt.h DXRPT_OMM_*");
+    if (!uvs || !texels || !words || w == 0 || h == 0 || fmt > DXRPT_TEX_R8_UNORM) return DXRPT_E_INVALID_ARG;
+    if (size_t(w) * h > (size_t(1) << 26)) return DXRPT_E_INVALID_ARG;
+    try {
+        const uint32_t lut = fmt == DXRPT_TEX_RGBA8_SRGB ? 256u : 0u;
+        std::vector<float> v(size_t(w) * h);
+        for (size_t i = 0; i < v.size(); ++i) {
+            const uint32_t b = fmt == DXRPT_TEX_R8_UNORM ? static_cast<const uint8_t*>(texels)[i]
+                                                         : static_cast<const uint32_t*>(texels)[i] & 0xFFu;
+            v[i] = omm_decode(lut, b);
+        }
+        const OpacityField f(w, h, std::move(v));
+        for (uint32_t t = 0; t < num_tris; ++t) omm_triangle(f, uvs + size_t(t) * 6u, words + size_t(t) * kOmmWords);
+        return DXRPT_OK;
+    } catch (const std::bad_alloc&) {
+        return DXRPT_E_OOM;
+    }
 }
 
 int dxrpt_sample_cmj(dxrpt_ctx* ctx, const uint32_t* cases, uint32_t num_cases, float* out, void* stream) {
@@ -1253,6 +1456,7 @@ int dxrpt_bake_lightmap(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, co
                         float* accum, float* lightmap, uint32_t width, uint32_t height, void* stream) {
     if (!ctx) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
+        drain_overlap(ctx);
         require(ctx->bvh_built, "dxrpt_bake_lightmap: acceleration structure not built", DXRPT_E_STATE);
         require(ctx->sky_set, "dxrpt_bake_lightmap: sky cubemap not set", DXRPT_E_STATE);
         require(rtc && settings && surface_pos && surface_normal && accum && lightmap, "dxrpt_bake_lightmap: null argument");
@@ -1269,6 +1473,7 @@ int dxrpt_bake_lightmap(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, co
         if (nl) {
             std::vector<dxrpt_spot_light> L(lights->Lights, lights->Lights + nl);
             if (L.size() != ctx->lights_cache.size() || std::memcmp(L.data(), ctx->lights_cache.data(), nl * sizeof(dxrpt_spot_light)) != 0) {
+                drain_overlap(ctx);
                 ctx->d_lights.upload(L.data(), nl * sizeof(dxrpt_spot_light));
                 ctx->lights_cache = L;
             }

@@ -99,6 +99,7 @@ struct SceneDev {
     const uint32_t* texels = nullptr;
     const uint16_t* sky = nullptr;
     const float* lut = nullptr;  // [0..255] unorm, [256..511] sRGB->linear
+    const uint32_t* omm = nullptr;  // opacity micromap, kOmmWords per alpha-tested triangle slot (pt_layout.h); null: off
     uint32_t sky_res = 0;
     uint32_t num_textures = 0;
     int width = 8;  // BVH width actually built: 2 or 8
@@ -172,6 +173,10 @@ struct FrameParams {
     // Split-schedule frame parts (launch_split_part): this part traces the frame's path slots
     // [path_base, path_base + num_paths) (path_base a multiple of 64); 0 otherwise.
     uint32_t path_base;
+    // Overlapped frames (DXRPT_OPT_FRAME_OVERLAP): the single-kernel megakernel writes each path's
+    // radiance and target index to stage[p] (float4: rgb, bits(accum index)) instead of blending it into
+    // accum; launch_accum_stage blends the slots afterwards.  Null: blend in the kernel.
+    float4* stage = nullptr;
 };
 
 constexpr uint32_t kWaveClasses = 256;
@@ -234,6 +239,9 @@ uint32_t trace_rays_threads(uint32_t n);
 
 // Primary-only AOV of the frame's tiles into fp.accum (one float4 per path slot's accumulation index).
 hipError_t launch_primary_aov(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream);
+// RaygenShader's progressive blend (RayTrace.hlsl:140-148) of an overlapped frame's fp.stage slots into
+// fp.accum (fp.num_paths slots).
+hipError_t launch_accum_stage(const FrameParams& fp, hipStream_t stream);
 
 // SampleCMJ2D on device cases (x = sampleIdx, y = numSamplesX, z = numSamplesY, w = pattern) -> out.
 hipError_t launch_sample_cmj(const uint4* cases, uint32_t n, float2* out, hipStream_t stream);

@@ -262,22 +262,42 @@ PT_DEV float opacity_finish(const SceneDev& S, const OpacityTap& t) {
     return lerpf(lerpf(a, b, t.fx), lerpf(c, d, t.fx), t.fy);
 }
 
+// Opacity micromap (pt_layout.h kOmm*): the word holding the cell of a candidate at barycentrics
+// (b1, b2) of the triangle in micromap slot `slot` (TriRecord flags >> 1), and its verdict
+// (kOmmOpaque / kOmmTransparent decide AnyHitShader without its tap, kOmmUnknown: tap).
+struct OmmProbe {
+    uint32_t word, shift;
+};
+PT_DEV OmmProbe omm_probe(const SceneDev& S, uint32_t slot, float b1, float b2) {
+    OmmProbe p{0u, 0u};
+    if (S.omm && b1 + b2 <= 2.0f) {  // NaN barycentrics: the tap decides
+        const uint32_t c = omm_cell(b1, b2);
+        p.word = S.omm[size_t(slot) * kOmmWords + (c >> 4)];
+        p.shift = 2u * (c & 15u);
+    }
+    return p;
+}
+PT_DEV uint32_t omm_verdict(const OmmProbe& p) { return (p.word >> p.shift) & 3u; }
+
 #ifndef DXRPT_ALPHA_ONE_TRIP
 #define DXRPT_ALPHA_ONE_TRIP 1
 #endif
-PT_DEV bool alpha_accepts(const SceneDev& S, uint32_t geom, uint32_t gtri, float b1, float b2) {
+PT_DEV bool alpha_accepts(const SceneDev& S, uint32_t geom, uint32_t gtri, uint32_t slot, float b1, float b2) {
     const GeoTex opacity = S.geoshade[geom].opacity;
     const float2* V = reinterpret_cast<const float2*>(S.tri_verts + size_t(gtri) * 12u);
     float2 uv[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) uv[k] = V[k * 8 + 3];  // float2 #3 of MeshVertex k = UV
+    const OmmProbe om = omm_probe(S, slot, b1, b2);
 #if DXRPT_ALPHA_ONE_TRIP
-    // the opacity descriptor and the UVs in one memory round trip (a triangle that reaches here is
-    // alpha tested, so its geometry has an opacity map; otherwise the UVs are simply unused)
+    // the opacity descriptor, the UVs and the micromap word in one memory round trip (a triangle that
+    // reaches here is alpha tested, so its geometry has an opacity map; otherwise they are unused)
     asm volatile("" ::"v"(opacity.offset), "v"(opacity.whf), "v"(uv[0].x), "v"(uv[0].y), "v"(uv[1].x), "v"(uv[1].y),
-                 "v"(uv[2].x), "v"(uv[2].y));
+                 "v"(uv[2].x), "v"(uv[2].y), "v"(om.word));
 #endif
     if (opacity.whf == 0u) return true;
+    const uint32_t verdict = omm_verdict(om);
+    if (verdict != kOmmUnknown) return verdict == kOmmOpaque;
     const float w0 = (1.0f - b1) - b2;
     float u = bary_lerp(uv[0].x, uv[1].x, uv[2].x, w0, b1, b2);
     float v = bary_lerp(uv[0].y, uv[1].y, uv[2].y, w0, b1, b2);
@@ -360,7 +380,7 @@ PT_DEV bool test_tri_rec(const SceneDev& S, const TriRec& r, f3 o, f3 d, float t
         if (!(t < h.t || (t == h.t && gtri < h.tri))) return false;
     }
     const uint32_t geom = fbits(p1.w);
-    if (alpha && !(fbits(p2.w) & kTriOpaque) && !alpha_accepts(S, geom, gtri, u, v)) return false;
+    if (alpha && !(fbits(p2.w) & kTriOpaque) && !alpha_accepts(S, geom, gtri, fbits(p2.w) >> 1, u, v)) return false;
     h.t = t;
     h.tri = gtri;
     h.b1 = u;
@@ -943,14 +963,21 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
             if (any0 || any1) {
                 OpacityTap q0{}, q1{};
                 bool m0 = false, m1 = false;
+                // lanes whose micromap cell decides skip the tap (o = 0: reject; 1: accept)
                 if (any0) {
                     const AlphaInputs ai = alpha_inputs_uniform(S, fbits(r0.p1.w), fbits(r0.p0.w));
-                    m0 = n0 && ai.op.whf != 0u;
+                    const OmmProbe pr = omm_probe(S, fbits(r0.p2.w) >> 1, u0, v0);  // per lane, same round trip
+                    const uint32_t vd = n0 && ai.op.whf != 0u ? omm_verdict(pr) : kOmmOpaque;
+                    m0 = n0 && ai.op.whf != 0u && vd == kOmmUnknown;
+                    if (vd == kOmmTransparent) o0 = 0.0f;
                     if (m0) q0 = opacity_issue(S, tex_desc(ai.op), ai.u(u0, v0), ai.v(u0, v0));
                 }
                 if (any1) {
                     const AlphaInputs ai = alpha_inputs_uniform(S, fbits(r1.p1.w), fbits(r1.p0.w));
-                    m1 = n1 && ai.op.whf != 0u;
+                    const OmmProbe pr = omm_probe(S, fbits(r1.p2.w) >> 1, u1, v1);
+                    const uint32_t vd = n1 && ai.op.whf != 0u ? omm_verdict(pr) : kOmmOpaque;
+                    m1 = n1 && ai.op.whf != 0u && vd == kOmmUnknown;
+                    if (vd == kOmmTransparent) o1 = 0.0f;
                     if (m1) q1 = opacity_issue(S, tex_desc(ai.op), ai.u(u1, v1), ai.v(u1, v1));
                 }
                 if (m0) o0 = opacity_finish(S, q0);
@@ -1826,6 +1853,24 @@ PT_DEV void accumulate_pixel(const KArgs& A, uint32_t a, float4 r) {
     A.P.accum[a] = make_float4(lerpf(rx, cur.x, f), lerpf(ry, cur.y, f), lerpf(rz, cur.z, f), 1.0f);
 }
 
+// A finished camera path's radiance: into the accumulation target, or -- frames that overlap their
+// neighbours (DXRPT_OPT_FRAME_OVERLAP) -- into the frame's staging slot p with its target index, blended by
+// k_accum_stage once the previous frame's blend is done (same arithmetic, same order per pixel).
+PT_DEV void finish_pixel(const KArgs& A, uint32_t p, uint32_t a, float4 r) {
+    if (A.P.stage) {
+        A.P.stage[p] = make_float4(r.x, r.y, r.z, bitsf(a));
+        return;
+    }
+    accumulate_pixel(A, a, r);
+}
+
+__global__ __launch_bounds__(kBlock) void k_accum_stage(KArgs A) {
+    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= A.P.num_paths) return;
+    const float4 v = A.P.stage[p];
+    accumulate_pixel(A, fbits(v.w), v);
+}
+
 __global__ __launch_bounds__(kBlock) void k_accumulate(KArgs A) {
     const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
     if (p >= A.P.num_paths) return;
@@ -2147,14 +2192,16 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
 struct LaneAlpha {
     GeoTex op;
     float2 uv0, uv1, uv2;
+    OmmProbe omm;
 };
-PT_DEV LaneAlpha lane_alpha_issue(const SceneDev& S, uint32_t geom, uint32_t gtri) {
+PT_DEV LaneAlpha lane_alpha_issue(const SceneDev& S, uint32_t geom, uint32_t gtri, uint32_t slot, float b1, float b2) {
     LaneAlpha a;
     a.op = S.geoshade[geom].opacity;
     const float2* V = reinterpret_cast<const float2*>(S.tri_verts + size_t(gtri) * 12u);
     a.uv0 = V[3];
     a.uv1 = V[11];
     a.uv2 = V[19];
+    a.omm = omm_probe(S, slot, b1, b2);
     return a;
 }
 
@@ -2187,12 +2234,18 @@ PT_DEV bool trav8_tris_pairs(const SceneDev& S, const Ray8& R, uint32_t tbase, u
         const bool n1 = c1 && R.alpha && !(fbits(r1.p2.w) & kTriOpaque);
         float o0 = 1.0f, o1 = 1.0f;
         if (n0 || n1) {  // AnyHitShader (RayTrace.hlsl:485-507) for the candidates on alpha-tested geometry
-            const LaneAlpha a0 = lane_alpha_issue(S, fbits(r0.p1.w), fbits(r0.p0.w));
-            const LaneAlpha a1 = lane_alpha_issue(S, fbits(r1.p1.w), fbits(r1.p0.w));
+            const LaneAlpha a0 = lane_alpha_issue(S, fbits(r0.p1.w), fbits(r0.p0.w), fbits(r0.p2.w) >> 1, u0, v0);
+            const LaneAlpha a1 = lane_alpha_issue(S, fbits(r1.p1.w), fbits(r1.p0.w), fbits(r1.p2.w) >> 1, u1, v1);
             asm volatile("" ::"v"(a0.op.offset), "v"(a0.op.whf), "v"(a0.uv0.x), "v"(a0.uv0.y), "v"(a0.uv1.x), "v"(a0.uv1.y),
                          "v"(a0.uv2.x), "v"(a0.uv2.y), "v"(a1.op.offset), "v"(a1.op.whf), "v"(a1.uv0.x), "v"(a1.uv0.y),
                          "v"(a1.uv1.x), "v"(a1.uv1.y), "v"(a1.uv2.x), "v"(a1.uv2.y));
-            const bool m0 = n0 && a0.op.whf != 0u, m1 = n1 && a1.op.whf != 0u;
+            asm volatile("" ::"v"(a0.omm.word), "v"(a1.omm.word));
+            // a candidate whose micromap cell decides skips the tap (o = 0: reject; 1: accept)
+            const uint32_t vd0 = n0 && a0.op.whf != 0u ? omm_verdict(a0.omm) : kOmmOpaque;
+            const uint32_t vd1 = n1 && a1.op.whf != 0u ? omm_verdict(a1.omm) : kOmmOpaque;
+            if (vd0 == kOmmTransparent) o0 = 0.0f;
+            if (vd1 == kOmmTransparent) o1 = 0.0f;
+            const bool m0 = n0 && a0.op.whf != 0u && vd0 == kOmmUnknown, m1 = n1 && a1.op.whf != 0u && vd1 == kOmmUnknown;
             OpacityTap q0{}, q1{};
             if (m0) q0 = lane_alpha_tap(S, a0, u0, v0);
             if (m1) q1 = lane_alpha_tap(S, a1, u1, v1);
@@ -2375,14 +2428,14 @@ PT_DEV void camera_path(const KArgs& A, uint32_t p, lds_int* stk, const NodeCach
     const PrimaryRay pr = primary_ray(A, p);
     const uint32_t packet = (p | 63u) < A.P.num_paths ? A.P.packet : 0u;
     const float4 rad = trace_path<false, kCount>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, packet, nc, cnt, pa);
-    accumulate_pixel(A, pr.accumIdx, rad);
+    finish_pixel(A, p, pr.accumIdx, rad);
 }
 
 // A path of a path group (DXRPT_OPT_MEGAKERNEL_LANES; g paths per wave): only member 0 writes the pixel.
 PT_DEV void camera_path_group(const KArgs& A, uint32_t p, lds_int* stk, bool member0, uint32_t g) {
     const PrimaryRay pr = primary_ray(A, p);
     const float4 rad = trace_path_group(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, g);
-    if (member0) accumulate_pixel(A, pr.accumIdx, rad);
+    if (member0) finish_pixel(A, p, pr.accumIdx, rad);
 }
 
 // A vertex's shadow rays (ShadowHit/Miss/AnyHit, RayTrace.hlsl:497-507, 532-542) walked slot by slot by
@@ -3028,6 +3081,13 @@ hipError_t launch_split_part(const SceneDev& scene, const FrameBuffers& fb, cons
     KArgs A{scene, fb, fp};
     const size_t lds = size_t(scene.stack_ints) * 64u * sizeof(int);
     launch_split(A, (fp.num_paths + 63u) / 64u, lds, stream);
+    return hipGetLastError();
+}
+
+hipError_t launch_accum_stage(const FrameParams& fp, hipStream_t stream) {
+    if (fp.num_paths == 0 || !fp.stage) return hipSuccess;
+    KArgs A{SceneDev{}, FrameBuffers{}, fp};
+    hipLaunchKernelGGL(k_accum_stage, dim3((fp.num_paths + kBlock - 1u) / kBlock), dim3(kBlock), 0, stream, A);
     return hipGetLastError();
 }
 

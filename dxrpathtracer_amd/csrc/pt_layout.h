@@ -77,7 +77,8 @@ constexpr uint8_t kMetaInternal = 0x80;
 // Leaf triangle record, 48 B.
 //   p0 = (v0.x, v0.y, v0.z, bits(gtri))      gtri = global triangle id = IdxOffset/3 + PrimitiveIndex
 //   p1 = (e1.x, e1.y, e1.z, bits(geometry))  geometry = GeometryIndex()
-//   p2 = (e2.x, e2.y, e2.z, bits(flags))     flags bit0 = opaque geometry
+//   p2 = (e2.x, e2.y, e2.z, bits(flags))     flags bit0 = opaque geometry; on alpha-tested geometry
+//                                            bits 1..31 = the triangle's opacity micromap slot
 struct TriRecord {
     float p0[4];
     float p1[4];
@@ -117,6 +118,32 @@ static_assert(sizeof(GeoShade) == 48, "GeoShade must be 48 B");
 constexpr uint32_t kTexTileWords = 32;  // 128 B
 constexpr uint32_t kTexTileW32 = 8, kTexTileH32 = 4;
 constexpr uint32_t kTexTileW8 = 16, kTexTileH8 = 8;
+
+// Opacity micromap (DXRPT_OPT_OPACITY_MICROMAP, built by omm.cpp): kOmmWords 32-bit words per triangle
+// of alpha-tested geometry, at slot (TriRecord flags >> 1) -- a candidate reads the one word holding its
+// cell, issued with the UV and descriptor loads of its tap.  The triangle's barycentric domain is cut
+// into kOmmSplit x kOmmSplit square cells (b1, b2) of which kOmmCells touch the triangle; cell c holds
+// 2 bits at bit 2(c & 15) of word c >> 4: kOmmOpaque / kOmmTransparent when AnyHitShader's opacity tap
+// (RayTrace.hlsl:485-507: bilinear, wrap, mip 0, `.x < 0.35` rejects) has the same verdict at every
+// point of the cell, kOmmUnknown otherwise (the tap decides).  A verdict is an exact shortcut of the tap,
+// never an approximation: the builder checks every texel any point of the cell can filter.
+constexpr uint32_t kOmmSplit = 32;  // include/dxrpt.h DXRPT_OMM_SPLIT
+constexpr uint32_t kOmmCells = kOmmSplit * (kOmmSplit + 1u) / 2u;  // 528
+constexpr uint32_t kOmmWords = (2u * kOmmCells + 31u) / 32u;        // 33 words = 132 B per triangle
+constexpr uint32_t kOmmUnknown = 0u, kOmmOpaque = 1u, kOmmTransparent = 2u;
+
+// The cell of barycentrics (b1, b2), b1, b2 >= 0, b1 + b2 <= 1 (the triangle test guarantees it up to
+// rounding): row i = floor(b1 * kOmmSplit), column j = floor(b2 * kOmmSplit), clamped into the triangle;
+// rows are stored one after another (row i holds kOmmSplit - i cells).
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline uint32_t omm_cell(float b1, float b2) {
+    uint32_t i = uint32_t(b1 * float(kOmmSplit)), j = uint32_t(b2 * float(kOmmSplit));
+    i = i < kOmmSplit - 1u ? i : kOmmSplit - 1u;
+    j = j < kOmmSplit - 1u - i ? j : kOmmSplit - 1u - i;
+    return i * (2u * kOmmSplit + 1u - i) / 2u + j;
+}
 
 
 

@@ -230,6 +230,7 @@ typedef struct dxrpt_stats {
 #define DXRPT_SCHED_CENSUS 16u       /* the counting (DXRPT_OPT_COUNT_TRAVERSAL) instantiation */
 #define DXRPT_SCHED_SPLIT 32u        /* depth-split megakernel: k_path_head then compacted k_path_tail */
 #define DXRPT_SCHED_PARTS 64u        /* ... as two concurrent halves of the frame's paths */
+#define DXRPT_SCHED_OVERLAP 128u     /* overlapped with its neighbour frames (DXRPT_OPT_FRAME_OVERLAP) */
 
 /* BVH summary (dxrpt_get_bvh_info). */
 typedef struct dxrpt_bvh_info {
@@ -390,6 +391,20 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 #define DXRPT_OPT_TAIL_OCCUPANCY 34u   /* register budget of the split schedule's tail kernels in waves/SIMD:
                                           0 = by default 7 (the head's 6, or DXRPT_OPT_MEGAKERNEL_OCCUPANCY
                                           when set), 4..8 */
+#define DXRPT_OPT_FRAME_OVERLAP 37u    /* 1 (default): consecutive single-kernel megakernel frames alternate
+                                          between two internal streams with their own path buffers and
+                                          stage their radiance; the caller's stream blends a frame's stage
+                                          (RaygenShader's progressive rule, RayTrace.hlsl:140-148) once it is
+                                          done, so the next frame's waves fill the previous frame's drain.
+                                          dxrpt_render still returns with every launch enqueued, and the
+                                          target is complete when the caller's stream reaches that point.
+                                          0: one frame at a time on the caller's stream.  Identical results. */
+#define DXRPT_OPT_OPACITY_MICROMAP 36u /* 1 (default): candidates on alpha-tested geometry first read a 16-B
+                                          opacity micromap word of their triangle (built on the host from
+                                          the opacity map: per barycentric cell, "every tap here accepts",
+                                          "every tap here rejects" or "tap"), and skip the opacity tap of
+                                          AnyHitShader (RayTrace.hlsl:485-507) where the cell decides it.
+                                          0: always tap.  Identical results. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);
@@ -454,6 +469,18 @@ int dxrpt_trace_rays(dxrpt_ctx* ctx, const float* rays, uint32_t num_rays, uint3
  * path's own code on num_cases device cases of 4 uint32 (sampleIdx, numSamplesX, numSamplesY, pattern);
  * out (device) receives 2 floats per case.  Pins the kernels' sampler against the reference's vectors. */
 int dxrpt_sample_cmj(dxrpt_ctx* ctx, const uint32_t* cases, uint32_t num_cases, float* out, void* stream);
+
+/* The opacity micromap words (DXRPT_OPT_OPACITY_MICROMAP; host only, no context or GPU needed) of
+ * num_tris triangles with vertex UVs uvs[6t .. 6t+5] = (u0, v0, u1, v1, u2, v2) on one opacity map given
+ * as dxrpt_add_texture takes it (w x h, fmt, row-major texels): words[W t .. W t + W-1], W =
+ * DXRPT_OMM_WORDS, hold 2 bits per barycentric cell c at bit 2 (c mod 16) of word c / 16, cells
+ * i = floor(S b1), j = floor(S b2) (S = DXRPT_OMM_SPLIT) clamped to i + j <= S-1, numbered row-major by
+ * i: 1 = AnyHitShader accepts every hit in the cell, 2 = rejects every hit, 0 = tap.  Exposed so the
+ * verdicts can be checked against the oracle's AnyHitShader without a GPU. */
+#define DXRPT_OMM_SPLIT 32u
+#define DXRPT_OMM_WORDS 33u
+int dxrpt_opacity_micromap(const float* uvs, uint32_t num_tris, uint32_t w, uint32_t h, uint32_t fmt, const void* texels,
+                           uint32_t* words);
 
 /* ---- multi-GPU frame (no reference counterpart: the reference is single-GPU) -------
  * The frame is split into screen tiles across the GPUs of a node, one process and context per GPU: rank

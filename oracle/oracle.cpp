@@ -1133,6 +1133,17 @@ void oracle_median3x3(const float* in, float* out, uint32_t width, uint32_t heig
         }
 }
 
+// AnyHitShader's verdict (AlphaAccepts, RayTrace.hlsl:485-507) for n candidates (global triangle id,
+// barycentrics b1, b2): out[i] = 1 accept, 0 reject.  Checks the GPU path's opacity micromap.
+int oracle_alpha_accepts(const oracle_scene* scene, const uint32_t* gtri, const float* bary, uint32_t n, uint8_t* out) {
+    const Scene& S = reinterpret_cast<const OracleScene*>(scene)->S;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (gtri[i] >= S.tgeom.size()) return -1;
+        out[i] = AlphaAccepts(S, S.tgeom[gtri[i]], gtri[i], bary[2 * i], bary[2 * i + 1]) ? 1u : 0u;
+    }
+    return 0;
+}
+
 int oracle_trace_rays(const oracle_scene* scene, const float* rays, uint32_t n, uint32_t flags, float* hits) {
     const Scene& S = reinterpret_cast<const OracleScene*>(scene)->S;
     Stats st;

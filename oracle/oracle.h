@@ -69,6 +69,7 @@ int oracle_bake(const oracle_scene* scene, const oracle_ray_trace_constants* rtc
 void oracle_median3x3(const float* in, float* out, uint32_t width, uint32_t height);
 /* rays: n x 8 floats (o.xyz, tmin, d.xyz, tmax); hits: n x 4 (same encoding as dxrpt_trace_rays). */
 int oracle_trace_rays(const oracle_scene* scene, const float* rays, uint32_t n, uint32_t flags, float* hits);
+int oracle_alpha_accepts(const oracle_scene* scene, const uint32_t* gtri, const float* bary, uint32_t n, uint8_t* out);
 
 #ifdef __cplusplus
 }

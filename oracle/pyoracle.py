@@ -50,6 +50,7 @@ def lib() -> C.CDLL:
         L.oracle_scene_build_ms.restype = C.c_double
         L.oracle_render.argtypes = [P, P, P, P] + [C.c_uint32] * 6 + [P, C.c_uint32, C.POINTER(OracleStats)]
         L.oracle_trace_rays.argtypes = [P, P, C.c_uint32, C.c_uint32, P]
+        L.oracle_alpha_accepts.argtypes = [P, P, P, C.c_uint32, P]
         L.oracle_render_aov.argtypes = [P, P, P] + [C.c_uint32] * 6 + [P]
         L.oracle_bake.argtypes = [P, P, P, P, P, P] + [C.c_uint32] * 4 + [P, P, C.c_uint32, C.POINTER(OracleStats)]
         L.oracle_median3x3.argtypes = [P, P, C.c_uint32, C.c_uint32]
@@ -126,6 +127,15 @@ class OracleScene:
         hits = np.zeros((rays.shape[0], 4), dtype=np.float32)
         lib().oracle_trace_rays(self.ptr, rays.ctypes.data, rays.shape[0], flags, hits.ctypes.data)
         return hits
+
+    def alpha_accepts(self, gtri: np.ndarray, bary: np.ndarray) -> np.ndarray:
+        """AnyHitShader's verdict (RayTrace.hlsl:485-507) per (global triangle, b1, b2): True = accept."""
+        gtri = np.ascontiguousarray(gtri, dtype=np.uint32)
+        bary = np.ascontiguousarray(bary, dtype=np.float32).reshape(-1, 2)
+        out = np.zeros(gtri.shape[0], dtype=np.uint8)
+        if lib().oracle_alpha_accepts(self.ptr, gtri.ctypes.data, bary.ctypes.data, gtri.shape[0], out.ctypes.data) != 0:
+            raise ValueError("oracle_alpha_accepts: triangle id out of range")
+        return out.astype(bool)
 
     def bake(self, rtc, settings, lights, pos, nrm, accum, lightmap, first=0, count=None, threads=0):
         """One BakeRayGen pass over texels [first, first + count); updates accum / lightmap (H, W, 4) in place."""

@@ -744,3 +744,40 @@ def test_primary_aov_matches_oracle(torch_cuda, name, W, H, crops):
         ref = oracle_scene(name).render_aov(rtc, st, W, H, crop=(x0, y0, w, h))
         np.testing.assert_array_equal(got[off:off + w * h].reshape(h, w, 4), ref)
         off += w * h
+
+
+@pytest.mark.parametrize("name,L,anyhit,W,H,mega,lanes,split", [
+    ("suntemple", 3, 1, 480, 270, 1 << 30, 64, 0), ("suntemple", 4, 4, 320, 180, 1 << 30, 32, 0),
+    ("sponza", 3, 3, 480, 270, 1 << 30, 64, 0), ("sponza", 3, 1, 480, 270, 1 << 30, 16, 0),
+    ("suntemple", 5, 5, 320, 180, 1 << 30, 64, 1), ("sponza", 4, 4, 320, 180, 0, 64, 0)])
+def test_opacity_micromap_is_bit_identical(torch_cuda, name, L, anyhit, W, H, mega, lanes, split):
+    # DXRPT_OPT_OPACITY_MICROMAP: alpha-tested candidates whose barycentric cell decides AnyHitShader
+    # (RayTrace.hlsl:485-507) skip the opacity tap -- every schedule's alpha paths (packet primaries and
+    # depth-1 sun shadows, per-lane rays, path-group pairs, the split tails, the wavefront passes) must
+    # give the frame of the always-tapping build, with alpha testing on every depth (MaxAnyHitPathLength)
+    torch = torch_cuda
+    sc, sky = scene_bundle(name)
+    st = sc.settings(MaxPathLength=L, MaxAnyHitPathLength=anyhit)
+    t = tracer(name)
+    rtc = D.make_constants(sc, st, sky, W, H, 3)
+    try:
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, mega)
+        t.set_option(A.OPT_MEGAKERNEL_LANES, lanes)
+        t.set_option(A.OPT_MEGAKERNEL_SPLIT, split)
+        t.set_option(A.OPT_WAVE_ORDER, 0)
+        frames = []
+        for omm in (0, 1):
+            t.set_option(A.OPT_OPACITY_MICROMAP, omm)
+            acc = torch.full((W * H, 4), 0.25, dtype=torch.float32, device="cuda")
+            frames.append(gpu_render(torch, name, W, H, st, 3, accum=acc, rtc=rtc).cpu().numpy())
+            s = t.stats()
+            if mega:
+                assert bool(s.schedule & A.SCHED_SPLIT) == bool(split), s.schedule
+                assert s.paths_per_wave == lanes, s.paths_per_wave
+        np.testing.assert_array_equal(frames[1], frames[0])
+    finally:
+        t.set_option(A.OPT_OPACITY_MICROMAP, A.DEFAULT_OPACITY_MICROMAP)
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
+        t.set_option(A.OPT_MEGAKERNEL_LANES, A.DEFAULT_MEGAKERNEL_LANES)
+        t.set_option(A.OPT_MEGAKERNEL_SPLIT, A.DEFAULT_MEGAKERNEL_SPLIT)
+        t.set_option(A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)

@@ -125,3 +125,38 @@ def test_c3_1080p_L8_sixteen_samples(torch_cuda):
         assert s.schedule & A.SCHED_SPLIT and s.schedule & A.SCHED_PARTS, (f, s.schedule)
 
     _steady_frames(torch_cuda, "sponza", W, H, 8, 16, crops, expect=check)
+
+
+@pytest.mark.parametrize("W,H,L,frames,share", [(1280, 720, 3, 20, None), (1920, 1080, 3, 20, (8, 5)),
+                                                (1920, 1080, 3, 6, None), (1920, 1080, 4, 18, (4, 1))])
+def test_overlapped_frames_are_bit_identical(torch_cuda, W, H, L, frames, share):
+    # DXRPT_OPT_FRAME_OVERLAP: back-to-back frames (no host sync between them, as bench.py and every rank
+    # render them) alternate between two internal streams and stage their radiance; the caller's stream
+    # blends each stage in frame order (RayTrace.hlsl:140-148).  >= 17 frames cross a cost-order rebuild
+    # (every 16th frame records, the next frame waits for the new order).  The accumulated target must
+    # equal the one-frame-at-a-time schedule's bit for bit.
+    torch = torch_cuda
+    sc, sky = scene_bundle("sponza")
+    st = sc.settings(MaxPathLength=L)
+    lights = D.make_lights(sc)
+    tiles, n = None, W * H
+    if share is not None:
+        lay = band_layout(W, H, share[0])
+        tiles, n = lay.tile_array(share[1]), lay.counts[share[1]]
+    consts = [D.make_constants(sc, st, sky, W, H, f % 16) for f in range(frames)]
+    stream = torch.cuda.current_stream().cuda_stream
+    out = []
+    for overlap in (0, 1):
+        t = _fresh("sponza")
+        try:
+            t.set_option(A.OPT_FRAME_OVERLAP, overlap)
+            acc = torch.full((n, 4), 0.5, dtype=torch.float32, device="cuda")
+            for f in range(frames):
+                t.render_raw(consts[f], st, acc.data_ptr(), W, H, tiles=tiles, stream=stream, lights=lights)
+            torch.cuda.synchronize()
+            s = t.stats()
+            assert bool(s.schedule & A.SCHED_OVERLAP) == bool(overlap), s.schedule
+            out.append(acc.cpu().numpy())
+        finally:
+            t.close()
+    np.testing.assert_array_equal(out[1], out[0])
