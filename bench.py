@@ -177,6 +177,8 @@ def schedule_name(bits, ppw, A):
         s += f", path groups ({ppw} paths per wave)"
     if bits & A.SCHED_COST_ORDERED:
         s += ", cost-ordered waves"
+    if bits & A.SCHED_OVERLAP:
+        s += ", overlapped frames"
     return s
 
 
@@ -387,7 +389,15 @@ def main():
                          if roof_kernel == "k_path" else None,
                          "avg_launch_ms": round(roof_ms_avg, 4), "traffic_source": traffic_src,
                          "traffic_kernel": pmc.get("kernel"), "l2_hit_rate": l2_hit,
-                         "hbm_write_bytes": write_bytes, "wait_any_per_wave_cycle": wait_frac},
+                         "hbm_write_bytes": write_bytes, "wait_any_per_wave_cycle": wait_frac,
+                         # overlapped frames (DXRPT_SCHED_OVERLAP): a launch shares the GPU with its
+                         # neighbour frames for part of its event span, so the per-launch figure above
+                         # understates the kernel; the steady-state frame interval prices the same bytes
+                         "frames_overlap": bool(stats.schedule & A.SCHED_OVERLAP),
+                         "achieved_per_frame": round(roof_bytes / (float(np.median(frame_ms)) * 1e-3) / 1e9, 1)
+                         if roof_kernel == "k_path" else None,
+                         "frac_per_frame": round(roof_bytes / (float(np.median(frame_ms)) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                         if roof_kernel == "k_path" else None},
             "cpu_baseline": cpu,
             # the headline counts the reference's HUD rays (W*H*(1+2(L-1)) per frame); the kernels skip
             # shadow rays whose pending contribution is exactly 0 (identical image), so fewer are traced:
