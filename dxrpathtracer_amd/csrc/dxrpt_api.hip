@@ -135,7 +135,7 @@ struct dxrpt_ctx {
         hipStream_t stream = nullptr;
         hipEvent_t done = nullptr;
     };
-    FramePart part[2];
+    FramePart part[4];  // split halves 0, 1; overlapped frames: parity ov uses parts 2ov (and 2ov + 1)
     hipEvent_t part_fork = nullptr;
     std::vector<const uint32_t*> stat_counters;  // counter sets of the last frame (several with parts)
     uint32_t opt_tail_occ = 0;              // DXRPT_OPT_TAIL_OCCUPANCY (0 = the head's budget)
@@ -144,6 +144,7 @@ struct dxrpt_ctx {
     // streams/buffers (frame f on part f % 2) and stage their radiance (d_stage[f % 2]); the caller's
     // stream blends the stage once the frame is done, so frame f+1's waves start while frame f drains
     uint32_t opt_overlap = 1;
+    uint32_t accum_extent = 0;  // 1 + the largest accumulation index of the current tile list (stage size)
     DevBuf d_stage[2];
     hipEvent_t stage_free[2] = {nullptr, nullptr};  // caller stream: the part's last stage has been blended
     bool stage_used[2] = {false, false};
@@ -946,6 +947,9 @@ uint32_t prepare_tiles(dxrpt_ctx* ctx, const dxrpt_tile* tiles, uint32_t num_til
         require(total < 0x7FFFFFFFull, std::string(who) + ": too many pixels in one call");
     }
     prefix[tl.size()] = uint32_t(total);
+    uint64_t extent = 0;
+    for (const dxrpt_tile& t : tl) extent = std::max<uint64_t>(extent, t.accum_offset + uint64_t(t.h - 1) * t.accum_pitch + t.w);
+    ctx->accum_extent = uint32_t(extent);
     if (tl.size() != ctx->tiles_cache.size() || std::memcmp(tl.data(), ctx->tiles_cache.data(), tl.size() * sizeof(dxrpt_tile)) != 0) {
         drain_overlap(ctx);
         ctx->d_tiles.upload(tl.data(), tl.size() * sizeof(dxrpt_tile));
@@ -1068,15 +1072,23 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // continuation and shadow rays concurrently, shortening those chains (1/8 share 0.72-0.76 ->
         // 0.68-0.69 ms at 6 waves/SIMD, profiles/r02_ab_path_groups_shares.txt); from the 1/4 share up
         // the doubled waves cost more than the shorter chains save.
-        const uint32_t lanes = ctx->opt_mega_lanes ? ctx->opt_mega_lanes : (paths <= 400000u ? 32u : 64u);
+        // With overlapped frames (r03, profiles/r03_ab_overlap_tune*.txt) the next frame's waves fill a
+        // small frame's end, and 64-lane waves win at every size: 1/8 share 0.41 -> 0.31 ms (ranks 5, 0),
+        // 0.41 -> 0.36 (rank 2); C3's 1/8 share 1.32 -> 0.99.  Path groups stay the default only for
+        // one-frame-at-a-time contexts (DXRPT_OPT_FRAME_OVERLAP 0).
+        const uint32_t lanes = ctx->opt_mega_lanes ? ctx->opt_mega_lanes
+                             : (!ctx->opt_overlap && paths <= 400000u ? 32u : 64u);
         // (with cost-ordered waves, r02: path groups 5 waves/SIMD, 1/8 share 0.574 -> 0.562 ms; 600k-1.5M
         // paths 6, 720p 1.111 -> 1.095 and the 1/2 share 1.20 -> 1.165 ms; profiles/r02_ab_occ_mid_frames.txt)
         // (r02, late: a GPU's 1/4 share, 518k paths, 4 waves/SIMD instead of 5: slowest rank 0.742 -> 0.729 ms,
         // profiles/r02_ab_occ_quarter_share.txt; 600k-1.5M paths 7 instead of 6: 720p 1.098 -> 1.090, the 1/2
         // share 1.174 -> 1.164, profiles/r02_ab_occ_mid_frames_head.txt)
+        // (r03, overlapped frames: 64-lane frames of 300k-600k paths 6 waves/SIMD, a 1/4 share 0.560 ->
+        // 0.520 ms; up to 300k 4 -- 1/8 share 0.305 / 0.317 / 0.329 ms at 4 / 5 / 6)
         fp.megakernel_occupancy = ctx->opt_mega_occ ? ctx->opt_mega_occ
                                 : lanes < 64u ? 5u
-                                : (paths > 600000u ? 7u : 4u);
+                                : paths > 600000u ? 7u
+                                : (ctx->opt_overlap && paths > 300000u ? 6u : 4u);
         fp.mega_persistent = ctx->opt_mega_persistent;
         fp.mega_lanes = lanes;
         // depth-split schedule (k_path_head + one compacting k_path_tail per depth): 64-lane path-ordered
@@ -1106,44 +1118,63 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // their time (a GPU's share of a multi-GPU frame, 720p: -10..-14 %); a full 1080p frame (4.5
         // rounds) keeps path order, where concurrent neighbouring blocks share more cache than the
         // shorter tail saves (profiles/r02_ab_wave_order.txt).
-        // Overlapped frames (DXRPT_OPT_FRAME_OVERLAP, single-kernel megakernel frames): this frame runs on
-        // part ov's stream with its buffers, counters and BVH8 stack-spill slab, stages its radiance, and
-        // the caller's stream blends the stage after it -- the next frame (the other part) may start as
-        // soon as it is launched, filling this frame's drain.  Its waits: the stage's previous blend, and
-        // the previous frame's order pass (a recording frame).  The first overlapped frame after other
-        // work waits for the caller's stream.
-        const bool overlap = ctx->opt_overlap && fp.megakernel && !fp.split && !ctx->opt_count && !ctx->opt_wave_clocks &&
+        // Overlapped frames (DXRPT_OPT_FRAME_OVERLAP, megakernel frames): frame parity ov runs on parts 2ov
+        // (and 2ov + 1 for a split frame's second half) -- their streams, buffers, counters and BVH8
+        // stack-spill slabs -- and stages its radiance; the caller's stream blends the stage after it, so
+        // the next frame (the other parity) may start as soon as it is launched, filling this frame's
+        // drain.  Its waits: the stage's previous blend, and the previous frame's order pass (a recording
+        // frame).  The first overlapped frame after other work waits for the caller's stream.
+        const bool overlap = ctx->opt_overlap && fp.megakernel && !ctx->opt_count && !ctx->opt_wave_clocks &&
                              !fp.mega_persistent && !ctx->opt_lds_nodes && paths > 0;
+        // split frames of at most kSplitPartsMaxPaths paths run as two concurrent parts (the top and the
+        // bottom half of the path slots, each with its own queues and counters, on two internal streams):
+        // one part's per-depth kernels fill the other's drains (1080p L=8 6.52 -> 5.91 ms; a 4K frame
+        // keeps one part: its kernels are long enough, 17.04 -> 17.15 with two)
+        const uint32_t nparts = !(fp.split && !ctx->opt_count && !fp.mega_persistent && !ctx->opt_lds_nodes) ? 1u
+                              : ctx->opt_split_parts ? ctx->opt_split_parts : (paths <= kSplitPartsMaxPaths ? 2u : 1u);
+        const bool halves = nparts == 2u && paths >= 128u;
+        const uint32_t half = ((paths / 64u) / 2u) * 64u;  // a multiple of 64: parts keep whole 8x8 blocks
+        const uint32_t cnt[2] = {halves ? half : paths, paths - half}, base[2] = {0u, half};
         const int ov = int(ctx->ovl_parity);
+        const int pb = overlap ? 2 * ov : 0;  // the frame's first part
         hipStream_t fs = s;
         FrameParams fo{};
         if (overlap) {
-            dxrpt_ctx::FramePart& P = ctx->part[ov];
-            if (!(paths <= P.fb.capacity && 2u + nl <= P.fb.shadow_slots && P.fb.counters) ||
-                ctx->d_stage[ov].bytes < size_t(paths) * 16u)
-                drain_overlap(ctx);  // buffers about to be (re)allocated
-            ensure_part(ctx, ov, paths, 2u + nl);
-            ctx->d_stage[ov].ensure(size_t(paths) * 16u);
+            const size_t stage_bytes = size_t(ctx->accum_extent) * 16u;
+            bool fits = ctx->d_stage[ov].bytes >= stage_bytes;
+            for (int k = 0; k < (halves ? 2 : 1); ++k) {
+                const FrameBuffers& b = ctx->part[pb + k].fb;
+                fits = fits && cnt[k] <= b.capacity && 2u + nl <= b.shadow_slots && b.counters;
+            }
+            if (!fits) drain_overlap(ctx);  // buffers about to be (re)allocated
+            for (int k = 0; k < (halves ? 2 : 1); ++k) ensure_part(ctx, pb + k, cnt[k], 2u + nl);
+            ctx->d_stage[ov].ensure(stage_bytes);
             if (!ctx->stage_free[ov]) HIP_CHECK(hipEventCreateWithFlags(&ctx->stage_free[ov], hipEventDisableTiming));
             if (!ctx->ovl_gate) HIP_CHECK(hipEventCreateWithFlags(&ctx->ovl_gate, hipEventDisableTiming));
-            fs = P.stream;
-            if (!ctx->ovl_inflight) {  // after non-overlapped work: start behind the caller's stream
+            fs = ctx->part[pb].stream;
+            const bool first = !ctx->ovl_inflight;
+            if (first) {  // after non-overlapped work: start behind the caller's stream
                 HIP_CHECK(hipEventRecord(ctx->part_fork, s));
-                HIP_CHECK(hipStreamWaitEvent(fs, ctx->part_fork, 0));
                 ctx->stage_used[0] = ctx->stage_used[1] = false;
                 ctx->ovl_gate_set = false;
             }
-            if (ctx->stage_used[ov]) HIP_CHECK(hipStreamWaitEvent(fs, ctx->stage_free[ov], 0));
-            if (ctx->ovl_gate_set) {
-                HIP_CHECK(hipStreamWaitEvent(fs, ctx->ovl_gate, 0));
-                ctx->ovl_gate_set = false;
+            for (int k = 0; k < (halves ? 2 : 1); ++k) {
+                hipStream_t st = ctx->part[pb + k].stream;
+                if (first) HIP_CHECK(hipStreamWaitEvent(st, ctx->part_fork, 0));
+                if (ctx->stage_used[ov]) HIP_CHECK(hipStreamWaitEvent(st, ctx->stage_free[ov], 0));
+                if (ctx->ovl_gate_set) HIP_CHECK(hipStreamWaitEvent(st, ctx->ovl_gate, 0));
             }
+            ctx->ovl_gate_set = false;
         }
         uint32_t order_waves = 0;
         bool order_pass = false;
         const uint32_t waves = lanes < 64u ? (paths + lanes - 1u) / lanes : (paths + 63u) / 64u;
         const uint64_t slots = uint64_t(ctx->num_cus) * 4u * fp.megakernel_occupancy;
-        const bool order_on = !fp.split && (ctx->opt_wave_order == 1 || (ctx->opt_wave_order == 2 && waves <= 3u * slots));
+        // (r03: with overlapped frames only frames of <= 1.5 rounds keep the cost order -- the next frame
+        // hides a longer frame's end, and path order's cache locality wins: 1/2 share 1.004 -> 0.980 ms,
+        // 720p 0.925 -> 0.896, C5's 1/8 share 2.418 -> 2.342; the 1/8 share keeps it, 0.329 -> 0.305)
+        const bool order_size = ctx->opt_overlap ? 2u * uint64_t(waves) <= 3u * slots : waves <= 3u * slots;
+        const bool order_on = !fp.split && (ctx->opt_wave_order == 1 || (ctx->opt_wave_order == 2 && order_size));
         const bool order_kernel = lanes < 64u || (fp.megakernel_occupancy >= 4u && fp.megakernel_occupancy <= 7u);
         if (order_on && order_kernel && fp.megakernel && !ctx->opt_count && !fp.mega_persistent && !ctx->opt_lds_nodes) {
             order_waves = waves;
@@ -1205,32 +1236,30 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             aux = ctx->aux;
         }
         uint32_t sched = 0;
-        // split frames of at most kSplitPartsMaxPaths paths run as two concurrent parts (the top and the
-        // bottom half of the path slots, each with its own queues and counters, on two internal streams):
-        // one part's per-depth kernels fill the other's drains (1080p L=8 6.52 -> 5.91 ms; a 4K frame
-        // keeps one part: its kernels are long enough, 17.04 -> 17.15 with two)
-        const uint32_t nparts = !(fp.split && !ctx->opt_count && !fp.mega_persistent && !ctx->opt_lds_nodes) ? 1u
-                              : ctx->opt_split_parts ? ctx->opt_split_parts : (paths <= kSplitPartsMaxPaths ? 2u : 1u);
-        if (nparts == 2u && paths >= 128u) {
-            const uint32_t half = ((paths / 64u) / 2u) * 64u;  // a multiple of 64: parts keep whole 8x8 blocks
-            const uint32_t cnt[2] = {half, paths - half}, base[2] = {0u, half};
+        if (overlap) {  // (after the order setup above filled fp's order fields)
+            fo = fp;
+            fo.stage = ctx->d_stage[ov].as<float4>();
+        }
+        if (halves) {
             const uint32_t threads = frame_traversal_threads(paths, 2u + nl, 0);
-            for (int k = 0; k < 2; ++k) ensure_part(ctx, k, cnt[k], 2u + nl);  // (creates the streams and events)
-            if (ev) HIP_CHECK(hipEventRecord(ev[0], s));
-            HIP_CHECK(hipEventRecord(ctx->part_fork, s));
+            if (!overlap) {
+                for (int k = 0; k < 2; ++k) ensure_part(ctx, k, cnt[k], 2u + nl);  // (creates the streams and events)
+                HIP_CHECK(hipEventRecord(ctx->part_fork, s));
+            }
+            if (ev) HIP_CHECK(hipEventRecord(ev[0], overlap ? fs : s));
             ctx->stat_counters.clear();
             for (int k = 0; k < 2; ++k) {
-                dxrpt_ctx::FramePart& P = ctx->part[k];
+                dxrpt_ctx::FramePart& P = ctx->part[pb + k];
                 const uint32_t cur = P.ctr_set;
                 uint32_t* cb = P.counters.as<uint32_t>();
                 P.fb.counters = cb + cur * kCounterWords;
                 P.fb.counters_clean = P.ctr_clean[cur];
                 P.fb.counters_next = cb + (1u - cur) * kCounterWords;
-                FrameParams fk = fp;
+                FrameParams fk = overlap ? fo : fp;
                 fk.num_paths = cnt[k];
                 fk.path_base = base[k];
-                HIP_CHECK(hipStreamWaitEvent(P.stream, ctx->part_fork, 0));
-                HIP_CHECK(launch_split_part(scene_dev(ctx, threads, 2u, uint32_t(k)), P.fb, fk, P.stream));
+                if (!overlap) HIP_CHECK(hipStreamWaitEvent(P.stream, ctx->part_fork, 0));
+                HIP_CHECK(launch_split_part(scene_dev(ctx, threads, overlap ? 4u : 2u, uint32_t(pb + k)), P.fb, fk, P.stream));
                 HIP_CHECK(hipEventRecord(P.done, P.stream));
                 HIP_CHECK(hipStreamWaitEvent(s, P.done, 0));
                 P.ctr_clean[cur] = false;
@@ -1241,15 +1270,13 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             if (ev) HIP_CHECK(hipEventRecord(ev[1], s));
             sched = DXRPT_SCHED_MEGAKERNEL | DXRPT_SCHED_SPLIT | DXRPT_SCHED_PARTS;
         } else if (overlap) {
-            dxrpt_ctx::FramePart& P = ctx->part[ov];
+            dxrpt_ctx::FramePart& P = ctx->part[pb];
             const uint32_t cur = P.ctr_set;
             uint32_t* cb = P.counters.as<uint32_t>();
             P.fb.counters = cb + cur * kCounterWords;
             P.fb.counters_clean = P.ctr_clean[cur];
             P.fb.counters_next = cb + (1u - cur) * kCounterWords;  // zeroed in-kernel for this part's next frame
-            fo = fp;
-            fo.stage = ctx->d_stage[ov].as<float4>();
-            const SceneDev so = scene_dev(ctx, frame_traversal_threads(paths, 2u + nl, 0), 2u, uint32_t(ov));
+            const SceneDev so = scene_dev(ctx, frame_traversal_threads(paths, 2u + nl, 0), 4u, uint32_t(pb));
             HIP_CHECK(launch_frame(so, P.fb, fo, fs, ev, nullptr, nullptr, &sched));
             P.ctr_clean[cur] = false;
             P.ctr_clean[1u - cur] = true;
@@ -1257,15 +1284,15 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             P.fb.counters_next = nullptr;
             P.fb.counters_clean = false;
             ctx->stat_counters.assign(1, P.fb.counters);
-            sched |= DXRPT_SCHED_OVERLAP;
         } else {
-            const SceneDev sd = scene_dev(ctx, frame_traversal_threads(paths, ctx->fb.shadow_slots, fp.chunks_per_wave));   // counter sets: this frame's is fb.counters (read by dxrpt_get_stats); a megakernel frame zeroes
+            // counter sets: this frame's is fb.counters (read by dxrpt_get_stats); a megakernel frame zeroes
             // the other one in-kernel, so the next frame skips the fill launch
-            uint32_t* base = ctx->f_counters.as<uint32_t>();
+            const SceneDev sd = scene_dev(ctx, frame_traversal_threads(paths, ctx->fb.shadow_slots, fp.chunks_per_wave));
+            uint32_t* cbase = ctx->f_counters.as<uint32_t>();
             const uint32_t cur = ctx->ctr_set;
-            ctx->fb.counters = base + cur * kCounterWords;
+            ctx->fb.counters = cbase + cur * kCounterWords;
             ctx->fb.counters_clean = ctx->ctr_clean[cur];
-            ctx->fb.counters_next = fp.megakernel ? base + (1u - cur) * kCounterWords : nullptr;
+            ctx->fb.counters_next = fp.megakernel ? cbase + (1u - cur) * kCounterWords : nullptr;
             HIP_CHECK(launch_frame(sd, ctx->fb, fp, s, ev, aux, aux ? ctx->fork_ev.data() : nullptr, &sched));
             ctx->ctr_clean[cur] = false;
             if (fp.megakernel) {
@@ -1276,13 +1303,14 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             ctx->fb.counters_clean = false;
             ctx->stat_counters.assign(1, ctx->fb.counters);
         }
+        if (overlap) sched |= DXRPT_SCHED_OVERLAP;
         if (order_waves) ++ctx->order_frame;
         if (order_waves && order_pass) {  // the next frames' order from this frame's wave classes (after the frame events)
             uint32_t* h = ctx->d_wave_hist.as<uint32_t>();
             uint32_t* cur = h + ctx->order_parity * 2 * kWaveClasses;
             uint32_t* nxt = h + (1u - ctx->order_parity) * 2 * kWaveClasses;
             // overlapped: the previous frame (the other part) may still read the order being rewritten
-            if (overlap && ctx->ovl_inflight) HIP_CHECK(hipStreamWaitEvent(fs, ctx->part[1 - ov].done, 0));
+            if (overlap && ctx->ovl_inflight) HIP_CHECK(hipStreamWaitEvent(fs, ctx->part[2 * (1 - ov)].done, 0));
             HIP_CHECK(launch_wave_order(fp.wave_cost, cur, cur + kWaveClasses, nxt, nxt + kWaveClasses,
                                         ctx->d_wave_order.as<uint32_t>(), order_waves, fs));
             ctx->order_ready = true;
@@ -1293,9 +1321,11 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             }
         }
         if (overlap) {  // the caller's stream blends the stage once the frame is done
-            dxrpt_ctx::FramePart& P = ctx->part[ov];
-            HIP_CHECK(hipEventRecord(P.done, fs));
-            HIP_CHECK(hipStreamWaitEvent(s, P.done, 0));
+            if (!halves) {  // (the halves recorded theirs and the caller's stream waits for them)
+                dxrpt_ctx::FramePart& P = ctx->part[pb];
+                HIP_CHECK(hipEventRecord(P.done, fs));
+                HIP_CHECK(hipStreamWaitEvent(s, P.done, 0));
+            }
             HIP_CHECK(launch_accum_stage(fo, s));
             HIP_CHECK(hipEventRecord(ctx->stage_free[ov], s));
             ctx->stage_used[ov] = true;

@@ -173,9 +173,9 @@ struct FrameParams {
     // Split-schedule frame parts (launch_split_part): this part traces the frame's path slots
     // [path_base, path_base + num_paths) (path_base a multiple of 64); 0 otherwise.
     uint32_t path_base;
-    // Overlapped frames (DXRPT_OPT_FRAME_OVERLAP): the single-kernel megakernel writes each path's
-    // radiance and target index to stage[p] (float4: rgb, bits(accum index)) instead of blending it into
-    // accum; launch_accum_stage blends the slots afterwards.  Null: blend in the kernel.
+    // Overlapped frames (DXRPT_OPT_FRAME_OVERLAP): the megakernel schedules write each path's radiance to
+    // stage[accumulation index] instead of blending it into accum; launch_accum_stage blends the frame's
+    // paths afterwards.  Null: blend in the kernel.
     float4* stage = nullptr;
 };
 
@@ -239,8 +239,8 @@ uint32_t trace_rays_threads(uint32_t n);
 
 // Primary-only AOV of the frame's tiles into fp.accum (one float4 per path slot's accumulation index).
 hipError_t launch_primary_aov(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream);
-// RaygenShader's progressive blend (RayTrace.hlsl:140-148) of an overlapped frame's fp.stage slots into
-// fp.accum (fp.num_paths slots).
+// RaygenShader's progressive blend (RayTrace.hlsl:140-148) of an overlapped frame's stage into fp.accum
+// (the fp.num_paths paths of fp.tiles).
 hipError_t launch_accum_stage(const FrameParams& fp, hipStream_t stream);
 
 // SampleCMJ2D on device cases (x = sampleIdx, y = numSamplesX, z = numSamplesY, w = pattern) -> out.

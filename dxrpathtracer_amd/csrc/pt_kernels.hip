@@ -1208,8 +1208,12 @@ struct PrimaryRay {
     uint32_t pixelIdx, accumIdx;
 };
 
-PT_DEV PrimaryRay primary_ray(const KArgs& A, uint32_t p) {
-    // path slot -> tile (binary search over the prefix table) -> pixel
+// Path slot p -> its pixel (x, y) and accumulation index: the tile by binary search over the prefix
+// table, then the pixel inside the tile.
+struct PathPixel {
+    uint32_t x, y, accumIdx;
+};
+PT_DEV PathPixel path_pixel(const KArgs& A, uint32_t p) {
     uint32_t lo = 0, hi = A.P.num_tiles;
     while (hi - lo > 1u) {
         uint32_t mid = (lo + hi) >> 1;
@@ -1228,9 +1232,14 @@ PT_DEV PrimaryRay primary_ray(const KArgs& A, uint32_t p) {
         lx = local % tl.w;
         ly = local / tl.w;
     }
-    const uint32_t x = tl.x0 + lx, y = tl.y0 + ly;
+    return PathPixel{tl.x0 + lx, tl.y0 + ly, uint32_t(tl.accum_offset) + ly * tl.accum_pitch + lx};
+}
+
+PT_DEV PrimaryRay primary_ray(const KArgs& A, uint32_t p) {
+    const PathPixel pp = path_pixel(A, p);
+    const uint32_t x = pp.x, y = pp.y;
     const uint32_t pixelIdx = y * A.P.width + x;
-    const uint32_t accumIdx = uint32_t(tl.accum_offset) + ly * tl.accum_pitch + lx;
+    const uint32_t accumIdx = pp.accumIdx;
 
     const uint32_t nS = uint32_t(A.P.set.SqrtNumSamples);
     float sx, sy;
@@ -1854,11 +1863,11 @@ PT_DEV void accumulate_pixel(const KArgs& A, uint32_t a, float4 r) {
 }
 
 // A finished camera path's radiance: into the accumulation target, or -- frames that overlap their
-// neighbours (DXRPT_OPT_FRAME_OVERLAP) -- into the frame's staging slot p with its target index, blended by
+// neighbours (DXRPT_OPT_FRAME_OVERLAP) -- into the frame's stage at the same index, blended by
 // k_accum_stage once the previous frame's blend is done (same arithmetic, same order per pixel).
-PT_DEV void finish_pixel(const KArgs& A, uint32_t p, uint32_t a, float4 r) {
+PT_DEV void finish_pixel(const KArgs& A, uint32_t a, float4 r) {
     if (A.P.stage) {
-        A.P.stage[p] = make_float4(r.x, r.y, r.z, bitsf(a));
+        A.P.stage[a] = r;
         return;
     }
     accumulate_pixel(A, a, r);
@@ -1867,8 +1876,8 @@ PT_DEV void finish_pixel(const KArgs& A, uint32_t p, uint32_t a, float4 r) {
 __global__ __launch_bounds__(kBlock) void k_accum_stage(KArgs A) {
     const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
     if (p >= A.P.num_paths) return;
-    const float4 v = A.P.stage[p];
-    accumulate_pixel(A, fbits(v.w), v);
+    const uint32_t a = path_pixel(A, p).accumIdx;
+    accumulate_pixel(A, a, A.P.stage[a]);
 }
 
 __global__ __launch_bounds__(kBlock) void k_accumulate(KArgs A) {
@@ -2428,14 +2437,14 @@ PT_DEV void camera_path(const KArgs& A, uint32_t p, lds_int* stk, const NodeCach
     const PrimaryRay pr = primary_ray(A, p);
     const uint32_t packet = (p | 63u) < A.P.num_paths ? A.P.packet : 0u;
     const float4 rad = trace_path<false, kCount>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, packet, nc, cnt, pa);
-    finish_pixel(A, p, pr.accumIdx, rad);
+    finish_pixel(A, pr.accumIdx, rad);
 }
 
 // A path of a path group (DXRPT_OPT_MEGAKERNEL_LANES; g paths per wave): only member 0 writes the pixel.
 PT_DEV void camera_path_group(const KArgs& A, uint32_t p, lds_int* stk, bool member0, uint32_t g) {
     const PrimaryRay pr = primary_ray(A, p);
     const float4 rad = trace_path_group(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, stk, g);
-    if (member0) finish_pixel(A, p, pr.accumIdx, rad);
+    if (member0) finish_pixel(A, pr.accumIdx, rad);
 }
 
 // A vertex's shadow rays (ShadowHit/Miss/AnyHit, RayTrace.hlsl:497-507, 532-542) walked slot by slot by
@@ -2825,7 +2834,7 @@ PT_DEV void split_finish(const KArgs& A, int d, bool cont, uint32_t qpos, bool n
     if (cont)
         A.F.q[(d + 1) & 1].rad[qpos] = make_float4(rad.x, rad.y, rad.z, bitsf(nextDiffuse ? 1u : 0u));
     else
-        accumulate_pixel(A, accumIdx, rad);
+        finish_pixel(A, accumIdx, rad);
 }
 
 // Raygen + depth 1 of every camera path (one 64-path 8x8 block per wave, XCD runs as k_path).

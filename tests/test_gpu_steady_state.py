@@ -1,10 +1,13 @@
 """GPU parity of the STEADY-STATE shipped schedule: consecutive progressive frames through one fresh,
 untouched context, as bench.py and every rank of an N-GPU run render them.
 
-A frame of at most 3 rounds of resident waves runs the cost-ordered megakernel instantiation: frame 0
+Defaults (r03, overlapped frames, DXRPT_OPT_FRAME_OVERLAP 1): every megakernel frame stages its radiance
+and is blended on the caller's stream; 64-lane waves at every size; a frame of at most 1.5 rounds of
+resident waves (a GPU's 1/8 share of the metric frame) runs the cost-ordered instantiation -- frame 0
 records its wave costs in path order, frames 1+ start their waves in the cost order built from them
-(DXRPT_OPT_WAVE_ORDER, default "by frame size").  Frames of at most 400,000 paths (a GPU's 1/8 share of
-the metric frame) run path groups.  Each test renders >= 3 consecutive frames (RaygenShader over
+(DXRPT_OPT_WAVE_ORDER, default "by frame size") -- larger ones path order.  With overlap off the r02
+defaults hold (path groups up to 400,000 paths, the cost order up to 3 rounds).  Each test renders >= 3
+consecutive frames (RaygenShader over
 DispatchRays(W, H, 1), RayTrace.hlsl:92-149) into ONE accumulation target, checks after every frame
 that the schedule it expects actually ran (dxrpt_stats.schedule / paths_per_wave), and compares the
 accumulated crops with the oracle accumulated the same way (the progressive rule, RayTrace.hlsl:140-148).
@@ -48,11 +51,13 @@ def _frame_crops(W, H):
     return [(cr, cr[1] * W + cr[0], W) for cr in crops]
 
 
-def _steady_frames(torch, name, W, H, L, frames, crops, tiles=None, n_out=None, expect=None):
+def _steady_frames(torch, name, W, H, L, frames, crops, tiles=None, n_out=None, expect=None, options=()):
     sc, sky = scene_bundle(name)
     st = sc.settings(MaxPathLength=L)
     lights = D.make_lights(sc)
     t = _fresh(name)
+    for opt, val in options:
+        t.set_option(opt, val)
     n = W * H if n_out is None else n_out
     acc = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
     refs = [None] * len(crops)
@@ -77,31 +82,37 @@ def _steady_frames(torch, name, W, H, L, frames, crops, tiles=None, n_out=None, 
     return scheds
 
 
-def _expect_ordered(lanes):
+def _expect(lanes, ordered, overlap=True):
     def check(f, s):
         assert s.schedule & A.SCHED_MEGAKERNEL and not s.schedule & A.SCHED_CENSUS, s.schedule
-        assert s.schedule & A.SCHED_ORDER_KERNEL, f"frame {f}: the cost-ordered instantiation did not run ({s.schedule})"
+        assert bool(s.schedule & A.SCHED_OVERLAP) == overlap, f"frame {f}: schedule {s.schedule}"
+        assert bool(s.schedule & A.SCHED_ORDER_KERNEL) == ordered, \
+            f"frame {f}: the {'cost-ordered' if ordered else 'path-ordered'} instantiation did not run ({s.schedule})"
         # frame 0 builds the order from its own wave costs; frames 1+ start their waves in that order
-        assert bool(s.schedule & A.SCHED_COST_ORDERED) == (f > 0), f"frame {f}: schedule {s.schedule}"
+        assert bool(s.schedule & A.SCHED_COST_ORDERED) == (ordered and f > 0), f"frame {f}: schedule {s.schedule}"
         assert s.paths_per_wave == lanes, (f, s.paths_per_wave)
         assert bool(s.schedule & A.SCHED_PATH_GROUPS) == (lanes < 64)
     return check
 
 
 def test_c2_720p_L3_consecutive_frames(torch_cuda):
-    # BASELINE.json configs[1]: 14,400 waves <= 3 rounds of resident waves -> cost-ordered k_path from frame 1
+    # BASELINE.json configs[1]: 14,400 waves, 2 rounds of resident waves -> path-ordered k_path, overlapped
     W, H = 1280, 720
-    _steady_frames(torch_cuda, "sponza", W, H, 3, 3, _frame_crops(W, H), expect=_expect_ordered(64))
+    _steady_frames(torch_cuda, "sponza", W, H, 3, 3, _frame_crops(W, H), expect=_expect(64, False))
 
 
-@pytest.mark.parametrize("world,rank,lanes", [(8, 5, 32), (8, 0, 32), (2, 1, 64)])
-def test_metric_band_share_consecutive_frames(torch_cuda, world, rank, lanes):
-    # one GPU's share of the metric frame (bench.py --gpus N): 1/8 = 259,200 paths in path groups of 32
-    # per wave, 1/2 = 1,036,800 paths 64 per wave; both cost-ordered from their second frame
+@pytest.mark.parametrize("world,rank,lanes,ordered,overlap", [(8, 5, 64, True, 1), (8, 0, 64, True, 1),
+                                                              (2, 1, 64, False, 1), (8, 5, 32, True, 0),
+                                                              (4, 1, 64, True, 1)])
+def test_metric_band_share_consecutive_frames(torch_cuda, world, rank, lanes, ordered, overlap):
+    # one GPU's share of the metric frame (bench.py --gpus N): 1/8 = 259,200 paths (4,050 waves, one round
+    # at 4 waves/SIMD: cost-ordered from its second frame), 1/4 = 518,400 (1.3 rounds at 6: ordered),
+    # 1/2 = 1,036,800 paths (path order); overlap off: the 1/8 share in path groups of 32 per wave
     W, H = 1920, 1080
     lay = band_layout(W, H, world)
     _steady_frames(torch_cuda, "sponza", W, H, 3, 3, _band_crops(lay, rank), tiles=lay.rank_tiles(rank),
-                   n_out=lay.counts[rank], expect=_expect_ordered(lanes))
+                   n_out=lay.counts[rank], expect=_expect(lanes, ordered, bool(overlap)),
+                   options=((A.OPT_FRAME_OVERLAP, overlap),))
 
 
 def test_c5_4k_L6_gpu_share_consecutive_frames(torch_cuda):
@@ -110,7 +121,7 @@ def test_c5_4k_L6_gpu_share_consecutive_frames(torch_cuda):
     W, H = 3840, 2160
     lay = band_layout(W, H, 8)
     _steady_frames(torch_cuda, "sponza", W, H, 6, 3, _band_crops(lay, 3, w=96), tiles=lay.rank_tiles(3),
-                   n_out=lay.counts[3], expect=_expect_ordered(64))
+                   n_out=lay.counts[3], expect=_expect(64, False))
 
 
 def test_c3_1080p_L8_sixteen_samples(torch_cuda):
@@ -120,20 +131,25 @@ def test_c3_1080p_L8_sixteen_samples(torch_cuda):
     crops = [((x0, y0, 48, 48), y0 * W + x0, W) for (x0, y0) in ((0, 0), (936, 516), (1500, 880), (300, 1032))]
 
     def check(f, s):
-        # 2.07M paths x 7 vertices: the depth-split schedule as two concurrent halves (default by frame size)
+        # 2.07M paths x 7 vertices: the depth-split schedule as two concurrent halves (default by frame size),
+        # overlapped with the neighbour frames
         assert s.schedule & A.SCHED_MEGAKERNEL and s.paths_per_wave == 64, (f, s.schedule, s.paths_per_wave)
         assert s.schedule & A.SCHED_SPLIT and s.schedule & A.SCHED_PARTS, (f, s.schedule)
+        assert s.schedule & A.SCHED_OVERLAP, (f, s.schedule)
 
     _steady_frames(torch_cuda, "sponza", W, H, 8, 16, crops, expect=check)
 
 
 @pytest.mark.parametrize("W,H,L,frames,share", [(1280, 720, 3, 20, None), (1920, 1080, 3, 20, (8, 5)),
-                                                (1920, 1080, 3, 6, None), (1920, 1080, 4, 18, (4, 1))])
+                                                (1920, 1080, 3, 6, None), (1920, 1080, 4, 18, (4, 1)),
+                                                (1920, 1080, 8, 5, None), (3840, 2160, 6, 3, None),
+                                                (1920, 1080, 8, 5, (2, 1))])
 def test_overlapped_frames_are_bit_identical(torch_cuda, W, H, L, frames, share):
     # DXRPT_OPT_FRAME_OVERLAP: back-to-back frames (no host sync between them, as bench.py and every rank
-    # render them) alternate between two internal streams and stage their radiance; the caller's stream
-    # blends each stage in frame order (RayTrace.hlsl:140-148).  >= 17 frames cross a cost-order rebuild
-    # (every 16th frame records, the next frame waits for the new order).  The accumulated target must
+    # render them) alternate between two sets of internal streams and stage their radiance; the caller's
+    # stream blends each stage in frame order (RayTrace.hlsl:140-148).  >= 17 frames cross a cost-order
+    # rebuild (every 16th frame records, the next frame waits for the new order); L=8 1080p runs the
+    # depth-split schedule as two halves per frame, 4K L=6 as one part.  The accumulated target must
     # equal the one-frame-at-a-time schedule's bit for bit.
     torch = torch_cuda
     sc, sky = scene_bundle("sponza")
