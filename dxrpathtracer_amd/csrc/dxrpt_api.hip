@@ -63,7 +63,10 @@ struct DevBuf {
 
 // Depth-split schedule by frame size (DXRPT_OPT_MEGAKERNEL_SPLIT 2): frames of at least this many path
 // vertices (paths x (L - 1)); two concurrent parts up to kSplitPartsMaxPaths paths (DXRPT_OPT_SPLIT_PARTS 0).
+// Overlapped frames (DXRPT_OPT_FRAME_OVERLAP): from kSplitMinVerticesOverlap, one part -- the next frame
+// fills a split frame's drains, which is what the second part did.
 constexpr uint64_t kSplitMinVertices = 8000000;
+constexpr uint64_t kSplitMinVerticesOverlap = 4000000;
 constexpr uint32_t kSplitPartsMaxPaths = 4000000;
 
 }  // namespace
@@ -144,6 +147,7 @@ struct dxrpt_ctx {
     // streams/buffers (frame f on part f % 2) and stage their radiance (d_stage[f % 2]); the caller's
     // stream blends the stage once the frame is done, so frame f+1's waves start while frame f drains
     uint32_t opt_overlap = 1;
+    uint32_t opt_split_bins = 0;            // DXRPT_OPT_SPLIT_BINS
     uint32_t accum_extent = 0;  // 1 + the largest accumulation index of the current tile list (stage size)
     DevBuf d_stage[2];
     hipEvent_t stage_free[2] = {nullptr, nullptr};  // caller stream: the part's last stage has been blended
@@ -400,19 +404,27 @@ void upload_textures(dxrpt_ctx* c) {
     c->geoshade_dirty = false;
 }
 
+// Do buffers for `paths` paths with `slots` shadow slots (and the context's queue binning) fit f?
+bool frame_fits(const dxrpt_ctx* c, const FrameBuffers& f, uint32_t paths, uint32_t slots) {
+    return paths <= f.capacity && slots <= f.shadow_slots && f.counters &&
+           f.cap_q >= f.cap_r * (c->opt_split_bins ? kSplitBins : 1u);
+}
+
 void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
     FrameBuffers& f = c->fb;
-    if (paths <= f.capacity && slots <= f.shadow_slots && f.counters) return;
+    if (frame_fits(c, f, paths, slots)) return;
     const uint32_t cap = std::max(paths, f.capacity);
     const uint32_t sl = std::max(slots, std::max(f.shadow_slots, 2u));
     const uint32_t cap_r = queue_shard_capacity(cap);
-    const size_t qsize = size_t(kQueueShards) * cap_r;
-    require(qsize * sl < (size_t(1) << 32), "frame too large for 32-bit shadow slot ids", DXRPT_E_INVALID_ARG);
+    const uint32_t cap_q = std::max(f.cap_q, cap_r * (c->opt_split_bins ? kSplitBins : 1u));
+    const size_t qsize = size_t(kQueueShards) * cap_r, qbuf = size_t(kQueueShards) * cap_q;
+    require(qsize * sl < (size_t(1) << 32) && qbuf < (size_t(1) << 32), "frame too large for 32-bit shadow slot ids",
+            DXRPT_E_INVALID_ARG);
     c->f_pix.ensure(size_t(cap) * 8);
     c->f_pxrad.ensure(size_t(cap) * 16);
     for (int b = 0; b < 2; ++b) {
-        for (int k = 0; k < 4; ++k) c->f_q[b][k].ensure(qsize * 16);
-        c->f_q[b][4].ensure(qsize * 4);
+        for (int k = 0; k < 4; ++k) c->f_q[b][k].ensure(qbuf * 16);
+        c->f_q[b][4].ensure(qbuf * 4);
         f.q[b].org = c->f_q[b][0].as<float4>();
         f.q[b].dir = c->f_q[b][1].as<float4>();
         f.q[b].thr = c->f_q[b][2].as<float4>();
@@ -442,6 +454,7 @@ void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
     f.counters = c->f_counters.as<uint32_t>() + c->ctr_set * kCounterWords;
     f.capacity = cap;
     f.cap_r = cap_r;
+    f.cap_q = cap_q;
     f.qsize = uint32_t(qsize);
     f.shadow_slots = sl;
 }
@@ -455,15 +468,17 @@ void ensure_part(dxrpt_ctx* c, int k, uint32_t paths, uint32_t slots) {
         HIP_CHECK(hipEventCreateWithFlags(&P.done, hipEventDisableTiming));
     }
     if (!c->part_fork) HIP_CHECK(hipEventCreateWithFlags(&c->part_fork, hipEventDisableTiming));
-    if (paths <= f.capacity && slots <= f.shadow_slots && f.counters) return;
+    if (frame_fits(c, f, paths, slots)) return;
     const uint32_t cap = std::max(paths, f.capacity);
     const uint32_t sl = std::max(slots, std::max(f.shadow_slots, 2u));
     const uint32_t cap_r = queue_shard_capacity(cap);
-    const size_t qsize = size_t(kQueueShards) * cap_r;
-    require(qsize * sl < (size_t(1) << 32), "frame too large for 32-bit shadow slot ids", DXRPT_E_INVALID_ARG);
+    const uint32_t cap_q = std::max(f.cap_q, cap_r * (c->opt_split_bins ? kSplitBins : 1u));
+    const size_t qsize = size_t(kQueueShards) * cap_r, qbuf = size_t(kQueueShards) * cap_q;
+    require(qsize * sl < (size_t(1) << 32) && qbuf < (size_t(1) << 32), "frame too large for 32-bit shadow slot ids",
+            DXRPT_E_INVALID_ARG);
     for (int b = 0; b < 2; ++b) {
-        for (int i = 0; i < 4; ++i) P.q[b][i].ensure(qsize * 16);
-        P.q[b][4].ensure(qsize * 4);
+        for (int i = 0; i < 4; ++i) P.q[b][i].ensure(qbuf * 16);
+        P.q[b][4].ensure(qbuf * 4);
         f.q[b].org = P.q[b][0].as<float4>();
         f.q[b].dir = P.q[b][1].as<float4>();
         f.q[b].thr = P.q[b][2].as<float4>();
@@ -482,6 +497,7 @@ void ensure_part(dxrpt_ctx* c, int k, uint32_t paths, uint32_t slots) {
     f.sh_con = P.shcon.as<float4>();
     f.capacity = cap;
     f.cap_r = cap_r;
+    f.cap_q = cap_q;
     f.qsize = uint32_t(qsize);
     f.shadow_slots = sl;
 }
@@ -705,6 +721,9 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_SPLIT_PARTS) {
             require(value <= 2, "dxrpt_set_option: split parts must be 0 (by frame size), 1 or 2");
             ctx->opt_split_parts = uint32_t(value);
+        } else if (option == DXRPT_OPT_SPLIT_BINS) {
+            require(value <= 1, "dxrpt_set_option: split bins must be 0 (off) or 1 (on)");
+            ctx->opt_split_bins = uint32_t(value);
         } else if (option == DXRPT_OPT_FRAME_OVERLAP) {
             require(value <= 1, "dxrpt_set_option: frame overlap must be 0 (off) or 1 (on)");
             ctx->opt_overlap = uint32_t(value);
@@ -1095,10 +1114,17 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // frames.  By frame size (r03 A/B, profiles/r03_ab_msplit*.txt): it wins where there are many path
         // vertices per frame (1080p L=8 6.90 -> 6.52 ms, 4K L=6 18.50 -> 17.04) and loses on short paths
         // (1080p L=3 2.07 -> 2.23, L=4 3.09 -> 3.18; L=5 even), where each kernel's drain is a larger
-        // part of its time.  Budgets: head 6 waves/SIMD (80 VGPRs), tails 7 (72).
-        const bool split_by_size = vertices >= kSplitMinVertices && lanes == 64u;
+        // part of its time.  Budgets: head 6 waves/SIMD (80 VGPRs), tails 7 (72); with overlapped frames
+        // the head 7 too (metric 1.879 -> 1.862 ms, C4 2.031 -> 2.004, C3 5.58 -> 5.56, C5 share even)
+        // (r03, overlapped frames, profiles/r03_ab_msplit_overlap*.txt: the next frame's waves fill each
+        // per-depth kernel's drain, so the split pays from 4M vertices: metric 1.909 -> 1.875 ms, C4 2.042 ->
+        // 2.029, C5's 1/8 share 2.349 -> 2.098, C3 5.65 -> 5.59 with one part; it still loses below --
+        // 720p 0.902 -> 0.925, C3's 1/8 share 0.979 -> 1.031; the 1/2 share even)
+        const bool split_by_size =
+            vertices >= (ctx->opt_overlap ? kSplitMinVerticesOverlap : kSplitMinVertices) && lanes == 64u;
         fp.split = (ctx->opt_split == 1u || (ctx->opt_split == 2u && split_by_size)) && lanes == 64u && fp.megakernel ? 1u : 0u;
-        if (fp.split && !ctx->opt_mega_occ) fp.megakernel_occupancy = 6u;
+        if (fp.split && !ctx->opt_mega_occ) fp.megakernel_occupancy = ctx->opt_overlap ? 7u : 6u;
+        fp.split_bins = fp.split ? ctx->opt_split_bins : 0u;
         fp.tail_occupancy = ctx->opt_tail_occ ? ctx->opt_tail_occ : (ctx->opt_mega_occ ? fp.megakernel_occupancy : 7u);
         fp.path_base = 0;
         fp.num_cus = ctx->num_cus;
@@ -1129,9 +1155,11 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // split frames of at most kSplitPartsMaxPaths paths run as two concurrent parts (the top and the
         // bottom half of the path slots, each with its own queues and counters, on two internal streams):
         // one part's per-depth kernels fill the other's drains (1080p L=8 6.52 -> 5.91 ms; a 4K frame
-        // keeps one part: its kernels are long enough, 17.04 -> 17.15 with two)
+        // keeps one part: its kernels are long enough, 17.04 -> 17.15 with two).  Overlapped frames keep
+        // one part: the next frame fills the drains (C3 5.65 -> 5.59 ms, C5's 1/8 share 2.295 -> 2.098)
         const uint32_t nparts = !(fp.split && !ctx->opt_count && !fp.mega_persistent && !ctx->opt_lds_nodes) ? 1u
-                              : ctx->opt_split_parts ? ctx->opt_split_parts : (paths <= kSplitPartsMaxPaths ? 2u : 1u);
+                              : ctx->opt_split_parts ? ctx->opt_split_parts
+                              : (!ctx->opt_overlap && paths <= kSplitPartsMaxPaths ? 2u : 1u);
         const bool halves = nparts == 2u && paths >= 128u;
         const uint32_t half = ((paths / 64u) / 2u) * 64u;  // a multiple of 64: parts keep whole 8x8 blocks
         const uint32_t cnt[2] = {halves ? half : paths, paths - half}, base[2] = {0u, half};
@@ -1144,7 +1172,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             bool fits = ctx->d_stage[ov].bytes >= stage_bytes;
             for (int k = 0; k < (halves ? 2 : 1); ++k) {
                 const FrameBuffers& b = ctx->part[pb + k].fb;
-                fits = fits && cnt[k] <= b.capacity && 2u + nl <= b.shadow_slots && b.counters;
+                fits = fits && frame_fits(ctx, b, cnt[k], 2u + nl);
             }
             if (!fits) drain_overlap(ctx);  // buffers about to be (re)allocated
             for (int k = 0; k < (halves ? 2 : 1); ++k) ensure_part(ctx, pb + k, cnt[k], 2u + nl);

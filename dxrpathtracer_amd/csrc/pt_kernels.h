@@ -21,6 +21,8 @@ __host__ __device__ __attribute__((always_inline)) inline uint32_t tex_tile_word
 // the shard counts (queue_pos in pt_kernels.hip).
 constexpr uint32_t kQueueShards = 64;
 constexpr uint32_t kMaxDepthQueues = 16;  // radiance queues 0..15 by depth, shadow queues 16..31
+// Direction-binned split queues (FrameParams::split_bins): shard = 8 x screen region + ray octant.
+constexpr uint32_t kSplitBins = 8;
 
 // Radiance ray queue of one depth (SoA of 16-B words: one dwordx4 per lane, coalesced).  The path
 // state travels with its ray, so every per-depth kernel reads and writes it at the queue position.
@@ -70,6 +72,10 @@ struct FrameBuffers {
     bool counters_clean = false;   // counters already zero: launch_frame skips its fill
     uint32_t capacity = 0;         // paths
     uint32_t cap_r = 0;            // radiance queue shard capacity (multiple of 64)
+    // split-schedule queue shard capacity: cap_r, or kSplitBins * cap_r with direction-binned queues
+    // (FrameParams::split_bins: a shard may then receive a whole screen region); queue buffers hold
+    // kQueueShards * cap_q entries
+    uint32_t cap_q = 0;
     uint32_t qsize = 0;            // kQueueShards * cap_r >= capacity
     uint32_t shadow_slots = 0;     // slots per queue position; shadow shard capacity = shadow_slots * cap_r
 };
@@ -170,6 +176,10 @@ struct FrameParams {
     // tail_occupancy: the tails' register budget (waves/SIMD).
     uint32_t split;
     uint32_t tail_occupancy;
+    // split_bins (DXRPT_OPT_SPLIT_BINS): the compacting pushes bin the surviving paths by screen region
+    // (8, in producer order) AND direction octant of the continuation ray -- shard 8 r + octant -- so a
+    // tail wave holds rays of one octant from one screen region; 0: shard by producer wave only.
+    uint32_t split_bins;
     // Split-schedule frame parts (launch_split_part): this part traces the frame's path slots
     // [path_base, path_base + num_paths) (path_base a multiple of 64); 0 otherwise.
     uint32_t path_base;

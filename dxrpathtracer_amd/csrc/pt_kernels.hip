@@ -1147,6 +1147,23 @@ PT_DEV uint32_t queue_pos(const uint32_t* __restrict__ cnt, uint32_t cap, uint32
     return s * cap + (i - base);
 }
 
+// Append to shard `region_base + oct` (region_base wave-uniform, oct per lane in 0..7): the lanes of each
+// octant form one group (three ballots), each group's first lane reserves the group's run with one atomic
+// -- at most 8 lanes of one vector atomic per wave.  Returns this lane's position (meaningful where `want`).
+PT_DEV uint32_t queue_append_oct(uint32_t* counters, uint32_t cap, bool want, uint32_t region_base, uint32_t oct) {
+    const unsigned long long m = __ballot(want);
+    const unsigned long long b4 = __ballot(want && (oct & 4u)), b2 = __ballot(want && (oct & 2u)),
+                             b1 = __ballot(want && (oct & 1u));
+    const unsigned long long same = m & ((oct & 4u) ? b4 : ~b4) & ((oct & 2u) ? b2 : ~b2) & ((oct & 1u) ? b1 : ~b1);
+    const int lane = __lane_id();
+    const int leader = want ? __ffsll(static_cast<long long>(same)) - 1 : lane;
+    const uint32_t shard = region_base + oct;
+    uint32_t base = 0;
+    if (want && lane == leader) base = atomicAdd(&counters[shard], uint32_t(__popcll(same)));
+    base = uint32_t(__shfl(int(base), leader));
+    return shard * cap + base + uint32_t(__popcll(same & ((1ull << lane) - 1ull)));
+}
+
 // Wave-aggregated append to `shard` (wave-uniform) of a queue: one atomic per wave.  Returns the
 // position of this lane's item (only meaningful where `want`).  Must be called by all active lanes.
 PT_DEV uint32_t queue_append(uint32_t* counters, uint32_t cap, bool want, uint32_t shard) {
@@ -2814,10 +2831,20 @@ void k_path(KArgs A) {
 // run of screen blocks, so the next depth's waves, which take the queue in shard order, sweep the
 // image like the head's (neighbouring origins resident together share the BVH nodes and texels in
 // cache), while the waves running at any time still spread their atomics over several shards.
+// split_bins: shard 8 r + octant(continuation direction), r = the producer's screen region (8, in producer
+// order): a tail wave then holds rays of one octant from one region -- the same near-to-far child order
+// and nearby origins, so its lanes walk similar node sequences (fewer idle lanes, more shared lines).
 PT_DEV uint32_t split_push(const KArgs& A, int d, bool cont, const VertexOut& O, uint32_t pix, uint32_t accumIdx,
                            uint32_t w, uint32_t nw) {
-    const uint32_t shard = uint32_t((uint64_t(w) * kQueueShards) / nw);
-    const uint32_t pos = queue_append(A.F.counters + uint32_t(d + 1) * kQueueShards, A.F.cap_r, cont, shard);
+    uint32_t* ctr = A.F.counters + uint32_t(d + 1) * kQueueShards;
+    uint32_t pos;
+    if (A.P.split_bins) {
+        const uint32_t region = uint32_t((uint64_t(w) * (kQueueShards / kSplitBins)) / nw);
+        const uint32_t oct = (O.nextDir.x < 0.0f ? 4u : 0u) | (O.nextDir.y < 0.0f ? 2u : 0u) | (O.nextDir.z < 0.0f ? 1u : 0u);
+        pos = queue_append_oct(ctr, A.F.cap_q, cont, region * kSplitBins, oct);
+    } else {
+        pos = queue_append(ctr, A.F.cap_q, cont, uint32_t((uint64_t(w) * kQueueShards) / nw));
+    }
     if (cont) {
         const RayQueue& Q = A.F.q[(d + 1) & 1];
         Q.org[pos] = make_float4(O.nextOrigin.x, O.nextOrigin.y, O.nextOrigin.z, kFP32Max);
@@ -2900,7 +2927,7 @@ void k_path_tail(KArgs A, int d) {
     const uint32_t i = j * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const dxrpt_app_settings& set = A.P.set;
-    const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
+    const uint32_t pos = queue_pos(cnt, A.F.cap_q, i);
     const RayQueue& Q = A.F.q[d & 1];
     HitRec h;
     {
@@ -2922,7 +2949,7 @@ void k_path_tail(KArgs A, int d) {
     VertexOut O;
     uint32_t nsh = 0;
     path_vertex(A, d, V, [&](int, f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
-        emit_shadow(A, pos, nsh, o, dd, tmn, tmx, c, fo);
+        emit_shadow(A, i, nsh, o, dd, tmn, tmx, c, fo);  // shadow slots by the dense index (< qsize)
     }, O);
     count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, nsh);
     const bool cont = O.cont;
@@ -2933,7 +2960,7 @@ void k_path_tail(KArgs A, int d) {
     rad.x += V.pathThr.x * O.local.x;
     rad.y += V.pathThr.y * O.local.y;
     rad.z += V.pathThr.z * O.local.z;
-    vertex_shadows(A, d, pos, nsh, false, 0u, rad);
+    vertex_shadows(A, d, i, nsh, false, 0u, rad);
     split_finish(A, d, cont, qpos, nextDiffuse, accumIdx, rad);
 }
 

@@ -383,14 +383,19 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                           compacted into full waves (wave64 ballot, one atomic per wave),
                                           with the path state in the queue instead of registers and its own
                                           register budget.  0: the single k_path.  2 (default): by frame
-                                          size -- frames of >= 8M path vertices (paths x (L-1)).
+                                          size -- frames of >= 4M path vertices (paths x (L-1)) with
+                                          overlapped frames, >= 8M without.
                                           Identical results. */
 #define DXRPT_OPT_SPLIT_PARTS 35u      /* split frames as this many concurrent parts (halves of the path slots,
                                           each with its own queues on an internal stream): 0 = by frame size
-                                          (default: 2 up to 4M paths, else 1), 1 or 2.  Identical results. */
+                                          (default: 1 with overlapped frames; without, 2 up to 4M paths,
+                                          else 1), 1 or 2.  Identical results. */
 #define DXRPT_OPT_TAIL_OCCUPANCY 34u   /* register budget of the split schedule's tail kernels in waves/SIMD:
                                           0 = by default 7 (the head's 6, or DXRPT_OPT_MEGAKERNEL_OCCUPANCY
                                           when set), 4..8 */
+#define DXRPT_OPT_SPLIT_BINS 38u     /* split frames: the compacting pushes bin surviving paths by screen region x
+                                          direction octant of the continuation ray (1) instead of by
+                                          producer wave only (0, default).  Identical results. */
 #define DXRPT_OPT_FRAME_OVERLAP 37u    /* 1 (default): consecutive single-kernel megakernel frames alternate
                                           between two internal streams with their own path buffers and
                                           stage their radiance; the caller's stream blends a frame's stage

@@ -680,15 +680,18 @@ def test_megakernel_split_is_bit_identical(torch_cuda, name, L, W, H, occ, tocc,
             t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, occ)
             t.set_option(A.OPT_TAIL_OCCUPANCY, tocc)
             t.set_option(A.OPT_SPLIT_PARTS, parts)
-            got = gpu_render(torch, name, W, H, st, 4, tiles=tiles, n_out=n, accum=acc0.clone(), rtc=rtc,
-                             lights=lights).cpu().numpy()
-            s_got = t.stats()
-            assert s_got.schedule & A.SCHED_SPLIT, s_got.schedule
-            assert bool(s_got.schedule & A.SCHED_PARTS) == (parts == 2), s_got.schedule
-            np.testing.assert_array_equal(got, ref)
-            assert list(s_got.radiance_rays_per_depth) == list(s_ref.radiance_rays_per_depth)
-            assert list(s_got.shadow_rays_per_depth) == list(s_ref.shadow_rays_per_depth)
+            for bins in (0, 1):  # DXRPT_OPT_SPLIT_BINS: queues binned by screen region x ray octant
+                t.set_option(A.OPT_SPLIT_BINS, bins)
+                got = gpu_render(torch, name, W, H, st, 4, tiles=tiles, n_out=n, accum=acc0.clone(), rtc=rtc,
+                                 lights=lights).cpu().numpy()
+                s_got = t.stats()
+                assert s_got.schedule & A.SCHED_SPLIT, s_got.schedule
+                assert bool(s_got.schedule & A.SCHED_PARTS) == (parts == 2), s_got.schedule
+                np.testing.assert_array_equal(got, ref)
+                assert list(s_got.radiance_rays_per_depth) == list(s_ref.radiance_rays_per_depth)
+                assert list(s_got.shadow_rays_per_depth) == list(s_ref.shadow_rays_per_depth)
     finally:
+        t.set_option(A.OPT_SPLIT_BINS, A.DEFAULT_SPLIT_BINS)
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
         t.set_option(A.OPT_MEGAKERNEL_SPLIT, A.DEFAULT_MEGAKERNEL_SPLIT)
         t.set_option(A.OPT_SPLIT_PARTS, A.DEFAULT_SPLIT_PARTS)

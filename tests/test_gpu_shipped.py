@@ -2,8 +2,9 @@
 
 The other parity tests pin the wavefront schedule (tests/test_gpu_parity.py) and reach the megakernel
 only through bit-identity.  Here every context is fresh and untouched, so each frame runs exactly what
-bench.py times: the megakernel k_path (packet primaries and depth-1 sun shadows, the occupancy picked
-by frame size) for every BASELINE config; frame buffers sized for the whole frame.  One test also runs
+bench.py times: the megakernel (packet primaries and depth-1 sun shadows, the occupancy picked by frame
+size; from 4M path vertices its depth-split form) for every BASELINE config; frame buffers sized for
+the whole frame.  One test also runs
 the wavefront passes at full size (DXRPT_OPT_MEGAKERNEL_PATHS 0, the only option it sets).
 Each full frame (RaygenShader over DispatchRays(W, H, 1), RayTrace.hlsl:92-149) is compared with the
 oracle on >= 6 crops: the four corners, the last rows, a sky region, the centre, and -- for sizes that
@@ -32,6 +33,10 @@ def shipped(name):
         t.build_rt_acceleration_structure()
         _CTX[name] = t
     return _CTX[name]
+
+
+def t_sched(name):
+    return shipped(name).stats().schedule
 
 
 def frame_crops(W, H, extra=()):
@@ -109,18 +114,20 @@ def compare_crops(name, W, H, out, st, rtc, crops, prefill, what, origin=None):
 
 @pytest.mark.parametrize("sample,prefill", [(0, 0.0), (7, 0.375)])
 def test_metric_frame_1080p_L3(torch_cuda, sample, prefill):
-    # BASELINE.json metric: Sponza(-proxy) 1920x1080 MaxPathLength 3, the bench's kernel configuration
+    # BASELINE.json metric: Sponza(-proxy) 1920x1080 MaxPathLength 3, the bench's kernel configuration:
+    # 2.07M paths x 2 vertices, the depth-split megakernel (head + one compacted depth-2 tail) as one part
     W, H = 1920, 1080
     out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 3, sample, prefill, check_kernel="megakernel",
-                                  sched=A.SCHED_MEGAKERNEL)
+                                  sched=A.SCHED_MEGAKERNEL | A.SCHED_SPLIT | A.SCHED_OVERLAP)
     assert np.isfinite(out).all() and (out[:, 3] == 1.0).all()
     compare_crops("sponza", W, H, out, st, rtc, frame_crops(W, H, [SKY["sponza"]]), prefill, f"metric s{sample}")
 
 
 def test_suntemple_1080p_L3(torch_cuda):
-    # BASELINE.json configs[3]: alpha-tested foliage through the megakernel's any-hit paths
+    # BASELINE.json configs[3]: alpha-tested foliage through the megakernel's any-hit paths (depth split)
     W, H = 1920, 1080
-    out, st, rtc = render_shipped(torch_cuda, "suntemple", W, H, 3, 1, check_kernel="megakernel")
+    out, st, rtc = render_shipped(torch_cuda, "suntemple", W, H, 3, 1, check_kernel="megakernel",
+                                  sched=A.SCHED_MEGAKERNEL | A.SCHED_SPLIT)
     compare_crops("suntemple", W, H, out, st, rtc, frame_crops(W, H, [(800, 400, 96, 96), (1200, 600, 96, 64)]), 0.0,
                   "C4")
 
@@ -134,10 +141,11 @@ def test_sponza_720p_L3(torch_cuda):
 
 def test_sponza_1080p_L8(torch_cuda):
     # BASELINE.json configs[2]: 2.07M paths x 7 vertices, the default schedule: the depth-split megakernel
-    # (head + one compacting tail per depth) as two concurrent halves of the frame
+    # (head + one compacting tail per depth), one part (overlapped frames fill its drains)
     W, H = 1920, 1080
     out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 8, 15, 0.125, check_kernel="megakernel",
-                                  sched=A.SCHED_MEGAKERNEL | A.SCHED_SPLIT | A.SCHED_PARTS)
+                                  sched=A.SCHED_MEGAKERNEL | A.SCHED_SPLIT)
+    assert not t_sched("sponza") & A.SCHED_PARTS
     compare_crops("sponza", W, H, out, st, rtc, frame_crops(W, H), 0.125, "C3 s15")
 
 

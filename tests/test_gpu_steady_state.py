@@ -82,9 +82,12 @@ def _steady_frames(torch, name, W, H, L, frames, crops, tiles=None, n_out=None, 
     return scheds
 
 
-def _expect(lanes, ordered, overlap=True):
+def _expect(lanes, ordered, overlap=True, split=False):
     def check(f, s):
         assert s.schedule & A.SCHED_MEGAKERNEL and not s.schedule & A.SCHED_CENSUS, s.schedule
+        # from 4M path vertices (overlapped frames) the depth-split schedule, one part
+        assert bool(s.schedule & A.SCHED_SPLIT) == split, f"frame {f}: schedule {s.schedule}"
+        assert not s.schedule & A.SCHED_PARTS, f"frame {f}: schedule {s.schedule}"
         assert bool(s.schedule & A.SCHED_OVERLAP) == overlap, f"frame {f}: schedule {s.schedule}"
         assert bool(s.schedule & A.SCHED_ORDER_KERNEL) == ordered, \
             f"frame {f}: the {'cost-ordered' if ordered else 'path-ordered'} instantiation did not run ({s.schedule})"
@@ -99,6 +102,14 @@ def test_c2_720p_L3_consecutive_frames(torch_cuda):
     # BASELINE.json configs[1]: 14,400 waves, 2 rounds of resident waves -> path-ordered k_path, overlapped
     W, H = 1280, 720
     _steady_frames(torch_cuda, "sponza", W, H, 3, 3, _frame_crops(W, H), expect=_expect(64, False))
+
+
+@pytest.mark.parametrize("name", ["sponza", "suntemple"])
+def test_metric_1080p_L3_consecutive_frames(torch_cuda, name):
+    # the bench's workload (BASELINE.json metric) and configs[3]: 2.07M paths x 2 vertices -> the
+    # depth-split schedule (k_path_head + the compacted depth-2 k_path_tail), overlapped, four frames
+    W, H = 1920, 1080
+    _steady_frames(torch_cuda, name, W, H, 3, 4, _frame_crops(W, H), expect=_expect(64, False, split=True))
 
 
 @pytest.mark.parametrize("world,rank,lanes,ordered,overlap", [(8, 5, 64, True, 1), (8, 0, 64, True, 1),
@@ -117,11 +128,12 @@ def test_metric_band_share_consecutive_frames(torch_cuda, world, rank, lanes, or
 
 def test_c5_4k_L6_gpu_share_consecutive_frames(torch_cuda):
     # BASELINE.json configs[4]: what each of the 8 GPUs renders -- a 1/8 band share of 3840x2160 at
-    # MaxPathLength 6 (1,036,800 paths) on the default schedule, three consecutive frames
+    # MaxPathLength 6 (1,036,800 paths x 5 vertices: the depth-split schedule) on the default schedule,
+    # three consecutive frames
     W, H = 3840, 2160
     lay = band_layout(W, H, 8)
     _steady_frames(torch_cuda, "sponza", W, H, 6, 3, _band_crops(lay, 3, w=96), tiles=lay.rank_tiles(3),
-                   n_out=lay.counts[3], expect=_expect(64, False))
+                   n_out=lay.counts[3], expect=_expect(64, False, split=True))
 
 
 def test_c3_1080p_L8_sixteen_samples(torch_cuda):
@@ -131,10 +143,10 @@ def test_c3_1080p_L8_sixteen_samples(torch_cuda):
     crops = [((x0, y0, 48, 48), y0 * W + x0, W) for (x0, y0) in ((0, 0), (936, 516), (1500, 880), (300, 1032))]
 
     def check(f, s):
-        # 2.07M paths x 7 vertices: the depth-split schedule as two concurrent halves (default by frame size),
+        # 2.07M paths x 7 vertices: the depth-split schedule as one part (default by frame size),
         # overlapped with the neighbour frames
         assert s.schedule & A.SCHED_MEGAKERNEL and s.paths_per_wave == 64, (f, s.schedule, s.paths_per_wave)
-        assert s.schedule & A.SCHED_SPLIT and s.schedule & A.SCHED_PARTS, (f, s.schedule)
+        assert s.schedule & A.SCHED_SPLIT and not s.schedule & A.SCHED_PARTS, (f, s.schedule)
         assert s.schedule & A.SCHED_OVERLAP, (f, s.schedule)
 
     _steady_frames(torch_cuda, "sponza", W, H, 8, 16, crops, expect=check)
@@ -148,9 +160,9 @@ def test_overlapped_frames_are_bit_identical(torch_cuda, W, H, L, frames, share)
     # DXRPT_OPT_FRAME_OVERLAP: back-to-back frames (no host sync between them, as bench.py and every rank
     # render them) alternate between two sets of internal streams and stage their radiance; the caller's
     # stream blends each stage in frame order (RayTrace.hlsl:140-148).  >= 17 frames cross a cost-order
-    # rebuild (every 16th frame records, the next frame waits for the new order); L=8 1080p runs the
-    # depth-split schedule as two halves per frame, 4K L=6 as one part.  The accumulated target must
-    # equal the one-frame-at-a-time schedule's bit for bit.
+    # rebuild (every 16th frame records, the next frame waits for the new order); 1080p L=3 and L=8 and
+    # 4K L=6 run the depth-split schedule overlapped (one part) against k_path / two halves one frame at
+    # a time.  The accumulated target must equal the one-frame-at-a-time schedule's bit for bit.
     torch = torch_cuda
     sc, sky = scene_bundle("sponza")
     st = sc.settings(MaxPathLength=L)
