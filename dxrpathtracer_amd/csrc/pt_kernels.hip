@@ -1088,6 +1088,138 @@ PT_DEV bool traverse8_from(const SceneDev& S, const Ray8& R, lds_int* stk, HitRe
     return h.tri != kMiss;
 }
 
+// Two any-hit rays of one lane down ONE node sequence (DXRPT_SHADOW_PAIRS).  A vertex's sun and
+// sky-visibility rays both start at the hit position (RayTrace.hlsl:241-244, 415-425), so they cross the
+// same nodes around it; walked one after the other they fetch those nodes twice and chain two traversals'
+// round trips.  Here a child is entered when either live ray enters its box (each ray tested against its
+// own [tmin, tmax]) and every live ray tests each triangle of the visited leaves until it finds an
+// occluder (then it drops out of the box tests).  An any-hit answer is whether some accepted hit lies in
+// [tmin, tmax] among the triangles its own traversal (traverse8<true>) would test; the union visits a
+// superset of those and tests them exactly, so each answer is that traversal's, for any two rays.
+// live: bit 0 ray a, bit 1 ray b.  Returns the occluded bits.  kCount: node and triangle-record fetches
+// (shared by both rays) into nvisit / ntest.
+// The pair keeps each ray lean (origin, direction, inverse, interval, alpha flag): the box-test terms
+// o * inv and the octant are recomputed per node visit -- the same products ray8_init forms, so the same
+// box hits -- which keeps the pair inside the traversal's register budget.
+struct RayLean {
+    f3 o, d, inv;
+    float tmin, tmax;
+    bool alpha;
+};
+
+PT_DEV void ray_lean_init(RayLean& R, f3 o, f3 d, float tmin, float tmax, bool alpha) {
+    R.o = o;
+    R.d = d;
+    R.inv = safe_inverse(d);
+    R.tmin = tmin;
+    R.tmax = tmax;
+    R.alpha = alpha;
+}
+
+PT_DEV uint32_t lean_oct(const RayLean& R) {
+    return (R.inv.x < 0.0f ? 4u : 0u) | (R.inv.y < 0.0f ? 2u : 0u) | (R.inv.z < 0.0f ? 1u : 0u);
+}
+
+PT_DEV uint32_t box8_hits_lean(const RayLean& L, const Node8Words& W) {
+    Ray8 R;
+    R.o = L.o;
+    R.d = L.d;
+    R.inv = L.inv;
+    R.ood = mul(L.o, L.inv);
+    R.tmin = L.tmin;
+    R.tmax = L.tmax;
+    R.oct = lean_oct(L);
+    R.alpha = L.alpha;
+    return box8_hits(R, W, L.tmax);
+}
+
+template <bool kCount>
+PT_DEV uint32_t traverse8_anyhit2(const SceneDev& S, const RayLean& Ra, const RayLean& Rb, uint32_t live, lds_int* stk,
+                                  uint32_t& nvisit, uint32_t& ntest) {
+    uint32_t occ = 0;
+    if (!live) return occ;
+    const uint32_t oct = lean_oct((live & 1u) ? Ra : Rb);  // child order of the walk (any order: same answers)
+    uint32_t node = 0;
+    int sp = 0;
+    uint2 tos = make_uint2(0u, 0u);
+    while (true) {
+        if (kCount) ++nvisit;
+        const uint4* N = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(S.nodes8) + size_t(node) * kNode8Stride);
+        const Node8Words W{N[0], N[1], N[2], N[3], N[4]};  // not pinned: the pair's registers are scarce
+        uint32_t hm = 0;
+        if (live & 1u) hm |= box8_hits_lean(Ra, W);
+        if (live & 2u) hm |= box8_hits_lean(Rb, W);
+        // the group logic of trav8_node_w on the union mask, keyed by `oct`
+        const uint4 w0 = W.w0, w1 = W.w1;
+        const uint32_t imask = w0.w >> 24;
+        uint32_t ihits = hm & imask;
+        if (oct & 1u) ihits = ((ihits & 0x55u) << 1) | ((ihits >> 1) & 0x55u);
+        if (oct & 2u) ihits = ((ihits & 0x33u) << 2) | ((ihits >> 2) & 0x33u);
+        if (oct & 4u) ihits = ((ihits & 0x0Fu) << 4) | ((ihits >> 4) & 0x0Fu);
+        uint32_t tbits = 0;
+        uint32_t lh = hm & ~imask;
+        const unsigned long long meta = (static_cast<unsigned long long>(w1.w) << 32) | w1.z;
+        while (lh) {
+            const uint32_t c = uint32_t(__builtin_ctz(lh));
+            lh &= lh - 1u;
+            const uint32_t m = uint32_t(meta >> (8u * c)) & 0xFFu;
+            tbits |= ((1u << (m >> 5)) - 1u) << (m & 31u);
+        }
+        const uint32_t tbase = w1.y;
+        uint32_t gbase = w1.x;
+        uint32_t gword = (ihits << 24) | imask;
+        bool more = false;
+        while (true) {
+            if (gword >> 24) {
+                const uint32_t k = 31u - uint32_t(__builtin_clz(gword));
+                gword &= ~(1u << k);
+                const uint32_t slot = (k - 24u) ^ oct;
+                node = gbase + uint32_t(__builtin_popcount(gword & 0xFFu & ((1u << slot) - 1u)));
+                if (gword >> 24) {
+                    if (sp > 0) stack8_store(S, stk, sp - 1, tos);
+                    tos = make_uint2(gbase, gword);
+                    ++sp;
+                }
+                more = true;
+                break;
+            }
+            if (sp == 0) break;
+            gbase = tos.x;
+            gword = tos.y;
+            if (--sp > 0) tos = stack8_load(S, stk, sp - 1);
+        }
+        while (tbits) {
+            const uint32_t b = uint32_t(__builtin_ctz(tbits));
+            tbits &= tbits - 1u;
+            if (kCount) ++ntest;
+            const TriRec r = load_tri(S, tbase + b);
+            // one inlined test for both rays (the ray's fields selected), not two copies of the alpha test
+            uint32_t todo = live;
+#pragma nounroll
+            while (todo) {
+                const uint32_t j = uint32_t(__builtin_ctz(todo));
+                todo &= todo - 1u;
+                const bool jb = j != 0u;
+                const f3 o = jb ? Rb.o : Ra.o, d = jb ? Rb.d : Ra.d;
+                HitRec h;
+                if (test_tri_rec<true>(S, r, o, d, jb ? Rb.tmin : Ra.tmin, jb ? Rb.tmax : Ra.tmax, jb ? Rb.alpha : Ra.alpha, h)) {
+                    live &= ~(1u << j);
+                    occ |= 1u << j;
+                }
+            }
+            if (!live) return occ;
+        }
+        if (!more) return occ;
+    }
+}
+
+// DXRPT_SHADOW_PAIRS: a vertex's per-lane shadow rays go two slots at a time through traverse8_anyhit2
+// -- 1: in the split schedule's tails, 2: there and in k_path / k_bake (trace_path); 0: one slot at a
+// time through traverse8<true> everywhere.  Same answers either way.
+#ifndef DXRPT_SHADOW_PAIRS
+#define DXRPT_SHADOW_PAIRS 0
+#endif
+
 template <int W, bool kAnyHit, bool kCount, int kPipe = 0>
 PT_DEV bool traverse(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, lds_int* stk, HitRec& h,
                      uint32_t& nvisit, uint32_t& ntest, const NodeCache& nc = NodeCache{nullptr, 0u}) {
@@ -1375,6 +1507,40 @@ PT_DEV void emit_shadow(const KArgs& A, uint32_t pos, uint32_t& n, f3 o, f3 d, f
 }
 
 PT_DEV bool nonzero3(f3 c) { return !(c.x == 0.0f && c.y == 0.0f && c.z == 0.0f); }
+
+// A vertex's per-lane shadow rays in slots k0 .. nsh-1 (per-slot buffers at slot_p), two slots at a time
+// through traverse8_anyhit2 (the wave walks the pairs together); contribution * visibility is added to
+// rad in slot order -- the sum of the one-slot-at-a-time loop.  cnt: any-hit node / triangle fetches.
+template <bool kCount>
+PT_DEV void shadow_pairs(const KArgs& A, uint32_t slot_p, uint32_t k0, uint32_t nsh, lds_int* stk, float4& rad,
+                         uint32_t& nvisit, uint32_t& ntest) {
+    for (uint32_t k = k0; __ballot(k < nsh) != 0ull; k += 2u) {
+        const uint32_t live = (k < nsh ? 1u : 0u) | (k + 1u < nsh ? 2u : 0u);
+        const size_t sa = size_t(k) * A.F.qsize + slot_p, sb = sa + A.F.qsize;
+        RayLean Ra, Rb;
+        if (live & 1u) {
+            const float4 o4 = A.F.sh_org[sa], d4 = A.F.sh_dir[sa];
+            ray_lean_init(Ra, ld3(o4), ld3(d4), d4.w, o4.w, fbits(A.F.sh_con[sa].w) == 0u);
+        }
+        if (live & 2u) {
+            const float4 o4 = A.F.sh_org[sb], d4 = A.F.sh_dir[sb];
+            ray_lean_init(Rb, ld3(o4), ld3(d4), d4.w, o4.w, fbits(A.F.sh_con[sb].w) == 0u);
+        }
+        const uint32_t occ = traverse8_anyhit2<kCount>(A.S, Ra, Rb, live, stk, nvisit, ntest);
+        if (live & 1u) {
+            const float4 c4 = A.F.sh_con[sa];
+            rad.x += (occ & 1u) ? c4.x * 0.0f : c4.x;
+            rad.y += (occ & 1u) ? c4.y * 0.0f : c4.y;
+            rad.z += (occ & 1u) ? c4.z * 0.0f : c4.z;
+        }
+        if (live & 2u) {
+            const float4 c4 = A.F.sh_con[sb];
+            rad.x += (occ & 2u) ? c4.x * 0.0f : c4.x;
+            rad.y += (occ & 2u) ? c4.y * 0.0f : c4.y;
+            rad.z += (occ & 2u) ? c4.z * 0.0f : c4.z;
+        }
+    }
+}
 
 // Shadow ray kinds, in the order a vertex emits them (RayTrace.hlsl:224-262, 265-313, 415-425).
 constexpr int kShadowSun = 0, kShadowSpot = 1, kShadowSky = 2;
@@ -2101,6 +2267,30 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
             }
         }
         if (!DXRPT_DIAG_NO_SHADOW) shadow_rays_chained<kCount>(A, slot_p, k0, nsh, stk, rad, cnt, nc);
+#elif DXRPT_SHADOW_PAIRS >= 2
+        // slot 0 of a depth-1 vertex through the packet traversal (sun lanes), the rest two at a time
+        uint32_t k0 = 0;
+        if (d == 1 && (packet & 2u) && !DXRPT_DIAG_NO_SHADOW) {
+            const bool live = nsh > 0u;
+            float4 o4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d4 = make_float4(0.0f, 0.0f, 1.0f, 0.0f), c4 = o4;
+            if (live) {
+                o4 = A.F.sh_org[slot_p];
+                d4 = A.F.sh_dir[slot_p];
+                c4 = A.F.sh_con[slot_p];
+            }
+            HitRec hs;
+            bool occluded = traverse8_packet<true, kCount>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u,
+                                                           live && sun0, hs, 0u, nullptr, cnt + 2);
+            if (live && !sun0)
+                occluded = traverse<8, true, kCount, DXRPT_MEGA_PIPE_AH>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, stk, hs, cnt[2], cnt[3], nc);
+            if (live) {
+                rad.x += occluded ? c4.x * 0.0f : c4.x;
+                rad.y += occluded ? c4.y * 0.0f : c4.y;
+                rad.z += occluded ? c4.z * 0.0f : c4.z;
+            }
+            k0 = 1u;
+        }
+        if (!DXRPT_DIAG_NO_SHADOW) shadow_pairs<kCount>(A, slot_p, k0, nsh, stk, rad, cnt[2], cnt[3]);
 #else
         for (uint32_t k = 0; !DXRPT_DIAG_NO_SHADOW && __ballot(k < nsh) != 0ull; ++k) {
             const bool live = k < nsh;
@@ -2470,6 +2660,14 @@ PT_DEV void camera_path_group(const KArgs& A, uint32_t p, lds_int* stk, bool mem
 PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh, bool sun0, uint32_t packet,
                            float4& rad) {
     uint32_t nv = 0, nt = 0;
+#if DXRPT_SHADOW_PAIRS
+    // depth >= 2 (the tails: the sun and sky-visibility rays of the last vertex share their origin): two
+    // slots at a time.  The head (d == 1, a constant there) keeps the slot loop below.
+    if (d > 1) {
+        shadow_pairs<false>(A, slot_p, 0u, nsh, nullptr, rad, nv, nt);
+        return;
+    }
+#endif
     for (uint32_t k = 0; __ballot(k < nsh) != 0ull; ++k) {
         const bool live = k < nsh;
         const size_t slot = size_t(k) * A.F.qsize + slot_p;
