@@ -3133,15 +3133,17 @@ void k_path_tail(KArgs A, int d) {
         uint32_t nv = 0, nt = 0;
         traverse<8, false, false>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= set.MaxAnyHitPathLength, nullptr, h, nv, nt);
     }
-    // the rest of the path state comes back from the queue after the traversal
-    const float4 o4 = Q.org[pos], d4 = Q.dir[pos], t4 = Q.thr[pos], r4 = Q.rad[pos];
+    // the rest of the path state comes back from the queue after the traversal (the radiance so far only
+    // once the vertex is shaded: it is not live across path_vertex)
+    const float4 o4 = Q.org[pos], d4 = Q.dir[pos], t4 = Q.thr[pos];
+    const float rw = reinterpret_cast<const float*>(Q.rad + pos)[3];
     const uint32_t accumIdx = fbits(d4.w);
     VertexIn V;
     V.inOrigin = ld3(o4);
     V.inDir = ld3(d4);
     V.pathThr = ld3(t4);
     V.payloadRoughness = t4.w;
-    V.payloadIsDiffuse = (fbits(r4.w) & 1u) != 0u;
+    V.payloadIsDiffuse = (fbits(rw) & 1u) != 0u;
     V.pix = Q.pix[pos];
     V.hit = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
     VertexOut O;
@@ -3154,6 +3156,7 @@ void k_path_tail(KArgs A, int d) {
     const bool nextDiffuse = O.nextIsDiffuse;
     const int L = set.MaxPathLength < 2 ? 2 : set.MaxPathLength;
     const uint32_t qpos = d + 1 <= L - 1 ? split_push(A, d, cont, O, V.pix, accumIdx, j, nw) : 0u;
+    const float4 r4 = Q.rad[pos];
     float4 rad = make_float4(r4.x, r4.y, r4.z, 0.0f);
     rad.x += V.pathThr.x * O.local.x;
     rad.y += V.pathThr.y * O.local.y;
