@@ -784,3 +784,49 @@ def test_opacity_micromap_is_bit_identical(torch_cuda, name, L, anyhit, W, H, me
         t.set_option(A.OPT_MEGAKERNEL_LANES, A.DEFAULT_MEGAKERNEL_LANES)
         t.set_option(A.OPT_MEGAKERNEL_SPLIT, A.DEFAULT_MEGAKERNEL_SPLIT)
         t.set_option(A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)
+
+
+@pytest.mark.parametrize("world,rank,overlap", [(8, 5, 0), (8, 2, 1), (16, 3, 0)])
+def test_census_wave_clocks_small_frames(torch_cuda, world, rank, overlap):
+    # DXRPT_OPT_COUNT_TRAVERSAL + DXRPT_OPT_WAVE_CLOCKS on a frame of <= 400k paths (a GPU's band share:
+    # path groups when frames do not overlap): the census runs the 64-lane per-path kernel, records one
+    # stamp pair per 64 paths and nothing past them (the clock buffer is sized for
+    # ceil(paths / 64) waves); the frame equals the uninstrumented one, and the next uninstrumented
+    # frame reports no stale stamps.
+    torch = torch_cuda
+    W, H = 1920, 1080
+    sc, sky = scene_bundle("sponza")
+    st = sc.settings(MaxPathLength=3)
+    lay = band_layout(W, H, world)
+    tiles, n = lay.rank_tiles(rank), lay.counts[rank]
+    rtc = D.make_constants(sc, st, sky, W, H, 2)
+    lights = D.make_lights(sc)
+    t = DXRPathTracer(0)
+
+    def render():
+        acc = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
+        t.render_raw(rtc, st, acc.data_ptr(), W, H, tiles=tiles, stream=torch.cuda.current_stream().cuda_stream,
+                     lights=lights)
+        torch.cuda.synchronize()
+        return acc.cpu().numpy()
+
+    try:
+        t.initialize_scene(sc, sky)
+        t.build_rt_acceleration_structure()
+        t.set_option(A.OPT_FRAME_OVERLAP, overlap)
+        ref = render()
+        t.set_option(A.OPT_COUNT_TRAVERSAL, 1)
+        t.set_option(A.OPT_WAVE_CLOCKS, 1)
+        got = render()
+        s = t.stats()
+        wc = t.wave_clocks()
+        assert s.schedule & A.SCHED_CENSUS and s.paths_per_wave == 64, (s.schedule, s.paths_per_wave)
+        assert wc.shape == ((n + 63) // 64, 2), (wc.shape, n)
+        assert (wc[:, 0] > 0).all() and (wc[:, 1] >= wc[:, 0]).all()
+        np.testing.assert_array_equal(got, ref)
+        t.set_option(A.OPT_WAVE_CLOCKS, 0)
+        t.set_option(A.OPT_COUNT_TRAVERSAL, 0)
+        np.testing.assert_array_equal(render(), ref)
+        assert t.wave_clocks().shape[0] == 0  # no stale stamps from the census frame
+    finally:
+        t.close()
