@@ -68,6 +68,8 @@ struct DevBuf {
 constexpr uint64_t kSplitMinVertices = 8000000;
 constexpr uint64_t kSplitMinVerticesOverlap = 4000000;
 constexpr uint32_t kSplitPartsMaxPaths = 4000000;
+// Overlapped frames (DXRPT_OPT_FRAME_OVERLAP v): up to v + 1 frames in flight, v <= kMaxOverlapFrames - 1.
+constexpr uint32_t kMaxOverlapFrames = 3;
 
 }  // namespace
 
@@ -138,20 +140,20 @@ struct dxrpt_ctx {
         hipStream_t stream = nullptr;
         hipEvent_t done = nullptr;
     };
-    FramePart part[4];  // split halves 0, 1; overlapped frames: parity ov uses parts 2ov (and 2ov + 1)
+    FramePart part[2 * kMaxOverlapFrames];  // split halves 0, 1; overlapped frames: slot ov uses parts 2ov (and 2ov + 1)
     hipEvent_t part_fork = nullptr;
     std::vector<const uint32_t*> stat_counters;  // counter sets of the last frame (several with parts)
     uint32_t opt_tail_occ = 0;              // DXRPT_OPT_TAIL_OCCUPANCY (0 = the head's budget)
     uint32_t opt_omm = 1;                   // DXRPT_OPT_OPACITY_MICROMAP
-    // DXRPT_OPT_FRAME_OVERLAP: single-kernel megakernel frames alternate between the two FramePart
-    // streams/buffers (frame f on part f % 2) and stage their radiance (d_stage[f % 2]); the caller's
-    // stream blends the stage once the frame is done, so frame f+1's waves start while frame f drains
+    // DXRPT_OPT_FRAME_OVERLAP v: megakernel frames rotate over v + 1 slots of FramePart streams/buffers
+    // (frame f on slot f % (v + 1)) and stage their radiance (d_stage[slot]); the caller's stream blends
+    // the stage once the frame is done, so frame f+1's waves start while frame f drains
     uint32_t opt_overlap = 1;
     uint32_t opt_split_bins = 0;            // DXRPT_OPT_SPLIT_BINS
     uint32_t accum_extent = 0;  // 1 + the largest accumulation index of the current tile list (stage size)
-    DevBuf d_stage[2];
-    hipEvent_t stage_free[2] = {nullptr, nullptr};  // caller stream: the part's last stage has been blended
-    bool stage_used[2] = {false, false};
+    DevBuf d_stage[kMaxOverlapFrames];
+    hipEvent_t stage_free[kMaxOverlapFrames] = {};  // caller stream: the slot's last stage has been blended
+    bool stage_used[kMaxOverlapFrames] = {};
     hipEvent_t ovl_gate = nullptr;                   // the next overlapped frame waits for it (an order pass)
     bool ovl_gate_set = false;
     uint32_t ovl_parity = 0;
@@ -226,7 +228,7 @@ struct dxrpt_ctx {
             if (fp.done) (void)hipEventDestroy(fp.done);
         }
         if (part_fork) (void)hipEventDestroy(part_fork);
-        for (int k = 0; k < 2; ++k) {
+        for (uint32_t k = 0; k < kMaxOverlapFrames; ++k) {
             d_stage[k].release();
             if (stage_free[k]) (void)hipEventDestroy(stage_free[k]);
         }
@@ -725,7 +727,11 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
             require(value <= 1, "dxrpt_set_option: split bins must be 0 (off) or 1 (on)");
             ctx->opt_split_bins = uint32_t(value);
         } else if (option == DXRPT_OPT_FRAME_OVERLAP) {
-            require(value <= 1, "dxrpt_set_option: frame overlap must be 0 (off) or 1 (on)");
+            require(value < kMaxOverlapFrames, "dxrpt_set_option: frame overlap must be 0 (off), 1 (two frames in flight) or 2 (three)");
+            if (uint32_t(value) != ctx->opt_overlap) {  // the slot rotation restarts
+                drain_overlap(ctx);
+                ctx->ovl_parity = 0;
+            }
             ctx->opt_overlap = uint32_t(value);
         } else if (option == DXRPT_OPT_OPACITY_MICROMAP) {
             require(value <= 1, "dxrpt_set_option: opacity micromap must be 0 (off) or 1 (on)");
@@ -1183,7 +1189,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             const bool first = !ctx->ovl_inflight;
             if (first) {  // after non-overlapped work: start behind the caller's stream
                 HIP_CHECK(hipEventRecord(ctx->part_fork, s));
-                ctx->stage_used[0] = ctx->stage_used[1] = false;
+                for (bool& u : ctx->stage_used) u = false;
                 ctx->ovl_gate_set = false;
             }
             for (int k = 0; k < (halves ? 2 : 1); ++k) {
@@ -1287,7 +1293,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
                 fk.num_paths = cnt[k];
                 fk.path_base = base[k];
                 if (!overlap) HIP_CHECK(hipStreamWaitEvent(P.stream, ctx->part_fork, 0));
-                HIP_CHECK(launch_split_part(scene_dev(ctx, threads, overlap ? 4u : 2u, uint32_t(pb + k)), P.fb, fk, P.stream));
+                HIP_CHECK(launch_split_part(scene_dev(ctx, threads, overlap ? 2u * kMaxOverlapFrames : 2u, uint32_t(pb + k)), P.fb, fk, P.stream));
                 HIP_CHECK(hipEventRecord(P.done, P.stream));
                 HIP_CHECK(hipStreamWaitEvent(s, P.done, 0));
                 P.ctr_clean[cur] = false;
@@ -1304,7 +1310,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             P.fb.counters = cb + cur * kCounterWords;
             P.fb.counters_clean = P.ctr_clean[cur];
             P.fb.counters_next = cb + (1u - cur) * kCounterWords;  // zeroed in-kernel for this part's next frame
-            const SceneDev so = scene_dev(ctx, frame_traversal_threads(paths, 2u + nl, 0), 4u, uint32_t(pb));
+            const SceneDev so = scene_dev(ctx, frame_traversal_threads(paths, 2u + nl, 0), 2u * kMaxOverlapFrames, uint32_t(pb));
             HIP_CHECK(launch_frame(so, P.fb, fo, fs, ev, nullptr, nullptr, &sched));
             P.ctr_clean[cur] = false;
             P.ctr_clean[1u - cur] = true;
@@ -1338,7 +1344,9 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             uint32_t* cur = h + ctx->order_parity * 2 * kWaveClasses;
             uint32_t* nxt = h + (1u - ctx->order_parity) * 2 * kWaveClasses;
             // overlapped: the previous frame (the other part) may still read the order being rewritten
-            if (overlap && ctx->ovl_inflight) HIP_CHECK(hipStreamWaitEvent(fs, ctx->part[2 * (1 - ov)].done, 0));
+            if (overlap && ctx->ovl_inflight)  // every other slot's frame
+                for (uint32_t k = 0; k < kMaxOverlapFrames; ++k)
+                    if (int(k) != ov && ctx->stage_used[k]) HIP_CHECK(hipStreamWaitEvent(fs, ctx->part[2 * k].done, 0));
             HIP_CHECK(launch_wave_order(fp.wave_cost, cur, cur + kWaveClasses, nxt, nxt + kWaveClasses,
                                         ctx->d_wave_order.as<uint32_t>(), order_waves, fs));
             ctx->order_ready = true;
@@ -1357,7 +1365,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             HIP_CHECK(launch_accum_stage(fo, s));
             HIP_CHECK(hipEventRecord(ctx->stage_free[ov], s));
             ctx->stage_used[ov] = true;
-            ctx->ovl_parity ^= 1u;
+            ctx->ovl_parity = (ctx->ovl_parity + 1u) % (ctx->opt_overlap + 1u);
             ctx->ovl_inflight = true;
         }
         ctx->last_stream = s;

@@ -396,9 +396,9 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 #define DXRPT_OPT_SPLIT_BINS 38u     /* split frames: the compacting pushes bin surviving paths by screen region x
                                           direction octant of the continuation ray (1) instead of by
                                           producer wave only (0, default).  Identical results. */
-#define DXRPT_OPT_FRAME_OVERLAP 37u    /* 1 (default): consecutive single-kernel megakernel frames alternate
-                                          between two internal streams with their own path buffers and
-                                          stage their radiance; the caller's stream blends a frame's stage
+#define DXRPT_OPT_FRAME_OVERLAP 37u    /* 1 (default): consecutive megakernel frames alternate between two
+                                          internal streams with their own path buffers (2: rotate over
+                                          three, three frames in flight) and stage their radiance; the caller's stream blends a frame's stage
                                           (RaygenShader's progressive rule, RayTrace.hlsl:140-148) once it is
                                           done, so the next frame's waves fill the previous frame's drain.
                                           dxrpt_render still returns with every launch enqueued, and the

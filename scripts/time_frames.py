@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--msplit", type=int, default=None, help="DXRPT_OPT_MEGAKERNEL_SPLIT override (0 off, 1 on, 2 by size)")
     ap.add_argument("--tail-occ", type=int, default=None, help="DXRPT_OPT_TAIL_OCCUPANCY override")
     ap.add_argument("--omm", type=int, default=None, help="DXRPT_OPT_OPACITY_MICROMAP override")
-    ap.add_argument("--overlap", type=int, default=None, help="DXRPT_OPT_FRAME_OVERLAP override")
+    ap.add_argument("--overlap", type=int, default=None, help="DXRPT_OPT_FRAME_OVERLAP override (0 off, 1 two frames in flight, 2 three)")
     ap.add_argument("--bins", type=int, default=None, help="DXRPT_OPT_SPLIT_BINS override (split frames)")
     ap.add_argument("--parts", type=int, default=None, help="DXRPT_OPT_SPLIT_PARTS override (split frames)")
     ap.add_argument("--max-path", type=int, default=None, help="MaxPathLength override (a cost breakdown by depth)")

@@ -174,7 +174,7 @@ def test_overlapped_frames_are_bit_identical(torch_cuda, W, H, L, frames, share)
     consts = [D.make_constants(sc, st, sky, W, H, f % 16) for f in range(frames)]
     stream = torch.cuda.current_stream().cuda_stream
     out = []
-    for overlap in (0, 1):
+    for overlap in (0, 1, 2):  # one frame at a time, two / three frames in flight
         t = _fresh("sponza")
         try:
             t.set_option(A.OPT_FRAME_OVERLAP, overlap)
@@ -188,3 +188,4 @@ def test_overlapped_frames_are_bit_identical(torch_cuda, W, H, L, frames, share)
         finally:
             t.close()
     np.testing.assert_array_equal(out[1], out[0])
+    np.testing.assert_array_equal(out[2], out[0])
