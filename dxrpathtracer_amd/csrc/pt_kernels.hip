@@ -2112,6 +2112,14 @@ PT_DEV void count_rays(uint32_t* counters, uint32_t n) {
 #ifndef DXRPT_MEGA_PIPE_AH
 #define DXRPT_MEGA_PIPE_AH 0
 #endif
+// The same traversal pipelining (traverse8_pipe kPipe bits) for the split schedule's per-lane closest hit
+// (k_path_tail) and per-lane shadow rays (vertex_shadows), separately.
+#ifndef DXRPT_SPLIT_PIPE_CH
+#define DXRPT_SPLIT_PIPE_CH 0
+#endif
+#ifndef DXRPT_SPLIT_PIPE_AH
+#define DXRPT_SPLIT_PIPE_AH 0
+#endif
 
 // DXRPT_CHAIN_SHADOWS: a lane's per-lane shadow rays (slots k0 .. n-1) are traced back to back in ONE
 // loop -- a lane that finishes ray k starts ray k+1 at its next step, instead of idling until the
@@ -2683,7 +2691,7 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
         if (pk)
             occluded = traverse8_packet<true, false>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live && sun0, hs);
         if (live && !(pk && sun0))
-            occluded = traverse<8, true, false>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, nullptr, hs, nv, nt);
+            occluded = traverse<8, true, false, DXRPT_SPLIT_PIPE_AH>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, nullptr, hs, nv, nt);
         if (live) {
             rad.x += occluded ? c4.x * 0.0f : c4.x;
             rad.y += occluded ? c4.y * 0.0f : c4.y;
@@ -3131,7 +3139,7 @@ void k_path_tail(KArgs A, int d) {
     {
         const float4 o4 = Q.org[pos], d4 = Q.dir[pos];
         uint32_t nv = 0, nt = 0;
-        traverse<8, false, false>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= set.MaxAnyHitPathLength, nullptr, h, nv, nt);
+        traverse<8, false, false, DXRPT_SPLIT_PIPE_CH>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= set.MaxAnyHitPathLength, nullptr, h, nv, nt);
     }
     // the rest of the path state comes back from the queue after the traversal (the radiance so far only
     // once the vertex is shaded: it is not live across path_vertex)
