@@ -2113,9 +2113,11 @@ PT_DEV void count_rays(uint32_t* counters, uint32_t n) {
 #define DXRPT_MEGA_PIPE_AH 0
 #endif
 // The same traversal pipelining (traverse8_pipe kPipe bits) for the split schedule's per-lane closest hit
-// (k_path_tail) and per-lane shadow rays (vertex_shadows), separately.
+// (k_path_tail) and per-lane shadow rays (vertex_shadows), separately.  r03 A/B
+// (profiles/r03_ab_split_pipe.txt): closest-hit triangle pairs (1) -0.8..-1.0 % on the metric, C3, C4 and
+// C5's share; the next-node prefetch (2, 3) and any-hit pairs / prefetch lose 3-35 %.
 #ifndef DXRPT_SPLIT_PIPE_CH
-#define DXRPT_SPLIT_PIPE_CH 0
+#define DXRPT_SPLIT_PIPE_CH 1
 #endif
 #ifndef DXRPT_SPLIT_PIPE_AH
 #define DXRPT_SPLIT_PIPE_AH 0
