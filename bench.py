@@ -243,8 +243,20 @@ def main():
 
     # frame-end gather of the band slabs to rank 0 (RCCL), overlapped with the next frame's render
     pg = None
+    gather_used = None
     if world > 1:
-        pg = NativeGather(lay, rank, local_rank, full) if args.gather == "native" else PipelinedGather(lay, rank, full, idx)
+        gather_used = args.gather
+        if args.gather == "native":
+            try:
+                pg = NativeGather(lay, rank, local_rank, full)
+            except RuntimeError as e:  # e.g. an RCCL communicator that cannot be built on this node
+                # every rank takes the same branch (dxrpt_comm_create is collective: it fails on all ranks)
+                log(f"native gather unavailable ({e}); falling back to torch.distributed.gather")
+                gather_used = f"torch (native failed: {e})"
+        if pg is None:
+            if idx is None and rank == 0:
+                idx = torch.tensor(source_index(lay), dtype=torch.long, device="cuda")
+            pg = PipelinedGather(lay, rank, full, idx)
 
     def frame(f):
         tracer.render_raw(consts[f % 16], settings, accum.data_ptr(), WIDTH, HEIGHT, tiles=tiles, stream=sh,
@@ -384,7 +396,7 @@ def main():
             "config": {"workload": f"{SCENE}-proxy {WIDTH}x{HEIGHT} L={PATH_LENGTH} 1spp/frame progressive",
                        "width": WIDTH, "height": HEIGHT, "max_path_length": PATH_LENGTH,
                        "sqrt_num_samples": 4, "triangles": scene.num_triangles, "sky": sky.model,
-                       "parallelism": (f"screen {args.layout} x{world} + RCCL gather ({args.gather})" if world > 1
+                       "parallelism": (f"screen {args.layout} x{world} + RCCL gather ({gather_used})" if world > 1
                                        else "single GPU")},
             "roofline": {"bound": bound, "roofline_kind": "hbm",
                          "kernel": ("k_path_head + k_path_tail (one frame)" if roof_kernel == "k_path" and stats.schedule & A.SCHED_SPLIT

@@ -211,13 +211,27 @@ class NativeGather:
         self.layout, self.rank, self.full = layout, rank, full
         self.L = A.lib()
         uid = C.create_string_buffer(A.DXRPT_COMM_ID_BYTES)
+        # failures are made collective, so every rank raises together (a caller may then fall back to
+        # another gather) instead of the other ranks blocking in the next collective
+        obj = [None]
         if rank == 0:
-            self._check(self.L.dxrpt_comm_unique_id(uid), "dxrpt_comm_unique_id")
-        obj = [bytes(uid.raw) if rank == 0 else None]
+            rc = self.L.dxrpt_comm_unique_id(uid)
+            obj = [bytes(uid.raw) if rc == A.DXRPT_OK else ("error", self._msg(rc))]
         dist.broadcast_object_list(obj, src=0, group=group)
+        if isinstance(obj[0], tuple):
+            raise RuntimeError(f"dxrpt_comm_unique_id failed on rank 0: {obj[0][1]}")
         uid = C.create_string_buffer(obj[0], A.DXRPT_COMM_ID_BYTES)
         self.comm = C.c_void_p()
-        self._check(self.L.dxrpt_comm_create(device, layout.world, rank, uid, C.byref(self.comm)), "dxrpt_comm_create")
+        rc = self.L.dxrpt_comm_create(device, layout.world, rank, uid, C.byref(self.comm))
+        ok = [rc == A.DXRPT_OK]
+        oks = [None] * layout.world
+        dist.all_gather_object(oks, ok[0], group=group)
+        if not all(oks):
+            if rc == A.DXRPT_OK:
+                self.L.dxrpt_comm_destroy(self.comm)
+            self.comm = C.c_void_p()
+            raise RuntimeError(f"dxrpt_comm_create failed on ranks {[r for r, v in enumerate(oks) if not v]}: "
+                               f"{self._msg(rc) if rc != A.DXRPT_OK else 'see those ranks'}")
         self.counts = (C.c_uint64 * layout.world)(*layout.counts)
         self.tiles = gathered_tiles(layout)
         self.tarr = (A.Tile * len(self.tiles))(*self.tiles)
@@ -228,10 +242,13 @@ class NativeGather:
         self.pending = None
         self.count = 0
 
+    def _msg(self, rc):
+        msg = self.L.dxrpt_multi_last_error()
+        return f"({rc}) {msg.decode() if msg else ''}"
+
     def _check(self, rc, what):
         if rc != A.DXRPT_OK:
-            msg = self.L.dxrpt_multi_last_error()
-            raise RuntimeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+            raise RuntimeError(f"{what} failed {self._msg(rc)}")
 
     def submit(self, local):
         import ctypes as C

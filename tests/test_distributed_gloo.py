@@ -165,3 +165,39 @@ def test_tile_array_matches_rank_tiles():
         assert sum(t.w * t.h for t in gt) == lay.width * lay.height
         ends = sorted((t.accum_offset, t.accum_offset + t.h * t.accum_pitch) for t in gt)
         assert ends[0][0] == 0 and all(a[1] <= b[0] for a, b in zip(ends, ends[1:]))
+
+
+def _worker_native_fail(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dxrpathtracer_amd.distributed import NativeGather, band_layout
+        try:
+            NativeGather(band_layout(64, 32, world), rank, 0, None)
+            q.put((rank, "built"))
+        except RuntimeError as e:
+            q.put((rank, "raised", str(e)[:200]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="needs a host without a usable GPU (the RCCL communicator must fail)")
+def test_native_gather_failure_is_collective():
+    # On a host where the RCCL communicator cannot be built, NativeGather raises on EVERY rank (rank 0's
+    # unique-id failure is broadcast, dxrpt_comm_create's result is all-gathered) instead of leaving the
+    # other ranks blocked in the next collective -- so bench.py can fall back to torch.distributed.gather.
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_native_fail, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    got = sorted(q.get(timeout=10) for _ in range(world))
+    assert [g[:2] for g in got] == [(r, "raised") for r in range(world)], got
