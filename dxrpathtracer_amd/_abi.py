@@ -84,7 +84,7 @@ KERNEL_NAMES = ("k_raygen", "k_trace", "k_shade", "k_shadow", "k_accumulate", "k
  OPT_KERNEL_TIMING_MASK, OPT_XCD_MAPPING, OPT_PACKET_SWITCH, OPT_MEGAKERNEL_PATHS, OPT_MEGAKERNEL_OCCUPANCY,
  OPT_BAKE_CHUNK, OPT_MEGAKERNEL_PERSISTENT, OPT_MEGAKERNEL_LANES, OPT_WAVE_CLOCKS,
  OPT_WAVE_ORDER, OPT_SPLIT_UNITS, OPT_XCD_CHUNK, OPT_WAVE_ORDER_PERIOD, OPT_MEGAKERNEL_SPLIT,
- OPT_TAIL_OCCUPANCY, OPT_SPLIT_PARTS, OPT_OPACITY_MICROMAP, OPT_FRAME_OVERLAP, OPT_SPLIT_BINS) = range(1, 39)
+ OPT_TAIL_OCCUPANCY, OPT_SPLIT_PARTS, OPT_OPACITY_MICROMAP, OPT_FRAME_OVERLAP, OPT_SPLIT_BINS, OPT_SPLIT_ALPHA) = range(1, 40)
 # context defaults of the traversal options (dxrpt_api.hip)
 DEFAULT_TRAVERSAL_PIPELINE = 0
 POST_FLOAT4, POST_RGBA8 = 0, 1  # dxrpt_post_process output formats

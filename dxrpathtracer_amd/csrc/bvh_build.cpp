@@ -203,6 +203,7 @@ struct SpatialBuilder {
         Box box;
     };
     const float* pos = nullptr;  // ntris * 9
+    const uint8_t* keep_whole = nullptr;  // per triangle: never split (BvhBuildParams::keep_whole)
     std::vector<TNode> tree;
     std::vector<uint32_t> refs;  // leaf order, duplicates allowed
     uint32_t depth_cap = 32;
@@ -320,6 +321,14 @@ struct SpatialBuilder {
             Box bb[kBins];
             uint32_t enter[kBins] = {}, exit_[kBins] = {};
             for (const Ref& r : rs) {
+                if (keep_whole && keep_whole[r.tri]) {  // goes whole to the side of its centroid
+                    int c = int((0.5f * (r.box.lo[ax] + r.box.hi[ax]) - lo) / bs);
+                    c = std::min(std::max(c, 0), kBins - 1);
+                    bb[c].grow(r.box);
+                    enter[c]++;
+                    exit_[c]++;
+                    continue;
+                }
                 int b0 = int((r.box.lo[ax] - lo) / bs), b1 = int((r.box.hi[ax] - lo) / bs);
                 b0 = std::min(std::max(b0, 0), kBins - 1);
                 b1 = std::min(std::max(b1, b0), kBins - 1);
@@ -421,8 +430,9 @@ struct SpatialBuilder {
                         else if (r.box.lo[ss.axis] >= ss.plane) R.push_back(r);
                         else {
                             Box bl, br;
-                            split_ref(r, ss.axis, ss.plane, bl, br);
-                            if (!bl.empty() && !br.empty() && bl.lo[ss.axis] <= bl.hi[ss.axis] && br.lo[ss.axis] <= br.hi[ss.axis]) {
+                            const bool whole = keep_whole && keep_whole[r.tri];
+                            if (!whole) split_ref(r, ss.axis, ss.plane, bl, br);
+                            if (!whole && !bl.empty() && !br.empty() && bl.lo[ss.axis] <= bl.hi[ss.axis] && br.lo[ss.axis] <= br.hi[ss.axis]) {
                                 L.push_back(Ref{r.tri, bl});
                                 R.push_back(Ref{r.tri, br});
                                 live_refs++;
@@ -857,6 +867,7 @@ bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildRe
         const std::vector<uint32_t>* refs = &B.refs;
         if (spatial) {
             SB.pos = tri_positions;
+            SB.keep_whole = params ? params->keep_whole : nullptr;
             SB.depth_cap = cap;
             SB.ref_budget = size_t(double(ntris) * (params ? params->ref_budget : BvhBuildParams().ref_budget));
             if (!SB.build(ntris, B.tri_box, err)) return false;

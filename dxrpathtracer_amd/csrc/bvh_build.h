@@ -31,6 +31,9 @@ struct BvhBuildParams {
     double ref_budget = 1.5;        // BVH8: maximum triangle references / triangles with spatial splits
     double leaf_cost = 1.5;         // BVH8 collapse: SAH cost of a triangle test relative to a node visit
                                     // (latency-bound traversal: each test is a dependent memory round trip)
+    // per global triangle, non-zero: never cut by a spatial split (an alpha-tested triangle: every extra
+    // reference is another opacity test); null: every triangle may be split
+    const uint8_t* keep_whole = nullptr;
 };
 
 // tri_positions: ntris * 9 floats (v0.xyz, v1.xyz, v2.xyz) in global triangle order.

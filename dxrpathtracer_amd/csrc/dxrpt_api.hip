@@ -150,6 +150,7 @@ struct dxrpt_ctx {
     // the stage once the frame is done, so frame f+1's waves start while frame f drains
     uint32_t opt_overlap = 1;
     uint32_t opt_split_bins = 0;            // DXRPT_OPT_SPLIT_BINS
+    uint32_t opt_split_alpha = 1;           // DXRPT_OPT_SPLIT_ALPHA
     uint32_t accum_extent = 0;  // 1 + the largest accumulation index of the current tile list (stage size)
     DevBuf d_stage[kMaxOverlapFrames];
     hipEvent_t stage_free[kMaxOverlapFrames] = {};  // caller stream: the slot's last stage has been blended
@@ -723,6 +724,9 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_SPLIT_PARTS) {
             require(value <= 2, "dxrpt_set_option: split parts must be 0 (by frame size), 1 or 2");
             ctx->opt_split_parts = uint32_t(value);
+        } else if (option == DXRPT_OPT_SPLIT_ALPHA) {
+            require(value <= 1, "dxrpt_set_option: split alpha must be 0 or 1");
+            ctx->opt_split_alpha = uint32_t(value);  // takes effect at the next dxrpt_build_bvh
         } else if (option == DXRPT_OPT_SPLIT_BINS) {
             require(value <= 1, "dxrpt_set_option: split bins must be 0 (off) or 1 (on)");
             ctx->opt_split_bins = uint32_t(value);
@@ -873,7 +877,17 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
         }
         BvhBuildResult res;
         std::string err;
-        if (!build_bvh(pos.data(), ntris, ctx->opt_width, res, err, &ctx->build_params))
+        // DXRPT_OPT_SPLIT_ALPHA 0: spatial splits leave alpha-tested triangles whole (each extra reference
+        // of one is another AnyHitShader opacity test)
+        std::vector<uint8_t> keep_whole;
+        BvhBuildParams bp = ctx->build_params;
+        if (!ctx->opt_split_alpha) {
+            keep_whole.resize(ntris);
+            for (uint32_t t = 0; t < ntris; ++t)
+                keep_whole[t] = ctx->mats[ctx->geos[tri_geom[t]].MaterialIdx].Opacity != DXRPT_INVALID_INDEX ? 1u : 0u;
+            bp.keep_whole = keep_whole.data();
+        }
+        if (!build_bvh(pos.data(), ntris, ctx->opt_width, res, err, &bp))
             throw ApiError(DXRPT_E_INVALID_ARG, err);
         // one record per leaf reference (BVH8 spatial splits may reference a triangle more than once)
         const uint32_t nrefs = uint32_t(res.tri_order.size());

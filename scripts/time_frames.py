@@ -41,6 +41,9 @@ def main():
     ap.add_argument("--tail-occ", type=int, default=None, help="DXRPT_OPT_TAIL_OCCUPANCY override")
     ap.add_argument("--omm", type=int, default=None, help="DXRPT_OPT_OPACITY_MICROMAP override")
     ap.add_argument("--overlap", type=int, default=None, help="DXRPT_OPT_FRAME_OVERLAP override (0 off, 1 two frames in flight, 2 three)")
+    ap.add_argument("--leaf-cost", type=int, default=None, help="DXRPT_OPT_LEAF_COST before the BVH build (percent)")
+    ap.add_argument("--spatial", type=int, default=None, help="DXRPT_OPT_SPATIAL_SPLITS before the BVH build (percent)")
+    ap.add_argument("--split-alpha", type=int, default=None, help="DXRPT_OPT_SPLIT_ALPHA before the BVH build")
     ap.add_argument("--bins", type=int, default=None, help="DXRPT_OPT_SPLIT_BINS override (split frames)")
     ap.add_argument("--parts", type=int, default=None, help="DXRPT_OPT_SPLIT_PARTS override (split frames)")
     ap.add_argument("--max-path", type=int, default=None, help="MaxPathLength override (a cost breakdown by depth)")
@@ -87,6 +90,12 @@ def main():
         t.set_option(A.OPT_SPLIT_PARTS, args.parts)
     if args.bins is not None:
         t.set_option(A.OPT_SPLIT_BINS, args.bins)
+    if args.leaf_cost is not None:
+        t.set_option(A.OPT_LEAF_COST, args.leaf_cost)
+    if args.spatial is not None:
+        t.set_option(A.OPT_SPATIAL_SPLITS, args.spatial)
+    if args.split_alpha is not None:
+        t.set_option(A.OPT_SPLIT_ALPHA, args.split_alpha)
     t.initialize_scene(sc, sky)
     t.build_rt_acceleration_structure()
     tiles, n = None, W * H
@@ -143,7 +152,7 @@ def main():
         torch.cuda.synchronize()
         rounds.append(a.elapsed_time(b) / args.frames)
     s = t.stats()
-    print(f"{args.label:24s} {args.config}{'' if args.max_path is None else f' L={L}'}{'' if args.wave_order is None else f' order={args.wave_order}'}{'' if args.split is None else f' split={args.split}'}{'' if args.xcd_chunk is None else f' xcd={args.xcd_chunk}'}{'' if args.mega_paths is None else f' mega={args.mega_paths}'}{'' if args.order_period is None else f' period={args.order_period}'}{'' if args.msplit is None else f' msplit={args.msplit}'}{'' if args.occ is None else f' occ={args.occ}'}{'' if args.tail_occ is None else f' tocc={args.tail_occ}'}{'' if args.omm is None else f' omm={args.omm}'}{'' if args.overlap is None else f' ovl={args.overlap}'}{'' if args.parts is None else f' parts={args.parts}'}{'' if args.bins is None else f' bins={args.bins}'} share 1/{args.share} r{args.rank} {args.layout if args.share > 1 else ''}{args.band or ''}{' tile ' + args.tile if args.tile else ''}: median {statistics.median(rounds):.4f} "
+    print(f"{args.label:24s} {args.config}{'' if args.max_path is None else f' L={L}'}{'' if args.wave_order is None else f' order={args.wave_order}'}{'' if args.split is None else f' split={args.split}'}{'' if args.xcd_chunk is None else f' xcd={args.xcd_chunk}'}{'' if args.mega_paths is None else f' mega={args.mega_paths}'}{'' if args.order_period is None else f' period={args.order_period}'}{'' if args.msplit is None else f' msplit={args.msplit}'}{'' if args.occ is None else f' occ={args.occ}'}{'' if args.tail_occ is None else f' tocc={args.tail_occ}'}{'' if args.omm is None else f' omm={args.omm}'}{'' if args.overlap is None else f' ovl={args.overlap}'}{'' if args.parts is None else f' parts={args.parts}'}{'' if args.bins is None else f' bins={args.bins}'}{'' if args.leaf_cost is None else f' leaf={args.leaf_cost}'}{'' if args.spatial is None else f' sbvh={args.spatial}'}{'' if args.split_alpha is None else f' salpha={args.split_alpha}'} share 1/{args.share} r{args.rank} {args.layout if args.share > 1 else ''}{args.band or ''}{' tile ' + args.tile if args.tile else ''}: median {statistics.median(rounds):.4f} "
           f"mean {statistics.mean(rounds):.4f} min {min(rounds):.4f} ms/frame  rays {s.radiance_rays + s.shadow_rays} sched {s.schedule} ppw {s.paths_per_wave}",
           flush=True)
     if args.phases:
