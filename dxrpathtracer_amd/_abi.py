@@ -111,6 +111,7 @@ DEFAULT_MEGAKERNEL_SPLIT = 2  # by frame size
 DEFAULT_SPLIT_PARTS = 0  # by frame size
 DEFAULT_TAIL_OCCUPANCY = 0
 DEFAULT_SPLIT_BINS = 0
+DEFAULT_SPLIT_ALPHA = 0
 
 
 class Stats(C.Structure):

@@ -150,7 +150,10 @@ struct dxrpt_ctx {
     // the stage once the frame is done, so frame f+1's waves start while frame f drains
     uint32_t opt_overlap = 1;
     uint32_t opt_split_bins = 0;            // DXRPT_OPT_SPLIT_BINS
-    uint32_t opt_split_alpha = 1;           // DXRPT_OPT_SPLIT_ALPHA
+    // DXRPT_OPT_SPLIT_ALPHA (r03: 0 -- alpha-tested triangles stay whole: metric 1.867 -> 1.823 ms, C4
+    // 2.006 -> 1.980, C3 5.54 -> 5.45, C2 0.902 -> 0.882, 1/2 share -2.4 %; the 1/8 shares' mean is
+    // unchanged and their maximum +2-3 %, profiles/r03_ab_split_alpha*.txt)
+    uint32_t opt_split_alpha = 0;
     uint32_t accum_extent = 0;  // 1 + the largest accumulation index of the current tile list (stage size)
     DevBuf d_stage[kMaxOverlapFrames];
     hipEvent_t stage_free[kMaxOverlapFrames] = {};  // caller stream: the slot's last stage has been blended

@@ -393,8 +393,9 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 #define DXRPT_OPT_TAIL_OCCUPANCY 34u   /* register budget of the split schedule's tail kernels in waves/SIMD:
                                           0 = by default 7 (the head's 6, or DXRPT_OPT_MEGAKERNEL_OCCUPANCY
                                           when set), 4..8 */
-#define DXRPT_OPT_SPLIT_ALPHA 39u    /* BVH8 build: 1 (default) spatial splits may cut alpha-tested triangles;
-                                          0: they stay whole (each reference of one costs an opacity test).
+#define DXRPT_OPT_SPLIT_ALPHA 39u    /* BVH8 build: 0 (default) spatial splits leave alpha-tested triangles
+                                          whole (each reference of one costs an opacity test); 1: they
+                                          may cut them like any other triangle.
                                           Takes effect at the next dxrpt_build_bvh.  Identical results. */
 #define DXRPT_OPT_SPLIT_BINS 38u     /* split frames: the compacting pushes bin surviving paths by screen region x
                                           direction octant of the continuation ray (1) instead of by
