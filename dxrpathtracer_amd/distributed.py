@@ -55,6 +55,49 @@ def band_layout(width: int, height: int, world: int, band: int = BAND_ROWS) -> B
     return BandLayout(width, height, world, band, tiles, counts, max(counts))
 
 
+def balanced_band_layout(width: int, height: int, world: int, band_costs, band: int = BAND_ROWS) -> BandLayout:
+    """Cost-balanced bands: the same `band`-row bands as band_layout, dealt by measured cost instead of
+    round robin -- costliest band first, each to the rank with the least cost so far (LPT; ties to the
+    lower rank), so every rank's share costs about the same.  With overlapped frames a share's time per
+    frame is its throughput (the sum of its waves' durations over the resident slots), so equal cost
+    sums mean equal times, where round robin leaves the rank holding the dense-geometry rows slowest
+    (profiles/r03_shares_all_ranks.txt).  `band_costs[b]`: cost of band b (rows b*band ..), e.g. the
+    summed wave durations of one census frame (band_costs_from_wave_clocks).  Each rank renders its bands
+    in image order; slabs may differ in size (counts)."""
+    nb = (height + band - 1) // band
+    if len(band_costs) != nb:
+        raise ValueError(f"band_costs has {len(band_costs)} entries, the image has {nb} bands")
+    load = [0.0] * world
+    owner = [0] * nb
+    for b in sorted(range(nb), key=lambda k: (-float(band_costs[k]), k)):
+        r = min(range(world), key=lambda q: (load[q], q))
+        owner[b] = r
+        load[r] += float(band_costs[b])
+    tiles = [[] for _ in range(world)]
+    counts = [0] * world
+    for b, y0 in enumerate(range(0, height, band)):
+        r = owner[b]
+        h = min(band, height - y0)
+        tiles[r].append(A.Tile(0, y0, width, h, counts[r], width, 0))
+        counts[r] += width * h
+    return BandLayout(width, height, world, band, tiles, counts, max(counts))
+
+
+def band_costs_from_wave_clocks(width: int, height: int, wave_clocks, band: int = BAND_ROWS):
+    """Per-band cost from the (start, end) stamps of a full-frame census frame (DXRPathTracer.wave_clocks:
+    wave w = the w-th 8x8 pixel block in raster order): the summed durations of the blocks in each band."""
+    bw = (width + 7) // 8
+    bh = (height + 7) // 8
+    per_block_row = [0.0] * bh
+    for w, (t0, t1) in enumerate(wave_clocks):
+        row = w // bw
+        if row < bh:
+            per_block_row[row] += float(int(t1) - int(t0))
+    rows_per_band = band // 8
+    nb = (height + band - 1) // band
+    return [sum(per_block_row[b * rows_per_band:(b + 1) * rows_per_band]) for b in range(nb)]
+
+
 def _mix64(x: int) -> int:
     """splitmix64 finaliser: the partition's only source of pseudo-randomness (deterministic)."""
     x = (x + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF

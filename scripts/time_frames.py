@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--share", type=int, default=1)
     ap.add_argument("--rank", type=int, default=0)
-    ap.add_argument("--layout", default="bands", choices=["blocks", "bands", "blocks-raster", "blocks-lpt"],
+    ap.add_argument("--layout", default="bands", choices=["blocks", "bands", "blocks-raster", "blocks-lpt", "bands-balanced"],
                     help="screen partition of --share (blocks-raster: 8x8 tiles in raster order, block k -> rank k %% N)")
     ap.add_argument("--any-hit", type=int, default=None, help="MaxAnyHitPathLength override")
     ap.add_argument("--packet", type=int, default=None, help="DXRPT_OPT_PACKET_TRAVERSAL override")
@@ -128,6 +128,20 @@ def main():
             tiles = [AA.Tile(t.x0, t.y0, 8, 8, 64 * k, 8, 0) for k, t in enumerate(tiles)]
         n = 64 * len(tiles)
         tiles = (AA.Tile * len(tiles))(*tiles)
+    elif args.layout == "bands-balanced" and args.share > 1:  # bands dealt by one census frame's costs
+        import numpy as np
+        from dxrpathtracer_amd.distributed import balanced_band_layout, band_costs_from_wave_clocks
+        acc0 = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+        t.set_option(A.OPT_COUNT_TRAVERSAL, 1)
+        t.set_option(A.OPT_WAVE_CLOCKS, 1)
+        t.render_raw(D.make_constants(sc, st, sky, W, H, 0), st, acc0.data_ptr(), W, H,
+                     stream=torch.cuda.current_stream().cuda_stream, lights=D.make_lights(sc))
+        torch.cuda.synchronize()
+        costs = band_costs_from_wave_clocks(W, H, t.wave_clocks())
+        t.set_option(A.OPT_WAVE_CLOCKS, 0)
+        t.set_option(A.OPT_COUNT_TRAVERSAL, 0)
+        lay = balanced_band_layout(W, H, args.share, costs)
+        tiles, n = lay.tile_array(args.rank), lay.counts[args.rank]
     elif args.share > 1:
         from dxrpathtracer_amd.distributed import band_layout
         lay = (band_layout(W, H, args.share, args.band) if args.layout == "bands" and args.band
