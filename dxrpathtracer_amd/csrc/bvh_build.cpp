@@ -40,7 +40,13 @@ struct Box {
     }
 };
 
-constexpr int kBins = 32;
+#ifndef DXRPT_BVH_BINS
+#define DXRPT_BVH_BINS 32
+#endif
+#ifndef DXRPT_SBVH_ALPHA
+#define DXRPT_SBVH_ALPHA 1e-5
+#endif
+constexpr int kBins = DXRPT_BVH_BINS;  // SAH bins per axis (object and spatial splits)
 constexpr uint32_t kMaxDepth2 = kTraversalStack;  // a BVH2 node at depth d has <= d stack entries above it
 
 // Generic binary tree node.
@@ -208,7 +214,7 @@ struct SpatialBuilder {
     std::vector<uint32_t> refs;  // leaf order, duplicates allowed
     uint32_t depth_cap = 32;
     double root_area = 1.0;
-    double alpha = 1e-5;         // overlap / root area that enables a spatial search
+    double alpha = DXRPT_SBVH_ALPHA;  // overlap / root area that enables a spatial search
     size_t ref_budget = 0;       // maximum live references (duplication budget)
     size_t live_refs = 0;
     double sah = 0.0;            // binary tree, C_trav = 1, C_tri = 1, relative to the root area
