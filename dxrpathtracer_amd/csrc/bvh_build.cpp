@@ -601,6 +601,9 @@ struct Emit8 {
     std::vector<double> cost;     // [n * 8 + i], i in 1..7 (index 0: D(n, 8) for the node case)
     std::vector<uint8_t> pick;    // [n * 8 + i]: i == 1: 0 leaf / 1 node; i >= 2: 0 = use C(n, i-1), k = split
     std::vector<uint8_t> dsplit;  // k of D(n, 8)
+    // test-cost weight prefix over `refs` (leaf order): a binary node's triangle cost is
+    // wsum[end] - wsum[begin] (alpha-tested references weigh BvhBuildParams::alpha_cost); empty: counts
+    std::vector<double> wsum;
 
     static uint32_t ntris(const TNode& n) { return n.end - n.begin; }
     bool is_leaf(int32_t t) const { return pick[size_t(t) * 8 + 1] == 0; }
@@ -617,7 +620,8 @@ struct Emit8 {
             const double A = n.box.area();
             double* C = &cost[ni * 8];
             uint8_t* P = &pick[ni * 8];
-            const double leaf = ntris(n) <= uint32_t(kMaxLeafTris8) ? A * kCPrim * double(ntris(n)) : DBL_MAX;
+            const double w = wsum.empty() ? double(ntris(n)) : wsum[n.end] - wsum[n.begin];
+            const double leaf = ntris(n) <= uint32_t(kMaxLeafTris8) ? A * kCPrim * w : DBL_MAX;
             if (n.count) {  // binary leaf
                 for (int i = 1; i < 8; ++i) { C[i] = leaf; P[i] = 0; }
                 C[0] = DBL_MAX;
@@ -885,7 +889,12 @@ bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildRe
             B.depth_cap = cap;
             if (!B.build(ntris, err, sah)) return false;
         }
-        Emit8 E{*tree, *refs, pad, {}, {}, 0, 0, 1.0, params ? params->leaf_cost : BvhBuildParams().leaf_cost, {}, {}, {}, {}};
+        Emit8 E{*tree, *refs, pad, {}, {}, 0, 0, 1.0, params ? params->leaf_cost : BvhBuildParams().leaf_cost, {}, {}, {}, {}, {}};
+        if (params && params->alpha_tri && params->alpha_cost != 1.0) {
+            E.wsum.assign(refs->size() + 1, 0.0);
+            for (size_t i = 0; i < refs->size(); ++i)
+                E.wsum[i + 1] = E.wsum[i] + (params->alpha_tri[(*refs)[i]] ? params->alpha_cost : 1.0);
+        }
         E.run();
         last_depth = E.max_depth;
         if (E.max_depth > max_depth8) continue;

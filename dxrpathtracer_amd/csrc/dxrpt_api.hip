@@ -61,6 +61,11 @@ struct DevBuf {
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
+// BVH8 collapse: an alpha-tested triangle's test priced this many opaque tests (BvhBuildParams::alpha_cost)
+#ifndef DXRPT_ALPHA_TRI_COST
+#define DXRPT_ALPHA_TRI_COST 1.0
+#endif
+
 // Depth-split schedule by frame size (DXRPT_OPT_MEGAKERNEL_SPLIT 2): frames of at least this many path
 // vertices (paths x (L - 1)); two concurrent parts up to kSplitPartsMaxPaths paths (DXRPT_OPT_SPLIT_PARTS 0).
 // Overlapped frames (DXRPT_OPT_FRAME_OVERLAP): from kSplitMinVerticesOverlap, one part -- the next frame
@@ -882,14 +887,13 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
         std::string err;
         // DXRPT_OPT_SPLIT_ALPHA 0: spatial splits leave alpha-tested triangles whole (each extra reference
         // of one is another AnyHitShader opacity test)
-        std::vector<uint8_t> keep_whole;
+        std::vector<uint8_t> alpha_tri(ntris);
+        for (uint32_t t = 0; t < ntris; ++t)
+            alpha_tri[t] = ctx->mats[ctx->geos[tri_geom[t]].MaterialIdx].Opacity != DXRPT_INVALID_INDEX ? 1u : 0u;
         BvhBuildParams bp = ctx->build_params;
-        if (!ctx->opt_split_alpha) {
-            keep_whole.resize(ntris);
-            for (uint32_t t = 0; t < ntris; ++t)
-                keep_whole[t] = ctx->mats[ctx->geos[tri_geom[t]].MaterialIdx].Opacity != DXRPT_INVALID_INDEX ? 1u : 0u;
-            bp.keep_whole = keep_whole.data();
-        }
+        if (!ctx->opt_split_alpha) bp.keep_whole = alpha_tri.data();
+        bp.alpha_tri = alpha_tri.data();
+        bp.alpha_cost = DXRPT_ALPHA_TRI_COST;  // (build-time A/B knob, see below)
         if (!build_bvh(pos.data(), ntris, ctx->opt_width, res, err, &bp))
             throw ApiError(DXRPT_E_INVALID_ARG, err);
         // one record per leaf reference (BVH8 spatial splits may reference a triangle more than once)
