@@ -2116,6 +2116,11 @@ PT_DEV void count_rays(uint32_t* counters, uint32_t n) {
 // (k_path_tail) and per-lane shadow rays (vertex_shadows), separately.  r03 A/B
 // (profiles/r03_ab_split_pipe.txt): closest-hit triangle pairs (1) -0.8..-1.0 % on the metric, C3, C4 and
 // C5's share; the next-node prefetch (2, 3) and any-hit pairs / prefetch lose 3-35 %.
+// The split head's packet traversals with leaf triangles two at a time (traverse8_packet kPair): bit 0
+// the primary closest hit, bit 1 the depth-1 sun shadow rays.
+#ifndef DXRPT_HEAD_PACKET_PAIR
+#define DXRPT_HEAD_PACKET_PAIR 0
+#endif
 #ifndef DXRPT_SPLIT_PIPE_CH
 #define DXRPT_SPLIT_PIPE_CH 1
 #endif
@@ -2691,7 +2696,7 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
         bool occluded = false;
         const bool pk = d == 1 && k == 0 && (packet & 2u);
         if (pk)
-            occluded = traverse8_packet<true, false>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live && sun0, hs);
+            occluded = traverse8_packet<true, false, (DXRPT_HEAD_PACKET_PAIR & 2) != 0>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live && sun0, hs);
         if (live && !(pk && sun0))
             occluded = traverse<8, true, false, DXRPT_SPLIT_PIPE_AH>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, nullptr, hs, nv, nt);
         if (live) {
@@ -3089,7 +3094,7 @@ void k_path_head(KArgs A) {
     HitRec h;
     uint32_t nv = 0, nt = 0;
     if (packet & 1u)  // coherent primary rays: wave-coherent traversal (same results)
-        traverse8_packet<false, false>(A.S, pr.start, pr.dir, 0.0f, pr.length, 1 <= set.MaxAnyHitPathLength, true, h);
+        traverse8_packet<false, false, (DXRPT_HEAD_PACKET_PAIR & 1) != 0>(A.S, pr.start, pr.dir, 0.0f, pr.length, 1 <= set.MaxAnyHitPathLength, true, h);
     else
         traverse<8, false, false>(A.S, pr.start, pr.dir, 0.0f, pr.length, 1 <= set.MaxAnyHitPathLength, nullptr, h, nv, nt);
     VertexIn V;
