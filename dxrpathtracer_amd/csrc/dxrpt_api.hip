@@ -1150,7 +1150,9 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         const bool split_by_size =
             vertices >= (ctx->opt_overlap ? kSplitMinVerticesOverlap : kSplitMinVertices) && lanes == 64u;
         fp.split = (ctx->opt_split == 1u || (ctx->opt_split == 2u && split_by_size)) && lanes == 64u && fp.megakernel ? 1u : 0u;
-        if (fp.split && !ctx->opt_mega_occ) fp.megakernel_occupancy = ctx->opt_overlap ? 7u : 6u;
+        // (r03 final: with overlapped frames the head at 5 waves/SIMD -- 96 VGPRs, no spills -- metric
+        // -0.2 %, C3 -0.4 %, C5's share -1.0 %, C4 +0.5 % against 7, profiles/r03_ab_head_occ_final.txt)
+        if (fp.split && !ctx->opt_mega_occ) fp.megakernel_occupancy = ctx->opt_overlap ? 5u : 6u;
         fp.split_bins = fp.split ? ctx->opt_split_bins : 0u;
         fp.tail_occupancy = ctx->opt_tail_occ ? ctx->opt_tail_occ : (ctx->opt_mega_occ ? fp.megakernel_occupancy : 7u);
         fp.path_base = 0;
