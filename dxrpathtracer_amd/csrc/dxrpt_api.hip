@@ -71,7 +71,7 @@ struct DevBuf {
 // Overlapped frames (DXRPT_OPT_FRAME_OVERLAP): from kSplitMinVerticesOverlap, one part -- the next frame
 // fills a split frame's drains, which is what the second part did.
 constexpr uint64_t kSplitMinVertices = 8000000;
-constexpr uint64_t kSplitMinVerticesOverlap = 4000000;
+constexpr uint64_t kSplitMinVerticesOverlap = 2000000;
 constexpr uint32_t kSplitPartsMaxPaths = 4000000;
 // Overlapped frames (DXRPT_OPT_FRAME_OVERLAP v): up to v + 1 frames in flight, v <= kMaxOverlapFrames - 1.
 constexpr uint32_t kMaxOverlapFrames = 3;
@@ -1147,6 +1147,9 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // per-depth kernel's drain, so the split pays from 4M vertices: metric 1.909 -> 1.875 ms, C4 2.042 ->
         // 2.029, C5's 1/8 share 2.349 -> 2.098, C3 5.65 -> 5.59 with one part; it still loses below --
         // 720p 0.902 -> 0.925, C3's 1/8 share 0.979 -> 1.031; the 1/2 share even)
+        // (r03 final, spill-free head: from 2M vertices -- the metric's 1/2 share, 2.07M, 0.961 -> 0.939 ms;
+        // still not 720p, 1.84M, 0.881 -> 0.893, C3's 1/8 share, 1.81M, 0.965 -> 0.986, or the 1/4 share,
+        // 1.04M, 0.512 -> 0.566; profiles/r03_ab_split_small.txt)
         const bool split_by_size =
             vertices >= (ctx->opt_overlap ? kSplitMinVerticesOverlap : kSplitMinVertices) && lanes == 64u;
         fp.split = (ctx->opt_split == 1u || (ctx->opt_split == 2u && split_by_size)) && lanes == 64u && fp.megakernel ? 1u : 0u;

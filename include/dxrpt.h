@@ -383,7 +383,7 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                           compacted into full waves (wave64 ballot, one atomic per wave),
                                           with the path state in the queue instead of registers and its own
                                           register budget.  0: the single k_path.  2 (default): by frame
-                                          size -- frames of >= 4M path vertices (paths x (L-1)) with
+                                          size -- frames of >= 2M path vertices (paths x (L-1)) with
                                           overlapped frames, >= 8M without.
                                           Identical results. */
 #define DXRPT_OPT_SPLIT_PARTS 35u      /* split frames as this many concurrent parts (halves of the path slots,

@@ -3,7 +3,7 @@
 The other parity tests pin the wavefront schedule (tests/test_gpu_parity.py) and reach the megakernel
 only through bit-identity.  Here every context is fresh and untouched, so each frame runs exactly what
 bench.py times: the megakernel (packet primaries and depth-1 sun shadows, the occupancy picked by frame
-size; from 4M path vertices its depth-split form) for every BASELINE config; frame buffers sized for
+size; from 2M path vertices its depth-split form) for every BASELINE config; frame buffers sized for
 the whole frame.  One test also runs
 the wavefront passes at full size (DXRPT_OPT_MEGAKERNEL_PATHS 0, the only option it sets).
 Each full frame (RaygenShader over DispatchRays(W, H, 1), RayTrace.hlsl:92-149) is compared with the

@@ -85,7 +85,7 @@ def _steady_frames(torch, name, W, H, L, frames, crops, tiles=None, n_out=None, 
 def _expect(lanes, ordered, overlap=True, split=False):
     def check(f, s):
         assert s.schedule & A.SCHED_MEGAKERNEL and not s.schedule & A.SCHED_CENSUS, s.schedule
-        # from 4M path vertices (overlapped frames) the depth-split schedule, one part
+        # from 2M path vertices (overlapped frames) the depth-split schedule, one part
         assert bool(s.schedule & A.SCHED_SPLIT) == split, f"frame {f}: schedule {s.schedule}"
         assert not s.schedule & A.SCHED_PARTS, f"frame {f}: schedule {s.schedule}"
         assert bool(s.schedule & A.SCHED_OVERLAP) == overlap, f"frame {f}: schedule {s.schedule}"
@@ -121,8 +121,9 @@ def test_metric_band_share_consecutive_frames(torch_cuda, world, rank, lanes, or
     # 1/2 = 1,036,800 paths (path order); overlap off: the 1/8 share in path groups of 32 per wave
     W, H = 1920, 1080
     lay = band_layout(W, H, world)
+    # the 1/2 share (2.07M path vertices) runs the depth-split schedule when frames overlap
     _steady_frames(torch_cuda, "sponza", W, H, 3, 3, _band_crops(lay, rank), tiles=lay.rank_tiles(rank),
-                   n_out=lay.counts[rank], expect=_expect(lanes, ordered, bool(overlap)),
+                   n_out=lay.counts[rank], expect=_expect(lanes, ordered, bool(overlap), split=world == 2 and bool(overlap)),
                    options=((A.OPT_FRAME_OVERLAP, overlap),))
 
 
