@@ -9,10 +9,13 @@ A step is one frame (DispatchRays(1920,1080,1) equivalent, DXRPathTracer.cpp:202
 image.  With N ranks the image is split into 8-row bands, band b -> rank b % N (distributed.band_layout;
 --layout blocks: 8x8-pixel blocks dealt in a seeded random order) and every frame ends
 with an RCCL gather of the rank slabs to rank 0 plus the un-permute: total work per
-frame is fixed, so scaling is "strong".  The gather of frame f runs on RCCL's stream while frame f+1
-renders (distributed.PipelinedGather); the last frame's gather is inside the timed region.  value = nominal Mrays/s of the whole job (W*H*(1+2(L-1))
-rays per frame, the reference's HUD formula DXRPathTracer.cpp:2171) over the max-over-ranks time.
-Rank 0 prints one JSON line.
+frame is fixed, so scaling is "strong".  The gather of frame f runs on a side stream while frame f+1
+renders (distributed.NativeGather); the last frame's gather is inside the timed region.  value = nominal
+Mrays/s of the whole job (W*H*(1+2(L-1)) rays per frame, the reference's HUD formula
+DXRPathTracer.cpp:2171) over the max-over-ranks time.  Rank 0 prints one JSON line; with N > 1 it carries
+every rank's render time, the gather's and un-permute's times and RCCL's rank count ("multi_gpu").
+roofline: the dominant kernel's SURVEY.md 8(d) bytes per launch over its average launch duration from a
+frame-at-a-time pass (HIP events, DXRPT_OPT_FRAME_OVERLAP 0); the overlapped frame-interval rate beside it.
 """
 from __future__ import annotations
 
@@ -35,15 +38,7 @@ CONFIGS = {"metric": ("sponza", 1920, 1080, 3), "c2": ("sponza", 1280, 720, 3), 
            "c4": ("suntemple", 1920, 1080, 3), "c5": ("sponza", 3840, 2160, 6)}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "Mrays/sec + ms/frame, Sponza 1920x1080 path-length 3 at 1/2/4/8 GPU"
-# Algorithmic bytes, per ray, plus the BVH nodes (80 B) and triangle records (48 B) it
-# visits (counted by the instrumented kernels):
-#   k_trace  (closest hit): 32 B ray in (2 x float4) + 16 B hit out
-#   k_shadow (any hit):     4 B queue entry + 48 B shadow slot in (origin, direction, contribution);
-#                           the 16-B contribution write of occluded rays is not counted (lower bound)
-#   k_path   (megakernel, one launch per frame): all of the above + 32 B accumulation RMW per pixel
-RAY_IN_BYTES, HIT_OUT_BYTES = 32, 16
-SHADOW_IN_BYTES = 52
-ACCUM_BYTES = 32
+ACCUM_BYTES = 32  # RaygenShader's progressive blend: 16-B read + 16-B write per path
 
 
 def log(*a):
@@ -110,11 +105,12 @@ def cpu_baseline(scene, sky, settings, threads):
             "cpu_model": cpu_model(), **cpus[1]}
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` (k_trace / k_shadow) from the committed rocprofv3 PMC summary, if
-    one exists for this config (profiles/*_pmc_<kernel>.json, written by scripts/pmc_summary.py)."""
+def pmc_kernels(config):
+    """Per-kernel, per-LAUNCH counters of the non-overlapped launch profile of this config (the newest
+    profiles/<round>_launch_<config>.json, written by scripts/pmc_summary.py over scripts/profile.sh's
+    rocprofv3 passes of scripts/launch_profile.py): {kernel kind: summary}."""
     import glob
-    for p in sorted(glob.glob(os.path.join(REPO, "profiles", f"*_pmc_{kernel}.json")), reverse=True):
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", f"*_launch_{config}.json")), reverse=True):
         try:
             d = json.load(open(p))
         except Exception:
@@ -124,58 +120,59 @@ def pmc_traffic(kernel):
     return {}, None
 
 
-def pmc_frame(config):
-    """Per-FRAME counters of the megakernel schedule (k_path, or the split schedule's head + tails) from
-    the newest committed summary for this config (profiles/<round>_pmc_frame_<config>.json, written by
-    scripts/pmc_summary.py over scripts/profile.sh's rocprofv3 passes)."""
-    import glob
-    for p in sorted(glob.glob(os.path.join(REPO, "profiles", f"*_pmc_frame_{config}.json")), reverse=True):
-        try:
-            d = json.load(open(p))
-        except Exception:
-            continue
-        if d.get("config") == f"{SCENE}-proxy {WIDTH}x{HEIGHT} L={PATH_LENGTH}":
-            return d, os.path.basename(p)
-    return {}, None
-
-
-def full_formula_bytes(census, settings, bvh, pixels):
-    """SURVEY.md 8(d)'s algorithmic bytes of one frame, term by term as the survey writes them:
+def full_formula_bytes(c, settings, bvh):
+    """SURVEY.md 8(d)'s algorithmic bytes of a set of rays, term by term as the survey writes them:
       per ray: 32 B in (o, d, tmax, flags) + 16 B hit out (radiance) or 4 B visibility (shadow)
                + N_node x S_node + N_tri x S_tri (the census' fetches of the timed schedule)
       per radiance hit: 12 (3 indices) + 192 (3 vertices) + 16 (GeometryInfo) + 24 (Material)
                + taps x 4 texels x 4 B (RGBA8: normal, albedo if enabled; metallic, roughness, emissive)
                + 64 (path-state RMW) + 32 (next-ray write) + 32 (shadow-ray write)
       per miss: 4 x 8 B (FP16 cube bilinear)
-      + 32 B accumulation RMW per pixel.
-    Alpha-test opacity taps of any-hit candidates are not counted (a lower bound for C4)."""
-    hits = int(census.radiance_hits)
-    misses = int(census.radiance_rays) - hits
+      + 32 B accumulation RMW per path that ends.
+    `c`: radiance_rays, shadow_rays, node_fetches, tri_fetches, hits, paths_ending.  Alpha-test opacity
+    taps of any-hit candidates are not counted (a lower bound for C4)."""
+    hits = int(c["hits"])
+    misses = int(c["radiance_rays"]) - hits
     taps = 3 + int(settings.EnableNormalMaps) + int(settings.EnableAlbedoMaps)
     per_hit = 12 + 192 + 16 + 24 + taps * 16 + 64 + 32 + 32
     terms = {
-        "radiance_ray_io": int(census.radiance_rays) * (32 + 16),
-        "shadow_ray_io": int(census.shadow_rays) * (32 + 4),
-        "bvh_node_fetches": int(census.node_visits_radiance + census.node_visits_shadow) * int(bvh.node_bytes),
-        "triangle_fetches": int(census.tri_tests_radiance + census.tri_tests_shadow) * int(bvh.tri_bytes),
+        "radiance_ray_io": int(c["radiance_rays"]) * (32 + 16),
+        "shadow_ray_io": int(c["shadow_rays"]) * (32 + 4),
+        "bvh_node_fetches": int(c["node_fetches"]) * int(bvh.node_bytes),
+        "triangle_fetches": int(c["tri_fetches"]) * int(bvh.tri_bytes),
         "radiance_hit_shading": hits * per_hit,
         "miss_sky_taps": misses * 32,
-        "accumulation": ACCUM_BYTES * int(pixels),
+        "accumulation": ACCUM_BYTES * int(c["paths_ending"]),
     }
-    return sum(terms.values()), {"terms": terms, "radiance_hits": hits, "misses": misses,
+    return sum(terms.values()), {"terms": terms, "counts": {k: int(v) for k, v in c.items()}, "misses": misses,
                                  "taps_per_hit": taps, "bytes_per_hit": per_hit}
 
 
-def schedule_name(bits, ppw, A):
+def census_parts(census, pixels, L):
+    """The census of one frame split by kernel: the split schedule's head runs every depth-1 vertex, its
+    tails every deeper one (the single k_path runs both).  Depth-1 counts are dxrpt_stats.census_depth1;
+    a path ends in the head iff it has no depth-2 ray."""
+    rr = [int(census.radiance_rays_per_depth[d]) for d in range(8)]
+    sr = [int(census.shadow_rays_per_depth[d]) for d in range(8)]
+    d1 = [int(v) for v in census.census_depth1]
+    tot = {"radiance_rays": int(census.radiance_rays), "shadow_rays": int(census.shadow_rays),
+           "node_fetches": int(census.node_visits_radiance + census.node_visits_shadow),
+           "tri_fetches": int(census.tri_tests_radiance + census.tri_tests_shadow),
+           "hits": int(census.radiance_hits), "paths_ending": int(pixels)}
+    ends_head = int(pixels) - (rr[2] if L > 2 else 0)
+    head = {"radiance_rays": rr[1], "shadow_rays": sr[1], "node_fetches": d1[0] + d1[2], "tri_fetches": d1[1] + d1[3],
+            "hits": d1[4], "paths_ending": ends_head}
+    tail = {k: tot[k] - head[k] for k in tot}
+    return {"frame": tot, "head": head, "tail": tail}
+
+
+def schedule_name(bits, A):
     if not bits & A.SCHED_MEGAKERNEL:
         return "wavefront passes"
     if bits & A.SCHED_SPLIT:
-        return ("depth-split megakernel (k_path_head + k_path_tail per depth)"
-                + (", two concurrent halves" if bits & A.SCHED_PARTS else "")
-                + (", overlapped frames" if bits & A.SCHED_OVERLAP else ""))
+        return "depth-split megakernel (k_path_head + k_path_tail per depth)" + (
+            ", overlapped frames" if bits & A.SCHED_OVERLAP else "")
     s = "megakernel (k_path)"
-    if bits & A.SCHED_PATH_GROUPS:
-        s += f", path groups ({ppw} paths per wave)"
     if bits & A.SCHED_COST_ORDERED:
         s += ", cost-ordered waves"
     if bits & A.SCHED_OVERLAP:
@@ -248,9 +245,9 @@ def main():
         gather_used = args.gather
         if args.gather == "native":
             try:
-                pg = NativeGather(lay, rank, local_rank, full)
+                pg = NativeGather(lay, rank, local_rank, full, timing=True)
             except RuntimeError as e:  # e.g. an RCCL communicator that cannot be built on this node
-                # every rank takes the same branch (dxrpt_comm_create is collective: it fails on all ranks)
+                # every rank takes the same branch (NativeGather's checks and results are all-gathered)
                 log(f"native gather unavailable ({e}); falling back to torch.distributed.gather")
                 gather_used = f"torch (native failed: {e})"
         if pg is None:
@@ -258,9 +255,17 @@ def main():
                 idx = torch.tensor(source_index(lay), dtype=torch.long, device="cuda")
             pg = PipelinedGather(lay, rank, full, idx)
 
-    def frame(f):
+    render_ev = []
+
+    def frame(f, record=False):
+        if record:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
         tracer.render_raw(consts[f % 16], settings, accum.data_ptr(), WIDTH, HEIGHT, tiles=tiles, stream=sh,
                           lights=lights)
+        if record:
+            b.record(stream)
+            render_ev.append((a, b))
         if pg is not None:
             pg.submit(accum)
 
@@ -268,38 +273,65 @@ def main():
         if pg is not None:
             pg.flush()
 
-    # ---- traversal work census (instrumented kernels, untimed): nodes / triangles per ray
+    # ---- traversal work census (instrumented kernels, untimed): nodes / triangles per ray, split by the
+    # kernel that traces them (depth 1: the split schedule's head; deeper: its tails)
     tracer.set_option(A.OPT_COUNT_TRAVERSAL, 1)
     frame(0)
     flush()
     census = tracer.stats()
     tracer.set_option(A.OPT_COUNT_TRAVERSAL, 0)
 
+    # ---- per-launch kernel durations (untimed pass): the shipped kernels one frame at a time
+    # (DXRPT_OPT_FRAME_OVERLAP 0), so each launch's HIP-event span is the launch alone -- with overlapped
+    # frames a launch shares the GPU with the neighbour frame for part of its span.  The events are on the
+    # stream the kernels run on (the render stream when frames do not overlap).  The pass pins the timed
+    # frames' schedule (split or single k_path, register budgets, wave order), which the by-size defaults
+    # would otherwise pick differently without overlap.
+    for f in range(3):
+        frame(f)
+    flush()
+    torch.cuda.synchronize()
+    timed = tracer.stats()
+    pinned = {A.OPT_MEGAKERNEL_SPLIT: 1 if timed.schedule & A.SCHED_SPLIT else 0,
+              A.OPT_MEGAKERNEL_OCCUPANCY: int(timed.occupancy),
+              A.OPT_TAIL_OCCUPANCY: int(timed.tail_occupancy) if timed.schedule & A.SCHED_SPLIT else 0,
+              A.OPT_WAVE_ORDER: 1 if timed.schedule & A.SCHED_ORDER_KERNEL else 0}
+    for o, v in pinned.items():
+        tracer.set_option(o, v)
+    tracer.set_option(A.OPT_FRAME_OVERLAP, 0)
+    for f in range(3):
+        frame(f)
+    flush()
+    torch.cuda.synchronize()
+    tracer.set_option(A.OPT_KERNEL_TIMING_MASK, (1 << A.K_COUNT) - 1)
+    tracer.set_option(A.OPT_KERNEL_TIMING, 1)
+    tracer.reset_timing()
+    for f in range(min(args.steps, 32)):
+        frame(f)
+    flush()
+    torch.cuda.synchronize()
+    launches = tracer.stats()
+    tracer.set_option(A.OPT_KERNEL_TIMING, 0)
+    same = ~(A.SCHED_OVERLAP | A.SCHED_COST_ORDERED)
+    assert launches.schedule & same == timed.schedule & same, (launches.schedule, timed.schedule)
+    tracer.set_option(A.OPT_FRAME_OVERLAP, A.DEFAULT_FRAME_OVERLAP)
+    for o, v in ((A.OPT_MEGAKERNEL_SPLIT, A.DEFAULT_MEGAKERNEL_SPLIT), (A.OPT_MEGAKERNEL_OCCUPANCY, A.DEFAULT_MEGAKERNEL_OCCUPANCY),
+                 (A.OPT_TAIL_OCCUPANCY, A.DEFAULT_TAIL_OCCUPANCY), (A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)):
+        tracer.set_option(o, v)
+    per_launch = {A.KERNEL_NAMES[k]: {"avg_ms": launches.kernel_ms[k] / launches.kernel_launches[k],
+                                      "launches_per_frame": launches.kernel_launches[k] / max(1, launches.timed_frames)}
+                  for k in range(A.K_COUNT) if launches.kernel_launches[k]}
+    frame_at_a_time_ms = launches.frame_ms / max(1, launches.timed_frames)
+
     for f in range(args.warmup):
         frame(f)
     flush()
     torch.cuda.synchronize()
 
-    # ---- per-kernel breakdown (all kinds, untimed pass before the timed region): picks the dominant
-    # kernel whose roofline is reported.  ~26 events per frame cost ~0.1 ms of frame time, so the timed
-    # region below brackets only the dominant kernel's launches (plus the frame span).
-    tracer.set_option(A.OPT_KERNEL_TIMING_MASK, (1 << A.K_COUNT) - 1)
-    tracer.set_option(A.OPT_KERNEL_TIMING, 1)
-    tracer.reset_timing()
-    for f in range(min(args.steps, 16)):
-        frame(f)
-    flush()
-    torch.cuda.synchronize()
-    breakdown = tracer.stats()
-    kms = {A.KERNEL_NAMES[k]: breakdown.kernel_ms[k] for k in range(A.K_COUNT)}
-    dominant = max(kms, key=kms.get)
-    roof_kernel = dominant if dominant in ("k_trace", "k_shadow", "k_path") else "k_trace"
-    K_ROOF = {"k_trace": A.K_TRACE, "k_shadow": A.K_SHADOW, "k_path": A.K_PATH}[roof_kernel]
-
-    # ---- timed region: production schedule (any-hit / closest-hit stream overlap), events on the
-    # launching streams around the roofline kernel's launches only
-    tracer.set_option(A.OPT_KERNEL_TIMING_MASK, 1 << K_ROOF)
-    tracer.reset_timing()
+    # ---- timed region: the shipped defaults (overlapped frames); per-frame events on the render stream
+    if hasattr(pg, "reset_times"):
+        pg.reset_times()
+    render_ev.clear()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -307,7 +339,7 @@ def main():
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     for f in range(args.steps):
         ev[f][0].record(stream)
-        frame(args.warmup + f)
+        frame(args.warmup + f, record=True)
         ev[f][1].record(stream)
     flush()  # the last frame's gather + un-permute are inside the timed region
     torch.cuda.synchronize()
@@ -315,70 +347,80 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     stats = tracer.stats()
-    tracer.set_option(A.OPT_KERNEL_TIMING, 0)
-    roof_ms_avg = stats.kernel_ms[K_ROOF] / max(1, stats.kernel_launches[K_ROOF])
-    gpu_frame_ms = stats.frame_ms / max(1, stats.timed_frames)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    frame_ms = np.array([a.elapsed_time(b) for a, b in ev])  # per frame on the render stream
+    frame_ms = np.array([a.elapsed_time(b) for a, b in ev])  # per frame on the render stream (incl. the gather's)
+    render_ms = float(np.median([a.elapsed_time(b) for a, b in render_ev]))  # this rank's dxrpt_render per frame
     nominal_per_frame = WIDTH * HEIGHT * (1 + 2 * (PATH_LENGTH - 1))
     ms_per_step = elapsed / args.steps * 1e3
     value = nominal_per_frame * args.steps / elapsed / 1e6
 
-    # ---- roofline of the dominant kernel (measured live with HIP events on its launching stream)
-    launches_per_frame = PATH_LENGTH - 1  # one closest-hit and one any-hit pass per depth
-    trace_bytes_frame = (census.radiance_rays * (RAY_IN_BYTES + HIT_OUT_BYTES)
-                         + census.node_visits_radiance * bvh.node_bytes + census.tri_tests_radiance * bvh.tri_bytes)
-    shadow_bytes_frame = (census.shadow_rays * SHADOW_IN_BYTES
-                          + census.node_visits_shadow * bvh.node_bytes + census.tri_tests_shadow * bvh.tri_bytes)
-    # k_path (the whole frame in one launch, rays and path state in registers): the node and triangle
-    # FETCHES its census counted (per lane in the per-lane traversals, once per wave in the packet
-    # traversals) + the accumulation RMW; the shading gathers are not counted, so it is a lower bound
-    fetch_bytes_frame = ((census.node_visits_radiance + census.node_visits_shadow) * bvh.node_bytes
-                         + (census.tri_tests_radiance + census.tri_tests_shadow) * bvh.tri_bytes)
-    path_bytes_lower = fetch_bytes_frame + ACCUM_BYTES * n_local
-    path_bytes_full, full_detail = full_formula_bytes(census, settings, bvh, n_local)
-    # k_path: the survey's full formula (census of the timed schedule); the fetch-only figure stays beside it
-    roof_bytes = {"k_trace": trace_bytes_frame / launches_per_frame, "k_shadow": shadow_bytes_frame / launches_per_frame,
-                  "k_path": path_bytes_full}[roof_kernel]
-    achieved_launch = roof_bytes / (roof_ms_avg * 1e-3) / 1e9
-    # Overlapped frames (DXRPT_SCHED_OVERLAP): a launch's event span runs from its stream becoming ready
-    # (while the previous frame still holds the GPU) to its end, so it overlaps its neighbours' spans; the
-    # steady-state frame interval (per-frame events on the render stream) is the time the GPU spends per
-    # launch, and prices the kernel's bytes.  Without overlap the two agree.
-    frame_interval_ms = float(np.median(np.array([a.elapsed_time(b) for a, b in ev])))
-    overlapped = bool(stats.schedule & A.SCHED_OVERLAP)
-    achieved = roof_bytes / (frame_interval_ms * 1e-3) / 1e9 if overlapped and roof_kernel == "k_path" else achieved_launch
-    pmc, traffic_src = pmc_traffic(roof_kernel)
-    traffic = pmc.get("hbm_bytes_per_launch")
-    l2_hit = pmc.get("l2_hit_rate")
-    wait_frac = pmc.get("wait_any_per_wave_cycle")
-    write_bytes = pmc.get("hbm_write_bytes_per_launch")
-    if roof_kernel == "k_path":  # per-frame PMC summary of the megakernel schedule of this config
-        fr, src = pmc_frame(args.config)
-        if fr:
-            traffic, traffic_src = fr.get("hbm_bytes_per_frame"), src
-            l2_hit, wait_frac, write_bytes = fr.get("l2_hit_rate"), fr.get("wait_any_per_wave_cycle"), fr.get("hbm_write_bytes")
-            pmc = {"kernel": " + ".join(fr.get("kernels", []))}
-    # what limits the kernel, from its counters: waves parked on s_waitcnt for most of their cycles with
-    # HBM far from its peak = latency of dependent loads (the roofline below is still priced against HBM)
+    multi = None
+    if world > 1:
+        ranks_ms = [None] * world
+        dist.all_gather_object(ranks_ms, render_ms)
+        g_ms, u_ms, g_frames = pg.times() if hasattr(pg, "times") else (None, None, 0)
+        multi = {"render_ms_per_rank": [round(v, 4) for v in ranks_ms], "render_ms_max": round(max(ranks_ms), 4),
+                 "render_ms_min": round(min(ranks_ms), 4),
+                 "gather": gather_used,
+                 "gather_ms": None if g_ms is None else round(g_ms, 4),
+                 "unpermute_ms": None if u_ms is None else round(u_ms, 4),
+                 "gather_frames_timed": g_frames,
+                 "rccl_ranks": getattr(pg, "comm_ranks", None),
+                 # the part of the frame time the gather adds beyond the slowest rank's render (the gather of
+                 # frame f runs while frame f+1 renders; the last frame's is inside the timed region)
+                 "gather_exposed_ms": round(ms_per_step - max(ranks_ms), 4),
+                 "gather_what": "dxrpt_gather_slabs (grouped ncclSend/ncclRecv of every rank's slab to rank 0) "
+                                "timed with events on its side stream, dxrpt_unpermute on rank 0's render stream; "
+                                "per-rank render ms = median events around dxrpt_render on each rank's stream"}
+
+    # ---- roofline of the dominant kernel, per launch (SURVEY.md 8(d) bytes / the launch's own duration)
+    parts = census_parts(census, n_local, PATH_LENGTH)
+    part_bytes = {k: full_formula_bytes(v, settings, bvh) for k, v in parts.items()}
+    frame_bytes = part_bytes["frame"][0]
+    kern = {}
+    if "k_path_head" in per_launch:  # the depth-split schedule: head (depth 1) and tails (depths >= 2)
+        for name, part in (("k_path_head", "head"), ("k_path_tail", "tail")):
+            if name in per_launch:
+                n = per_launch[name]["launches_per_frame"]
+                kern[name] = {"bytes_per_launch": part_bytes[part][0] / n, "avg_launch_ms": per_launch[name]["avg_ms"],
+                              "launches_per_frame": n, "bytes_part": part}
+    elif "k_path" in per_launch:
+        kern["k_path"] = {"bytes_per_launch": frame_bytes, "avg_launch_ms": per_launch["k_path"]["avg_ms"],
+                          "launches_per_frame": 1.0, "bytes_part": "frame"}
+    for k, e in kern.items():
+        e["achieved"] = e["bytes_per_launch"] / (e["avg_launch_ms"] * 1e-3) / 1e9
+        e["frac"] = e["achieved"] / HBM_PEAK_GBS
+    dominant = max(kern, key=lambda k: kern[k]["avg_launch_ms"] * kern[k]["launches_per_frame"]) if kern else None
+    pmc, pmc_src = pmc_kernels(args.config)
+    pk = pmc.get("kernels_by_kind") or {}
+    for k, e in kern.items():
+        c = pk.get(k, {})
+        e["pmc_avg_launch_ms"] = c.get("avg_ms")
+        e["traffic"] = c.get("l2_fabric_bytes_per_launch")
+        e["write_bytes"] = c.get("write_bytes_per_launch")
+        e["l2_hit_rate"] = c.get("l2_hit_rate")
+        e["wait_any_per_wave_cycle"] = c.get("wait_any_per_wave_cycle")
+        e["valu_lane_utilisation"] = c.get("valu_lane_utilisation")
+    d = kern.get(dominant, {})
+    wait_frac = d.get("wait_any_per_wave_cycle")
+    achieved = d.get("achieved", 0.0)
+    # what limits the kernel, from its counters: waves parked on s_waitcnt for much of their cycles with
+    # HBM far from its peak = latency of dependent loads (the roofline is still priced against HBM)
     bound = "latency" if (wait_frac is not None and wait_frac > 0.3 and achieved < 0.6 * HBM_PEAK_GBS) else "hbm"
-    # the other traversal kernel, from the breakdown pass (for the record; wavefront schedule only)
-    other = "k_shadow" if roof_kernel == "k_trace" else "k_trace"
-    K_OTHER = A.K_SHADOW if other == "k_shadow" else A.K_TRACE
-    other_ms = breakdown.kernel_ms[K_OTHER] / max(1, breakdown.kernel_launches[K_OTHER])
-    other_bytes = (shadow_bytes_frame if other == "k_shadow" else trace_bytes_frame) / launches_per_frame
-    other_pmc, _ = pmc_traffic(other)
+    frame_interval_ms = float(np.median(frame_ms))
+
+    def r4(v):
+        return round(v, 4) if isinstance(v, float) else v
 
     result = None
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(scene, sky, settings, args.cpu_threads)
-        frames = breakdown.timed_frames or 1
         result = {
             "metric": metric,
             "value": round(value, 2),
@@ -398,27 +440,30 @@ def main():
                        "sqrt_num_samples": 4, "triangles": scene.num_triangles, "sky": sky.model,
                        "parallelism": (f"screen {args.layout} x{world} + RCCL gather ({gather_used})" if world > 1
                                        else "single GPU")},
-            "roofline": {"bound": bound, "roofline_kind": "hbm",
-                         "kernel": ("k_path_head + k_path_tail (one frame)" if roof_kernel == "k_path" and stats.schedule & A.SCHED_SPLIT
-                                    else roof_kernel), "achieved": round(achieved, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "bytes_per_launch": int(roof_bytes),
-                         "bytes_formula": "SURVEY.md 8(d) full formula" if roof_kernel == "k_path" else "per-ray I/O + fetches",
-                         "bytes_fetch_lower_bound": int(path_bytes_lower) if roof_kernel == "k_path" else None,
-                         "frac_fetch_lower_bound": round(path_bytes_lower / (roof_bytes / achieved * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
-                         if roof_kernel == "k_path" else None,
-                         "avg_launch_ms": round(roof_ms_avg, 4), "traffic_source": traffic_src,
-                         "traffic_kernel": pmc.get("kernel"), "l2_hit_rate": l2_hit,
-                         "hbm_write_bytes": write_bytes, "wait_any_per_wave_cycle": wait_frac,
-                         # overlapped frames (DXRPT_SCHED_OVERLAP): a launch shares the GPU with its
-                         # neighbour frames for part of its event span, so the per-launch figure above
-                         # understates the kernel; the steady-state frame interval prices the same bytes
-                         "frames_overlap": overlapped,
-                         "achieved_over": "steady-state frame interval (median per-frame events)" if overlapped
-                         and roof_kernel == "k_path" else "average launch span (HIP events on the launching stream)",
-                         "frame_interval_ms": round(frame_interval_ms, 4),
-                         "achieved_launch_span": round(achieved_launch, 1),
-                         "frac_launch_span": round(achieved_launch / HBM_PEAK_GBS, 4)},
+            "roofline": {"bound": bound, "roofline_kind": "hbm", "kernel": dominant,
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": d.get("traffic"),
+                         "traffic_kind": "L2->fabric bytes per launch (rocprofv3 FETCH_SIZE + WRITE_SIZE, raw, no x2 "
+                                         "read correction): Infinity-Cache hits included, so not HBM bytes",
+                         "traffic_source": pmc_src,
+                         "bytes_per_launch": int(d.get("bytes_per_launch", 0)),
+                         "bytes_formula": "SURVEY.md 8(d) full formula over the rays this kernel traces (census split "
+                                          "by depth: head = depth 1, tails = depths >= 2)",
+                         "avg_launch_ms": r4(d.get("avg_launch_ms", 0.0)),
+                         "achieved_over": "the kernel's average launch duration: HIP events on its stream in a "
+                                          "frame-at-a-time pass (DXRPT_OPT_FRAME_OVERLAP 0) inside bench.py",
+                         "pmc_avg_launch_ms": d.get("pmc_avg_launch_ms"),
+                         "l2_hit_rate": d.get("l2_hit_rate"), "hbm_write_bytes": d.get("write_bytes"),
+                         "wait_any_per_wave_cycle": wait_frac,
+                         "valu_lane_utilisation": d.get("valu_lane_utilisation"),
+                         "per_kernel": {k: {kk: r4(vv) for kk, vv in e.items()} for k, e in kern.items()},
+                         # the shipped throughput rate: the whole frame's bytes over the overlapped frame
+                         # interval (two frames in flight: not a launch duration)
+                         "frame_interval": {"bytes": int(frame_bytes), "ms": round(frame_interval_ms, 4),
+                                            "achieved": round(frame_bytes / (frame_interval_ms * 1e-3) / 1e9, 1),
+                                            "frac": round(frame_bytes / (frame_interval_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                            "frame_at_a_time_ms": round(frame_at_a_time_ms, 4)}},
             "cpu_baseline": cpu,
             # the headline counts the reference's HUD rays (W*H*(1+2(L-1)) per frame); the kernels skip
             # shadow rays whose pending contribution is exactly 0 (identical image), so fewer are traced:
@@ -426,27 +471,26 @@ def main():
             "counted_rays_per_frame": int(stats.radiance_rays + stats.shadow_rays),
             "counted_Mrays_s": round((stats.radiance_rays + stats.shadow_rays) * args.steps / elapsed / 1e6, 2)
             if world == 1 else None,
+            "multi_gpu": multi,
             "detail": {
-                "kernel_ms_per_frame": {k: round(v / frames, 4) for k, v in kms.items()},
-                "dominant_kernel": dominant,
-                "roofline_other": {"kernel": other, "bytes_per_launch": int(other_bytes),
-                                   "avg_launch_ms": round(other_ms, 4),
-                                   "achieved_GBs": round(other_bytes / (other_ms * 1e-3) / 1e9, 1),
-                                   "traffic": other_pmc.get("hbm_bytes_per_launch"),
-                                   "l2_hit_rate": other_pmc.get("l2_hit_rate")} if other_ms > 0 else None,
-                "schedule": schedule_name(stats.schedule, stats.paths_per_wave, A),
+                "per_launch_kernel_ms": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in per_launch.items()},
+                "schedule": schedule_name(stats.schedule, A),
                 "schedule_bits": int(stats.schedule),
-                "algorithmic_bytes": full_detail,
-                "gpu_frame_ms_events": round(gpu_frame_ms, 4),
-                "kernel_breakdown_note": "kernel_ms_per_frame from a separate all-kernel event pass before the timed region",
+                "frame_at_a_time_schedule_bits": int(launches.schedule),
+                "occupancy": {"head_or_path": int(stats.occupancy), "tail": int(stats.tail_occupancy)},
+                "algorithmic_bytes": {k: v[1] for k, v in part_bytes.items()},
                 "frame_ms": {"mean": round(float(frame_ms.mean()), 4), "median": round(float(np.median(frame_ms)), 4),
                              "max": round(float(frame_ms.max()), 4)},
+                "render_ms_median": round(render_ms, 4),
                 "census": {"what": "node / triangle-record fetches of the timed schedule (per lane in per-lane "
                                    "traversals, per wave in packet traversals), one instrumented frame",
                            "node_fetches_radiance": int(census.node_visits_radiance),
                            "tri_fetches_radiance": int(census.tri_tests_radiance),
                            "node_fetches_shadow": int(census.node_visits_shadow),
                            "tri_fetches_shadow": int(census.tri_tests_shadow),
+                           "depth1": [int(v) for v in census.census_depth1],
+                           "radiance_rays_per_depth": [int(v) for v in census.radiance_rays_per_depth],
+                           "shadow_rays_per_depth": [int(v) for v in census.shadow_rays_per_depth],
                            "node_bytes": int(bvh.node_bytes), "tri_bytes": int(bvh.tri_bytes),
                            "accum_bytes_per_pixel": ACCUM_BYTES, "pixels": int(n_local)},
                 "node_fetches_per_radiance_ray": round(census.node_visits_radiance / max(1, census.radiance_rays), 2),

@@ -76,42 +76,47 @@ class Tile(C.Structure):
                 ("accum_pitch", u32), ("pad", u32)]
 
 
-K_RAYGEN, K_TRACE, K_SHADE, K_SHADOW, K_ACCUMULATE, K_RESOLVE, K_PATH, K_COUNT = range(8)
-KERNEL_NAMES = ("k_raygen", "k_trace", "k_shade", "k_shadow", "k_accumulate", "k_resolve", "k_path")
-(OPT_COUNT_TRAVERSAL, OPT_KERNEL_TIMING, OPT_BVH_WIDTH, OPT_TRAVERSAL_MODE, OPT_REFILL_LANES, OPT_CHUNKS_PER_WAVE,
- OPT_POSTPONE_TRIS, OPT_TRACE_BLOCK, OPT_OCCUPANCY, OPT_SHADE_BLOCK, OPT_SHADE_OCCUPANCY, OPT_SPATIAL_SPLITS,
- OPT_LEAF_COST, OPT_SHADOW_OCCUPANCY, OPT_SHADOW_GRID, OPT_CONCURRENCY, OPT_TRAVERSAL_PIPELINE, OPT_PACKET_TRAVERSAL, OPT_LDS_NODES,
- OPT_KERNEL_TIMING_MASK, OPT_XCD_MAPPING, OPT_PACKET_SWITCH, OPT_MEGAKERNEL_PATHS, OPT_MEGAKERNEL_OCCUPANCY,
- OPT_BAKE_CHUNK, OPT_MEGAKERNEL_PERSISTENT, OPT_MEGAKERNEL_LANES, OPT_WAVE_CLOCKS,
- OPT_WAVE_ORDER, OPT_SPLIT_UNITS, OPT_XCD_CHUNK, OPT_WAVE_ORDER_PERIOD, OPT_MEGAKERNEL_SPLIT,
- OPT_TAIL_OCCUPANCY, OPT_SPLIT_PARTS, OPT_OPACITY_MICROMAP, OPT_FRAME_OVERLAP, OPT_SPLIT_BINS, OPT_SPLIT_ALPHA) = range(1, 40)
-# context defaults of the traversal options (dxrpt_api.hip)
-DEFAULT_TRAVERSAL_PIPELINE = 0
+K_RAYGEN, K_TRACE, K_SHADE, K_SHADOW, K_ACCUMULATE, K_RESOLVE, K_PATH, K_PATH_HEAD, K_PATH_TAIL, K_COUNT = range(10)
+KERNEL_NAMES = ("k_raygen", "k_trace", "k_shade", "k_shadow", "k_accumulate", "k_resolve", "k_path", "k_path_head",
+                "k_path_tail")
+ABI_VERSION = 3
+# dxrpt_set_option ids (include/dxrpt.h); the ids missing here were retired in ABI 3 (DXRPT_E_UNSUPPORTED)
+OPT_COUNT_TRAVERSAL = 1
+OPT_KERNEL_TIMING = 2
+OPT_SPATIAL_SPLITS = 12
+OPT_LEAF_COST = 13
+OPT_PACKET_TRAVERSAL = 18
+OPT_KERNEL_TIMING_MASK = 20
+OPT_MEGAKERNEL_PATHS = 23
+OPT_MEGAKERNEL_OCCUPANCY = 24
+OPT_BAKE_CHUNK = 25
+OPT_WAVE_CLOCKS = 28
+OPT_WAVE_ORDER = 29
+OPT_XCD_CHUNK = 31
+OPT_WAVE_ORDER_PERIOD = 32
+OPT_MEGAKERNEL_SPLIT = 33
+OPT_TAIL_OCCUPANCY = 34
+OPT_OPACITY_MICROMAP = 36
+OPT_FRAME_OVERLAP = 37
+RETIRED_OPTIONS = (3, 4, 5, 6, 7, 8, 9, 10, 11, 14, 15, 16, 17, 19, 21, 22, 26, 27, 30, 35, 38, 39)
+DXRPT_E_UNSUPPORTED = -6
+# context defaults (dxrpt_api.hip)
 POST_FLOAT4, POST_RGBA8 = 0, 1  # dxrpt_post_process output formats
 DEFAULT_PACKET_TRAVERSAL = 3
-DEFAULT_LDS_NODES = 0
-DEFAULT_XCD_MAPPING = 0
-DEFAULT_PACKET_SWITCH = 0
 DEFAULT_MEGAKERNEL_PATHS = 0xFFFFFFFF
 DEFAULT_MEGAKERNEL_OCCUPANCY = 0
 DEFAULT_BAKE_CHUNK = 1 << 21
-DEFAULT_SPLIT_UNITS = 0
 DEFAULT_XCD_CHUNK = 8
 DEFAULT_WAVE_ORDER_PERIOD = 16
 DEFAULT_OPACITY_MICROMAP = 1
 DEFAULT_FRAME_OVERLAP = 1
+DEFAULT_WAVE_ORDER = 2  # by frame size
+DEFAULT_MEGAKERNEL_SPLIT = 2  # by frame size
+DEFAULT_TAIL_OCCUPANCY = 0
 # opacity micromap (pt_layout.h kOmm*): cells per barycentric axis, verdicts
 OMM_SPLIT = 32  # include/dxrpt.h DXRPT_OMM_SPLIT
 OMM_WORDS = 33  # DXRPT_OMM_WORDS
 OMM_UNKNOWN, OMM_OPAQUE, OMM_TRANSPARENT = 0, 1, 2
-DEFAULT_MEGAKERNEL_PERSISTENT = 0
-DEFAULT_MEGAKERNEL_LANES = 0  # by frame size
-DEFAULT_WAVE_ORDER = 2  # by frame size
-DEFAULT_MEGAKERNEL_SPLIT = 2  # by frame size
-DEFAULT_SPLIT_PARTS = 0  # by frame size
-DEFAULT_TAIL_OCCUPANCY = 0
-DEFAULT_SPLIT_BINS = 0
-DEFAULT_SPLIT_ALPHA = 0
 
 
 class Stats(C.Structure):
@@ -122,12 +127,12 @@ class Stats(C.Structure):
                 ("node_visits_shadow", C.c_uint64), ("tri_tests_shadow", C.c_uint64),
                 ("kernel_ms", C.c_double * K_COUNT), ("kernel_launches", C.c_uint64 * K_COUNT),
                 ("timed_frames", C.c_uint64), ("frame_ms", C.c_double), ("schedule", u32), ("paths_per_wave", u32),
-                ("occupancy", u32), ("pad", u32), ("radiance_hits", C.c_uint64)]
+                ("occupancy", u32), ("tail_occupancy", u32), ("radiance_hits", C.c_uint64),
+                ("census_depth1", C.c_uint64 * 5)]
 
 
 # dxrpt_stats.schedule bits
-SCHED_MEGAKERNEL, SCHED_PATH_GROUPS, SCHED_ORDER_KERNEL, SCHED_COST_ORDERED, SCHED_CENSUS, SCHED_SPLIT, SCHED_PARTS, \
-    SCHED_OVERLAP = 1, 2, 4, 8, 16, 32, 64, 128
+SCHED_MEGAKERNEL, SCHED_ORDER_KERNEL, SCHED_COST_ORDERED, SCHED_CENSUS, SCHED_SPLIT, SCHED_OVERLAP = 1, 4, 8, 16, 32, 128
 
 
 class BvhInfo(C.Structure):
@@ -166,7 +171,7 @@ DXRPT_SYMBOLS = ("dxrpt_abi_version", "dxrpt_default_settings", "dxrpt_create", 
                  "dxrpt_render", "dxrpt_get_stats", "dxrpt_trace_rays", "dxrpt_set_option", "dxrpt_reset_timing",
                  "dxrpt_post_process", "dxrpt_bake_lightmap", "dxrpt_denoise_median", "dxrpt_get_wave_clocks",
                  "dxrpt_get_phase_clocks", "dxrpt_sample_cmj", "dxrpt_render_aov", "dxrpt_comm_unique_id", "dxrpt_comm_create",
-                 "dxrpt_comm_destroy", "dxrpt_gather_slabs", "dxrpt_unpermute", "dxrpt_multi_last_error",
+                 "dxrpt_comm_destroy", "dxrpt_comm_info", "dxrpt_gather_slabs", "dxrpt_unpermute", "dxrpt_multi_last_error",
                  "dxrpt_opacity_micromap")
 DXRPT_HOST_SYMBOLS = ("dxrpt_host_scene_create", "dxrpt_host_scene_load", "dxrpt_host_scene_destroy", "dxrpt_host_last_error",
                       "dxrpt_host_inv_view_projection", "dxrpt_host_sky_create", "dxrpt_host_fill_constants",
@@ -227,6 +232,8 @@ def lib() -> C.CDLL:
         L.dxrpt_comm_unique_id.argtypes = [P]
         L.dxrpt_comm_create.argtypes = [C.c_int, C.c_int, C.c_int, P, C.POINTER(P)]
         L.dxrpt_comm_destroy.argtypes = [P]
+        if hasattr(L, "dxrpt_comm_info"):  # ABI 3 (absent from older builds loaded for A/B runs)
+            L.dxrpt_comm_info.argtypes = [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.dxrpt_gather_slabs.argtypes = [P, P, C.POINTER(C.c_uint64), P, P]
         L.dxrpt_unpermute.argtypes = [P, C.POINTER(Tile), u32, P, u32, u32, P]
         L.dxrpt_multi_last_error.restype = C.c_char_p

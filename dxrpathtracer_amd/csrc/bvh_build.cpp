@@ -40,13 +40,11 @@ struct Box {
     }
 };
 
-#ifndef DXRPT_BVH_BINS
-#define DXRPT_BVH_BINS 32
-#endif
-#ifndef DXRPT_SBVH_ALPHA
-#define DXRPT_SBVH_ALPHA 1e-5
-#endif
-constexpr int kBins = DXRPT_BVH_BINS;  // SAH bins per axis (object and spatial splits)
+// SAH bins per axis (object and spatial splits); r03: 64 bins measured within +-1 % (a 1/8 share +2.5 %)
+constexpr int kBins = 32;
+// spatial-split search when the object split's child overlap exceeds this fraction of the root area
+// (r03: 1e-6 / 1e-4 measured +1-3 %)
+constexpr double kSbvhAlpha = 1e-5;
 constexpr uint32_t kMaxDepth2 = kTraversalStack;  // a BVH2 node at depth d has <= d stack entries above it
 
 // Generic binary tree node.
@@ -214,7 +212,7 @@ struct SpatialBuilder {
     std::vector<uint32_t> refs;  // leaf order, duplicates allowed
     uint32_t depth_cap = 32;
     double root_area = 1.0;
-    double alpha = DXRPT_SBVH_ALPHA;  // overlap / root area that enables a spatial search
+    double alpha = kSbvhAlpha;  // overlap / root area that enables a spatial search
     size_t ref_budget = 0;       // maximum live references (duplication budget)
     size_t live_refs = 0;
     double sah = 0.0;            // binary tree, C_trav = 1, C_tri = 1, relative to the root area
@@ -601,9 +599,6 @@ struct Emit8 {
     std::vector<double> cost;     // [n * 8 + i], i in 1..7 (index 0: D(n, 8) for the node case)
     std::vector<uint8_t> pick;    // [n * 8 + i]: i == 1: 0 leaf / 1 node; i >= 2: 0 = use C(n, i-1), k = split
     std::vector<uint8_t> dsplit;  // k of D(n, 8)
-    // test-cost weight prefix over `refs` (leaf order): a binary node's triangle cost is
-    // wsum[end] - wsum[begin] (alpha-tested references weigh BvhBuildParams::alpha_cost); empty: counts
-    std::vector<double> wsum;
 
     static uint32_t ntris(const TNode& n) { return n.end - n.begin; }
     bool is_leaf(int32_t t) const { return pick[size_t(t) * 8 + 1] == 0; }
@@ -620,8 +615,7 @@ struct Emit8 {
             const double A = n.box.area();
             double* C = &cost[ni * 8];
             uint8_t* P = &pick[ni * 8];
-            const double w = wsum.empty() ? double(ntris(n)) : wsum[n.end] - wsum[n.begin];
-            const double leaf = ntris(n) <= uint32_t(kMaxLeafTris8) ? A * kCPrim * w : DBL_MAX;
+            const double leaf = ntris(n) <= uint32_t(kMaxLeafTris8) ? A * kCPrim * double(ntris(n)) : DBL_MAX;
             if (n.count) {  // binary leaf
                 for (int i = 1; i < 8; ++i) { C[i] = leaf; P[i] = 0; }
                 C[0] = DBL_MAX;
@@ -792,8 +786,8 @@ struct Emit8 {
     }
 
     // Breadth-first emission: the wide nodes of each level are contiguous and the top levels come
-    // first, so a prefix of the node array is the top of the tree (the traversal kernels keep such a
-    // prefix in LDS, DXRPT_OPT_LDS_NODES).  A node's internal children stay contiguous.
+    // first, so a prefix of the node array is the top of the tree (the levels every ray visits stay
+    // together in the caches).  A node's internal children stay contiguous.
     struct Pending {
         uint32_t idx;
         int32_t t;
@@ -889,12 +883,7 @@ bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildRe
             B.depth_cap = cap;
             if (!B.build(ntris, err, sah)) return false;
         }
-        Emit8 E{*tree, *refs, pad, {}, {}, 0, 0, 1.0, params ? params->leaf_cost : BvhBuildParams().leaf_cost, {}, {}, {}, {}, {}};
-        if (params && params->alpha_tri && params->alpha_cost != 1.0) {
-            E.wsum.assign(refs->size() + 1, 0.0);
-            for (size_t i = 0; i < refs->size(); ++i)
-                E.wsum[i + 1] = E.wsum[i] + (params->alpha_tri[(*refs)[i]] ? params->alpha_cost : 1.0);
-        }
+        Emit8 E{*tree, *refs, pad, {}, {}, 0, 0, 1.0, params ? params->leaf_cost : BvhBuildParams().leaf_cost, {}, {}, {}, {}};
         E.run();
         last_depth = E.max_depth;
         if (E.max_depth > max_depth8) continue;

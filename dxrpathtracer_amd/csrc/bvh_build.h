@@ -34,10 +34,6 @@ struct BvhBuildParams {
     // per global triangle, non-zero: never cut by a spatial split (an alpha-tested triangle: every extra
     // reference is another opacity test); null: every triangle may be split
     const uint8_t* keep_whole = nullptr;
-    // BVH8 collapse: per global triangle, non-zero = alpha-tested; such a triangle's test is priced
-    // alpha_cost times an opaque one (its opacity test is one or two more dependent round trips)
-    const uint8_t* alpha_tri = nullptr;
-    double alpha_cost = 1.0;
 };
 
 // tri_positions: ntris * 9 floats (v0.xyz, v1.xyz, v2.xyz) in global triangle order.

@@ -3,8 +3,16 @@
 // Host-side counterpart of DXRPathTracer::BuildRTAccelerationStructure (DXRPathTracer.cpp:2331-2488)
 // and DXRPathTracer::RenderRayTracing (DXRPathTracer.cpp:2024-2090).  No exception crosses the ABI:
 // every entry point catches, stores a message for dxrpt_last_error and returns a DXRPT_E_* code.
+//
+// Stream ordering (include/dxrpt.h "Stream ordering"): the reference records every frame into one
+// command queue (Graphics/DX12.cpp:263-305), so each frame sees the previous one's result.  Here every
+// call that enqueues work runs after all work this context enqueued before it, whatever stream the caller
+// passes: a call on a stream other than the previous call's first makes its stream wait on an event
+// recorded at the end of the previous one (enter_stream).  Overlapped frames run on two internal slot
+// streams and blend on the caller's stream, so the chain of caller streams orders them too.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -61,20 +69,16 @@ struct DevBuf {
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
-// BVH8 collapse: an alpha-tested triangle's test priced this many opaque tests (BvhBuildParams::alpha_cost)
-#ifndef DXRPT_ALPHA_TRI_COST
-#define DXRPT_ALPHA_TRI_COST 1.0
-#endif
-
 // Depth-split schedule by frame size (DXRPT_OPT_MEGAKERNEL_SPLIT 2): frames of at least this many path
-// vertices (paths x (L - 1)); two concurrent parts up to kSplitPartsMaxPaths paths (DXRPT_OPT_SPLIT_PARTS 0).
-// Overlapped frames (DXRPT_OPT_FRAME_OVERLAP): from kSplitMinVerticesOverlap, one part -- the next frame
-// fills a split frame's drains, which is what the second part did.
+// vertices (paths x (L - 1)); with overlapped frames the next frame fills the per-depth kernels' drains,
+// so the split pays from fewer vertices.
 constexpr uint64_t kSplitMinVertices = 8000000;
 constexpr uint64_t kSplitMinVerticesOverlap = 2000000;
-constexpr uint32_t kSplitPartsMaxPaths = 4000000;
-// Overlapped frames (DXRPT_OPT_FRAME_OVERLAP v): up to v + 1 frames in flight, v <= kMaxOverlapFrames - 1.
-constexpr uint32_t kMaxOverlapFrames = 3;
+// DXRPT_OPT_FRAME_OVERLAP: two frames in flight, frame f on slot f % 2
+constexpr uint32_t kOverlapSlots = 2;
+// BVH8 stack-spill slabs: 0 = work on the caller's stream, 1 + k = overlap slot k
+constexpr uint32_t kSpillSlabs = 1 + kOverlapSlots;
+constexpr uint32_t kTravCounters = 10;  // census: [0..4] depth-1 vertices, [5..9] deeper (dxrpt_stats)
 
 }  // namespace
 
@@ -91,105 +95,82 @@ struct dxrpt_ctx {
     bool scene_set = false, bvh_built = false, sky_set = false, tex_dirty = true, geoshade_dirty = true;
     uint32_t sky_res = 0;
     // device copies
-    DevBuf d_vertices, d_indices, d_geos, d_mats, d_texdesc, d_texels, d_sky, d_lut, d_nodes, d_nodes8, d_tris, d_geoshade;
+    DevBuf d_texels, d_sky, d_lut, d_nodes8, d_tris, d_geoshade;
     DevBuf d_lights, d_tiles, d_tile_prefix;
     DevBuf p_bloom0, p_bloom1;  // post-processing scratch (RGBA16F half-res)
     DevBuf d_tri_verts;  // per global triangle: its 3 MeshVertex records (3 x 64 B), built with the BVH
-    // per-frame wavefront buffers
+    // per-frame buffers of work on the caller's stream (wavefront passes, non-overlapped megakernel frames)
     DevBuf f_pix, f_pxrad, f_hit, f_fwd, f_shn, f_shq, f_shorg, f_shdir, f_shcon, f_counters;
     DevBuf f_q[2][5];  // RayQueue org, dir, thr, rad, pix per depth parity
     FrameBuffers fb;
+    uint32_t ctr_set = 0;                 // counter set of the next frame (f_counters holds two)
+    bool ctr_clean[2] = {false, false};   // set known to be zero (zeroed by the previous megakernel frame)
     dxrpt_bvh_info bvh{};
     std::vector<dxrpt_tile> tiles_cache;
     std::vector<dxrpt_spot_light> lights_cache;
-    hipStream_t last_stream = nullptr;
     dxrpt_stats last{};
     int last_L = 0;
     bool rendered = false;
+    // stream ordering: the stream of the last enqueuing call, whether anything may still be in flight
+    hipStream_t last_stream = nullptr;
+    bool have_last = false;
+    bool inflight = false;
+    hipEvent_t chain_ev = nullptr;
     // options
     bool opt_count = false, opt_timing = false;
     uint32_t opt_timing_mask = (1u << DXRPT_K_COUNT) - 1u;  // DXRPT_OPT_KERNEL_TIMING_MASK
-    int opt_width = 8;   // DXRPT_OPT_BVH_WIDTH
     uint32_t num_cus = 256;
-    uint32_t opt_trav_mode = 0;     // DXRPT_OPT_TRAVERSAL_MODE: 0 one thread per ray, 1 persistent
-    uint32_t opt_refill = 16;       // DXRPT_OPT_REFILL_LANES
-    uint32_t opt_chunks = 4;        // DXRPT_OPT_CHUNKS_PER_WAVE
-    uint32_t opt_postpone = 0;      // DXRPT_OPT_POSTPONE_TRIS
-    uint32_t opt_trace_block = 64;  // DXRPT_OPT_TRACE_BLOCK
-    uint32_t opt_occupancy = 7;     // DXRPT_OPT_OCCUPANCY
-    uint32_t opt_shadow_occ = 8;    // DXRPT_OPT_SHADOW_OCCUPANCY
-    uint32_t opt_shadow_grid = 0;   // DXRPT_OPT_SHADOW_GRID
-    uint32_t opt_pipeline = 0;      // DXRPT_OPT_TRAVERSAL_PIPELINE
     uint32_t opt_packet = 3;        // DXRPT_OPT_PACKET_TRAVERSAL
-    uint32_t opt_lds_nodes = 0;     // DXRPT_OPT_LDS_NODES
-    uint32_t opt_concurrency = 1;   // DXRPT_OPT_CONCURRENCY
-    hipStream_t aux = nullptr;      // any-hit pass stream (created on first use)
+    hipStream_t aux = nullptr;      // wavefront any-hit pass stream (created on first use)
     std::vector<hipEvent_t> fork_ev;
-    uint32_t opt_shade_block = 256; // DXRPT_OPT_SHADE_BLOCK
-    uint32_t opt_shade_occ = 0;     // DXRPT_OPT_SHADE_OCCUPANCY
-    uint32_t opt_xcd = 0;           // DXRPT_OPT_XCD_MAPPING
-    uint32_t opt_packet_switch = 0; // DXRPT_OPT_PACKET_SWITCH
-    uint32_t opt_mega_paths = 0xFFFFFFFFu;  // DXRPT_OPT_MEGAKERNEL_PATHS (path vertices; r02: every config)
+    uint32_t opt_mega_paths = 0xFFFFFFFFu;  // DXRPT_OPT_MEGAKERNEL_PATHS (path vertices; default: every frame)
     uint32_t opt_mega_occ = 0;              // DXRPT_OPT_MEGAKERNEL_OCCUPANCY (0 = by frame size)
+    uint32_t opt_tail_occ = 0;              // DXRPT_OPT_TAIL_OCCUPANCY (0 = 7, or the megakernel's when set)
     uint32_t opt_bake_chunk = 1u << 21;     // DXRPT_OPT_BAKE_CHUNK (texels per bake launch)
-    uint32_t opt_mega_persistent = 0;       // DXRPT_OPT_MEGAKERNEL_PERSISTENT (waves per CU, 0 = off)
-    uint32_t opt_mega_lanes = 0;            // DXRPT_OPT_MEGAKERNEL_LANES (paths per megakernel wave, 0 = by size)
     uint32_t opt_split = 2;                 // DXRPT_OPT_MEGAKERNEL_SPLIT (0 off, 1 on, 2 by frame size)
-    uint32_t opt_split_parts = 0;           // DXRPT_OPT_SPLIT_PARTS (0 = by frame size, 1, 2)
-    // split-schedule frame parts beyond the first (own queues, shadow slots, counters, stream)
-    struct FramePart {
-        DevBuf q[2][5], shorg, shdir, shcon, counters;
+    uint32_t opt_omm = 1;                   // DXRPT_OPT_OPACITY_MICROMAP
+    uint32_t opt_overlap = 1;               // DXRPT_OPT_FRAME_OVERLAP
+    // overlapped frames: frame f runs on slot f % kOverlapSlots -- its own stream, path buffers, counters,
+    // stage and BVH8 stack-spill slab -- and stages its radiance (d_stage); the caller's stream blends the
+    // stage once the frame is done, so frame f+1's waves start while frame f drains
+    struct Slot {
+        DevBuf q[2][5], shorg, shdir, shcon, counters, stage;
         FrameBuffers fb;
         uint32_t ctr_set = 0;
         bool ctr_clean[2] = {false, false};
         hipStream_t stream = nullptr;
-        hipEvent_t done = nullptr;
+        hipEvent_t done = nullptr;        // the slot's last frame (and its order pass) is done
+        hipEvent_t stage_free = nullptr;  // caller's stream: the slot's last stage has been blended
+        bool stage_used = false;
     };
-    FramePart part[2 * kMaxOverlapFrames];  // split halves 0, 1; overlapped frames: slot ov uses parts 2ov (and 2ov + 1)
-    hipEvent_t part_fork = nullptr;
-    std::vector<const uint32_t*> stat_counters;  // counter sets of the last frame (several with parts)
-    uint32_t opt_tail_occ = 0;              // DXRPT_OPT_TAIL_OCCUPANCY (0 = the head's budget)
-    uint32_t opt_omm = 1;                   // DXRPT_OPT_OPACITY_MICROMAP
-    // DXRPT_OPT_FRAME_OVERLAP v: megakernel frames rotate over v + 1 slots of FramePart streams/buffers
-    // (frame f on slot f % (v + 1)) and stage their radiance (d_stage[slot]); the caller's stream blends
-    // the stage once the frame is done, so frame f+1's waves start while frame f drains
-    uint32_t opt_overlap = 1;
-    uint32_t opt_split_bins = 0;            // DXRPT_OPT_SPLIT_BINS
-    // DXRPT_OPT_SPLIT_ALPHA (r03: 0 -- alpha-tested triangles stay whole: metric 1.867 -> 1.823 ms, C4
-    // 2.006 -> 1.980, C3 5.54 -> 5.45, C2 0.902 -> 0.882, 1/2 share -2.4 %; the 1/8 shares' mean is
-    // unchanged and their maximum +2-3 %, profiles/r03_ab_split_alpha*.txt)
-    uint32_t opt_split_alpha = 0;
-    uint32_t accum_extent = 0;  // 1 + the largest accumulation index of the current tile list (stage size)
-    DevBuf d_stage[kMaxOverlapFrames];
-    hipEvent_t stage_free[kMaxOverlapFrames] = {};  // caller stream: the slot's last stage has been blended
-    bool stage_used[kMaxOverlapFrames] = {};
-    hipEvent_t ovl_gate = nullptr;                   // the next overlapped frame waits for it (an order pass)
+    Slot slot[kOverlapSlots];
+    hipEvent_t ovl_fork = nullptr;  // the first overlapped frame after other work starts behind the caller's stream
+    bool ovl_active = false;        // the slot streams run overlapped frames (no fork needed)
+    hipEvent_t ovl_gate = nullptr;  // the next overlapped frame waits for it (a rebuilt wave order)
     bool ovl_gate_set = false;
     uint32_t ovl_parity = 0;
-    bool ovl_inflight = false;                       // overlapped frames may still run on the part streams
+    std::vector<const uint32_t*> stat_counters;  // counter set of the last frame
+    uint32_t accum_extent = 0;  // 1 + the largest accumulation index of the current tile list (stage size)
     DevBuf d_omm;                           // kOmmWords per micromap slot (pt_layout.h kOmm*)
     std::vector<uint32_t> omm_tris;         // slot -> global triangle (alpha-tested geometry), set by the BVH build
     bool omm_dirty = true, omm_any = false; // any: some triangle has a verdict (else d_omm is not read)
     BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
-    int built_width = 0;
-    DevBuf d_trav;   // 5 x u64 census counters (DXRPT_OPT_COUNT_TRAVERSAL): node / triangle fetches, radiance hits
-    uint32_t ctr_set = 0;                 // counter set of the next frame (f_counters holds two)
-    bool ctr_clean[2] = {false, false};   // set known to be zero (zeroed by the previous megakernel frame)
+    DevBuf d_trav;   // kTravCounters x u64 census counters (DXRPT_OPT_COUNT_TRAVERSAL)
     DevBuf d_wclock;  // 2 x u64 per wave (DXRPT_OPT_WAVE_CLOCKS)
     bool opt_wave_clocks = false;
     uint32_t wclock_waves = 0;
     // DXRPT_OPT_WAVE_ORDER: per wave slot, the last frame's duration and the order built from it
     uint32_t opt_wave_order = 2;  // 0 off, 1 on, 2 by frame size (see render)
-    uint32_t opt_split_permille = 0;  // DXRPT_OPT_SPLIT_UNITS
     uint32_t opt_xcd_chunk = 8;       // DXRPT_OPT_XCD_CHUNK (r02: 1080p 2.100 -> 2.075 ms, C4 2.276 -> 2.252)
     DevBuf d_wave_cost, d_wave_order, d_wave_hist;  // hist: 2 frames x (histogram, cursor) x kWaveClasses
     uint32_t order_parity = 0;
-    uint64_t order_key = 0;     // (waves, lanes, tiles generation) the order was built for
+    uint64_t order_key = 0;     // (waves, tiles generation) the order was built for
     bool order_ready = false;   // d_wave_order holds an order for order_key
     uint32_t order_frame = 0;   // ordered frames since the order (re)started
     uint32_t opt_order_period = 16;  // DXRPT_OPT_WAVE_ORDER_PERIOD (r02: 1/8 share 0.549 -> 0.534 ms)
     uint64_t tiles_gen = 0;     // bumped whenever the tile list changes
-    DevBuf d_spill;  // BVH8 traversal stack entries beyond the LDS part (deep trees only)
+    DevBuf d_spill;  // BVH8 traversal stack entries beyond the LDS part (deep trees only), kSpillSlabs slabs
+    uint32_t spill_threads = 0;  // per-slab stride: the largest traversal launch seen
     DevBuf d_bake_list;  // live lightmap texels of the last bake pass + their count
     // kernel timing: a ring of per-frame event sets, harvested lazily
     struct FrameEvents {
@@ -197,7 +178,8 @@ struct dxrpt_ctx {
         int L = 0;
         uint32_t mask = 0;  // kernel kinds whose events were recorded
         bool pending = false;
-        bool mega = false;  // megakernel frame: ev[0], ev[1] bracket its k_path launch
+        bool mega = false;   // megakernel frame: ev[0], ev[1] bracket its launches
+        bool split = false;  // ... the depth-split schedule: ev[2] after the head
     };
     std::vector<FrameEvents> ring;
     size_t ring_head = 0;
@@ -207,41 +189,36 @@ struct dxrpt_ctx {
     double frame_ms = 0.0;
 
     ~dxrpt_ctx() {
-        DevBuf* all[] = {&d_vertices, &d_indices, &d_geos, &d_mats, &d_texdesc, &d_texels, &d_sky, &d_lut, &d_geoshade, &d_nodes,
-                         &d_nodes8, &d_tris, &d_tri_verts, &d_lights, &d_tiles, &d_tile_prefix, &f_pix, &f_pxrad, &f_hit, &f_fwd,
-                         &f_shn, &f_shq, &f_shorg, &f_shdir, &f_shcon, &f_counters, &p_bloom0, &p_bloom1, &d_wclock, &d_omm};
+        for (Slot& P : slot)
+            if (P.stream) (void)hipStreamSynchronize(P.stream);
+        if (have_last) (void)hipStreamSynchronize(last_stream);
+        if (aux) (void)hipStreamSynchronize(aux);
+        DevBuf* all[] = {&d_texels, &d_sky, &d_lut, &d_geoshade, &d_nodes8, &d_tris, &d_tri_verts, &d_lights, &d_tiles,
+                         &d_tile_prefix, &f_pix, &f_pxrad, &f_hit, &f_fwd, &f_shn, &f_shq, &f_shorg, &f_shdir, &f_shcon,
+                         &f_counters, &p_bloom0, &p_bloom1, &d_wclock, &d_omm, &d_trav, &d_spill, &d_bake_list,
+                         &d_wave_cost, &d_wave_order, &d_wave_hist};
         for (DevBuf* b : all) b->release();
         for (auto& qb : f_q)
             for (DevBuf& b : qb) b.release();
-        d_trav.release();
-        d_spill.release();
-        d_bake_list.release();
         for (auto& f : ring)
             for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
-        if (aux) {
-            (void)hipStreamSynchronize(aux);
-            (void)hipStreamDestroy(aux);
-        }
+        if (aux) (void)hipStreamDestroy(aux);
         for (hipEvent_t e : fork_ev) (void)hipEventDestroy(e);
-        for (FramePart& fp : part) {
-            for (auto& qb : fp.q)
+        for (Slot& P : slot) {
+            for (auto& qb : P.q)
                 for (DevBuf& b : qb) b.release();
-            fp.shorg.release();
-            fp.shdir.release();
-            fp.shcon.release();
-            fp.counters.release();
-            if (fp.stream) {
-                (void)hipStreamSynchronize(fp.stream);
-                (void)hipStreamDestroy(fp.stream);
-            }
-            if (fp.done) (void)hipEventDestroy(fp.done);
+            P.shorg.release();
+            P.shdir.release();
+            P.shcon.release();
+            P.counters.release();
+            P.stage.release();
+            if (P.stream) (void)hipStreamDestroy(P.stream);
+            if (P.done) (void)hipEventDestroy(P.done);
+            if (P.stage_free) (void)hipEventDestroy(P.stage_free);
         }
-        if (part_fork) (void)hipEventDestroy(part_fork);
-        for (uint32_t k = 0; k < kMaxOverlapFrames; ++k) {
-            d_stage[k].release();
-            if (stage_free[k]) (void)hipEventDestroy(stage_free[k]);
-        }
+        if (ovl_fork) (void)hipEventDestroy(ovl_fork);
         if (ovl_gate) (void)hipEventDestroy(ovl_gate);
+        if (chain_ev) (void)hipEventDestroy(chain_ev);
     }
 };
 
@@ -280,60 +257,61 @@ std::vector<float> make_lut() {
     return l;
 }
 
-void drain_overlap(dxrpt_ctx* c);
+// Waits until nothing this context enqueued is in flight: before anything in-flight work reads is
+// replaced or freed (scene, texture, tile, light and buffer uploads, buffer growth, the cost order's
+// restart).  The caller streams form one chain (enter_stream), so the last one covers the older ones.
+void drain_frames(dxrpt_ctx* c) {
+    if (!c->inflight) return;
+    for (dxrpt_ctx::Slot& P : c->slot)
+        if (P.stream) HIP_CHECK(hipStreamSynchronize(P.stream));
+    if (c->have_last) HIP_CHECK(hipStreamSynchronize(c->last_stream));
+    c->inflight = false;
+    c->ovl_active = false;
+}
 
-// Device view of the scene for launches of up to `traversal_threads` global threads (sizes the
-// BVH8 stack spill slab, allocated only when the tree is deeper than the LDS part of the stack).
-// `slabs` concurrent launches (split-schedule frame parts) each get their own BVH8 stack-spill slab;
-// this SceneDev uses slab `slab`.
-SceneDev scene_dev(dxrpt_ctx* c, uint32_t traversal_threads, uint32_t slabs = 1, uint32_t slab = 0) {
+// Every enqueuing call starts here: on a stream other than the previous call's, the new stream first
+// waits for everything the previous one carries (which, through the blends, includes every overlapped
+// frame).  Afterwards `s` is the context's stream until the next call.
+void enter_stream(dxrpt_ctx* c, hipStream_t s) {
+    if (c->inflight && c->have_last && s != c->last_stream) {
+        if (!c->chain_ev) HIP_CHECK(hipEventCreateWithFlags(&c->chain_ev, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(c->chain_ev, c->last_stream));
+        HIP_CHECK(hipStreamWaitEvent(s, c->chain_ev, 0));
+    }
+    c->last_stream = s;
+    c->have_last = true;
+}
+
+// BVH8 stack-spill slab `slab` (0: the caller's stream, 1 + k: overlap slot k) for launches of up to
+// `threads` global threads.  Every slab has the stride of the largest launch seen, so frames in flight
+// on different slots never share entries whatever their sizes; growing it waits for in-flight frames.
+void ensure_spill(dxrpt_ctx* c, uint32_t threads) {
+    if (c->bvh.max_depth + 1u <= uint32_t(kStackLds8) || threads <= c->spill_threads) return;
+    drain_frames(c);
+    const size_t per = size_t(kTraversalStack8 - kStackLds8) * threads;
+    c->d_spill.ensure(per * kSpillSlabs * sizeof(uint2));
+    c->spill_threads = threads;
+}
+
+// Device view of the scene; `slab` selects the BVH8 stack-spill slab (ensure_spill sized it).
+SceneDev scene_dev(dxrpt_ctx* c, uint32_t slab) {
     SceneDev s;
-    s.nodes = c->d_nodes.as<BvhNode>();
     s.nodes8 = c->d_nodes8.as<Bvh8Node>();
-    s.width = c->built_width;
     const uint32_t entries = c->bvh.max_depth + 1u;
-    if (c->built_width == 8) {
-        s.num_nodes = c->bvh.num_nodes;
-        s.stack_ints = 2u * std::min<uint32_t>(entries, uint32_t(kStackLds8));
-        if (entries > uint32_t(kStackLds8)) {
-            const size_t per = size_t(kTraversalStack8 - kStackLds8) * traversal_threads;
-            if (c->d_spill.bytes < per * slabs * sizeof(uint2)) drain_overlap(c);  // (re)allocation
-            c->d_spill.ensure(per * slabs * sizeof(uint2));
-            s.spill8 = c->d_spill.as<uint2>() + per * slab;
-            s.spill_stride = traversal_threads;
-        }
-    } else {
-        s.stack_ints = std::min<uint32_t>(entries, uint32_t(kTraversalStack));
+    s.stack_ints = 2u * std::min<uint32_t>(entries, uint32_t(kStackLds8));
+    if (entries > uint32_t(kStackLds8)) {
+        s.spill8 = c->d_spill.as<uint2>() + size_t(kTraversalStack8 - kStackLds8) * c->spill_threads * slab;
+        s.spill_stride = c->spill_threads;
     }
     s.tris = c->d_tris.as<TriRecord>();
     s.tri_verts = c->d_tri_verts.as<float4>();
-    s.vertices = c->d_vertices.as<dxrpt_mesh_vertex>();
-    s.indices = c->d_indices.as<uint32_t>();
-    s.geoinfo = c->d_geos.as<dxrpt_geometry_info>();
-    s.materials = c->d_mats.as<dxrpt_material>();
-    s.texdesc = c->d_texdesc.as<TexDesc>();
     s.geoshade = c->d_geoshade.as<GeoShade>();
     s.texels = c->d_texels.as<uint32_t>();
     s.sky = c->d_sky.as<uint16_t>();
     s.lut = c->d_lut.as<float>();
     s.sky_res = c->sky_res;
-    s.num_textures = uint32_t(c->texdesc.size());
     s.omm = c->opt_omm && c->omm_any ? c->d_omm.as<uint32_t>() : nullptr;
     return s;
-}
-
-// Uploads added textures and (re)builds the per-geometry shading records (pt_layout.h GeoShade):
-// GeometryInfo.MaterialIdx -> Material -> the texture descriptors, resolved once on the host.  A
-// material index that names no added texture resolves to "none" (the render path rejects such
-// materials before it launches; an opacity of DXRPT_INVALID_INDEX is the reference's "opaque").
-// Waits for the overlapped frames still in flight (DXRPT_OPT_FRAME_OVERLAP) before anything they read is
-// replaced or freed: scene, texture, tile, light and buffer uploads, and calls that share their buffers.
-void drain_overlap(dxrpt_ctx* c) {
-    if (!c->ovl_inflight) return;
-    for (dxrpt_ctx::FramePart& P : c->part)
-        if (P.stream) HIP_CHECK(hipStreamSynchronize(P.stream));
-    if (c->last_stream) HIP_CHECK(hipStreamSynchronize(c->last_stream));  // the stage blends
-    c->ovl_inflight = false;
 }
 
 // The opacity micromap of every triangle on alpha-tested geometry (omm.cpp), one slot per triangle in
@@ -388,15 +366,18 @@ void build_omm(dxrpt_ctx* c) {
 
 void upload_textures(dxrpt_ctx* c) {
     if ((c->omm_dirty && c->opt_omm && c->bvh_built) || c->tex_dirty || (c->geoshade_dirty && !c->geos.empty()))
-        drain_overlap(c);
+        drain_frames(c);
     if (c->omm_dirty && c->opt_omm && c->bvh_built) build_omm(c);
     if (c->tex_dirty) {
-        c->d_texdesc.upload(c->texdesc.data(), c->texdesc.size() * sizeof(TexDesc));
         c->d_texels.upload(c->texels.data(), c->texels.size() * sizeof(uint32_t));
         c->tex_dirty = false;
         c->geoshade_dirty = true;
     }
     if (!c->geoshade_dirty || c->geos.empty()) return;
+    // per-geometry shading records (pt_layout.h GeoShade): GeometryInfo.MaterialIdx -> Material -> the
+    // texture descriptors, resolved once on the host; a material index that names no added texture
+    // resolves to "none" (the render path rejects such materials before it launches; an opacity of
+    // DXRPT_INVALID_INDEX is the reference's "opaque")
     auto ref = [&](uint32_t t) {
         GeoTex g{0u, 0u};
         if (t < c->texdesc.size()) {
@@ -415,40 +396,54 @@ void upload_textures(dxrpt_ctx* c) {
     c->geoshade_dirty = false;
 }
 
-// Do buffers for `paths` paths with `slots` shadow slots (and the context's queue binning) fit f?
-bool frame_fits(const dxrpt_ctx* c, const FrameBuffers& f, uint32_t paths, uint32_t slots) {
-    return paths <= f.capacity && slots <= f.shadow_slots && f.counters &&
-           f.cap_q >= f.cap_r * (c->opt_split_bins ? kSplitBins : 1u);
+// Do buffers for `paths` paths with `slots` shadow slots fit f?
+bool frame_fits(const FrameBuffers& f, uint32_t paths, uint32_t slots) {
+    return paths <= f.capacity && slots <= f.shadow_slots && f.counters;
 }
 
-void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
-    FrameBuffers& f = c->fb;
-    if (frame_fits(c, f, paths, slots)) return;
+// Queue + shadow-slot buffers of `f` for `paths` paths and `slots` shadow slots (grown, never shrunk).
+// q: the two RayQueue parities; sh*: the shadow slots.
+void alloc_frame(FrameBuffers& f, DevBuf (&q)[2][5], DevBuf& shorg, DevBuf& shdir, DevBuf& shcon, uint32_t paths,
+                 uint32_t slots) {
     const uint32_t cap = std::max(paths, f.capacity);
     const uint32_t sl = std::max(slots, std::max(f.shadow_slots, 2u));
     const uint32_t cap_r = queue_shard_capacity(cap);
-    const uint32_t cap_q = std::max(f.cap_q, cap_r * (c->opt_split_bins ? kSplitBins : 1u));
-    const size_t qsize = size_t(kQueueShards) * cap_r, qbuf = size_t(kQueueShards) * cap_q;
-    require(qsize * sl < (size_t(1) << 32) && qbuf < (size_t(1) << 32), "frame too large for 32-bit shadow slot ids",
-            DXRPT_E_INVALID_ARG);
-    c->f_pix.ensure(size_t(cap) * 8);
-    c->f_pxrad.ensure(size_t(cap) * 16);
+    const size_t qsize = size_t(kQueueShards) * cap_r;
+    require(qsize * sl < (size_t(1) << 32), "frame too large for 32-bit shadow slot ids", DXRPT_E_INVALID_ARG);
     for (int b = 0; b < 2; ++b) {
-        for (int k = 0; k < 4; ++k) c->f_q[b][k].ensure(qbuf * 16);
-        c->f_q[b][4].ensure(qbuf * 4);
-        f.q[b].org = c->f_q[b][0].as<float4>();
-        f.q[b].dir = c->f_q[b][1].as<float4>();
-        f.q[b].thr = c->f_q[b][2].as<float4>();
-        f.q[b].rad = c->f_q[b][3].as<float4>();
-        f.q[b].pix = c->f_q[b][4].as<uint32_t>();
+        for (int k = 0; k < 4; ++k) q[b][k].ensure(qsize * 16);
+        q[b][4].ensure(qsize * 4);
+        f.q[b].org = q[b][0].as<float4>();
+        f.q[b].dir = q[b][1].as<float4>();
+        f.q[b].thr = q[b][2].as<float4>();
+        f.q[b].rad = q[b][3].as<float4>();
+        f.q[b].pix = q[b][4].as<uint32_t>();
     }
+    shorg.ensure(qsize * sl * 16);
+    shdir.ensure(qsize * sl * 16);
+    shcon.ensure(qsize * sl * 16);
+    f.sh_org = shorg.as<float4>();
+    f.sh_dir = shdir.as<float4>();
+    f.sh_con = shcon.as<float4>();
+    f.capacity = cap;
+    f.cap_r = cap_r;
+    f.qsize = uint32_t(qsize);
+    f.shadow_slots = sl;
+}
+
+// Buffers of work on the caller's stream (drains first when they grow: in-flight work may read them).
+void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
+    FrameBuffers& f = c->fb;
+    if (frame_fits(f, paths, slots)) return;
+    drain_frames(c);
+    alloc_frame(f, c->f_q, c->f_shorg, c->f_shdir, c->f_shcon, paths, slots);
+    const size_t qsize = f.qsize, sl = f.shadow_slots;
+    c->f_pix.ensure(size_t(f.capacity) * 8);
+    c->f_pxrad.ensure(size_t(f.capacity) * 16);
     c->f_hit.ensure(qsize * 16);
     c->f_fwd.ensure(qsize * 4);
     c->f_shn.ensure(qsize * 4);
     c->f_shq.ensure(qsize * sl * 4);
-    c->f_shorg.ensure(qsize * sl * 16);
-    c->f_shdir.ensure(qsize * sl * 16);
-    c->f_shcon.ensure(qsize * sl * 16);
     if (!c->f_counters.p) {  // two counter sets (ping-pong across megakernel frames), both dirty at first
         c->f_counters.ensure(2 * kCounterWords * sizeof(uint32_t));
         c->ctr_clean[0] = c->ctr_clean[1] = false;
@@ -459,58 +454,32 @@ void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
     f.fwd = c->f_fwd.as<uint32_t>();
     f.sh_n = c->f_shn.as<uint32_t>();
     f.sh_queue = c->f_shq.as<uint32_t>();
-    f.sh_org = c->f_shorg.as<float4>();
-    f.sh_dir = c->f_shdir.as<float4>();
-    f.sh_con = c->f_shcon.as<float4>();
     f.counters = c->f_counters.as<uint32_t>() + c->ctr_set * kCounterWords;
-    f.capacity = cap;
-    f.cap_r = cap_r;
-    f.cap_q = cap_q;
-    f.qsize = uint32_t(qsize);
-    f.shadow_slots = sl;
 }
 
-// Buffers of split-schedule frame part k (queues, shadow slots, counters) for `paths` paths.
-void ensure_part(dxrpt_ctx* c, int k, uint32_t paths, uint32_t slots) {
-    dxrpt_ctx::FramePart& P = c->part[k];
-    FrameBuffers& f = P.fb;
+// Overlap slot k (stream, events, queues, shadow slots, counters, stage) for `paths` paths; drains first
+// when a buffer grows.
+void ensure_slot(dxrpt_ctx* c, uint32_t k, uint32_t paths, uint32_t slots, size_t stage_bytes) {
+    dxrpt_ctx::Slot& P = c->slot[k];
     if (!P.stream) {
         HIP_CHECK(hipStreamCreateWithFlags(&P.stream, hipStreamNonBlocking));
         HIP_CHECK(hipEventCreateWithFlags(&P.done, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&P.stage_free, hipEventDisableTiming));
     }
-    if (!c->part_fork) HIP_CHECK(hipEventCreateWithFlags(&c->part_fork, hipEventDisableTiming));
-    if (frame_fits(c, f, paths, slots)) return;
-    const uint32_t cap = std::max(paths, f.capacity);
-    const uint32_t sl = std::max(slots, std::max(f.shadow_slots, 2u));
-    const uint32_t cap_r = queue_shard_capacity(cap);
-    const uint32_t cap_q = std::max(f.cap_q, cap_r * (c->opt_split_bins ? kSplitBins : 1u));
-    const size_t qsize = size_t(kQueueShards) * cap_r, qbuf = size_t(kQueueShards) * cap_q;
-    require(qsize * sl < (size_t(1) << 32) && qbuf < (size_t(1) << 32), "frame too large for 32-bit shadow slot ids",
-            DXRPT_E_INVALID_ARG);
-    for (int b = 0; b < 2; ++b) {
-        for (int i = 0; i < 4; ++i) P.q[b][i].ensure(qbuf * 16);
-        P.q[b][4].ensure(qbuf * 4);
-        f.q[b].org = P.q[b][0].as<float4>();
-        f.q[b].dir = P.q[b][1].as<float4>();
-        f.q[b].thr = P.q[b][2].as<float4>();
-        f.q[b].rad = P.q[b][3].as<float4>();
-        f.q[b].pix = P.q[b][4].as<uint32_t>();
+    if (!c->ovl_fork) HIP_CHECK(hipEventCreateWithFlags(&c->ovl_fork, hipEventDisableTiming));
+    if (!c->ovl_gate) HIP_CHECK(hipEventCreateWithFlags(&c->ovl_gate, hipEventDisableTiming));
+    const bool fits = frame_fits(P.fb, paths, slots) && P.stage.bytes >= stage_bytes;
+    if (fits) return;
+    drain_frames(c);
+    if (!frame_fits(P.fb, paths, slots)) {
+        alloc_frame(P.fb, P.q, P.shorg, P.shdir, P.shcon, paths, slots);
+        if (!P.counters.p) {
+            P.counters.ensure(2 * kCounterWords * sizeof(uint32_t));
+            P.ctr_clean[0] = P.ctr_clean[1] = false;
+            P.fb.counters = P.counters.as<uint32_t>();
+        }
     }
-    P.shorg.ensure(qsize * sl * 16);
-    P.shdir.ensure(qsize * sl * 16);
-    P.shcon.ensure(qsize * sl * 16);
-    if (!P.counters.p) {
-        P.counters.ensure(2 * kCounterWords * sizeof(uint32_t));
-        P.ctr_clean[0] = P.ctr_clean[1] = false;
-    }
-    f.sh_org = P.shorg.as<float4>();
-    f.sh_dir = P.shdir.as<float4>();
-    f.sh_con = P.shcon.as<float4>();
-    f.capacity = cap;
-    f.cap_r = cap_r;
-    f.cap_q = cap_q;
-    f.qsize = uint32_t(qsize);
-    f.shadow_slots = sl;
+    P.stage.ensure(stage_bytes);
 }
 
 // Adds one timed frame's event intervals to the per-kernel sums (blocks until the frame is done).
@@ -526,6 +495,16 @@ void harvest(dxrpt_ctx* c, dxrpt_ctx::FrameEvents& f) {
         if ((f.mask >> DXRPT_K_PATH) & 1u) {
             c->kernel_ms[DXRPT_K_PATH] += span(0, 1);
             c->kernel_launches[DXRPT_K_PATH]++;
+        }
+        if (f.split) {  // the head, then the tails back to back on the same stream
+            if ((f.mask >> DXRPT_K_PATH_HEAD) & 1u) {
+                c->kernel_ms[DXRPT_K_PATH_HEAD] += span(0, 2);
+                c->kernel_launches[DXRPT_K_PATH_HEAD]++;
+            }
+            if ((f.mask >> DXRPT_K_PATH_TAIL) & 1u && f.L > 2) {
+                c->kernel_ms[DXRPT_K_PATH_TAIL] += span(2, 1);
+                c->kernel_launches[DXRPT_K_PATH_TAIL] += uint64_t(f.L - 2);
+            }
         }
         c->frame_ms += span(0, 1);
         c->timed_frames++;
@@ -638,18 +617,9 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
     return guarded(ctx, [&] {
         if (option == DXRPT_OPT_COUNT_TRAVERSAL) {
             ctx->opt_count = value != 0;
-            if (ctx->opt_count) ctx->d_trav.ensure(5 * sizeof(unsigned long long));
+            if (ctx->opt_count) ctx->d_trav.ensure(kTravCounters * sizeof(unsigned long long));
         } else if (option == DXRPT_OPT_KERNEL_TIMING) {
             ctx->opt_timing = value != 0;
-        } else if (option == DXRPT_OPT_TRAVERSAL_MODE) {
-            require(value <= 1, "dxrpt_set_option: traversal mode must be 0 or 1");
-            ctx->opt_trav_mode = uint32_t(value);
-        } else if (option == DXRPT_OPT_TRACE_BLOCK) {
-            require(value == 64 || value == 128 || value == 256, "dxrpt_set_option: trace block must be 64, 128 or 256");
-            ctx->opt_trace_block = uint32_t(value);
-        } else if (option == DXRPT_OPT_OCCUPANCY || option == DXRPT_OPT_SHADOW_OCCUPANCY) {
-            require(value == 0 || value == 7 || value == 8, "dxrpt_set_option: occupancy must be 0, 7 or 8");
-            (option == DXRPT_OPT_OCCUPANCY ? ctx->opt_occupancy : ctx->opt_shadow_occ) = uint32_t(value);
         } else if (option == DXRPT_OPT_SPATIAL_SPLITS) {
             require(value <= 400, "dxrpt_set_option: spatial-split budget must be 0..400 (percent of triangles)");
             ctx->build_params.spatial_splits = value > 100;
@@ -657,49 +627,17 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_LEAF_COST) {
             require(value >= 5 && value <= 1000, "dxrpt_set_option: leaf cost must be 5..1000 (percent of a node visit)");
             ctx->build_params.leaf_cost = double(value) / 100.0;
-        } else if (option == DXRPT_OPT_CONCURRENCY) {
-            require(value <= 1, "dxrpt_set_option: concurrency must be 0 or 1");
-            ctx->opt_concurrency = uint32_t(value);
-        } else if (option == DXRPT_OPT_SHADOW_GRID) {
-            require(value <= 1u << 20, "dxrpt_set_option: shadow grid cap too large");
-            ctx->opt_shadow_grid = uint32_t(value);
-        } else if (option == DXRPT_OPT_TRAVERSAL_PIPELINE) {
-            require(value <= 3, "dxrpt_set_option: traversal pipeline must be 0..3");
-            ctx->opt_pipeline = uint32_t(value);
         } else if (option == DXRPT_OPT_PACKET_TRAVERSAL) {
             require(value <= 15, "dxrpt_set_option: packet traversal mask must be 0..15");
             ctx->opt_packet = uint32_t(value);
-        } else if (option == DXRPT_OPT_LDS_NODES) {
-            require(value <= 1024, "dxrpt_set_option: LDS node cache must be 0..1024 nodes");
-            ctx->opt_lds_nodes = uint32_t(value);
         } else if (option == DXRPT_OPT_KERNEL_TIMING_MASK) {
             require(value != 0 && value < (1u << DXRPT_K_COUNT), "dxrpt_set_option: timing mask must select kernel kinds");
             ctx->opt_timing_mask = uint32_t(value);
-        } else if (option == DXRPT_OPT_SHADE_BLOCK) {
-            require(value == 64 || value == 128 || value == 256, "dxrpt_set_option: shade block must be 64, 128 or 256");
-            ctx->opt_shade_block = uint32_t(value);
-        } else if (option == DXRPT_OPT_SHADE_OCCUPANCY) {
-            require(value == 0 || (value >= 6 && value <= 8), "dxrpt_set_option: shade occupancy must be 0, 6, 7 or 8");
-            ctx->opt_shade_occ = uint32_t(value);
-        } else if (option == DXRPT_OPT_POSTPONE_TRIS) {
-            require(value <= 64, "dxrpt_set_option: postpone threshold must be 0..64 lanes");
-            ctx->opt_postpone = uint32_t(value);
-        } else if (option == DXRPT_OPT_CHUNKS_PER_WAVE) {
-            require(value >= 1 && value <= 64, "dxrpt_set_option: chunks per wave must be 1..64");
-            ctx->opt_chunks = uint32_t(value);
-        } else if (option == DXRPT_OPT_REFILL_LANES) {
-            require(value >= 1 && value <= 64, "dxrpt_set_option: refill lanes must be in [1, 64]");
-            ctx->opt_refill = uint32_t(value);
-        } else if (option == DXRPT_OPT_XCD_MAPPING) {
-            require(value <= 1, "dxrpt_set_option: XCD mapping must be 0 or 1");
-            ctx->opt_xcd = uint32_t(value);
-        } else if (option == DXRPT_OPT_PACKET_SWITCH) {
-            require(value <= 100, "dxrpt_set_option: packet switch threshold must be 0..100 (percent)");
-            ctx->opt_packet_switch = uint32_t(value);
         } else if (option == DXRPT_OPT_WAVE_CLOCKS) {
             ctx->opt_wave_clocks = value != 0;
         } else if (option == DXRPT_OPT_WAVE_ORDER) {
             require(value <= 2, "dxrpt_set_option: wave order must be 0, 1 or 2");
+            drain_frames(ctx);  // an in-flight frame may read the order
             ctx->opt_wave_order = uint32_t(value);
             ctx->order_ready = false;
         } else if (option == DXRPT_OPT_XCD_CHUNK) {
@@ -708,52 +646,36 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
         } else if (option == DXRPT_OPT_WAVE_ORDER_PERIOD) {
             require(value >= 1 && value <= 1024, "dxrpt_set_option: wave order period must be 1..1024 frames");
             ctx->opt_order_period = uint32_t(value);
-        } else if (option == DXRPT_OPT_SPLIT_UNITS) {
-            require(value <= 1000, "dxrpt_set_option: split units must be 0..1000 (per mille of the waves)");
-            ctx->opt_split_permille = uint32_t(value);
         } else if (option == DXRPT_OPT_MEGAKERNEL_PATHS) {
             ctx->opt_mega_paths = value > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(value);
         } else if (option == DXRPT_OPT_MEGAKERNEL_OCCUPANCY) {
-            require(value == 0 || (value >= 3 && value <= 8), "dxrpt_set_option: megakernel occupancy must be 0 or 3..8");
+            require(value == 0 || (value >= 4 && value <= 7), "dxrpt_set_option: megakernel occupancy must be 0 or 4..7");
             ctx->opt_mega_occ = uint32_t(value);
-        } else if (option == DXRPT_OPT_MEGAKERNEL_PERSISTENT) {
-            require(value <= 64, "dxrpt_set_option: persistent megakernel waves per CU must be 0..64");
-            ctx->opt_mega_persistent = uint32_t(value);
-        } else if (option == DXRPT_OPT_MEGAKERNEL_LANES) {
-            require(value == 0 || value == 16 || value == 32 || value == 64,
-                    "dxrpt_set_option: megakernel lanes must be 0 (by frame size), 16, 32 or 64");
-            ctx->opt_mega_lanes = uint32_t(value);
+        } else if (option == DXRPT_OPT_TAIL_OCCUPANCY) {
+            require(value == 0 || (value >= 4 && value <= 7), "dxrpt_set_option: tail occupancy must be 0 or 4..7");
+            ctx->opt_tail_occ = uint32_t(value);
         } else if (option == DXRPT_OPT_BAKE_CHUNK) {
             require(value >= 64 && value <= (1u << 26), "dxrpt_set_option: bake chunk must be 64..2^26 texels");
             ctx->opt_bake_chunk = uint32_t(value);
         } else if (option == DXRPT_OPT_MEGAKERNEL_SPLIT) {
             require(value <= 2, "dxrpt_set_option: megakernel split must be 0 (off), 1 (on) or 2 (by frame size)");
             ctx->opt_split = uint32_t(value);
-        } else if (option == DXRPT_OPT_SPLIT_PARTS) {
-            require(value <= 2, "dxrpt_set_option: split parts must be 0 (by frame size), 1 or 2");
-            ctx->opt_split_parts = uint32_t(value);
-        } else if (option == DXRPT_OPT_SPLIT_ALPHA) {
-            require(value <= 1, "dxrpt_set_option: split alpha must be 0 or 1");
-            ctx->opt_split_alpha = uint32_t(value);  // takes effect at the next dxrpt_build_bvh
-        } else if (option == DXRPT_OPT_SPLIT_BINS) {
-            require(value <= 1, "dxrpt_set_option: split bins must be 0 (off) or 1 (on)");
-            ctx->opt_split_bins = uint32_t(value);
         } else if (option == DXRPT_OPT_FRAME_OVERLAP) {
-            require(value < kMaxOverlapFrames, "dxrpt_set_option: frame overlap must be 0 (off), 1 (two frames in flight) or 2 (three)");
+            require(value <= 1, "dxrpt_set_option: frame overlap must be 0 (off) or 1 (two frames in flight)");
             if (uint32_t(value) != ctx->opt_overlap) {  // the slot rotation restarts
-                drain_overlap(ctx);
+                drain_frames(ctx);
                 ctx->ovl_parity = 0;
             }
             ctx->opt_overlap = uint32_t(value);
         } else if (option == DXRPT_OPT_OPACITY_MICROMAP) {
             require(value <= 1, "dxrpt_set_option: opacity micromap must be 0 (off) or 1 (on)");
+            drain_frames(ctx);  // in-flight frames may read the micromap
             ctx->opt_omm = uint32_t(value);
-        } else if (option == DXRPT_OPT_TAIL_OCCUPANCY) {
-            require(value == 0 || (value >= 4 && value <= 8), "dxrpt_set_option: tail occupancy must be 0 (by frame) or 4..8");
-            ctx->opt_tail_occ = uint32_t(value);
-        } else if (option == DXRPT_OPT_BVH_WIDTH) {
-            require(value == 2 || value == 8, "dxrpt_set_option: BVH width must be 2 or 8");
-            ctx->opt_width = int(value);  // takes effect at the next dxrpt_build_bvh
+        } else if ((option >= 3 && option <= 11) || (option >= 14 && option <= 17) || option == 19 || option == 21 ||
+                   option == 22 || option == 26 || option == 27 || option == 30 || option == 35 || option == 38 ||
+                   option == 39) {
+            throw ApiError(DXRPT_E_UNSUPPORTED, "dxrpt_set_option: option " + std::to_string(option) +
+                                                    " was retired in ABI 3 (measured slower or neutral; DESIGN.md §7a)");
         } else {
             throw ApiError(DXRPT_E_INVALID_ARG, "dxrpt_set_option: unknown option " + std::to_string(option));
         }
@@ -778,7 +700,7 @@ int dxrpt_set_scene(dxrpt_ctx* ctx, const dxrpt_mesh_vertex* vertices, uint32_t 
                     uint32_t num_geometries, const dxrpt_material* materials, uint32_t num_materials) {
     if (!ctx) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
-        drain_overlap(ctx);
+        drain_frames(ctx);
         require(vertices && indices && geometries && materials, "dxrpt_set_scene: null array");
         require(idx_bytes == 2 || idx_bytes == 4, "dxrpt_set_scene: idx_bytes must be 2 or 4");
         require(num_indices % 3 == 0 && num_indices > 0, "dxrpt_set_scene: num_indices must be a positive multiple of 3");
@@ -798,10 +720,6 @@ int dxrpt_set_scene(dxrpt_ctx* ctx, const dxrpt_mesh_vertex* vertices, uint32_t 
             require(gi.IdxOffset % 3 == 0 && gi.IdxOffset < num_indices, "dxrpt_set_scene: bad IdxOffset in geometry " + std::to_string(g));
             require(gi.MaterialIdx < num_materials, "dxrpt_set_scene: bad MaterialIdx in geometry " + std::to_string(g));
         }
-        ctx->d_vertices.upload(ctx->vertices.data(), ctx->vertices.size() * sizeof(dxrpt_mesh_vertex));
-        ctx->d_indices.upload(ctx->indices.data(), ctx->indices.size() * 4);
-        ctx->d_geos.upload(ctx->geos.data(), ctx->geos.size() * sizeof(dxrpt_geometry_info));
-        ctx->d_mats.upload(ctx->mats.data(), ctx->mats.size() * sizeof(dxrpt_material));
         ctx->geoshade_dirty = true;
         ctx->omm_dirty = true;
         ctx->scene_set = true;
@@ -812,7 +730,7 @@ int dxrpt_set_scene(dxrpt_ctx* ctx, const dxrpt_mesh_vertex* vertices, uint32_t 
 int dxrpt_add_texture(dxrpt_ctx* ctx, uint32_t w, uint32_t h, uint32_t fmt, const void* texels, uint32_t* out_index) {
     if (!ctx) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
-        drain_overlap(ctx);
+        drain_frames(ctx);
         require(texels && w > 0 && h > 0, "dxrpt_add_texture: empty texture");
         require(w <= 16384 && h <= 16384, "dxrpt_add_texture: texture larger than 16384");
         require(fmt <= DXRPT_TEX_R8_UNORM, "dxrpt_add_texture: unknown format");
@@ -849,7 +767,7 @@ int dxrpt_add_texture(dxrpt_ctx* ctx, uint32_t w, uint32_t h, uint32_t fmt, cons
 int dxrpt_set_sky(dxrpt_ctx* ctx, const uint16_t* cube, uint32_t res) {
     if (!ctx) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
-        drain_overlap(ctx);
+        drain_frames(ctx);
         require(cube && res > 0 && res <= 4096, "dxrpt_set_sky: bad cube");
         ctx->d_sky.upload(cube, size_t(res) * res * 6 * 4 * sizeof(uint16_t));
         ctx->sky_res = res;
@@ -860,7 +778,7 @@ int dxrpt_set_sky(dxrpt_ctx* ctx, const uint16_t* cube, uint32_t res) {
 int dxrpt_build_bvh(dxrpt_ctx* ctx) {
     if (!ctx) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
-        drain_overlap(ctx);
+        drain_frames(ctx);
         require(ctx->scene_set, "dxrpt_build_bvh: no scene (call dxrpt_set_scene first)", DXRPT_E_STATE);
         auto t0 = std::chrono::steady_clock::now();
         // Global triangle list: gtri = IdxOffset/3 + PrimitiveIndex for every geometry.
@@ -885,24 +803,21 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
         }
         BvhBuildResult res;
         std::string err;
-        // DXRPT_OPT_SPLIT_ALPHA 0: spatial splits leave alpha-tested triangles whole (each extra reference
-        // of one is another AnyHitShader opacity test)
+        // spatial splits leave alpha-tested triangles whole: each extra reference of one is another
+        // AnyHitShader opacity test (r03: SAH 67.5 -> 63.1 on the Sponza proxy, metric -2.4 %, C4 -1.3 %)
         std::vector<uint8_t> alpha_tri(ntris);
         for (uint32_t t = 0; t < ntris; ++t)
             alpha_tri[t] = ctx->mats[ctx->geos[tri_geom[t]].MaterialIdx].Opacity != DXRPT_INVALID_INDEX ? 1u : 0u;
         BvhBuildParams bp = ctx->build_params;
-        if (!ctx->opt_split_alpha) bp.keep_whole = alpha_tri.data();
-        bp.alpha_tri = alpha_tri.data();
-        bp.alpha_cost = DXRPT_ALPHA_TRI_COST;  // (build-time A/B knob, see below)
-        if (!build_bvh(pos.data(), ntris, ctx->opt_width, res, err, &bp))
-            throw ApiError(DXRPT_E_INVALID_ARG, err);
-        // one record per leaf reference (BVH8 spatial splits may reference a triangle more than once)
+        bp.keep_whole = alpha_tri.data();
+        if (!build_bvh(pos.data(), ntris, 8, res, err, &bp)) throw ApiError(DXRPT_E_INVALID_ARG, err);
+        // one record per leaf reference (spatial splits may reference a triangle more than once)
         const uint32_t nrefs = uint32_t(res.tri_order.size());
         // opacity micromap slots: the triangles of alpha-tested geometry in global order
         std::vector<uint32_t> slot_of(ntris, 0u);
         ctx->omm_tris.clear();
         for (uint32_t t = 0; t < ntris; ++t)
-            if (ctx->mats[ctx->geos[tri_geom[t]].MaterialIdx].Opacity != DXRPT_INVALID_INDEX) {
+            if (alpha_tri[t]) {
                 slot_of[t] = uint32_t(ctx->omm_tris.size());
                 ctx->omm_tris.push_back(t);
             }
@@ -912,8 +827,7 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
             const float* v = &pos[size_t(t) * 9];
             TriRecord& r = tris[i];
             const uint32_t g = tri_geom[t];
-            const bool opaque = ctx->mats[ctx->geos[g].MaterialIdx].Opacity == DXRPT_INVALID_INDEX;
-            uint32_t flags = opaque ? kTriOpaque : slot_of[t] << 1;
+            uint32_t flags = alpha_tri[t] ? slot_of[t] << 1 : kTriOpaque;
             r.p0[0] = v[0]; r.p0[1] = v[1]; r.p0[2] = v[2];
             r.p1[0] = v[3] - v[0]; r.p1[1] = v[4] - v[1]; r.p1[2] = v[5] - v[2];
             r.p2[0] = v[6] - v[0]; r.p2[1] = v[7] - v[1]; r.p2[2] = v[8] - v[2];
@@ -921,19 +835,14 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
             std::memcpy(&r.p1[3], &g, 4);
             std::memcpy(&r.p2[3], &flags, 4);
         }
-        if (ctx->opt_width == 8) {
-            if (kNode8Stride == sizeof(Bvh8Node)) {
-                ctx->d_nodes8.upload(res.nodes8.data(), res.nodes8.size() * sizeof(Bvh8Node));
-            } else {  // padded device layout (pt_layout.h kNode8Stride)
-                std::vector<uint8_t> padded(res.nodes8.size() * size_t(kNode8Stride), 0u);
-                for (size_t i = 0; i < res.nodes8.size(); ++i)
-                    std::memcpy(padded.data() + i * kNode8Stride, &res.nodes8[i], sizeof(Bvh8Node));
-                ctx->d_nodes8.upload(padded.data(), padded.size());
-            }
-        } else {
-            ctx->d_nodes.upload(res.nodes.data(), res.nodes.size() * sizeof(BvhNode));
+        if (kNode8Stride == sizeof(Bvh8Node)) {
+            ctx->d_nodes8.upload(res.nodes8.data(), res.nodes8.size() * sizeof(Bvh8Node));
+        } else {  // padded device layout (pt_layout.h kNode8Stride)
+            std::vector<uint8_t> padded(res.nodes8.size() * size_t(kNode8Stride), 0u);
+            for (size_t i = 0; i < res.nodes8.size(); ++i)
+                std::memcpy(padded.data() + i * kNode8Stride, &res.nodes8[i], sizeof(Bvh8Node));
+            ctx->d_nodes8.upload(padded.data(), padded.size());
         }
-        tris.resize(size_t(nrefs) + 6u, TriRecord{});  // padding: packet chunk loads read up to 256 B past a record
         ctx->d_tris.upload(tris.data(), tris.size() * sizeof(TriRecord));
         {   // shading-side copy of each triangle's vertices: one contiguous 192-B record per gtri, so a
             // hit gathers 2 cache lines in one round trip instead of 3 indices then 3 vertices
@@ -944,16 +853,16 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
             ctx->d_tri_verts.upload(tv.data(), tv.size() * sizeof(dxrpt_mesh_vertex));
         }
         auto t1 = std::chrono::steady_clock::now();
-        ctx->bvh.num_nodes = uint32_t(ctx->opt_width == 8 ? res.nodes8.size() : res.nodes.size());
+        ctx->bvh.num_nodes = uint32_t(res.nodes8.size());
         ctx->bvh.num_leaves = res.num_leaves;
         ctx->bvh.num_tris = ntris;
         ctx->bvh.max_depth = res.max_depth;
-        ctx->bvh.node_bytes = ctx->opt_width == 8 ? uint32_t(sizeof(Bvh8Node)) : uint32_t(sizeof(BvhNode));
-        ctx->bvh.width = uint32_t(ctx->opt_width);
+        ctx->bvh.node_bytes = uint32_t(sizeof(Bvh8Node));
+        ctx->bvh.width = 8u;
         ctx->bvh.tri_bytes = sizeof(TriRecord);
         ctx->bvh.build_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
         ctx->bvh.sah_cost = res.sah_cost;
-        ctx->built_width = ctx->opt_width;
+        ctx->spill_threads = 0;  // the depth may have changed: the next launch re-sizes the spill slabs
         ctx->bvh_built = true;
         ctx->omm_dirty = true;
         ctx->omm_any = false;
@@ -997,7 +906,7 @@ uint32_t prepare_tiles(dxrpt_ctx* ctx, const dxrpt_tile* tiles, uint32_t num_til
     for (const dxrpt_tile& t : tl) extent = std::max<uint64_t>(extent, t.accum_offset + uint64_t(t.h - 1) * t.accum_pitch + t.w);
     ctx->accum_extent = uint32_t(extent);
     if (tl.size() != ctx->tiles_cache.size() || std::memcmp(tl.data(), ctx->tiles_cache.data(), tl.size() * sizeof(dxrpt_tile)) != 0) {
-        drain_overlap(ctx);
+        drain_frames(ctx);
         ctx->d_tiles.upload(tl.data(), tl.size() * sizeof(dxrpt_tile));
         ctx->d_tile_prefix.upload(prefix.data(), prefix.size() * sizeof(uint32_t));
         ctx->tiles_cache = tl;
@@ -1010,15 +919,16 @@ int dxrpt_render_aov(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const
                      uint32_t width, uint32_t height, const dxrpt_tile* tiles, uint32_t num_tiles, void* stream) {
     if (!ctx) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
-        drain_overlap(ctx);
         require(ctx->bvh_built, "dxrpt_render_aov: acceleration structure not built", DXRPT_E_STATE);
-        require(ctx->built_width == 8, "dxrpt_render_aov: needs the BVH8 layout", DXRPT_E_UNSUPPORTED);
         require(rtc && settings && out, "dxrpt_render_aov: null argument");
         require(width > 0 && height > 0, "dxrpt_render_aov: empty image");
         require(uint64_t(width) * height == rtc->TotalNumPixels, "dxrpt_render_aov: TotalNumPixels != width*height");
         require(settings->SqrtNumSamples >= 1, "dxrpt_render_aov: SqrtNumSamples must be >= 1");
+        const hipStream_t s = static_cast<hipStream_t>(stream);
+        enter_stream(ctx, s);
         upload_textures(ctx);
         const uint32_t paths = prepare_tiles(ctx, tiles, num_tiles, width, height, "dxrpt_render_aov");
+        ensure_spill(ctx, frame_traversal_threads(paths, 1u, true));
         FrameParams fp{};
         fp.rtc = *rtc;
         fp.set = *settings;
@@ -1030,8 +940,9 @@ int dxrpt_render_aov(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const
         fp.width = width;
         fp.height = height;
         fp.packet = ctx->opt_packet;
-        HIP_CHECK(launch_primary_aov(scene_dev(ctx, ((paths + 255u) / 256u) * 256u), ctx->fb, fp,
-                                     static_cast<hipStream_t>(stream)));
+        HIP_CHECK(launch_primary_aov(scene_dev(ctx, 0), ctx->fb, fp, s));
+        ctx->ovl_active = false;  // the next overlapped frame starts behind this call (slab 0)
+        ctx->inflight = true;
     });
 }
 
@@ -1050,26 +961,28 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
                 "dxrpt_render: MaxPathLength must be in [1, 8]");
         const bool useLights = settings->RenderLights && rtc->NumLights > 0;
         require(!useLights || (lights && rtc->NumLights <= DXRPT_MAX_SPOT_LIGHTS), "dxrpt_render: bad lights");
-        upload_textures(ctx);
         for (const dxrpt_material& m : ctx->mats) {
             const uint32_t nt = uint32_t(ctx->texdesc.size());
             require(m.Albedo < nt && m.Normal < nt && m.Roughness < nt && m.Metallic < nt && m.Emissive < nt &&
                         (m.Opacity == DXRPT_INVALID_INDEX || m.Opacity < nt),
                     "dxrpt_render: material references a texture that was not added");
         }
+        const hipStream_t s = static_cast<hipStream_t>(stream);
+        enter_stream(ctx, s);
+        upload_textures(ctx);
         const uint32_t paths = prepare_tiles(ctx, tiles, num_tiles, width, height, "dxrpt_render");
-        const std::vector<dxrpt_tile>& tl = ctx->tiles_cache;
-        uint32_t nl = useLights ? rtc->NumLights : 0u;
+        const uint32_t nl = useLights ? rtc->NumLights : 0u;
         if (nl) {
             std::vector<dxrpt_spot_light> L(lights->Lights, lights->Lights + nl);
             if (L.size() != ctx->lights_cache.size() || std::memcmp(L.data(), ctx->lights_cache.data(), nl * sizeof(dxrpt_spot_light)) != 0) {
-                drain_overlap(ctx);
+                drain_frames(ctx);
                 ctx->d_lights.upload(L.data(), nl * sizeof(dxrpt_spot_light));
                 ctx->lights_cache = L;
             }
         }
-        ensure_frame(ctx, paths, 2u + nl);
-        FrameParams fp;
+        const uint32_t slots = 2u + nl;  // shadow slots per vertex: sun, spot lights, final sky visibility
+        const int L = settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength;
+        FrameParams fp{};
         fp.rtc = *rtc;
         fp.rtc.NumLights = nl;
         fp.set = *settings;
@@ -1077,170 +990,87 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.tiles = ctx->d_tiles.as<dxrpt_tile>();
         fp.tile_prefix = ctx->d_tile_prefix.as<uint32_t>();
         fp.accum = reinterpret_cast<float4*>(accum);
-        fp.num_tiles = uint32_t(tl.size());
+        fp.num_tiles = uint32_t(ctx->tiles_cache.size());
         fp.num_paths = paths;
         fp.width = width;
         fp.height = height;
-        fp.trav = nullptr;
-        fp.wave_clock = nullptr;
-        fp.wave_order = nullptr;
-        fp.wave_cost = nullptr;
-        fp.wave_hist = nullptr;
-        fp.split_units = 0;
         fp.xcd_chunk = ctx->opt_xcd_chunk;
-        // 32 KiB of LDS per 256-thread workgroup -> 5 resident workgroups per CU (160 KiB)
-        fp.chunks_per_wave = ctx->opt_trav_mode == 1 ? ctx->opt_chunks : 0u;
-        fp.refill_lanes = ctx->opt_refill;
-        fp.postpone_tris = ctx->opt_postpone;
-        fp.trace_block = ctx->opt_trace_block;
-        fp.occupancy = ctx->opt_occupancy;
-        fp.shadow_occupancy = ctx->opt_shadow_occ;
-        fp.shadow_grid = ctx->opt_shadow_grid;
-        fp.pipeline = ctx->opt_pipeline;
         fp.packet = ctx->opt_packet;
-        fp.lds_nodes = ctx->opt_lds_nodes;
         fp.timing_mask = ctx->opt_timing_mask;
-        fp.shade_block = ctx->opt_shade_block;
-        fp.shade_occupancy = ctx->opt_shade_occ;
-        fp.xcd_map = ctx->opt_xcd;
-        fp.packet_switch = ctx->opt_packet_switch;
-        // megakernel schedule for every frame by default (BVH8, one thread per ray traversal):
-        // DXRPT_OPT_MEGAKERNEL_PATHS bounds it by path vertices = paths x (L-1); since r02 the megakernel
-        // (and, from 8M vertices, its depth-split form) beats the wavefront passes at every BASELINE size,
-        // which stay selectable (DXRPT_OPT_MEGAKERNEL_PATHS 0) and parity-tested at full size
-        const uint64_t vertices = uint64_t(paths) * uint64_t((settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength) - 1);
-        fp.megakernel = (vertices <= ctx->opt_mega_paths && ctx->built_width == 8 && ctx->opt_trav_mode == 0) ? 1u : 0u;
-        // register budget by frame size (measured, Sponza proxy 1080p L=3 and its 1/2, 1/4, 1/8 shares):
-        // more resident waves hide more latency once a frame has waves for several rounds; a GPU's 1/8
-        // share (~4k waves) fits in one round at 4 waves/SIMD without spills
-        // Small frames (a GPU's 1/8 share of 1080p and below) end with their slowest waves' paths
-        // (alpha-tested foliage, scripts/wave_clocks.py): two lanes per path trace a vertex's
-        // continuation and shadow rays concurrently, shortening those chains (1/8 share 0.72-0.76 ->
-        // 0.68-0.69 ms at 6 waves/SIMD, profiles/r02_ab_path_groups_shares.txt); from the 1/4 share up
-        // the doubled waves cost more than the shorter chains save.
-        // With overlapped frames (r03, profiles/r03_ab_overlap_tune*.txt) the next frame's waves fill a
-        // small frame's end, and 64-lane waves win at every size: 1/8 share 0.41 -> 0.31 ms (ranks 5, 0),
-        // 0.41 -> 0.36 (rank 2); C3's 1/8 share 1.32 -> 0.99.  Path groups stay the default only for
-        // one-frame-at-a-time contexts (DXRPT_OPT_FRAME_OVERLAP 0).
-        const uint32_t lanes = ctx->opt_mega_lanes ? ctx->opt_mega_lanes
-                             : (!ctx->opt_overlap && paths <= 400000u ? 32u : 64u);
-        // (with cost-ordered waves, r02: path groups 5 waves/SIMD, 1/8 share 0.574 -> 0.562 ms; 600k-1.5M
-        // paths 6, 720p 1.111 -> 1.095 and the 1/2 share 1.20 -> 1.165 ms; profiles/r02_ab_occ_mid_frames.txt)
-        // (r02, late: a GPU's 1/4 share, 518k paths, 4 waves/SIMD instead of 5: slowest rank 0.742 -> 0.729 ms,
-        // profiles/r02_ab_occ_quarter_share.txt; 600k-1.5M paths 7 instead of 6: 720p 1.098 -> 1.090, the 1/2
-        // share 1.174 -> 1.164, profiles/r02_ab_occ_mid_frames_head.txt)
-        // (r03, overlapped frames: 64-lane frames of 300k-600k paths 6 waves/SIMD, a 1/4 share 0.560 ->
-        // 0.520 ms; up to 300k 4 -- 1/8 share 0.305 / 0.317 / 0.329 ms at 4 / 5 / 6)
+        fp.num_cus = ctx->num_cus;
+        // megakernel schedules for every frame by default: DXRPT_OPT_MEGAKERNEL_PATHS bounds them by path
+        // vertices = paths x (L-1); the wavefront passes (the north star's per-stage kernels) stay selectable
+        // (DXRPT_OPT_MEGAKERNEL_PATHS 0) and parity-tested at full size
+        const uint64_t vertices = uint64_t(paths) * uint64_t(L - 1);
+        fp.megakernel = vertices <= ctx->opt_mega_paths ? 1u : 0u;
+        // register budget by frame size (measured on the Sponza proxy 1080p L=3 and its band shares): more
+        // resident waves hide more latency once a frame has waves for several rounds; a GPU's 1/8 share fits
+        // in one round at 4 waves/SIMD without spills.  r03 with overlapped frames: 600k+ paths 7, 300k-600k
+        // 6 (a 1/4 share 0.560 -> 0.520 ms), below 4 (1/8 share 0.305 / 0.317 / 0.329 ms at 4 / 5 / 6)
         fp.megakernel_occupancy = ctx->opt_mega_occ ? ctx->opt_mega_occ
-                                : lanes < 64u ? 5u
                                 : paths > 600000u ? 7u
                                 : (ctx->opt_overlap && paths > 300000u ? 6u : 4u);
-        fp.mega_persistent = ctx->opt_mega_persistent;
-        fp.mega_lanes = lanes;
-        // depth-split schedule (k_path_head + one compacting k_path_tail per depth): 64-lane path-ordered
-        // frames.  By frame size (r03 A/B, profiles/r03_ab_msplit*.txt): it wins where there are many path
-        // vertices per frame (1080p L=8 6.90 -> 6.52 ms, 4K L=6 18.50 -> 17.04) and loses on short paths
-        // (1080p L=3 2.07 -> 2.23, L=4 3.09 -> 3.18; L=5 even), where each kernel's drain is a larger
-        // part of its time.  Budgets: head 6 waves/SIMD (80 VGPRs), tails 7 (72); with overlapped frames
-        // the head 7 too (metric 1.879 -> 1.862 ms, C4 2.031 -> 2.004, C3 5.58 -> 5.56, C5 share even)
-        // (r03, overlapped frames, profiles/r03_ab_msplit_overlap*.txt: the next frame's waves fill each
-        // per-depth kernel's drain, so the split pays from 4M vertices: metric 1.909 -> 1.875 ms, C4 2.042 ->
-        // 2.029, C5's 1/8 share 2.349 -> 2.098, C3 5.65 -> 5.59 with one part; it still loses below --
-        // 720p 0.902 -> 0.925, C3's 1/8 share 0.979 -> 1.031; the 1/2 share even)
-        // (r03 final, spill-free head: from 2M vertices -- the metric's 1/2 share, 2.07M, 0.961 -> 0.939 ms;
-        // still not 720p, 1.84M, 0.881 -> 0.893, C3's 1/8 share, 1.81M, 0.965 -> 0.986, or the 1/4 share,
-        // 1.04M, 0.512 -> 0.566; profiles/r03_ab_split_small.txt)
-        const bool split_by_size =
-            vertices >= (ctx->opt_overlap ? kSplitMinVerticesOverlap : kSplitMinVertices) && lanes == 64u;
-        fp.split = (ctx->opt_split == 1u || (ctx->opt_split == 2u && split_by_size)) && lanes == 64u && fp.megakernel ? 1u : 0u;
-        // (r03 final: with overlapped frames the head at 5 waves/SIMD -- 96 VGPRs, no spills -- metric
-        // -0.2 %, C3 -0.4 %, C5's share -1.0 %, C4 +0.5 % against 7, profiles/r03_ab_head_occ_final.txt)
+        // depth-split schedule (k_path_head + one compacting k_path_tail per depth): it wins where there are
+        // many path vertices per frame and loses on short paths, where each kernel's drain is a larger part
+        // of its time -- unless overlapped frames fill the drains (r03: from 2M vertices, the metric's 1/2
+        // share 0.961 -> 0.939 ms; 720p, C3's 1/8 share and the 1/4 share stay k_path, +1.4 / +2.2 / +10.6 %
+        // split; profiles/r03_ab_msplit*.txt, r03_ab_split_small.txt)
+        const bool split_by_size = vertices >= (ctx->opt_overlap ? kSplitMinVerticesOverlap : kSplitMinVertices);
+        fp.split = fp.megakernel && (ctx->opt_split == 1u || (ctx->opt_split == 2u && split_by_size)) ? 1u : 0u;
+        // split budgets: the head 5 waves/SIMD (96 VGPRs, no spills; r03: metric -0.2 %, C3 -0.4 %, C5's share
+        // -1.0 %, C4 +0.5 % against 7), the tails 7 (72 VGPRs; 6: -2-3 %)
         if (fp.split && !ctx->opt_mega_occ) fp.megakernel_occupancy = ctx->opt_overlap ? 5u : 6u;
-        fp.split_bins = fp.split ? ctx->opt_split_bins : 0u;
         fp.tail_occupancy = ctx->opt_tail_occ ? ctx->opt_tail_occ : (ctx->opt_mega_occ ? fp.megakernel_occupancy : 7u);
-        fp.path_base = 0;
-        fp.num_cus = ctx->num_cus;
-        hipStream_t s = static_cast<hipStream_t>(stream);
         ctx->wclock_waves = 0;  // set again below only by a frame that records stamps
+        // Overlapped frames (DXRPT_OPT_FRAME_OVERLAP, megakernel frames): frame parity ov runs on slot ov --
+        // its stream, buffers, counters and BVH8 stack-spill slab -- and stages its radiance; the caller's
+        // stream blends the stage after it, so the next frame (the other parity) may start as soon as it is
+        // launched, filling this frame's drain.  Census and wave-clock frames run on the caller's stream.
+        const bool overlap = ctx->opt_overlap && fp.megakernel && !ctx->opt_count && !ctx->opt_wave_clocks && paths > 0;
+        ensure_spill(ctx, frame_traversal_threads(paths, slots, fp.megakernel != 0));
+        const uint32_t ov = ctx->ovl_parity;
+        dxrpt_ctx::Slot& P = ctx->slot[ov];
+        hipStream_t fs = s;  // the frame's stream
+        if (overlap) {
+            ensure_slot(ctx, ov, paths, slots, size_t(ctx->accum_extent) * 16u);
+            fs = P.stream;
+            if (!ctx->ovl_active) {  // after other work: start behind the caller's stream
+                HIP_CHECK(hipEventRecord(ctx->ovl_fork, s));
+                HIP_CHECK(hipStreamWaitEvent(fs, ctx->ovl_fork, 0));
+                for (dxrpt_ctx::Slot& Q : ctx->slot) Q.stage_used = false;
+                ctx->ovl_gate_set = false;
+            }
+            if (P.stage_used) HIP_CHECK(hipStreamWaitEvent(fs, P.stage_free, 0));  // the stage's previous blend
+            if (ctx->ovl_gate_set) HIP_CHECK(hipStreamWaitEvent(fs, ctx->ovl_gate, 0));  // the new wave order
+            ctx->ovl_gate_set = false;
+        } else {
+            ensure_frame(ctx, paths, slots);
+        }
         if (ctx->opt_count) {
             fp.trav = ctx->d_trav.as<unsigned long long>();
-            HIP_CHECK(hipMemsetAsync(fp.trav, 0, 5 * sizeof(unsigned long long), s));
+            HIP_CHECK(hipMemsetAsync(fp.trav, 0, kTravCounters * sizeof(unsigned long long), s));
             if (ctx->opt_wave_clocks && fp.megakernel) {  // census: the 64-lane kernel, one slot per 64 paths
                 ctx->wclock_waves = (paths + 63u) / 64u;
                 ctx->d_wclock.ensure(size_t(ctx->wclock_waves) * 2 * sizeof(unsigned long long));
                 fp.wave_clock = ctx->d_wclock.as<unsigned long long>();
             }
         }
-        // cost-ordered waves (default megakernel schedules only: not the census, persistent or LDS-node ones)
-        // By frame size (2): frames of at most 3 rounds of resident waves, whose end is a large part of
-        // their time (a GPU's share of a multi-GPU frame, 720p: -10..-14 %); a full 1080p frame (4.5
-        // rounds) keeps path order, where concurrent neighbouring blocks share more cache than the
-        // shorter tail saves (profiles/r02_ab_wave_order.txt).
-        // Overlapped frames (DXRPT_OPT_FRAME_OVERLAP, megakernel frames): frame parity ov runs on parts 2ov
-        // (and 2ov + 1 for a split frame's second half) -- their streams, buffers, counters and BVH8
-        // stack-spill slabs -- and stages its radiance; the caller's stream blends the stage after it, so
-        // the next frame (the other parity) may start as soon as it is launched, filling this frame's
-        // drain.  Its waits: the stage's previous blend, and the previous frame's order pass (a recording
-        // frame).  The first overlapped frame after other work waits for the caller's stream.
-        const bool overlap = ctx->opt_overlap && fp.megakernel && !ctx->opt_count && !ctx->opt_wave_clocks &&
-                             !fp.mega_persistent && !ctx->opt_lds_nodes && paths > 0;
-        // split frames of at most kSplitPartsMaxPaths paths run as two concurrent parts (the top and the
-        // bottom half of the path slots, each with its own queues and counters, on two internal streams):
-        // one part's per-depth kernels fill the other's drains (1080p L=8 6.52 -> 5.91 ms; a 4K frame
-        // keeps one part: its kernels are long enough, 17.04 -> 17.15 with two).  Overlapped frames keep
-        // one part: the next frame fills the drains (C3 5.65 -> 5.59 ms, C5's 1/8 share 2.295 -> 2.098)
-        const uint32_t nparts = !(fp.split && !ctx->opt_count && !fp.mega_persistent && !ctx->opt_lds_nodes) ? 1u
-                              : ctx->opt_split_parts ? ctx->opt_split_parts
-                              : (!ctx->opt_overlap && paths <= kSplitPartsMaxPaths ? 2u : 1u);
-        const bool halves = nparts == 2u && paths >= 128u;
-        const uint32_t half = ((paths / 64u) / 2u) * 64u;  // a multiple of 64: parts keep whole 8x8 blocks
-        const uint32_t cnt[2] = {halves ? half : paths, paths - half}, base[2] = {0u, half};
-        const int ov = int(ctx->ovl_parity);
-        const int pb = overlap ? 2 * ov : 0;  // the frame's first part
-        hipStream_t fs = s;
-        FrameParams fo{};
-        if (overlap) {
-            const size_t stage_bytes = size_t(ctx->accum_extent) * 16u;
-            bool fits = ctx->d_stage[ov].bytes >= stage_bytes;
-            for (int k = 0; k < (halves ? 2 : 1); ++k) {
-                const FrameBuffers& b = ctx->part[pb + k].fb;
-                fits = fits && frame_fits(ctx, b, cnt[k], 2u + nl);
-            }
-            if (!fits) drain_overlap(ctx);  // buffers about to be (re)allocated
-            for (int k = 0; k < (halves ? 2 : 1); ++k) ensure_part(ctx, pb + k, cnt[k], 2u + nl);
-            ctx->d_stage[ov].ensure(stage_bytes);
-            if (!ctx->stage_free[ov]) HIP_CHECK(hipEventCreateWithFlags(&ctx->stage_free[ov], hipEventDisableTiming));
-            if (!ctx->ovl_gate) HIP_CHECK(hipEventCreateWithFlags(&ctx->ovl_gate, hipEventDisableTiming));
-            fs = ctx->part[pb].stream;
-            const bool first = !ctx->ovl_inflight;
-            if (first) {  // after non-overlapped work: start behind the caller's stream
-                HIP_CHECK(hipEventRecord(ctx->part_fork, s));
-                for (bool& u : ctx->stage_used) u = false;
-                ctx->ovl_gate_set = false;
-            }
-            for (int k = 0; k < (halves ? 2 : 1); ++k) {
-                hipStream_t st = ctx->part[pb + k].stream;
-                if (first) HIP_CHECK(hipStreamWaitEvent(st, ctx->part_fork, 0));
-                if (ctx->stage_used[ov]) HIP_CHECK(hipStreamWaitEvent(st, ctx->stage_free[ov], 0));
-                if (ctx->ovl_gate_set) HIP_CHECK(hipStreamWaitEvent(st, ctx->ovl_gate, 0));
-            }
-            ctx->ovl_gate_set = false;
-        }
+        // cost-ordered waves (the single k_path only).  By frame size (2): frames of at most 3 rounds of
+        // resident waves -- with overlapped frames 1.5 -- whose end is a large part of their time (a GPU's
+        // share of a multi-GPU frame); larger frames keep path order, where concurrent neighbouring blocks
+        // share more cache than the shorter tail saves (profiles/r02_ab_wave_order.txt; r03: 1/2 share
+        // 1.004 -> 0.980 ms, 720p 0.925 -> 0.896 without it, the 1/8 share 0.329 -> 0.305 with it).
         uint32_t order_waves = 0;
         bool order_pass = false;
-        const uint32_t waves = lanes < 64u ? (paths + lanes - 1u) / lanes : (paths + 63u) / 64u;
-        const uint64_t slots = uint64_t(ctx->num_cus) * 4u * fp.megakernel_occupancy;
-        // (r03: with overlapped frames only frames of <= 1.5 rounds keep the cost order -- the next frame
-        // hides a longer frame's end, and path order's cache locality wins: 1/2 share 1.004 -> 0.980 ms,
-        // 720p 0.925 -> 0.896, C5's 1/8 share 2.418 -> 2.342; the 1/8 share keeps it, 0.329 -> 0.305)
-        const bool order_size = ctx->opt_overlap ? 2u * uint64_t(waves) <= 3u * slots : waves <= 3u * slots;
+        const uint32_t waves = (paths + 63u) / 64u;
+        const uint64_t rounds_slots = uint64_t(ctx->num_cus) * 4u * fp.megakernel_occupancy;
+        const bool order_size = ctx->opt_overlap ? 2u * uint64_t(waves) <= 3u * rounds_slots : waves <= 3u * rounds_slots;
         const bool order_on = !fp.split && (ctx->opt_wave_order == 1 || (ctx->opt_wave_order == 2 && order_size));
-        const bool order_kernel = lanes < 64u || (fp.megakernel_occupancy >= 4u && fp.megakernel_occupancy <= 7u);
-        if (order_on && order_kernel && fp.megakernel && !ctx->opt_count && !fp.mega_persistent && !ctx->opt_lds_nodes) {
+        if (order_on && fp.megakernel && !ctx->opt_count) {
             order_waves = waves;
-            const uint64_t key = (uint64_t(order_waves) << 32) ^ (uint64_t(lanes) << 24) ^ ctx->tiles_gen;
+            const uint64_t key = (uint64_t(order_waves) << 32) ^ ctx->tiles_gen;
             if (key != ctx->order_key || !ctx->order_ready || ctx->d_wave_order.bytes < size_t(order_waves) * sizeof(uint32_t))
-                drain_overlap(ctx);  // the other part's frame may still read the order / record classes
+                drain_frames(ctx);  // the other slot's frame may still read the order / record classes
             ctx->d_wave_cost.ensure(size_t(order_waves) * sizeof(uint32_t));
             ctx->d_wave_order.ensure(size_t(order_waves) * sizeof(uint32_t));
             ctx->d_wave_hist.ensure(4 * kWaveClasses * sizeof(uint32_t));
@@ -1252,22 +1082,17 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
                 HIP_CHECK(hipMemsetAsync(ctx->d_wave_hist.p, 0, 4 * kWaveClasses * sizeof(uint32_t), fs));
             }
             // every opt_order_period-th ordered frame records its wave classes and rebuilds the order
-            // (progressive frames cost alike); the frames between reuse it -- no recording atomics, no
-            // order pass
+            // (progressive frames cost alike); the frames between reuse it -- no recording atomics, no pass
             order_pass = ctx->opt_wave_clocks || ctx->order_frame % ctx->opt_order_period == 0u;
             fp.wave_cost = order_pass ? ctx->d_wave_cost.as<uint32_t>() : nullptr;
             fp.wave_hist = order_pass ? ctx->d_wave_hist.as<uint32_t>() + ctx->order_parity * 2 * kWaveClasses : nullptr;
             fp.wave_order = ctx->order_ready ? ctx->d_wave_order.as<uint32_t>() : nullptr;
-            // the costliest slots of the order split in two (path groups, once an order exists)
-            if (lanes < 64u && ctx->order_ready && ctx->opt_split_permille)
-                fp.split_units = std::min<uint32_t>(order_waves, uint32_t((uint64_t(order_waves) * ctx->opt_split_permille + 999u) / 1000u));
             if (ctx->opt_wave_clocks) {  // per-slot stamps of an ordered frame (diagnostic)
                 ctx->wclock_waves = order_waves;
                 ctx->d_wclock.ensure(size_t(order_waves) * 2 * sizeof(unsigned long long));
                 fp.wave_clock = ctx->d_wclock.as<unsigned long long>();
             }
         }
-        const int L = settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength;
         hipEvent_t* ev = nullptr;
         if (ctx->opt_timing) {
             if (ctx->ring.empty()) ctx->ring.resize(64);
@@ -1284,10 +1109,11 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             f.mask = ctx->opt_timing_mask;
             f.pending = true;
             f.mega = fp.megakernel != 0;
+            f.split = fp.megakernel && fp.split && !ctx->opt_count && !order_waves;
             ev = f.ev.data();
         }
         hipStream_t aux = nullptr;
-        if (ctx->opt_concurrency) {
+        if (!fp.megakernel) {  // the wavefront's any-hit passes run on an internal stream
             if (!ctx->aux) {
                 HIP_CHECK(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
                 ctx->fork_ev.resize(2 * kMaxDepthQueues);
@@ -1296,48 +1122,14 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             aux = ctx->aux;
         }
         uint32_t sched = 0;
-        if (overlap) {  // (after the order setup above filled fp's order fields)
-            fo = fp;
-            fo.stage = ctx->d_stage[ov].as<float4>();
-        }
-        if (halves) {
-            const uint32_t threads = frame_traversal_threads(paths, 2u + nl, 0);
-            if (!overlap) {
-                for (int k = 0; k < 2; ++k) ensure_part(ctx, k, cnt[k], 2u + nl);  // (creates the streams and events)
-                HIP_CHECK(hipEventRecord(ctx->part_fork, s));
-            }
-            if (ev) HIP_CHECK(hipEventRecord(ev[0], overlap ? fs : s));
-            ctx->stat_counters.clear();
-            for (int k = 0; k < 2; ++k) {
-                dxrpt_ctx::FramePart& P = ctx->part[pb + k];
-                const uint32_t cur = P.ctr_set;
-                uint32_t* cb = P.counters.as<uint32_t>();
-                P.fb.counters = cb + cur * kCounterWords;
-                P.fb.counters_clean = P.ctr_clean[cur];
-                P.fb.counters_next = cb + (1u - cur) * kCounterWords;
-                FrameParams fk = overlap ? fo : fp;
-                fk.num_paths = cnt[k];
-                fk.path_base = base[k];
-                if (!overlap) HIP_CHECK(hipStreamWaitEvent(P.stream, ctx->part_fork, 0));
-                HIP_CHECK(launch_split_part(scene_dev(ctx, threads, overlap ? 2u * kMaxOverlapFrames : 2u, uint32_t(pb + k)), P.fb, fk, P.stream));
-                HIP_CHECK(hipEventRecord(P.done, P.stream));
-                HIP_CHECK(hipStreamWaitEvent(s, P.done, 0));
-                P.ctr_clean[cur] = false;
-                P.ctr_clean[1u - cur] = true;
-                P.ctr_set = 1u - cur;
-                ctx->stat_counters.push_back(P.fb.counters);
-            }
-            if (ev) HIP_CHECK(hipEventRecord(ev[1], s));
-            sched = DXRPT_SCHED_MEGAKERNEL | DXRPT_SCHED_SPLIT | DXRPT_SCHED_PARTS;
-        } else if (overlap) {
-            dxrpt_ctx::FramePart& P = ctx->part[pb];
+        if (overlap) {
+            fp.stage = P.stage.as<float4>();
             const uint32_t cur = P.ctr_set;
             uint32_t* cb = P.counters.as<uint32_t>();
             P.fb.counters = cb + cur * kCounterWords;
             P.fb.counters_clean = P.ctr_clean[cur];
-            P.fb.counters_next = cb + (1u - cur) * kCounterWords;  // zeroed in-kernel for this part's next frame
-            const SceneDev so = scene_dev(ctx, frame_traversal_threads(paths, 2u + nl, 0), 2u * kMaxOverlapFrames, uint32_t(pb));
-            HIP_CHECK(launch_frame(so, P.fb, fo, fs, ev, nullptr, nullptr, &sched));
+            P.fb.counters_next = cb + (1u - cur) * kCounterWords;  // zeroed in-kernel for this slot's next frame
+            HIP_CHECK(launch_frame(scene_dev(ctx, 1u + ov), P.fb, fp, fs, ev, nullptr, nullptr, &sched));
             P.ctr_clean[cur] = false;
             P.ctr_clean[1u - cur] = true;
             P.ctr_set = 1u - cur;
@@ -1347,13 +1139,12 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         } else {
             // counter sets: this frame's is fb.counters (read by dxrpt_get_stats); a megakernel frame zeroes
             // the other one in-kernel, so the next frame skips the fill launch
-            const SceneDev sd = scene_dev(ctx, frame_traversal_threads(paths, ctx->fb.shadow_slots, fp.chunks_per_wave));
             uint32_t* cbase = ctx->f_counters.as<uint32_t>();
             const uint32_t cur = ctx->ctr_set;
             ctx->fb.counters = cbase + cur * kCounterWords;
             ctx->fb.counters_clean = ctx->ctr_clean[cur];
             ctx->fb.counters_next = fp.megakernel ? cbase + (1u - cur) * kCounterWords : nullptr;
-            HIP_CHECK(launch_frame(sd, ctx->fb, fp, s, ev, aux, aux ? ctx->fork_ev.data() : nullptr, &sched));
+            HIP_CHECK(launch_frame(scene_dev(ctx, 0), ctx->fb, fp, s, ev, aux, aux ? ctx->fork_ev.data() : nullptr, &sched));
             ctx->ctr_clean[cur] = false;
             if (fp.megakernel) {
                 ctx->ctr_clean[1u - cur] = true;
@@ -1369,10 +1160,10 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             uint32_t* h = ctx->d_wave_hist.as<uint32_t>();
             uint32_t* cur = h + ctx->order_parity * 2 * kWaveClasses;
             uint32_t* nxt = h + (1u - ctx->order_parity) * 2 * kWaveClasses;
-            // overlapped: the previous frame (the other part) may still read the order being rewritten
-            if (overlap && ctx->ovl_inflight)  // every other slot's frame
-                for (uint32_t k = 0; k < kMaxOverlapFrames; ++k)
-                    if (int(k) != ov && ctx->stage_used[k]) HIP_CHECK(hipStreamWaitEvent(fs, ctx->part[2 * k].done, 0));
+            // overlapped: the other slot's frame may still read the order being rewritten
+            if (overlap)
+                for (uint32_t k = 0; k < kOverlapSlots; ++k)
+                    if (k != ov && ctx->slot[k].stage_used) HIP_CHECK(hipStreamWaitEvent(fs, ctx->slot[k].done, 0));
             HIP_CHECK(launch_wave_order(fp.wave_cost, cur, cur + kWaveClasses, nxt, nxt + kWaveClasses,
                                         ctx->d_wave_order.as<uint32_t>(), order_waves, fs));
             ctx->order_ready = true;
@@ -1383,25 +1174,27 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             }
         }
         if (overlap) {  // the caller's stream blends the stage once the frame is done
-            if (!halves) {  // (the halves recorded theirs and the caller's stream waits for them)
-                dxrpt_ctx::FramePart& P = ctx->part[pb];
-                HIP_CHECK(hipEventRecord(P.done, fs));
-                HIP_CHECK(hipStreamWaitEvent(s, P.done, 0));
-            }
-            HIP_CHECK(launch_accum_stage(fo, s));
-            HIP_CHECK(hipEventRecord(ctx->stage_free[ov], s));
-            ctx->stage_used[ov] = true;
-            ctx->ovl_parity = (ctx->ovl_parity + 1u) % (ctx->opt_overlap + 1u);
-            ctx->ovl_inflight = true;
+            HIP_CHECK(hipEventRecord(P.done, fs));
+            HIP_CHECK(hipStreamWaitEvent(s, P.done, 0));
+            HIP_CHECK(launch_accum_stage(fp, s));
+            HIP_CHECK(hipEventRecord(P.stage_free, s));
+            P.stage_used = true;
+            ctx->ovl_parity = (ctx->ovl_parity + 1u) % kOverlapSlots;
+            ctx->ovl_active = true;
+        } else {
+            // the next overlapped frame starts behind this one: it used slab 0 and, through the stream
+            // chain, runs after every earlier overlapped frame
+            ctx->ovl_active = false;
         }
-        ctx->last_stream = s;
-        ctx->last_L = settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength;
+        ctx->inflight = true;
+        ctx->last_L = L;
         std::memset(&ctx->last, 0, sizeof(ctx->last));
         ctx->last.pixels = paths;
-        ctx->last.nominal_rays = uint64_t(paths) * uint64_t(1 + (ctx->last_L - 1) * 2);
+        ctx->last.nominal_rays = uint64_t(paths) * uint64_t(1 + (L - 1) * 2);
         ctx->last.schedule = sched;
-        ctx->last.paths_per_wave = fp.megakernel ? ((sched & DXRPT_SCHED_PATH_GROUPS) ? lanes : 64u) : 0u;
+        ctx->last.paths_per_wave = fp.megakernel ? 64u : 0u;
         ctx->last.occupancy = fp.megakernel ? fp.megakernel_occupancy : 0u;
+        ctx->last.tail_occupancy = (sched & DXRPT_SCHED_SPLIT) ? fp.tail_occupancy : 0u;
         ctx->rendered = true;
     });
 }
@@ -1410,10 +1203,10 @@ int dxrpt_get_stats(dxrpt_ctx* ctx, dxrpt_stats* out) {
     if (!ctx || !out) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
         require(ctx->rendered, "dxrpt_get_stats: nothing rendered yet", DXRPT_E_STATE);
-        HIP_CHECK(hipStreamSynchronize(ctx->last_stream));
+        drain_frames(ctx);
         uint32_t shards[2 * kMaxDepthQueues * kQueueShards];
         uint32_t cnt[2 * kMaxDepthQueues] = {};
-        for (const uint32_t* set : ctx->stat_counters) {  // one counter set per frame part
+        for (const uint32_t* set : ctx->stat_counters) {
             HIP_CHECK(hipMemcpy(shards, set, sizeof(shards), hipMemcpyDeviceToHost));
             for (uint32_t q = 0; q < 2 * kMaxDepthQueues; ++q)
                 for (uint32_t k = 0; k < kQueueShards; ++k) cnt[q] += shards[q * kQueueShards + k];
@@ -1426,13 +1219,15 @@ int dxrpt_get_stats(dxrpt_ctx* ctx, dxrpt_stats* out) {
             s.shadow_rays += cnt[16 + d];
         }
         if (ctx->opt_count && ctx->d_trav.p) {
-            unsigned long long tr[5];
+            unsigned long long tr[kTravCounters];
             HIP_CHECK(hipMemcpy(tr, ctx->d_trav.p, sizeof(tr), hipMemcpyDeviceToHost));
-            s.radiance_hits = (s.schedule & DXRPT_SCHED_CENSUS) ? tr[4] : 0u;  // the megakernel census counts hits
-            s.node_visits_radiance = tr[0];
-            s.tri_tests_radiance = tr[1];
-            s.node_visits_shadow = tr[2];
-            s.tri_tests_shadow = tr[3];
+            const bool mega = (s.schedule & DXRPT_SCHED_CENSUS) != 0;  // the megakernel census counts hits
+            s.node_visits_radiance = tr[0] + tr[5];
+            s.tri_tests_radiance = tr[1] + tr[6];
+            s.node_visits_shadow = tr[2] + tr[7];
+            s.tri_tests_shadow = tr[3] + tr[8];
+            s.radiance_hits = mega ? tr[4] + tr[9] : 0u;
+            for (int k = 0; k < 5; ++k) s.census_depth1[k] = (k < 4 || mega) ? tr[k] : 0u;
         }
         harvest_all(ctx);
         for (int k = 0; k < DXRPT_K_COUNT; ++k) {
@@ -1449,7 +1244,7 @@ int dxrpt_get_wave_clocks(dxrpt_ctx* ctx, uint64_t* out, uint32_t max_waves, uin
     if (!ctx || !num_waves) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
         require(ctx->rendered, "dxrpt_get_wave_clocks: nothing rendered yet", DXRPT_E_STATE);
-        HIP_CHECK(hipStreamSynchronize(ctx->last_stream));
+        drain_frames(ctx);
         *num_waves = ctx->wclock_waves;
         const uint32_t n = std::min(max_waves, ctx->wclock_waves);
         if (n && out) HIP_CHECK(hipMemcpy(out, ctx->d_wclock.p, size_t(n) * 2 * sizeof(uint64_t), hipMemcpyDeviceToHost));
@@ -1468,12 +1263,16 @@ int dxrpt_get_phase_clocks(dxrpt_ctx* ctx, uint64_t out[8]) {
 int dxrpt_trace_rays(dxrpt_ctx* ctx, const float* rays, uint32_t num_rays, uint32_t flags, float* hits, void* stream) {
     if (!ctx) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
-        drain_overlap(ctx);
         require(ctx->bvh_built, "dxrpt_trace_rays: acceleration structure not built", DXRPT_E_STATE);
         require(num_rays == 0 || (rays && hits), "dxrpt_trace_rays: null argument");
+        const hipStream_t s = static_cast<hipStream_t>(stream);
+        enter_stream(ctx, s);
         upload_textures(ctx);
-        HIP_CHECK(launch_trace_rays(scene_dev(ctx, trace_rays_threads(num_rays)), reinterpret_cast<const float4*>(rays), num_rays, flags,
-                                    reinterpret_cast<float4*>(hits), static_cast<hipStream_t>(stream)));
+        ensure_spill(ctx, trace_rays_threads(num_rays));
+        HIP_CHECK(launch_trace_rays(scene_dev(ctx, 0), reinterpret_cast<const float4*>(rays), num_rays, flags,
+                                    reinterpret_cast<float4*>(hits), s));
+        ctx->ovl_active = false;
+        ctx->inflight = true;
     });
 }
 
@@ -1515,7 +1314,10 @@ int dxrpt_post_process(dxrpt_ctx* ctx, const dxrpt_app_settings* settings, const
         require(settings && accum && out, "dxrpt_post_process: null argument");
         require(width >= 2 && height >= 2, "dxrpt_post_process: image must be at least 2 x 2");
         require(out_format == DXRPT_POST_FLOAT4 || out_format == DXRPT_POST_RGBA8, "dxrpt_post_process: bad output format");
+        const hipStream_t s = static_cast<hipStream_t>(stream);
+        enter_stream(ctx, s);  // after the frames whose blends write `accum`
         const size_t half = size_t(width / 2) * (height / 2) * 8u;
+        if (ctx->p_bloom0.bytes < half) drain_frames(ctx);  // an earlier post pass may still use the scratch
         ctx->p_bloom0.ensure(half);
         ctx->p_bloom1.ensure(half);
         PostParams p{};
@@ -1536,7 +1338,8 @@ int dxrpt_post_process(dxrpt_ctx* ctx, const dxrpt_app_settings* settings, const
         p.bloom_magnitude = settings->BloomMagnitude;
         p.bloom_exp2 = float(std::exp2(double(settings->BloomExposure)));
         p.exposure_scale = float(std::exp2(double(settings->Exposure)) / 0.0009765625);
-        HIP_CHECK(launch_post_process(p, static_cast<hipStream_t>(stream)));
+        HIP_CHECK(launch_post_process(p, s));
+        ctx->inflight = true;
     });
 }
 
@@ -1548,7 +1351,6 @@ int dxrpt_bake_lightmap(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, co
                         float* accum, float* lightmap, uint32_t width, uint32_t height, void* stream) {
     if (!ctx) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
-        drain_overlap(ctx);
         require(ctx->bvh_built, "dxrpt_bake_lightmap: acceleration structure not built", DXRPT_E_STATE);
         require(ctx->sky_set, "dxrpt_bake_lightmap: sky cubemap not set", DXRPT_E_STATE);
         require(rtc && settings && surface_pos && surface_normal && accum && lightmap, "dxrpt_bake_lightmap: null argument");
@@ -1560,12 +1362,14 @@ int dxrpt_bake_lightmap(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, co
                 "dxrpt_bake_lightmap: MaxPathLength must be in [1, 8]");
         const bool useLights = settings->RenderLights && rtc->NumLights > 0;
         require(!useLights || (lights && rtc->NumLights <= DXRPT_MAX_SPOT_LIGHTS), "dxrpt_bake_lightmap: bad lights");
+        const hipStream_t s = static_cast<hipStream_t>(stream);
+        enter_stream(ctx, s);
         upload_textures(ctx);
         const uint32_t nl = useLights ? rtc->NumLights : 0u;
         if (nl) {
             std::vector<dxrpt_spot_light> L(lights->Lights, lights->Lights + nl);
             if (L.size() != ctx->lights_cache.size() || std::memcmp(L.data(), ctx->lights_cache.data(), nl * sizeof(dxrpt_spot_light)) != 0) {
-                drain_overlap(ctx);
+                drain_frames(ctx);
                 ctx->d_lights.upload(L.data(), nl * sizeof(dxrpt_spot_light));
                 ctx->lights_cache = L;
             }
@@ -1573,7 +1377,10 @@ int dxrpt_bake_lightmap(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, co
         const uint32_t total = width * height;
         const uint32_t chunk = std::min<uint32_t>(total, ctx->opt_bake_chunk);
         ensure_frame(ctx, chunk, 2u + nl);
-        FrameParams fp;
+        ensure_spill(ctx, frame_traversal_threads(chunk, 2u + nl, true));
+        if (ctx->d_bake_list.bytes < size_t(total) * sizeof(uint32_t) + 64) drain_frames(ctx);
+        ctx->d_bake_list.ensure(size_t(total) * sizeof(uint32_t) + 64);
+        FrameParams fp{};
         fp.rtc = *rtc;
         fp.rtc.NumLights = nl;
         fp.set = *settings;
@@ -1583,8 +1390,7 @@ int dxrpt_bake_lightmap(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, co
         fp.megakernel_occupancy = ctx->opt_mega_occ ? ctx->opt_mega_occ : (chunk > 1500000u ? 6u : (chunk > 300000u ? 5u : 4u));
         fp.width = width;
         fp.height = height;
-        const SceneDev sd = scene_dev(ctx, frame_traversal_threads(chunk, ctx->fb.shadow_slots, 0));
-        hipStream_t s = static_cast<hipStream_t>(stream);
+        const SceneDev sd = scene_dev(ctx, 0);
         BakeArgs b;
         b.pos = reinterpret_cast<const float4*>(surface_pos);
         b.nrm = reinterpret_cast<const float4*>(surface_normal);
@@ -1592,7 +1398,6 @@ int dxrpt_bake_lightmap(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, co
         b.lightmap = reinterpret_cast<float4*>(lightmap);
         b.width = width;
         b.height = height;
-        ctx->d_bake_list.ensure(size_t(total) * sizeof(uint32_t) + 64);
         b.list = ctx->d_bake_list.as<uint32_t>();
         b.count = b.list + total;  // the entry count lives after the list
         HIP_CHECK(launch_bake_compact(b.pos, total, const_cast<uint32_t*>(b.list), const_cast<uint32_t*>(b.count), s));
@@ -1609,7 +1414,8 @@ int dxrpt_bake_lightmap(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, co
             HIP_CHECK(launch_bake(sd, ctx->fb, fp, b, s));
         }
         // dxrpt_get_stats then reports this pass: texels and the rays its paths traced
-        ctx->last_stream = s;
+        ctx->ovl_active = false;
+        ctx->inflight = true;
         ctx->last_L = settings->MaxPathLength < 2 ? 2 : settings->MaxPathLength;
         std::memset(&ctx->last, 0, sizeof(ctx->last));
         ctx->last.pixels = total;

@@ -12,6 +12,7 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -54,18 +55,37 @@ void nccl_check(ncclResult_t r, const char* what) {
     if (r != ncclSuccess) throw MultiError(DXRPT_E_HIP, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
-// Per-thread scratch of the un-permute (device tile list + prefix), reused across frames.
+// Scratch of the un-permute (device tile list + prefix) per thread and HIP device, reused across frames.
+// `done` is recorded after each launch that reads it: a new tile list waits for it before overwriting or
+// freeing the buffer (the last launch may still be queued on a non-blocking caller stream).
 struct UnpermuteScratch {
+    int device = -1;
     void* buf = nullptr;
     size_t bytes = 0;
+    hipEvent_t done = nullptr;
     std::vector<dxrpt_tile> tiles;
-    std::vector<uint32_t> prefix;
     ~UnpermuteScratch() {
+        if (device >= 0) (void)hipSetDevice(device);
+        if (done) {
+            (void)hipEventSynchronize(done);
+            (void)hipEventDestroy(done);
+        }
         if (buf) (void)hipFree(buf);
     }
 };
-thread_local UnpermuteScratch g_scratch;
+thread_local std::vector<std::unique_ptr<UnpermuteScratch>> g_scratch;
 thread_local std::string g_err;
+
+UnpermuteScratch& scratch_for_current_device() {
+    int dev = 0;
+    hip_check(hipGetDevice(&dev), "hipGetDevice");
+    for (auto& s : g_scratch)
+        if (s->device == dev) return *s;
+    g_scratch.push_back(std::make_unique<UnpermuteScratch>());
+    g_scratch.back()->device = dev;
+    hip_check(hipEventCreateWithFlags(&g_scratch.back()->done, hipEventDisableTiming), "hipEventCreate");
+    return *g_scratch.back();
+}
 
 template <class F>
 int guarded(F&& f) {
@@ -99,7 +119,7 @@ int dxrpt_unpermute(const float* src, const dxrpt_tile* tiles, uint32_t num_tile
     return guarded([&] {
         require(src && dst && (tiles || num_tiles == 0), "dxrpt_unpermute: null argument");
         if (num_tiles == 0) return;
-        UnpermuteScratch& s = g_scratch;
+        UnpermuteScratch& s = scratch_for_current_device();
         std::vector<uint32_t> prefix(num_tiles + 1, 0u);
         uint64_t total = 0;
         for (uint32_t k = 0; k < num_tiles; ++k) {
@@ -116,6 +136,7 @@ int dxrpt_unpermute(const float* src, const dxrpt_tile* tiles, uint32_t num_tile
                           std::memcmp(s.tiles.data(), tiles, num_tiles * sizeof(dxrpt_tile)) == 0;
         const size_t tb = num_tiles * sizeof(dxrpt_tile), pb = prefix.size() * sizeof(uint32_t);
         if (!same) {  // upload the tile list once per distinct list (a frame-rate caller reuses it)
+            hip_check(hipEventSynchronize(s.done), "hipEventSynchronize");  // the previous list's last reader
             if (tb + pb > s.bytes) {
                 if (s.buf) hip_check(hipFree(s.buf), "hipFree");
                 s.buf = nullptr;
@@ -132,6 +153,7 @@ int dxrpt_unpermute(const float* src, const dxrpt_tile* tiles, uint32_t num_tile
                            static_cast<hipStream_t>(stream), reinterpret_cast<const float4*>(src), dt, dp, num_tiles,
                            reinterpret_cast<float4*>(dst), width);
         hip_check(hipGetLastError(), "k_unpermute");
+        hip_check(hipEventRecord(s.done, static_cast<hipStream_t>(stream)), "hipEventRecord");
     });
 }
 
@@ -159,6 +181,14 @@ int dxrpt_comm_create(int hip_device, int nranks, int rank, const void* id, void
 int dxrpt_comm_destroy(void* comm) {
     return guarded([&] {
         if (comm) nccl_check(ncclCommDestroy(static_cast<ncclComm_t>(comm)), "ncclCommDestroy");
+    });
+}
+
+int dxrpt_comm_info(void* comm, int* nranks, int* rank) {
+    return guarded([&] {
+        require(comm && nranks && rank, "dxrpt_comm_info: null argument");
+        nccl_check(ncclCommCount(static_cast<ncclComm_t>(comm), nranks), "ncclCommCount");
+        nccl_check(ncclCommUserRank(static_cast<ncclComm_t>(comm), rank), "ncclCommUserRank");
     });
 }
 

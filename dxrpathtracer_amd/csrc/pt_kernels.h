@@ -1,4 +1,4 @@
-// pt_kernels.h — launch interface of the wavefront kernels (pt_kernels.hip), used by dxrpt_api.hip.
+// pt_kernels.h — launch interface of the path tracer's kernels (pt_kernels.hip), used by dxrpt_api.hip.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -15,19 +15,17 @@ __host__ __device__ __attribute__((always_inline)) inline uint32_t tex_tile_word
     return ((y >> 2) * tiles_x + (x >> 3)) * kTexTileWords + (y & 3u) * 8u + (x & 7u);
 }
 
-// Queue counters are sharded: a producer wave w appends to shard (w % kQueueShards) of the queue,
-// so concurrent waves spread their atomics over kQueueShards addresses instead of one.  Shard s of a
-// queue owns positions [s * cap, (s + 1) * cap); consumers enumerate item i of the queue by walking
-// the shard counts (queue_pos in pt_kernels.hip).
+// Queue counters are sharded: a producer wave appends to one shard of the queue (wave % kQueueShards in
+// the wavefront passes, its screen run in the split schedule), so concurrent waves spread their atomics
+// over kQueueShards addresses instead of one.  Shard s of a queue owns positions [s * cap, (s + 1) * cap);
+// consumers enumerate item i of the queue by walking the shard counts (queue_pos in pt_kernels.hip).
 constexpr uint32_t kQueueShards = 64;
 constexpr uint32_t kMaxDepthQueues = 16;  // radiance queues 0..15 by depth, shadow queues 16..31
-// Direction-binned split queues (FrameParams::split_bins): shard = 8 x screen region + ray octant.
-constexpr uint32_t kSplitBins = 8;
 
 // Radiance ray queue of one depth (SoA of 16-B words: one dwordx4 per lane, coalesced).  The path
 // state travels with its ray, so every per-depth kernel reads and writes it at the queue position.
 //   org[pos] float4 (origin xyz, tmax)
-//   dir[pos] float4 (direction xyz, bits(path slot p))
+//   dir[pos] float4 (direction xyz, bits(path slot p) -- split schedule: bits(accumulation index))
 //   thr[pos] float4 (path throughput rgb, payload roughness)                RayTrace.hlsl:63-71
 //   rad[pos] float4 (radiance rgb accumulated so far, bits(payload IsDiffuse))
 //   pix[pos] uint32 global pixel index y*W+x (CMJ pattern seed)
@@ -39,16 +37,16 @@ struct RayQueue {
     uint32_t* pix = nullptr;
 };
 
-// Per-frame wavefront buffers.
+// Per-frame buffers.
 //   path slot p in [0, num_paths): one path per pixel of the rendered tiles
-//     ps_pix[p]  uint2   (global pixel index, accumulation index), written by raygen
-//     px_rad[p]  float4  final path radiance: written once by k_shade when the path ends, plus the
-//                        path's last pending shadow contributions (k_resolve)
+//     ps_pix[p]  uint2   (global pixel index, accumulation index), written by raygen (wavefront)
+//     px_rad[p]  float4  final path radiance (wavefront)
 //   queue position pos in [0, qsize) of depth d (sharded layout, see above):
 //     q[d&1]     RayQueue
-//     hit[pos]   float4 (b1, b2, bits(global tri id) or ~0u on miss, bits(geometry index))
+//     hit[pos]   float4 (b1, b2, bits(global tri id) or ~0u on miss, bits(geometry index))     (wavefront)
 //     fwd[pos]   uint32 position of the path's continuation ray in queue d+1, ~0u if the path ended
-//     sh_n[pos]  uint32 number of shadow rays the vertex emitted; ray k lives in slot k * qsize + pos:
+//     sh_n[pos]  uint32 number of shadow rays the vertex emitted; ray k lives in slot k * qsize + pos
+//                (megakernel schedules: pos = the path slot / the tail's dense queue index):
 //       sh_org  float4 (origin xyz, tmax)
 //       sh_dir  float4 (direction xyz, tmin)
 //       sh_con  float4 (contribution rgb = pathThroughput * CalcLighting or sky*throughput,
@@ -65,58 +63,41 @@ struct FrameBuffers {
     float4* sh_org = nullptr;
     float4* sh_dir = nullptr;
     float4* sh_con = nullptr;
-    uint32_t* counters = nullptr;  // [queue][shard]: 2 * kMaxDepthQueues * kQueueShards (+ the k_path work counter)
-    // megakernel frames: the other counter set of the ping-pong pair (the next frame's), zeroed by k_path's
-    // workgroup 0 -- so the next frame needs no fill launch (null: nothing to zero)
+    uint32_t* counters = nullptr;  // [queue][shard]: 2 * kMaxDepthQueues * kQueueShards
+    // megakernel frames: the other counter set of the ping-pong pair (the next frame's), zeroed by the
+    // frame's first kernel's workgroup 0 -- so the next frame needs no fill launch (null: nothing to zero)
     uint32_t* counters_next = nullptr;
     bool counters_clean = false;   // counters already zero: launch_frame skips its fill
     uint32_t capacity = 0;         // paths
-    uint32_t cap_r = 0;            // radiance queue shard capacity (multiple of 64)
-    // split-schedule queue shard capacity: cap_r, or kSplitBins * cap_r with direction-binned queues
-    // (FrameParams::split_bins: a shard may then receive a whole screen region); queue buffers hold
-    // kQueueShards * cap_q entries
-    uint32_t cap_q = 0;
+    uint32_t cap_r = 0;            // queue shard capacity (multiple of 64)
     uint32_t qsize = 0;            // kQueueShards * cap_r >= capacity
     uint32_t shadow_slots = 0;     // slots per queue position; shadow shard capacity = shadow_slots * cap_r
 };
 
 // Shard capacity for producers of at most `paths` items (one wave of producers adds <= 64 items per
-// queue).  Unbinned: waves w, w + kQueueShards, ... share a shard.  XCD mapping (region_shard): shard
-// 8r + j holds the waves = j (mod 8) of region r, <= ceil(nw / 8) consecutive waves.  The larger of
-// the two (+1 wave of slack) serves both mappings.
+// queue).  Wavefront passes: waves w, w + kQueueShards, ... share a shard.  Split schedule: shard
+// w * kQueueShards / nw holds <= ceil(nw / kQueueShards) consecutive waves.  +1 wave of slack.
 inline uint32_t queue_shard_capacity(uint32_t paths) {
     const uint32_t nw = (paths + 63u) / 64u;
-    const uint32_t a = (nw + kQueueShards - 1u) / kQueueShards;
-    const uint32_t b = ((nw + 7u) / 8u + 7u) / 8u;
-    return 64u * ((a > b ? a : b) + 1u);
+    return 64u * ((nw + kQueueShards - 1u) / kQueueShards + 1u);
 }
 
 struct SceneDev {
-    const BvhNode* nodes = nullptr;     // width 2
-    const Bvh8Node* nodes8 = nullptr;   // width 8
+    const Bvh8Node* nodes8 = nullptr;
     const TriRecord* tris = nullptr;
     const float4* tri_verts = nullptr;  // per global triangle: 3 MeshVertex records = 12 float4
-    const dxrpt_mesh_vertex* vertices = nullptr;
-    const uint32_t* indices = nullptr;
-    const dxrpt_geometry_info* geoinfo = nullptr;
-    const dxrpt_material* materials = nullptr;
-    const TexDesc* texdesc = nullptr;
     const GeoShade* geoshade = nullptr;  // per geometry: its material's textures, resolved
     const uint32_t* texels = nullptr;
     const uint16_t* sky = nullptr;
     const float* lut = nullptr;  // [0..255] unorm, [256..511] sRGB->linear
     const uint32_t* omm = nullptr;  // opacity micromap, kOmmWords per alpha-tested triangle slot (pt_layout.h); null: off
     uint32_t sky_res = 0;
-    uint32_t num_textures = 0;
-    int width = 8;  // BVH width actually built: 2 or 8
-    // LDS traversal stack, ints per lane: BVH2 one node index per entry, entries = tree depth + 1
-    // (<= kTraversalStack); BVH8 two words (node-group base, hit/internal masks) per entry, entries =
-    // min(tree depth + 1, kStackLds8).  Less LDS per workgroup -> more resident waves.
-    uint32_t stack_ints = kTraversalStack;
-    // BVH8 group-stack entries kStackLds8 .. kTraversalStack8-1: [entry * spill_stride + global thread]
+    // LDS traversal stack, ints per lane: two words (node-group base, hit/internal masks) per entry,
+    // entries = min(tree depth + 1, kStackLds8).  Less LDS per workgroup -> more resident waves.
+    uint32_t stack_ints = 2u * kStackLds8;
+    // group-stack entries kStackLds8 .. kTraversalStack8-1: [entry * spill_stride + global thread]
     uint2* spill8 = nullptr;
-    uint32_t spill_stride = 0;  // >= the global thread count of every BVH8 traversal launch
-    uint32_t num_nodes = 0;     // BVH8 nodes (bounds the LDS node cache)
+    uint32_t spill_stride = 0;  // >= the global thread count of every traversal launch using this slab
 };
 
 struct FrameParams {
@@ -129,60 +110,28 @@ struct FrameParams {
     uint32_t num_tiles;
     uint32_t num_paths;
     uint32_t width, height;
-    unsigned long long* trav;        // non-null: count traversal work ([0..1] closest node/tri, [2..3] shadow)
+    unsigned long long* trav;        // non-null: count traversal work ([0..1] closest node/tri, [2..3] shadow, [4] hits)
     unsigned long long* wave_clock;  // census frames, non-null: per-wave (start, end) s_memrealtime stamps
-    uint32_t chunks_per_wave;        // BVH8 wave-pool traversal: 64-ray chunks per wave; 0 = one thread per ray
-    uint32_t refill_lanes;           // wave-pool kernels: refill once this many lanes of a wave are idle
-    uint32_t trace_block;            // workgroup size of the one-thread-per-ray traversal kernels (64..256)
-    uint32_t occupancy;              // BVH8 closest-hit kernel: 0 compiler default, 7 or 8 waves per SIMD
-    uint32_t shadow_occupancy;       // BVH8 any-hit kernel: 0 compiler default, 7 or 8 waves per SIMD
-    uint32_t shadow_grid;            // any-hit kernel grid cap in 256-thread workgroups (0 = one thread per ray)
-    uint32_t shade_block;            // workgroup size of k_shade (64..256)
     uint32_t packet;                 // wave-coherent traversal: bit 0/1 closest/any hit at depth 1, bit 2/3 at depth >= 2
     uint32_t timing_mask;            // per-kernel timing events: kinds (1 << DXRPT_K_*) bracketed
-    uint32_t lds_nodes;              // BVH8 per-lane traversal: top nodes kept in LDS per workgroup (0 = none)
-    uint32_t pipeline;               // BVH8 one-thread-per-ray traversal: bit 0 triangle pairs, bit 1 next-node prefetch
-    uint32_t shade_occupancy;        // k_shade register budget: 0 compiler default, 6, 7 or 8 waves per SIMD
-    uint32_t postpone_tris;          // wave-pool kernels: test pending triangles once this many lanes hold
-                                     // some (0 = with their node visit)
-    uint32_t xcd_map;                // 1: XCD-aware queue ranges and region shards (xcd_block / region_shard)
-    uint32_t packet_switch;          // packet traversal: fall back to one ray per lane below this coherence (%)
-    uint32_t megakernel;             // 1: the whole frame runs in k_path (one thread per path, no passes)
-    uint32_t megakernel_occupancy;   // k_path register budget: 0 compiler default, 6 waves per SIMD
-    uint32_t mega_persistent;        // >0: k_path as a persistent grid of this many waves per CU, each wave
-                                     // fetching 64-path chunks from a counter after fb.counters' shards
-    uint32_t mega_lanes;             // k_path: paths per 64-lane wave (64, 32, 16); lanes >= mega_lanes
-                                     // re-trace lane (l mod mega_lanes)'s path and write nothing
+    uint32_t megakernel;             // 1: the frame runs as megakernel(s) (k_path, or k_path_head + k_path_tail)
+    uint32_t megakernel_occupancy;   // k_path / k_path_head register budget: 4..7 waves per SIMD
     uint32_t num_cus;
-    // DXRPT_OPT_WAVE_ORDER (default megakernel schedules): wave w of the launch traces the paths of wave
-    // slot wave_order[w] (a permutation, costliest first, built from the previous frame; null:
-    // identity).  Non-null wave_cost: each wave slot's duration class (kWaveClasses log-scale classes
-    // of its s_memrealtime span, 0 = costliest) goes to wave_cost[slot] and is counted in
-    // wave_hist[class].
+    // DXRPT_OPT_WAVE_ORDER (k_path): wave w of the launch traces the paths of wave slot wave_order[w] (a
+    // permutation, costliest first, built from the previous frame; null: identity).  Non-null wave_cost:
+    // each wave slot's duration class (kWaveClasses log-scale classes of its s_memrealtime span, 0 =
+    // costliest) goes to wave_cost[slot] and is counted in wave_hist[class].
     const uint32_t* wave_order;
     uint32_t* wave_cost;
     uint32_t* wave_hist;
-    // Path-group frames with an order (DXRPT_OPT_SPLIT_UNITS): the first split_units slots of the order
-    // (the costliest) each run as TWO waves of mega_lanes / 2 paths (twice the lanes per path), launch
-    // waves 0 .. 2 split_units - 1; the other slots follow one wave each.  A split slot keeps the
-    // class it was measured with unsplit.
-    uint32_t split_units;
     // Megakernel, path-ordered frames (DXRPT_OPT_XCD_CHUNK): workgroup i runs on XCD i mod 8, so the
     // kernel maps it to pixel block (8 t + (i mod 8 + t) mod 8) C + (i / 8) mod C, t = (i / 8) / C: each
     // XCD (own L2) takes runs of C consecutive 8x8 blocks, runs dealt to the XCDs in rotation.  0: block i.
     uint32_t xcd_chunk;
-    // Depth-split megakernel (DXRPT_OPT_MEGAKERNEL_SPLIT; 64-lane path-ordered frames): 1 = k_path_head
-    // (depth 1) then one compacting k_path_tail per further depth; 0 = the single k_path.
-    // tail_occupancy: the tails' register budget (waves/SIMD).
+    // Depth-split megakernel (DXRPT_OPT_MEGAKERNEL_SPLIT): 1 = k_path_head (depth 1) then one compacting
+    // k_path_tail per further depth; 0 = the single k_path.  tail_occupancy: the tails' register budget.
     uint32_t split;
     uint32_t tail_occupancy;
-    // split_bins (DXRPT_OPT_SPLIT_BINS): the compacting pushes bin the surviving paths by screen region
-    // (8, in producer order) AND direction octant of the continuation ray -- shard 8 r + octant -- so a
-    // tail wave holds rays of one octant from one screen region; 0: shard by producer wave only.
-    uint32_t split_bins;
-    // Split-schedule frame parts (launch_split_part): this part traces the frame's path slots
-    // [path_base, path_base + num_paths) (path_base a multiple of 64); 0 otherwise.
-    uint32_t path_base;
     // Overlapped frames (DXRPT_OPT_FRAME_OVERLAP): the megakernel schedules write each path's radiance to
     // stage[accumulation index] instead of blending it into accum; launch_accum_stage blends the frame's
     // paths afterwards.  Null: blend in the kernel.
@@ -190,27 +139,21 @@ struct FrameParams {
 };
 
 constexpr uint32_t kWaveClasses = 256;
-// words of one counter set: the sharded queue counters, the k_path work counter, padding to 16 B
+// words of one counter set: the sharded queue counters, padded to 16 B
 constexpr uint32_t kCounterWords = 2 * 16 * 64 + 16;
 
-// Kernel sequence of one frame: raygen, then (trace, shade, shadow, resolve) per depth 1..L-1, then
-// accumulate.  With `aux` and 2 * kMaxDepthQueues `fork_ev` events, each depth's any-hit pass runs on
-// `aux` concurrently with the next depth's closest-hit pass.  When `ev` is non-null (per-kernel
+// Kernel sequence of one wavefront frame: raygen, then (trace, shade, shadow, resolve) per depth 1..L-1,
+// then accumulate.  With `aux` and 2 * kMaxDepthQueues `fork_ev` events, each depth's any-hit pass runs
+// on `aux` concurrently with the next depth's closest-hit pass.  When `ev` is non-null (per-kernel
 // timing), launch slot i = raygen, 1 + 4(d-1) + {trace, shade, shadow, resolve}, 1 + 4(L-1) =
 // accumulate is bracketed by events ev[2i], ev[2i+1] on the stream it runs on.  A megakernel frame
-// (fp.megakernel) records ev[0], ev[1] around its single k_path launch.
+// (fp.megakernel) records ev[0], ev[1] around its launches.
 inline int frame_event_count(int L) { return 2 * (2 + 4 * (L - 1)); }
 // Builds `order` (n wave slots, costliest first) from the classes in `cls` and their histogram `hist`
 // (kWaveClasses counts) with `cursor` (kWaveClasses zeros) as scratch, and zeroes `hist_next` and
 // `cursor_next` (the next frame's).  Order within a class is unspecified: it only schedules.
 hipError_t launch_wave_order(const uint32_t* cls, const uint32_t* hist, uint32_t* cursor, uint32_t* hist_next,
                              uint32_t* cursor_next, uint32_t* order, uint32_t n, hipStream_t stream);
-
-// One part of a depth-split frame (FrameParams::path_base / num_paths) on its own stream: zeroes the
-// part's counters unless fb.counters_clean, then k_path_head and the k_path_tail launches.  Parts of
-// one frame run concurrently on separate streams with separate FrameBuffers (queues, shadow slots,
-// counters) and SceneDev::spill8 slabs.
-hipError_t launch_split_part(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream);
 
 // *sched_out (if non-null) receives the DXRPT_SCHED_* bits of the schedule launched.
 hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const FrameParams& fp, hipStream_t stream,
@@ -242,9 +185,9 @@ hipError_t launch_bake(const SceneDev& scene, const FrameBuffers& fb, const Fram
 hipError_t launch_trace_rays(const SceneDev& scene, const float4* rays, uint32_t n, uint32_t flags, float4* hits,
                              hipStream_t stream);
 
-// Global thread count of the largest BVH8 traversal launch of a frame / of a trace_rays call (sizes
-// the stack spill slab).
-uint32_t frame_traversal_threads(uint32_t num_paths, uint32_t shadow_slots, uint32_t chunks_per_wave);
+// Global thread count of the largest traversal launch of a frame (sizes the stack spill slab): one
+// lane per path slot in the megakernel schedules, one per possible shadow ray in the wavefront's.
+uint32_t frame_traversal_threads(uint32_t num_paths, uint32_t shadow_slots, bool megakernel);
 uint32_t trace_rays_threads(uint32_t n);
 
 // Primary-only AOV of the frame's tiles into fp.accum (one float4 per path slot's accumulation index).

@@ -55,49 +55,6 @@ def band_layout(width: int, height: int, world: int, band: int = BAND_ROWS) -> B
     return BandLayout(width, height, world, band, tiles, counts, max(counts))
 
 
-def balanced_band_layout(width: int, height: int, world: int, band_costs, band: int = BAND_ROWS) -> BandLayout:
-    """Cost-balanced bands: the same `band`-row bands as band_layout, dealt by measured cost instead of
-    round robin -- costliest band first, each to the rank with the least cost so far (LPT; ties to the
-    lower rank), so every rank's share costs about the same.  With overlapped frames a share's time per
-    frame is its throughput (the sum of its waves' durations over the resident slots), so equal cost
-    sums mean equal times, where round robin leaves the rank holding the dense-geometry rows slowest
-    (profiles/r03_shares_all_ranks.txt).  `band_costs[b]`: cost of band b (rows b*band ..), e.g. the
-    summed wave durations of one census frame (band_costs_from_wave_clocks).  Each rank renders its bands
-    in image order; slabs may differ in size (counts)."""
-    nb = (height + band - 1) // band
-    if len(band_costs) != nb:
-        raise ValueError(f"band_costs has {len(band_costs)} entries, the image has {nb} bands")
-    load = [0.0] * world
-    owner = [0] * nb
-    for b in sorted(range(nb), key=lambda k: (-float(band_costs[k]), k)):
-        r = min(range(world), key=lambda q: (load[q], q))
-        owner[b] = r
-        load[r] += float(band_costs[b])
-    tiles = [[] for _ in range(world)]
-    counts = [0] * world
-    for b, y0 in enumerate(range(0, height, band)):
-        r = owner[b]
-        h = min(band, height - y0)
-        tiles[r].append(A.Tile(0, y0, width, h, counts[r], width, 0))
-        counts[r] += width * h
-    return BandLayout(width, height, world, band, tiles, counts, max(counts))
-
-
-def band_costs_from_wave_clocks(width: int, height: int, wave_clocks, band: int = BAND_ROWS):
-    """Per-band cost from the (start, end) stamps of a full-frame census frame (DXRPathTracer.wave_clocks:
-    wave w = the w-th 8x8 pixel block in raster order): the summed durations of the blocks in each band."""
-    bw = (width + 7) // 8
-    bh = (height + 7) // 8
-    per_block_row = [0.0] * bh
-    for w, (t0, t1) in enumerate(wave_clocks):
-        row = w // bw
-        if row < bh:
-            per_block_row[row] += float(int(t1) - int(t0))
-    rows_per_band = band // 8
-    nb = (height + band - 1) // band
-    return [sum(per_block_row[b * rows_per_band:(b + 1) * rows_per_band]) for b in range(nb)]
-
-
 def _mix64(x: int) -> int:
     """splitmix64 finaliser: the partition's only source of pseudo-randomness (deterministic)."""
     x = (x + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
@@ -247,15 +204,24 @@ class NativeGather:
     snapshotted on the render stream, gathered on a side stream while frame f+1 renders, and un-permuted
     on the render stream once frame f+1 is submitted (or at flush())."""
 
-    def __init__(self, layout: BandLayout, rank: int, device: int, full=None, group=None):
+    def __init__(self, layout: BandLayout, rank: int, device: int, full=None, group=None, timing: bool = False):
         import ctypes as C
         import torch
         import torch.distributed as dist
         self.layout, self.rank, self.full = layout, rank, full
         self.L = A.lib()
         uid = C.create_string_buffer(A.DXRPT_COMM_ID_BYTES)
-        # failures are made collective, so every rank raises together (a caller may then fall back to
-        # another gather) instead of the other ranks blocking in the next collective
+        # Failures BEFORE ncclCommInitRank are made collective, so every rank raises together (a caller may
+        # then fall back to another gather) instead of the others blocking inside the collective init: the
+        # ranks first agree that each one's device and arguments are valid, then rank 0 makes the id.  A
+        # rank that fails inside ncclCommInitRank itself still leaves the others blocked there (RCCL's
+        # blocking init), which no check before it can cover.
+        ready = torch.cuda.is_available() and 0 <= device < torch.cuda.device_count() and 0 <= rank < layout.world
+        flags = [None] * layout.world
+        dist.all_gather_object(flags, bool(ready), group=group)
+        if not all(flags):
+            raise RuntimeError(f"native gather: ranks {[r for r, v in enumerate(flags) if not v]} cannot use their "
+                               "device; not creating the RCCL communicator")
         obj = [None]
         if rank == 0:
             rc = self.L.dxrpt_comm_unique_id(uid)
@@ -275,6 +241,9 @@ class NativeGather:
             self.comm = C.c_void_p()
             raise RuntimeError(f"dxrpt_comm_create failed on ranks {[r for r, v in enumerate(oks) if not v]}: "
                                f"{self._msg(rc) if rc != A.DXRPT_OK else 'see those ranks'}")
+        nr, rk = C.c_int(), C.c_int()
+        self._check(self.L.dxrpt_comm_info(self.comm, C.byref(nr), C.byref(rk)), "dxrpt_comm_info")
+        self.comm_ranks, self.comm_rank = nr.value, rk.value  # what RCCL runs the gather over
         self.counts = (C.c_uint64 * layout.world)(*layout.counts)
         self.tiles = gathered_tiles(layout)
         self.tarr = (A.Tile * len(self.tiles))(*self.tiles)
@@ -284,6 +253,10 @@ class NativeGather:
         self.recv = None
         self.pending = None
         self.count = 0
+        # timing=True: events around each frame's dxrpt_gather_slabs (side stream) and dxrpt_unpermute
+        # (render stream), read by times() once the frames are done
+        self.timing = timing
+        self.gather_ev, self.unpermute_ev = [], []
 
     def _msg(self, rc):
         msg = self.L.dxrpt_multi_last_error()
@@ -306,11 +279,17 @@ class NativeGather:
         self.count += 1
         self.staging[k].copy_(local[:n])
         self.side.wait_stream(cur)
+        if self.timing:
+            g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            g0.record(self.side)
         self._check(self.L.dxrpt_gather_slabs(self.comm, C.c_void_p(self.staging[k].data_ptr()), self.counts,
                                               C.c_void_p(self.recv[k].data_ptr()) if self.rank == 0 else None,
                                               C.c_void_p(self.side.cuda_stream)), "dxrpt_gather_slabs")
         ev = torch.cuda.Event()
         ev.record(self.side)
+        if self.timing:
+            g1.record(self.side)
+            self.gather_ev.append((g0, g1))
         prev, self.pending = self.pending, (ev, k)
         if prev is not None:
             self._finish(prev)
@@ -327,9 +306,26 @@ class NativeGather:
         cur = torch.cuda.current_stream()
         cur.wait_event(ev)
         if self.rank == 0:
+            if self.timing:
+                u0, u1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                u0.record(cur)
             self._check(self.L.dxrpt_unpermute(C.c_void_p(self.recv[k].data_ptr()), self.tarr, len(self.tiles),
                                                C.c_void_p(self.full.data_ptr()), self.layout.width, self.layout.height,
                                                C.c_void_p(cur.cuda_stream)), "dxrpt_unpermute")
+            if self.timing:
+                u1.record(cur)
+                self.unpermute_ev.append((u0, u1))
+
+    def reset_times(self):
+        self.gather_ev, self.unpermute_ev = [], []
+
+    def times(self):
+        """(mean ms of dxrpt_gather_slabs on the side stream, mean ms of dxrpt_unpermute on rank 0's render
+        stream, frames) over the frames submitted since reset_times(); call after the frames are done."""
+        import statistics
+        g = [a.elapsed_time(b) for a, b in self.gather_ev]
+        u = [a.elapsed_time(b) for a, b in self.unpermute_ev]
+        return (statistics.mean(g) if g else None, statistics.mean(u) if u else None, len(g))
 
     def close(self):
         if self.comm:

@@ -32,6 +32,13 @@
  *     `rtTarget` RGBA32F UAV, DXRPathTracer.cpp:919-927).
  *   - dxrpt_render only enqueues work on `stream` (a hipStream_t, or NULL for
  *     the default stream); the caller synchronises.
+ *   - Stream ordering: every call that reads or writes context-owned buffers or the accumulation
+ *     target (dxrpt_render, dxrpt_render_aov, dxrpt_trace_rays, dxrpt_bake_lightmap,
+ *     dxrpt_post_process) runs after all such work the context enqueued before it, on whatever stream
+ *     the caller passes: a call on a different stream than the previous call first makes its stream
+ *     wait for the previous stream's work (one command queue, as the reference's, Graphics/DX12.cpp:
+ *     263-305).  Overlapped frames (DXRPT_OPT_FRAME_OVERLAP) keep this: a frame's result is in `accum`
+ *     once the stream of its call reaches the point where dxrpt_render returned.
  *   - One host thread per context.
  */
 #ifndef DXRPT_H_
@@ -44,7 +51,7 @@
 extern "C" {
 #endif
 
-#define DXRPT_ABI_VERSION 2
+#define DXRPT_ABI_VERSION 3
 
 /* ---- status codes ---------------------------------------------------------------------------- */
 #define DXRPT_OK 0
@@ -191,8 +198,10 @@ typedef struct dxrpt_tile {
 #define DXRPT_K_SHADOW 3      /* any-hit traversal of shadow rays (all depths) */
 #define DXRPT_K_ACCUMULATE 4
 #define DXRPT_K_RESOLVE 5     /* adds visibility-weighted shadow contributions to path radiance */
-#define DXRPT_K_PATH 6        /* megakernel frames (DXRPT_OPT_MEGAKERNEL_PATHS): the whole frame in one launch */
-#define DXRPT_K_COUNT 7
+#define DXRPT_K_PATH 6        /* megakernel frames (DXRPT_OPT_MEGAKERNEL_PATHS): all of the frame's launches */
+#define DXRPT_K_PATH_HEAD 7   /* depth-split frames: k_path_head (raygen + depth 1) */
+#define DXRPT_K_PATH_TAIL 8   /* depth-split frames: the k_path_tail launches (depths >= 2), back to back */
+#define DXRPT_K_COUNT 9
 
 /* Counters of the last dxrpt_render call (read back with a stream sync in dxrpt_get_stats), plus
  * per-kernel HIP-event timings accumulated since dxrpt_reset_timing (DXRPT_OPT_KERNEL_TIMING). */
@@ -213,23 +222,26 @@ typedef struct dxrpt_stats {
     uint64_t timed_frames;
     double frame_ms;                   /* summed raygen-start -> accumulate-end time of the timed frames */
     /* The schedule the last dxrpt_render ran (DXRPT_SCHED_* bits), the paths each 64-lane wave of its
-       megakernel carried (64, or 32 / 16 with path groups; 0 for the wavefront passes) and its register
-       budget in waves per SIMD. */
+       megakernel carried (64; 0 for the wavefront passes), its register budget in waves per SIMD (the
+       head's on a depth-split frame) and the tails' (depth-split frames, else 0). */
     uint32_t schedule;
     uint32_t paths_per_wave;
     uint32_t occupancy;
-    uint32_t pad;
+    uint32_t tail_occupancy;
     /* DXRPT_OPT_COUNT_TRAVERSAL on a megakernel frame: radiance rays that hit a triangle (the vertices
        PathTrace shades); the other radiance rays ran MissShader.  0 otherwise. */
     uint64_t radiance_hits;
+    /* DXRPT_OPT_COUNT_TRAVERSAL: the part of the census above that belongs to depth-1 vertices (the split
+       schedule's head kernel; the rest is its tails'): node and triangle fetches of closest-hit and of
+       any-hit rays, and (megakernel census) radiance hits. */
+    uint64_t census_depth1[5];
 } dxrpt_stats;
 #define DXRPT_SCHED_MEGAKERNEL 1u    /* k_path (or the split head/tail kernels): no wavefront passes */
-#define DXRPT_SCHED_PATH_GROUPS 2u   /* several lanes per path (paths_per_wave < 64) */
+/* 2u (path groups) and 64u (two concurrent halves) are retired (ABI 3) */
 #define DXRPT_SCHED_ORDER_KERNEL 4u  /* the cost-ordered instantiation ran (it records wave costs) */
 #define DXRPT_SCHED_COST_ORDERED 8u  /* ... and started the waves in a cost order built by earlier frames */
 #define DXRPT_SCHED_CENSUS 16u       /* the counting (DXRPT_OPT_COUNT_TRAVERSAL) instantiation */
 #define DXRPT_SCHED_SPLIT 32u        /* depth-split megakernel: k_path_head then compacted k_path_tail */
-#define DXRPT_SCHED_PARTS 64u        /* ... as two concurrent halves of the frame's paths */
 #define DXRPT_SCHED_OVERLAP 128u     /* overlapped with its neighbour frames (DXRPT_OPT_FRAME_OVERLAP) */
 
 /* BVH summary (dxrpt_get_bvh_info). */
@@ -240,7 +252,7 @@ typedef struct dxrpt_bvh_info {
     uint32_t max_depth;
     uint32_t node_bytes;      /* bytes per node of the layout traversed on the GPU */
     uint32_t tri_bytes;       /* bytes per leaf triangle record */
-    uint32_t width;           /* 2 (BVH2, 64-B nodes) or 8 (compressed BVH8, 80-B nodes) */
+    uint32_t width;           /* 8: compressed BVH8, 80-B nodes */
     uint32_t pad;
     double build_ms;          /* host build time */
     double sah_cost;
@@ -278,77 +290,36 @@ int dxrpt_set_sky(dxrpt_ctx* ctx, const uint16_t* rgba16f_cube, uint32_t res);
 int dxrpt_build_bvh(dxrpt_ctx* ctx);
 int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 
-/* ---- options ---------------------------------------------------------------------------------- */
+/* ---- options ----------------------------------------------------------------------------------
+ * Retired in ABI 3 (measured slower or neutral on MI355X; DESIGN.md §7a holds the table and the A/B
+ * records): 3 BVH_WIDTH, 4-7 wave-pool traversal, 8-11 and 14-15 wavefront launch shapes and budgets,
+ * 16 CONCURRENCY, 17 TRAVERSAL_PIPELINE, 19 LDS_NODES, 21 XCD_MAPPING, 22 PACKET_SWITCH,
+ * 26 MEGAKERNEL_PERSISTENT, 27 MEGAKERNEL_LANES (path groups), 30 SPLIT_UNITS, 35 SPLIT_PARTS,
+ * 38 SPLIT_BINS, 39 SPLIT_ALPHA.  dxrpt_set_option rejects them with DXRPT_E_UNSUPPORTED. */
 #define DXRPT_OPT_COUNT_TRAVERSAL 1u  /* 1: instrumented kernels of the same schedule count node / triangle
                                          fetches (slower; images identical) */
-#define DXRPT_OPT_KERNEL_TIMING 2u    /* 1: record a hipEvent after every launch of dxrpt_render */
-#define DXRPT_OPT_BVH_WIDTH 3u        /* 2 or 8 (default): layout built by the next dxrpt_build_bvh */
-#define DXRPT_OPT_TRAVERSAL_MODE 4u   /* BVH8: 0 = one thread per ray (default), 1 = wave pools with lane refill */
-#define DXRPT_OPT_REFILL_LANES 5u     /* wave-pool mode: refill a wave once this many lanes are idle */
-#define DXRPT_OPT_CHUNKS_PER_WAVE 6u  /* wave-pool mode: 64-ray chunks owned by each wave (1..64, default 4) */
-#define DXRPT_OPT_POSTPONE_TRIS 7u    /* wave-pool mode: batch triangle tests until this many lanes have some
-                                         (0 = test with the node visit, default) */
-#define DXRPT_OPT_TRACE_BLOCK 8u      /* workgroup size of the one-thread-per-ray traversal kernels of the
-                                        wavefront schedule: 64 (default), 128, 256 (the megakernel always
-                                        runs one wave per workgroup) */
-#define DXRPT_OPT_OCCUPANCY 9u        /* BVH8 closest-hit register budget: 0 = compiler default, 7 (default) or 8 waves/SIMD */
-#define DXRPT_OPT_SHADE_BLOCK 10u     /* workgroup size of the shading kernel: 64, 128, 256 (default) */
-#define DXRPT_OPT_SHADE_OCCUPANCY 11u /* shading kernel register budget: 0 = compiler default, 6, 7 or 8 waves/SIMD */
+#define DXRPT_OPT_KERNEL_TIMING 2u    /* 1: record hipEvents around the launches of dxrpt_render */
 #define DXRPT_OPT_SPATIAL_SPLITS 12u  /* BVH8 build: spatial-split reference budget in percent of the triangle count
                                          (101..400; <= 100 disables spatial splits; default 150) */
 #define DXRPT_OPT_LEAF_COST 13u       /* BVH8 build: triangle-test cost in percent of a node visit (default 150) */
-#define DXRPT_OPT_SHADOW_OCCUPANCY 14u /* BVH8 any-hit register budget: 0 = compiler default, 7 or 8 (default) waves/SIMD */
-#define DXRPT_OPT_SHADOW_GRID 15u     /* any-hit kernel: grid-stride cap in 256-thread workgroups;
-                                         0 = one thread per queued shadow ray (default) */
-#define DXRPT_OPT_CONCURRENCY 16u     /* 1 (default): each depth's any-hit pass runs on an internal stream
-                                         concurrently with the next closest-hit pass (joined before the
-                                         next shading pass); 0: one stream.  Per-kernel timing events
-                                         (DXRPT_OPT_KERNEL_TIMING) are recorded on the stream each kernel
-                                         runs on, so concurrent passes are timed as they overlap. */
-#define DXRPT_OPT_TRAVERSAL_PIPELINE 17u /* BVH8 one-thread-per-ray traversal: bit 0 = load leaf triangles two at a
-                                            time, bit 1 = load the next node before the current node's triangle
-                                            tests (default 0).  Results are identical for every value. */
 #define DXRPT_OPT_PACKET_TRAVERSAL 18u /* BVH8 wave-coherent traversal (the 64 rays of a wave share one node
                                           sequence fetched with scalar loads) per pass, bit mask: 1 = closest
                                           hit at depth 1 (primary rays), 2 = any hit at depth 1 (megakernel:
                                           the sun shadow rays of the primary hits), 4 = closest hit at depth
                                           >= 2, 8 = any hit at depth >= 2 (wavefront only); default 3.
                                           Identical results. */
-#define DXRPT_OPT_LDS_NODES 19u       /* BVH8 per-lane traversal: each workgroup copies the top this-many nodes
-                                         (breadth-first prefix of the tree, 80 B each) into LDS and visits them
-                                         there (0..1024, default 0; when set, it replaces
-                                         DXRPT_OPT_TRAVERSAL_PIPELINE).  Identical results. */
 #define DXRPT_OPT_KERNEL_TIMING_MASK 20u /* kernel kinds bracketed by events when DXRPT_OPT_KERNEL_TIMING is on
                                             (bit 1 << DXRPT_K_*, default all); the frame span is always timed.
                                             Fewer events, less timing overhead in the measured frames. */
-#define DXRPT_OPT_XCD_MAPPING 21u   /* 1: each pass's queue is cut into 8 ranges run by the 8 XCDs (workgroup
-                                         b -> XCD b % 8) and rays are queued by screen region, so each XCD's L2
-                                         serves one region of the image; 0 (default): dispatch order (all XCDs
-                                         sweep the image together, which measured faster: no load imbalance
-                                         between regions).  Identical results. */
-#define DXRPT_OPT_PACKET_SWITCH 22u /* packet traversal: a wave whose share of live lanes entering the visited
-                                         nodes falls below this percentage continues one ray per lane
-                                         (0 = never).  Identical results. */
 #define DXRPT_OPT_MEGAKERNEL_PATHS 23u /* frames of at most this many path vertices (paths x (MaxPathLength-1);
-                                            default 0xFFFFFFFF: every frame) run as ONE kernel, one thread
-                                            per path: raygen, every depth's traversals and shading,
-                                            accumulation -- no passes, no queues; larger frames run the
-                                            wavefront passes (compacted queues between depths).  0 = always
+                                            default 0xFFFFFFFF: every frame) run as megakernels, one lane per
+                                            path (the single k_path, or the depth-split k_path_head +
+                                            k_path_tail); larger frames run the wavefront passes (one kernel
+                                            per stage and depth, compacted queues between depths).  0 = always
                                             the wavefront.  Identical results. */
 #define DXRPT_OPT_MEGAKERNEL_OCCUPANCY 24u /* megakernel register budget in waves/SIMD: 0 = by frame size
-                                              (default: 5 with path groups, else 7 above 600,000 paths,
-                                              else 4),
-                                              4 (no spills), 5, 6, 7, 8, or 3 = the compiler's */
-#define DXRPT_OPT_MEGAKERNEL_PERSISTENT 26u /* > 0: the megakernel as a persistent grid of this many
-                                               waves per CU pulling 64-path chunks (0 = one wave per
-                                               64 paths, default); occupancy 8 runs at the 7-wave budget.
-                                               Identical results. */
-#define DXRPT_OPT_MEGAKERNEL_LANES 27u /* paths per 64-lane megakernel wave: 0 = by frame size (default:
-                                          32 up to 400,000 paths -- a GPU's share of an 8-GPU 1080p frame --
-                                          else 64), 64, 32 or 16; each path is then carried by 64/value
-                                          lanes that shade it together and trace its continuation and
-                                          shadow rays concurrently (shorter dependent-traversal chains on
-                                          small frames).  Identical results. */
+                                              (default: 7 above 600,000 paths, 6 from 300,000 with overlapped
+                                              frames, else 4; the split head 5), or 4..7 */
 #define DXRPT_OPT_BAKE_CHUNK 25u /* texels per dxrpt_bake_lightmap launch (default 2^21; bounds the
                                     per-texel shadow-slot buffers).  Identical results. */
 #define DXRPT_OPT_WAVE_CLOCKS 28u /* 1: with DXRPT_OPT_COUNT_TRAVERSAL, the megakernel census frame also
@@ -362,13 +333,8 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                      so the frame does not end on long waves started last.  The order
                                      resets when the frame's tiles or path count change.  0: waves in
                                      path order.  2 (default): 1 for frames of at most 3 rounds of
-                                     resident waves (a GPU's share of a multi-GPU frame), else 0.
-                                     Images identical in every mode. */
-#define DXRPT_OPT_SPLIT_UNITS 30u    /* path-group frames with a wave order: the costliest this-many
-                                        per mille of the frame's waves (at least one when > 0) each run
-                                        as two waves of half the paths, twice the lanes per path -- the
-                                        slowest waves set a small frame's time.  Default 0.  Identical
-                                        results. */
+                                     resident waves (1.5 with overlapped frames; a GPU's share of a
+                                     multi-GPU frame), else 0.  Images identical in every mode. */
 #define DXRPT_OPT_XCD_CHUNK 31u      /* path-ordered megakernel frames: each XCD (its own L2) takes runs of
                                         this many consecutive 8x8 pixel blocks, runs dealt to the 8 XCDs
                                         in rotation (default 8; 0: block i on workgroup i, i.e.
@@ -377,43 +343,31 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                            durations and rebuilds the order, the frames between reuse it
                                            (default 16, one SqrtNumSamples^2 = 16 cycle of progressive
                                            frames; 1 = every frame).  Identical results. */
-#define DXRPT_OPT_MEGAKERNEL_SPLIT 33u /* 1: 64-lane path-ordered megakernel frames run as one kernel per path
-                                          depth -- a head kernel runs raygen and depth 1 of every camera
-                                          path, then per further depth one kernel runs the surviving paths,
-                                          compacted into full waves (wave64 ballot, one atomic per wave),
-                                          with the path state in the queue instead of registers and its own
-                                          register budget.  0: the single k_path.  2 (default): by frame
-                                          size -- frames of >= 2M path vertices (paths x (L-1)) with
-                                          overlapped frames, >= 8M without.
-                                          Identical results. */
-#define DXRPT_OPT_SPLIT_PARTS 35u      /* split frames as this many concurrent parts (halves of the path slots,
-                                          each with its own queues on an internal stream): 0 = by frame size
-                                          (default: 1 with overlapped frames; without, 2 up to 4M paths,
-                                          else 1), 1 or 2.  Identical results. */
+#define DXRPT_OPT_MEGAKERNEL_SPLIT 33u /* 1: megakernel frames run as one kernel per path depth -- a head
+                                          kernel runs raygen and depth 1 of every camera path, then per
+                                          further depth one kernel runs the surviving paths, compacted into
+                                          full waves (wave64 ballot, one atomic per wave), with the path
+                                          state in the queue instead of registers and its own register
+                                          budget.  0: the single k_path.  2 (default): by frame size --
+                                          frames of >= 2M path vertices (paths x (L-1)) with overlapped
+                                          frames, >= 8M without.  Identical results. */
 #define DXRPT_OPT_TAIL_OCCUPANCY 34u   /* register budget of the split schedule's tail kernels in waves/SIMD:
-                                          0 = by default 7 (the head's 6, or DXRPT_OPT_MEGAKERNEL_OCCUPANCY
-                                          when set), 4..8 */
-#define DXRPT_OPT_SPLIT_ALPHA 39u    /* BVH8 build: 0 (default) spatial splits leave alpha-tested triangles
-                                          whole (each reference of one costs an opacity test); 1: they
-                                          may cut them like any other triangle.
-                                          Takes effect at the next dxrpt_build_bvh.  Identical results. */
-#define DXRPT_OPT_SPLIT_BINS 38u     /* split frames: the compacting pushes bin surviving paths by screen region x
-                                          direction octant of the continuation ray (1) instead of by
-                                          producer wave only (0, default).  Identical results. */
-#define DXRPT_OPT_FRAME_OVERLAP 37u    /* 1 (default): consecutive megakernel frames alternate between two
-                                          internal streams with their own path buffers (2: rotate over
-                                          three, three frames in flight) and stage their radiance; the caller's stream blends a frame's stage
-                                          (RaygenShader's progressive rule, RayTrace.hlsl:140-148) once it is
-                                          done, so the next frame's waves fill the previous frame's drain.
-                                          dxrpt_render still returns with every launch enqueued, and the
-                                          target is complete when the caller's stream reaches that point.
-                                          0: one frame at a time on the caller's stream.  Identical results. */
-#define DXRPT_OPT_OPACITY_MICROMAP 36u /* 1 (default): candidates on alpha-tested geometry first read a 16-B
-                                          opacity micromap word of their triangle (built on the host from
-                                          the opacity map: per barycentric cell, "every tap here accepts",
+                                          0 = 7 (or DXRPT_OPT_MEGAKERNEL_OCCUPANCY when set), 4..7 */
+#define DXRPT_OPT_OPACITY_MICROMAP 36u /* 1 (default): candidates on alpha-tested geometry first read a
+                                          micromap word of their triangle (built on the host from the
+                                          opacity map: per barycentric cell, "every tap here accepts",
                                           "every tap here rejects" or "tap"), and skip the opacity tap of
                                           AnyHitShader (RayTrace.hlsl:485-507) where the cell decides it.
                                           0: always tap.  Identical results. */
+#define DXRPT_OPT_FRAME_OVERLAP 37u    /* 1 (default): consecutive megakernel frames alternate between two
+                                          internal streams with their own path buffers and stage their
+                                          radiance; the caller's stream blends a frame's stage
+                                          (RaygenShader's progressive rule, RayTrace.hlsl:140-148) once it is
+                                          done, so the next frame's waves fill the previous frame's drain.
+                                          dxrpt_render still returns with every launch enqueued, and the
+                                          target is complete when the caller's stream reaches that point
+                                          (see "Stream ordering" above).  0: one frame at a time on the
+                                          caller's stream.  Identical results. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);
@@ -505,6 +459,9 @@ int dxrpt_comm_unique_id(void* id);
  * calls it with the same id).  *comm is an ncclComm_t, released with dxrpt_comm_destroy. */
 int dxrpt_comm_create(int hip_device, int nranks, int rank, const void* id, void** comm);
 int dxrpt_comm_destroy(void* comm);
+/* The number of ranks of the RCCL communicator (ncclCommCount) and this process's rank in it
+ * (ncclCommUserRank): what the gather runs over, for the multi-GPU bench line. */
+int dxrpt_comm_info(void* comm, int* nranks, int* rank);
 /* Collective frame-end gather: rank r sends counts[r] float4 pixels of its device `slab`; rank 0 receives
  * all ranks' slabs back to back into its device `gathered` (rank r at sum(counts[0..r-1]) float4s; its
  * own slab is copied on `stream`).  Every rank passes the same counts[nranks]; stream-ordered. */

@@ -965,6 +965,23 @@ void oracle_cmj2d(uint32_t sample_idx, uint32_t nx, uint32_t ny, uint32_t patter
 
 void oracle_sincos(float x, float out[2]) { sincos_det(x, &out[0], &out[1]); }
 
+// Batched evaluations of the sampling / BRDF helpers for the reference-compiled golden vectors
+// (tests/golden/make_sampling_golden.py): n inputs each.
+void oracle_concentric_disk(const float* xy, uint32_t n, float* out) {
+    for (uint32_t i = 0; i < n; ++i) SquareToConcentricDiskMapping(xy[2 * i], xy[2 * i + 1], out + 2 * i);
+}
+void oracle_cosine_hemisphere(const float* uv, uint32_t n, float* out) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const F3 d = SampleDirectionCosineHemisphere(uv[2 * i], uv[2 * i + 1]);
+        out[3 * i] = d.x;
+        out[3 * i + 1] = d.y;
+        out[3 * i + 2] = d.z;
+    }
+}
+void oracle_ggx_v1(const float* m2_ndotx, uint32_t n, float* out) {
+    for (uint32_t i = 0; i < n; ++i) out[i] = GGXV1(m2_ndotx[2 * i], m2_ndotx[2 * i + 1]);
+}
+
 oracle_scene* oracle_scene_create(const oracle_vertex* vertices, uint32_t num_vertices, const void* indices, uint32_t idx_bytes,
                                   uint32_t num_indices, const oracle_geometry_info* geometries, uint32_t num_geometries,
                                   const oracle_material* materials, uint32_t num_materials, const oracle_texture* textures,

@@ -44,6 +44,11 @@ typedef struct oracle_scene oracle_scene;
 
 void oracle_cmj2d(uint32_t sample_idx, uint32_t nx, uint32_t ny, uint32_t pattern, float out[2]);
 void oracle_sincos(float x, float out[2]);
+/* Sampling.hlsl:72-114 SquareToConcentricDiskMapping (out 2 per input), 181-196 SampleDirectionCosineHemisphere
+ * (out 3 per input) on n (x, y) pairs; BRDF.hlsl:89-92 GGX_V1 on n (m2, nDotX) pairs (out 1 per input). */
+void oracle_concentric_disk(const float* xy, uint32_t n, float* out);
+void oracle_cosine_hemisphere(const float* uv, uint32_t n, float* out);
+void oracle_ggx_v1(const float* m2_ndotx, uint32_t n, float* out);
 /* Arrays must outlive the scene (not copied), except indices which are widened into the scene. */
 oracle_scene* oracle_scene_create(const oracle_vertex* vertices, uint32_t num_vertices, const void* indices, uint32_t idx_bytes,
                                   uint32_t num_indices, const oracle_geometry_info* geometries, uint32_t num_geometries,

@@ -55,6 +55,9 @@ def lib() -> C.CDLL:
         L.oracle_bake.argtypes = [P, P, P, P, P, P] + [C.c_uint32] * 4 + [P, P, C.c_uint32, C.POINTER(OracleStats)]
         L.oracle_median3x3.argtypes = [P, P, C.c_uint32, C.c_uint32]
         L.oracle_median3x3.restype = None
+        for fn in ("oracle_concentric_disk", "oracle_cosine_hemisphere", "oracle_ggx_v1"):
+            getattr(L, fn).argtypes = [P, C.c_uint32, P]
+            getattr(L, fn).restype = None
         _lib = L
     return _lib
 
@@ -69,6 +72,29 @@ def sincos(x: float) -> tuple[float, float]:
     out = (C.c_float * 2)()
     lib().oracle_sincos(x, out)
     return out[0], out[1]
+
+
+def _batched(fn: str, pairs, width: int):
+    import numpy as np
+    a = np.ascontiguousarray(pairs, dtype=np.float32).reshape(-1, 2)
+    out = np.zeros((a.shape[0], width), dtype=np.float32)
+    getattr(lib(), fn)(a.ctypes.data, a.shape[0], out.ctypes.data)
+    return out
+
+
+def concentric_disk(xy):
+    """SquareToConcentricDiskMapping (Sampling.hlsl:72-114) on an (n, 2) array -> (n, 2) float32."""
+    return _batched("oracle_concentric_disk", xy, 2)
+
+
+def cosine_hemisphere(uv):
+    """SampleDirectionCosineHemisphere (Sampling.hlsl:181-196) on an (n, 2) array -> (n, 3) float32."""
+    return _batched("oracle_cosine_hemisphere", uv, 3)
+
+
+def ggx_v1(m2_ndotx):
+    """GGX_V1 (BRDF.hlsl:89-92) on an (n, 2) array of (m2, nDotX) -> (n,) float32."""
+    return _batched("oracle_ggx_v1", m2_ndotx, 1)[:, 0]
 
 
 class OracleScene:

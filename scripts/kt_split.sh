@@ -6,7 +6,7 @@ OUT=gpurun_out/kt_split
 mkdir -p $OUT
 for c in ${CONFIGS:-metric c3}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/$c -o run -- python3 scripts/time_frames.py --config $c \
-      --rounds 1 --frames 8 --msplit ${MSPLIT:-1} --occ ${OCC:-6} --tail-occ ${TOCC:-7} > $OUT/$c.txt 2>&1 || exit $?
+      --rounds 1 --frames 8 --opt MEGAKERNEL_SPLIT=${MSPLIT:-1} --opt FRAME_OVERLAP=${OVERLAP:-0} > $OUT/$c.txt 2>&1 || exit $?
   python3 - "$OUT/$c" "$c" <<'PY'
 import csv, glob, sys, collections
 f = glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True)[0]

@@ -1,155 +1,127 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 outputs of scripts/profile.sh into profiles/<round>_*.
+"""Summarise the rocprofv3 outputs of scripts/profile.sh (kernel trace + stats of bench.py, then one
+rocprofv3 --pmc pass per counter group over the same command) into profiles/<round>_*.
 
-Per kernel: launches, average duration (kernel trace), and per-launch PMC averages.  HBM traffic per
-launch follows MI355X_MICROARCH.md section HBM: FETCH_SIZE and WRITE_SIZE come from separate passes,
-are in KiB, and on gfx950 FETCH_SIZE reports half the bytes of 16-B/lane reads, so the read side is
-doubled (our traversal loads are 16-B/lane dwordx4; the guide marks other shapes uncalibrated, so the
-raw value is kept next to the corrected one).
-usage: scripts/pmc_summary.py gpurun_out/prof r01
+bench.py runs, in one process: a census frame (the counting k_path<7, true> on the caller's stream), a
+frame-at-a-time pass (DXRPT_OPT_FRAME_OVERLAP 0: every kernel on the caller's stream, one launch at a
+time -- the per-launch durations of the bench line's roofline), then the timed overlapped frames (the
+kernels on two internal slot streams).  Per kernel kind (k_path_head / k_path_tail / k_path) this writes:
+  - avg_ms: the kernel trace's average duration of the launches on the caller's stream (the queue of
+    the census kernel), i.e. the frame-at-a-time launches, which bench.py's roofline times with HIP events;
+    avg_ms_all: over every launch (overlapped launches share the GPU with the neighbour frame);
+  - per-launch counters of those launches.  l2_fabric_bytes_per_launch = FETCH_SIZE + WRITE_SIZE (KiB x 1024,
+    RAW: no x2 read correction -- MI355X_MICROARCH.md calibrates that on 16-B/lane streaming reads only, and
+    these are scattered gathers): L2 -> fabric traffic, Infinity-Cache hits included, so not HBM bytes.
+usage: PMC_CONFIG_TAG=<config> PMC_CONFIG="<scene>-proxy WxH L=n" scripts/pmc_summary.py gpurun_out/prof_<config> <round>
 """
 import csv
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
 CONFIG = os.environ.get("PMC_CONFIG", "sponza-proxy 1920x1080 L=3")
+TAG = os.environ.get("PMC_CONFIG_TAG", "metric")
 
 
 def short(name):
-    """'void dxrpt::k_trace<false, 8, 8>(dxrpt::KArgs, int)' -> 'k_trace<false, 8, 8>'"""
-    import re
+    """'void dxrpt::k_path_tail<7>(dxrpt::KArgs, int)' -> 'k_path_tail<7>'"""
     m = re.search(r"dxrpt::(k_\w+)(<[^>]*>)?", name)
     return (m.group(1) + (m.group(2) or "")) if m else None
 
 
-def counters(path):
-    acc = defaultdict(lambda: defaultdict(list))
-    with open(path) as f:
-        for row in csv.DictReader(f):
-            k = short(row["Kernel_Name"])
-            if k:
-                acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
-    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
+def kind(k):
+    """Kernel kind of a short name; None for the census instantiation k_path<occ, true, ...>."""
+    if k is None:
+        return None
+    base = k.split("<")[0]
+    if base == "k_path":
+        targs = k[k.index("<") + 1:-1].split(", ") if "<" in k else []
+        return None if targs[1:2] == ["true"] else "k_path"
+    return base
+
+
+def census_queue(rows, qcol):
+    for r in rows:
+        k = short(r["Kernel_Name"])
+        if k and k.startswith("k_path<") and kind(k) is None:
+            return r[qcol]
+    return None
 
 
 def main(prof, rnd):
-    stats = {}
-    with open(os.path.join(prof, "kt", "run_kernel_stats.csv")) as f:
-        for row in csv.DictReader(f):
-            k = short(row["Name"])
-            if k:
-                stats[k] = {"calls": int(row["Calls"]), "avg_ms": float(row["AverageNs"]) / 1e6,
-                            "total_ms": float(row["TotalDurationNs"]) / 1e6, "pct": float(row["Percentage"])}
-    pmc = {}
-    for d in sorted(os.listdir(prof)):
-        p = os.path.join(prof, d, "run_counter_collection.csv")
-        if d.startswith("pmc_") and os.path.exists(p):
-            for k, cs in counters(p).items():
-                pmc.setdefault(k, {}).update(cs)
-    out = {"config": CONFIG, "source": f"rocprofv3 via scripts/profile.sh ({prof})", "kernels": {}}
-    for k in sorted(set(stats) | set(pmc)):
-        e = dict(stats.get(k, {}))
-        c = pmc.get(k, {})
-        e["pmc"] = c
-        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            e["hbm_read_bytes_raw"] = c["FETCH_SIZE"] * 1024
-            e["hbm_bytes_per_launch"] = c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024
-        if "WRITE_SIZE" in c:
-            e["hbm_write_bytes"] = c["WRITE_SIZE"] * 1024
-        if c.get("SQ_WAVE_CYCLES"):
-            e["wait_any_frac"] = c.get("SQ_WAIT_ANY", 0.0) / c["SQ_WAVE_CYCLES"]
-            e["issue_frac"] = c.get("SQ_ACTIVE_INST_ANY", 0.0) / c["SQ_WAVE_CYCLES"]
-        if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c and c["TCC_HIT_sum"] + c["TCC_MISS_sum"] > 0:
-            e["l2_hit_rate"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
-        out["kernels"][k] = e
     os.makedirs("profiles", exist_ok=True)
-    sfx = "" if os.environ.get("PMC_CONFIG_TAG", "metric") == "metric" else "_" + os.environ["PMC_CONFIG_TAG"]
-    with open(f"profiles/{rnd}_kernels{sfx}.json", "w") as f:
-        json.dump(out, f, indent=2)
-    # the timed kinds (DXRPT_K_TRACE / DXRPT_K_SHADOW): the uninstrumented instantiations of the frame
-    # (packet and per-lane variants), launch-weighted
-    for kind, prefixes in (("k_trace", ("k_trace<false", "k_trace_packet")),
-                           ("k_shadow", ("k_shadow<false", "k_shadow_packet")), ("k_path", ("k_path<",))):
-        # k_path<occ, persistent, lds, group, kCount = true, order> is the bench's one instrumented census
-        # frame, not a timed launch
-        cands = [k for k in out["kernels"] if k.startswith(prefixes)
-                 and not (kind == "k_path" and k[k.index("<") + 1:-1].split(", ")[4:5] == ["true"])]
-        if not cands:
+    sfx = "" if TAG == "metric" else "_" + TAG
+    # kernel trace: per-kind durations, caller-stream launches vs all
+    rows = list(csv.DictReader(open(os.path.join(prof, "kt", "run_kernel_trace.csv"))))
+    q0 = census_queue(rows, "Queue_Id")
+    dur = defaultdict(lambda: {"caller": [], "all": [], "names": set(), "vgpr": None, "scratch": None})
+    for r in rows:
+        k = short(r["Kernel_Name"])
+        kd = kind(k)
+        if kd not in ("k_path", "k_path_head", "k_path_tail"):
             continue
-        calls = sum(out["kernels"][k].get("calls", 0) for k in cands)
-
-        def wavg(key):
-            vals = [(out["kernels"][k].get("calls", 0), out["kernels"][k].get(key)) for k in cands]
-            if not calls or any(v is None for _, v in vals):
-                return None
-            return sum(c * v for c, v in vals) / calls
-
-        def wavg_pmc(counter):
-            vals = [(out["kernels"][k].get("calls", 0), out["kernels"][k]["pmc"].get(counter)) for k in cands]
-            if not calls or any(v is None for _, v in vals):
-                return None
-            return sum(c * v for c, v in vals) / calls
-        with open(f"profiles/{rnd}_pmc_{kind}{sfx}.json", "w") as f:
-            json.dump({"config": CONFIG, "kernel": " + ".join(sorted(cands)), "calls": calls,
-                       "avg_ms": (sum(out["kernels"][k].get("total_ms", 0.0) for k in cands) / calls) if calls else None,
-                       "per_kernel_avg_ms": {k: out["kernels"][k].get("avg_ms") for k in cands},
-                       "hbm_bytes_per_launch": wavg("hbm_bytes_per_launch"),
-                       "hbm_read_bytes_raw": wavg("hbm_read_bytes_raw"), "l2_hit_rate": wavg("l2_hit_rate"),
-                       "hbm_write_bytes_per_launch": wavg("hbm_write_bytes"),
-                       "wait_any_per_wave_cycle": wavg("wait_any_frac"),
-                       "active_inst_any_per_wave_cycle": wavg("issue_frac"),
-                       "counters_per_launch": ({c: wavg_pmc(c) for c in sorted(out["kernels"][cands[0]]["pmc"])}
-                                               if cands else {}),
-                       "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 16-B/lane read correction) + WRITE_SIZE KiB x1024"},
-                      f, indent=2)
-    # per FRAME of the megakernel schedule (k_path, or the split schedule's k_path_head + k_path_tail per
-    # depth): counters summed over every megakernel launch (the census frame's counting k_path excluded)
-    # and divided by the frames (launches of the frame's first kernel)
-    fam = [k for k in out["kernels"] if k.startswith(("k_path<", "k_path_head<", "k_path_tail<"))
-           and not (k.startswith("k_path<") and k[k.index("<") + 1:-1].split(", ")[4:5] == ["true"])]
-    firsts = [k for k in fam if k.startswith(("k_path<", "k_path_head<"))]
-    frames = sum(out["kernels"][k].get("calls", 0) for k in firsts)
-    if fam and frames:
-        tot = defaultdict(float)
-        ms = 0.0
-        for k in fam:
-            e = out["kernels"][k]
-            n = e.get("calls", 0)
-            ms += e.get("total_ms", 0.0)
-            for c, v in e["pmc"].items():
-                tot[c] += v * n
-        pf = {c: v / frames for c, v in tot.items()}
-        fr = {"config": CONFIG, "kernels": sorted(fam), "frames": frames, "ms_per_frame": ms / frames,
-              "per_kernel": {k: {"calls": out["kernels"][k].get("calls"), "avg_ms": out["kernels"][k].get("avg_ms")}
-                             for k in fam},
-              "counters_per_frame": pf,
-              "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 16-B/lane read correction) + WRITE_SIZE KiB x1024"}
-        if "FETCH_SIZE" in pf and "WRITE_SIZE" in pf:
-            fr["hbm_read_bytes_raw"] = pf["FETCH_SIZE"] * 1024
-            fr["hbm_write_bytes"] = pf["WRITE_SIZE"] * 1024
-            fr["hbm_bytes_per_frame"] = pf["FETCH_SIZE"] * 1024 * 2 + pf["WRITE_SIZE"] * 1024
-        if pf.get("SQ_WAVE_CYCLES"):
-            fr["wait_any_per_wave_cycle"] = pf.get("SQ_WAIT_ANY", 0.0) / pf["SQ_WAVE_CYCLES"]
-            fr["active_inst_any_per_wave_cycle"] = pf.get("SQ_ACTIVE_INST_ANY", 0.0) / pf["SQ_WAVE_CYCLES"]
-        if pf.get("SQ_ACTIVE_INST_VALU"):
-            fr["valu_lane_utilisation"] = pf.get("SQ_THREAD_CYCLES_VALU", 0.0) / (pf["SQ_ACTIVE_INST_VALU"] * 64.0)
-        if pf.get("TCC_HIT_sum", 0) + pf.get("TCC_MISS_sum", 0) > 0:
-            fr["l2_hit_rate"] = pf["TCC_HIT_sum"] / (pf["TCC_HIT_sum"] + pf["TCC_MISS_sum"])
-        tag = os.environ.get("PMC_CONFIG_TAG", "metric")
-        with open(f"profiles/{rnd}_pmc_frame_{tag}.json", "w") as f:
-            json.dump(fr, f, indent=2)
-        print(f"per frame ({tag}): {fr['ms_per_frame']:.4f} ms, HBM {fr.get('hbm_bytes_per_frame', 0) / 1e9:.3f} GB "
-              f"(writes {fr.get('hbm_write_bytes', 0) / 1e9:.3f}), L2 hit {fr.get('l2_hit_rate', 0):.3f}, "
-              f"wait {fr.get('wait_any_per_wave_cycle', 0):.3f}, lanes {fr.get('valu_lane_utilisation', 0):.3f}")
-    for src in ("kt/run_kernel_stats.csv",):
-        tag = os.environ.get("PMC_CONFIG_TAG", "metric")
-        with open(os.path.join(prof, src)) as f, open(f"profiles/{rnd}_kernel_stats{'' if tag == 'metric' else '_' + tag}.csv", "w") as g:
-            g.write(f.read())
-    for k, e in out["kernels"].items():
-        print(f"{k:26s} calls {e.get('calls', 0):4d} avg {e.get('avg_ms', 0):8.4f} ms  "
-              f"hbm/launch {e.get('hbm_bytes_per_launch', 0) / 1e6:9.1f} MB  L2 hit {e.get('l2_hit_rate', 0):.3f}")
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        e = dur[kd]
+        e["all"].append(d)
+        e["names"].add(k)
+        e["vgpr"], e["scratch"] = int(r["VGPR_Count"]), int(r["Scratch_Size"])
+        if r["Queue_Id"] == q0:
+            e["caller"].append(d)
+    # PMC passes: per-launch averages of the caller-queue launches of each kind
+    pmc = defaultdict(lambda: defaultdict(list))
+    pmc_all = defaultdict(lambda: defaultdict(list))
+    for dname in sorted(os.listdir(prof)):
+        p = os.path.join(prof, dname, "run_counter_collection.csv")
+        if not (dname.startswith("pmc_") and os.path.exists(p)):
+            continue
+        prow = list(csv.DictReader(open(p)))
+        pq = census_queue(prow, "Queue_Id")
+        for r in prow:
+            kd = kind(short(r["Kernel_Name"]))
+            if kd not in ("k_path", "k_path_head", "k_path_tail"):
+                continue
+            v = float(r["Counter_Value"])
+            pmc_all[kd][r["Counter_Name"]].append(v)
+            if r["Queue_Id"] == pq:
+                pmc[kd][r["Counter_Name"]].append(v)
+    by_kind = {}
+    for kd, e in dur.items():
+        c = {n: sum(v) / len(v) for n, v in pmc[kd].items() if v}
+        s = {"kernels": sorted(e["names"]), "calls": len(e["caller"]), "calls_all": len(e["all"]),
+             "avg_ms": sum(e["caller"]) / len(e["caller"]) if e["caller"] else None,
+             "avg_ms_all": sum(e["all"]) / len(e["all"]), "vgpr": e["vgpr"], "scratch_bytes_per_lane": e["scratch"],
+             "counters_per_launch": c}
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            s["l2_fabric_bytes_per_launch"] = (c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+        if "WRITE_SIZE" in c:
+            s["write_bytes_per_launch"] = c["WRITE_SIZE"] * 1024
+        if "FETCH_SIZE" in c:
+            s["fetch_bytes_per_launch_raw"] = c["FETCH_SIZE"] * 1024
+        if c.get("SQ_WAVE_CYCLES"):
+            s["wait_any_per_wave_cycle"] = c.get("SQ_WAIT_ANY", 0.0) / c["SQ_WAVE_CYCLES"]
+            s["active_inst_any_per_wave_cycle"] = c.get("SQ_ACTIVE_INST_ANY", 0.0) / c["SQ_WAVE_CYCLES"]
+        if c.get("SQ_ACTIVE_INST_VALU"):
+            s["valu_lane_utilisation"] = c.get("SQ_THREAD_CYCLES_VALU", 0.0) / (c["SQ_ACTIVE_INST_VALU"] * 64.0)
+        if c.get("TCC_HIT_sum", 0) + c.get("TCC_MISS_sum", 0) > 0:
+            s["l2_hit_rate"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+        by_kind[kd] = s
+    out = {"config": CONFIG, "source": f"rocprofv3 --kernel-trace --stats and --pmc passes of bench.py ({prof})",
+           "queue": "caller-stream launches (the bench's frame-at-a-time pass; the census kernel's queue)",
+           "traffic": "l2_fabric_bytes = FETCH_SIZE + WRITE_SIZE raw (L2 -> fabric requests; Infinity-Cache hits "
+                      "included; no x2 read correction)",
+           "kernels_by_kind": by_kind}
+    with open(f"profiles/{rnd}_launch_{TAG}.json", "w") as f:
+        json.dump(out, f, indent=2)
+    with open(os.path.join(prof, "kt", "run_kernel_stats.csv")) as f, open(f"profiles/{rnd}_kernel_stats{sfx}.csv", "w") as g:
+        g.write(f.read())
+    for kd, s in sorted(by_kind.items()):
+        print(f"{TAG:7s} {kd:12s} {','.join(s['kernels']):28s} launches {s['calls']:4d} avg {s['avg_ms'] or 0:8.4f} ms "
+              f"(all {s['avg_ms_all']:.4f})  fabric {s.get('l2_fabric_bytes_per_launch', 0) / 1e9:6.3f} GB "
+              f"writes {s.get('write_bytes_per_launch', 0) / 1e9:6.3f} GB  L2 hit {s.get('l2_hit_rate', 0):.3f} "
+              f"wait {s.get('wait_any_per_wave_cycle', 0):.3f} lanes {s.get('valu_lane_utilisation', 0):.3f} "
+              f"vgpr {s['vgpr']} scratch {s['scratch_bytes_per_lane']}")
 
 
 if __name__ == "__main__":

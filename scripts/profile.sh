@@ -3,6 +3,8 @@
 # with other tracing domains).  CONFIG=metric|c2|c3|c4|c5 (bench.py --config).  Outputs under
 # gpurun_out/prof_<config>/; summarise with
 #   PMC_CONFIG_TAG=<config> PMC_CONFIG="<scene>-proxy WxH L=n" scripts/pmc_summary.py gpurun_out/prof_<config> <round>
+# (bench.py's frame-at-a-time pass runs on the caller's stream: pmc_summary.py reads those launches as the
+# per-launch durations / counters of the bench line's roofline.)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 CFG=${CONFIG:-metric}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # scripts/profile.sh for several configs, each summarised into profiles/<round>_* (pmc_summary.py).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-RND=${RND:-r03}
+RND=${RND:-r04}
 for c in ${CONFIGS:-metric c3 c5}; do
   case $c in
     metric) cfg="sponza-proxy 1920x1080 L=3";; c2) cfg="sponza-proxy 1280x720 L=3";; c3) cfg="sponza-proxy 1920x1080 L=8";;

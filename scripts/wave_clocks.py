@@ -27,7 +27,6 @@ def main():
     ap.add_argument("--frames", type=int, default=3, help="census frames (the last one is reported)")
     ap.add_argument("--json", default=None)
     ap.add_argument("--occ", type=int, default=0, help="megakernel occupancy (0: default by size)")
-    ap.add_argument("--lanes", type=int, default=0, help="DXRPT_OPT_MEGAKERNEL_LANES (0: default by size)")
     ap.add_argument("--ordered", action="store_true", help="time the default (cost-ordered) frames, not a census")
     ap.add_argument("--slots", type=int, default=256 * 4 * 7, help="resident wave slots (CUs x SIMDs x waves/SIMD)")
     args = ap.parse_args()
@@ -55,8 +54,6 @@ def main():
     t.set_option(A.OPT_WAVE_CLOCKS, 1)
     if args.occ:
         t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, args.occ)
-    if args.lanes:
-        t.set_option(A.OPT_MEGAKERNEL_LANES, args.lanes)
     for f in range(args.frames):
         t.render_raw(D.make_constants(sc, st, sky, W, H, f), st, acc.data_ptr(), W, H, tiles=tiles, stream=stream,
                      lights=D.make_lights(sc))
@@ -69,7 +66,7 @@ def main():
     dur = end - start
     order = np.argsort(-dur)
     # block position of wave w: the tiles are walked in order, 64 paths per wave (8x8 blocks when the
-    # tile is a multiple of 8 in both sizes; path-group frames: 2 waves per block)
+    # tile is a multiple of 8 in both sizes)
     tl = tiles if tiles else [A.Tile(0, 0, W, H, 0, W, 0)]
     blocks = []
     for tt in tl:

@@ -34,7 +34,7 @@ def test_libdxrpt_host_exports_every_declared_function():
 
 def test_abi_version_and_defaults():
     L = A.lib()
-    assert L.dxrpt_abi_version() == 2
+    assert L.dxrpt_abi_version() == A.ABI_VERSION == 3
     s = A.AppSettings()
     L.dxrpt_default_settings(C.byref(s))
     py = A.default_settings()
@@ -73,11 +73,37 @@ def test_oracle_is_not_linked_by_the_product():
         assert b"oracle_" not in data, lib
 
 
-def test_option_ids_match_header():
-    # every DXRPT_OPT_* id of include/dxrpt.h has the same value in the Python binding
-    import re
-    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "dxrpt.h")).read()
-    ids = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define DXRPT_OPT_(\w+)\s+(\d+)u", hdr)}
-    assert len(ids) >= 29
-    for name, v in ids.items():
-        assert getattr(A, "OPT_" + name) == v, name
+def test_option_ids_match_the_header():
+    # every DXRPT_OPT_* of include/dxrpt.h is mirrored with the same id; retired ids are neither
+    txt = open(os.path.join(REPO, "include", "dxrpt.h")).read()
+    hdr = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define DXRPT_OPT_(\w+) (\d+)u", txt)}
+    py = {k[4:]: v for k, v in vars(A).items() if k.startswith("OPT_")}
+    assert hdr == py
+    assert not set(hdr.values()) & set(A.RETIRED_OPTIONS)
+    kinds = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define DXRPT_K_(\w+) (\d+)", txt)}
+    assert kinds["COUNT"] == A.K_COUNT == len(A.KERNEL_NAMES)
+    assert (kinds["PATH"], kinds["PATH_HEAD"], kinds["PATH_TAIL"]) == (A.K_PATH, A.K_PATH_HEAD, A.K_PATH_TAIL)
+
+
+def test_stats_and_tile_layouts_match_the_header(tmp_path):
+    # the ctypes mirrors of dxrpt_stats / dxrpt_tile / dxrpt_bvh_info against the C compiler's layout of
+    # include/dxrpt.h (gcc, host only)
+    import subprocess
+    src = tmp_path / "layout.c"
+    src.write_text("""#include <stdio.h>
+#include <stddef.h>
+#include "dxrpt.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(dxrpt_stats), offsetof(dxrpt_stats, kernel_ms),
+         offsetof(dxrpt_stats, schedule), offsetof(dxrpt_stats, tail_occupancy),
+         offsetof(dxrpt_stats, radiance_hits), offsetof(dxrpt_stats, census_depth1), sizeof(dxrpt_tile),
+         sizeof(dxrpt_bvh_info));
+  return 0;
+}
+""")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    want = [C.sizeof(A.Stats), A.Stats.kernel_ms.offset, A.Stats.schedule.offset, A.Stats.tail_occupancy.offset,
+            A.Stats.radiance_hits.offset, A.Stats.census_depth1.offset, C.sizeof(A.Tile), C.sizeof(A.BvhInfo)]
+    assert got == want

@@ -186,9 +186,10 @@ def _worker_native_fail(rank, world, port, q):
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="needs a host without a usable GPU (the RCCL communicator must fail)")
 def test_native_gather_failure_is_collective():
-    # On a host where the RCCL communicator cannot be built, NativeGather raises on EVERY rank (rank 0's
-    # unique-id failure is broadcast, dxrpt_comm_create's result is all-gathered) instead of leaving the
-    # other ranks blocked in the next collective -- so bench.py can fall back to torch.distributed.gather.
+    # On a host where the RCCL communicator cannot be built, NativeGather raises on EVERY rank (the ranks
+    # all-gather their device checks before anything collective in RCCL, rank 0's unique-id failure is
+    # broadcast, dxrpt_comm_create's result is all-gathered) instead of leaving the other ranks blocked in
+    # the next collective -- so bench.py can fall back to torch.distributed.gather.
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -201,27 +202,3 @@ def test_native_gather_failure_is_collective():
         assert p.exitcode == 0
     got = sorted(q.get(timeout=10) for _ in range(world))
     assert [g[:2] for g in got] == [(r, "raised") for r in range(world)], got
-
-
-def test_balanced_band_layout_covers_image_once():
-    # every pixel in exactly one rank's slab, slabs compact, the costliest bands spread over the ranks
-    from dxrpathtracer_amd.distributed import balanced_band_layout, band_costs_from_wave_clocks
-    W, H, world = 64, 200, 3
-    nb = (H + 7) // 8
-    costs = [float((b * 7919) % 23) for b in range(nb)]
-    lay = balanced_band_layout(W, H, world, costs)
-    seen = np.zeros((H, W), dtype=np.int32)
-    for r in range(world):
-        off = 0
-        for t in lay.rank_tiles(r):
-            assert t.accum_offset == off and t.accum_pitch == W
-            seen[t.y0:t.y0 + t.h, t.x0:t.x0 + t.w] += 1
-            off += t.w * t.h
-        assert off == lay.counts[r]
-    assert (seen == 1).all()
-    loads = [sum(costs[t.y0 // 8] for t in lay.rank_tiles(r)) for r in range(world)]
-    assert max(loads) - min(loads) <= max(costs)  # LPT: within one band's cost
-    # wave clocks -> band costs: wave w = 8x8 block w in raster order
-    clocks = np.array([[0, 1 + (w // (W // 8))] for w in range((W // 8) * nb)], dtype=np.uint64)
-    bc = band_costs_from_wave_clocks(W, nb * 8, clocks)
-    assert bc == [float((W // 8) * (1 + b)) for b in range(nb)]

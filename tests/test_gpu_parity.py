@@ -23,26 +23,24 @@ pytestmark = pytest.mark.gpu
 _TRACERS = {}
 
 
-def tracer(name, width=8):
-    """A context per (scene, BVH width): 8 = compressed BVH8 (default), 2 = BVH2."""
-    if (name, width) not in _TRACERS:
+def tracer(name):
+    """A context per scene (compressed BVH8)."""
+    if name not in _TRACERS:
         sc, sky = scene_bundle(name)
         t = DXRPathTracer(0)
-        t.set_option(A.OPT_BVH_WIDTH, width)
-        # the wavefront schedule for every test here; the megakernel (default for small frames) is
-        # checked against it bit for bit in test_megakernel_is_bit_identical
+        # the wavefront schedule for every test here; the megakernels (the default schedules) are
+        # checked against it bit for bit in test_megakernel_is_bit_identical / _split_is_bit_identical
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
         t.initialize_scene(sc, sky)
         info = t.build_rt_acceleration_structure()
-        assert info.width == width
-        _TRACERS[(name, width)] = t
-    return _TRACERS[(name, width)]
+        assert info.width == 8
+        _TRACERS[name] = t
+    return _TRACERS[name]
 
 
-def gpu_render(torch, name, W, H, settings, sample, tiles=None, n_out=None, accum=None, rtc=None, lights=None,
-               width=8):
+def gpu_render(torch, name, W, H, settings, sample, tiles=None, n_out=None, accum=None, rtc=None, lights=None):
     sc, sky = scene_bundle(name)
-    t = tracer(name, width)
+    t = tracer(name)
     if rtc is None:
         rtc = D.make_constants(sc, settings, sky, W, H, sample)
     n = n_out if n_out is not None else W * H
@@ -63,11 +61,11 @@ def crop_tiles(crops, W):
     return tiles, off
 
 
-def check_crops(torch, name, W, H, crops, sample=0, width=8, **overrides):
+def check_crops(torch, name, W, H, crops, sample=0, **overrides):
     sc, sky = scene_bundle(name)
     st = sc.settings(**overrides)
     tiles, n = crop_tiles(crops, W)
-    out = gpu_render(torch, name, W, H, st, sample, tiles=tiles, n_out=n, width=width).cpu().numpy()
+    out = gpu_render(torch, name, W, H, st, sample, tiles=tiles, n_out=n).cpu().numpy()
     rtc = D.make_constants(sc, st, sky, W, H, sample)
     off = 0
     for (x0, y0, w, h) in crops:
@@ -95,10 +93,10 @@ def test_boxtest_256_full_frame(torch_cuda):
 SPONZA_CROPS = [(900, 480, 96, 96), (0, 0, 64, 64), (1700, 900, 80, 64), (300, 700, 128, 48), (1500, 200, 64, 96)]
 
 
-@pytest.mark.parametrize("sample,width", [(0, 8), (7, 8), (7, 2)])
-def test_sponza_1080p_L3_crops(torch_cuda, sample, width):
-    # BASELINE.json metric config: Sponza(-proxy) 1920x1080, MaxPathLength 3 (both BVH layouts)
-    check_crops(torch_cuda, "sponza", 1920, 1080, SPONZA_CROPS, sample=sample, width=width, MaxPathLength=3)
+@pytest.mark.parametrize("sample", [0, 7])
+def test_sponza_1080p_L3_crops(torch_cuda, sample):
+    # BASELINE.json metric config: Sponza(-proxy) 1920x1080, MaxPathLength 3
+    check_crops(torch_cuda, "sponza", 1920, 1080, SPONZA_CROPS, sample=sample, MaxPathLength=3)
 
 
 def test_sponza_720p_L3_crops(torch_cuda):
@@ -115,11 +113,11 @@ def test_sponza_4k_L6_crops(torch_cuda):
     check_crops(torch_cuda, "sponza", 3840, 2160, [(1900, 1000, 64, 64), (3000, 1800, 48, 48)], sample=2, MaxPathLength=6)
 
 
-@pytest.mark.parametrize("any_hit_len,width", [(1, 8), (8, 8), (1, 2)])
-def test_suntemple_alpha_tested_crops(torch_cuda, any_hit_len, width):
+@pytest.mark.parametrize("any_hit_len", [1, 8])
+def test_suntemple_alpha_tested_crops(torch_cuda, any_hit_len):
     # BASELINE.json configs[3]: alpha-tested foliage (any-hit path)
     check_crops(torch_cuda, "suntemple", 1920, 1080, [(800, 400, 96, 96), (1200, 600, 96, 64), (100, 200, 64, 64)],
-                sample=1, width=width, MaxPathLength=3, MaxAnyHitPathLength=any_hit_len)
+                sample=1, MaxPathLength=3, MaxAnyHitPathLength=any_hit_len)
 
 
 def test_white_furnace_full_frame(torch_cuda):
@@ -194,123 +192,39 @@ def test_deterministic_run_to_run(torch_cuda):
     np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("chunks,refill,postpone", [(1, 64, 0), (4, 16, 0), (8, 32, 0), (4, 16, 16), (8, 16, 8)])
-def test_wave_pool_traversal_is_bit_identical(torch_cuda, chunks, refill, postpone):
-    # DXRPT_OPT_TRAVERSAL_MODE 1 (wave pools with lane refill, optional triangle postponement) only
-    # changes which lane traces which ray when: frames must equal the one-thread-per-ray kernels bit
-    # for bit (SunTemple: alpha-tested any-hit too)
-    torch = torch_cuda
-    for name in ("sponza", "suntemple"):
-        sc, _ = scene_bundle(name)
-        st = sc.settings(MaxPathLength=4)
-        t = tracer(name)
-        ref = gpu_render(torch, name, 480, 270, st, 2).cpu().numpy()
-        t.set_option(A.OPT_TRAVERSAL_MODE, 1)
-        t.set_option(A.OPT_CHUNKS_PER_WAVE, chunks)
-        t.set_option(A.OPT_REFILL_LANES, refill)
-        t.set_option(A.OPT_POSTPONE_TRIS, postpone)
-        try:
-            got = gpu_render(torch, name, 480, 270, st, 2).cpu().numpy()
-        finally:
-            t.set_option(A.OPT_TRAVERSAL_MODE, 0)
-        np.testing.assert_array_equal(got, ref)
-
-
-@pytest.mark.parametrize("block,occ,sblock,socc", [(256, 0, 64, 6), (128, 7, 128, 7), (256, 8, 256, 8), (64, 0, 64, 0)])
-def test_traversal_launch_options_are_bit_identical(torch_cuda, block, occ, sblock, socc):
-    # DXRPT_OPT_TRACE_BLOCK / _OCCUPANCY / _SHADE_BLOCK / _SHADE_OCCUPANCY change the launch shape and
-    # register budget only
-    torch = torch_cuda
-    sc, _ = scene_bundle("suntemple")
-    st = sc.settings(MaxPathLength=3)
-    t = tracer("suntemple")
-    ref = gpu_render(torch, "suntemple", 480, 270, st, 5).cpu().numpy()
-    t.set_option(A.OPT_TRACE_BLOCK, block)
-    t.set_option(A.OPT_OCCUPANCY, occ)
-    t.set_option(A.OPT_SHADOW_OCCUPANCY, 15 - occ if occ else 0)
-    t.set_option(A.OPT_SHADOW_GRID, 0 if block == 256 else 512)  # grid-stride any-hit loop vs one ray per thread
-    t.set_option(A.OPT_CONCURRENCY, 0 if occ == 7 else 1)
-    t.set_option(A.OPT_SHADE_BLOCK, sblock)
-    t.set_option(A.OPT_SHADE_OCCUPANCY, socc)
-    try:
-        got = gpu_render(torch, "suntemple", 480, 270, st, 5).cpu().numpy()
-    finally:
-        t.set_option(A.OPT_TRACE_BLOCK, 64)
-        t.set_option(A.OPT_OCCUPANCY, 7)
-        t.set_option(A.OPT_SHADE_BLOCK, 256)
-        t.set_option(A.OPT_SHADE_OCCUPANCY, 0)
-        t.set_option(A.OPT_SHADOW_OCCUPANCY, 8)
-        t.set_option(A.OPT_SHADOW_GRID, 0)
-        t.set_option(A.OPT_CONCURRENCY, 1)
-    np.testing.assert_array_equal(got, ref)
-
-
-@pytest.mark.parametrize("packet,pipe,lds,switch", [(0, 1, 0, 0), (0, 2, 0, 0), (0, 3, 0, 0), (1, 0, 0, 0), (2, 0, 0, 0),
-                                                    (3, 0, 0, 0), (12, 0, 0, 0), (15, 0, 0, 0), (15, 3, 0, 0),
-                                                    (0, 0, 73, 0), (1, 3, 256, 0), (0, 0, 1024, 0), (15, 0, 0, 30),
-                                                    (3, 0, 0, 60), (15, 0, 0, 100)])
-def test_traversal_variants_are_bit_identical(torch_cuda, packet, pipe, lds, switch):
-    # DXRPT_OPT_PACKET_TRAVERSAL (wave-coherent traversal with scalar node/triangle loads) and
-    # DXRPT_OPT_TRAVERSAL_PIPELINE (paired triangle loads, next-node prefetch) and DXRPT_OPT_LDS_NODES
-    # (top of the tree read from LDS) and DXRPT_OPT_PACKET_SWITCH (packet waves that turn incoherent
-    # continue one ray per lane) change which triangles a
-    # lane tests and when, never the closest (t, id) or the occlusion boolean: frames must equal the
-    # per-lane traversal bit for bit (SunTemple: alpha-tested any-hit at depth 1)
+@pytest.mark.parametrize("packet", [1, 2, 3, 12, 15])
+def test_traversal_variants_are_bit_identical(torch_cuda, packet):
+    # DXRPT_OPT_PACKET_TRAVERSAL (wave-coherent traversal with scalar node/triangle loads) changes which
+    # triangles a lane tests and when, never the closest (t, id) or the occlusion boolean: frames must equal
+    # the per-lane traversal bit for bit (SunTemple: alpha-tested any-hit at depth 1)
     torch = torch_cuda
     for name in ("sponza", "suntemple"):
         sc, _ = scene_bundle(name)
         st = sc.settings(MaxPathLength=4)
         t = tracer(name)
         t.set_option(A.OPT_PACKET_TRAVERSAL, 0)
-        t.set_option(A.OPT_TRAVERSAL_PIPELINE, 0)
-        t.set_option(A.OPT_LDS_NODES, 0)
         try:
             ref = gpu_render(torch, name, 480, 270, st, 4).cpu().numpy()
             t.set_option(A.OPT_PACKET_TRAVERSAL, packet)
-            t.set_option(A.OPT_TRAVERSAL_PIPELINE, pipe)
-            t.set_option(A.OPT_LDS_NODES, lds)
-            t.set_option(A.OPT_PACKET_SWITCH, switch)
             got = gpu_render(torch, name, 480, 270, st, 4).cpu().numpy()
         finally:
-            t.set_option(A.OPT_PACKET_SWITCH, A.DEFAULT_PACKET_SWITCH)
             t.set_option(A.OPT_PACKET_TRAVERSAL, A.DEFAULT_PACKET_TRAVERSAL)
-            t.set_option(A.OPT_TRAVERSAL_PIPELINE, A.DEFAULT_TRAVERSAL_PIPELINE)
-            t.set_option(A.OPT_LDS_NODES, A.DEFAULT_LDS_NODES)
         np.testing.assert_array_equal(got, ref)
 
 
-@pytest.mark.parametrize("packet,shadow_grid", [(0, 0), (1, 0), (15, 0), (1, 64)])
-def test_xcd_mapping_is_bit_identical(torch_cuda, packet, shadow_grid):
-    # DXRPT_OPT_XCD_MAPPING (per-XCD queue ranges, region shards) only changes which workgroup takes
-    # which ray and the queue order: frames must equal dispatch-order queues bit for bit, for L=8 paths,
-    # odd image sizes (partial waves, partial regions) and several shadow rays per vertex (spot lights)
-    torch = torch_cuda
-    for name, W, H in (("sponza", 400, 224), ("suntemple", 333, 187), ("boxtest", 97, 61)):
-        sc, sky = scene_bundle(name)
-        st = sc.settings(MaxPathLength=8)
-        rtc = D.make_constants(sc, st, sky, W, H, 5)
-        lights = D.make_lights(sc)
-        if name == "boxtest":
-            for i, (p, d) in enumerate([((1.5, 4.0, -2.0), (0.3, 1.0, -0.4)), ((-2.5, 1.5, -1.5), (-0.8, 0.2, -0.5))]):
-                L = lights.Lights[i]
-                L.Position[:] = p
-                L.Direction[:] = d
-                L.Intensity[:] = (50.0, 45.0, 37.5)
-                L.AngularAttenuationX, L.AngularAttenuationY, L.Range = 0.99, 0.95, 7.5
-            rtc.NumLights = 2
-        t = tracer(name)
-        t.set_option(A.OPT_PACKET_TRAVERSAL, packet)
-        t.set_option(A.OPT_SHADOW_GRID, shadow_grid)
-        try:
-            t.set_option(A.OPT_XCD_MAPPING, 0)
-            ref = gpu_render(torch, name, W, H, st, 5, rtc=rtc, lights=lights).cpu().numpy()
-            t.set_option(A.OPT_XCD_MAPPING, 1)
-            got = gpu_render(torch, name, W, H, st, 5, rtc=rtc, lights=lights).cpu().numpy()
-        finally:
-            t.set_option(A.OPT_XCD_MAPPING, A.DEFAULT_XCD_MAPPING)
-            t.set_option(A.OPT_PACKET_TRAVERSAL, A.DEFAULT_PACKET_TRAVERSAL)
-            t.set_option(A.OPT_SHADOW_GRID, 0)
-        np.testing.assert_array_equal(got, ref)
+def test_retired_options_are_rejected(torch_cuda):
+    # ABI 3 retired the options measured slower or neutral: setting one fails with
+    # DXRPT_E_UNSUPPORTED and a message, and changes nothing
+    t = tracer("boxtest")
+    for opt in A.RETIRED_OPTIONS:
+        rc = A.lib().dxrpt_set_option(t._ctx, opt, 1)
+        assert rc == A.DXRPT_E_UNSUPPORTED, (opt, rc)
+        assert b"retired" in A.lib().dxrpt_last_error(t._ctx)
+    assert A.lib().dxrpt_abi_version() == A.ABI_VERSION
+    with pytest.raises(Exception, match="frame overlap"):
+        t.set_option(A.OPT_FRAME_OVERLAP, 2)
+    with pytest.raises(Exception, match="occupancy"):
+        t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, 8)
 
 
 def _boxtest_lights(sc, sky, st, W, H, sample):
@@ -327,12 +241,10 @@ def _boxtest_lights(sc, sky, st, W, H, sample):
     return rtc, lights
 
 
-@pytest.mark.parametrize("name,L,any_hit,occ,packet,persist", [
-    ("sponza", 3, 1, 4, 3, 0), ("sponza", 8, 1, 6, 0, 0), ("suntemple", 4, 3, 3, 1, 0), ("boxtest", 5, 1, 5, 2, 0),
-    ("whitefurnace", 3, 1, 6, 3, 0), ("suntemple", 3, 1, 5, 3, 0), ("sponza", 4, 1, 7, 3, 0), ("boxtest", 3, 1, 8, 1, 0),
-    # persistent grid (DXRPT_OPT_MEGAKERNEL_PERSISTENT): few waves per CU so every wave loops
-    ("sponza", 3, 1, 6, 3, 1), ("boxtest", 5, 1, 5, 3, 2), ("suntemple", 3, 1, 4, 3, 24)])
-def test_megakernel_is_bit_identical(torch_cuda, name, L, any_hit, occ, packet, persist):
+@pytest.mark.parametrize("name,L,any_hit,occ,packet", [
+    ("sponza", 3, 1, 4, 3), ("sponza", 8, 1, 6, 0), ("suntemple", 4, 3, 7, 1), ("boxtest", 5, 1, 5, 2),
+    ("whitefurnace", 3, 1, 6, 3), ("suntemple", 3, 1, 5, 3), ("sponza", 4, 1, 7, 3), ("boxtest", 3, 1, 4, 1)])
+def test_megakernel_is_bit_identical(torch_cuda, name, L, any_hit, occ, packet):
     # DXRPT_OPT_MEGAKERNEL_PATHS: the whole frame as one kernel (one thread per path) must equal the
     # wavefront frame bit for bit -- same shading code, same per-path summation order -- and count the
     # same rays per depth; on full frames, on band tiles (a GPU's share) and with 3 spot lights
@@ -355,7 +267,7 @@ def test_megakernel_is_bit_identical(torch_cuda, name, L, any_hit, occ, packet, 
             t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30)
             t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, occ)
             t.set_option(A.OPT_PACKET_TRAVERSAL, packet)
-            t.set_option(A.OPT_MEGAKERNEL_PERSISTENT, persist)
+            t.set_option(A.OPT_MEGAKERNEL_SPLIT, 0)
             got = gpu_render(torch, name, W, H, st, 2, tiles=tiles, n_out=n, accum=acc0.clone(), rtc=rtc,
                              lights=lights).cpu().numpy()
             s_got = t.stats()
@@ -364,7 +276,7 @@ def test_megakernel_is_bit_identical(torch_cuda, name, L, any_hit, occ, packet, 
             assert list(s_got.shadow_rays_per_depth) == list(s_ref.shadow_rays_per_depth)
     finally:
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
-        t.set_option(A.OPT_MEGAKERNEL_PERSISTENT, 0)
+        t.set_option(A.OPT_MEGAKERNEL_SPLIT, A.DEFAULT_MEGAKERNEL_SPLIT)
         t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, A.DEFAULT_MEGAKERNEL_OCCUPANCY)
         t.set_option(A.OPT_PACKET_TRAVERSAL, A.DEFAULT_PACKET_TRAVERSAL)
 
@@ -389,6 +301,32 @@ def test_megakernel_timing(torch_cuda):
     assert stt.frame_ms >= stt.kernel_ms[A.K_PATH] * 0.99
 
 
+def test_split_frame_timing_head_and_tails(torch_cuda):
+    # DXRPT_OPT_KERNEL_TIMING on depth-split frames: the head and the tails (L - 2 launches) are bracketed
+    # separately and add up to the frame's megakernel span
+    torch = torch_cuda
+    t = tracer("sponza")
+    sc, _ = scene_bundle("sponza")
+    st = sc.settings(MaxPathLength=5)
+    t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30)
+    t.set_option(A.OPT_MEGAKERNEL_SPLIT, 1)
+    t.set_option(A.OPT_KERNEL_TIMING, 1)
+    t.reset_timing()
+    try:
+        for s in range(3):
+            gpu_render(torch, "sponza", 320, 180, st, s)
+        stt = t.stats()
+    finally:
+        t.set_option(A.OPT_KERNEL_TIMING, 0)
+        t.set_option(A.OPT_MEGAKERNEL_SPLIT, A.DEFAULT_MEGAKERNEL_SPLIT)
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
+    assert stt.schedule & A.SCHED_SPLIT and stt.tail_occupancy > 0
+    assert stt.kernel_launches[A.K_PATH_HEAD] == 3 and stt.kernel_launches[A.K_PATH_TAIL] == 3 * 3
+    assert stt.kernel_ms[A.K_PATH_HEAD] > 0 and stt.kernel_ms[A.K_PATH_TAIL] > 0
+    total = stt.kernel_ms[A.K_PATH_HEAD] + stt.kernel_ms[A.K_PATH_TAIL]
+    assert abs(total - stt.kernel_ms[A.K_PATH]) <= 1e-3 * max(1.0, stt.kernel_ms[A.K_PATH]) + 1e-3
+
+
 def _random_rays(rng, n, lo, hi):
     o = rng.uniform(lo, hi, size=(n, 3)).astype(np.float32)
     d = rng.standard_normal((n, 3)).astype(np.float32)
@@ -401,10 +339,9 @@ def _random_rays(rng, n, lo, hi):
     return rays
 
 
-@pytest.mark.parametrize("width", [2, 8])
 @pytest.mark.parametrize("name,flags", [("sponza", 0), ("sponza", A.TRACE_ANY_HIT), ("suntemple", A.TRACE_ALPHA),
                                         ("suntemple", A.TRACE_ANY_HIT | A.TRACE_ALPHA), ("boxtest", 0)])
-def test_trace_rays_matches_oracle_exactly(torch_cuda, name, flags, width):
+def test_trace_rays_matches_oracle_exactly(torch_cuda, name, flags):
     # TraceRay (RayTrace.hlsl:138,258,305,407,425) on random rays: same hit, same t, same barycentrics
     torch = torch_cuda
     rng = np.random.default_rng(42)
@@ -414,7 +351,7 @@ def test_trace_rays_matches_oracle_exactly(torch_cuda, name, flags, width):
     ref = oracle_scene(name).trace_rays(rays, flags)
     dr = torch.from_numpy(rays).cuda()
     dh = torch.zeros((rays.shape[0], 4), dtype=torch.float32, device="cuda")
-    tracer(name, width).trace_rays(dr.data_ptr(), rays.shape[0], flags, dh.data_ptr(),
+    tracer(name).trace_rays(dr.data_ptr(), rays.shape[0], flags, dh.data_ptr(),
                                    torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     got = dh.cpu().numpy()
@@ -447,13 +384,11 @@ def test_stats_and_counting_option(torch_cuda):
     assert s2.node_visits_shadow > 0
 
 
-@pytest.mark.parametrize("concurrency", [0, 1])
-def test_kernel_timing_option(torch_cuda, concurrency):
+def test_kernel_timing_option(torch_cuda):
     torch = torch_cuda
     t = tracer("boxtest")
     sc, _ = scene_bundle("boxtest")
     st = sc.settings(MaxPathLength=3)
-    t.set_option(A.OPT_CONCURRENCY, concurrency)
     t.set_option(A.OPT_KERNEL_TIMING, 1)
     t.reset_timing()
     try:
@@ -462,16 +397,13 @@ def test_kernel_timing_option(torch_cuda, concurrency):
         stt = t.stats()
     finally:
         t.set_option(A.OPT_KERNEL_TIMING, 0)
-        t.set_option(A.OPT_CONCURRENCY, 1)
     assert stt.timed_frames == 5
     assert stt.kernel_launches[A.K_TRACE] == 10 and stt.kernel_launches[A.K_RAYGEN] == 5
-    wavefront = [k for k in range(A.K_COUNT) if k != A.K_PATH]
+    wavefront = [k for k in range(A.K_COUNT) if k not in (A.K_PATH, A.K_PATH_HEAD, A.K_PATH_TAIL)]
     assert all(stt.kernel_ms[k] > 0 for k in wavefront) and stt.kernel_launches[A.K_PATH] == 0
     busy = sum(stt.kernel_ms[k] for k in wavefront)
-    if concurrency == 0:  # one stream: the frame spans every kernel
-        assert stt.frame_ms >= busy * 0.99
-    else:  # the any-hit passes overlap the next closest-hit passes
-        assert stt.frame_ms >= (busy - stt.kernel_ms[A.K_SHADOW]) * 0.99
+    # the any-hit passes overlap the next closest-hit passes
+    assert stt.frame_ms >= (busy - stt.kernel_ms[A.K_SHADOW]) * 0.99
 
 
 def test_kernel_timing_mask(torch_cuda):
@@ -519,72 +451,12 @@ def test_errors_are_reported_not_raised(torch_cuda):
     assert float(buf.abs().sum()) == 0.0  # nothing was launched
 
 
-@pytest.mark.parametrize("name,block,nodes", [("sponza", 64, 9), ("sponza", 256, 73), ("suntemple", 128, 200)])
-def test_megakernel_lds_node_cache_is_bit_identical(torch_cuda, name, block, nodes):
-    # DXRPT_OPT_LDS_NODES in the megakernel: the top BVH8 nodes read from the workgroup's LDS copy
-    torch = torch_cuda
-    sc, sky = scene_bundle(name)
-    st = sc.settings(MaxPathLength=4)
-    W, H = 320, 180
-    t = tracer(name)
-    try:
-        t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30)
-        ref = gpu_render(torch, name, W, H, st, 1).cpu().numpy()
-        t.set_option(A.OPT_TRACE_BLOCK, block)
-        t.set_option(A.OPT_LDS_NODES, nodes)
-        got = gpu_render(torch, name, W, H, st, 1).cpu().numpy()
-        np.testing.assert_array_equal(got, ref)
-    finally:
-        t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
-        t.set_option(A.OPT_TRACE_BLOCK, 64)
-        t.set_option(A.OPT_LDS_NODES, A.DEFAULT_LDS_NODES)
-
-
-@pytest.mark.parametrize("name,L,lanes,W,H", [
-    ("sponza", 3, 32, 352, 200), ("sponza", 4, 16, 352, 200), ("suntemple", 3, 32, 320, 180),
-    # frames whose last wave is partial (5000 = 78 x 64 + 8 paths): packets off in that wave
-    ("sponza", 3, 64, 100, 50), ("suntemple", 3, 32, 100, 50), ("boxtest", 5, 16, 100, 50)])
-def test_megakernel_lanes_and_partial_waves_are_bit_identical(torch_cuda, name, L, lanes, W, H):
-    # DXRPT_OPT_MEGAKERNEL_LANES: `lanes` paths per wave, the other lanes re-trace a twin's path and
-    # write nothing -- the image and the ray counts must equal the wavefront frame's, on the full frame
-    # and on a band share
-    torch = torch_cuda
-    sc, sky = scene_bundle(name)
-    st = sc.settings(MaxPathLength=L)
-    t = tracer(name)
-    rtc, lights = D.make_constants(sc, st, sky, W, H, 3), D.make_lights(sc)
-    lay = band_layout(W, H, 2)
-    try:
-        for tiles, n in ((None, W * H), (lay.rank_tiles(1), lay.counts[1])):
-            acc0 = torch.full((n, 4), 0.5, dtype=torch.float32, device="cuda")
-            t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
-            t.set_option(A.OPT_PACKET_TRAVERSAL, 0)
-            ref = gpu_render(torch, name, W, H, st, 3, tiles=tiles, n_out=n, accum=acc0.clone(), rtc=rtc,
-                             lights=lights).cpu().numpy()
-            s_ref = t.stats()
-            t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30)
-            t.set_option(A.OPT_PACKET_TRAVERSAL, A.DEFAULT_PACKET_TRAVERSAL)
-            t.set_option(A.OPT_MEGAKERNEL_LANES, lanes)
-            got = gpu_render(torch, name, W, H, st, 3, tiles=tiles, n_out=n, accum=acc0.clone(), rtc=rtc,
-                             lights=lights).cpu().numpy()
-            s_got = t.stats()
-            np.testing.assert_array_equal(got, ref)
-            assert list(s_got.radiance_rays_per_depth) == list(s_ref.radiance_rays_per_depth)
-            assert list(s_got.shadow_rays_per_depth) == list(s_ref.shadow_rays_per_depth)
-    finally:
-        t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
-        t.set_option(A.OPT_MEGAKERNEL_LANES, A.DEFAULT_MEGAKERNEL_LANES)
-        t.set_option(A.OPT_PACKET_TRAVERSAL, A.DEFAULT_PACKET_TRAVERSAL)
-
-
-@pytest.mark.parametrize("name,lanes,W,H", [("sponza", 64, 352, 200), ("suntemple", 32, 320, 180),
-                                            ("sponza", 64, 100, 50), ("sponza", 32, 100, 50)])
-def test_wave_order_is_bit_identical(torch_cuda, name, lanes, W, H):
+@pytest.mark.parametrize("name,W,H", [("sponza", 352, 200), ("suntemple", 320, 180), ("sponza", 100, 50)])
+def test_wave_order_is_bit_identical(torch_cuda, name, W, H):
     # DXRPT_OPT_WAVE_ORDER: from the second frame on, waves start costliest first (the order is built
     # on the device from the previous frame's wave durations); every frame -- a progressive sequence
     # into one accumulation buffer, then a switch to a band share (the order resets) and back -- must
-    # equal the path-ordered frames bit for bit.  Path-group frames also split their costliest slots
-    # (DXRPT_OPT_SPLIT_UNITS: 5 % of the slots, and every slot) into two half waves.
+    # equal the path-ordered frames bit for bit (100 x 50: a partial last wave).
     torch = torch_cuda
     sc, sky = scene_bundle(name)
     st = sc.settings(MaxPathLength=3)
@@ -594,10 +466,8 @@ def test_wave_order_is_bit_identical(torch_cuda, name, lanes, W, H):
     runs = []
     try:
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30)
-        t.set_option(A.OPT_MEGAKERNEL_LANES, lanes)
-        for order, split, period in ((0, 0, 1), (1, 0, 1), (1, 0, 2)) + (((1, 50, 1), (1, 1000, 3)) if lanes < 64 else ()):
+        for order, period in ((0, 1), (1, 1), (1, 2)):
             t.set_option(A.OPT_WAVE_ORDER, order)
-            t.set_option(A.OPT_SPLIT_UNITS, split)
             t.set_option(A.OPT_WAVE_ORDER_PERIOD, period)
             acc = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
             share = torch.zeros((lay.counts[1], 4), dtype=torch.float32, device="cuda")
@@ -611,15 +481,15 @@ def test_wave_order_is_bit_identical(torch_cuda, name, lanes, W, H):
                     gpu_render(torch, name, W, H, st, f, tiles=lay.rank_tiles(1), n_out=lay.counts[1], accum=share,
                                rtc=rtc, lights=lights)
                     frames.append(share.cpu().numpy().copy())
+                if order:
+                    assert t.stats().schedule & A.SCHED_ORDER_KERNEL
             runs.append(frames)
         for run in runs[1:]:
             for a, b in zip(runs[0], run):
                 np.testing.assert_array_equal(b, a)
     finally:
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
-        t.set_option(A.OPT_MEGAKERNEL_LANES, A.DEFAULT_MEGAKERNEL_LANES)
         t.set_option(A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)
-        t.set_option(A.OPT_SPLIT_UNITS, A.DEFAULT_SPLIT_UNITS)
         t.set_option(A.OPT_WAVE_ORDER_PERIOD, A.DEFAULT_WAVE_ORDER_PERIOD)
 
 
@@ -634,7 +504,6 @@ def test_xcd_chunk_mapping_is_bit_identical(torch_cuda, name, W, H):
     t = tracer(name)
     try:
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30)
-        t.set_option(A.OPT_MEGAKERNEL_LANES, 64)
         t.set_option(A.OPT_WAVE_ORDER, 0)
         imgs = []
         for c in (0, 8, 3):
@@ -644,21 +513,19 @@ def test_xcd_chunk_mapping_is_bit_identical(torch_cuda, name, W, H):
             np.testing.assert_array_equal(img, imgs[0])
     finally:
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
-        t.set_option(A.OPT_MEGAKERNEL_LANES, A.DEFAULT_MEGAKERNEL_LANES)
         t.set_option(A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)
         t.set_option(A.OPT_XCD_CHUNK, A.DEFAULT_XCD_CHUNK)
 
 
-@pytest.mark.parametrize("name,L,W,H,occ,tocc,parts", [
-    ("sponza", 3, 352, 200, 7, 7, 1), ("sponza", 8, 352, 200, 5, 6, 2), ("suntemple", 3, 320, 180, 6, 5, 2),
-    ("boxtest", 5, 100, 50, 4, 8, 2), ("sponza", 6, 100, 50, 8, 4, 1), ("whitefurnace", 3, 128, 128, 7, 7, 2),
-    ("sponza", 8, 97, 61, 6, 7, 2)])
-def test_megakernel_split_is_bit_identical(torch_cuda, name, L, W, H, occ, tocc, parts):
+@pytest.mark.parametrize("name,L,W,H,occ,tocc", [
+    ("sponza", 3, 352, 200, 7, 7), ("sponza", 8, 352, 200, 5, 6), ("suntemple", 3, 320, 180, 6, 5),
+    ("boxtest", 5, 100, 50, 4, 7), ("sponza", 6, 100, 50, 7, 4), ("whitefurnace", 3, 128, 128, 7, 7),
+    ("sponza", 8, 97, 61, 6, 7)])
+def test_megakernel_split_is_bit_identical(torch_cuda, name, L, W, H, occ, tocc):
     # DXRPT_OPT_MEGAKERNEL_SPLIT: one kernel per depth with the surviving paths compacted between depths
     # (wave64 ballot, one atomic per wave) and the path state carried in the queue -- the frame and the
     # ray counts per depth must equal the wavefront frame's, on full frames (partial last waves at 100 x
-    # 50 and 97 x 61), on a band share, with 3 spot lights (BoxTest) and alpha-tested any hit (SunTemple);
-    # DXRPT_OPT_SPLIT_PARTS 2: the frame's path slots as two concurrent halves on two internal streams
+    # 50 and 97 x 61), on a band share, with 3 spot lights (BoxTest) and alpha-tested any hit (SunTemple)
     torch = torch_cuda
     sc, sky = scene_bundle(name)
     st = sc.settings(MaxPathLength=L)
@@ -674,30 +541,23 @@ def test_megakernel_split_is_bit_identical(torch_cuda, name, L, W, H, occ, tocc,
                              lights=lights).cpu().numpy()
             s_ref = t.stats()
             t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30)
-            t.set_option(A.OPT_MEGAKERNEL_LANES, 64)
             t.set_option(A.OPT_WAVE_ORDER, 0)
             t.set_option(A.OPT_MEGAKERNEL_SPLIT, 1)
             t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, occ)
             t.set_option(A.OPT_TAIL_OCCUPANCY, tocc)
-            t.set_option(A.OPT_SPLIT_PARTS, parts)
-            for bins in (0, 1):  # DXRPT_OPT_SPLIT_BINS: queues binned by screen region x ray octant
-                t.set_option(A.OPT_SPLIT_BINS, bins)
-                got = gpu_render(torch, name, W, H, st, 4, tiles=tiles, n_out=n, accum=acc0.clone(), rtc=rtc,
-                                 lights=lights).cpu().numpy()
-                s_got = t.stats()
-                assert s_got.schedule & A.SCHED_SPLIT, s_got.schedule
-                assert bool(s_got.schedule & A.SCHED_PARTS) == (parts == 2), s_got.schedule
-                np.testing.assert_array_equal(got, ref)
-                assert list(s_got.radiance_rays_per_depth) == list(s_ref.radiance_rays_per_depth)
-                assert list(s_got.shadow_rays_per_depth) == list(s_ref.shadow_rays_per_depth)
+            got = gpu_render(torch, name, W, H, st, 4, tiles=tiles, n_out=n, accum=acc0.clone(), rtc=rtc,
+                             lights=lights).cpu().numpy()
+            s_got = t.stats()
+            assert s_got.schedule & A.SCHED_SPLIT, s_got.schedule
+            assert s_got.occupancy == occ and s_got.tail_occupancy == tocc, (s_got.occupancy, s_got.tail_occupancy)
+            np.testing.assert_array_equal(got, ref)
+            assert list(s_got.radiance_rays_per_depth) == list(s_ref.radiance_rays_per_depth)
+            assert list(s_got.shadow_rays_per_depth) == list(s_ref.shadow_rays_per_depth)
     finally:
-        t.set_option(A.OPT_SPLIT_BINS, A.DEFAULT_SPLIT_BINS)
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
         t.set_option(A.OPT_MEGAKERNEL_SPLIT, A.DEFAULT_MEGAKERNEL_SPLIT)
-        t.set_option(A.OPT_SPLIT_PARTS, A.DEFAULT_SPLIT_PARTS)
         t.set_option(A.OPT_TAIL_OCCUPANCY, A.DEFAULT_TAIL_OCCUPANCY)
         t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, A.DEFAULT_MEGAKERNEL_OCCUPANCY)
-        t.set_option(A.OPT_MEGAKERNEL_LANES, A.DEFAULT_MEGAKERNEL_LANES)
         t.set_option(A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)
 
 
@@ -749,14 +609,13 @@ def test_primary_aov_matches_oracle(torch_cuda, name, W, H, crops):
         off += w * h
 
 
-@pytest.mark.parametrize("name,L,anyhit,W,H,mega,lanes,split", [
-    ("suntemple", 3, 1, 480, 270, 1 << 30, 64, 0), ("suntemple", 4, 4, 320, 180, 1 << 30, 32, 0),
-    ("sponza", 3, 3, 480, 270, 1 << 30, 64, 0), ("sponza", 3, 1, 480, 270, 1 << 30, 16, 0),
-    ("suntemple", 5, 5, 320, 180, 1 << 30, 64, 1), ("sponza", 4, 4, 320, 180, 0, 64, 0)])
-def test_opacity_micromap_is_bit_identical(torch_cuda, name, L, anyhit, W, H, mega, lanes, split):
+@pytest.mark.parametrize("name,L,anyhit,W,H,mega,split", [
+    ("suntemple", 3, 1, 480, 270, 1 << 30, 0), ("suntemple", 4, 4, 320, 180, 1 << 30, 0),
+    ("sponza", 3, 3, 480, 270, 1 << 30, 0), ("suntemple", 5, 5, 320, 180, 1 << 30, 1), ("sponza", 4, 4, 320, 180, 0, 0)])
+def test_opacity_micromap_is_bit_identical(torch_cuda, name, L, anyhit, W, H, mega, split):
     # DXRPT_OPT_OPACITY_MICROMAP: alpha-tested candidates whose barycentric cell decides AnyHitShader
     # (RayTrace.hlsl:485-507) skip the opacity tap -- every schedule's alpha paths (packet primaries and
-    # depth-1 sun shadows, per-lane rays, path-group pairs, the split tails, the wavefront passes) must
+    # depth-1 sun shadows, per-lane rays, the split tails, the wavefront passes) must
     # give the frame of the always-tapping build, with alpha testing on every depth (MaxAnyHitPathLength)
     torch = torch_cuda
     sc, sky = scene_bundle(name)
@@ -765,7 +624,6 @@ def test_opacity_micromap_is_bit_identical(torch_cuda, name, L, anyhit, W, H, me
     rtc = D.make_constants(sc, st, sky, W, H, 3)
     try:
         t.set_option(A.OPT_MEGAKERNEL_PATHS, mega)
-        t.set_option(A.OPT_MEGAKERNEL_LANES, lanes)
         t.set_option(A.OPT_MEGAKERNEL_SPLIT, split)
         t.set_option(A.OPT_WAVE_ORDER, 0)
         frames = []
@@ -776,20 +634,19 @@ def test_opacity_micromap_is_bit_identical(torch_cuda, name, L, anyhit, W, H, me
             s = t.stats()
             if mega:
                 assert bool(s.schedule & A.SCHED_SPLIT) == bool(split), s.schedule
-                assert s.paths_per_wave == lanes, s.paths_per_wave
+                assert s.paths_per_wave == 64, s.paths_per_wave
         np.testing.assert_array_equal(frames[1], frames[0])
     finally:
         t.set_option(A.OPT_OPACITY_MICROMAP, A.DEFAULT_OPACITY_MICROMAP)
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
-        t.set_option(A.OPT_MEGAKERNEL_LANES, A.DEFAULT_MEGAKERNEL_LANES)
         t.set_option(A.OPT_MEGAKERNEL_SPLIT, A.DEFAULT_MEGAKERNEL_SPLIT)
         t.set_option(A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)
 
 
 @pytest.mark.parametrize("world,rank,overlap", [(8, 5, 0), (8, 2, 1), (16, 3, 0)])
 def test_census_wave_clocks_small_frames(torch_cuda, world, rank, overlap):
-    # DXRPT_OPT_COUNT_TRAVERSAL + DXRPT_OPT_WAVE_CLOCKS on a frame of <= 400k paths (a GPU's band share:
-    # path groups when frames do not overlap): the census runs the 64-lane per-path kernel, records one
+    # DXRPT_OPT_COUNT_TRAVERSAL + DXRPT_OPT_WAVE_CLOCKS on a frame of <= 400k paths (a GPU's band share,
+    # cost-ordered when frames overlap): the census runs the 64-lane per-path kernel, records one
     # stamp pair per 64 paths and nothing past them (the clock buffer is sized for
     # ceil(paths / 64) waves); the frame equals the uninstrumented one, and the next uninstrumented
     # frame reports no stale stamps.

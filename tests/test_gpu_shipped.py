@@ -141,16 +141,15 @@ def test_sponza_720p_L3(torch_cuda):
 
 def test_sponza_1080p_L8(torch_cuda):
     # BASELINE.json configs[2]: 2.07M paths x 7 vertices, the default schedule: the depth-split megakernel
-    # (head + one compacting tail per depth), one part (overlapped frames fill its drains)
+    # (head + one compacting tail per depth; overlapped frames fill its drains)
     W, H = 1920, 1080
     out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 8, 15, 0.125, check_kernel="megakernel",
                                   sched=A.SCHED_MEGAKERNEL | A.SCHED_SPLIT)
-    assert not t_sched("sponza") & A.SCHED_PARTS
     compare_crops("sponza", W, H, out, st, rtc, frame_crops(W, H), 0.125, "C3 s15")
 
 
 def test_sponza_4k_L6(torch_cuda):
-    # BASELINE.json configs[4] on one GPU: 8.3M paths x 5 vertices, the depth-split megakernel (one part)
+    # BASELINE.json configs[4] on one GPU: 8.3M paths x 5 vertices, the depth-split megakernel
     W, H = 3840, 2160
     out, st, rtc = render_shipped(torch_cuda, "sponza", W, H, 6, 2, 0.0, check_kernel="megakernel",
                                   sched=A.SCHED_MEGAKERNEL | A.SCHED_SPLIT)

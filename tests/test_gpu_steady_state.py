@@ -5,8 +5,8 @@ Defaults (r03, overlapped frames, DXRPT_OPT_FRAME_OVERLAP 1): every megakernel f
 and is blended on the caller's stream; 64-lane waves at every size; a frame of at most 1.5 rounds of
 resident waves (a GPU's 1/8 share of the metric frame) runs the cost-ordered instantiation -- frame 0
 records its wave costs in path order, frames 1+ start their waves in the cost order built from them
-(DXRPT_OPT_WAVE_ORDER, default "by frame size") -- larger ones path order.  With overlap off the r02
-defaults hold (path groups up to 400,000 paths, the cost order up to 3 rounds).  Each test renders >= 3
+(DXRPT_OPT_WAVE_ORDER, default "by frame size") -- larger ones path order.  With overlap off the cost
+order holds up to 3 rounds.  Each test renders >= 3
 consecutive frames (RaygenShader over
 DispatchRays(W, H, 1), RayTrace.hlsl:92-149) into ONE accumulation target, checks after every frame
 that the schedule it expects actually ran (dxrpt_stats.schedule / paths_per_wave), and compares the
@@ -87,14 +87,12 @@ def _expect(lanes, ordered, overlap=True, split=False):
         assert s.schedule & A.SCHED_MEGAKERNEL and not s.schedule & A.SCHED_CENSUS, s.schedule
         # from 2M path vertices (overlapped frames) the depth-split schedule, one part
         assert bool(s.schedule & A.SCHED_SPLIT) == split, f"frame {f}: schedule {s.schedule}"
-        assert not s.schedule & A.SCHED_PARTS, f"frame {f}: schedule {s.schedule}"
         assert bool(s.schedule & A.SCHED_OVERLAP) == overlap, f"frame {f}: schedule {s.schedule}"
         assert bool(s.schedule & A.SCHED_ORDER_KERNEL) == ordered, \
             f"frame {f}: the {'cost-ordered' if ordered else 'path-ordered'} instantiation did not run ({s.schedule})"
         # frame 0 builds the order from its own wave costs; frames 1+ start their waves in that order
         assert bool(s.schedule & A.SCHED_COST_ORDERED) == (ordered and f > 0), f"frame {f}: schedule {s.schedule}"
         assert s.paths_per_wave == lanes, (f, s.paths_per_wave)
-        assert bool(s.schedule & A.SCHED_PATH_GROUPS) == (lanes < 64)
     return check
 
 
@@ -113,12 +111,12 @@ def test_metric_1080p_L3_consecutive_frames(torch_cuda, name):
 
 
 @pytest.mark.parametrize("world,rank,lanes,ordered,overlap", [(8, 5, 64, True, 1), (8, 0, 64, True, 1),
-                                                              (2, 1, 64, False, 1), (8, 5, 32, True, 0),
+                                                              (2, 1, 64, False, 1), (8, 5, 64, True, 0),
                                                               (4, 1, 64, True, 1)])
 def test_metric_band_share_consecutive_frames(torch_cuda, world, rank, lanes, ordered, overlap):
     # one GPU's share of the metric frame (bench.py --gpus N): 1/8 = 259,200 paths (4,050 waves, one round
     # at 4 waves/SIMD: cost-ordered from its second frame), 1/4 = 518,400 (1.3 rounds at 6: ordered),
-    # 1/2 = 1,036,800 paths (path order); overlap off: the 1/8 share in path groups of 32 per wave
+    # 1/2 = 1,036,800 paths (path order); overlap off: the 1/8 share one frame at a time
     W, H = 1920, 1080
     lay = band_layout(W, H, world)
     # the 1/2 share (2.07M path vertices) runs the depth-split schedule when frames overlap
@@ -147,7 +145,7 @@ def test_c3_1080p_L8_sixteen_samples(torch_cuda):
         # 2.07M paths x 7 vertices: the depth-split schedule as one part (default by frame size),
         # overlapped with the neighbour frames
         assert s.schedule & A.SCHED_MEGAKERNEL and s.paths_per_wave == 64, (f, s.schedule, s.paths_per_wave)
-        assert s.schedule & A.SCHED_SPLIT and not s.schedule & A.SCHED_PARTS, (f, s.schedule)
+        assert s.schedule & A.SCHED_SPLIT, (f, s.schedule)
         assert s.schedule & A.SCHED_OVERLAP, (f, s.schedule)
 
     _steady_frames(torch_cuda, "sponza", W, H, 8, 16, crops, expect=check)
@@ -162,8 +160,8 @@ def test_overlapped_frames_are_bit_identical(torch_cuda, W, H, L, frames, share)
     # render them) alternate between two sets of internal streams and stage their radiance; the caller's
     # stream blends each stage in frame order (RayTrace.hlsl:140-148).  >= 17 frames cross a cost-order
     # rebuild (every 16th frame records, the next frame waits for the new order); 1080p L=3 and L=8 and
-    # 4K L=6 run the depth-split schedule overlapped (one part) against k_path / two halves one frame at
-    # a time.  The accumulated target must equal the one-frame-at-a-time schedule's bit for bit.
+    # 4K L=6 run the depth-split schedule overlapped against k_path / the split one frame at a time.  The
+    # accumulated target must equal the one-frame-at-a-time schedule's bit for bit.
     torch = torch_cuda
     sc, sky = scene_bundle("sponza")
     st = sc.settings(MaxPathLength=L)
@@ -175,7 +173,7 @@ def test_overlapped_frames_are_bit_identical(torch_cuda, W, H, L, frames, share)
     consts = [D.make_constants(sc, st, sky, W, H, f % 16) for f in range(frames)]
     stream = torch.cuda.current_stream().cuda_stream
     out = []
-    for overlap in (0, 1, 2):  # one frame at a time, two / three frames in flight
+    for overlap in (0, 1):  # one frame at a time, two frames in flight
         t = _fresh("sponza")
         try:
             t.set_option(A.OPT_FRAME_OVERLAP, overlap)
@@ -189,4 +187,89 @@ def test_overlapped_frames_are_bit_identical(torch_cuda, W, H, L, frames, share)
         finally:
             t.close()
     np.testing.assert_array_equal(out[1], out[0])
-    np.testing.assert_array_equal(out[2], out[0])
+
+
+def _frames(torch, W, H, L, frames, overlap, streams=None, between=None, name="sponza", lights_of=None):
+    """`frames` back-to-back frames into one target through a fresh context with DXRPT_OPT_FRAME_OVERLAP
+    `overlap`, no host sync between them: frame f on streams[f % len(streams)] (torch streams; default the
+    current one), between(t, f) called before frame f, lights_of(f) the frame's (rtc.NumLights, lights)."""
+    sc, sky = scene_bundle(name)
+    st = sc.settings(MaxPathLength=L)
+    t = _fresh(name)
+    try:
+        t.set_option(A.OPT_FRAME_OVERLAP, overlap)
+        acc = torch.full((W * H, 4), 0.5, dtype=torch.float32, device="cuda")
+        streams = streams or [torch.cuda.current_stream()]
+        for st_ in streams:  # the target was written on the current stream
+            st_.wait_stream(torch.cuda.current_stream())
+        for f in range(frames):
+            if between is not None:
+                between(t, f)
+            rtc = D.make_constants(sc, st, sky, W, H, f % 16)
+            lights = D.make_lights(sc)
+            if lights_of is not None:
+                rtc.NumLights, lights = lights_of(f, sc, lights)
+            t.render_raw(rtc, st, acc.data_ptr(), W, H, stream=streams[f % len(streams)].cuda_stream, lights=lights)
+        torch.cuda.synchronize()
+        return acc.cpu().numpy(), t.stats()
+    finally:
+        t.close()
+
+
+@pytest.mark.parametrize("W,H,L", [(1280, 720, 3), (1920, 1080, 3), (320, 180, 5)])
+def test_overlapped_frames_on_alternating_streams(torch_cuda, W, H, L):
+    # include/dxrpt.h "Stream ordering": a caller that submits consecutive frames on two streams (a ring of
+    # command queues) still gets the frames in submission order -- each call on a new stream first waits
+    # for the previous stream -- so the progressive blend (order dependent) equals the one-stream,
+    # one-frame-at-a-time result bit for bit, over >= 6 frames (1080p: the depth-split schedule)
+    torch = torch_cuda
+    ref, _ = _frames(torch, W, H, L, 8, 0)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    got, s = _frames(torch, W, H, L, 8, 1, streams=streams)
+    assert s.schedule & A.SCHED_OVERLAP, s.schedule
+    np.testing.assert_array_equal(got, ref)
+    got0, _ = _frames(torch, W, H, L, 8, 0, streams=streams)
+    np.testing.assert_array_equal(got0, ref)
+
+
+def test_census_frame_between_overlapped_frames(torch_cuda):
+    # ADVICE r03: a non-overlapped frame (here a census frame, DXRPT_OPT_COUNT_TRAVERSAL) between
+    # overlapped frames, with no host sync, runs after them and before the next one (it shares the BVH8
+    # stack-spill slab and, through the stream, the target): the frames equal the one-at-a-time result
+    torch = torch_cuda
+    W, H = 1920, 1080
+
+    def census_on_3(t, f):
+        t.set_option(A.OPT_COUNT_TRAVERSAL, 1 if f in (3, 4) else 0)
+
+    ref, _ = _frames(torch, W, H, 3, 8, 0)
+    got, s = _frames(torch, W, H, 3, 8, 1, between=census_on_3)
+    np.testing.assert_array_equal(got, ref)
+    got2, _ = _frames(torch, 1280, 720, 3, 8, 1, between=census_on_3)
+    ref2, _ = _frames(torch, 1280, 720, 3, 8, 0)
+    np.testing.assert_array_equal(got2, ref2)
+
+
+@pytest.mark.parametrize("name,W,H", [("boxtest", 256, 256), ("sponza", 640, 360)])
+def test_light_count_changes_between_overlapped_frames(torch_cuda, name, W, H):
+    # ADVICE r03: frames in flight with different shadow-slot counts (spot lights toggled between frames)
+    # keep their own buffers and stack-spill slabs: equal to the one-frame-at-a-time result
+    torch = torch_cuda
+    import math
+
+    def lights_of(f, sc, lights):
+        n = (0, 2, 3, 0, 1, 3, 2, 0)[f % 8]
+        for i in range(3):
+            L = lights.Lights[i]
+            p, d = [((1.5, 4.0, -2.0), (-0.3, -1.0, 0.4)), ((-2.5, 1.5, -1.5), (0.8, -0.2, 0.5)),
+                    ((0.5, 3.0, 2.0), (0.0, -1.0, -0.2))][i]
+            nn = math.sqrt(sum(x * x for x in d))
+            L.Position[:] = p
+            L.Direction[:] = tuple(-x / nn for x in d)
+            L.Intensity[:] = (50.0, 45.0, 37.5)
+            L.AngularAttenuationX, L.AngularAttenuationY, L.Range = math.cos(0.3), math.cos(0.6), 7.5
+        return n, lights
+
+    ref, _ = _frames(torch, W, H, 4, 8, 0, name=name, lights_of=lights_of)
+    got, _ = _frames(torch, W, H, 4, 8, 1, name=name, lights_of=lights_of)
+    np.testing.assert_array_equal(got, ref)
