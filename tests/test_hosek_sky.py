@@ -1,12 +1,14 @@
 """Hosek-Wilkie sky (the reference's SkyCache::Init sky, host/hosek.cpp) on CPU.
 
-Pins: the zenith probe of SURVEY.md 8(c) (Sponza sun, turbidity 2, ground albedo 0.25: R radiance
-x 683 x 2^-10 = 3.04945, computed from the reference's ArHosekSkyModel.cpp) and regression vectors of
-this restatement (tests/golden/hosek_sky.json, tests/golden/make_hosek_golden.py).  The rest of the
-model (the spectral sun disc, DirectXMath float details) is parity-unpinned: no reference output of
-it exists here.  The tables come from the packaged file (data/hosek_tables.bin), so these tests run
-without the reference checkout; where the checkout is present, the packaged file is checked against
-the reference's dataset sources table by table and cube by cube.
+Pins: the reference's own sky code compiled verbatim (tests/golden/make_hosek_reference.py: the whole of
+HosekSky/ArHosekSkyModel.cpp and Graphics/Spectrum.cpp, SkyCache::Init / Sample's statements from
+Graphics/Skybox.cpp:31-154,254-269, DirectXMath's four Float3 ops restated from its SSE2 paths) ->
+tests/golden/hosek_reference.npz: SunIrradiance, SunRenderColor and every FP16 texel of the full
+6 x 128 x 128 cube for the scenes' skies, plus a 6 x 16 x 16 sweep over turbidity 1..10, coloured albedo and
+sun elevation -- matched BIT FOR BIT (tolerance 0).  Also the zenith probe of SURVEY.md 8(c) (3.04945) and
+regression vectors of this restatement (tests/golden/hosek_sky.json).  The tables come from the packaged
+file (data/hosek_tables.bin), so these tests run without the reference checkout; where the checkout is
+present, the packaged file is checked against the reference's dataset sources table by table.
 """
 import json
 import math
@@ -20,6 +22,7 @@ import dxrpathtracer_amd._abi as A
 
 HOSEK = D.scene.load_hosek()
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "hosek_sky.json")
+REFERENCE = os.path.join(os.path.dirname(__file__), "golden", "hosek_reference.npz")
 
 
 def _f32(x):
@@ -34,6 +37,36 @@ def test_zenith_probe_matches_reference():
     r = HOSEK.rgb_radiance(2.0, 0.25, float(elevation), 0.0, float(theta_s), 0)
     v = _f32(_f32(_f32(r) * _f32(683.0)) * _f32(2.0 ** -10))
     assert abs(float(v) - 3.04945) < 1e-5
+
+
+def _sky(p, res):
+    import ctypes as C
+    cube = np.zeros(6 * res * res * 4, dtype=np.uint16)
+    irr, ren = (C.c_float * 3)(), (C.c_float * 3)()
+    rc = A.host().dxrpt_host_sky_create_hosek(HOSEK.handle, (C.c_float * 3)(*p[:3]), float(p[3]), float(p[4]),
+                                              (C.c_float * 3)(*p[5:8]), res, cube.ctypes.data, irr, ren)
+    assert rc == 0, A.host().dxrpt_host_hosek_last_error()
+    return np.array(irr, np.float32), np.array(ren, np.float32), cube.reshape(6, res, res, 4)
+
+
+def test_sky_matches_reference_skycache_bit_for_bit():
+    """SkyCache::Init + Sample of the reference, compiled verbatim (make_hosek_reference.py): sun irradiance,
+    sun render colour and every FP16 cube texel identical (tolerance 0) for each case."""
+    g = np.load(REFERENCE)
+    names = [str(n) for n in g["names"]]
+    assert {"sponza", "suntemple"} <= set(names) and len(names) >= 8
+    for i, name in enumerate(names):
+        p, res = g["params"][i], int(g["res"][i])
+        irr, ren, cube = _sky(p, res)
+        np.testing.assert_array_equal(irr.view(np.uint32), g[f"{name}_sun_irradiance"].view(np.uint32), err_msg=name)
+        np.testing.assert_array_equal(ren.view(np.uint32), g[f"{name}_sun_render_color"].view(np.uint32), err_msg=name)
+        # the reference's texels: XMStoreHalf4 of Sample()'s float32 radiance (round to nearest even), alpha 1
+        ref = g[f"{name}_cube_f16"] if f"{name}_cube_f16" in g.files else g[f"{name}_cube"].astype(np.float16).view(np.uint16)
+        assert ref.shape == (6, res, res, 3)
+        np.testing.assert_array_equal(cube[..., :3], ref, err_msg=name)
+        assert (cube[..., 3] == 0x3C00).all()
+        if f"{name}_cube_f32_every8" in g.files:  # the stored float32 samples are the texels' source values
+            np.testing.assert_array_equal(g[f"{name}_cube_f32_every8"].astype(np.float16).view(np.uint16), ref[:, 4::8, 4::8])
 
 
 def test_radiance_depends_on_view_and_sun_angles_only():
