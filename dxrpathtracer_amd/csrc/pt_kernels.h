@@ -63,13 +63,7 @@ struct FrameBuffers {
     float4* sh_org = nullptr;
     float4* sh_dir = nullptr;
     float4* sh_con = nullptr;
-    // depth-split tails with k_path_tail_shadow: per queued vertex, (partial radiance rgb, bits(queue
-    // position of the continuation or accumulation index)) and (tail slot index, nsh | cont << 8 |
-    // next IsDiffuse << 9); queue d's counters are the third counter group
-    float4* pend = nullptr;
-    uint2* pend_meta = nullptr;
-    float4* thit = nullptr;  // ... with k_path_tail_trace: the closest hit per dense tail index (hit[] layout)
-    uint32_t* counters = nullptr;  // [queue][shard]: 3 * kMaxDepthQueues * kQueueShards
+    uint32_t* counters = nullptr;  // [queue][shard]: 2 * kMaxDepthQueues * kQueueShards
     // megakernel frames: the other counter set of the ping-pong pair (the next frame's), zeroed by the
     // frame's first kernel's workgroup 0 -- so the next frame needs no fill launch (null: nothing to zero)
     uint32_t* counters_next = nullptr;
@@ -145,8 +139,8 @@ struct FrameParams {
 };
 
 constexpr uint32_t kWaveClasses = 256;
-// words of one counter set: the sharded queue counters (radiance, shadow, pending-shadow queues), padded to 16 B
-constexpr uint32_t kCounterWords = 3 * 16 * 64 + 16;
+// words of one counter set: the sharded queue counters, padded to 16 B
+constexpr uint32_t kCounterWords = 2 * 16 * 64 + 16;
 
 // Kernel sequence of one wavefront frame: raygen, then (trace, shade, shadow, resolve) per depth 1..L-1,
 // then accumulate.  With `aux` and 2 * kMaxDepthQueues `fork_ev` events, each depth's any-hit pass runs

@@ -33,22 +33,6 @@
 #include "pt_kernels.h"
 #include "pt_math.h"
 
-// Depth-split tails: the vertices' shadow rays in their own kernel (k_path_tail_shadow) with its own
-// register budget, instead of inside k_path_tail.
-#ifndef DXRPT_TAIL_SHADOW
-#define DXRPT_TAIL_SHADOW 0
-#endif
-#ifndef DXRPT_TAIL_SHADOW_OCC
-#define DXRPT_TAIL_SHADOW_OCC 8
-#endif
-// ... and their closest hits in their own kernel too (k_path_tail_trace), so k_path_tail only shades.
-#ifndef DXRPT_TAIL_TRACE
-#define DXRPT_TAIL_TRACE 0
-#endif
-#ifndef DXRPT_TAIL_TRACE_OCC
-#define DXRPT_TAIL_TRACE_OCC 7
-#endif
-
 namespace dxrpt {
 
 constexpr int kBlock = 256;                   // streaming kernels (raygen, shade, resolve, accumulate)
@@ -1597,28 +1581,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     split_finish(A, 1, cont, qpos, nextDiffuse, pr.accumIdx, rad);
 }
 
-#if DXRPT_TAIL_TRACE
-// The closest hit of depth d's queued rays (one per lane), into thit[dense index] for k_path_tail.
-template <int kOcc>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_path_tail_trace(KArgs A, int d) {
-    const uint32_t* cnt = A.F.counters + uint32_t(d) * kQueueShards;
-    const uint32_t n = queue_total(cnt);
-    const uint32_t nw = (n + 63u) / 64u;
-    if (blockIdx.x >= nw) return;
-    const uint32_t j = A.P.xcd_chunk ? xcd_position(blockIdx.x, nw, A.P.xcd_chunk) : blockIdx.x;
-    lut_fill(A.S);
-    const uint32_t i = j * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
-    const RayQueue& Q = A.F.q[d & 1];
-    const float4 o4 = Q.org[pos], d4 = Q.dir[pos];
-    HitRec h;
-    uint32_t nv = 0, nt = 0;
-    traverse8<false, false, true>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= A.P.set.MaxAnyHitPathLength, h, nv, nt);
-    A.F.thit[i] = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
-}
-#endif
-
 // Depth d of the paths queued for it (one per lane); waves past the queued count exit at once (the grid
 // covers every path of the frame).
 template <int kOcc>
@@ -1637,21 +1599,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
     const RayQueue& Q = A.F.q[d & 1];
     HitRec h;
-#if DXRPT_TAIL_TRACE
-    {  // the closest hit from k_path_tail_trace
-        const float4 hv = A.F.thit[i];
-        h.b1 = hv.x;
-        h.b2 = hv.y;
-        h.tri = fbits(hv.z);
-        h.geom = fbits(hv.w);
-    }
-#else
     {
         const float4 o4 = Q.org[pos], d4 = Q.dir[pos];
         uint32_t nv = 0, nt = 0;
         traverse8<false, false, true>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= set.MaxAnyHitPathLength, h, nv, nt);
     }
-#endif
     // the rest of the path state comes back from the queue after the traversal (the radiance so far only
     // once the vertex is shaded: it is not live across path_vertex)
     const float4 o4 = Q.org[pos], d4 = Q.dir[pos], t4 = Q.thr[pos];
@@ -1680,47 +1632,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     rad.x += V.pathThr.x * O.local.x;
     rad.y += V.pathThr.y * O.local.y;
     rad.z += V.pathThr.z * O.local.z;
-#if DXRPT_TAIL_SHADOW
-    // the vertex's shadow rays go to k_path_tail_shadow: paths with any are queued (their partial sum, where
-    // it ends up and the slot index of their rays), the others finish here
-    const bool has = nsh > 0u;
-    const uint32_t ppos = queue_append(A.F.counters + (2u * kMaxDepthQueues + uint32_t(d)) * kQueueShards, A.F.cap_r, has,
-                                       uint32_t((uint64_t(j) * kQueueShards) / nw));
-    if (has) {
-        A.F.pend[ppos] = make_float4(rad.x, rad.y, rad.z, bitsf(cont ? qpos : accumIdx));
-        A.F.pend_meta[ppos] = make_uint2(i, nsh | (cont ? 0x100u : 0u) | (nextDiffuse ? 0x200u : 0u));
-    } else {
-        split_finish(A, d, cont, qpos, nextDiffuse, accumIdx, rad);
-    }
-#else
     vertex_shadows<false>(A, d, i, nsh, false, 0u, rad, nullptr);
     split_finish(A, d, cont, qpos, nextDiffuse, accumIdx, rad);
-#endif
 }
-
-#if DXRPT_TAIL_SHADOW
-// The shadow rays of depth d's tail vertices, one lane per queued vertex (only vertices that emitted any),
-// in slot order onto the vertex's partial sum -- the same additions as in k_path_tail -- then the sum goes
-// to the continuation's queue entry or the pixel.  Any-hit traversal only: its own, smaller register budget.
-template <int kOcc>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_path_tail_shadow(KArgs A, int d) {
-    const uint32_t* cnt = A.F.counters + (2u * kMaxDepthQueues + uint32_t(d)) * kQueueShards;
-    const uint32_t n = queue_total(cnt);
-    const uint32_t nw = (n + 63u) / 64u;
-    if (blockIdx.x >= nw) return;
-    const uint32_t j = A.P.xcd_chunk ? xcd_position(blockIdx.x, nw, A.P.xcd_chunk) : blockIdx.x;
-    lut_fill(A.S);
-    const uint32_t i = j * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
-    const uint2 m = A.F.pend_meta[pos];
-    const float4 p4 = A.F.pend[pos];
-    float4 rad = make_float4(p4.x, p4.y, p4.z, 0.0f);
-    vertex_shadows<false>(A, d, m.x, m.y & 0xFFu, false, 0u, rad, nullptr);
-    const uint32_t dest = fbits(p4.w);
-    split_finish(A, d, (m.y & 0x100u) != 0u, dest, (m.y & 0x200u) != 0u, dest, rad);
-}
-#endif
 
 // ---- lightmap baking (Baking.hlsl:336-465, BakeRayGen) -------------------------------------------
 // One thread per lightmap texel of the chunk [first, first + count): the surface map's world position
@@ -1840,15 +1754,9 @@ static void launch_split(const KArgs& A, uint32_t gm, size_t lds, hipStream_t s,
 #undef DXRPT_HEAD
     if (head_ev) (void)hipEventRecord(head_ev, s);
     for (int d = 2; d <= L - 1; ++d) {
-#if DXRPT_TAIL_TRACE
-        hipLaunchKernelGGL((k_path_tail_trace<DXRPT_TAIL_TRACE_OCC>), dim3(gm), dim3(kWave), lds, s, A, d);
-#endif
 #define DXRPT_TAIL(O) hipLaunchKernelGGL((k_path_tail<O>), dim3(gm), dim3(kWave), lds, s, A, d)
         DXRPT_OCC_SWITCH(fp.tail_occupancy, DXRPT_TAIL)
 #undef DXRPT_TAIL
-#if DXRPT_TAIL_SHADOW
-        hipLaunchKernelGGL((k_path_tail_shadow<DXRPT_TAIL_SHADOW_OCC>), dim3(gm), dim3(kWave), lds, s, A, d);
-#endif
     }
 }
 
