@@ -9,7 +9,10 @@ kernels on two internal slot streams).  Per kernel kind (k_path_head / k_path_ta
   - avg_ms: the kernel trace's average duration of the launches on the caller's stream (the queue of
     the census kernel), i.e. the frame-at-a-time launches, which bench.py's roofline times with HIP events;
     avg_ms_all: over every launch (overlapped launches share the GPU with the neighbour frame);
-  - per-launch counters of those launches.  l2_fabric_bytes_per_launch = FETCH_SIZE + WRITE_SIZE (KiB x 1024,
+  - per-launch counters of those launches;
+  - profiles/<round>_kernel_stats[_<config>].csv: rocprofv3's statistics columns over those caller-stream
+    launches only (the non-overlapped per-launch durations), <round>_kernel_stats_all[_<config>].csv:
+    rocprofv3's own statistics over every launch, <round>_kernel_trace[_<config>].csv: the raw trace.  l2_fabric_bytes_per_launch = FETCH_SIZE + WRITE_SIZE (KiB x 1024,
     RAW: no x2 read correction -- MI355X_MICROARCH.md calibrates that on 16-B/lane streaming reads only, and
     these are scattered gathers): L2 -> fabric traffic, Infinity-Cache hits included, so not HBM bytes.
 usage: PMC_CONFIG_TAG=<config> PMC_CONFIG="<scene>-proxy WxH L=n" scripts/pmc_summary.py gpurun_out/prof_<config> <round>
@@ -48,6 +51,22 @@ def census_queue(rows, qcol):
         if k and k.startswith("k_path<") and kind(k) is None:
             return r[qcol]
     return None
+
+
+def write_stats(rows, q0, path):
+    """rocprofv3's kernel-stats columns over the launches on queue q0 (the caller's stream)."""
+    import statistics
+    per = defaultdict(list)
+    for r in rows:
+        if r["Queue_Id"] == q0:
+            per[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    total = sum(sum(v) for v in per.values()) or 1
+    with open(path, "w") as g:
+        g.write('"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev","Launches"\n')
+        for name, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
+            sd = statistics.pstdev(v) if len(v) > 1 else 0.0
+            g.write(f'"{name}",{len(v)},{sum(v)},{sum(v) / len(v):.6f},{100.0 * sum(v) / total:.4g},{min(v)},{max(v)},{sd:.6f},'
+                    f'"caller stream"\n')
 
 
 def main(prof, rnd):
@@ -114,7 +133,13 @@ def main(prof, rnd):
            "kernels_by_kind": by_kind}
     with open(f"profiles/{rnd}_launch_{TAG}.json", "w") as f:
         json.dump(out, f, indent=2)
-    with open(os.path.join(prof, "kt", "run_kernel_stats.csv")) as f, open(f"profiles/{rnd}_kernel_stats{sfx}.csv", "w") as g:
+    # kernel statistics of the frame-at-a-time (caller-stream) launches only -- the per-launch durations
+    # the roofline uses; rocprofv3's own statistics over every launch (overlapped ones included) beside
+    # them, and the raw trace for recomputation
+    write_stats(rows, q0, f"profiles/{rnd}_kernel_stats{sfx}.csv")
+    with open(os.path.join(prof, "kt", "run_kernel_stats.csv")) as f, open(f"profiles/{rnd}_kernel_stats_all{sfx}.csv", "w") as g:
+        g.write(f.read())
+    with open(os.path.join(prof, "kt", "run_kernel_trace.csv")) as f, open(f"profiles/{rnd}_kernel_trace{sfx}.csv", "w") as g:
         g.write(f.read())
     for kd, s in sorted(by_kind.items()):
         print(f"{TAG:7s} {kd:12s} {','.join(s['kernels']):28s} launches {s['calls']:4d} avg {s['avg_ms'] or 0:8.4f} ms "

@@ -10,3 +10,5 @@ for c in ${CONFIGS:-metric c3 c5}; do
   CONFIG=$c STEPS=${STEPS:-24} bash scripts/profile.sh > gpurun_out/profile_$c.log 2>&1 || { echo "profile $c failed"; tail -5 gpurun_out/profile_$c.log; exit 1; }
   PMC_CONFIG_TAG=$c PMC_CONFIG="$cfg" python3 scripts/pmc_summary.py gpurun_out/prof_$c $RND || exit 1
 done
+# only gpurun_out/ comes back from the GPU box: the summaries travel with it
+mkdir -p gpurun_out/profiles && cp profiles/${RND}_launch_* profiles/${RND}_kernel_* gpurun_out/profiles/
