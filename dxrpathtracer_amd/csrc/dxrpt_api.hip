@@ -102,7 +102,6 @@ struct dxrpt_ctx {
     // per-frame buffers of work on the caller's stream (wavefront passes, non-overlapped megakernel frames)
     DevBuf f_pix, f_pxrad, f_hit, f_fwd, f_shn, f_shq, f_shorg, f_shdir, f_shcon, f_counters;
     DevBuf f_q[2][5];  // RayQueue org, dir, thr, rad, pix per depth parity
-    DevBuf f_thit;     // FrameBuffers::thit
     FrameBuffers fb;
     uint32_t ctr_set = 0;                 // counter set of the next frame (f_counters holds two)
     bool ctr_clean[2] = {false, false};   // set known to be zero (zeroed by the previous megakernel frame)
@@ -135,7 +134,7 @@ struct dxrpt_ctx {
     // stage and BVH8 stack-spill slab -- and stages its radiance (d_stage); the caller's stream blends the
     // stage once the frame is done, so frame f+1's waves start while frame f drains
     struct Slot {
-        DevBuf q[2][5], shorg, shdir, shcon, thit, counters, stage;
+        DevBuf q[2][5], shorg, shdir, shcon, counters, stage;
         FrameBuffers fb;
         uint32_t ctr_set = 0;
         bool ctr_clean[2] = {false, false};
@@ -196,7 +195,7 @@ struct dxrpt_ctx {
         if (aux) (void)hipStreamSynchronize(aux);
         DevBuf* all[] = {&d_texels, &d_sky, &d_lut, &d_geoshade, &d_nodes8, &d_tris, &d_tri_verts, &d_lights, &d_tiles,
                          &d_tile_prefix, &f_pix, &f_pxrad, &f_hit, &f_fwd, &f_shn, &f_shq, &f_shorg, &f_shdir, &f_shcon,
-                         &f_counters, &f_thit, &p_bloom0, &p_bloom1, &d_wclock, &d_omm, &d_trav, &d_spill, &d_bake_list,
+                         &f_counters, &p_bloom0, &p_bloom1, &d_wclock, &d_omm, &d_trav, &d_spill, &d_bake_list,
                          &d_wave_cost, &d_wave_order, &d_wave_hist};
         for (DevBuf* b : all) b->release();
         for (auto& qb : f_q)
@@ -211,7 +210,6 @@ struct dxrpt_ctx {
             P.shorg.release();
             P.shdir.release();
             P.shcon.release();
-            P.thit.release();
             P.counters.release();
             P.stage.release();
             if (P.stream) (void)hipStreamDestroy(P.stream);
@@ -405,8 +403,8 @@ bool frame_fits(const FrameBuffers& f, uint32_t paths, uint32_t slots) {
 
 // Queue + shadow-slot buffers of `f` for `paths` paths and `slots` shadow slots (grown, never shrunk).
 // q: the two RayQueue parities; sh*: the shadow slots.
-void alloc_frame(FrameBuffers& f, DevBuf (&q)[2][5], DevBuf& shorg, DevBuf& shdir, DevBuf& shcon, DevBuf& thit,
-                 uint32_t paths, uint32_t slots) {
+void alloc_frame(FrameBuffers& f, DevBuf (&q)[2][5], DevBuf& shorg, DevBuf& shdir, DevBuf& shcon, uint32_t paths,
+                 uint32_t slots) {
     const uint32_t cap = std::max(paths, f.capacity);
     const uint32_t sl = std::max(slots, std::max(f.shadow_slots, 2u));
     const uint32_t cap_r = queue_shard_capacity(cap);
@@ -427,8 +425,6 @@ void alloc_frame(FrameBuffers& f, DevBuf (&q)[2][5], DevBuf& shorg, DevBuf& shdi
     f.sh_org = shorg.as<float4>();
     f.sh_dir = shdir.as<float4>();
     f.sh_con = shcon.as<float4>();
-    thit.ensure(qsize * 16);
-    f.thit = thit.as<float4>();
     f.capacity = cap;
     f.cap_r = cap_r;
     f.qsize = uint32_t(qsize);
@@ -440,7 +436,7 @@ void ensure_frame(dxrpt_ctx* c, uint32_t paths, uint32_t slots) {
     FrameBuffers& f = c->fb;
     if (frame_fits(f, paths, slots)) return;
     drain_frames(c);
-    alloc_frame(f, c->f_q, c->f_shorg, c->f_shdir, c->f_shcon, c->f_thit, paths, slots);
+    alloc_frame(f, c->f_q, c->f_shorg, c->f_shdir, c->f_shcon, paths, slots);
     const size_t qsize = f.qsize, sl = f.shadow_slots;
     c->f_pix.ensure(size_t(f.capacity) * 8);
     c->f_pxrad.ensure(size_t(f.capacity) * 16);
@@ -476,7 +472,7 @@ void ensure_slot(dxrpt_ctx* c, uint32_t k, uint32_t paths, uint32_t slots, size_
     if (fits) return;
     drain_frames(c);
     if (!frame_fits(P.fb, paths, slots)) {
-        alloc_frame(P.fb, P.q, P.shorg, P.shdir, P.shcon, P.thit, paths, slots);
+        alloc_frame(P.fb, P.q, P.shorg, P.shdir, P.shcon, paths, slots);
         if (!P.counters.p) {
             P.counters.ensure(2 * kCounterWords * sizeof(uint32_t));
             P.ctr_clean[0] = P.ctr_clean[1] = false;

@@ -63,7 +63,6 @@ struct FrameBuffers {
     float4* sh_org = nullptr;
     float4* sh_dir = nullptr;
     float4* sh_con = nullptr;
-    float4* thit = nullptr;        // split tails with DXRPT_TAIL_POOL: closest hit per dense tail index (hit[] layout)
     uint32_t* counters = nullptr;  // [queue][shard]: 2 * kMaxDepthQueues * kQueueShards
     // megakernel frames: the other counter set of the ping-pong pair (the next frame's), zeroed by the
     // frame's first kernel's workgroup 0 -- so the next frame needs no fill launch (null: nothing to zero)

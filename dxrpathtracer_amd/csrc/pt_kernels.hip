@@ -33,15 +33,6 @@
 #include "pt_kernels.h"
 #include "pt_math.h"
 
-// DXRPT_TAIL_POOL K (0: off): the depth-split tails trace their closest hits with lane refill over K
-// chunks of 64 paths per wave (k_path_tail); refill once DXRPT_TAIL_POOL_REFILL lanes are idle.
-#ifndef DXRPT_TAIL_POOL
-#define DXRPT_TAIL_POOL 0
-#endif
-#ifndef DXRPT_TAIL_POOL_REFILL
-#define DXRPT_TAIL_POOL_REFILL 16
-#endif
-
 namespace dxrpt {
 
 constexpr int kBlock = 256;                   // streaming kernels (raygen, shade, resolve, accumulate)
@@ -1590,12 +1581,29 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     split_finish(A, 1, cont, qpos, nextDiffuse, pr.accumIdx, rad);
 }
 
-// Depth d's vertex of the path at dense queue index i (< n) whose closest hit is h: shading, the
-// continuation into queue d + 1 (producer chunk j of nw), the vertex's shadow rays, the radiance sum.
-PT_DEV void tail_vertex(const KArgs& A, int d, const uint32_t* cnt, uint32_t i, uint32_t pos, uint32_t j, uint32_t nw,
-                        const HitRec& h) {
+// Depth d of the paths queued for it (one per lane); waves past the queued count exit at once (the grid
+// covers every path of the frame).
+template <int kOcc>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_path_tail(KArgs A, int d) {
+    const uint32_t* cnt = A.F.counters + uint32_t(d) * kQueueShards;
+    const uint32_t n = queue_total(cnt);
+    const uint32_t nw = (n + 63u) / 64u;  // waves with work
+    // wave j of the queue: XCD runs of A.P.xcd_chunk consecutive queue chunks among the nw live waves
+    // (workgroup b runs on XCD b mod 8; the grid's surplus workgroups exit at once)
+    if (blockIdx.x >= nw) return;
+    const uint32_t j = A.P.xcd_chunk ? xcd_position(blockIdx.x, nw, A.P.xcd_chunk) : blockIdx.x;
+    lut_fill(A.S);
+    const uint32_t i = j * blockDim.x + threadIdx.x;
+    if (i >= n) return;
     const dxrpt_app_settings& set = A.P.set;
+    const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
     const RayQueue& Q = A.F.q[d & 1];
+    HitRec h;
+    {
+        const float4 o4 = Q.org[pos], d4 = Q.dir[pos];
+        uint32_t nv = 0, nt = 0;
+        traverse8<false, false, true>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= set.MaxAnyHitPathLength, h, nv, nt);
+    }
     // the rest of the path state comes back from the queue after the traversal (the radiance so far only
     // once the vertex is shaded: it is not live across path_vertex)
     const float4 o4 = Q.org[pos], d4 = Q.dir[pos], t4 = Q.thr[pos];
@@ -1626,109 +1634,6 @@ PT_DEV void tail_vertex(const KArgs& A, int d, const uint32_t* cnt, uint32_t i, 
     rad.z += V.pathThr.z * O.local.z;
     vertex_shadows<false>(A, d, i, nsh, false, 0u, rad, nullptr);
     split_finish(A, d, cont, qpos, nextDiffuse, accumIdx, rad);
-}
-
-#if DXRPT_TAIL_POOL
-// Closest hits of queue items [begin, end) of depth d into thit[item], with lane refill (Aila & Laine
-// 2009, "replacing terminated rays"): every lane advances its ray by one node visit (and that node's leaf
-// triangles) per iteration, and lanes whose ray finished take the next items once at least
-// DXRPT_TAIL_POOL_REFILL lanes are idle -- the wave's traversal time follows its pool's total work
-// instead of each 64-ray chunk's slowest ray.  Refilled items are consecutive and ascend with the lane
-// id, as queue_pos requires.
-PT_DEV void tail_pool_trace(const KArgs& A, int d, const uint32_t* cnt, uint32_t begin, uint32_t end) {
-    const RayQueue& Q = A.F.q[d & 1];
-    const bool alpha = d <= A.P.set.MaxAnyHitPathLength;
-    const unsigned long long lt = (1ull << __lane_id()) - 1ull;
-    uint32_t next = begin, item = 0, node = 0;
-    bool active = false;
-    int sp = 0;
-    uint2 tos = make_uint2(0u, 0u);
-    Ray8 R;
-    HitRec h;
-    while (true) {
-        const unsigned long long idle = __ballot(!active);
-        const uint32_t nidle = uint32_t(__popcll(idle));
-        if (next < end && nidle >= uint32_t(DXRPT_TAIL_POOL_REFILL)) {
-            if (!active) {
-                const uint32_t k = next + uint32_t(__popcll(idle & lt));
-                if (k < end) {
-                    const uint32_t pos = queue_pos(cnt, A.F.cap_r, k);
-                    const float4 o4 = Q.org[pos], d4 = Q.dir[pos];
-                    ray8_init(R, ld3(o4), ld3(d4), kRayTMin, o4.w, alpha, h);
-                    node = 0;
-                    sp = 0;
-                    item = k;
-                    active = true;
-                }
-            }
-            next += nidle;
-        }
-        if (__ballot(active) == 0ull) break;  // every lane idle: nidle = 64 refilled them unless next >= end
-        if (active) {
-            uint32_t tbase = 0, tbits = 0, nv = 0, nt = 0;
-            const bool more = trav8_node<false>(A.S, R, load_node8(A.S, node), node, sp, tos, h, tbase, tbits, nv);
-            if (tbits) trav8_tris2<false, false>(A.S, R, tbase, tbits, h, nt);
-            if (!more) {
-                A.F.thit[item] = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
-                active = false;
-            }
-        }
-    }
-}
-#endif
-
-// Depth d of the paths queued for it (one per lane); waves past the queued count exit at once (the grid
-// covers every path of the frame).  DXRPT_TAIL_POOL K: each wave owns K consecutive 64-path chunks,
-// traces their closest hits with lane refill (tail_pool_trace), then shades them chunk by chunk.
-template <int kOcc>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_path_tail(KArgs A, int d) {
-    const uint32_t* cnt = A.F.counters + uint32_t(d) * kQueueShards;
-    const uint32_t n = queue_total(cnt);
-    const uint32_t nw = (n + 63u) / 64u;  // 64-path chunks with work
-#if DXRPT_TAIL_POOL
-    constexpr uint32_t K = DXRPT_TAIL_POOL;
-    const uint32_t nwp = (nw + K - 1u) / K;  // waves with work
-    if (blockIdx.x >= nwp) return;
-    const uint32_t xc = A.P.xcd_chunk / K > 0u ? A.P.xcd_chunk / K : 1u;
-    const uint32_t wp = A.P.xcd_chunk ? xcd_position(blockIdx.x, nwp, xc) : blockIdx.x;
-    lut_fill(A.S);
-    const uint32_t begin = wp * K * 64u;
-    tail_pool_trace(A, d, cnt, begin, min(n, begin + K * 64u));
-    __threadfence_block();  // the hits written by other lanes of this wave
-    for (uint32_t c = 0; c < K; ++c) {
-        const uint32_t j = wp * K + c;
-        if (j >= nw) break;
-        const uint32_t i = j * 64u + threadIdx.x;
-        if (i < n) {
-            const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
-            const float4 hv = A.F.thit[i];
-            HitRec h;
-            h.t = 0.0f;
-            h.b1 = hv.x;
-            h.b2 = hv.y;
-            h.tri = fbits(hv.z);
-            h.geom = fbits(hv.w);
-            tail_vertex(A, d, cnt, i, pos, j, nw, h);
-        }
-    }
-#else
-    // wave j of the queue: XCD runs of A.P.xcd_chunk consecutive queue chunks among the nw live waves
-    // (workgroup b runs on XCD b mod 8; the grid's surplus workgroups exit at once)
-    if (blockIdx.x >= nw) return;
-    const uint32_t j = A.P.xcd_chunk ? xcd_position(blockIdx.x, nw, A.P.xcd_chunk) : blockIdx.x;
-    lut_fill(A.S);
-    const uint32_t i = j * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
-    HitRec h;
-    {
-        const RayQueue& Q = A.F.q[d & 1];
-        const float4 o4 = Q.org[pos], d4 = Q.dir[pos];
-        uint32_t nv = 0, nt = 0;
-        traverse8<false, false, true>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= A.P.set.MaxAnyHitPathLength, h, nv, nt);
-    }
-    tail_vertex(A, d, cnt, i, pos, j, nw, h);
-#endif
 }
 
 // ---- lightmap baking (Baking.hlsl:336-465, BakeRayGen) -------------------------------------------
