@@ -877,16 +877,23 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info) {
 }
 
 // The call's tile list (NULL: the full frame) validated and uploaded with its pixel prefix sums (only when it
-// changed); returns the number of paths (pixels).
+// changed); returns the number of paths (pixels).  Tiles of zero area are valid and dropped; a list with no
+// pixels at all returns 0 before touching the device (the caller then enqueues nothing).
 uint32_t prepare_tiles(dxrpt_ctx* ctx, const dxrpt_tile* tiles, uint32_t num_tiles, uint32_t width, uint32_t height,
                        const char* who) {
     std::vector<dxrpt_tile> tl;
-    if (!tiles || num_tiles == 0) {
+    if (!tiles) {
         dxrpt_tile t{};
         t.x0 = 0; t.y0 = 0; t.w = width; t.h = height; t.accum_offset = 0; t.accum_pitch = width;
         tl.push_back(t);
     } else {
-        tl.assign(tiles, tiles + num_tiles);
+        for (uint32_t k = 0; k < num_tiles; ++k) {
+            const dxrpt_tile& t = tiles[k];
+            require(uint64_t(t.x0) + t.w <= width && uint64_t(t.y0) + t.h <= height,
+                    std::string(who) + ": tile " + std::to_string(k) + " outside the image");
+            if (t.w > 0 && t.h > 0) tl.push_back(t);
+        }
+        if (tl.empty()) return 0u;
     }
     std::vector<uint32_t> prefix(tl.size() + 1, 0);
     uint64_t total = 0;
@@ -928,6 +935,7 @@ int dxrpt_render_aov(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const
         enter_stream(ctx, s);
         upload_textures(ctx);
         const uint32_t paths = prepare_tiles(ctx, tiles, num_tiles, width, height, "dxrpt_render_aov");
+        if (paths == 0u) return;  // a tile list without pixels: nothing to do
         ensure_spill(ctx, frame_traversal_threads(paths, 1u, true));
         FrameParams fp{};
         fp.rtc = *rtc;
@@ -971,6 +979,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         enter_stream(ctx, s);
         upload_textures(ctx);
         const uint32_t paths = prepare_tiles(ctx, tiles, num_tiles, width, height, "dxrpt_render");
+        if (paths == 0u) return;  // a tile list without pixels (e.g. a rank of a tiny frame): nothing to do
         const uint32_t nl = useLights ? rtc->NumLights : 0u;
         if (nl) {
             std::vector<dxrpt_spot_light> L(lights->Lights, lights->Lights + nl);

@@ -102,9 +102,9 @@ class DXRPathTracer:
         if isinstance(tiles, C.Array):
             # a ctypes Tile array built once by the caller (BandLayout.tile_array: an N-GPU block partition
             # has thousands of tiles, marshalling them every frame would starve the GPU)
-            tarr, nt = tiles, len(tiles)
-        elif tiles:  # a list of Tile / tuples: marshalled on every call, so later edits to it are seen
-            tarr = (A.Tile * len(tiles))()
+            tarr, nt = (tiles if len(tiles) else (A.Tile * 1)()), len(tiles)
+        elif tiles is not None:  # a list of Tile / tuples: marshalled on every call, so later edits to it are seen
+            tarr = (A.Tile * max(1, len(tiles)))()  # an empty list: a non-null array of 0 tiles (no pixels)
             for i, t in enumerate(tiles):
                 tarr[i] = t if isinstance(t, A.Tile) else A.Tile(*t)
             nt = len(tiles)
@@ -116,8 +116,9 @@ class DXRPathTracer:
                    tiles=None, stream: int = 0):
         """Primary-only AOV (dxrpt_render_aov): (albedo rgb, 1) at each pixel's primary hit, 0 on a miss."""
         tarr, nt = None, 0
-        if tiles:
-            tarr = tiles if isinstance(tiles, C.Array) else (A.Tile * len(tiles))(*[t if isinstance(t, A.Tile) else A.Tile(*t) for t in tiles])
+        if tiles is not None:
+            tarr = tiles if isinstance(tiles, C.Array) and len(tiles) else \
+                (A.Tile * max(1, len(tiles)))(*[t if isinstance(t, A.Tile) else A.Tile(*t) for t in tiles])
             nt = len(tiles)
         self._check(self._L.dxrpt_render_aov(self._ctx, C.byref(rtc), C.byref(settings), C.c_void_p(out_ptr), width,
                                              height, tarr, nt, C.c_void_p(stream)), "dxrpt_render_aov")

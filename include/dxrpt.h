@@ -375,7 +375,11 @@ int dxrpt_reset_timing(dxrpt_ctx* ctx);
 /* ---- the hot path ----------------------------------------------------------------------------- */
 /* One sample per pixel for every pixel of `tiles` (one DispatchRays(W,H,1)), progressively
  * accumulated into `accum` (device float4): accum = lerp(new, accum, s/(s+1)), s = CurrSampleIdx
- * (RayTrace.hlsl:140-148).  rtc->TotalNumPixels must equal W*H.  `stream` is a hipStream_t. */
+ * (RayTrace.hlsl:140-148).  rtc->TotalNumPixels must equal W*H.  `stream` is a hipStream_t.
+ * `tiles` NULL: the full W x H frame into accum[y*W + x].  Otherwise tile k's pixel (lx, ly) is image pixel
+ * (x0 + lx, y0 + ly) accumulated at accum[accum_offset + ly*accum_pitch + lx]; tiles must lie inside
+ * the image; zero-area tiles are skipped, and a list without pixels (num_tiles 0, e.g. a rank of an
+ * N-GPU partition that holds no band) returns DXRPT_OK and enqueues nothing. */
 int dxrpt_render(dxrpt_ctx* ctx,
                  const dxrpt_ray_trace_constants* rtc,
                  const dxrpt_app_settings* settings,
