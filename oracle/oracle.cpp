@@ -981,6 +981,23 @@ void oracle_cosine_hemisphere(const float* uv, uint32_t n, float* out) {
 void oracle_ggx_v1(const float* m2_ndotx, uint32_t n, float* out) {
     for (uint32_t i = 0; i < n; ++i) out[i] = GGXV1(m2_ndotx[2 * i], m2_ndotx[2 * i + 1]);
 }
+// in: n x (specAlbedo xyz, h xyz, l xyz); out: n x rgb
+void oracle_fresnel(const float* in, uint32_t n, float* out) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const float* a = in + 9 * i;
+        const F3 f = Fresnel(F3{a[0], a[1], a[2]}, F3{a[3], a[4], a[5]}, F3{a[6], a[7], a[8]});
+        out[3 * i] = f.x;
+        out[3 * i + 1] = f.y;
+        out[3 * i + 2] = f.z;
+    }
+}
+// in: n x (m, n xyz, h xyz, v xyz, l xyz); out: n
+void oracle_ggx_specular(const float* in, uint32_t n, float* out) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const float* a = in + 13 * i;
+        out[i] = GGXSpecular(a[0], F3{a[1], a[2], a[3]}, F3{a[4], a[5], a[6]}, F3{a[7], a[8], a[9]}, F3{a[10], a[11], a[12]});
+    }
+}
 
 oracle_scene* oracle_scene_create(const oracle_vertex* vertices, uint32_t num_vertices, const void* indices, uint32_t idx_bytes,
                                   uint32_t num_indices, const oracle_geometry_info* geometries, uint32_t num_geometries,

@@ -49,6 +49,8 @@ void oracle_sincos(float x, float out[2]);
 void oracle_concentric_disk(const float* xy, uint32_t n, float* out);
 void oracle_cosine_hemisphere(const float* uv, uint32_t n, float* out);
 void oracle_ggx_v1(const float* m2_ndotx, uint32_t n, float* out);
+void oracle_fresnel(const float* in, uint32_t n, float* out);
+void oracle_ggx_specular(const float* in, uint32_t n, float* out);
 /* Arrays must outlive the scene (not copied), except indices which are widened into the scene. */
 oracle_scene* oracle_scene_create(const oracle_vertex* vertices, uint32_t num_vertices, const void* indices, uint32_t idx_bytes,
                                   uint32_t num_indices, const oracle_geometry_info* geometries, uint32_t num_geometries,

@@ -55,7 +55,8 @@ def lib() -> C.CDLL:
         L.oracle_bake.argtypes = [P, P, P, P, P, P] + [C.c_uint32] * 4 + [P, P, C.c_uint32, C.POINTER(OracleStats)]
         L.oracle_median3x3.argtypes = [P, P, C.c_uint32, C.c_uint32]
         L.oracle_median3x3.restype = None
-        for fn in ("oracle_concentric_disk", "oracle_cosine_hemisphere", "oracle_ggx_v1"):
+        for fn in ("oracle_concentric_disk", "oracle_cosine_hemisphere", "oracle_ggx_v1", "oracle_fresnel",
+                   "oracle_ggx_specular"):
             getattr(L, fn).argtypes = [P, C.c_uint32, P]
             getattr(L, fn).restype = None
         _lib = L
@@ -74,9 +75,9 @@ def sincos(x: float) -> tuple[float, float]:
     return out[0], out[1]
 
 
-def _batched(fn: str, pairs, width: int):
+def _batched(fn: str, pairs, width: int, arity: int = 2):
     import numpy as np
-    a = np.ascontiguousarray(pairs, dtype=np.float32).reshape(-1, 2)
+    a = np.ascontiguousarray(pairs, dtype=np.float32).reshape(-1, arity)
     out = np.zeros((a.shape[0], width), dtype=np.float32)
     getattr(lib(), fn)(a.ctypes.data, a.shape[0], out.ctypes.data)
     return out
@@ -95,6 +96,16 @@ def cosine_hemisphere(uv):
 def ggx_v1(m2_ndotx):
     """GGX_V1 (BRDF.hlsl:89-92) on an (n, 2) array of (m2, nDotX) -> (n,) float32."""
     return _batched("oracle_ggx_v1", m2_ndotx, 1)[:, 0]
+
+
+def fresnel(args):
+    """Fresnel (BRDF.hlsl:16-24) on an (n, 9) array of (specAlbedo, h, l) -> (n, 3) float32."""
+    return _batched("oracle_fresnel", args, 3, 9)
+
+
+def ggx_specular(args):
+    """GGXSpecular (BRDF.hlsl:128-145) on an (n, 13) array of (m, n, h, v, l) -> (n,) float32."""
+    return _batched("oracle_ggx_specular", args, 1, 13)[:, 0]
 
 
 class OracleScene:

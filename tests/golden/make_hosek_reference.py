@@ -17,7 +17,8 @@ Compiled with g++ into oracle/_ref/hosek/ (git-ignored), from the reference chec
                            members declared as plain variables.
 Added text (types only, plus the one absent third-party dependency):
   * the SF12 struct layouts (Float2, Float3, Float3x3 -- SF12_Math.h also pulls in DirectXMath and Windows
-    headers, so it is not compiled itself) and the standard headers PCH.h would bring;
+    headers, so it is not compiled itself) and the standard headers PCH.h would bring (with <math.h>, so an
+    unqualified sqrt(float) resolves to the float overload as under MSVC's <cmath>);
   * DirectXMath (Windows SDK; not in the checkout) behind Float3::Dot / Cross / Normalize / Transform(Float3x3),
     restated from its published SSE2 paths: XMVector3Dot = (x*x' + y*y') + z*z'; XMVector3Cross = products then
     differences; XMVector3Normalize = v / sqrt(dot); XMVector3TransformCoord with a 3x3 (r3 = (0,0,0,1)) =
@@ -100,7 +101,7 @@ def sources():
     typedefs = "\n".join(re.findall(r"^typedef \w+ \w+;$", pch, re.M))
     write(os.path.join(INC, "PCH.h"), "#pragma once\n#include <cmath>\n#include <cstdint>\n#include <cstdio>\n#include <cstdlib>\n"
           "#include <cstring>\n#include <limits>\n#include <vector>\n#include <algorithm>\n#include <ostream>\n#include <utility>\n"
-          "#include <stdint.h>\n#include <wchar.h>\n// ---- PCH.h, verbatim ----\n" + typedefs + "\n")
+          "#include <stdint.h>\n#include <wchar.h>\n#include <math.h>\n// ---- PCH.h, verbatim ----\n" + typedefs + "\n")
     write(os.path.join(INC, "..\\\\Assert.h"), "#pragma once\n// ---- Assert.h, verbatim (release: Assert_ is empty) ----\n" +
           between(assert_h, "#ifdef _DEBUG", "#define StaticAssertMsg_(x, msg)\n#endif") + "\n")
     # SF12_Math.h: types only, then its constants and scalar templates verbatim

@@ -223,3 +223,34 @@ def test_sampling_matches_verbatim_reference_within_the_trig_bound():
     assert np.abs(hemi[:, :2] - ref[:, :2]).max() <= eps
     assert np.abs(hemi[:, 2] ** 2 - ref[:, 2] ** 2).max() <= 4 * eps
     assert (np.sign(hemi) == np.sign(ref))[:, :2].mean() > 0.999  # same quadrant (exact zeros aside)
+
+
+def _ulps(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Distance in float32 units in the last place (same-sign finite values)."""
+    return np.abs(a.view(np.int32).astype(np.int64) - b.view(np.int32).astype(np.int64))
+
+
+def test_fresnel_matches_reference_cpp():
+    # Fresnel (Graphics/BRDF.h:17-26, statement-identical to BRDF.hlsl:16-24, the one CalcLighting calls) compiled
+    # verbatim on 4,096 (specAlbedo, h, l) triples -- an eighth of them below the 0.1 % albedo fade, exact 0 and 1
+    # albedos among them.  With std::pow(x, 5) as the (x*x)*(x*x)*x the kernels and the oracle define HLSL's
+    # pow(x, 5) to be (build "det"): bit-exact.  Against glibc's powf (build "libm"): within 2 ulp.
+    from oracle import pyoracle as O
+    g = _sampling_golden()
+    ours = O.fresnel(g["fresnel_in"])
+    np.testing.assert_array_equal(ours.view(np.uint32), g["fresnel_det"])
+    assert _ulps(ours, g["fresnel_libm"].view(np.float32)).max() <= 2
+
+
+def test_ggx_specular_matches_reference_cpp_within_its_association():
+    # GGX_Specular (Graphics/BRDF.h:59-77) against the oracle's GGXSpecular (BRDF.hlsl:128-145) on 4,096
+    # (m, n, h = normalize(v + l), v, l) inputs: the two texts differ in one association -- the C++ divides by
+    # Pi * Square(x), the HLSL by (Pi * x) * x -- so the bound is stated, not equality: 3 ulp (1 ulp of the
+    # product's rounding through the division and the two GGX_V1 factors), with no libm call involved.
+    from oracle import pyoracle as O
+    g = _sampling_golden()
+    ours = O.ggx_specular(g["ggx_spec_in"])
+    ref = g["ggx_spec_det"].view(np.float32)
+    np.testing.assert_array_equal(g["ggx_spec_det"], g["ggx_spec_libm"])  # no trig / pow on this path
+    assert _ulps(ours, ref).max() <= 3
+    assert (_ulps(ours, ref) == 0).mean() > 0.8
