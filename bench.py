@@ -410,7 +410,7 @@ def main():
     achieved = d.get("achieved", 0.0)
     # what limits the kernel, from its counters: waves parked on s_waitcnt for much of their cycles with
     # HBM far from its peak = latency of dependent loads (the roofline is still priced against HBM)
-    bound = "latency" if (wait_frac is not None and wait_frac > 0.3 and achieved < 0.6 * HBM_PEAK_GBS) else "hbm"
+    limiter = "latency" if (wait_frac is not None and wait_frac > 0.3 and achieved < 0.6 * HBM_PEAK_GBS) else "hbm"
     frame_interval_ms = float(np.median(frame_ms))
 
     def r4(v):
@@ -440,7 +440,9 @@ def main():
                        "sqrt_num_samples": 4, "triangles": scene.num_triangles, "sky": sky.model,
                        "parallelism": (f"screen {args.layout} x{world} + RCCL gather ({gather_used})" if world > 1
                                        else "single GPU")},
-            "roofline": {"bound": bound, "roofline_kind": "hbm", "kernel": dominant,
+            # the roofline this kernel is priced against (no MFMA on this path); "limiter": what its counters
+            # say holds it below that roof
+            "roofline": {"bound": "hbm", "limiter": limiter, "kernel": dominant,
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": d.get("traffic"),
