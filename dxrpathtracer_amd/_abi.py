@@ -98,6 +98,7 @@ OPT_MEGAKERNEL_SPLIT = 33
 OPT_TAIL_OCCUPANCY = 34
 OPT_OPACITY_MICROMAP = 36
 OPT_FRAME_OVERLAP = 37
+OPT_TREELET_PASSES = 40
 RETIRED_OPTIONS = (3, 4, 5, 6, 7, 8, 9, 10, 11, 14, 15, 16, 17, 19, 21, 22, 26, 27, 30, 35, 38, 39)
 DXRPT_E_UNSUPPORTED = -6
 # context defaults (dxrpt_api.hip)

@@ -13,6 +13,9 @@
 #include <cfloat>
 #include <cmath>
 #include <cstring>
+#include <atomic>
+#include <functional>
+#include <thread>
 
 namespace dxrpt {
 namespace {
@@ -523,6 +526,207 @@ Box padded(const Box& bx, float pad_abs) {
     return o;
 }
 
+// ---- treelet restructuring (Karras & Aila 2013) ---------------------------------------------------------
+// Bottom-up, every internal node R roots a treelet: its two children, then repeatedly the treelet leaf of
+// largest surface area replaced by its two children, up to kTreeletLeaves leaves.  A dynamic programme over
+// the subsets of those leaves finds the binary topology of least SAH cost (C_node * area + the children's
+// costs; a treelet leaf keeps its subtree and its cost), and the treelet's internal nodes are rewired into
+// it when that is cheaper.  Leaves, their references and boxes are unchanged, so the tree is over the same
+// geometry and traversal results cannot change (the triangle tests alone decide hits); the tree is then
+// renumbered in depth-first order (children after parents, subtree references contiguous) for the
+// collapse.  Costs: C_node = 1, C_tri = 1 per reference, as the SBVH's split search.
+constexpr int kTreeletLeaves = 7;
+
+// Restructures the treelet rooted at internal node r (cost[] holds every node's subtree SAH cost, its
+// descendants' already final).  Touches only r's subtree.
+void restructure_treelet(std::vector<TNode>& tree, std::vector<double>& cost, int32_t r) {
+    constexpr int kMaxSub = 1 << kTreeletLeaves;
+    double area[kMaxSub], best[kMaxSub];
+    uint8_t split[kMaxSub];
+    int32_t leaves[kTreeletLeaves], internals[kTreeletLeaves];
+    int nl = 2, ni = 1;
+    leaves[0] = tree[size_t(r)].child[0];
+    leaves[1] = tree[size_t(r)].child[1];
+    internals[0] = r;
+    while (nl < kTreeletLeaves) {  // expand the treelet leaf of largest area
+        int bi = -1;
+        double ba = -1.0;
+        for (int i = 0; i < nl; ++i)
+            if (!tree[size_t(leaves[i])].count && tree[size_t(leaves[i])].box.area() > ba) {
+                ba = tree[size_t(leaves[i])].box.area();
+                bi = i;
+            }
+        if (bi < 0) break;
+        const int32_t x = leaves[bi];
+        internals[ni++] = x;
+        leaves[bi] = tree[size_t(x)].child[0];
+        leaves[nl++] = tree[size_t(x)].child[1];
+    }
+    if (nl < 3) return;  // two leaves have one topology
+    const int full = (1 << nl) - 1;
+    for (int sset = 1; sset <= full; ++sset) {
+        Box bx;
+        for (int i = 0; i < nl; ++i)
+            if (sset & (1 << i)) bx.grow(tree[size_t(leaves[i])].box);
+        area[sset] = bx.area();
+    }
+    for (int i = 0; i < nl; ++i) best[1 << i] = cost[size_t(leaves[i])];
+    // a proper subset of S is numerically smaller than S: increasing order is a valid DP order
+    for (int sset = 1; sset <= full; ++sset) {
+        if ((sset & (sset - 1)) == 0) continue;
+        const int low = sset & -sset;
+        double bc = DBL_MAX;
+        int bp = 0;
+        for (int p = (sset - 1) & sset; p; p = (p - 1) & sset) {  // partitions {P, S \ P} with S's lowest leaf in P
+            if (!(p & low)) continue;
+            const double c = best[p] + best[sset ^ p];
+            if (c < bc) {
+                bc = c;
+                bp = p;
+            }
+        }
+        best[sset] = area[sset] + bc;
+        split[sset] = uint8_t(bp);
+    }
+    if (!(best[full] < cost[size_t(r)] * (1.0 - 1e-9))) return;
+    // rewire: the new topology's internal nodes reuse the treelet's (r stays the root)
+    int next = 0;
+    std::function<int32_t(int)> build = [&](int sset) -> int32_t {
+        if ((sset & (sset - 1)) == 0) return leaves[__builtin_ctz(unsigned(sset))];
+        const int32_t idx = internals[next++];
+        const int p = split[sset];
+        const int32_t x = build(p), y = build(sset ^ p);
+        TNode& t = tree[size_t(idx)];
+        t.child[0] = x;
+        t.child[1] = y;
+        t.box = tree[size_t(x)].box;
+        t.box.grow(tree[size_t(y)].box);
+        cost[size_t(idx)] = best[sset];
+        return idx;
+    };
+    build(full);
+}
+
+void restructure_treelets(std::vector<TNode>& tree, std::vector<uint32_t>& refs, int passes, const uint8_t* alpha) {
+    const size_t nn = tree.size();
+    if (nn < 3) return;
+    std::vector<double> cost(nn, 0.0);
+    std::vector<uint32_t> depth(nn, 0);
+    std::vector<uint8_t> fixed(nn, 0);  // subtree holds an alpha-tested reference: left as built
+    // post-order of the subtree at `root`, internal nodes only
+    auto post_order = [&](int32_t root, std::vector<int32_t>& order) {
+        order.clear();
+        std::vector<std::pair<int32_t, bool>> st{{root, false}};
+        while (!st.empty()) {
+            auto [n, done] = st.back();
+            st.pop_back();
+            if (tree[size_t(n)].count) continue;
+            if (done) {
+                order.push_back(n);
+                continue;
+            }
+            st.push_back({n, true});
+            st.push_back({tree[size_t(n)].child[1], false});
+            st.push_back({tree[size_t(n)].child[0], false});
+        }
+    };
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    for (int pass = 0; pass < passes; ++pass) {
+        // costs bottom-up and depths top-down over the current topology
+        std::vector<int32_t> all;
+        post_order(0, all);
+        for (size_t i = 0; i < nn; ++i)
+            if (tree[i].count) {
+                cost[i] = tree[i].box.area() * double(tree[i].count);
+                fixed[i] = 0;
+                if (alpha)
+                    for (uint32_t k = 0; k < tree[i].count; ++k) fixed[i] |= alpha[refs[tree[i].first + k]];
+            }
+        for (int32_t n : all) {
+            const TNode& t = tree[size_t(n)];
+            cost[size_t(n)] = t.box.area() + cost[size_t(t.child[0])] + cost[size_t(t.child[1])];
+            fixed[size_t(n)] = fixed[size_t(t.child[0])] | fixed[size_t(t.child[1])];
+        }
+        for (auto it = all.rbegin(); it != all.rend(); ++it) {  // reverse post-order: parents first
+            const TNode& t = tree[size_t(*it)];
+            depth[size_t(t.child[0])] = depth[size_t(t.child[1])] = depth[size_t(*it)] + 1;
+        }
+        // disjoint subtrees at the cut depth are restructured in parallel, the levels above serially
+        constexpr uint32_t kCut = 7;
+        std::vector<int32_t> roots;
+        for (int32_t n : all)
+            if (depth[size_t(n)] == kCut) roots.push_back(n);
+        std::atomic<size_t> cursor{0};
+        auto worker = [&] {
+            std::vector<int32_t> order;
+            for (size_t k; (k = cursor.fetch_add(1)) < roots.size();) {
+                post_order(roots[k], order);
+                for (int32_t n : order)
+                    if (!fixed[size_t(n)]) restructure_treelet(tree, cost, n);
+            }
+        };
+        std::vector<std::thread> pool;
+        for (unsigned t = 1; t < hw; ++t) pool.emplace_back(worker);
+        worker();
+        for (std::thread& t : pool) t.join();
+        std::vector<int32_t> top;
+        post_order(0, top);
+        for (int32_t n : top)
+            if (depth[size_t(n)] < kCut && !fixed[size_t(n)]) restructure_treelet(tree, cost, n);
+    }
+    // depth-first renumbering: parents before children, each subtree's references contiguous
+    std::vector<TNode> out;
+    out.reserve(nn);
+    std::vector<uint32_t> rout;
+    rout.reserve(refs.size());
+    struct Item {
+        int32_t old;
+        int32_t slot;
+    };
+    out.emplace_back();
+    std::vector<Item> st{{0, 0}};
+    std::vector<std::pair<int32_t, int32_t>> fix;  // (new node, old node) of internal nodes, in pre-order
+    while (!st.empty()) {
+        const Item it = st.back();
+        st.pop_back();
+        const TNode& o = tree[size_t(it.old)];
+        TNode& t = out[size_t(it.slot)];
+        t.box = o.box;
+        if (o.count) {
+            t.first = uint32_t(rout.size());
+            t.count = o.count;
+            for (uint32_t i = 0; i < o.count; ++i) rout.push_back(refs[o.first + i]);
+            t.begin = t.first;
+            t.end = t.first + t.count;
+            continue;
+        }
+        const int32_t c0 = int32_t(out.size()), c1 = c0 + 1;
+        out.emplace_back();
+        out.emplace_back();
+        out[size_t(it.slot)].child[0] = c0;
+        out[size_t(it.slot)].child[1] = c1;
+        fix.push_back({it.slot, it.old});
+        st.push_back({o.child[1], c1});
+        st.push_back({o.child[0], c0});
+    }
+    // subtree reference ranges (children have larger indices: a reverse sweep is a post-order)
+    for (size_t i = out.size(); i-- > 0;) {
+        TNode& t = out[i];
+        if (t.count) continue;
+        t.begin = std::min(out[size_t(t.child[0])].begin, out[size_t(t.child[1])].begin);
+        t.end = std::max(out[size_t(t.child[0])].end, out[size_t(t.child[1])].end);
+    }
+    tree.swap(out);
+    refs.swap(rout);
+}
+
+double tree_sah(const std::vector<TNode>& tree) {
+    const double ra = std::max(tree[0].box.area(), 1e-30);
+    double sah = 0.0;
+    for (const TNode& t : tree) sah += t.box.area() / ra * (t.count ? double(t.count) : 1.0);
+    return sah;
+}
+
 // ---- BVH2 emission -------------------------------------------------------------------------------------
 struct Emit2 {
     const std::vector<TNode>& tree;
@@ -875,7 +1079,9 @@ bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildRe
             SB.depth_cap = cap;
             SB.ref_budget = size_t(double(ntris) * (params ? params->ref_budget : BvhBuildParams().ref_budget));
             if (!SB.build(ntris, B.tri_box, err)) return false;
-            sah = SB.sah;
+            const uint32_t tp = params ? params->treelet_passes : BvhBuildParams().treelet_passes;
+            if (tp > 0) restructure_treelets(SB.tree, SB.refs, int(tp), params ? params->keep_whole : nullptr);
+            sah = tp > 0 ? tree_sah(SB.tree) : SB.sah;
             tree = &SB.tree;
             refs = &SB.refs;
         } else {
@@ -892,6 +1098,7 @@ bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildRe
             return false;
         }
         out.sah_cost = sah;
+        out.wide_sah = (tree->front().box.area() + E.cost[0]) / tree->front().box.area();
         out.nodes8 = std::move(E.nodes);
         out.tri_order = std::move(E.tri_order);
         out.max_depth = E.max_depth;

@@ -20,6 +20,7 @@ struct BvhBuildResult {
     uint32_t max_depth = 0;           // of the emitted layout
     uint32_t num_leaves = 0;
     double sah_cost = 0.0;            // binary tree, C_trav = 1, C_tri = 1, relative to root area
+    double wide_sah = 0.0;            // BVH8: the collapse's cost (C_node = 1, C_tri = leaf_cost), relative to root area
     uint32_t binary_depth_cap = 0;    // BVH8: depth cap of the binary tree that was collapsed
 };
 
@@ -34,6 +35,13 @@ struct BvhBuildParams {
     // per global triangle, non-zero: never cut by a spatial split (an alpha-tested triangle: every extra
     // reference is another opacity test); null: every triangle may be split
     const uint8_t* keep_whole = nullptr;
+    // BVH8 with spatial splits: passes of treelet restructuring (Karras & Aila 2013) of the binary tree
+    // before the collapse (0: none; DXRPT_OPT_TREELET_PASSES).  r04: 1 pass -2.3 % metric, -1.4..-2.0 %
+    // C2/C3/C5, C4 +0.6 %; 2 passes C4 +6 % (profiles/r04_ab_treelet.txt)
+#ifndef DXRPT_TREELET_PASSES
+#define DXRPT_TREELET_PASSES 1
+#endif
+    uint32_t treelet_passes = DXRPT_TREELET_PASSES;
 };
 
 // tri_positions: ntris * 9 floats (v0.xyz, v1.xyz, v2.xyz) in global triangle order.

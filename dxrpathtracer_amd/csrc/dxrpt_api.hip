@@ -154,7 +154,7 @@ struct dxrpt_ctx {
     DevBuf d_omm;                           // kOmmWords per micromap slot (pt_layout.h kOmm*)
     std::vector<uint32_t> omm_tris;         // slot -> global triangle (alpha-tested geometry), set by the BVH build
     bool omm_dirty = true, omm_any = false; // any: some triangle has a verdict (else d_omm is not read)
-    BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST
+    BvhBuildParams build_params;    // DXRPT_OPT_SPATIAL_SPLITS, DXRPT_OPT_LEAF_COST, DXRPT_OPT_TREELET_PASSES
     DevBuf d_trav;   // kTravCounters x u64 census counters (DXRPT_OPT_COUNT_TRAVERSAL)
     DevBuf d_wclock;  // 2 x u64 per wave (DXRPT_OPT_WAVE_CLOCKS)
     bool opt_wave_clocks = false;
@@ -667,6 +667,9 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
                 ctx->ovl_parity = 0;
             }
             ctx->opt_overlap = uint32_t(value);
+        } else if (option == DXRPT_OPT_TREELET_PASSES) {
+            require(value <= 8, "dxrpt_set_option: treelet passes must be 0..8");
+            ctx->build_params.treelet_passes = uint32_t(value);
         } else if (option == DXRPT_OPT_OPACITY_MICROMAP) {
             require(value <= 1, "dxrpt_set_option: opacity micromap must be 0 (off) or 1 (on)");
             drain_frames(ctx);  // in-flight frames may read the micromap

@@ -39,13 +39,14 @@ V3 norm(V3 a) {
 
 struct Counters {
     std::vector<uint64_t> keys;  // optional per-ray sort keys (bounce rays)
-    uint64_t rays = 0, nodes = 0, tris = 0, hits = 0;
+    uint64_t rays = 0, nodes = 0, tris = 0, hits = 0, alpha_tris = 0;
     uint64_t stack_hist[40] = {};  // rays by maximum stack occupancy
     std::vector<std::vector<uint8_t>> seqs;  // per ray: triangles tested at each node visit, in order
 };
 
 struct Scene {
     std::vector<float> pos;  // ntris * 9
+    std::vector<uint8_t> alpha;  // per triangle: alpha-tested material (kept whole by the builder)
     uint32_t ntris = 0;
 };
 
@@ -120,6 +121,7 @@ float trace8(const Scene& S, const BvhBuildResult& B, V3 o, V3 d, float tmin, fl
             thits &= thits - 1;
             c.tris++;
             uint32_t t = B.tri_order[n.base_tri + bit];
+            c.alpha_tris += S.alpha[t];
             float tt = hit_tri(S, t, o, d, tmin, best);
             if (tt >= 0.0f) {
                 best = tt;
@@ -265,8 +267,9 @@ void simulate_all(const char* name, const Counters& c) {
 }
 
 void report(const char* name, const Counters& c) {
-    printf("  %-9s rays %8llu  nodes/ray %6.2f  tris/ray %6.2f  hit %5.1f%%  stack>4 %.3f%% >6 %.4f%% >8 %.5f%% max ",
-           name, (unsigned long long)c.rays, double(c.nodes) / c.rays, double(c.tris) / c.rays, 100.0 * c.hits / c.rays,
+    printf("  %-9s rays %8llu  nodes/ray %6.2f  tris/ray %6.2f (alpha %5.2f)  hit %5.1f%%  stack>4 %.3f%% >6 %.4f%% >8 %.5f%% max ",
+           name, (unsigned long long)c.rays, double(c.nodes) / c.rays, double(c.tris) / c.rays, double(c.alpha_tris) / c.rays,
+           100.0 * c.hits / c.rays,
            [&] { uint64_t n = 0; for (int i = 5; i < 40; ++i) n += c.stack_hist[i]; return 100.0 * n / c.rays; }(),
            [&] { uint64_t n = 0; for (int i = 7; i < 40; ++i) n += c.stack_hist[i]; return 100.0 * n / c.rays; }(),
            [&] { uint64_t n = 0; for (int i = 9; i < 40; ++i) n += c.stack_hist[i]; return 100.0 * n / c.rays; }());
@@ -280,6 +283,11 @@ void report(const char* name, const Counters& c) {
 
 int main(int argc, char** argv) {
     const uint32_t scene_id = argc > 1 ? uint32_t(atoi(argv[1])) : 0u;
+    {   // packaged assets: dxrpathtracer_amd/data, two levels above this binary (csrc/build/bvh_stats)
+        std::string dir(argv[0]);
+        dir = dir.find('/') == std::string::npos ? std::string(".") : dir.substr(0, dir.rfind('/'));
+        dxrpt_host_set_asset_dir((dir + "/../../data").c_str());
+    }
     const uint32_t gw = argc > 2 ? uint32_t(atoi(argv[2])) : 320u;
     const uint32_t gh = argc > 3 ? uint32_t(atoi(argv[3])) : 180u;
     BvhBuildParams params;  // argv[4]: binary depth cap to explore (0: default; the wide depth is then unbounded)
@@ -291,6 +299,7 @@ int main(int argc, char** argv) {
         params.ref_budget = atof(argv[5]);
         params.spatial_splits = params.ref_budget > 0.0;
     }
+    if (argc > 6) params.treelet_passes = uint32_t(atoi(argv[6]));  // argv[6]: treelet restructuring passes
     dxrpt_host_scene* hs = nullptr;
     if (dxrpt_host_scene_create(scene_id, 0, 0, &hs) != 0) {
         fprintf(stderr, "scene: %s\n", dxrpt_host_last_error());
@@ -309,6 +318,13 @@ int main(int argc, char** argv) {
                 memcpy(&S.pos[size_t(t) * 9 + k * 3], hs->vertices[idx + gi.VtxOffset].Position, 12);
             }
     }
+    S.alpha.assign(S.ntris, 0u);
+    for (uint32_t g = 0; g < hs->num_geometries; ++g) {
+        uint32_t end = g + 1 < hs->num_geometries ? hs->geometries[g + 1].IdxOffset / 3 : S.ntris;
+        if (hs->materials[hs->geometries[g].MaterialIdx].Opacity != DXRPT_INVALID_INDEX)
+            for (uint32_t t = hs->geometries[g].IdxOffset / 3; t < end; ++t) S.alpha[t] = 1u;
+    }
+    params.keep_whole = S.alpha.data();  // as dxrpt_build_bvh
     printf("scene %u: %u triangles\n", scene_id, S.ntris);
     BvhBuildResult B;
     std::string err;
@@ -328,9 +344,9 @@ int main(int argc, char** argv) {
                     leaf_tris += n.meta[s] >> 5;
                 }
             }
-    printf("BVH8: %zu nodes, depth %u (binary cap %u), %.2f children/node, %llu leaves, %.2f tris/leaf, build %.0f ms, SAH(bin) %.2f\n",
+    printf("BVH8: %zu nodes, depth %u (binary cap %u), %.2f children/node, %llu leaves, %.2f tris/leaf, build %.0f ms, SAH(bin) %.2f SAH(wide) %.2f\n",
            B.nodes8.size(), B.max_depth, B.binary_depth_cap, double(slots) / B.nodes8.size(), (unsigned long long)leaves,
-           double(leaf_tris) / leaves, ms, B.sah_cost);
+           double(leaf_tris) / leaves, ms, B.sah_cost, B.wide_sah);
 
     float M[16];
     dxrpt_host_inv_view_projection(hs->camera_position, hs->camera_rotation[0], hs->camera_rotation[1], 3.14159265f / 4.0f,

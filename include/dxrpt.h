@@ -368,6 +368,12 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                           target is complete when the caller's stream reaches that point
                                           (see "Stream ordering" above).  0: one frame at a time on the
                                           caller's stream.  Identical results. */
+#define DXRPT_OPT_TREELET_PASSES 40u /* BVH8 build: passes of treelet restructuring (Karras & Aila 2013:
+                                        every 7-leaf treelet of the binary SBVH re-wired to its SAH-optimal
+                                        topology; subtrees holding alpha-tested triangles are left as
+                                        built) before the collapse to BVH8, 0..8 (default 1).  Identical
+                                        results (the closest hit does not depend on the tree); only node
+                                        visits change. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

@@ -17,7 +17,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 CONFIGS = {"metric": ("sponza", 1920, 1080, 3), "c2": ("sponza", 1280, 720, 3), "c3": ("sponza", 1920, 1080, 8),
            "c4": ("suntemple", 1920, 1080, 3), "c5": ("sponza", 3840, 2160, 6)}
-BUILD_OPTIONS = ("LEAF_COST", "SPATIAL_SPLITS")  # set before the BVH build
+BUILD_OPTIONS = ("LEAF_COST", "SPATIAL_SPLITS", "TREELET_PASSES")  # set before the BVH build
 
 
 def main():
