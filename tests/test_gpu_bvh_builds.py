@@ -69,3 +69,20 @@ def test_treelet_option_range(torch_cuda):
     with pytest.raises(RuntimeError, match="treelet passes"):
         t.set_option(A.OPT_TREELET_PASSES, 9)
     t.close()
+
+
+def test_parallel_treelet_build_is_deterministic(torch_cuda):
+    """The treelet pass restructures disjoint subtrees on host threads: two builds of the same scene give
+    the same tree (node count, SAH) and the same frame."""
+    sc, sky = scene_bundle("sponza")
+    t = DXRPathTracer(0)
+    t.initialize_scene(sc, sky)
+    info = t.build_rt_acceleration_structure()
+    assert (info.num_nodes, round(info.sah_cost, 6)) == context("sponza", "shipped")[1]
+    st = sc.settings(MaxPathLength=3)
+    acc = torch_cuda.zeros((W * H, 4), dtype=torch_cuda.float32, device="cuda")
+    t.render_raw(D.make_constants(sc, st, sky, W, H, 0), st, acc.data_ptr(), W, H,
+                 stream=torch_cuda.cuda.current_stream().cuda_stream, lights=D.make_lights(sc))
+    torch_cuda.cuda.synchronize()
+    np.testing.assert_array_equal(acc.cpu().numpy(), frame(torch_cuda, "sponza", "shipped", 3, 0))
+    t.close()
