@@ -74,7 +74,8 @@ float trace8(const Scene& S, const BvhBuildResult& B, V3 o, V3 d, float tmin, fl
     V3 inv{1.0f / (fabsf(d.x) > 1e-20f ? d.x : copysignf(1e-20f, d.x)), 1.0f / (fabsf(d.y) > 1e-20f ? d.y : copysignf(1e-20f, d.y)),
            1.0f / (fabsf(d.z) > 1e-20f ? d.z : copysignf(1e-20f, d.z))};
     V3 ood{o.x * inv.x, o.y * inv.y, o.z * inv.z};
-    const uint32_t oct = (inv.x < 0 ? 4u : 0u) | (inv.y < 0 ? 2u : 0u) | (inv.z < 0 ? 1u : 0u);
+    // key octant: near to far for closest hits, far to near for any-hit rays (pt_kernels.hip key_octant)
+    const uint32_t oct = ((inv.x < 0 ? 4u : 0u) | (inv.y < 0 ? 2u : 0u) | (inv.z < 0 ? 1u : 0u)) ^ (any ? 7u : 0u);
     float best = tmax;
     uint32_t best_tri = ~0u;
     std::vector<std::pair<uint32_t, uint32_t>> stk;
