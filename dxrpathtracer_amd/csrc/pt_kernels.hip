@@ -382,8 +382,10 @@ PT_DEV Node8Words load_node8(const SceneDev& S, uint32_t node) {
     return w;
 }
 
-// Slot mask of the node's children whose quantised box the ray enters within [tmin, tmx].
-PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx) {
+// Slot mask of the node's children whose quantised box the ray enters within [tmin, tmx].  kNearest:
+// also the slot of the internal child entered first (smallest entry distance; *nslot, 8 if none).
+template <bool kNearest = false>
+PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_t* nslot = nullptr) {
     const uint4 w0 = W.w0, w2 = W.w2, w3 = W.w3, w4 = W.w4;
     const float ax = __uint_as_float((w0.w & 0xFFu) << 23) * R.inv.x;
     const float ay = __uint_as_float(((w0.w >> 8) & 0xFFu) << 23) * R.inv.y;
@@ -400,6 +402,9 @@ PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx) {
     const uint32_t ny0 = syn ? w4.x : w2.z, ny1 = syn ? w4.y : w2.w, fy0 = syn ? w2.z : w4.x, fy1 = syn ? w2.w : w4.y;
     const uint32_t nz0 = szn ? w4.z : w3.x, nz1 = szn ? w4.w : w3.y, fz0 = szn ? w3.x : w4.z, fz1 = szn ? w3.y : w4.w;
     uint32_t hm = 0;  // hit children, slot space
+    const uint32_t imask = w0.w >> 24;
+    float best_tn = kFP32Max;
+    uint32_t best_c = 8u;
     // near and far plane of one axis in one packed FMA (v_pk_fma_f32): (qn, qf) * (a, a) + (b, b)
     const f2v A2x = {ax, ax}, A2y = {ay, ay}, A2z = {az, az};
     const f2v B2x = {bx, bx}, B2y = {by, by}, B2z = {bz, bz};
@@ -416,7 +421,12 @@ PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx) {
         const float tf = fminf(fminf(tx.y, ty.y), fminf(tz.y, tmx));
         // empty slots carry inverted boxes (qlo 255, qhi 0: never entered) and meta 0 (no triangles)
         hm |= uint32_t(tn <= tf) << c;
+        if (kNearest && tn <= tf && ((imask >> c) & 1u) && tn < best_tn) {
+            best_tn = tn;
+            best_c = uint32_t(c);
+        }
     }
+    if (kNearest) *nslot = best_c;
     return hm;
 }
 
@@ -453,12 +463,13 @@ PT_DEV uint32_t leaf_tri_bits(uint32_t lh, const uint4& w1) {
 template <bool kAnyHit>
 PT_DEV uint32_t key_octant(uint32_t oct) { return kAnyHit ? oct ^ 7u : oct; }
 
-template <bool kCount, bool kAnyHit = false>
+template <bool kCount, bool kAnyHit = false, bool kNearest = false>
 PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, const Node8Words& W, uint32_t& node, int& sp, uint2& tos,
                        const HitRec& h, uint32_t& tbase, uint32_t& tbits, uint32_t& nvisit) {
     if (kCount) ++nvisit;
     const uint4 w0 = W.w0, w1 = W.w1;
-    const uint32_t hm = box8_hits(R, W, h.t);  // hit children, slot space
+    uint32_t nslot = 8u;
+    const uint32_t hm = box8_hits<kNearest>(R, W, h.t, &nslot);  // hit children, slot space
     const uint32_t imask = w0.w >> 24;
     const uint32_t koct = key_octant<kAnyHit>(R.oct);
     const uint32_t ihits = key_order(hm & imask, koct);
@@ -466,6 +477,16 @@ PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, const Node8Words& W, ui
     tbits = leaf_tri_bits(hm & ~imask, w1);
     uint32_t gbase = w1.x;
     uint32_t gword = (ihits << 24) | imask;
+    if (kNearest && !kAnyHit && nslot < 8u) {  // the nearest internal child first, the rest as a group
+        gword &= ~(1u << (24u + (nslot ^ koct)));
+        node = gbase + uint32_t(__builtin_popcount(imask & ((1u << nslot) - 1u)));
+        if (gword >> 24) {
+            if (sp > 0) stack8_store(S, sp - 1, tos);
+            tos = make_uint2(gbase, gword);
+            ++sp;
+        }
+        return true;
+    }
     while (true) {
         if (gword >> 24) {
             const uint32_t k = 31u - uint32_t(__builtin_clz(gword));
@@ -520,8 +541,12 @@ PT_DEV bool trav8_tris2(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32
 }
 
 // One ray per lane from the root.  kPairs: leaf triangles two at a time (trav8_tris2; the split tails'
-// closest hit, r03: -0.8..-1.0 %).  Returns h.tri != kMiss (hit / occluded).
-template <bool kAnyHit, bool kCount, bool kPairs = false>
+// closest hit, r03: -0.8..-1.0 %).  kNearest (closest hit): each node descends into its nearest hit
+// internal child first (exact entry distance) and keeps the others as one octant-ordered group -- fewer
+// node visits and triangle tests, for a few more registers in the box test, so only kernels with the
+// budget use it (r04: the split tails and k_path at <= 5 waves/SIMD; k_path<7> spills, C2 +9 %).
+// Returns h.tri != kMiss (hit / occluded).
+template <bool kAnyHit, bool kCount, bool kPairs = false, bool kNearest = false>
 PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, HitRec& h, uint32_t& nvisit,
                       uint32_t& ntest) {
     Ray8 R;
@@ -531,7 +556,8 @@ PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
     uint2 tos = make_uint2(0u, 0u);
     while (true) {
         uint32_t tbase = 0, tbits = 0;
-        const bool more = trav8_node<kCount, kAnyHit>(S, R, load_node8(S, node), node, sp, tos, h, tbase, tbits, nvisit);
+        const bool more = trav8_node<kCount, kAnyHit, kNearest>(S, R, load_node8(S, node), node, sp, tos, h, tbase, tbits,
+                                                                nvisit);
         if (tbits) {
             const bool done = kPairs ? trav8_tris2<kAnyHit, kCount>(S, R, tbase, tbits, h, ntest)
                                      : trav8_tris<kAnyHit, kCount>(S, R, tbase, tbits, h, ntest);
@@ -592,7 +618,11 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
     if (lv == 0ull) return false;
     // key order of the first live lane's octant for the whole wave (any order gives the same results;
     // any-hit rays far to near, key_octant)
-    const uint32_t oct = key_octant<kAnyHit>(uint32_t(__builtin_amdgcn_readlane(int(R.oct), __ffsll(static_cast<long long>(lv)) - 1)));
+#ifndef DXRPT_PACKET_ANYHIT_FAR
+#define DXRPT_PACKET_ANYHIT_FAR 1
+#endif
+    const uint32_t oct = key_octant<kAnyHit && DXRPT_PACKET_ANYHIT_FAR>(
+        uint32_t(__builtin_amdgcn_readlane(int(R.oct), __ffsll(static_cast<long long>(lv)) - 1)));
     const uint32_t lane = uint32_t(__lane_id());
     const bool counter = kCount && lane == uint32_t(__ffsll(static_cast<long long>(lv)) - 1);
     uint32_t sbase = 0, sword = 0;  // stack entry j in lane j
@@ -1298,7 +1328,7 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
 // kCount: census of the traversal work, cnt[0..4] for depth-1 vertices and cnt[5..9] for deeper ones:
 // closest-hit node / triangle fetches, any-hit node / triangle fetches, radiance hits (per-lane traversals
 // fetch per lane, packet traversals once per wave).
-template <bool kBake, bool kCount = false>
+template <bool kBake, bool kCount = false, bool kNearest = false>
 PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, f3 dir, float tmax, uint32_t packet_mask,
                          uint32_t* cnt = nullptr, PhaseAcc* pa = nullptr) {
     const dxrpt_app_settings& set = A.P.set;
@@ -1317,7 +1347,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
         if (d == 1 && (packet & 1u))  // coherent primary rays: wave-coherent traversal (same results)
             traverse8_packet<false, kCount>(A.S, org, dir, tmin1, tmax, d <= set.MaxAnyHitPathLength, true, h, cd);
         else
-            traverse8<false, kCount>(A.S, org, dir, d == 1 ? tmin1 : kRayTMin, tmax, d <= set.MaxAnyHitPathLength, h, cd[0],
+            traverse8<false, kCount, false, kNearest>(A.S, org, dir, d == 1 ? tmin1 : kRayTMin, tmax, d <= set.MaxAnyHitPathLength, h, cd[0],
                                      cd[1]);
         phase_mark(pa, d == 1 ? 0 : d == 2 ? 3 : 6);
         if (kCount && h.tri != kMiss) ++cd[4];  // radiance hits: the vertices PathTrace shades
@@ -1357,11 +1387,11 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
 // Path p of a wave whose paths are 64-aligned (p & ~63 .. p | 63).  Packets need every lane of the wave
 // (the packet stack lives one entry per lane): a partial last wave (num_paths % 64 != 0) traverses one
 // ray per lane -- a wave-uniform scalar test, the other waves keep their packets (same results).
-template <bool kCount = false>
+template <bool kCount = false, bool kNearest = false>
 PT_DEV void camera_path(const KArgs& A, uint32_t p, uint32_t* cnt = nullptr, PhaseAcc* pa = nullptr) {
     const PrimaryRay pr = primary_ray(A, p);
     const uint32_t packet = (p | 63u) < A.P.num_paths ? A.P.packet : 0u;
-    const float4 rad = trace_path<false, kCount>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, packet, cnt, pa);
+    const float4 rad = trace_path<false, kCount, kNearest>(A, p, pr.pixelIdx, pr.start, pr.dir, pr.length, packet, cnt, pa);
     finish_pixel(A, pr.accumIdx, rad);
 }
 
@@ -1459,13 +1489,14 @@ hipError_t launch_wave_order(const uint32_t* cls, const uint32_t* hist, uint32_t
 // path-ordered with XCD-local runs of blocks (FrameParams::xcd_chunk).
 template <int kOcc, bool kCount = false, bool kOrder = false>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_path(KArgs A) {
+    constexpr bool kNear = kOcc <= 5;  // nearest-child-first closest hits where the register budget allows
     if (A.F.counters_next && blockIdx.x == 0u)  // the next frame's counter set (this stream's previous frame's)
         for (uint32_t i = threadIdx.x; i < kCounterWords; i += blockDim.x) A.F.counters_next[i] = 0u;
     lut_fill(A.S);
     if (kOrder) {
         const WaveSlot ws = wave_slot(A);
         const uint32_t p = (ws.slot << 6) | (threadIdx.x & 63u);
-        if (p < A.P.num_paths) camera_path(A, p);
+        if (p < A.P.num_paths) camera_path<false, kNear>(A, p);
         wave_slot_done(A, ws);
         return;
     }
@@ -1473,7 +1504,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     if (kCount) {
         const unsigned long long t0 = A.P.wave_clock ? __builtin_amdgcn_s_memrealtime() : 0ull;
         uint32_t cnt[10] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-        if (p < A.P.num_paths) camera_path<true>(A, p, cnt);
+        if (p < A.P.num_paths) camera_path<true, kNear>(A, p, cnt);
         if (A.P.wave_clock && (threadIdx.x & 63u) == 0u && p < A.P.num_paths) {  // vector stores from lane 0
             const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
             A.P.wave_clock[2 * (p >> 6)] = t0;
@@ -1489,7 +1520,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     }
 #if DXRPT_DIAG_PHASES
     PhaseAcc pa = {{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, uint32_t(__builtin_amdgcn_s_memrealtime())};
-    if (p < A.P.num_paths) camera_path(A, p, nullptr, &pa);
+    if (p < A.P.num_paths) camera_path<false, kNear>(A, p, nullptr, &pa);
     phase_mark(&pa, 7);
     phase_flush(&pa);
     return;
@@ -1497,7 +1528,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     // XCD-local runs of blocks (FrameParams::xcd_chunk); the tail stays in order.  Run t of XCD x is chunk
     // 8 t + (x + t) mod 8: the XCDs' chunks rotate from run to run, so no XCD keeps the same screen columns.
     const uint32_t q = A.P.xcd_chunk ? xcd_position(blockIdx.x, gridDim.x, A.P.xcd_chunk) * blockDim.x + threadIdx.x : p;
-    if (q < A.P.num_paths) camera_path(A, q);
+    if (q < A.P.num_paths) camera_path<false, kNear>(A, q);
 }
 
 // ---- depth-split megakernel (FrameParams::split) ---------------------------------------------
@@ -1612,7 +1643,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     {
         const float4 o4 = Q.org[pos], d4 = Q.dir[pos];
         uint32_t nv = 0, nt = 0;
-        traverse8<false, false, true>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= set.MaxAnyHitPathLength, h, nv, nt);
+        traverse8<false, false, true, true>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= set.MaxAnyHitPathLength, h, nv, nt);
     }
     // the rest of the path state comes back from the queue after the traversal (the radiance so far only
     // once the vertex is shaded: it is not live across path_vertex)
@@ -1794,9 +1825,14 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
         const bool ordered = fp.wave_cost || fp.wave_order;
         sched = DXRPT_SCHED_MEGAKERNEL;
         if (ev) (void)hipEventRecord(ev[0], stream);
-        if (count) {  // census frame (DXRPT_OPT_COUNT_TRAVERSAL): the single kernel's counting instantiation
+        if (count) {  // census frame (DXRPT_OPT_COUNT_TRAVERSAL): the single kernel's counting instantiation,
+                      // with the closest-hit child order of the schedule it stands for (k_path<5> walks
+                      // nearest-first like the split tails and the low-occupancy k_path)
             sched |= DXRPT_SCHED_CENSUS;
-            hipLaunchKernelGGL((k_path<7, true>), dim3(gm), dim3(kWave), lds, stream, A);
+            if ((fp.split && !ordered) || fp.megakernel_occupancy <= 5)
+                hipLaunchKernelGGL((k_path<5, true>), dim3(gm), dim3(kWave), lds, stream, A);
+            else
+                hipLaunchKernelGGL((k_path<7, true>), dim3(gm), dim3(kWave), lds, stream, A);
         } else if (fp.split && !ordered) {
             sched |= DXRPT_SCHED_SPLIT;
             launch_split(A, gm, lds, stream, ev ? ev[2] : nullptr);

@@ -103,6 +103,13 @@ float trace8(const Scene& S, const BvhBuildResult& B, V3 o, V3 d, float tmin, fl
             b[k] = fmaf(n.p[k], invp[k], -oodp[k]);
         }
         uint32_t ihits = 0, thits = 0;
+        // child order of closest-hit rays (env SIM_ORDER): 3 (default) nearest hit internal child first, the
+        // rest as one octant-keyed group (the split tails, k_path at <= 5 waves/SIMD); 0 octant key order
+        // (k_path<6/7>); 1 / 2 every child sorted by entry distance (any-hit: far first / widest first).
+        // Any-hit rays: far-to-near octant order in modes 0 and 3 (pt_kernels.hip key_octant).
+        static const int sim_order = getenv("SIM_ORDER") ? atoi(getenv("SIM_ORDER")) : 3;
+        std::pair<float, uint32_t> exact[8];
+        int nex = 0;
         for (int s = 0; s < 8; ++s) {
             uint32_t m = n.meta[s];
             if (!m) continue;
@@ -113,8 +120,19 @@ float trace8(const Scene& S, const BvhBuildResult& B, V3 o, V3 d, float tmin, fl
                 tf = std::min(tf, std::max(t0, t1));
             }
             if (tn > tf) continue;
-            if (m & kMetaInternal) ihits |= 1u << ((m & 7u) ^ oct);
-            else thits |= ((1u << (m >> 5)) - 1u) << (m & 31u);
+            if (m & kMetaInternal) {
+                ihits |= 1u << ((m & 7u) ^ oct);
+                exact[nex++] = {any ? (sim_order == 2 ? -(tf - tn) : -tn) : tn, m & 7u};
+            } else thits |= ((1u << (m >> 5)) - 1u) << (m & 31u);
+        }
+        if (sim_order != 3 && sim_order && nex) {  // exact order: push all but the first, far end first
+            std::sort(exact, exact + nex);
+            // children slots: node index = base_child + rank of slot among internal slots
+            for (int e = nex - 1; e >= 1; --e) {
+                uint32_t slot = exact[e].second;
+                stk.push_back({n.base_child + uint32_t(__builtin_popcount(n.imask & ((1u << slot) - 1u))), 0xFFFFFFFFu});
+            }
+            max_sp = std::max(max_sp, stk.size());
         }
         seq.push_back(uint8_t(__builtin_popcount(thits)));
         while (thits) {
@@ -133,6 +151,36 @@ float trace8(const Scene& S, const BvhBuildResult& B, V3 o, V3 d, float tmin, fl
                     return best;
                 }
             }
+        }
+        if (sim_order == 3) {  // nearest internal child first (closest hit only), the rest as an octant-keyed group
+            if (!any && nex) {
+                int bi = 0;
+                for (int e = 1; e < nex; ++e) if (exact[e].first < exact[bi].first) bi = e;
+                const uint32_t slot = exact[bi].second;
+                const uint32_t rest = ihits & ~(1u << (slot ^ oct));
+                if (rest) stk.push_back({n.base_child, (rest << 24) | n.imask});
+                max_sp = std::max(max_sp, stk.size());
+                node = n.base_child + uint32_t(__builtin_popcount(n.imask & ((1u << slot) - 1u)));
+                continue;
+            }
+        }
+        if (sim_order == 1 || sim_order == 2) {
+            // test the leaf triangles first (already done above), then go to the nearest internal child
+            if (nex) {
+                node = n.base_child + uint32_t(__builtin_popcount(n.imask & ((1u << exact[0].second) - 1u)));
+                continue;
+            }
+            for (;;) {
+                if (stk.empty()) {
+                    if (best_tri != ~0u) c.hits++;
+                    if (out_tri) *out_tri = best_tri;
+                    return best_tri != ~0u ? best : -1.0f;
+                }
+                node = stk.back().first;
+                stk.pop_back();
+                break;
+            }
+            continue;
         }
         uint32_t gbase = n.base_child, gword = (ihits << 24) | n.imask;
         for (;;) {
