@@ -384,7 +384,7 @@ PT_DEV Node8Words load_node8(const SceneDev& S, uint32_t node) {
 
 // Slot mask of the node's children whose quantised box the ray enters within [tmin, tmx].  kNearest:
 // also the slot of the internal child entered first (smallest entry distance; *nslot, 8 if none).
-template <bool kNearest = false>
+template <bool kNearest = false, bool kFarthest = false>
 PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_t* nslot = nullptr) {
     const uint4 w0 = W.w0, w2 = W.w2, w3 = W.w3, w4 = W.w4;
     const float ax = __uint_as_float((w0.w & 0xFFu) << 23) * R.inv.x;
@@ -403,7 +403,7 @@ PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_
     const uint32_t nz0 = szn ? w4.z : w3.x, nz1 = szn ? w4.w : w3.y, fz0 = szn ? w3.x : w4.z, fz1 = szn ? w3.y : w4.w;
     uint32_t hm = 0;  // hit children, slot space
     const uint32_t imask = w0.w >> 24;
-    float best_tn = kFP32Max;
+    float best_tn = kFarthest ? -kFP32Max : kFP32Max;
     uint32_t best_c = 8u;
     // near and far plane of one axis in one packed FMA (v_pk_fma_f32): (qn, qf) * (a, a) + (b, b)
     const f2v A2x = {ax, ax}, A2y = {ay, ay}, A2z = {az, az};
@@ -421,7 +421,7 @@ PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_
         const float tf = fminf(fminf(tx.y, ty.y), fminf(tz.y, tmx));
         // empty slots carry inverted boxes (qlo 255, qhi 0: never entered) and meta 0 (no triangles)
         hm |= uint32_t(tn <= tf) << c;
-        if (kNearest && tn <= tf && ((imask >> c) & 1u) && tn < best_tn) {
+        if (kNearest && tn <= tf && ((imask >> c) & 1u) && (kFarthest ? tn > best_tn : tn < best_tn)) {
             best_tn = tn;
             best_c = uint32_t(c);
         }
@@ -463,13 +463,18 @@ PT_DEV uint32_t leaf_tri_bits(uint32_t lh, const uint4& w1) {
 template <bool kAnyHit>
 PT_DEV uint32_t key_octant(uint32_t oct) { return kAnyHit ? oct ^ 7u : oct; }
 
+#ifndef DXRPT_ANYHIT_FARTHEST
+#define DXRPT_ANYHIT_FARTHEST 0
+#endif
 template <bool kCount, bool kAnyHit = false, bool kNearest = false>
 PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, const Node8Words& W, uint32_t& node, int& sp, uint2& tos,
                        const HitRec& h, uint32_t& tbase, uint32_t& tbits, uint32_t& nvisit) {
     if (kCount) ++nvisit;
     const uint4 w0 = W.w0, w1 = W.w1;
     uint32_t nslot = 8u;
-    const uint32_t hm = box8_hits<kNearest>(R, W, h.t, &nslot);  // hit children, slot space
+    // any-hit rays with kNearest: the farthest entry first (DXRPT_ANYHIT_FARTHEST)
+    constexpr bool kPick = kNearest && (!kAnyHit || DXRPT_ANYHIT_FARTHEST);
+    const uint32_t hm = box8_hits<kPick, kAnyHit>(R, W, h.t, &nslot);  // hit children, slot space
     const uint32_t imask = w0.w >> 24;
     const uint32_t koct = key_octant<kAnyHit>(R.oct);
     const uint32_t ihits = key_order(hm & imask, koct);
@@ -477,7 +482,7 @@ PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, const Node8Words& W, ui
     tbits = leaf_tri_bits(hm & ~imask, w1);
     uint32_t gbase = w1.x;
     uint32_t gword = (ihits << 24) | imask;
-    if (kNearest && !kAnyHit && nslot < 8u) {  // the nearest internal child first, the rest as a group
+    if (kPick && nslot < 8u) {  // the nearest (farthest) internal child first, the rest as a group
         gword &= ~(1u << (24u + (nslot ^ koct)));
         node = gbase + uint32_t(__builtin_popcount(imask & ((1u << nslot) - 1u)));
         if (gword >> 24) {
@@ -606,10 +611,12 @@ PT_DEV uint32_t wave_or8(uint32_t m) {
     return u;
 }
 
-// `live`: this lane holds a ray (lanes past the end join with live = false).  Returns this lane's
+// `live`: this lane holds a ray (lanes past the end join with live = false).  kFar: any-hit packets walk far
+// to near (the head's depth-1 sun shadows: metric -1 %); k_path at <= 5 waves/SIMD walks them near to far
+// (1/8 share -3.5 %, profiles/r04_ab_packet_order.txt).  Returns this lane's
 // result like traverse8 (h.tri != kMiss: hit / occluded).  kCount: node / triangle FETCHES are counted
 // in cnt[0] / cnt[1] by the wave's first live lane (a packet fetches each once per wave).
-template <bool kAnyHit, bool kCount = false>
+template <bool kAnyHit, bool kCount = false, bool kFar = true>
 PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, bool live, HitRec& h,
                              uint32_t* cnt = nullptr) {
     Ray8 R;
@@ -618,10 +625,7 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
     if (lv == 0ull) return false;
     // key order of the first live lane's octant for the whole wave (any order gives the same results;
     // any-hit rays far to near, key_octant)
-#ifndef DXRPT_PACKET_ANYHIT_FAR
-#define DXRPT_PACKET_ANYHIT_FAR 1
-#endif
-    const uint32_t oct = key_octant<kAnyHit && DXRPT_PACKET_ANYHIT_FAR>(
+    const uint32_t oct = key_octant<kAnyHit && kFar>(
         uint32_t(__builtin_amdgcn_readlane(int(R.oct), __ffsll(static_cast<long long>(lv)) - 1)));
     const uint32_t lane = uint32_t(__lane_id());
     const bool counter = kCount && lane == uint32_t(__ffsll(static_cast<long long>(lv)) - 1);
@@ -1289,7 +1293,7 @@ PT_DEV void phase_flush(PhaseAcc* pa) {
 // nearby origins -- take the wave-coherent traversal (all lanes active).  A lane whose slot 0 holds another
 // kind of ray (a spot light's, or at MaxPathLength 2 the sky visibility ray: random directions) traces it
 // per lane, after the packet.  cnt[2..3]: the census' any-hit node / triangle fetches.
-template <bool kCount>
+template <bool kCount, bool kNear = false>
 PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh, bool sun0, uint32_t packet, float4& rad,
                            uint32_t* cnt) {
     uint32_t unused[4] = {0u, 0u, 0u, 0u};
@@ -1307,10 +1311,11 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
         bool occluded = false;
         const bool pk = d == 1 && k == 0 && (packet & 2u);
         if (pk)
-            occluded = traverse8_packet<true, kCount>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live && sun0, hs,
+            occluded = traverse8_packet<true, kCount, !kNear>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live && sun0, hs,
                                                       cnt + 2);
         if (live && !(pk && sun0))
-            occluded = traverse8<true, kCount>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, hs, cnt[2], cnt[3]);
+            occluded = traverse8<true, kCount, false, kNear>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, hs, cnt[2],
+                                                         cnt[3]);
         if (live) {
             rad.x += occluded ? c4.x * 0.0f : c4.x;
             rad.y += occluded ? c4.y * 0.0f : c4.y;
@@ -1371,7 +1376,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
         rad.x += thr.x * O.local.x;
         rad.y += thr.y * O.local.y;
         rad.z += thr.z * O.local.z;
-        vertex_shadows<kCount>(A, d, slot_p, nsh, sun0, packet, rad, cd);
+        vertex_shadows<kCount, kNearest>(A, d, slot_p, nsh, sun0, packet, rad, cd);
         phase_mark(pa, d == 1 ? 2 : d == 2 ? 5 : 6);
         if (!O.cont) break;
         org = O.nextOrigin;
@@ -1673,7 +1678,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     rad.x += V.pathThr.x * O.local.x;
     rad.y += V.pathThr.y * O.local.y;
     rad.z += V.pathThr.z * O.local.z;
-    vertex_shadows<false>(A, d, i, nsh, false, 0u, rad, nullptr);
+    vertex_shadows<false, true>(A, d, i, nsh, false, 0u, rad, nullptr);
     split_finish(A, d, cont, qpos, nextDiffuse, accumIdx, rad);
 }
 
