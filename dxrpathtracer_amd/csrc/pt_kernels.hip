@@ -384,7 +384,7 @@ PT_DEV Node8Words load_node8(const SceneDev& S, uint32_t node) {
 
 // Slot mask of the node's children whose quantised box the ray enters within [tmin, tmx].  kNearest:
 // also the slot of the internal child entered first (smallest entry distance; *nslot, 8 if none).
-template <bool kNearest = false, bool kFarthest = false>
+template <bool kNearest = false>
 PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_t* nslot = nullptr) {
     const uint4 w0 = W.w0, w2 = W.w2, w3 = W.w3, w4 = W.w4;
     const float ax = __uint_as_float((w0.w & 0xFFu) << 23) * R.inv.x;
@@ -403,7 +403,7 @@ PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_
     const uint32_t nz0 = szn ? w4.z : w3.x, nz1 = szn ? w4.w : w3.y, fz0 = szn ? w3.x : w4.z, fz1 = szn ? w3.y : w4.w;
     uint32_t hm = 0;  // hit children, slot space
     const uint32_t imask = w0.w >> 24;
-    float best_tn = kFarthest ? -kFP32Max : kFP32Max;
+    float best_tn = kFP32Max;
     uint32_t best_c = 8u;
     // near and far plane of one axis in one packed FMA (v_pk_fma_f32): (qn, qf) * (a, a) + (b, b)
     const f2v A2x = {ax, ax}, A2y = {ay, ay}, A2z = {az, az};
@@ -421,7 +421,7 @@ PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_
         const float tf = fminf(fminf(tx.y, ty.y), fminf(tz.y, tmx));
         // empty slots carry inverted boxes (qlo 255, qhi 0: never entered) and meta 0 (no triangles)
         hm |= uint32_t(tn <= tf) << c;
-        if (kNearest && tn <= tf && ((imask >> c) & 1u) && (kFarthest ? tn > best_tn : tn < best_tn)) {
+        if (kNearest && tn <= tf && ((imask >> c) & 1u) && tn < best_tn) {
             best_tn = tn;
             best_c = uint32_t(c);
         }
@@ -463,18 +463,16 @@ PT_DEV uint32_t leaf_tri_bits(uint32_t lh, const uint4& w1) {
 template <bool kAnyHit>
 PT_DEV uint32_t key_octant(uint32_t oct) { return kAnyHit ? oct ^ 7u : oct; }
 
-#ifndef DXRPT_ANYHIT_FARTHEST
-#define DXRPT_ANYHIT_FARTHEST 0
-#endif
 template <bool kCount, bool kAnyHit = false, bool kNearest = false>
 PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, const Node8Words& W, uint32_t& node, int& sp, uint2& tos,
                        const HitRec& h, uint32_t& tbase, uint32_t& tbits, uint32_t& nvisit) {
     if (kCount) ++nvisit;
     const uint4 w0 = W.w0, w1 = W.w1;
     uint32_t nslot = 8u;
-    // any-hit rays with kNearest: the farthest entry first (DXRPT_ANYHIT_FARTHEST)
-    constexpr bool kPick = kNearest && (!kAnyHit || DXRPT_ANYHIT_FARTHEST);
-    const uint32_t hm = box8_hits<kPick, kAnyHit>(R, W, h.t, &nslot);  // hit children, slot space
+    // kNearest picks the nearest hit internal child for closest-hit rays (any-hit rays ignore it: their
+    // farthest-entry-first variant was +0.7..1.4 % on C3 / C5, profiles/r04_ab_farthest.txt)
+    constexpr bool kPick = kNearest && !kAnyHit;
+    const uint32_t hm = box8_hits<kPick>(R, W, h.t, &nslot);  // hit children, slot space
     const uint32_t imask = w0.w >> 24;
     const uint32_t koct = key_octant<kAnyHit>(R.oct);
     const uint32_t ihits = key_order(hm & imask, koct);
@@ -482,7 +480,7 @@ PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, const Node8Words& W, ui
     tbits = leaf_tri_bits(hm & ~imask, w1);
     uint32_t gbase = w1.x;
     uint32_t gword = (ihits << 24) | imask;
-    if (kPick && nslot < 8u) {  // the nearest (farthest) internal child first, the rest as a group
+    if (kPick && nslot < 8u) {  // the nearest internal child first, the rest as a group
         gword &= ~(1u << (24u + (nslot ^ koct)));
         node = gbase + uint32_t(__builtin_popcount(imask & ((1u << nslot) - 1u)));
         if (gword >> 24) {

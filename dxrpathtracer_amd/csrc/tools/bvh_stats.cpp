@@ -105,7 +105,8 @@ float trace8(const Scene& S, const BvhBuildResult& B, V3 o, V3 d, float tmin, fl
         uint32_t ihits = 0, thits = 0;
         // child order of closest-hit rays (env SIM_ORDER): 3 (default) nearest hit internal child first, the
         // rest as one octant-keyed group (the split tails, k_path at <= 5 waves/SIMD); 0 octant key order
-        // (k_path<6/7>); 1 / 2 every child sorted by entry distance (any-hit: far first / widest first).
+        // (k_path<6/7>); 1 / 2 every child sorted by entry distance (any-hit: far first / widest first);
+        // 4 as 3, and any-hit rays take the hit internal child with the farthest entry first.
         // Any-hit rays: far-to-near octant order in modes 0 and 3 (pt_kernels.hip key_octant).
         static const int sim_order = getenv("SIM_ORDER") ? atoi(getenv("SIM_ORDER")) : 3;
         std::pair<float, uint32_t> exact[8];
@@ -125,7 +126,7 @@ float trace8(const Scene& S, const BvhBuildResult& B, V3 o, V3 d, float tmin, fl
                 exact[nex++] = {any ? (sim_order == 2 ? -(tf - tn) : -tn) : tn, m & 7u};
             } else thits |= ((1u << (m >> 5)) - 1u) << (m & 31u);
         }
-        if (sim_order != 3 && sim_order && nex) {  // exact order: push all but the first, far end first
+        if (sim_order != 3 && sim_order != 4 && sim_order && nex) {  // exact order: push all but the first, far end first
             std::sort(exact, exact + nex);
             // children slots: node index = base_child + rank of slot among internal slots
             for (int e = nex - 1; e >= 1; --e) {
@@ -152,8 +153,9 @@ float trace8(const Scene& S, const BvhBuildResult& B, V3 o, V3 d, float tmin, fl
                 }
             }
         }
-        if (sim_order == 3) {  // nearest internal child first (closest hit only), the rest as an octant-keyed group
-            if (!any && nex) {
+        if (sim_order == 3 || sim_order == 4) {  // nearest internal child first (closest hit; mode 4: any-hit
+                                                  // rays the farthest entry first), the rest as an octant-keyed group
+            if ((!any || sim_order == 4) && nex) {
                 int bi = 0;
                 for (int e = 1; e < nex; ++e) if (exact[e].first < exact[bi].first) bi = e;
                 const uint32_t slot = exact[bi].second;
