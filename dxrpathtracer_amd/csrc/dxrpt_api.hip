@@ -1018,10 +1018,12 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // register budget by frame size (measured on the Sponza proxy 1080p L=3 and its band shares): more
         // resident waves hide more latency once a frame has waves for several rounds; a GPU's 1/8 share fits
         // in one round at 4 waves/SIMD without spills.  r03 with overlapped frames: 600k+ paths 7, 300k-600k
-        // 6 (a 1/4 share 0.560 -> 0.520 ms), below 4 (1/8 share 0.305 / 0.317 / 0.329 ms at 4 / 5 / 6)
+        // 6 (a 1/4 share 0.560 -> 0.520 ms), below 4 (1/8 share 0.305 / 0.317 / 0.329 ms at 4 / 5 / 6).  r04:
+        // 300k-600k 5, where k_path walks closest hits nearest-child-first (1/4 share 0.474 -> 0.466 ms,
+        // profiles/r04_ab_mid_frames.txt)
         fp.megakernel_occupancy = ctx->opt_mega_occ ? ctx->opt_mega_occ
                                 : paths > 600000u ? 7u
-                                : (ctx->opt_overlap && paths > 300000u ? 6u : 4u);
+                                : (ctx->opt_overlap && paths > 300000u ? 5u : 4u);
         // depth-split schedule (k_path_head + one compacting k_path_tail per depth): it wins where there are
         // many path vertices per frame and loses on short paths, where each kernel's drain is a larger part
         // of its time -- unless overlapped frames fill the drains (r03: from 2M vertices, the metric's 1/2

@@ -318,7 +318,7 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                             per stage and depth, compacted queues between depths).  0 = always
                                             the wavefront.  Identical results. */
 #define DXRPT_OPT_MEGAKERNEL_OCCUPANCY 24u /* megakernel register budget in waves/SIMD: 0 = by frame size
-                                              (default: 7 above 600,000 paths, 6 from 300,000 with overlapped
+                                              (default: 7 above 600,000 paths, 5 from 300,000 with overlapped
                                               frames, else 4; the split head 5), or 4..7 */
 #define DXRPT_OPT_BAKE_CHUNK 25u /* texels per dxrpt_bake_lightmap launch (default 2^21; bounds the
                                     per-texel shadow-slot buffers).  Identical results. */
