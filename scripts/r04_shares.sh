@@ -7,9 +7,10 @@ T="timeout -k 10 120 python -u scripts/time_frames.py --rounds 3 --frames 32"
 run() { $T "$@" 2>&1 | grep -v amdgpu.ids || exit 1; }
 run --config metric --label default
 for r in 0 1 2 3 4 5 6 7; do run --config metric --share 8 --rank $r --label default; done
-for alt in "WAVE_ORDER=0" "MEGAKERNEL_OCCUPANCY=5" "MEGAKERNEL_OCCUPANCY=6" "MEGAKERNEL_SPLIT=1"; do
+# DEFAULT_ONLY=1: the shipped defaults only (every rank of the 1/8, 1/4 and 1/2 shares)
+[ -z "$DEFAULT_ONLY" ] && for alt in "WAVE_ORDER=0" "MEGAKERNEL_OCCUPANCY=5" "MEGAKERNEL_OCCUPANCY=6" "MEGAKERNEL_SPLIT=1"; do
   for r in 0 1 2 3 4 5 6 7; do run --config metric --share 8 --rank $r --label "$alt" --opt $alt; done
 done
-for r in 0 1 2 3 4 5 6 7; do run --config metric --share 8 --rank $r --layout blocks --label blocks; done
+[ -z "$DEFAULT_ONLY" ] && for r in 0 1 2 3 4 5 6 7; do run --config metric --share 8 --rank $r --layout blocks --label blocks; done
 for r in 0 1 2 3; do run --config metric --share 4 --rank $r --label default; done
 for r in 0 1; do run --config metric --share 2 --rank $r --label default; done
