@@ -29,9 +29,10 @@ struct BvhBuildParams {
     uint32_t binary_depth_cap = 0;  // BVH8: force this binary depth cap (0: tighten until the tree fits)
     uint32_t max_wide_depth = 0;    // BVH8: accepted wide depth (0: kTraversalStack8 - 1)
     bool spatial_splits = true;     // BVH8: SBVH spatial splits
-    double ref_budget = 2.0;        // BVH8: maximum triangle references / triangles with spatial splits
-                                    // (r04: 2.0, C4 -11 % once any-hit rays walk far to near;
-                                    // profiles/r04_ab_split_budget.txt)
+    double ref_budget = 1.5;        // BVH8: maximum triangle references / triangles with spatial splits
+                                    // (r04: 2.0 is C4 -11 % but the Sponza proxy's tree one level
+                                    // deeper, metric +0.8 %, slowest 1/8 share +5 %;
+                                    // profiles/r04_ab_split_budget.txt, r04_shares_budget200.txt)
     double leaf_cost = 1.5;         // BVH8 collapse: SAH cost of a triangle test relative to a node visit
                                     // (latency-bound traversal: each test is a dependent memory round trip)
     // per global triangle, non-zero: never cut by a spatial split (an alpha-tested triangle: every extra

@@ -4,7 +4,7 @@ DXRPT_OPT_LEAF_COST, DXRPT_OPT_SPATIAL_SPLITS).
 The closest hit is the minimum (t, triangle) over every triangle the ray meets and an any-hit ray's
 visibility is a boolean over them, so any correct acceleration structure gives the same frame bit for bit
 (RayTrace.hlsl's TraceRay contract; the oracle builds its own tree).  Each variant context renders the
-frame the shipped context renders (1 treelet pass, 200 % spatial-split budget, leaf cost 1.5) and must
+frame the shipped context renders (1 treelet pass, 150 % spatial-split budget, leaf cost 1.5) and must
 match it exactly, while its BVH differs (node count or SAH), so the option did take effect.  SunTemple
 carries the alpha-tested foliage (any-hit shader on both ray kinds), whose subtrees the treelet pass
 leaves as built.
