@@ -1,0 +1,17 @@
+#!/bin/bash
+# r04 A/B: the 1/8 share's schedule options after the traversal-order changes (runtime options): 4 waves/SIMD (shipped) /
+# 5, cost order on (shipped) / off, on the slowest ranks.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -c "import torch; torch.zeros(1, device='cuda')" || exit 1
+T="timeout -k 10 150 python -u scripts/time_frames.py --rounds 3"
+for rk in 1 2 5; do
+  for r in 1 2; do
+    for o in "FRAME_OVERLAP=1" "MEGAKERNEL_OCCUPANCY=5" "WAVE_ORDER=0"; do
+      $T --config metric --share 8 --rank $rk --opt $o --label $o 2>> gpurun_out/ab_share_opts.err
+      rc=$?; [ $rc -ne 0 ] && { echo "$o rank $rk rc=$rc"; [ $rc -gt 1 ] && exit $rc; }
+    done
+  done
+done
+exit 0
