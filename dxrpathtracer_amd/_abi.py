@@ -108,7 +108,7 @@ DEFAULT_MEGAKERNEL_PATHS = 0xFFFFFFFF
 DEFAULT_MEGAKERNEL_OCCUPANCY = 0
 DEFAULT_BAKE_CHUNK = 1 << 21
 DEFAULT_XCD_CHUNK = 8
-DEFAULT_WAVE_ORDER_PERIOD = 16
+DEFAULT_WAVE_ORDER_PERIOD = 64
 DEFAULT_OPACITY_MICROMAP = 1
 DEFAULT_FRAME_OVERLAP = 1
 DEFAULT_WAVE_ORDER = 2  # by frame size
