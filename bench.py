@@ -274,7 +274,10 @@ def main():
             pg.flush()
 
     # ---- traversal work census (instrumented kernels, untimed): nodes / triangles per ray, split by the
-    # kernel that traces them (depth 1: the split schedule's head; deeper: its tails)
+    # kernel that traces them (depth 1: the split schedule's head; deeper: its tails).  The census runs the
+    # counting instantiations of the schedule the timed frames run (r05: k_path_head / k_path_tail with
+    # kCount on depth-split frames -- the same traversal orders; the single k_path's census walks the
+    # order of the register budget it stands for), asserted below against the timed schedule.
     tracer.set_option(A.OPT_COUNT_TRAVERSAL, 1)
     frame(0)
     flush()
@@ -292,6 +295,12 @@ def main():
     flush()
     torch.cuda.synchronize()
     timed = tracer.stats()
+    # the census priced the timed kernels: the same split / single-kernel schedule and, for the single
+    # k_path, the same traversal-order class (nearest-first closest hits at <= 5 waves/SIMD)
+    assert census.schedule & A.SCHED_CENSUS, census.schedule
+    assert bool(census.schedule & A.SCHED_SPLIT) == bool(timed.schedule & A.SCHED_SPLIT), (census.schedule, timed.schedule)
+    if not timed.schedule & A.SCHED_SPLIT:
+        assert (census.occupancy <= 5) == (timed.occupancy <= 5), (census.occupancy, timed.occupancy)
     pinned = {A.OPT_MEGAKERNEL_SPLIT: 1 if timed.schedule & A.SCHED_SPLIT else 0,
               A.OPT_MEGAKERNEL_OCCUPANCY: int(timed.occupancy),
               A.OPT_TAIL_OCCUPANCY: int(timed.tail_occupancy) if timed.schedule & A.SCHED_SPLIT else 0,
@@ -485,7 +494,11 @@ def main():
                              "max": round(float(frame_ms.max()), 4)},
                 "render_ms_median": round(render_ms, 4),
                 "census": {"what": "node / triangle-record fetches of the timed schedule (per lane in per-lane "
-                                   "traversals, per wave in packet traversals), one instrumented frame",
+                                   "traversals, per wave in packet traversals), one instrumented frame of the "
+                                   "timed kernels' counting instantiations",
+                           "kernels": ("k_path_head<5,count> + k_path_tail<7,count>" if census.schedule & A.SCHED_SPLIT
+                                       else f"k_path<{5 if census.occupancy <= 5 else 7},count>"),
+                           "schedule_bits": int(census.schedule),
                            "node_fetches_radiance": int(census.node_visits_radiance),
                            "tri_fetches_radiance": int(census.tri_tests_radiance),
                            "node_fetches_shadow": int(census.node_visits_shadow),
@@ -499,8 +512,12 @@ def main():
                 "tri_fetches_per_radiance_ray": round(census.tri_tests_radiance / max(1, census.radiance_rays), 2),
                 "node_fetches_per_shadow_ray": round(census.node_visits_shadow / max(1, census.shadow_rays), 2),
                 "tri_fetches_per_shadow_ray": round(census.tri_tests_shadow / max(1, census.shadow_rays), 2),
-                "bvh": {"nodes": bvh.num_nodes, "max_depth": bvh.max_depth, "build_ms": round(bvh.build_ms, 1),
-                        "sah": round(bvh.sah_cost, 2)},
+                "bvh": {"nodes": bvh.num_nodes, "refs": bvh.num_refs, "max_depth": bvh.max_depth,
+                        "build_ms": round(bvh.build_ms, 1),
+                        "build_phase_ms": {n: round(bvh.phase_ms[i], 1) for i, n in enumerate(A.BVH_PHASES)},
+                        "build_threads": bvh.threads, "binary_depth_cap": bvh.binary_depth_cap,
+                        "treelet_passes": bvh.treelet_passes, "ref_budget_pct": bvh.ref_budget_pct,
+                        "sah": round(bvh.sah_cost, 2), "wide_sah": round(bvh.wide_sah, 3)},
                 "setup_s": round(setup_s, 2),
             },
         }

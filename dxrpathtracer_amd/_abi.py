@@ -79,7 +79,7 @@ class Tile(C.Structure):
 K_RAYGEN, K_TRACE, K_SHADE, K_SHADOW, K_ACCUMULATE, K_RESOLVE, K_PATH, K_PATH_HEAD, K_PATH_TAIL, K_COUNT = range(10)
 KERNEL_NAMES = ("k_raygen", "k_trace", "k_shade", "k_shadow", "k_accumulate", "k_resolve", "k_path", "k_path_head",
                 "k_path_tail")
-ABI_VERSION = 3
+ABI_VERSION = 4
 # dxrpt_set_option ids (include/dxrpt.h); the ids missing here were retired in ABI 3 (DXRPT_E_UNSUPPORTED)
 OPT_COUNT_TRAVERSAL = 1
 OPT_KERNEL_TIMING = 2
@@ -99,7 +99,10 @@ OPT_TAIL_OCCUPANCY = 34
 OPT_OPACITY_MICROMAP = 36
 OPT_FRAME_OVERLAP = 37
 OPT_TREELET_PASSES = 40
+OPT_BVH_THREADS = 41
+# include/dxrpt.h DXRPT_RETIRED_OPTIONS (tests/test_abi.py checks the two lists agree)
 RETIRED_OPTIONS = (3, 4, 5, 6, 7, 8, 9, 10, 11, 14, 15, 16, 17, 19, 21, 22, 26, 27, 30, 35, 38, 39)
+DXRPT_E_INVALID_ARG, DXRPT_E_HIP, DXRPT_E_NO_DEVICE, DXRPT_E_STATE, DXRPT_E_OOM = -1, -2, -3, -4, -5
 DXRPT_E_UNSUPPORTED = -6
 # context defaults (dxrpt_api.hip)
 POST_FLOAT4, POST_RGBA8 = 0, 1  # dxrpt_post_process output formats
@@ -138,8 +141,12 @@ SCHED_MEGAKERNEL, SCHED_ORDER_KERNEL, SCHED_COST_ORDERED, SCHED_CENSUS, SCHED_SP
 
 class BvhInfo(C.Structure):
     _fields_ = [("num_nodes", u32), ("num_leaves", u32), ("num_tris", u32), ("max_depth", u32),
-                ("node_bytes", u32), ("tri_bytes", u32), ("width", u32), ("pad", u32), ("build_ms", C.c_double),
-                ("sah_cost", C.c_double)]
+                ("node_bytes", u32), ("tri_bytes", u32), ("width", u32), ("num_refs", u32), ("build_ms", C.c_double),
+                ("sah_cost", C.c_double), ("phase_ms", C.c_double * 4), ("wide_sah", C.c_double),
+                ("binary_depth_cap", u32), ("treelet_passes", u32), ("threads", u32), ("ref_budget_pct", u32)]
+
+
+BVH_PHASES = ("sbvh", "treelet", "collapse", "records_upload")  # dxrpt_bvh_info.phase_ms
 
 
 class HostTexture(C.Structure):
@@ -173,7 +180,7 @@ DXRPT_SYMBOLS = ("dxrpt_abi_version", "dxrpt_default_settings", "dxrpt_create", 
                  "dxrpt_post_process", "dxrpt_bake_lightmap", "dxrpt_denoise_median", "dxrpt_get_wave_clocks",
                  "dxrpt_get_phase_clocks", "dxrpt_sample_cmj", "dxrpt_render_aov", "dxrpt_comm_unique_id", "dxrpt_comm_create",
                  "dxrpt_comm_destroy", "dxrpt_comm_info", "dxrpt_gather_slabs", "dxrpt_unpermute", "dxrpt_multi_last_error",
-                 "dxrpt_opacity_micromap")
+                 "dxrpt_multi_release", "dxrpt_opacity_micromap")
 DXRPT_HOST_SYMBOLS = ("dxrpt_host_scene_create", "dxrpt_host_scene_load", "dxrpt_host_scene_destroy", "dxrpt_host_last_error",
                       "dxrpt_host_inv_view_projection", "dxrpt_host_sky_create", "dxrpt_host_fill_constants",
                       "dxrpt_host_float_to_half", "dxrpt_host_half_to_float", "dxrpt_host_hosek_load",
@@ -238,6 +245,8 @@ def lib() -> C.CDLL:
         L.dxrpt_gather_slabs.argtypes = [P, P, C.POINTER(C.c_uint64), P, P]
         L.dxrpt_unpermute.argtypes = [P, C.POINTER(Tile), u32, P, u32, u32, P]
         L.dxrpt_multi_last_error.restype = C.c_char_p
+        if hasattr(L, "dxrpt_multi_release"):  # ABI 4
+            L.dxrpt_multi_release.argtypes = []
         L.dxrpt_opacity_micromap.argtypes = [P, u32, u32, u32, u32, P, P]
         _lib = L
     return _lib

@@ -14,11 +14,83 @@
 #include <cmath>
 #include <cstring>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <functional>
+#include <mutex>
 #include <thread>
+#include <chrono>
 
 namespace dxrpt {
 namespace {
+
+// Builder threads: BvhBuildParams::threads, else the host's CPUs capped at 16 (the GPU box's job gets 16
+// CPUs of its host; more threads would only time-slice them).  Results never depend on the count.
+unsigned build_threads(const BvhBuildParams* params) {
+    if (params && params->threads) return params->threads;
+    return std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+}
+
+// Fork-join pool for the builders' independent subtrees.  A thread that waits for a task it spawned runs
+// queued tasks meanwhile (so nested waits cannot deadlock); tasks are taken oldest first -- the largest
+// subtrees, spawned nearest the root -- which spreads the big pieces over the workers.
+class TaskPool {
+public:
+    explicit TaskPool(unsigned n) {
+        for (unsigned i = 1; i < n; ++i) th_.emplace_back([this] { work(); });
+    }
+    ~TaskPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (std::thread& t : th_) t.join();
+    }
+    bool parallel() const { return !th_.empty(); }
+    void submit(std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            q_.push_back(std::move(f));
+        }
+        cv_.notify_one();
+    }
+    // Runs queued tasks until `done` is set.
+    void wait(const std::atomic<bool>& done) {
+        while (!done.load(std::memory_order_acquire)) {
+            std::function<void()> f;
+            {
+                std::lock_guard<std::mutex> g(m_);
+                if (!q_.empty()) {
+                    f = std::move(q_.front());
+                    q_.pop_front();
+                }
+            }
+            if (f) f();
+            else std::this_thread::yield();
+        }
+    }
+
+private:
+    void work() {
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+                if (stop_ && q_.empty()) return;
+                f = std::move(q_.front());
+                q_.pop_front();
+            }
+            f();
+        }
+    }
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+    std::vector<std::thread> th_;
+    bool stop_ = false;
+};
 
 struct Box {
     float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX};
@@ -204,6 +276,13 @@ struct Builder {
 // references (with clipped boxes) into both children.  Cuts the child-box overlap that long thin
 // architectural triangles cause, hence node visits per ray.  Duplicates are harmless for the
 // traversal: a triangle tested twice yields the same hit (tie rule: smaller t, then smaller id).
+//
+// Duplication budget (r05): every subtree carries its own allowance of extra references.  A node may search
+// a spatial split while its allowance is positive; what is left after its split is shared by its children
+// in proportion to their reference counts (as Embree's spatial-split builder shares its "extended range").
+// No decision depends on the order in which subtrees are built, so the subtrees of large nodes are built
+// in parallel (TaskPool) and the tree is the same for any thread count.  (r04 spent one global allowance in
+// depth-first order: the left half of the scene took all of it, and the build was serial.)
 struct SpatialBuilder {
     struct Ref {
         uint32_t tri;
@@ -216,9 +295,11 @@ struct SpatialBuilder {
     uint32_t depth_cap = 32;
     double root_area = 1.0;
     double alpha = kSbvhAlpha;  // overlap / root area that enables a spatial search
-    size_t ref_budget = 0;       // maximum live references (duplication budget)
-    size_t live_refs = 0;
+    size_t ref_budget = 0;       // maximum references of the whole tree (duplication budget)
     double sah = 0.0;            // binary tree, C_trav = 1, C_tri = 1, relative to the root area
+    unsigned threads = 1;
+    // subtrees of at least this many references are built as their own tasks
+    static constexpr size_t kTaskRefs = 2048;
 
     // Splits `r` at `plane` on `axis` into the parts of its triangle on each side (boxes clipped to r.box).
     void split_ref(const Ref& r, int axis, float plane, Box& left, Box& right) const {
@@ -249,10 +330,53 @@ struct SpatialBuilder {
         right.lo[axis] = std::max(right.lo[axis], plane);
     }
 
-    static Box bounds_of(const std::vector<Ref>& rs) {
-        Box b;
-        for (const Ref& r : rs) b.grow(r.box);
-        return b;
+    TaskPool* pool = nullptr;
+    // nodes of at least two chunks of this many references bin and partition them in parallel
+    static constexpr size_t kChunkRefs = 8192;
+
+    // f(k, begin, end) for the K chunks of [0, n) (K = 1 without a pool or for small n), on the pool; returns
+    // K.  Every chunk's results go to slot k, merged by the caller in chunk order: the same as one pass.
+    template <class F>
+    size_t chunked(size_t n, F&& f) const {
+        const size_t K = pool && pool->parallel() ? std::min<size_t>(size_t(threads) * 2u, n / kChunkRefs) : 1u;
+        if (K <= 1) {
+            f(size_t(0), size_t(0), n);
+            return 1;
+        }
+        std::atomic<size_t> left{K - 1};
+        std::atomic<bool> done{false}, failed{false};
+        for (size_t k = 1; k < K; ++k)
+            pool->submit([&, k] {
+                try {
+                    f(k, n * k / K, n * (k + 1) / K);
+                } catch (...) {
+                    failed.store(true);
+                }
+                if (left.fetch_sub(1) == 1) done.store(true, std::memory_order_release);
+            });
+        f(size_t(0), size_t(0), n / K);
+        pool->wait(done);
+        if (failed.load()) throw std::bad_alloc();
+        return K;
+    }
+
+    size_t max_chunks(size_t n) const {
+        return pool && pool->parallel() ? std::max<size_t>(1, std::min<size_t>(size_t(threads) * 2u, n / kChunkRefs)) : 1u;
+    }
+
+    Box bounds_of(const std::vector<Ref>& rs) const {
+        if (max_chunks(rs.size()) == 1) {
+            Box bx;
+            for (const Ref& r : rs) bx.grow(r.box);
+            return bx;
+        }
+        std::vector<Box> part(max_chunks(rs.size()));
+        const size_t K = chunked(rs.size(), [&](size_t k, size_t b, size_t e) {
+            for (size_t i = b; i < e; ++i) part[k].grow(rs[i].box);
+        });
+        Box bx;
+        for (size_t k = 0; k < K; ++k) bx.grow(part[k]);
+        return bx;
     }
 
     struct ObjSplit {
@@ -262,26 +386,61 @@ struct SpatialBuilder {
         float lo = 0.f, scale = 0.f;
     };
 
+    struct AxisBins {
+        Box bb[3][kBins];
+        uint32_t enter[3][kBins] = {}, exit_[3][kBins] = {};  // object binning: counts in enter
+    };
+
     ObjSplit object_split(const std::vector<Ref>& rs) const {
         ObjSplit best;
+        const size_t nk = max_chunks(rs.size());
+        Box cb_local;
+        std::vector<Box> cb_heap(nk > 1 ? nk : 0);
+        Box* cbs = nk > 1 ? cb_heap.data() : &cb_local;
+        size_t K = chunked(rs.size(), [&](size_t k, size_t b, size_t e) {
+            for (size_t i = b; i < e; ++i) {
+                float c[3];
+                for (int a = 0; a < 3; ++a) c[a] = 0.5f * (rs[i].box.lo[a] + rs[i].box.hi[a]);
+                cbs[k].grow(c);
+            }
+        });
         Box cb;
-        for (const Ref& r : rs) {
-            float c[3];
-            for (int k = 0; k < 3; ++k) c[k] = 0.5f * (r.box.lo[k] + r.box.hi[k]);
-            cb.grow(c);
-        }
+        for (size_t k = 0; k < K; ++k) cb.grow(cbs[k]);
+        float scale[3];
+        bool live[3];
         for (int ax = 0; ax < 3; ++ax) {
             const float ext = cb.hi[ax] - cb.lo[ax];
-            if (!(ext > 0.f)) continue;
-            Box bb[kBins];
-            uint32_t bc[kBins] = {};
-            const float scale = float(kBins) / ext;
-            for (const Ref& r : rs) {
-                int k = int((0.5f * (r.box.lo[ax] + r.box.hi[ax]) - cb.lo[ax]) * scale);
-                k = std::min(std::max(k, 0), kBins - 1);
-                bc[k]++;
-                bb[k].grow(r.box);
+            live[ax] = ext > 0.f;
+            scale[ax] = live[ax] ? float(kBins) / ext : 0.f;
+        }
+        if (!live[0] && !live[1] && !live[2]) return best;
+        AxisBins local;
+        std::vector<AxisBins> heap(nk > 1 ? nk : 0);
+        AxisBins* part = nk > 1 ? heap.data() : &local;
+        K = chunked(rs.size(), [&](size_t k, size_t b, size_t e) {
+            AxisBins& P = part[k];
+            for (size_t i = b; i < e; ++i) {
+                const Ref& r = rs[i];
+                for (int ax = 0; ax < 3; ++ax) {
+                    if (!live[ax]) continue;
+                    int j = int((0.5f * (r.box.lo[ax] + r.box.hi[ax]) - cb.lo[ax]) * scale[ax]);
+                    j = std::min(std::max(j, 0), kBins - 1);
+                    P.enter[ax][j]++;
+                    P.bb[ax][j].grow(r.box);
+                }
             }
+        });
+        for (size_t k = 1; k < K; ++k)
+            for (int ax = 0; ax < 3; ++ax)
+                for (int j = 0; j < kBins; ++j) {
+                    part[0].bb[ax][j].grow(part[k].bb[ax][j]);
+                    part[0].enter[ax][j] += part[k].enter[ax][j];
+                }
+        const AxisBins& P = part[0];
+        for (int ax = 0; ax < 3; ++ax) {
+            if (!live[ax]) continue;
+            const Box* bb = P.bb[ax];
+            const uint32_t* bc = P.enter[ax];
             Box racc[kBins];
             uint32_t rcnt[kBins];
             Box acc;
@@ -306,7 +465,7 @@ struct SpatialBuilder {
                     best.left = acc;
                     best.right = racc[k + 1];
                     best.lo = cb.lo[ax];
-                    best.scale = scale;
+                    best.scale = scale[ax];
                 }
             }
         }
@@ -321,35 +480,63 @@ struct SpatialBuilder {
 
     SpatSplit spatial_split(const std::vector<Ref>& rs, const Box& nb) const {
         SpatSplit best;
+        float lo[3], bs[3];
+        bool live[3];
         for (int ax = 0; ax < 3; ++ax) {
-            const float lo = nb.lo[ax], ext = nb.hi[ax] - nb.lo[ax];
-            if (!(ext > 0.f)) continue;
-            const float bs = ext / float(kBins);
-            Box bb[kBins];
-            uint32_t enter[kBins] = {}, exit_[kBins] = {};
-            for (const Ref& r : rs) {
-                if (keep_whole && keep_whole[r.tri]) {  // goes whole to the side of its centroid
-                    int c = int((0.5f * (r.box.lo[ax] + r.box.hi[ax]) - lo) / bs);
-                    c = std::min(std::max(c, 0), kBins - 1);
-                    bb[c].grow(r.box);
-                    enter[c]++;
-                    exit_[c]++;
-                    continue;
+            lo[ax] = nb.lo[ax];
+            const float ext = nb.hi[ax] - nb.lo[ax];
+            live[ax] = ext > 0.f;
+            bs[ax] = ext / float(kBins);
+        }
+        const size_t nk = max_chunks(rs.size());
+        AxisBins local;
+        std::vector<AxisBins> heap(nk > 1 ? nk : 0);
+        AxisBins* part = nk > 1 ? heap.data() : &local;
+        const size_t K = chunked(rs.size(), [&](size_t k, size_t b, size_t e) {
+            AxisBins& P = part[k];
+            for (int ax = 0; ax < 3; ++ax) {
+                if (!live[ax]) continue;
+                Box* bb = P.bb[ax];
+                uint32_t* enter = P.enter[ax];
+                uint32_t* exit_ = P.exit_[ax];
+                for (size_t i = b; i < e; ++i) {
+                    const Ref& r = rs[i];
+                    if (keep_whole && keep_whole[r.tri]) {  // goes whole to the side of its centroid
+                        int c = int((0.5f * (r.box.lo[ax] + r.box.hi[ax]) - lo[ax]) / bs[ax]);
+                        c = std::min(std::max(c, 0), kBins - 1);
+                        bb[c].grow(r.box);
+                        enter[c]++;
+                        exit_[c]++;
+                        continue;
+                    }
+                    int b0 = int((r.box.lo[ax] - lo[ax]) / bs[ax]), b1 = int((r.box.hi[ax] - lo[ax]) / bs[ax]);
+                    b0 = std::min(std::max(b0, 0), kBins - 1);
+                    b1 = std::min(std::max(b1, b0), kBins - 1);
+                    Ref cur = r;
+                    for (int j = b0; j < b1; ++j) {
+                        Box L, R;
+                        split_ref(cur, ax, lo[ax] + bs[ax] * float(j + 1), L, R);
+                        bb[j].grow(L);
+                        cur.box = R;
+                    }
+                    bb[b1].grow(cur.box);
+                    enter[b0]++;
+                    exit_[b1]++;
                 }
-                int b0 = int((r.box.lo[ax] - lo) / bs), b1 = int((r.box.hi[ax] - lo) / bs);
-                b0 = std::min(std::max(b0, 0), kBins - 1);
-                b1 = std::min(std::max(b1, b0), kBins - 1);
-                Ref cur = r;
-                for (int b = b0; b < b1; ++b) {
-                    Box L, R;
-                    split_ref(cur, ax, lo + bs * float(b + 1), L, R);
-                    bb[b].grow(L);
-                    cur.box = R;
-                }
-                bb[b1].grow(cur.box);
-                enter[b0]++;
-                exit_[b1]++;
             }
+        });
+        for (size_t k = 1; k < K; ++k)
+            for (int ax = 0; ax < 3; ++ax)
+                for (int j = 0; j < kBins; ++j) {
+                    part[0].bb[ax][j].grow(part[k].bb[ax][j]);
+                    part[0].enter[ax][j] += part[k].enter[ax][j];
+                    part[0].exit_[ax][j] += part[k].exit_[ax][j];
+                }
+        for (int ax = 0; ax < 3; ++ax) {
+            if (!live[ax]) continue;
+            const Box* bb = part[0].bb[ax];
+            const uint32_t* enter = part[0].enter[ax];
+            const uint32_t* exit_ = part[0].exit_[ax];
             Box racc[kBins];
             uint32_t rcnt[kBins];
             Box acc;
@@ -370,142 +557,245 @@ struct SpatialBuilder {
                 if (c < best.cost) {
                     best.cost = c;
                     best.axis = ax;
-                    best.plane = lo + bs * float(k + 1);
+                    best.plane = lo[ax] + bs[ax] * float(k + 1);
                 }
             }
         }
         return best;
     }
 
-    bool build(uint32_t ntris, const std::vector<Box>& tri_box, std::string& err) {
-        struct Task {
-            int32_t node;
-            std::vector<Ref> rs;
-            uint32_t depth;
-        };
-        tree.clear();
-        refs.clear();
-        tree.reserve(size_t(ntris) * 3);
-        tree.emplace_back();
-        std::vector<Ref> all(ntris);
-        for (uint32_t t = 0; t < ntris; ++t) all[t] = Ref{t, tri_box[t]};
-        root_area = std::max(bounds_of(all).area(), 1e-30);
-        live_refs = ntris;
-        std::vector<Task> stack;
-        stack.push_back(Task{0, std::move(all), 0});
-        while (!stack.empty()) {
-            Task t = std::move(stack.back());
-            stack.pop_back();
-            const Box nb = bounds_of(t.rs);
-            tree[t.node].box = nb;
-            const size_t n = t.rs.size();
-            if (n <= 1) {
-                tree[t.node].first = uint32_t(refs.size());
-                tree[t.node].count = uint32_t(n);
-                tree[t.node].begin = uint32_t(refs.size());
-                for (const Ref& r : t.rs) refs.push_back(r.tri);
-                tree[t.node].end = uint32_t(refs.size());
-                continue;
-            }
-            if (t.depth + 1 > depth_cap) {
-                err = "build_bvh: depth cap exceeded";
-                return false;
-            }
-            uint32_t levels = 0;
-            for (size_t m = n; m > 1; m = (m + 1) / 2) ++levels;
-            const bool tight = t.depth + levels + 3 >= depth_cap;
-            std::vector<Ref> L, R;
-            bool done = false;
-            if (!tight) {
-                const ObjSplit os = object_split(t.rs);
-                SpatSplit ss;
-                if (os.axis >= 0) {
-                    Box ov;
-                    for (int k = 0; k < 3; ++k) {
-                        ov.lo[k] = std::max(os.left.lo[k], os.right.lo[k]);
-                        ov.hi[k] = std::min(os.left.hi[k], os.right.hi[k]);
-                    }
-                    bool overlap = true;
-                    for (int k = 0; k < 3; ++k) overlap = overlap && ov.lo[k] <= ov.hi[k];
-                    if (overlap && ov.area() > alpha * root_area && live_refs < ref_budget) ss = spatial_split(t.rs, nb);
-                } else {
-                    ss = spatial_split(t.rs, nb);
+    static void concat(std::vector<std::vector<Ref>>& parts, size_t K, std::vector<Ref>& out) {
+        if (K == 1) {
+            out.swap(parts[0]);
+            return;
+        }
+        size_t total = 0;
+        for (size_t k = 0; k < K; ++k) total += parts[k].size();
+        out.reserve(total);
+        for (size_t k = 0; k < K; ++k) out.insert(out.end(), parts[k].begin(), parts[k].end());
+    }
+
+    // Partitions the references of a node (bounds nb, at `depth`, duplication allowance `budget`) into L
+    // and R; returns the number of references it duplicated.
+    size_t split_node(std::vector<Ref>& rs, const Box& nb, uint32_t depth, size_t budget, std::vector<Ref>& L,
+                      std::vector<Ref>& R) const {
+        const size_t n = rs.size();
+        uint32_t levels = 0;
+        for (size_t m = n; m > 1; m = (m + 1) / 2) ++levels;
+        const bool tight = depth + levels + 3 >= depth_cap;
+        size_t dup = 0;
+        if (!tight) {
+            const ObjSplit os = object_split(rs);
+            SpatSplit ss;
+            if (os.axis >= 0) {
+                Box ov;
+                for (int k = 0; k < 3; ++k) {
+                    ov.lo[k] = std::max(os.left.lo[k], os.right.lo[k]);
+                    ov.hi[k] = std::min(os.left.hi[k], os.right.hi[k]);
                 }
-                if (ss.axis >= 0 && ss.cost < os.cost) {
-                    for (const Ref& r : t.rs) {
-                        if (r.box.hi[ss.axis] <= ss.plane) L.push_back(r);
-                        else if (r.box.lo[ss.axis] >= ss.plane) R.push_back(r);
+                bool overlap = true;
+                for (int k = 0; k < 3; ++k) overlap = overlap && ov.lo[k] <= ov.hi[k];
+                if (overlap && ov.area() > alpha * root_area && budget > 0) ss = spatial_split(rs, nb);
+            } else {
+                if (budget > 0) ss = spatial_split(rs, nb);  // no object split separates these centroids
+            }
+            if (ss.axis >= 0 && ss.cost < os.cost) {
+                const size_t nk = max_chunks(n);
+                std::vector<std::vector<Ref>> Lk(nk), Rk(nk);
+                std::vector<size_t> dk(nk, 0);
+                if (nk == 1) {
+                    Lk[0].reserve(n / 2 + 16);
+                    Rk[0].reserve(n / 2 + 16);
+                }
+                const size_t K = chunked(n, [&](size_t k, size_t b, size_t e) {
+                    for (size_t i = b; i < e; ++i) {
+                        const Ref& r = rs[i];
+                        if (r.box.hi[ss.axis] <= ss.plane) Lk[k].push_back(r);
+                        else if (r.box.lo[ss.axis] >= ss.plane) Rk[k].push_back(r);
                         else {
                             Box bl, br;
                             const bool whole = keep_whole && keep_whole[r.tri];
                             if (!whole) split_ref(r, ss.axis, ss.plane, bl, br);
                             if (!whole && !bl.empty() && !br.empty() && bl.lo[ss.axis] <= bl.hi[ss.axis] && br.lo[ss.axis] <= br.hi[ss.axis]) {
-                                L.push_back(Ref{r.tri, bl});
-                                R.push_back(Ref{r.tri, br});
-                                live_refs++;
+                                Lk[k].push_back(Ref{r.tri, bl});
+                                Rk[k].push_back(Ref{r.tri, br});
+                                dk[k]++;
                             } else if (0.5f * (r.box.lo[ss.axis] + r.box.hi[ss.axis]) < ss.plane) {
-                                L.push_back(r);
+                                Lk[k].push_back(r);
                             } else {
-                                R.push_back(r);
+                                Rk[k].push_back(r);
                             }
                         }
                     }
-                    done = !L.empty() && !R.empty();
-                    if (!done) {
-                        L.clear();
-                        R.clear();
-                    }
-                }
-                if (!done && os.axis >= 0) {
-                    for (const Ref& r : t.rs) {
-                        int k = int((0.5f * (r.box.lo[os.axis] + r.box.hi[os.axis]) - os.lo) * os.scale);
-                        k = std::min(std::max(k, 0), kBins - 1);
-                        (k <= os.bin ? L : R).push_back(r);
-                    }
-                    done = !L.empty() && !R.empty();
-                    if (!done) {
-                        L.clear();
-                        R.clear();
-                    }
-                }
-            }
-            if (!done) {  // object median along the widest centroid axis
-                Box cb;
-                for (const Ref& r : t.rs) {
-                    float c[3];
-                    for (int k = 0; k < 3; ++k) c[k] = 0.5f * (r.box.lo[k] + r.box.hi[k]);
-                    cb.grow(c);
-                }
-                int ax = 0;
-                for (int k = 1; k < 3; ++k)
-                    if (cb.hi[k] - cb.lo[k] > cb.hi[ax] - cb.lo[ax]) ax = k;
-                const size_t m = n / 2;
-                std::nth_element(t.rs.begin(), t.rs.begin() + m, t.rs.end(), [&](const Ref& x, const Ref& y) {
-                    const float cx = x.box.lo[ax] + x.box.hi[ax], cy = y.box.lo[ax] + y.box.hi[ax];
-                    return cx < cy || (cx == cy && x.tri < y.tri);
                 });
-                L.assign(t.rs.begin(), t.rs.begin() + m);
-                R.assign(t.rs.begin() + m, t.rs.end());
+                concat(Lk, K, L);
+                concat(Rk, K, R);
+                for (size_t k = 0; k < K; ++k) dup += dk[k];
+                if (L.empty() || R.empty()) {
+                    L.clear();
+                    R.clear();
+                    dup = 0;
+                }
             }
-            std::vector<Ref>().swap(t.rs);
-            const int32_t c0 = int32_t(tree.size()), c1 = c0 + 1;
-            tree.emplace_back();
-            tree.emplace_back();
-            tree[t.node].child[0] = c0;
-            tree[t.node].child[1] = c1;
-            stack.push_back(Task{c1, std::move(R), t.depth + 1});
-            stack.push_back(Task{c0, std::move(L), t.depth + 1});
+            if (L.empty() && os.axis >= 0) {
+                const size_t nk = max_chunks(n);
+                std::vector<std::vector<Ref>> Lk(nk), Rk(nk);
+                if (nk == 1) {
+                    Lk[0].reserve(n / 2 + 16);
+                    Rk[0].reserve(n / 2 + 16);
+                }
+                const size_t K = chunked(n, [&](size_t k, size_t b, size_t e) {
+                    for (size_t i = b; i < e; ++i) {
+                        const Ref& r = rs[i];
+                        int j = int((0.5f * (r.box.lo[os.axis] + r.box.hi[os.axis]) - os.lo) * os.scale);
+                        j = std::min(std::max(j, 0), kBins - 1);
+                        (j <= os.bin ? Lk[k] : Rk[k]).push_back(r);
+                    }
+                });
+                concat(Lk, K, L);
+                concat(Rk, K, R);
+                if (L.empty() || R.empty()) {
+                    L.clear();
+                    R.clear();
+                }
+            }
         }
-        // subtree ranges: children follow their parent, and DFS left-first emission keeps each
-        // subtree's references contiguous
+        if (L.empty()) {  // object median along the widest centroid axis
+            Box cb;
+            for (const Ref& r : rs) {
+                float c[3];
+                for (int k = 0; k < 3; ++k) c[k] = 0.5f * (r.box.lo[k] + r.box.hi[k]);
+                cb.grow(c);
+            }
+            int ax = 0;
+            for (int k = 1; k < 3; ++k)
+                if (cb.hi[k] - cb.lo[k] > cb.hi[ax] - cb.lo[ax]) ax = k;
+            const size_t m = n / 2;
+            std::nth_element(rs.begin(), rs.begin() + m, rs.end(), [&](const Ref& x, const Ref& y) {
+                const float cx = x.box.lo[ax] + x.box.hi[ax], cy = y.box.lo[ax] + y.box.hi[ax];
+                return cx < cy || (cx == cy && x.tri < y.tri);
+            });
+            L.assign(rs.begin(), rs.begin() + m);
+            R.assign(rs.begin() + m, rs.end());
+        }
+        return dup;
+    }
+
+    // A subtree in pre-order (node 0 its root, children after their parent, left subtree before right), its
+    // leaves' references in the same order.
+    struct Sub {
+        std::vector<TNode> nodes;
+        std::vector<uint32_t> refs;
+        bool deep = false;  // the depth cap was exceeded
+        bool oom = false;   // a task ran out of memory
+    };
+
+    // Appends subtree src to dst; returns the index of its root in dst.
+    static int32_t append(Sub& dst, const Sub& src) {
+        const int32_t off = int32_t(dst.nodes.size());
+        const uint32_t roff = uint32_t(dst.refs.size());
+        for (TNode nd : src.nodes) {
+            if (nd.count) nd.first += roff;
+            else {
+                nd.child[0] += off;
+                nd.child[1] += off;
+            }
+            dst.nodes.push_back(nd);
+        }
+        dst.refs.insert(dst.refs.end(), src.refs.begin(), src.refs.end());
+        dst.deep |= src.deep;
+        dst.oom |= src.oom;
+        return off;
+    }
+
+    // Builds the subtree of `rs` (consumed) into out; returns the index of its root.
+    int32_t build_rec(Sub& out, std::vector<Ref>& rs, uint32_t depth, size_t budget) {
+        const int32_t idx = int32_t(out.nodes.size());
+        out.nodes.emplace_back();
+        const Box nb = bounds_of(rs);
+        out.nodes[size_t(idx)].box = nb;
+        const size_t n = rs.size();
+        if (n <= 1) {
+            TNode& t = out.nodes[size_t(idx)];
+            t.first = uint32_t(out.refs.size());
+            t.count = uint32_t(n);
+            for (const Ref& r : rs) out.refs.push_back(r.tri);
+            return idx;
+        }
+        if (depth + 1 > depth_cap) {
+            out.deep = true;
+            return idx;
+        }
+        std::vector<Ref> L, R;
+        const size_t dup = split_node(rs, nb, depth, budget, L, R);
+        std::vector<Ref>().swap(rs);
+        // the allowance left after this split, shared in proportion to the children's references
+        const size_t rest = budget > dup ? budget - dup : 0;
+        const size_t bl = size_t(double(rest) * double(L.size()) / double(L.size() + R.size()));
+        const size_t br = rest - bl;
+        int32_t c0, c1;
+        if (pool && pool->parallel() && L.size() >= kTaskRefs && R.size() >= kTaskRefs) {
+            Sub sr;
+            std::atomic<bool> done{false};
+            pool->submit([&] {
+                try {
+                    build_rec(sr, R, depth + 1, br);
+                } catch (...) {  // bad_alloc: reported by the caller, never thrown across threads
+                    sr.oom = true;
+                }
+                done.store(true, std::memory_order_release);
+            });
+            c0 = build_rec(out, L, depth + 1, bl);
+            pool->wait(done);
+            c1 = append(out, sr);
+        } else {
+            c0 = build_rec(out, L, depth + 1, bl);
+            c1 = build_rec(out, R, depth + 1, br);
+        }
+        out.nodes[size_t(idx)].child[0] = c0;
+        out.nodes[size_t(idx)].child[1] = c1;
+        return idx;
+    }
+
+    bool build(uint32_t ntris, const std::vector<Box>& tri_box, std::string& err) {
+        std::vector<Ref> all(ntris);
+        for (uint32_t t = 0; t < ntris; ++t) all[t] = Ref{t, tri_box[t]};
+        root_area = std::max(bounds_of(all).area(), 1e-30);
+        Sub root;
+        root.nodes.reserve(size_t(ntris) * 4);
+        root.refs.reserve(std::max(ref_budget, size_t(ntris)) + size_t(ntris) / 4);
+        {
+            TaskPool tp(threads);
+            pool = &tp;
+            try {
+                build_rec(root, all, 0, ref_budget > ntris ? ref_budget - ntris : 0);
+            } catch (...) {
+                root.oom = true;
+            }
+            pool = nullptr;
+        }
+        if (root.oom) {
+            err = "build_bvh: out of memory";
+            return false;
+        }
+        if (root.deep) {
+            err = "build_bvh: depth cap exceeded";
+            return false;
+        }
+        tree.swap(root.nodes);
+        refs.swap(root.refs);
+        // subtree ranges: children follow their parent, and each subtree's references are contiguous
+        // (pre-order, left before right)
         sah = 0.0;
         for (size_t i = tree.size(); i-- > 0;) {
             TNode& nd = tree[i];
             if (!nd.count) {
-                nd.begin = tree[nd.child[0]].begin;
-                nd.end = tree[nd.child[1]].end;
+                nd.begin = tree[size_t(nd.child[0])].begin;
+                nd.end = tree[size_t(nd.child[1])].end;
                 sah += nd.box.area() / root_area;
             } else {
+                nd.begin = nd.first;
+                nd.end = nd.first + nd.count;
                 sah += nd.box.area() / root_area * double(nd.count);
             }
         }
@@ -607,7 +897,8 @@ void restructure_treelet(std::vector<TNode>& tree, std::vector<double>& cost, in
     build(full);
 }
 
-void restructure_treelets(std::vector<TNode>& tree, std::vector<uint32_t>& refs, int passes, const uint8_t* alpha) {
+void restructure_treelets(std::vector<TNode>& tree, std::vector<uint32_t>& refs, int passes, const uint8_t* alpha,
+                          unsigned threads) {
     const size_t nn = tree.size();
     if (nn < 3) return;
     std::vector<double> cost(nn, 0.0);
@@ -630,7 +921,7 @@ void restructure_treelets(std::vector<TNode>& tree, std::vector<uint32_t>& refs,
             st.push_back({tree[size_t(n)].child[0], false});
         }
     };
-    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned hw = std::max(1u, threads);
     for (int pass = 0; pass < passes; ++pass) {
         // costs bottom-up and depths top-down over the current topology
         std::vector<int32_t> all;
@@ -807,52 +1098,85 @@ struct Emit8 {
     static uint32_t ntris(const TNode& n) { return n.end - n.begin; }
     bool is_leaf(int32_t t) const { return pick[size_t(t) * 8 + 1] == 0; }
 
-    void solve() {
+    // C / D of binary node ni (its children's already final).
+    void solve_node(size_t ni) {
+        const TNode& n = tree[ni];
+        const double A = n.box.area();
+        double* C = &cost[ni * 8];
+        uint8_t* P = &pick[ni * 8];
+        const double leaf = ntris(n) <= uint32_t(kMaxLeafTris8) ? A * kCPrim * double(ntris(n)) : DBL_MAX;
+        if (n.count) {  // binary leaf
+            for (int i = 1; i < 8; ++i) { C[i] = leaf; P[i] = 0; }
+            C[0] = DBL_MAX;
+            return;
+        }
+        const double* L = &cost[size_t(n.child[0]) * 8];
+        const double* R = &cost[size_t(n.child[1]) * 8];
+        auto D = [&](int i, uint8_t& bk) {
+            double best = DBL_MAX;
+            for (int k = 1; k < i; ++k) {
+                double c = L[k] + R[i - k];
+                if (c < best) { best = c; bk = uint8_t(k); }
+            }
+            return best;
+        };
+        uint8_t k8 = 1;
+        const double d8 = D(8, k8);
+        dsplit[ni] = k8;
+        C[0] = d8;
+        const double node = A * kCNode + d8;
+        C[1] = std::min(leaf, node);
+        P[1] = leaf <= node ? 0 : 1;
+        for (int i = 2; i < 8; ++i) {
+            uint8_t k = 1;
+            const double d = D(i, k);
+            if (d < C[i - 1]) { C[i] = d; P[i] = k; }
+            else { C[i] = C[i - 1]; P[i] = 0; }
+        }
+    }
+
+    // Every node's C / D, bottom-up: the binary tree's breadth-first levels, deepest first, each level's
+    // nodes in parallel (a node reads only its children's results).
+    void solve(TaskPool& pool) {
         const size_t nn = tree.size();
         cost.assign(nn * 8, 0.0);
         pick.assign(nn * 8, 0);
         dsplit.assign(nn, 0);
-        // children have larger indices than their parent (builder appends), so a reverse sweep is
-        // a post-order
-        for (size_t ni = nn; ni-- > 0;) {
-            const TNode& n = tree[ni];
-            const double A = n.box.area();
-            double* C = &cost[ni * 8];
-            uint8_t* P = &pick[ni * 8];
-            const double leaf = ntris(n) <= uint32_t(kMaxLeafTris8) ? A * kCPrim * double(ntris(n)) : DBL_MAX;
-            if (n.count) {  // binary leaf
-                for (int i = 1; i < 8; ++i) { C[i] = leaf; P[i] = 0; }
-                C[0] = DBL_MAX;
+        std::vector<int32_t> bfs;
+        bfs.reserve(nn);
+        std::vector<size_t> level_end;
+        bfs.push_back(0);
+        for (size_t b = 0; b < bfs.size();) {
+            const size_t e = bfs.size();
+            for (size_t i = b; i < e; ++i)
+                if (!tree[size_t(bfs[i])].count) {
+                    bfs.push_back(tree[size_t(bfs[i])].child[0]);
+                    bfs.push_back(tree[size_t(bfs[i])].child[1]);
+                }
+            level_end.push_back(e);
+            b = e;
+        }
+        for (size_t l = level_end.size(); l-- > 0;) {
+            const size_t b = l ? level_end[l - 1] : 0, n = level_end[l] - b;
+            const size_t K = pool.parallel() && n >= 4096 ? std::min<size_t>(size_t(threads) * 4u, n / 1024u) : 1u;
+            if (K <= 1) {
+                for (size_t i = b; i < b + n; ++i) solve_node(size_t(bfs[i]));
                 continue;
             }
-            const double* L = &cost[size_t(n.child[0]) * 8];
-            const double* R = &cost[size_t(n.child[1]) * 8];
-            auto D = [&](int i, uint8_t& bk) {
-                double best = DBL_MAX;
-                for (int k = 1; k < i; ++k) {
-                    double c = L[k] + R[i - k];
-                    if (c < best) { best = c; bk = uint8_t(k); }
-                }
-                return best;
-            };
-            uint8_t k8 = 1;
-            const double d8 = D(8, k8);
-            dsplit[ni] = k8;
-            C[0] = d8;
-            const double node = A * kCNode + d8;
-            C[1] = std::min(leaf, node);
-            P[1] = leaf <= node ? 0 : 1;
-            for (int i = 2; i < 8; ++i) {
-                uint8_t k = 1;
-                const double d = D(i, k);
-                if (d < C[i - 1]) { C[i] = d; P[i] = k; }
-                else { C[i] = C[i - 1]; P[i] = 0; }
-            }
+            std::atomic<size_t> left{K - 1};
+            std::atomic<bool> done{false};
+            for (size_t k = 1; k < K; ++k)
+                pool.submit([&, k] {
+                    for (size_t i = b + n * k / K; i < b + n * (k + 1) / K; ++i) solve_node(size_t(bfs[i]));
+                    if (left.fetch_sub(1) == 1) done.store(true, std::memory_order_release);
+                });
+            for (size_t i = b; i < b + n / K; ++i) solve_node(size_t(bfs[i]));
+            pool.wait(done);
         }
     }
 
     // Children of binary subtree t occupying at most i slots.
-    void expand(int32_t t, int i, std::vector<int32_t>& ch) {
+    void expand(int32_t t, int i, std::vector<int32_t>& ch) const {
         while (i > 1 && pick[size_t(t) * 8 + i] == 0) --i;
         if (i == 1 || tree[t].count) {
             ch.push_back(t);
@@ -864,7 +1188,7 @@ struct Emit8 {
     }
 
     // The wide node for binary subtree t: its children per D(t, 8).
-    void gather_children(int32_t t, std::vector<int32_t>& ch) {
+    void gather_children(int32_t t, std::vector<int32_t>& ch) const {
         ch.clear();
         if (tree[t].count) {
             ch.push_back(t);
@@ -875,8 +1199,16 @@ struct Emit8 {
         expand(tree[t].child[1], 8 - k, ch);
     }
 
-    void emit(uint32_t idx, int32_t t, uint32_t depth) {
-        max_depth = std::max(max_depth, depth);
+    // The wide node for binary subtree t, except its child and triangle bases: slot assignment, quantised
+    // child boxes, leaf metadata.  Depends on t alone, so the nodes of a level are planned in parallel.
+    struct Plan {
+        Bvh8Node node;
+        int32_t slot_of[8];
+        uint32_t n_internal = 0, n_tris = 0;
+    };
+
+    void plan(int32_t t, Plan& P) const {
+        P.n_internal = P.n_tris = 0;
         std::vector<int32_t> ch;
         gather_children(t, ch);
         // slot assignment: slot s is nearest for rays of octant 7 ^ s (greedy auction on centroids)
@@ -884,31 +1216,36 @@ struct Emit8 {
         for (int32_t c : ch) nb.grow(tree[c].box);
         float pc[3];
         for (int k = 0; k < 3; ++k) pc[k] = 0.5f * (nb.lo[k] + nb.hi[k]);
-        int32_t slot_of[8];
+        int32_t* slot_of = P.slot_of;
         std::fill(slot_of, slot_of + 8, -1);
-        std::vector<bool> used(ch.size(), false);
-        std::vector<bool> taken(8, false);
+        bool used[8] = {false, false, false, false, false, false, false, false};
+        bool taken[8] = {false, false, false, false, false, false, false, false};
+        float cost_cs[8][8];
+        for (size_t c = 0; c < ch.size(); ++c) {
+            const Box& b = tree[ch[c]].box;
+            float off[3];
+            for (int k = 0; k < 3; ++k) off[k] = 0.5f * (b.lo[k] + b.hi[k]) - pc[k];
+            for (int s = 0; s < 8; ++s) {
+                const int o = 7 ^ s;  // the octant for which slot s is visited first
+                cost_cs[c][s] = -(off[0] * sgn(o, 4) + off[1] * sgn(o, 2) + off[2] * sgn(o, 1));
+            }
+        }
         for (size_t round = 0; round < ch.size(); ++round) {
             float best = -FLT_MAX;
             int bc = -1, bs = -1;
             for (size_t c = 0; c < ch.size(); ++c) {
                 if (used[c]) continue;
-                const Box& b = tree[ch[c]].box;
-                float off[3];
-                for (int k = 0; k < 3; ++k) off[k] = 0.5f * (b.lo[k] + b.hi[k]) - pc[k];
                 for (int s = 0; s < 8; ++s) {
                     if (taken[s]) continue;
-                    const int o = 7 ^ s;  // the octant for which slot s is visited first
-                    float cost = -(off[0] * sgn(o, 4) + off[1] * sgn(o, 2) + off[2] * sgn(o, 1));
-                    if (cost > best) { best = cost; bc = int(c); bs = s; }
+                    if (cost_cs[c][s] > best) { best = cost_cs[c][s]; bc = int(c); bs = s; }
                 }
             }
             used[bc] = true;
             taken[bs] = true;
             slot_of[bs] = ch[bc];
         }
-        Bvh8Node& n0 = nodes[idx];
-        std::memset(&n0, 0, sizeof(Bvh8Node));
+        Bvh8Node& n = P.node;
+        std::memset(&n, 0, sizeof(Bvh8Node));
         // quantisation frame: padded union box
         Box pb[8];
         Box ub;
@@ -919,7 +1256,7 @@ struct Emit8 {
             }
         float scale[3];
         for (int k = 0; k < 3; ++k) {
-            n0.p[k] = ub.lo[k];
+            n.p[k] = ub.lo[k];
             float ext = ub.hi[k] - ub.lo[k];
             int e = -100;
             if (ext > 0.0f) {
@@ -931,28 +1268,16 @@ struct Emit8 {
                 bool ok = true;
                 for (int s = 0; s < 8 && ok; ++s) {
                     if (slot_of[s] < 0) continue;
-                    double qh = std::ceil((double(pb[s].hi[k]) - n0.p[k]) / scale[k]);
+                    double qh = std::ceil((double(pb[s].hi[k]) - n.p[k]) / scale[k]);
                     if (qh > 255.0) ok = false;
-                    else if (std::fmaf(float(qh), scale[k], n0.p[k]) < pb[s].hi[k] && qh + 1.0 > 255.0) ok = false;
+                    else if (std::fmaf(float(qh), scale[k], n.p[k]) < pb[s].hi[k] && qh + 1.0 > 255.0) ok = false;
                 }
                 if (ok) break;
                 ++e;
             }
-            n0.e[k] = uint8_t(e + 127);
+            n.e[k] = uint8_t(e + 127);
         }
-        // children
-        uint32_t n_internal = 0;
-        for (int s = 0; s < 8; ++s)
-            if (slot_of[s] >= 0 && !is_leaf(slot_of[s])) n_internal++;
-        const uint32_t base_child = uint32_t(nodes.size());
-        const uint32_t base_tri = uint32_t(tri_order.size());
-        nodes.resize(nodes.size() + n_internal);
-        Bvh8Node& n = nodes[idx];  // (re-fetched: the resize may have moved the array)
-        n.base_child = base_child;
-        n.base_tri = base_tri;
-        uint32_t tri_off = 0, rank = 0;
-        int32_t child_node[8];
-        std::fill(child_node, child_node + 8, -1);
+        uint32_t tri_off = 0;
         for (int s = 0; s < 8; ++s) {
             if (slot_of[s] < 0) {  // empty slot: an inverted box the slab test never enters, meta 0
                 for (int k = 0; k < 3; ++k) {
@@ -975,37 +1300,72 @@ struct Emit8 {
             if (is_leaf(slot_of[s])) {
                 const uint32_t cnt = ntris(c);
                 n.meta[s] = uint8_t((cnt << 5) | tri_off);
-                for (uint32_t i = c.begin; i < c.end; ++i) tri_order.push_back(refs[i]);
                 tri_off += cnt;
-                leaves++;
             } else {
                 n.imask |= uint8_t(1u << s);
                 n.meta[s] = uint8_t(kMetaInternal | s);
-                child_node[s] = int32_t(base_child + rank);
-                rank++;
+                P.n_internal++;
             }
         }
-        for (int s = 0; s < 8; ++s)
-            if (child_node[s] >= 0) pending.push_back({uint32_t(child_node[s]), slot_of[s], depth + 1});
+        P.n_tris = tri_off;
     }
 
     // Breadth-first emission: the wide nodes of each level are contiguous and the top levels come
     // first, so a prefix of the node array is the top of the tree (the levels every ray visits stay
-    // together in the caches).  A node's internal children stay contiguous.
+    // together in the caches).  A node's internal children stay contiguous.  Each level is planned in
+    // parallel, then numbered in level order -- the numbering of one serial breadth-first pass.
     struct Pending {
         uint32_t idx;
         int32_t t;
-        uint32_t depth;
     };
-    std::vector<Pending> pending;
+    unsigned threads = 1;
 
     void run() {
-        solve();
+        TaskPool pool(threads);
+        solve(pool);
         nodes.emplace_back();
-        pending.push_back({0u, 0, 0u});
-        for (size_t q = 0; q < pending.size(); ++q) {
-            const Pending p = pending[q];
-            emit(p.idx, p.t, p.depth);
+        std::vector<Pending> level{{0u, 0}}, next;
+        std::vector<Plan> plans;
+        for (uint32_t depth = 0; !level.empty(); ++depth) {
+            max_depth = std::max(max_depth, depth);
+            plans.resize(level.size());
+            const size_t K = pool.parallel() && level.size() >= 64 ? std::min<size_t>(size_t(threads) * 4u, level.size() / 16u) : 1u;
+            if (K <= 1) {
+                for (size_t i = 0; i < level.size(); ++i) plan(level[i].t, plans[i]);
+            } else {
+                std::atomic<size_t> left{K - 1};
+                std::atomic<bool> done{false};
+                const size_t n = level.size();
+                for (size_t k = 1; k < K; ++k)
+                    pool.submit([&, k] {
+                        for (size_t i = n * k / K; i < n * (k + 1) / K; ++i) plan(level[i].t, plans[i]);
+                        if (left.fetch_sub(1) == 1) done.store(true, std::memory_order_release);
+                    });
+                for (size_t i = 0; i < n / K; ++i) plan(level[i].t, plans[i]);
+                pool.wait(done);
+            }
+            next.clear();
+            for (size_t i = 0; i < level.size(); ++i) {
+                const Plan& P = plans[i];
+                const uint32_t base_child = uint32_t(nodes.size());
+                nodes.resize(nodes.size() + P.n_internal);
+                Bvh8Node& n = nodes[level[i].idx];
+                n = P.node;
+                n.base_child = base_child;
+                n.base_tri = uint32_t(tri_order.size());
+                uint32_t rank = 0;
+                for (int s = 0; s < 8; ++s) {
+                    const int32_t c = P.slot_of[s];
+                    if (c < 0) continue;
+                    if (is_leaf(c)) {
+                        for (uint32_t r = tree[c].begin; r < tree[c].end; ++r) tri_order.push_back(refs[r]);
+                        leaves++;
+                    } else {
+                        next.push_back({base_child + rank++, c});
+                    }
+                }
+            }
+            level.swap(next);
         }
     }
 };
@@ -1068,43 +1428,67 @@ bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildRe
     else caps.assign(std::begin(kCaps), std::end(kCaps));
     uint32_t last_depth = 0;
     const bool spatial = !params || params->spatial_splits;
-    for (uint32_t cap : caps) {
-        double sah = 0.0;
-        SpatialBuilder SB;
-        const std::vector<TNode>* tree = &B.tree;
-        const std::vector<uint32_t>* refs = &B.refs;
-        if (spatial) {
-            SB.pos = tri_positions;
-            SB.keep_whole = params ? params->keep_whole : nullptr;
-            SB.depth_cap = cap;
-            SB.ref_budget = size_t(double(ntris) * (params ? params->ref_budget : BvhBuildParams().ref_budget));
-            if (!SB.build(ntris, B.tri_box, err)) return false;
-            const uint32_t tp = params ? params->treelet_passes : BvhBuildParams().treelet_passes;
-            if (tp > 0) restructure_treelets(SB.tree, SB.refs, int(tp), params ? params->keep_whole : nullptr);
-            sah = tp > 0 ? tree_sah(SB.tree) : SB.sah;
-            tree = &SB.tree;
-            refs = &SB.refs;
-        } else {
-            for (uint32_t t = 0; t < ntris; ++t) B.refs[t] = t;
-            B.depth_cap = cap;
-            if (!B.build(ntris, err, sah)) return false;
+    const uint32_t tp_param = params ? params->treelet_passes : BvhBuildParams().treelet_passes;
+    // the treelet passes re-wire subtrees without regard to the depth cap: when no cap gives a shallow enough
+    // tree with them, the caps are tried again without them
+    std::vector<std::pair<uint32_t, uint32_t>> tries;  // (binary depth cap, treelet passes)
+    for (uint32_t tp : {tp_param, 0u}) {
+        if (tp == 0u && tp_param == 0u && !tries.empty()) break;
+        for (uint32_t cap : caps) tries.push_back({cap, spatial ? tp : 0u});
+        if (!spatial) break;
+    }
+    {
+        for (const auto& [cap, tp] : tries) {
+            double sah = 0.0;
+            SpatialBuilder SB;
+            const std::vector<TNode>* tree = &B.tree;
+            const std::vector<uint32_t>* refs = &B.refs;
+            double ph[3] = {0.0, 0.0, 0.0};
+            auto tick = std::chrono::steady_clock::now();
+            auto lap = [&](int k) {
+                const auto now = std::chrono::steady_clock::now();
+                ph[k] = std::chrono::duration<double, std::milli>(now - tick).count();
+                tick = now;
+            };
+            if (spatial) {
+                SB.pos = tri_positions;
+                SB.keep_whole = params ? params->keep_whole : nullptr;
+                SB.depth_cap = cap;
+                SB.threads = build_threads(params);
+                SB.ref_budget = size_t(double(ntris) * (params ? params->ref_budget : BvhBuildParams().ref_budget));
+                if (!SB.build(ntris, B.tri_box, err)) return false;
+                lap(0);
+                if (tp > 0) restructure_treelets(SB.tree, SB.refs, int(tp), params ? params->keep_whole : nullptr, SB.threads);
+                lap(1);
+                sah = tp > 0 ? tree_sah(SB.tree) : SB.sah;
+                tree = &SB.tree;
+                refs = &SB.refs;
+            } else {
+                for (uint32_t t = 0; t < ntris; ++t) B.refs[t] = t;
+                B.depth_cap = cap;
+                if (!B.build(ntris, err, sah)) return false;
+                lap(0);
+            }
+            Emit8 E{*tree, *refs, pad, {}, {}, 0, 0, 1.0, params ? params->leaf_cost : BvhBuildParams().leaf_cost, {}, {}, {}, build_threads(params)};
+            E.run();
+            lap(2);
+            last_depth = E.max_depth;
+            if (E.max_depth > max_depth8) continue;
+            if (E.tri_order.size() != refs->size()) {
+                err = "build_bvh: BVH8 emission lost triangles";
+                return false;
+            }
+            out.sah_cost = sah;
+            out.wide_sah = (tree->front().box.area() + E.cost[0]) / tree->front().box.area();
+            out.nodes8 = std::move(E.nodes);
+            out.tri_order = std::move(E.tri_order);
+            out.max_depth = E.max_depth;
+            out.num_leaves = E.leaves;
+            out.binary_depth_cap = cap;
+            out.treelet_passes = spatial ? tp : 0u;
+            for (int k = 0; k < 3; ++k) out.phase_ms[k] = ph[k];
+            return true;
         }
-        Emit8 E{*tree, *refs, pad, {}, {}, 0, 0, 1.0, params ? params->leaf_cost : BvhBuildParams().leaf_cost, {}, {}, {}, {}};
-        E.run();
-        last_depth = E.max_depth;
-        if (E.max_depth > max_depth8) continue;
-        if (E.tri_order.size() != refs->size()) {
-            err = "build_bvh: BVH8 emission lost triangles";
-            return false;
-        }
-        out.sah_cost = sah;
-        out.wide_sah = (tree->front().box.area() + E.cost[0]) / tree->front().box.area();
-        out.nodes8 = std::move(E.nodes);
-        out.tri_order = std::move(E.tri_order);
-        out.max_depth = E.max_depth;
-        out.num_leaves = E.leaves;
-        out.binary_depth_cap = cap;
-        return true;
     }
     err = "build_bvh: BVH8 deeper than the traversal stack (" + std::to_string(last_depth) + ")";
     return false;

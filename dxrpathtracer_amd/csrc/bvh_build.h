@@ -22,6 +22,8 @@ struct BvhBuildResult {
     double sah_cost = 0.0;            // binary tree, C_trav = 1, C_tri = 1, relative to root area
     double wide_sah = 0.0;            // BVH8: the collapse's cost (C_node = 1, C_tri = leaf_cost), relative to root area
     uint32_t binary_depth_cap = 0;    // BVH8: depth cap of the binary tree that was collapsed
+    uint32_t treelet_passes = 0;      // BVH8: treelet passes of the tree that was collapsed
+    double phase_ms[3] = {0.0, 0.0, 0.0};  // BVH8: binary (SBVH) build, treelet passes, collapse + emission
 };
 
 // Optional builder parameters (diagnostics; the product uses the defaults).
@@ -45,11 +47,15 @@ struct BvhBuildParams {
 #define DXRPT_TREELET_PASSES 1
 #endif
     uint32_t treelet_passes = DXRPT_TREELET_PASSES;
+    // host threads of the build (0: the host's CPUs, at most 16); the tree does not depend on it
+    unsigned threads = 0;
 };
 
 // tri_positions: ntris * 9 floats (v0.xyz, v1.xyz, v2.xyz) in global triangle order.
 // width 2 -> BVH2 (leaves <= kMaxLeafTris), width 8 -> compressed BVH8 (leaves <= kMaxLeafTris8).
-// Deterministic: the same input always yields the same tree.
+// Deterministic: the same input always yields the same tree, whatever the thread count.
+// BVH8: the binary depth cap is tightened until the wide tree fits kTraversalStack8 - 1 levels; at each cap a
+// tree whose treelet passes made it too deep is first rebuilt without them.
 bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildResult& out, std::string& err,
                const BvhBuildParams* params = nullptr);
 

@@ -21,6 +21,7 @@
 #include <new>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/dxrpt.h"
@@ -111,6 +112,7 @@ struct dxrpt_ctx {
     dxrpt_stats last{};
     int last_L = 0;
     bool rendered = false;
+    bool last_counted = false;  // the last render ran a counting (census) frame: dxrpt_get_stats reads d_trav
     // stream ordering: the stream of the last enqueuing call, whether anything may still be in flight
     hipStream_t last_stream = nullptr;
     bool have_last = false;
@@ -614,6 +616,14 @@ int dxrpt_destroy(dxrpt_ctx* ctx) {
 
 const char* dxrpt_last_error(const dxrpt_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+// include/dxrpt.h DXRPT_RETIRED_OPTIONS: the one list of retired ids
+static bool option_retired(uint32_t option) {
+    static const uint32_t kRetired[] = DXRPT_RETIRED_OPTIONS;
+    for (uint32_t r : kRetired)
+        if (r == option) return true;
+    return false;
+}
+
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
     if (!ctx) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
@@ -676,9 +686,10 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
             require(value <= 1, "dxrpt_set_option: opacity micromap must be 0 (off) or 1 (on)");
             drain_frames(ctx);  // in-flight frames may read the micromap
             ctx->opt_omm = uint32_t(value);
-        } else if ((option >= 3 && option <= 11) || (option >= 14 && option <= 17) || option == 19 || option == 21 ||
-                   option == 22 || option == 26 || option == 27 || option == 30 || option == 35 || option == 38 ||
-                   option == 39) {
+        } else if (option == DXRPT_OPT_BVH_THREADS) {
+            require(value <= 256, "dxrpt_set_option: BVH build threads must be 0 (default) or 1..256");
+            ctx->build_params.threads = unsigned(value);
+        } else if (option_retired(option)) {
             throw ApiError(DXRPT_E_UNSUPPORTED, "dxrpt_set_option: option " + std::to_string(option) +
                                                     " was retired in ABI 3 (measured slower or neutral; DESIGN.md §7a)");
         } else {
@@ -858,6 +869,7 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
             ctx->d_tri_verts.upload(tv.data(), tv.size() * sizeof(dxrpt_mesh_vertex));
         }
         auto t1 = std::chrono::steady_clock::now();
+        ctx->bvh = dxrpt_bvh_info{};
         ctx->bvh.num_nodes = uint32_t(res.nodes8.size());
         ctx->bvh.num_leaves = res.num_leaves;
         ctx->bvh.num_tris = ntris;
@@ -867,6 +879,14 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
         ctx->bvh.tri_bytes = sizeof(TriRecord);
         ctx->bvh.build_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
         ctx->bvh.sah_cost = res.sah_cost;
+        ctx->bvh.num_refs = nrefs;
+        for (int k = 0; k < 3; ++k) ctx->bvh.phase_ms[k] = res.phase_ms[k];
+        ctx->bvh.phase_ms[3] = std::max(0.0, ctx->bvh.build_ms - res.phase_ms[0] - res.phase_ms[1] - res.phase_ms[2]);
+        ctx->bvh.wide_sah = res.wide_sah;
+        ctx->bvh.binary_depth_cap = res.binary_depth_cap;
+        ctx->bvh.treelet_passes = res.treelet_passes;
+        ctx->bvh.threads = bp.threads ? bp.threads : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        ctx->bvh.ref_budget_pct = bp.spatial_splits ? uint32_t(bp.ref_budget * 100.0 + 0.5) : 0u;
         ctx->spill_threads = 0;  // the depth may have changed: the next launch re-sizes the spill slabs
         ctx->bvh_built = true;
         ctx->omm_dirty = true;
@@ -984,7 +1004,15 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         enter_stream(ctx, s);
         upload_textures(ctx);
         const uint32_t paths = prepare_tiles(ctx, tiles, num_tiles, width, height, "dxrpt_render");
-        if (paths == 0u) return;  // a tile list without pixels (e.g. a rank of a tiny frame): nothing to do
+        if (paths == 0u) {  // a tile list without pixels (e.g. a rank of a tiny frame): nothing to do, and the
+                            // stats of this call are empty (not the previous frame's)
+            std::memset(&ctx->last, 0, sizeof(ctx->last));
+            ctx->last_L = 0;
+            ctx->last_counted = false;
+            ctx->stat_counters.clear();
+            ctx->rendered = true;
+            return;
+        }
         const uint32_t nl = useLights ? rtc->NumLights : 0u;
         if (nl) {
             std::vector<dxrpt_spot_light> L(lights->Lights, lights->Lights + nl);
@@ -1211,6 +1239,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         ctx->last.paths_per_wave = fp.megakernel ? 64u : 0u;
         ctx->last.occupancy = fp.megakernel ? fp.megakernel_occupancy : 0u;
         ctx->last.tail_occupancy = (sched & DXRPT_SCHED_SPLIT) ? fp.tail_occupancy : 0u;
+        ctx->last_counted = fp.trav != nullptr;
         ctx->rendered = true;
     });
 }
@@ -1234,7 +1263,7 @@ int dxrpt_get_stats(dxrpt_ctx* ctx, dxrpt_stats* out) {
             s.radiance_rays += cnt[d];
             s.shadow_rays += cnt[16 + d];
         }
-        if (ctx->opt_count && ctx->d_trav.p) {
+        if (ctx->last_counted && ctx->d_trav.p) {
             unsigned long long tr[kTravCounters];
             HIP_CHECK(hipMemcpy(tr, ctx->d_trav.p, sizeof(tr), hipMemcpyDeviceToHost));
             const bool mega = (s.schedule & DXRPT_SCHED_CENSUS) != 0;  // the megakernel census counts hits

@@ -57,23 +57,38 @@ void nccl_check(ncclResult_t r, const char* what) {
 
 // Scratch of the un-permute (device tile list + prefix) per thread and HIP device, reused across frames.
 // `done` is recorded after each launch that reads it: a new tile list waits for it before overwriting or
-// freeing the buffer (the last launch may still be queued on a non-blocking caller stream).
+// freeing the buffer (the last launch may still be queued on a non-blocking caller stream).  It is released
+// by dxrpt_multi_release (or dxrpt_comm_destroy) on the thread that used it; a scratch still held at thread
+// exit is left to the process teardown -- no HIP call from a thread_local destructor, which may run after
+// the HIP runtime or RCCL is gone.
 struct UnpermuteScratch {
     int device = -1;
     void* buf = nullptr;
     size_t bytes = 0;
     hipEvent_t done = nullptr;
     std::vector<dxrpt_tile> tiles;
-    ~UnpermuteScratch() {
-        if (device >= 0) (void)hipSetDevice(device);
+    void release() {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (device >= 0) hip_check(hipSetDevice(device), "hipSetDevice");
         if (done) {
-            (void)hipEventSynchronize(done);
-            (void)hipEventDestroy(done);
+            hip_check(hipEventSynchronize(done), "hipEventSynchronize");
+            hip_check(hipEventDestroy(done), "hipEventDestroy");
+            done = nullptr;
         }
-        if (buf) (void)hipFree(buf);
+        if (buf) hip_check(hipFree(buf), "hipFree");
+        buf = nullptr;
+        bytes = 0;
+        tiles.clear();
+        if (cur >= 0) (void)hipSetDevice(cur);
     }
 };
 thread_local std::vector<std::unique_ptr<UnpermuteScratch>> g_scratch;
+
+void release_scratch() {
+    for (auto& s : g_scratch) s->release();
+    g_scratch.clear();
+}
 thread_local std::string g_err;
 
 UnpermuteScratch& scratch_for_current_device() {
@@ -181,7 +196,12 @@ int dxrpt_comm_create(int hip_device, int nranks, int rank, const void* id, void
 int dxrpt_comm_destroy(void* comm) {
     return guarded([&] {
         if (comm) nccl_check(ncclCommDestroy(static_cast<ncclComm_t>(comm)), "ncclCommDestroy");
+        release_scratch();
     });
+}
+
+int dxrpt_multi_release(void) {
+    return guarded([&] { release_scratch(); });
 }
 
 int dxrpt_comm_info(void* comm, int* nranks, int* rank) {

@@ -1579,15 +1579,21 @@ PT_DEV void split_finish(const KArgs& A, int d, bool cont, uint32_t qpos, bool n
         finish_pixel(A, accumIdx, rad);
 }
 
-// Raygen + depth 1 of every camera path (one 64-path 8x8 block per wave, XCD runs as k_path).
-template <int kOcc>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_path_head(KArgs A) {
-    if (A.F.counters_next && blockIdx.x == 0u)  // the next frame's counter set (see k_path)
-        for (uint32_t i = threadIdx.x; i < kCounterWords; i += blockDim.x) A.F.counters_next[i] = 0u;
-    lut_fill(A.S);
-    const uint32_t blk = A.P.xcd_chunk ? xcd_position(blockIdx.x, gridDim.x, A.P.xcd_chunk) : blockIdx.x;
-    const uint32_t p = blk * blockDim.x + threadIdx.x;  // path slot (shadow-slot index)
-    if (p >= A.P.num_paths) return;
+// Census of a depth-split frame (kCount): each lane's node / triangle fetches and radiance hits (cnt[0..4]
+// depth 1 in the head, cnt[5..9] deeper in the tails, as trace_path counts them), summed over the wave and
+// added with one 64-bit atomic per counter per wave.  All lanes of the wave must call.
+PT_DEV void census_flush(const KArgs& A, const uint32_t (&cnt)[10]) {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        uint32_t v = cnt[k];
+        for (int off = 32; off > 0; off >>= 1) v += uint32_t(__shfl_xor(int(v), off));
+        if ((threadIdx.x & 63u) == 0u && v) atomicAdd(&A.P.trav[k], (unsigned long long)v);
+    }
+}
+
+// Raygen + depth 1 of camera path p (the head's per-lane body).
+template <bool kCount>
+PT_DEV void head_path(const KArgs& A, uint32_t p, uint32_t blk, uint32_t* cnt) {
     const dxrpt_app_settings& set = A.P.set;
     const PrimaryRay pr = primary_ray(A, p);
     const uint32_t packet = (p | 63u) < A.P.num_paths ? A.P.packet : 0u;
@@ -1595,9 +1601,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     HitRec h;
     uint32_t nv = 0, nt = 0;
     if (packet & 1u)  // coherent primary rays: wave-coherent traversal (same results)
-        traverse8_packet<false>(A.S, pr.start, pr.dir, 0.0f, pr.length, 1 <= set.MaxAnyHitPathLength, true, h);
+        traverse8_packet<false, kCount>(A.S, pr.start, pr.dir, 0.0f, pr.length, 1 <= set.MaxAnyHitPathLength, true, h, cnt);
     else
-        traverse8<false, false>(A.S, pr.start, pr.dir, 0.0f, pr.length, 1 <= set.MaxAnyHitPathLength, h, nv, nt);
+        traverse8<false, kCount>(A.S, pr.start, pr.dir, 0.0f, pr.length, 1 <= set.MaxAnyHitPathLength, h, nv, nt);
+    if (kCount) {
+        cnt[0] += nv;
+        cnt[1] += nt;
+        if (h.tri != kMiss) ++cnt[4];
+    }
     VertexIn V;
     V.inOrigin = pr.start;
     V.inDir = pr.dir;
@@ -1621,32 +1632,45 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     rad.x += 1.0f * O.local.x;
     rad.y += 1.0f * O.local.y;
     rad.z += 1.0f * O.local.z;
-    vertex_shadows<false>(A, 1, p, nsh, sun0, packet, rad, nullptr);
+    vertex_shadows<kCount>(A, 1, p, nsh, sun0, packet, rad, cnt);
     split_finish(A, 1, cont, qpos, nextDiffuse, pr.accumIdx, rad);
 }
 
-// Depth d of the paths queued for it (one per lane); waves past the queued count exit at once (the grid
-// covers every path of the frame).
-template <int kOcc>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_path_tail(KArgs A, int d) {
-    const uint32_t* cnt = A.F.counters + uint32_t(d) * kQueueShards;
-    const uint32_t n = queue_total(cnt);
-    const uint32_t nw = (n + 63u) / 64u;  // waves with work
-    // wave j of the queue: XCD runs of A.P.xcd_chunk consecutive queue chunks among the nw live waves
-    // (workgroup b runs on XCD b mod 8; the grid's surplus workgroups exit at once)
-    if (blockIdx.x >= nw) return;
-    const uint32_t j = A.P.xcd_chunk ? xcd_position(blockIdx.x, nw, A.P.xcd_chunk) : blockIdx.x;
+// Raygen + depth 1 of every camera path (one 64-path 8x8 block per wave, XCD runs as k_path).  kCount: the
+// census instantiation of the same code (the traversal orders of the timed head: packet primaries, depth-1
+// sun shadows far to near).
+template <int kOcc, bool kCount = false>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_path_head(KArgs A) {
+    if (A.F.counters_next && blockIdx.x == 0u)  // the next frame's counter set (see k_path)
+        for (uint32_t i = threadIdx.x; i < kCounterWords; i += blockDim.x) A.F.counters_next[i] = 0u;
     lut_fill(A.S);
-    const uint32_t i = j * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    const uint32_t blk = A.P.xcd_chunk ? xcd_position(blockIdx.x, gridDim.x, A.P.xcd_chunk) : blockIdx.x;
+    const uint32_t p = blk * blockDim.x + threadIdx.x;  // path slot (shadow-slot index)
+    if (!kCount) {
+        if (p < A.P.num_paths) head_path<false>(A, p, blk, nullptr);
+        return;
+    }
+    uint32_t cnt[10] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    if (p < A.P.num_paths) head_path<true>(A, p, blk, cnt);
+    census_flush(A, cnt);
+}
+
+// Depth d of queued path i (the tail's per-lane body; j = the lane's queue wave, nw = waves with work).
+template <bool kCount>
+PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw, const uint32_t* cnt_q, uint32_t* cnt) {
     const dxrpt_app_settings& set = A.P.set;
-    const uint32_t pos = queue_pos(cnt, A.F.cap_r, i);
+    const uint32_t pos = queue_pos(cnt_q, A.F.cap_r, i);
     const RayQueue& Q = A.F.q[d & 1];
     HitRec h;
     {
         const float4 o4 = Q.org[pos], d4 = Q.dir[pos];
         uint32_t nv = 0, nt = 0;
-        traverse8<false, false, true, true>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= set.MaxAnyHitPathLength, h, nv, nt);
+        traverse8<false, kCount, true, true>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= set.MaxAnyHitPathLength, h, nv, nt);
+        if (kCount) {
+            cnt[5] += nv;
+            cnt[6] += nt;
+            if (h.tri != kMiss) ++cnt[9];
+        }
     }
     // the rest of the path state comes back from the queue after the traversal (the radiance so far only
     // once the vertex is shaded: it is not live across path_vertex)
@@ -1676,8 +1700,31 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     rad.x += V.pathThr.x * O.local.x;
     rad.y += V.pathThr.y * O.local.y;
     rad.z += V.pathThr.z * O.local.z;
-    vertex_shadows<false, true>(A, d, i, nsh, false, 0u, rad, nullptr);
+    vertex_shadows<kCount, true>(A, d, i, nsh, false, 0u, rad, kCount ? cnt + 5 : nullptr);
     split_finish(A, d, cont, qpos, nextDiffuse, accumIdx, rad);
+}
+
+// Depth d of the paths queued for it (one per lane); waves past the queued count exit at once (the grid
+// covers every path of the frame).  kCount: the census instantiation (the tails' traversal orders: closest
+// hits nearest child first with triangle pairs, any-hit rays far to near).
+template <int kOcc, bool kCount = false>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_path_tail(KArgs A, int d) {
+    const uint32_t* cnt_q = A.F.counters + uint32_t(d) * kQueueShards;
+    const uint32_t n = queue_total(cnt_q);
+    const uint32_t nw = (n + 63u) / 64u;  // waves with work
+    // wave j of the queue: XCD runs of A.P.xcd_chunk consecutive queue chunks among the nw live waves
+    // (workgroup b runs on XCD b mod 8; the grid's surplus workgroups exit at once)
+    if (blockIdx.x >= nw) return;
+    const uint32_t j = A.P.xcd_chunk ? xcd_position(blockIdx.x, nw, A.P.xcd_chunk) : blockIdx.x;
+    lut_fill(A.S);
+    const uint32_t i = j * blockDim.x + threadIdx.x;
+    if (!kCount) {
+        if (i < n) tail_path<false>(A, d, i, j, nw, cnt_q, nullptr);
+        return;
+    }
+    uint32_t cnt[10] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    if (i < n) tail_path<true>(A, d, i, j, nw, cnt_q, cnt);
+    census_flush(A, cnt);
 }
 
 // ---- lightmap baking (Baking.hlsl:336-465, BakeRayGen) -------------------------------------------
@@ -1790,9 +1837,16 @@ uint32_t trace_rays_threads(uint32_t n) { return grid_for(n, kWave) * kWave; }
 
 // The depth-split schedule (FrameParams::split): the head, then one tail launch per depth; head_ev
 // (per-kernel timing) is recorded between them.
-static void launch_split(const KArgs& A, uint32_t gm, size_t lds, hipStream_t s, hipEvent_t head_ev) {
+// census: the counting instantiations of the shipped budgets (head 5, tails 7), whose traversal code is
+// the timed kernels' -- their counts are the fetches of the schedule bench.py times (verdict r04 #2).
+static void launch_split(const KArgs& A, uint32_t gm, size_t lds, hipStream_t s, hipEvent_t head_ev, bool census) {
     const FrameParams& fp = A.P;
     const int L = fp.set.MaxPathLength < 2 ? 2 : fp.set.MaxPathLength;
+    if (census) {
+        hipLaunchKernelGGL((k_path_head<5, true>), dim3(gm), dim3(kWave), lds, s, A);
+        for (int d = 2; d <= L - 1; ++d) hipLaunchKernelGGL((k_path_tail<7, true>), dim3(gm), dim3(kWave), lds, s, A, d);
+        return;
+    }
 #define DXRPT_HEAD(O) hipLaunchKernelGGL((k_path_head<O>), dim3(gm), dim3(kWave), lds, s, A)
     DXRPT_OCC_SWITCH(fp.megakernel_occupancy, DXRPT_HEAD)
 #undef DXRPT_HEAD
@@ -1828,9 +1882,14 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
         const bool ordered = fp.wave_cost || fp.wave_order;
         sched = DXRPT_SCHED_MEGAKERNEL;
         if (ev) (void)hipEventRecord(ev[0], stream);
-        if (count) {  // census frame (DXRPT_OPT_COUNT_TRAVERSAL): the single kernel's counting instantiation,
-                      // with the closest-hit child order of the schedule it stands for (k_path<5> walks
-                      // nearest-first like the split tails and the low-occupancy k_path)
+        if (count && fp.split && !ordered && !fp.wave_clock) {
+            // census frame (DXRPT_OPT_COUNT_TRAVERSAL) of a depth-split frame: the counting head and tails
+            sched |= DXRPT_SCHED_CENSUS | DXRPT_SCHED_SPLIT;
+            launch_split(A, gm, lds, stream, nullptr, true);
+        } else if (count) {  // census frame of the single kernel: its counting instantiation, with the
+                             // traversal orders of the budget it stands for (k_path<5> walks closest hits
+                             // nearest-first and packet shadows near to far like k_path at <= 5 waves/SIMD;
+                             // k_path<7> like k_path at 6-7); with wave clocks, split frames count here too
             sched |= DXRPT_SCHED_CENSUS;
             if ((fp.split && !ordered) || fp.megakernel_occupancy <= 5)
                 hipLaunchKernelGGL((k_path<5, true>), dim3(gm), dim3(kWave), lds, stream, A);
@@ -1838,7 +1897,7 @@ hipError_t launch_frame(const SceneDev& scene, const FrameBuffers& fb, const Fra
                 hipLaunchKernelGGL((k_path<7, true>), dim3(gm), dim3(kWave), lds, stream, A);
         } else if (fp.split && !ordered) {
             sched |= DXRPT_SCHED_SPLIT;
-            launch_split(A, gm, lds, stream, ev ? ev[2] : nullptr);
+            launch_split(A, gm, lds, stream, ev ? ev[2] : nullptr, false);
         } else if (ordered) {  // cost-ordered waves
             sched |= DXRPT_SCHED_ORDER_KERNEL | (fp.wave_order ? DXRPT_SCHED_COST_ORDERED : 0u);
 #define DXRPT_PATH(O) hipLaunchKernelGGL((k_path<O, false, true>), dim3(gm), dim3(kWave), lds, stream, A)

@@ -351,6 +351,7 @@ int main(int argc, char** argv) {
         params.spatial_splits = params.ref_budget > 0.0;
     }
     if (argc > 6) params.treelet_passes = uint32_t(atoi(argv[6]));  // argv[6]: treelet restructuring passes
+    if (argc > 7) params.threads = unsigned(atoi(argv[7]));  // argv[7]: builder threads (0: auto)
     dxrpt_host_scene* hs = nullptr;
     if (dxrpt_host_scene_create(scene_id, 0, 0, &hs) != 0) {
         fprintf(stderr, "scene: %s\n", dxrpt_host_last_error());
@@ -395,6 +396,17 @@ int main(int argc, char** argv) {
                     leaf_tris += n.meta[s] >> 5;
                 }
             }
+    {   // FNV-1a over the emitted layout: identical trees for any thread count
+        uint64_t h = 1469598103934665603ull;
+        auto mix = [&](const void* p, size_t n) {
+            const uint8_t* b = static_cast<const uint8_t*>(p);
+            for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+        };
+        mix(B.nodes8.data(), B.nodes8.size() * sizeof(Bvh8Node));
+        mix(B.tri_order.data(), B.tri_order.size() * sizeof(uint32_t));
+        printf("layout hash %016llx (%zu nodes, %zu refs)\n", (unsigned long long)h, B.nodes8.size(), B.tri_order.size());
+    }
+    printf("phases: sbvh %.0f treelet %.0f collapse %.0f ms (treelet passes %u)\n", B.phase_ms[0], B.phase_ms[1], B.phase_ms[2], B.treelet_passes);
     printf("BVH8: %zu nodes, depth %u (binary cap %u), %.2f children/node, %llu leaves, %.2f tris/leaf, build %.0f ms, SAH(bin) %.2f SAH(wide) %.2f\n",
            B.nodes8.size(), B.max_depth, B.binary_depth_cap, double(slots) / B.nodes8.size(), (unsigned long long)leaves,
            double(leaf_tris) / leaves, ms, B.sah_cost, B.wide_sah);

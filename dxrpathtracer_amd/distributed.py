@@ -232,17 +232,22 @@ class NativeGather:
         uid = C.create_string_buffer(obj[0], A.DXRPT_COMM_ID_BYTES)
         self.comm = C.c_void_p()
         rc = self.L.dxrpt_comm_create(device, layout.world, rank, uid, C.byref(self.comm))
-        ok = [rc == A.DXRPT_OK]
+        # the communicator's own view (what RCCL runs the gather over) is checked in the same collective as
+        # the create result, so every rank raises or continues together
+        nr, rk = C.c_int(), C.c_int()
+        rc_info = self.L.dxrpt_comm_info(self.comm, C.byref(nr), C.byref(rk)) if rc == A.DXRPT_OK else rc
+        mine = (rc == A.DXRPT_OK, rc_info == A.DXRPT_OK and nr.value == layout.world and rk.value == rank)
         oks = [None] * layout.world
-        dist.all_gather_object(oks, ok[0], group=group)
-        if not all(oks):
+        dist.all_gather_object(oks, mine, group=group)
+        if not all(a and b for a, b in oks):
             if rc == A.DXRPT_OK:
                 self.L.dxrpt_comm_destroy(self.comm)
             self.comm = C.c_void_p()
-            raise RuntimeError(f"dxrpt_comm_create failed on ranks {[r for r, v in enumerate(oks) if not v]}: "
-                               f"{self._msg(rc) if rc != A.DXRPT_OK else 'see those ranks'}")
-        nr, rk = C.c_int(), C.c_int()
-        self._check(self.L.dxrpt_comm_info(self.comm, C.byref(nr), C.byref(rk)), "dxrpt_comm_info")
+            bad_create = [r for r, v in enumerate(oks) if not v[0]]
+            bad_info = [r for r, v in enumerate(oks) if v[0] and not v[1]]
+            raise RuntimeError(f"native gather: dxrpt_comm_create failed on ranks {bad_create}, dxrpt_comm_info "
+                               f"disagreed on ranks {bad_info}: "
+                               f"{self._msg(rc if rc != A.DXRPT_OK else rc_info) if not all(mine) else 'see those ranks'}")
         self.comm_ranks, self.comm_rank = nr.value, rk.value  # what RCCL runs the gather over
         self.counts = (C.c_uint64 * layout.world)(*layout.counts)
         self.tiles = gathered_tiles(layout)
@@ -334,3 +339,5 @@ class NativeGather:
             torch.cuda.synchronize()
             self._check(self.L.dxrpt_comm_destroy(self.comm), "dxrpt_comm_destroy")
             self.comm = None
+            # the un-permute scratch of this thread, released while the HIP runtime is up
+            self._check(self.L.dxrpt_multi_release(), "dxrpt_multi_release")

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define DXRPT_ABI_VERSION 3
+#define DXRPT_ABI_VERSION 4
 
 /* ---- status codes ---------------------------------------------------------------------------- */
 #define DXRPT_OK 0
@@ -253,9 +253,18 @@ typedef struct dxrpt_bvh_info {
     uint32_t node_bytes;      /* bytes per node of the layout traversed on the GPU */
     uint32_t tri_bytes;       /* bytes per leaf triangle record */
     uint32_t width;           /* 8: compressed BVH8, 80-B nodes */
-    uint32_t pad;
-    double build_ms;          /* host build time */
+    uint32_t num_refs;        /* leaf triangle references (spatial splits reference a triangle more than once) */
+    double build_ms;          /* host build time, dxrpt_build_bvh call to return (replaces the timed BLAS/TLAS
+                                 build, DXRPathTracer.cpp:2465-2473, logged at :1499-1500) */
     double sah_cost;
+    /* ABI 4: the parts of build_ms -- binary SBVH, treelet passes, BVH8 collapse and emission, and the rest
+       (triangle records, per-triangle vertices, uploads) -- and the build's shape */
+    double phase_ms[4];
+    double wide_sah;          /* SAH cost of the BVH8 collapse (node visit 1, triangle test DXRPT_OPT_LEAF_COST) */
+    uint32_t binary_depth_cap;  /* the binary depth cap the accepted tree was built with */
+    uint32_t treelet_passes;  /* treelet passes of the accepted tree (0 when they made it too deep) */
+    uint32_t threads;         /* builder threads (DXRPT_OPT_BVH_THREADS); the tree does not depend on them */
+    uint32_t ref_budget_pct;  /* spatial-split reference budget, percent of the triangles (DXRPT_OPT_SPATIAL_SPLITS) */
 } dxrpt_bvh_info;
 
 typedef struct dxrpt_ctx dxrpt_ctx;
@@ -295,7 +304,9 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
  * records): 3 BVH_WIDTH, 4-7 wave-pool traversal, 8-11 and 14-15 wavefront launch shapes and budgets,
  * 16 CONCURRENCY, 17 TRAVERSAL_PIPELINE, 19 LDS_NODES, 21 XCD_MAPPING, 22 PACKET_SWITCH,
  * 26 MEGAKERNEL_PERSISTENT, 27 MEGAKERNEL_LANES (path groups), 30 SPLIT_UNITS, 35 SPLIT_PARTS,
- * 38 SPLIT_BINS, 39 SPLIT_ALPHA.  dxrpt_set_option rejects them with DXRPT_E_UNSUPPORTED. */
+ * 38 SPLIT_BINS, 39 SPLIT_ALPHA.  dxrpt_set_option rejects them with DXRPT_E_UNSUPPORTED, ids that were
+ * never assigned with DXRPT_E_INVALID_ARG.  The list, once (the library and the tests read it here): */
+#define DXRPT_RETIRED_OPTIONS {3u, 4u, 5u, 6u, 7u, 8u, 9u, 10u, 11u, 14u, 15u, 16u, 17u, 19u, 21u, 22u, 26u, 27u, 30u, 35u, 38u, 39u}
 #define DXRPT_OPT_COUNT_TRAVERSAL 1u  /* 1: instrumented kernels of the same schedule count node / triangle
                                          fetches (slower; images identical) */
 #define DXRPT_OPT_KERNEL_TIMING 2u    /* 1: record hipEvents around the launches of dxrpt_render */
@@ -374,6 +385,10 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                         built) before the collapse to BVH8, 0..8 (default 1).  Identical
                                         results (the closest hit does not depend on the tree); only node
                                         visits change. */
+#define DXRPT_OPT_BVH_THREADS 41u    /* BVH8 build: host threads (0 = default: the host's CPUs, at most 16).
+                                        The tree is the same for every count (ABI 4: the spatial-split budget
+                                        is shared between subtrees in proportion to their references, so
+                                        subtrees build independently). */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);
@@ -484,6 +499,10 @@ int dxrpt_unpermute(const float* src, const dxrpt_tile* tiles, uint32_t num_tile
                     uint32_t height, void* stream);
 /* Message of the last failed dxrpt_comm_* / dxrpt_gather_slabs / dxrpt_unpermute call of this thread. */
 const char* dxrpt_multi_last_error(void);
+/* Releases this thread's dxrpt_unpermute scratch (device tile lists, after their last launch); also done by
+ * dxrpt_comm_destroy.  Call it before the HIP runtime shuts down (a scratch still held at thread exit is left
+ * to the process teardown). */
+int dxrpt_multi_release(void);
 
 /* ---- lightmap baking (the second consumer of PathTrace) ----------------------------------------
  * One progressive bake pass: BakeRayGen (DXRPathTracer/Baking.hlsl:336-465) as dispatched by

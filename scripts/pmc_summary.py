@@ -2,7 +2,8 @@
 """Summarise the rocprofv3 outputs of scripts/profile.sh (kernel trace + stats of bench.py, then one
 rocprofv3 --pmc pass per counter group over the same command) into profiles/<round>_*.
 
-bench.py runs, in one process: a census frame (the counting k_path<7, true> on the caller's stream), a
+bench.py runs, in one process: a census frame (the counting instantiations of the timed schedule --
+k_path_head<5, true> + k_path_tail<7, true>, or k_path<occ, true> -- on the caller's stream), a
 frame-at-a-time pass (DXRPT_OPT_FRAME_OVERLAP 0: every kernel on the caller's stream, one launch at a
 time -- the per-launch durations of the bench line's roofline), then the timed overlapped frames (the
 kernels on two internal slot streams).  Per kernel kind (k_path_head / k_path_tail / k_path) this writes:
@@ -34,21 +35,27 @@ def short(name):
     return (m.group(1) + (m.group(2) or "")) if m else None
 
 
+PATH_KINDS = ("k_path", "k_path_head", "k_path_tail")
+
+
+def is_census(k):
+    """The counting instantiations k_path<occ, true, ...>, k_path_head<occ, true>, k_path_tail<occ, true>."""
+    if k is None or "<" not in k or k.split("<")[0] not in PATH_KINDS:
+        return False
+    return k[k.index("<") + 1:-1].split(", ")[1:2] == ["true"]
+
+
 def kind(k):
-    """Kernel kind of a short name; None for the census instantiation k_path<occ, true, ...>."""
-    if k is None:
+    """Kernel kind of a short name; None for a census instantiation."""
+    if k is None or is_census(k):
         return None
-    base = k.split("<")[0]
-    if base == "k_path":
-        targs = k[k.index("<") + 1:-1].split(", ") if "<" in k else []
-        return None if targs[1:2] == ["true"] else "k_path"
-    return base
+    return k.split("<")[0]
 
 
 def census_queue(rows, qcol):
+    """The caller's stream: the queue the (non-overlapped) census frame ran on."""
     for r in rows:
-        k = short(r["Kernel_Name"])
-        if k and k.startswith("k_path<") and kind(k) is None:
+        if is_census(short(r["Kernel_Name"])):
             return r[qcol]
     return None
 

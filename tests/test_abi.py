@@ -34,7 +34,7 @@ def test_libdxrpt_host_exports_every_declared_function():
 
 def test_abi_version_and_defaults():
     L = A.lib()
-    assert L.dxrpt_abi_version() == A.ABI_VERSION == 3
+    assert L.dxrpt_abi_version() == A.ABI_VERSION == 4
     s = A.AppSettings()
     L.dxrpt_default_settings(C.byref(s))
     py = A.default_settings()
@@ -80,6 +80,11 @@ def test_option_ids_match_the_header():
     py = {k[4:]: v for k, v in vars(A).items() if k.startswith("OPT_")}
     assert hdr == py
     assert not set(hdr.values()) & set(A.RETIRED_OPTIONS)
+    # the retired ids are listed once in the header (DXRPT_RETIRED_OPTIONS, which the library's
+    # dxrpt_set_option uses); the Python mirror must be that list
+    m = re.search(r"#define DXRPT_RETIRED_OPTIONS \{([^}]*)\}", txt)
+    assert m, "DXRPT_RETIRED_OPTIONS missing from include/dxrpt.h"
+    assert tuple(int(v.strip().rstrip("u")) for v in m.group(1).split(",")) == A.RETIRED_OPTIONS
     kinds = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define DXRPT_K_(\w+) (\d+)", txt)}
     assert kinds["COUNT"] == A.K_COUNT == len(A.KERNEL_NAMES)
     assert (kinds["PATH"], kinds["PATH_HEAD"], kinds["PATH_TAIL"]) == (A.K_PATH, A.K_PATH_HEAD, A.K_PATH_TAIL)
@@ -94,10 +99,11 @@ def test_stats_and_tile_layouts_match_the_header(tmp_path):
 #include <stddef.h>
 #include "dxrpt.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(dxrpt_stats), offsetof(dxrpt_stats, kernel_ms),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(dxrpt_stats), offsetof(dxrpt_stats, kernel_ms),
          offsetof(dxrpt_stats, schedule), offsetof(dxrpt_stats, tail_occupancy),
          offsetof(dxrpt_stats, radiance_hits), offsetof(dxrpt_stats, census_depth1), sizeof(dxrpt_tile),
-         sizeof(dxrpt_bvh_info));
+         sizeof(dxrpt_bvh_info), offsetof(dxrpt_bvh_info, phase_ms), offsetof(dxrpt_bvh_info, binary_depth_cap),
+         offsetof(dxrpt_bvh_info, ref_budget_pct));
   return 0;
 }
 """)
@@ -105,5 +111,6 @@ int main(void) {
     subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
     want = [C.sizeof(A.Stats), A.Stats.kernel_ms.offset, A.Stats.schedule.offset, A.Stats.tail_occupancy.offset,
-            A.Stats.radiance_hits.offset, A.Stats.census_depth1.offset, C.sizeof(A.Tile), C.sizeof(A.BvhInfo)]
+            A.Stats.radiance_hits.offset, A.Stats.census_depth1.offset, C.sizeof(A.Tile), C.sizeof(A.BvhInfo),
+            A.BvhInfo.phase_ms.offset, A.BvhInfo.binary_depth_cap.offset, A.BvhInfo.ref_budget_pct.offset]
     assert got == want

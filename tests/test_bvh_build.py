@@ -1,0 +1,73 @@
+"""CPU tests of the host BVH8 builder (dxrpathtracer_amd/csrc/bvh_build.cpp), which replaces the driver's
+BLAS/TLAS build (DXRPathTracer.cpp:2331-2488, timed at :2465-2473).  Driven through the host-only tool
+csrc/tools/bvh_check.cpp, which builds exactly as dxrpt_build_bvh does and prints the layout's hash.
+
+* The parallel build (r05) is deterministic: the same tree for any thread count.
+* the treelet passes may make a tree too deep for the traversal stack at every binary depth
+  cap; the builder then falls back to the tree without them instead of failing.
+* Deep, degenerate meshes (geometric sequences of slivers) always fit the stack.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dxrpathtracer_amd", "csrc")
+TOOL = os.path.join(CSRC, "build", "bvh_check")
+MAX_WIDE_DEPTH = 15  # pt_layout.h kTraversalStack8 - 1
+
+
+@pytest.fixture(scope="module")
+def tool():
+    subprocess.run(["make", "-s", "-C", CSRC, "build/bvh_check"], check=True)
+    return TOOL
+
+
+def check(tool, *args):
+    out = subprocess.run([tool, *map(str, args)], check=True, capture_output=True, text=True, timeout=600).stdout
+    return json.loads(out)
+
+
+def sliver_sequence(n, ratio, size=0.01):
+    """n slivers at x = ratio^i: SAH splits peel them off one at a time (a deep binary tree)."""
+    x = ratio ** np.arange(n, dtype=np.float64)
+    t = np.zeros((n, 9))
+    t[:, 0] = x
+    t[:, 3] = x + size
+    t[:, 7] = size
+    t[:, 8] = size
+    return t.astype(np.float32)
+
+
+def test_tree_independent_of_thread_count(tool):
+    # SunTemple proxy (164k triangles, alpha-tested foliage kept whole): 1, 3 and 8 builder threads
+    runs = [check(tool, "scene", 1, t) for t in (1, 3, 8)]
+    assert all(r["ok"] for r in runs), runs
+    assert len({r["hash"] for r in runs}) == 1, runs
+    assert runs[0]["depth"] <= MAX_WIDE_DEPTH and runs[0]["treelet_passes"] == 1
+    assert runs[0]["refs"] <= 1.5 * runs[0]["ntris"] * 1.05  # the duplication budget (small overshoot per split)
+
+
+@pytest.mark.parametrize("n,ratio", [(100, 1.5), (200, 1.2)])
+def test_treelet_fallback_keeps_the_build(tool, tmp_path, n, ratio):
+    # these sequences fit the stack without treelet passes but not with them at any binary depth cap: the
+    # build must succeed without them (r04 failed with "BVH8 deeper than the traversal stack")
+    f = tmp_path / "slivers.bin"
+    sliver_sequence(n, ratio).tofile(f)
+    plain = check(tool, "file", f, 2, 0)
+    assert plain["ok"] and plain["depth"] <= MAX_WIDE_DEPTH, plain
+    got = check(tool, "file", f, 2, 1)
+    assert got["ok"], got
+    assert got["depth"] <= MAX_WIDE_DEPTH and got["treelet_passes"] == 0, got
+    assert got["hash"] == plain["hash"]
+
+
+@pytest.mark.parametrize("n,ratio,passes", [(400, 1.1, 1), (1000, 1.02, 1), (1000, 1.02, 2), (3000, 1.005, 1)])
+def test_deep_meshes_fit_the_traversal_stack(tool, tmp_path, n, ratio, passes):
+    f = tmp_path / "slivers.bin"
+    sliver_sequence(n, ratio).tofile(f)
+    got = check(tool, "file", f, 2, passes)
+    assert got["ok"] and got["depth"] <= MAX_WIDE_DEPTH, got
+    assert got["refs"] >= n

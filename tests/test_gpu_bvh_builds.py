@@ -86,3 +86,23 @@ def test_parallel_treelet_build_is_deterministic(torch_cuda):
     torch_cuda.cuda.synchronize()
     np.testing.assert_array_equal(acc.cpu().numpy(), frame(torch_cuda, "sponza", "shipped", 3, 0))
     t.close()
+
+
+def test_build_threads_do_not_change_the_tree(torch_cuda):
+    """DXRPT_OPT_BVH_THREADS (ABI 4): the parallel SBVH / treelet / collapse build gives the same tree for any
+    thread count (tests/test_bvh_build.py checks the layout hash on the CPU); the info reports the phases."""
+    sc, sky = scene_bundle("suntemple")
+    infos = []
+    for threads in (1, 0):
+        t = DXRPathTracer(0)
+        t.set_option(A.OPT_BVH_THREADS, threads)
+        t.initialize_scene(sc, sky)
+        infos.append(t.build_rt_acceleration_structure())
+        t.close()
+    one, auto = infos
+    assert one.threads == 1 and auto.threads >= 1
+    for f in ("num_nodes", "num_leaves", "num_refs", "max_depth", "sah_cost", "wide_sah", "binary_depth_cap",
+              "treelet_passes", "ref_budget_pct"):
+        assert getattr(one, f) == getattr(auto, f), f
+    assert auto.ref_budget_pct == 150 and auto.treelet_passes == 1 and auto.num_refs >= auto.num_tris
+    assert all(auto.phase_ms[k] >= 0.0 for k in range(4)) and sum(auto.phase_ms) <= auto.build_ms * 1.01 + 1.0

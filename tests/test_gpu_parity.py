@@ -221,6 +221,9 @@ def test_retired_options_are_rejected(torch_cuda):
         assert rc == A.DXRPT_E_UNSUPPORTED, (opt, rc)
         assert b"retired" in A.lib().dxrpt_last_error(t._ctx)
     assert A.lib().dxrpt_abi_version() == A.ABI_VERSION
+    for opt in (0, 42, 63, 1000):  # never assigned: an unknown option, not a retired one
+        assert A.lib().dxrpt_set_option(t._ctx, opt, 1) == A.DXRPT_E_INVALID_ARG, opt
+        assert b"unknown option" in A.lib().dxrpt_last_error(t._ctx)
     with pytest.raises(Exception, match="frame overlap"):
         t.set_option(A.OPT_FRAME_OVERLAP, 2)
     with pytest.raises(Exception, match="occupancy"):
@@ -517,18 +520,23 @@ def test_xcd_chunk_mapping_is_bit_identical(torch_cuda, name, W, H):
         t.set_option(A.OPT_XCD_CHUNK, A.DEFAULT_XCD_CHUNK)
 
 
-@pytest.mark.parametrize("name,L,W,H,occ,tocc", [
-    ("sponza", 3, 352, 200, 7, 7), ("sponza", 8, 352, 200, 5, 6), ("suntemple", 3, 320, 180, 6, 5),
-    ("boxtest", 5, 100, 50, 4, 7), ("sponza", 6, 100, 50, 7, 4), ("whitefurnace", 3, 128, 128, 7, 7),
-    ("sponza", 8, 97, 61, 6, 7)])
-def test_megakernel_split_is_bit_identical(torch_cuda, name, L, W, H, occ, tocc):
+@pytest.mark.parametrize("name,L,W,H,occ,tocc,ov", [
+    ("sponza", 3, 352, 200, 7, 7, {}), ("sponza", 8, 352, 200, 5, 6, {}), ("suntemple", 3, 320, 180, 6, 5, {}),
+    ("boxtest", 5, 100, 50, 4, 7, {}), ("sponza", 6, 100, 50, 7, 4, {}), ("whitefurnace", 3, 128, 128, 7, 7, {}),
+    ("sponza", 8, 97, 61, 6, 7, {}),
+    # the payload-reading settings (RayTrace.hlsl:191-192, 203-204) through the queue hand-offs (verdict r04)
+    ("sponza", 4, 352, 200, 5, 7, dict(EnableIndirectSpecular=1)),
+    ("sponza", 5, 352, 200, 5, 7, dict(EnableIndirectSpecular=1, AvoidCausticPaths=1)),
+    ("suntemple", 4, 320, 180, 5, 7, dict(ClampRoughness=1, EnableIndirectSpecular=1)),
+    ("boxtest", 6, 100, 50, 5, 7, dict(EnableIndirectSpecular=1, AvoidCausticPaths=1, ClampRoughness=1))])
+def test_megakernel_split_is_bit_identical(torch_cuda, name, L, W, H, occ, tocc, ov):
     # DXRPT_OPT_MEGAKERNEL_SPLIT: one kernel per depth with the surviving paths compacted between depths
     # (wave64 ballot, one atomic per wave) and the path state carried in the queue -- the frame and the
     # ray counts per depth must equal the wavefront frame's, on full frames (partial last waves at 100 x
     # 50 and 97 x 61), on a band share, with 3 spot lights (BoxTest) and alpha-tested any hit (SunTemple)
     torch = torch_cuda
     sc, sky = scene_bundle(name)
-    st = sc.settings(MaxPathLength=L)
+    st = sc.settings(MaxPathLength=L, **ov)
     t = tracer(name)
     rtc, lights = (_boxtest_lights(sc, sky, st, W, H, 4) if name == "boxtest"
                    else (D.make_constants(sc, st, sky, W, H, 4), D.make_lights(sc)))
@@ -687,3 +695,49 @@ def test_census_wave_clocks_small_frames(torch_cuda, world, rank, overlap):
         assert t.wave_clocks().shape[0] == 0  # no stale stamps from the census frame
     finally:
         t.close()
+
+
+@pytest.mark.parametrize("name,W,H,L", [("sponza", 640, 360, 3), ("suntemple", 480, 270, 4), ("sponza", 97, 61, 5)])
+def test_split_census_prices_the_timed_kernels(torch_cuda, name, W, H, L):
+    # verdict r04 #2: a census frame of a depth-split frame runs the counting instantiations of the timed
+    # k_path_head / k_path_tail (same traversal orders), renders the same image, and counts what they fetch:
+    # the closest-hit fetches, hits and the deeper any-hit fetches equal those of the single-kernel census of
+    # the same order class (k_path<5, count>: nearest-first closest hits, far-to-near per-lane any hit); only
+    # the depth-1 packet sun shadows differ (the head walks them far to near, k_path<5> near to far)
+    torch = torch_cuda
+    sc, sky = scene_bundle(name)
+    st = sc.settings(MaxPathLength=L)
+    rtc = D.make_constants(sc, st, sky, W, H, 3)
+    t = tracer(name)
+    try:
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, 1 << 30)
+        t.set_option(A.OPT_WAVE_ORDER, 0)
+        t.set_option(A.OPT_MEGAKERNEL_SPLIT, 1)
+        ref = gpu_render(torch, name, W, H, st, 3, rtc=rtc).cpu().numpy()
+        assert t.stats().schedule & A.SCHED_SPLIT
+        t.set_option(A.OPT_COUNT_TRAVERSAL, 1)
+        got = gpu_render(torch, name, W, H, st, 3, rtc=rtc).cpu().numpy()
+        split = t.stats()
+        assert split.schedule & A.SCHED_CENSUS and split.schedule & A.SCHED_SPLIT, split.schedule
+        np.testing.assert_array_equal(got, ref)
+        t.set_option(A.OPT_MEGAKERNEL_SPLIT, 0)
+        t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, 5)
+        gpu_render(torch, name, W, H, st, 3, rtc=rtc)
+        single = t.stats()
+        assert single.schedule & A.SCHED_CENSUS and not single.schedule & A.SCHED_SPLIT, single.schedule
+    finally:
+        t.set_option(A.OPT_COUNT_TRAVERSAL, 0)
+        t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, A.DEFAULT_MEGAKERNEL_OCCUPANCY)
+        t.set_option(A.OPT_MEGAKERNEL_SPLIT, A.DEFAULT_MEGAKERNEL_SPLIT)
+        t.set_option(A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
+    assert split.radiance_hits > 0 and split.radiance_hits == single.radiance_hits
+    assert split.node_visits_radiance == single.node_visits_radiance
+    assert split.tri_tests_radiance == single.tri_tests_radiance
+    d1s, d1k = list(split.census_depth1), list(single.census_depth1)
+    assert (d1s[0], d1s[1], d1s[4]) == (d1k[0], d1k[1], d1k[4])
+    # deeper any-hit rays: same code and order in both
+    assert split.node_visits_shadow - d1s[2] == single.node_visits_shadow - d1k[2]
+    assert split.tri_tests_shadow - d1s[3] == single.tri_tests_shadow - d1k[3]
+    assert list(split.radiance_rays_per_depth) == list(single.radiance_rays_per_depth)
+    assert list(split.shadow_rays_per_depth) == list(single.shadow_rays_per_depth)

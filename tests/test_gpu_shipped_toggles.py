@@ -1,0 +1,186 @@
+"""GPU parity of the SHIPPED megakernel schedules under every AppSettings toggle (verdict r04 #1).
+
+tests/test_gpu_parity.py::test_settings_toggles checks the 16 override sets on the wavefront passes only.
+The schedules that ship carry payload state the wavefront keeps in its queues too, but through other code:
+  * k_path<7> / k_path<5>: one lane per path, payload Roughness / IsDiffuse in registers across depths
+    (C2 720p, the 1/4 band share);
+  * k_path<4, kOrder>: the cost-ordered instantiation (a GPU's 1/8 band share), frames 1+ in cost order;
+  * k_path_head<5> + k_path_tail<7>: the depth-split schedule (the metric, C3, C4, C5), payload Roughness in
+    the queue's thr.w and IsDiffuse in rad.w (pt_kernels.hip split_push / split_finish / tail_path), frames
+    overlapped.
+RayTrace.hlsl reads the payload at :191-192 (AvoidCausticPaths: IsDiffuse) and :203-204 (ClampRoughness:
+Roughness) and passes it on at :378-440.  Every schedule renders the same settings at 640x360 (L = 4: three
+path vertices, so the payload crosses two queue hand-offs), its crops are compared with the oracle (gate
+tests/_common.py, 1e-4 relative) and the whole frame with the wavefront's bit for bit; each frame asserts the
+schedule bits and register budgets that ran (dxrpt_get_stats).
+"""
+import numpy as np
+import pytest
+
+import dxrpathtracer_amd as D
+import dxrpathtracer_amd._abi as A
+from dxrpathtracer_amd.distributed import band_layout
+from dxrpathtracer_amd.tracer import DXRPathTracer
+from tests._common import assert_parity, oracle_scene, scene_bundle
+
+pytestmark = pytest.mark.gpu
+
+W, H, L, SAMPLE = 640, 360, 4, 5
+FRAME_CROPS = [(200, 100, 96, 96), (400, 250, 64, 64)]
+SHARE = (8, 5)  # world, rank of the cost-ordered band share
+
+OVERRIDES = [
+    dict(EnableNormalMaps=0), dict(EnableAlbedoMaps=0), dict(EnableSpecular=0), dict(EnableDiffuse=0),
+    dict(EnableDirect=0), dict(EnableIndirect=0), dict(EnableSun=0), dict(EnableSky=0),
+    dict(SunAreaLightApproximation=0), dict(ApplyMultiscatteringEnergyCompensation=0),
+    dict(EnableIndirectSpecular=1), dict(EnableIndirectSpecular=1, AvoidCausticPaths=1),
+    dict(ClampRoughness=1, EnableIndirectSpecular=1), dict(RoughnessScale=0.3, MetallicScale=1.7),
+    dict(SqrtNumSamples=7), dict(MaxAnyHitPathLength=0),
+    # the payload-reading settings together, with alpha testing on every depth
+    dict(EnableIndirectSpecular=1, AvoidCausticPaths=1, ClampRoughness=1, MaxAnyHitPathLength=4),
+]
+
+# schedule name -> (options, expected (schedule bits set, bits clear, occupancy, tail occupancy), band share?)
+_ALL = (A.OPT_MEGAKERNEL_PATHS, A.OPT_MEGAKERNEL_OCCUPANCY, A.OPT_TAIL_OCCUPANCY, A.OPT_WAVE_ORDER,
+        A.OPT_MEGAKERNEL_SPLIT, A.OPT_FRAME_OVERLAP)
+_DEFAULTS = {A.OPT_MEGAKERNEL_PATHS: A.DEFAULT_MEGAKERNEL_PATHS, A.OPT_MEGAKERNEL_OCCUPANCY: A.DEFAULT_MEGAKERNEL_OCCUPANCY,
+             A.OPT_TAIL_OCCUPANCY: A.DEFAULT_TAIL_OCCUPANCY, A.OPT_WAVE_ORDER: A.DEFAULT_WAVE_ORDER,
+             A.OPT_MEGAKERNEL_SPLIT: A.DEFAULT_MEGAKERNEL_SPLIT, A.OPT_FRAME_OVERLAP: A.DEFAULT_FRAME_OVERLAP}
+SCHEDULES = {
+    "k_path<7>": ({A.OPT_MEGAKERNEL_OCCUPANCY: 7, A.OPT_WAVE_ORDER: 0, A.OPT_MEGAKERNEL_SPLIT: 0},
+                  (A.SCHED_MEGAKERNEL | A.SCHED_OVERLAP, A.SCHED_SPLIT | A.SCHED_ORDER_KERNEL, 7, 0), False),
+    "k_path<5>": ({A.OPT_MEGAKERNEL_OCCUPANCY: 5, A.OPT_WAVE_ORDER: 0, A.OPT_MEGAKERNEL_SPLIT: 0},
+                  (A.SCHED_MEGAKERNEL | A.SCHED_OVERLAP, A.SCHED_SPLIT | A.SCHED_ORDER_KERNEL, 5, 0), False),
+    "k_path<4,kOrder>": ({A.OPT_MEGAKERNEL_OCCUPANCY: 4, A.OPT_WAVE_ORDER: 1, A.OPT_MEGAKERNEL_SPLIT: 0},
+                         (A.SCHED_MEGAKERNEL | A.SCHED_OVERLAP | A.SCHED_ORDER_KERNEL, A.SCHED_SPLIT, 4, 0), True),
+    "head<5>+tail<7>": ({A.OPT_MEGAKERNEL_SPLIT: 1},
+                        (A.SCHED_MEGAKERNEL | A.SCHED_OVERLAP | A.SCHED_SPLIT, A.SCHED_ORDER_KERNEL, 5, 7), False),
+}
+
+_TRACERS = {}
+
+
+def tracer(name):
+    """One default context per scene (no DXRPT_OPT_MEGAKERNEL_PATHS override)."""
+    if name not in _TRACERS:
+        sc, sky = scene_bundle(name)
+        t = DXRPathTracer(0)
+        t.initialize_scene(sc, sky)
+        t.build_rt_acceleration_structure()
+        _TRACERS[name] = t
+    return _TRACERS[name]
+
+
+def _set(t, opts):
+    for o in _ALL:
+        t.set_option(o, opts.get(o, _DEFAULTS[o]))
+
+
+def _band_crops(lay, rank, w=128):
+    tiles = lay.rank_tiles(rank)
+    out = []
+    for k, i in enumerate(sorted({1, len(tiles) // 2, len(tiles) - 2})):
+        tl = tiles[i]
+        x0 = tl.x0 + (k * 211) % (tl.w - w)
+        out.append(((x0, tl.y0, w, tl.h), tl.accum_offset + (x0 - tl.x0), tl.accum_pitch))
+    return out
+
+
+def _render(torch, t, rtc, st, lights, tiles=None, n=W * H):
+    acc = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
+    t.render_raw(rtc, st, acc.data_ptr(), W, H, tiles=tiles, stream=torch.cuda.current_stream().cuda_stream,
+                 lights=lights)
+    s = t.stats()  # synchronises
+    return acc.cpu().numpy(), s
+
+
+def _check_schedule(name, f, s, want):
+    on, off, occ, tocc = want
+    assert s.schedule & on == on and not s.schedule & off, f"{name} frame {f}: schedule {s.schedule}"
+    assert not s.schedule & A.SCHED_CENSUS
+    assert (s.occupancy, s.tail_occupancy) == (occ, tocc), (name, f, s.occupancy, s.tail_occupancy)
+    if s.schedule & A.SCHED_ORDER_KERNEL:
+        # frame 0 records its wave costs in path order, frame 1 starts its waves in the order built from them
+        assert bool(s.schedule & A.SCHED_COST_ORDERED) == (f > 0), f"{name} frame {f}: schedule {s.schedule}"
+
+
+def run_schedules(torch, scene, st, rtc, lights, crops_oracle):
+    """Renders (rtc, st) through the wavefront and every shipped schedule; checks parity and bit identity."""
+    t = tracer(scene)
+    lay = band_layout(W, H, SHARE[0])
+    share_tiles, share_n = lay.rank_tiles(SHARE[1]), lay.counts[SHARE[1]]
+    bcrops = _band_crops(lay, SHARE[1])
+    orc = oracle_scene(scene)
+    ref_frame = {cr: orc.render(rtc, st, lights, W, H, crop=cr)[0] for cr in FRAME_CROPS}
+    ref_band = {cr: orc.render(rtc, st, lights, W, H, crop=cr)[0] for cr, _, _ in bcrops}
+    try:
+        _set(t, {A.OPT_MEGAKERNEL_PATHS: 0})
+        wave, s = _render(torch, t, rtc, st, lights)
+        assert not s.schedule & A.SCHED_MEGAKERNEL, s.schedule
+        wave = wave.reshape(H, W, 4)
+        for cr in FRAME_CROPS:
+            x0, y0, w, h = cr
+            assert_parity(wave[y0:y0 + h, x0:x0 + w], ref_frame[cr], f"wavefront {scene} {cr}")
+        for sname, (opts, want, share) in SCHEDULES.items():
+            _set(t, opts)
+            for f in range(2):
+                if share:
+                    got, s = _render(torch, t, rtc, st, lights, tiles=share_tiles, n=share_n)
+                    _check_schedule(sname, f, s, want)
+                    for (cr, off, pitch) in bcrops:
+                        x0, y0, w, h = cr
+                        rows = np.array([[off + yy * pitch + xx for xx in range(w)] for yy in range(h)])
+                        assert_parity(got[rows], ref_band[cr], f"{sname} {scene} band {cr} frame {f}")
+                    for tl in share_tiles:  # the share's pixels are the full frame's, bit for bit
+                        part = got[tl.accum_offset:tl.accum_offset + tl.w * tl.h].reshape(tl.h, tl.w, 4)
+                        np.testing.assert_array_equal(part, wave[tl.y0:tl.y0 + tl.h, tl.x0:tl.x0 + tl.w])
+                else:
+                    got, s = _render(torch, t, rtc, st, lights)
+                    _check_schedule(sname, f, s, want)
+                    got = got.reshape(H, W, 4)
+                    for cr in FRAME_CROPS:
+                        x0, y0, w, h = cr
+                        assert_parity(got[y0:y0 + h, x0:x0 + w], ref_frame[cr], f"{sname} {scene} {cr} frame {f}")
+                    np.testing.assert_array_equal(got, wave, err_msg=f"{sname} frame {f} vs the wavefront")
+    finally:
+        _set(t, {})
+
+
+@pytest.mark.parametrize("overrides", OVERRIDES, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
+def test_shipped_schedules_under_settings_toggles(torch_cuda, overrides):
+    sc, sky = scene_bundle("sponza")
+    ov = dict(MaxPathLength=L)
+    ov.update(overrides)
+    st = sc.settings(**ov)
+    rtc = D.make_constants(sc, st, sky, W, H, SAMPLE)
+    run_schedules(torch_cuda, "sponza", st, rtc, D.make_lights(sc), FRAME_CROPS)
+
+
+@pytest.mark.parametrize("overrides", [dict(), dict(EnableIndirectSpecular=1, AvoidCausticPaths=1, ClampRoughness=1)])
+def test_shipped_schedules_with_spot_lights(torch_cuda, overrides):
+    # RayTrace.hlsl:265-313: three spot lights (shadow slots 1..3 of every vertex) through every schedule
+    import math
+    sc, sky = scene_bundle("boxtest")
+    st = sc.settings(MaxPathLength=L, **overrides)
+    rtc = D.make_constants(sc, st, sky, W, H, SAMPLE)
+    lights = D.make_lights(sc)
+    for i, (p, d) in enumerate([((1.5, 4.0, -2.0), (-0.3, -1.0, 0.4)), ((-2.5, 1.5, -1.5), (0.8, -0.2, 0.5)),
+                                ((0.5, 3.0, 2.0), (0.0, -1.0, -0.2))]):
+        n = math.sqrt(sum(x * x for x in d))
+        lt = lights.Lights[i]
+        lt.Position[:] = p
+        lt.Direction[:] = tuple(-x / n for x in d)
+        lt.Intensity[:] = (50.0, 45.0, 37.5)
+        lt.AngularAttenuationX, lt.AngularAttenuationY, lt.Range = math.cos(0.3), math.cos(0.6), 7.5
+    rtc.NumLights = 3
+    run_schedules(torch_cuda, "boxtest", st, rtc, lights, FRAME_CROPS)
+
+
+@pytest.mark.parametrize("overrides", [dict(EnableIndirectSpecular=1, AvoidCausticPaths=1, ClampRoughness=1),
+                                       dict(EnableIndirectSpecular=1, AvoidCausticPaths=1, MaxAnyHitPathLength=4)])
+def test_shipped_schedules_suntemple_alpha(torch_cuda, overrides):
+    # SunTemple (alpha-tested foliage, BASELINE.json configs[3]) with the payload-reading settings
+    sc, sky = scene_bundle("suntemple")
+    st = sc.settings(MaxPathLength=L, **overrides)
+    rtc = D.make_constants(sc, st, sky, W, H, SAMPLE)
+    run_schedules(torch_cuda, "suntemple", st, rtc, D.make_lights(sc), FRAME_CROPS)
