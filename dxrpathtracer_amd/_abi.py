@@ -147,6 +147,7 @@ class BvhInfo(C.Structure):
 
 
 BVH_PHASES = ("sbvh", "treelet", "collapse", "records_upload")  # dxrpt_bvh_info.phase_ms
+PHASE_CLOCKS = 24  # dxrpt_get_phase_clocks: [0:8] k_path, [8:16] k_path_head, [16:24] k_path_tail
 
 
 class HostTexture(C.Structure):

@@ -854,11 +854,12 @@ void restructure_treelet(std::vector<TNode>& tree, std::vector<double>& cost, in
     }
     if (nl < 3) return;  // two leaves have one topology
     const int full = (1 << nl) - 1;
+    Box sbox[kMaxSub];  // the union of a subset's leaf boxes: the subset without its lowest leaf, grown by it
     for (int sset = 1; sset <= full; ++sset) {
-        Box bx;
-        for (int i = 0; i < nl; ++i)
-            if (sset & (1 << i)) bx.grow(tree[size_t(leaves[i])].box);
-        area[sset] = bx.area();
+        const int low = __builtin_ctz(unsigned(sset));
+        sbox[sset] = sbox[sset & (sset - 1)];
+        sbox[sset].grow(tree[size_t(leaves[low])].box);
+        area[sset] = sbox[sset].area();
     }
     for (int i = 0; i < nl; ++i) best[1 << i] = cost[size_t(leaves[i])];
     // a proper subset of S is numerically smaller than S: increasing order is a valid DP order
@@ -879,31 +880,86 @@ void restructure_treelet(std::vector<TNode>& tree, std::vector<double>& cost, in
         split[sset] = uint8_t(bp);
     }
     if (!(best[full] < cost[size_t(r)] * (1.0 - 1e-9))) return;
-    // rewire: the new topology's internal nodes reuse the treelet's (r stays the root)
-    int next = 0;
-    std::function<int32_t(int)> build = [&](int sset) -> int32_t {
-        if ((sset & (sset - 1)) == 0) return leaves[__builtin_ctz(unsigned(sset))];
-        const int32_t idx = internals[next++];
-        const int p = split[sset];
-        const int32_t x = build(p), y = build(sset ^ p);
-        TNode& t = tree[size_t(idx)];
-        t.child[0] = x;
-        t.child[1] = y;
-        t.box = tree[size_t(x)].box;
-        t.box.grow(tree[size_t(y)].box);
-        cost[size_t(idx)] = best[sset];
-        return idx;
+    // rewire: the new topology's internal nodes reuse the treelet's (r stays the root), assigned in the
+    // pre-order of the new topology
+    struct Rewire {
+        std::vector<TNode>& tree;
+        std::vector<double>& cost;
+        const int32_t* leaves;
+        const int32_t* internals;
+        const uint8_t* split;
+        const double* best;
+        int next;
+        int32_t build(int sset) {
+            if ((sset & (sset - 1)) == 0) return leaves[__builtin_ctz(unsigned(sset))];
+            const int32_t idx = internals[next++];
+            const int p = split[sset];
+            const int32_t x = build(p), y = build(sset ^ p);
+            TNode& t = tree[size_t(idx)];
+            t.child[0] = x;
+            t.child[1] = y;
+            t.box = tree[size_t(x)].box;
+            t.box.grow(tree[size_t(y)].box);
+            cost[size_t(idx)] = best[sset];
+            return idx;
+        }
     };
-    build(full);
+    Rewire{tree, cost, leaves, internals, split, best, 0}.build(full);
 }
 
-void restructure_treelets(std::vector<TNode>& tree, std::vector<uint32_t>& refs, int passes, const uint8_t* alpha,
+// Breadth-first order of the tree's nodes from the root (level_end[l]: end of level l in bfs).
+void bfs_levels(const std::vector<TNode>& tree, std::vector<int32_t>& bfs, std::vector<size_t>& level_end) {
+    bfs.clear();
+    level_end.clear();
+    bfs.reserve(tree.size());
+    bfs.push_back(0);
+    for (size_t b = 0; b < bfs.size();) {
+        const size_t e = bfs.size();
+        for (size_t i = b; i < e; ++i) {
+            const TNode& t = tree[size_t(bfs[i])];
+            if (!t.count) {
+                bfs.push_back(t.child[0]);
+                bfs.push_back(t.child[1]);
+            }
+        }
+        level_end.push_back(e);
+        b = e;
+    }
+}
+
+// f(i) for i in [b, e) on the pool in chunks (serial below a threshold); returns after every call.
+template <class F>
+void parallel_range(TaskPool& pool, unsigned threads, size_t b, size_t e, F&& f) {
+    const size_t n = e - b;
+    const size_t K = pool.parallel() && n >= 4096 ? std::min<size_t>(size_t(threads) * 4u, n / 1024u) : 1u;
+    if (K <= 1) {
+        for (size_t i = b; i < e; ++i) f(i);
+        return;
+    }
+    std::atomic<size_t> left{K - 1};
+    std::atomic<bool> done{false};
+    for (size_t k = 1; k < K; ++k)
+        pool.submit([&, k] {
+            for (size_t i = b + n * k / K; i < b + n * (k + 1) / K; ++i) f(i);
+            if (left.fetch_sub(1) == 1) done.store(true, std::memory_order_release);
+        });
+    for (size_t i = b; i < b + n / K; ++i) f(i);
+    pool.wait(done);
+}
+
+// Leaves, references and node slots are kept; only the topology of internal nodes changes, so the tree is not
+// renumbered: the collapse gathers each wide leaf's references by walking its (at most three-reference)
+// binary subtree left to right, the order of a depth-first renumbering.
+void restructure_treelets(std::vector<TNode>& tree, const std::vector<uint32_t>& refs, int passes, const uint8_t* alpha,
                           unsigned threads) {
     const size_t nn = tree.size();
     if (nn < 3) return;
     std::vector<double> cost(nn, 0.0);
-    std::vector<uint32_t> depth(nn, 0);
     std::vector<uint8_t> fixed(nn, 0);  // subtree holds an alpha-tested reference: left as built
+    const unsigned hw = std::max(1u, threads);
+    TaskPool pool(hw);
+    std::vector<int32_t> bfs;
+    std::vector<size_t> level_end;
     // post-order of the subtree at `root`, internal nodes only
     auto post_order = [&](int32_t root, std::vector<int32_t>& order) {
         order.clear();
@@ -921,94 +977,53 @@ void restructure_treelets(std::vector<TNode>& tree, std::vector<uint32_t>& refs,
             st.push_back({tree[size_t(n)].child[0], false});
         }
     };
-    const unsigned hw = std::max(1u, threads);
     for (int pass = 0; pass < passes; ++pass) {
-        // costs bottom-up and depths top-down over the current topology
-        std::vector<int32_t> all;
-        post_order(0, all);
-        for (size_t i = 0; i < nn; ++i)
-            if (tree[i].count) {
-                cost[i] = tree[i].box.area() * double(tree[i].count);
-                fixed[i] = 0;
-                if (alpha)
-                    for (uint32_t k = 0; k < tree[i].count; ++k) fixed[i] |= alpha[refs[tree[i].first + k]];
-            }
-        for (int32_t n : all) {
-            const TNode& t = tree[size_t(n)];
-            cost[size_t(n)] = t.box.area() + cost[size_t(t.child[0])] + cost[size_t(t.child[1])];
-            fixed[size_t(n)] = fixed[size_t(t.child[0])] | fixed[size_t(t.child[1])];
+        // costs bottom-up over the current topology, one breadth-first level at a time (deepest first)
+        bfs_levels(tree, bfs, level_end);
+        for (size_t l = level_end.size(); l-- > 0;) {
+            parallel_range(pool, hw, l ? level_end[l - 1] : 0, level_end[l], [&](size_t i) {
+                const size_t n = size_t(bfs[i]);
+                const TNode& t = tree[n];
+                if (t.count) {
+                    cost[n] = t.box.area() * double(t.count);
+                    uint8_t f = 0;
+                    if (alpha)
+                        for (uint32_t k = 0; k < t.count; ++k) f |= alpha[refs[t.first + k]];
+                    fixed[n] = f;
+                } else {
+                    cost[n] = t.box.area() + cost[size_t(t.child[0])] + cost[size_t(t.child[1])];
+                    fixed[n] = fixed[size_t(t.child[0])] | fixed[size_t(t.child[1])];
+                }
+            });
         }
-        for (auto it = all.rbegin(); it != all.rend(); ++it) {  // reverse post-order: parents first
-            const TNode& t = tree[size_t(*it)];
-            depth[size_t(t.child[0])] = depth[size_t(t.child[1])] = depth[size_t(*it)] + 1;
-        }
-        // disjoint subtrees at the cut depth are restructured in parallel, the levels above serially
-        constexpr uint32_t kCut = 7;
+        // disjoint subtrees at the cut depth are restructured in parallel (each bottom-up), the levels above
+        // serially, deepest level first (every node after its descendants, as a post-order)
+        constexpr size_t kCut = 7;
         std::vector<int32_t> roots;
-        for (int32_t n : all)
-            if (depth[size_t(n)] == kCut) roots.push_back(n);
+        if (level_end.size() > kCut)
+            for (size_t i = level_end[kCut - 1]; i < level_end[kCut]; ++i)
+                if (!tree[size_t(bfs[i])].count) roots.push_back(bfs[i]);
         std::atomic<size_t> cursor{0};
+        std::atomic<size_t> left{roots.size()};
+        std::atomic<bool> done{roots.empty()};
         auto worker = [&] {
             std::vector<int32_t> order;
             for (size_t k; (k = cursor.fetch_add(1)) < roots.size();) {
                 post_order(roots[k], order);
                 for (int32_t n : order)
                     if (!fixed[size_t(n)]) restructure_treelet(tree, cost, n);
+                if (left.fetch_sub(1) == 1) done.store(true, std::memory_order_release);
             }
         };
-        std::vector<std::thread> pool;
-        for (unsigned t = 1; t < hw; ++t) pool.emplace_back(worker);
+        for (unsigned t = 1; t < hw; ++t) pool.submit(worker);
         worker();
-        for (std::thread& t : pool) t.join();
-        std::vector<int32_t> top;
-        post_order(0, top);
-        for (int32_t n : top)
-            if (depth[size_t(n)] < kCut && !fixed[size_t(n)]) restructure_treelet(tree, cost, n);
+        pool.wait(done);
+        for (size_t l = std::min(kCut, level_end.size()); l-- > 0;)
+            for (size_t i = l ? level_end[l - 1] : 0; i < level_end[l]; ++i) {
+                const int32_t n = bfs[i];
+                if (!tree[size_t(n)].count && !fixed[size_t(n)]) restructure_treelet(tree, cost, n);
+            }
     }
-    // depth-first renumbering: parents before children, each subtree's references contiguous
-    std::vector<TNode> out;
-    out.reserve(nn);
-    std::vector<uint32_t> rout;
-    rout.reserve(refs.size());
-    struct Item {
-        int32_t old;
-        int32_t slot;
-    };
-    out.emplace_back();
-    std::vector<Item> st{{0, 0}};
-    std::vector<std::pair<int32_t, int32_t>> fix;  // (new node, old node) of internal nodes, in pre-order
-    while (!st.empty()) {
-        const Item it = st.back();
-        st.pop_back();
-        const TNode& o = tree[size_t(it.old)];
-        TNode& t = out[size_t(it.slot)];
-        t.box = o.box;
-        if (o.count) {
-            t.first = uint32_t(rout.size());
-            t.count = o.count;
-            for (uint32_t i = 0; i < o.count; ++i) rout.push_back(refs[o.first + i]);
-            t.begin = t.first;
-            t.end = t.first + t.count;
-            continue;
-        }
-        const int32_t c0 = int32_t(out.size()), c1 = c0 + 1;
-        out.emplace_back();
-        out.emplace_back();
-        out[size_t(it.slot)].child[0] = c0;
-        out[size_t(it.slot)].child[1] = c1;
-        fix.push_back({it.slot, it.old});
-        st.push_back({o.child[1], c1});
-        st.push_back({o.child[0], c0});
-    }
-    // subtree reference ranges (children have larger indices: a reverse sweep is a post-order)
-    for (size_t i = out.size(); i-- > 0;) {
-        TNode& t = out[i];
-        if (t.count) continue;
-        t.begin = std::min(out[size_t(t.child[0])].begin, out[size_t(t.child[1])].begin);
-        t.end = std::max(out[size_t(t.child[0])].end, out[size_t(t.child[1])].end);
-    }
-    tree.swap(out);
-    refs.swap(rout);
 }
 
 double tree_sah(const std::vector<TNode>& tree) {
@@ -1095,8 +1110,19 @@ struct Emit8 {
     std::vector<uint8_t> pick;    // [n * 8 + i]: i == 1: 0 leaf / 1 node; i >= 2: 0 = use C(n, i-1), k = split
     std::vector<uint8_t> dsplit;  // k of D(n, 8)
 
-    static uint32_t ntris(const TNode& n) { return n.end - n.begin; }
+    std::vector<uint32_t> ntri;   // references of each binary node's subtree
     bool is_leaf(int32_t t) const { return pick[size_t(t) * 8 + 1] == 0; }
+
+    // The references of binary subtree t, left to right (a wide leaf: at most kMaxLeafTris8 of them).
+    void leaf_refs(int32_t t, std::vector<uint32_t>& out) const {
+        const TNode& n = tree[size_t(t)];
+        if (n.count) {
+            for (uint32_t i = 0; i < n.count; ++i) out.push_back(refs[n.first + i]);
+            return;
+        }
+        leaf_refs(n.child[0], out);
+        leaf_refs(n.child[1], out);
+    }
 
     // C / D of binary node ni (its children's already final).
     void solve_node(size_t ni) {
@@ -1104,7 +1130,8 @@ struct Emit8 {
         const double A = n.box.area();
         double* C = &cost[ni * 8];
         uint8_t* P = &pick[ni * 8];
-        const double leaf = ntris(n) <= uint32_t(kMaxLeafTris8) ? A * kCPrim * double(ntris(n)) : DBL_MAX;
+        const uint32_t nt = ntri[ni] = n.count ? n.count : ntri[size_t(n.child[0])] + ntri[size_t(n.child[1])];
+        const double leaf = nt <= uint32_t(kMaxLeafTris8) ? A * kCPrim * double(nt) : DBL_MAX;
         if (n.count) {  // binary leaf
             for (int i = 1; i < 8; ++i) { C[i] = leaf; P[i] = 0; }
             C[0] = DBL_MAX;
@@ -1142,37 +1169,12 @@ struct Emit8 {
         cost.assign(nn * 8, 0.0);
         pick.assign(nn * 8, 0);
         dsplit.assign(nn, 0);
+        ntri.assign(nn, 0);
         std::vector<int32_t> bfs;
-        bfs.reserve(nn);
         std::vector<size_t> level_end;
-        bfs.push_back(0);
-        for (size_t b = 0; b < bfs.size();) {
-            const size_t e = bfs.size();
-            for (size_t i = b; i < e; ++i)
-                if (!tree[size_t(bfs[i])].count) {
-                    bfs.push_back(tree[size_t(bfs[i])].child[0]);
-                    bfs.push_back(tree[size_t(bfs[i])].child[1]);
-                }
-            level_end.push_back(e);
-            b = e;
-        }
-        for (size_t l = level_end.size(); l-- > 0;) {
-            const size_t b = l ? level_end[l - 1] : 0, n = level_end[l] - b;
-            const size_t K = pool.parallel() && n >= 4096 ? std::min<size_t>(size_t(threads) * 4u, n / 1024u) : 1u;
-            if (K <= 1) {
-                for (size_t i = b; i < b + n; ++i) solve_node(size_t(bfs[i]));
-                continue;
-            }
-            std::atomic<size_t> left{K - 1};
-            std::atomic<bool> done{false};
-            for (size_t k = 1; k < K; ++k)
-                pool.submit([&, k] {
-                    for (size_t i = b + n * k / K; i < b + n * (k + 1) / K; ++i) solve_node(size_t(bfs[i]));
-                    if (left.fetch_sub(1) == 1) done.store(true, std::memory_order_release);
-                });
-            for (size_t i = b; i < b + n / K; ++i) solve_node(size_t(bfs[i]));
-            pool.wait(done);
-        }
+        bfs_levels(tree, bfs, level_end);
+        for (size_t l = level_end.size(); l-- > 0;)
+            parallel_range(pool, threads, l ? level_end[l - 1] : 0, level_end[l], [&](size_t i) { solve_node(size_t(bfs[i])); });
     }
 
     // Children of binary subtree t occupying at most i slots.
@@ -1286,7 +1288,6 @@ struct Emit8 {
                 }
                 continue;
             }
-            const TNode& c = tree[slot_of[s]];
             for (int k = 0; k < 3; ++k) {
                 double ql = std::floor((double(pb[s].lo[k]) - n.p[k]) / scale[k]);
                 double qh = std::ceil((double(pb[s].hi[k]) - n.p[k]) / scale[k]);
@@ -1298,7 +1299,7 @@ struct Emit8 {
                 n.qhi[k][s] = uint8_t(qh);
             }
             if (is_leaf(slot_of[s])) {
-                const uint32_t cnt = ntris(c);
+                const uint32_t cnt = ntri[size_t(slot_of[s])];
                 n.meta[s] = uint8_t((cnt << 5) | tri_off);
                 tri_off += cnt;
             } else {
@@ -1358,7 +1359,7 @@ struct Emit8 {
                     const int32_t c = P.slot_of[s];
                     if (c < 0) continue;
                     if (is_leaf(c)) {
-                        for (uint32_t r = tree[c].begin; r < tree[c].end; ++r) tri_order.push_back(refs[r]);
+                        leaf_refs(c, tri_order);
                         leaves++;
                     } else {
                         next.push_back({base_child + rank++, c});
@@ -1469,7 +1470,8 @@ bool build_bvh(const float* tri_positions, uint32_t ntris, int width, BvhBuildRe
                 if (!B.build(ntris, err, sah)) return false;
                 lap(0);
             }
-            Emit8 E{*tree, *refs, pad, {}, {}, 0, 0, 1.0, params ? params->leaf_cost : BvhBuildParams().leaf_cost, {}, {}, {}, build_threads(params)};
+            Emit8 E{*tree, *refs, pad, {}, {}, 0, 0, 1.0, params ? params->leaf_cost : BvhBuildParams().leaf_cost, {}, {}, {}, {}};
+            E.threads = build_threads(params);
             E.run();
             lap(2);
             last_depth = E.max_depth;

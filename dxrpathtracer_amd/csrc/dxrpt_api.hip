@@ -539,6 +539,24 @@ void harvest_all(dxrpt_ctx* c) {
 
 }  // namespace
 
+// f(i) for i in [0, n) on up to `threads` host threads in contiguous chunks (the BVH build's per-triangle
+// record and vertex copies; each i writes only its own outputs).
+template <class F>
+static void host_parallel(uint32_t n, unsigned threads, F&& f) {
+    const unsigned k = std::max(1u, std::min(threads, n / 16384u));
+    if (k <= 1) {
+        for (uint32_t i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (unsigned j = 1; j < k; ++j)
+        th.emplace_back([&, j] {
+            for (uint32_t i = uint32_t(uint64_t(n) * j / k); i < uint32_t(uint64_t(n) * (j + 1) / k); ++i) f(i);
+        });
+    for (uint32_t i = 0; i < uint32_t(uint64_t(n) / k); ++i) f(i);
+    for (std::thread& t : th) t.join();
+}
+
 extern "C" {
 
 int dxrpt_abi_version(void) { return DXRPT_ABI_VERSION; }
@@ -807,16 +825,20 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
             require(end >= begin, "dxrpt_build_bvh: geometries must be sorted by IdxOffset");
             for (uint32_t t = begin; t < end; ++t) tri_geom[t] = g;
         }
-        std::vector<float> pos(size_t(ntris) * 9);
         for (uint32_t t = 0; t < ntris; ++t) {
-            uint32_t g = tri_geom[t];
-            require(g != 0xFFFFFFFFu, "dxrpt_build_bvh: triangle not covered by any geometry");
-            for (int k = 0; k < 3; ++k) {
-                uint32_t vi = ctx->indices[size_t(t) * 3 + k] + ctx->geos[g].VtxOffset;
-                require(vi < ctx->vertices.size(), "dxrpt_build_bvh: index out of range");
-                std::memcpy(&pos[size_t(t) * 9 + k * 3], ctx->vertices[vi].Position, 12);
-            }
+            require(tri_geom[t] != 0xFFFFFFFFu, "dxrpt_build_bvh: triangle not covered by any geometry");
+            for (int k = 0; k < 3; ++k)
+                require(ctx->indices[size_t(t) * 3 + k] + uint64_t(ctx->geos[tri_geom[t]].VtxOffset) < ctx->vertices.size(),
+                        "dxrpt_build_bvh: index out of range");
         }
+        const unsigned threads = ctx->build_params.threads ? ctx->build_params.threads
+                                                          : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::vector<float> pos(size_t(ntris) * 9);
+        host_parallel(ntris, threads, [&](uint32_t t) {
+            const uint32_t g = tri_geom[t];
+            for (int k = 0; k < 3; ++k)
+                std::memcpy(&pos[size_t(t) * 9 + k * 3], ctx->vertices[ctx->indices[size_t(t) * 3 + k] + ctx->geos[g].VtxOffset].Position, 12);
+        });
         BvhBuildResult res;
         std::string err;
         // spatial splits leave alpha-tested triangles whole: each extra reference of one is another
@@ -838,7 +860,7 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
                 ctx->omm_tris.push_back(t);
             }
         std::vector<TriRecord> tris(nrefs);
-        for (uint32_t i = 0; i < nrefs; ++i) {
+        host_parallel(nrefs, threads, [&](uint32_t i) {
             const uint32_t t = res.tri_order[i];
             const float* v = &pos[size_t(t) * 9];
             TriRecord& r = tris[i];
@@ -850,7 +872,7 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
             std::memcpy(&r.p0[3], &t, 4);
             std::memcpy(&r.p1[3], &g, 4);
             std::memcpy(&r.p2[3], &flags, 4);
-        }
+        });
         if (kNode8Stride == sizeof(Bvh8Node)) {
             ctx->d_nodes8.upload(res.nodes8.data(), res.nodes8.size() * sizeof(Bvh8Node));
         } else {  // padded device layout (pt_layout.h kNode8Stride)
@@ -863,9 +885,10 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
         {   // shading-side copy of each triangle's vertices: one contiguous 192-B record per gtri, so a
             // hit gathers 2 cache lines in one round trip instead of 3 indices then 3 vertices
             std::vector<dxrpt_mesh_vertex> tv(size_t(ntris) * 3);
-            for (uint32_t t = 0; t < ntris; ++t)
+            host_parallel(ntris, threads, [&](uint32_t t) {
                 for (int k = 0; k < 3; ++k)
                     tv[size_t(t) * 3 + k] = ctx->vertices[ctx->indices[size_t(t) * 3 + k] + ctx->geos[tri_geom[t]].VtxOffset];
+            });
             ctx->d_tri_verts.upload(tv.data(), tv.size() * sizeof(dxrpt_mesh_vertex));
         }
         auto t1 = std::chrono::steady_clock::now();
@@ -1296,12 +1319,13 @@ int dxrpt_get_wave_clocks(dxrpt_ctx* ctx, uint64_t* out, uint32_t max_waves, uin
     });
 }
 
-int dxrpt_get_phase_clocks(dxrpt_ctx* ctx, uint64_t out[8]) {
+int dxrpt_get_phase_clocks(dxrpt_ctx* ctx, uint64_t out[DXRPT_PHASE_CLOCKS]) {
     if (!ctx || !out) return DXRPT_E_INVALID_ARG;
     return guarded(ctx, [&] {
-        unsigned long long t[8];
+        static_assert(kPhaseClockWords == DXRPT_PHASE_CLOCKS, "include/dxrpt.h DXRPT_PHASE_CLOCKS");
+        unsigned long long t[kPhaseClockWords];
         HIP_CHECK(read_phase_ticks(t));
-        for (int k = 0; k < 8; ++k) out[k] = t[k];
+        for (int k = 0; k < kPhaseClockWords; ++k) out[k] = t[k];
     });
 }
 

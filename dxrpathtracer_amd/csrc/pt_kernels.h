@@ -200,6 +200,7 @@ hipError_t launch_accum_stage(const FrameParams& fp, hipStream_t stream);
 hipError_t launch_sample_cmj(const uint4* cases, uint32_t n, float2* out, hipStream_t stream);
 
 // DXRPT_DIAG_PHASES builds: the per-phase lane ticks since the last call (synchronises the device, zeroes them).
-hipError_t read_phase_ticks(unsigned long long out[8]);
+constexpr int kPhaseClockWords = 24;  // [0, 8) k_path, [8, 16) k_path_head, [16, 24) k_path_tail
+hipError_t read_phase_ticks(unsigned long long out[kPhaseClockWords]);
 
 }  // namespace dxrpt

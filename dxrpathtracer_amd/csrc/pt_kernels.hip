@@ -1264,7 +1264,12 @@ struct PhaseAcc {
     uint32_t a[8];
     uint32_t t;
 };
-__device__ unsigned long long g_phase_ticks[8];
+constexpr int kPhaseSets = 3;
+// Three sets of 8 phases: [0, 8) the single k_path (above), [8, 16) k_path_head, [16, 24) k_path_tail --
+// 0 ray setup + closest hit, 1 shading (path_vertex), 2 continuation push, 3 / 4 / 5 shadow slot 0 / 1 /
+// >= 2 (sun, sky visibility or first spot light, the rest), 6 radiance hand-off, 7 waiting for the wave's
+// other lanes after the lane's path ended.
+__device__ unsigned long long g_phase_ticks[kPhaseSets * 8];
 PT_DEV void phase_mark(PhaseAcc* pa, int k) {
 #if DXRPT_DIAG_PHASES
     if (pa) {
@@ -1274,15 +1279,22 @@ PT_DEV void phase_mark(PhaseAcc* pa, int k) {
     }
 #endif
 }
-PT_DEV void phase_flush(PhaseAcc* pa) {
+PT_DEV void phase_flush(PhaseAcc* pa, int set = 0) {
 #if DXRPT_DIAG_PHASES
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         uint32_t v = pa->a[k];
         for (int off = 32; off > 0; off >>= 1) v += uint32_t(__shfl_xor(int(v), off));
-        if ((threadIdx.x & 63u) == 0u) atomicAdd(&g_phase_ticks[k], (unsigned long long)v);
+        if ((threadIdx.x & 63u) == 0u) atomicAdd(&g_phase_ticks[set * 8 + k], (unsigned long long)v);
     }
 #endif
+}
+PT_DEV PhaseAcc phase_start() {
+    PhaseAcc pa = {{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, 0u};
+#if DXRPT_DIAG_PHASES
+    pa.t = uint32_t(__builtin_amdgcn_s_memrealtime());
+#endif
+    return pa;
 }
 
 // A vertex's shadow rays (ShadowHit/Miss/AnyHit, RayTrace.hlsl:497-507, 532-542) in its per-slot buffers
@@ -1293,10 +1305,10 @@ PT_DEV void phase_flush(PhaseAcc* pa) {
 // per lane, after the packet.  cnt[2..3]: the census' any-hit node / triangle fetches.
 template <bool kCount, bool kNear = false>
 PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh, bool sun0, uint32_t packet, float4& rad,
-                           uint32_t* cnt) {
+                           uint32_t* cnt, PhaseAcc* pa = nullptr) {
     uint32_t unused[4] = {0u, 0u, 0u, 0u};
     if (!kCount) cnt = unused;
-    for (uint32_t k = 0; __ballot(k < nsh) != 0ull; ++k) {
+    for (uint32_t k = 0; __ballot(k < nsh) != 0ull; phase_mark(pa, 3 + int(k < 2u ? k : 2u)), ++k) {
         const bool live = k < nsh;
         const size_t slot = size_t(k) * A.F.qsize + slot_p;
         float4 o4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d4 = make_float4(0.0f, 0.0f, 1.0f, 0.0f), c4 = o4;
@@ -1593,7 +1605,7 @@ PT_DEV void census_flush(const KArgs& A, const uint32_t (&cnt)[10]) {
 
 // Raygen + depth 1 of camera path p (the head's per-lane body).
 template <bool kCount>
-PT_DEV void head_path(const KArgs& A, uint32_t p, uint32_t blk, uint32_t* cnt) {
+PT_DEV void head_path(const KArgs& A, uint32_t p, uint32_t blk, uint32_t* cnt, PhaseAcc* pa = nullptr) {
     const dxrpt_app_settings& set = A.P.set;
     const PrimaryRay pr = primary_ray(A, p);
     const uint32_t packet = (p | 63u) < A.P.num_paths ? A.P.packet : 0u;
@@ -1609,6 +1621,7 @@ PT_DEV void head_path(const KArgs& A, uint32_t p, uint32_t blk, uint32_t* cnt) {
         cnt[1] += nt;
         if (h.tri != kMiss) ++cnt[4];
     }
+    phase_mark(pa, 0);
     VertexIn V;
     V.inOrigin = pr.start;
     V.inDir = pr.dir;
@@ -1625,6 +1638,7 @@ PT_DEV void head_path(const KArgs& A, uint32_t p, uint32_t blk, uint32_t* cnt) {
         emit_shadow(A, p, nsh, o, dd, tmn, tmx, c, fo);
     }, O);
     count_rays(A.F.counters + (kMaxDepthQueues + 1u) * kQueueShards, nsh);
+    phase_mark(pa, 1);
     const bool cont = O.cont;
     const bool nextDiffuse = O.nextIsDiffuse;
     const uint32_t qpos = split_push(A, 1, cont, O, pr.pixelIdx, pr.accumIdx, blk, gridDim.x);
@@ -1632,8 +1646,10 @@ PT_DEV void head_path(const KArgs& A, uint32_t p, uint32_t blk, uint32_t* cnt) {
     rad.x += 1.0f * O.local.x;
     rad.y += 1.0f * O.local.y;
     rad.z += 1.0f * O.local.z;
-    vertex_shadows<kCount>(A, 1, p, nsh, sun0, packet, rad, cnt);
+    phase_mark(pa, 2);
+    vertex_shadows<kCount>(A, 1, p, nsh, sun0, packet, rad, cnt, pa);
     split_finish(A, 1, cont, qpos, nextDiffuse, pr.accumIdx, rad);
+    phase_mark(pa, 6);
 }
 
 // Raygen + depth 1 of every camera path (one 64-path 8x8 block per wave, XCD runs as k_path).  kCount: the
@@ -1647,7 +1663,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     const uint32_t blk = A.P.xcd_chunk ? xcd_position(blockIdx.x, gridDim.x, A.P.xcd_chunk) : blockIdx.x;
     const uint32_t p = blk * blockDim.x + threadIdx.x;  // path slot (shadow-slot index)
     if (!kCount) {
+#if DXRPT_DIAG_PHASES
+        PhaseAcc pa = phase_start();
+        if (p < A.P.num_paths) head_path<false>(A, p, blk, nullptr, &pa);
+        phase_mark(&pa, 7);
+        phase_flush(&pa, 1);
+#else
         if (p < A.P.num_paths) head_path<false>(A, p, blk, nullptr);
+#endif
         return;
     }
     uint32_t cnt[10] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
@@ -1657,7 +1680,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
 
 // Depth d of queued path i (the tail's per-lane body; j = the lane's queue wave, nw = waves with work).
 template <bool kCount>
-PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw, const uint32_t* cnt_q, uint32_t* cnt) {
+PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw, const uint32_t* cnt_q, uint32_t* cnt,
+                      PhaseAcc* pa = nullptr) {
     const dxrpt_app_settings& set = A.P.set;
     const uint32_t pos = queue_pos(cnt_q, A.F.cap_r, i);
     const RayQueue& Q = A.F.q[d & 1];
@@ -1672,6 +1696,7 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
             if (h.tri != kMiss) ++cnt[9];
         }
     }
+    phase_mark(pa, 0);
     // the rest of the path state comes back from the queue after the traversal (the radiance so far only
     // once the vertex is shaded: it is not live across path_vertex)
     const float4 o4 = Q.org[pos], d4 = Q.dir[pos], t4 = Q.thr[pos];
@@ -1691,6 +1716,7 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
         emit_shadow(A, i, nsh, o, dd, tmn, tmx, c, fo);  // shadow slots by the dense index (< qsize)
     }, O);
     count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, nsh);
+    phase_mark(pa, 1);
     const bool cont = O.cont;
     const bool nextDiffuse = O.nextIsDiffuse;
     const int L = set.MaxPathLength < 2 ? 2 : set.MaxPathLength;
@@ -1700,8 +1726,10 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
     rad.x += V.pathThr.x * O.local.x;
     rad.y += V.pathThr.y * O.local.y;
     rad.z += V.pathThr.z * O.local.z;
-    vertex_shadows<kCount, true>(A, d, i, nsh, false, 0u, rad, kCount ? cnt + 5 : nullptr);
+    phase_mark(pa, 2);
+    vertex_shadows<kCount, true>(A, d, i, nsh, false, 0u, rad, kCount ? cnt + 5 : nullptr, pa);
     split_finish(A, d, cont, qpos, nextDiffuse, accumIdx, rad);
+    phase_mark(pa, 6);
 }
 
 // Depth d of the paths queued for it (one per lane); waves past the queued count exit at once (the grid
@@ -1719,7 +1747,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     lut_fill(A.S);
     const uint32_t i = j * blockDim.x + threadIdx.x;
     if (!kCount) {
+#if DXRPT_DIAG_PHASES
+        PhaseAcc pa = phase_start();
+        if (i < n) tail_path<false>(A, d, i, j, nw, cnt_q, nullptr, &pa);
+        phase_mark(&pa, 7);
+        phase_flush(&pa, 2);
+#else
         if (i < n) tail_path<false>(A, d, i, j, nw, cnt_q, nullptr);
+#endif
         return;
     }
     uint32_t cnt[10] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
@@ -2075,11 +2110,13 @@ hipError_t launch_sample_cmj(const uint4* cases, uint32_t n, float2* out, hipStr
     return hipGetLastError();
 }
 
-hipError_t read_phase_ticks(unsigned long long out[8]) {
+hipError_t read_phase_ticks(unsigned long long out[kPhaseClockWords]) {
+    static_assert(kPhaseClockWords == kPhaseSets * 8, "phase clock sets");
     hipError_t e = hipDeviceSynchronize();
     if (e != hipSuccess) return e;
-    if ((e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_ticks), 8 * sizeof(unsigned long long))) != hipSuccess) return e;
-    const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if ((e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_ticks), kPhaseClockWords * sizeof(unsigned long long))) != hipSuccess)
+        return e;
+    const unsigned long long zero[kPhaseClockWords] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_phase_ticks), zero, sizeof(zero));
 }
 

@@ -148,8 +148,9 @@ class DXRPathTracer:
 
     def phase_clocks(self):
         """Lane ticks per camera-path phase since the last call (kernel builds with -DDXRPT_DIAG_PHASES=1;
-        zeros otherwise), see dxrpt_get_phase_clocks."""
-        out = (C.c_uint64 * 8)()
+        zeros otherwise), see dxrpt_get_phase_clocks: 24 values, [0:8] k_path, [8:16] k_path_head, [16:24]
+        k_path_tail."""
+        out = (C.c_uint64 * A.PHASE_CLOCKS)()
         self._check(self._L.dxrpt_get_phase_clocks(self._ctx, out), "dxrpt_get_phase_clocks")
         return [int(v) for v in out]
 

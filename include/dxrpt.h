@@ -435,11 +435,16 @@ int dxrpt_get_stats(dxrpt_ctx* ctx, dxrpt_stats* out);
  * out[2 w + 1] and the slot count into *num_waves. */
 int dxrpt_get_wave_clocks(dxrpt_ctx* ctx, uint64_t* out, uint32_t max_waves, uint32_t* num_waves);
 /* Diagnostic of kernel builds made with -DDXRPT_DIAG_PHASES=1 (zeros in the shipped build): lane time,
- * in s_memrealtime ticks (100 MHz) summed over every lane of the full-frame megakernel, spent in each
- * phase of a camera path since the last call -- 0 raygen + depth-1 closest hit, 1 depth-1 shading,
- * 2 depth-1 shadow rays, 3/4/5 the same at depth 2, 6 depths >= 3, 7 accumulation and waiting for the
- * wave's other lanes after the path ended.  Synchronises the device; reads and zeroes the sums. */
-int dxrpt_get_phase_clocks(dxrpt_ctx* ctx, uint64_t out[8]);
+ * in s_memrealtime ticks (100 MHz) summed over every lane, spent in each phase of a camera path since the
+ * last call; reads and zeroes the sums (synchronises the device).  Three sets of 8 (ABI 4):
+ *   out[0..7]   the single k_path: 0 raygen + depth-1 closest hit, 1 depth-1 shading, 2 depth-1 shadow rays,
+ *               3/4/5 the same at depth 2, 6 depths >= 3, 7 accumulation and waiting for the wave's other
+ *               lanes after the path ended;
+ *   out[8..15]  k_path_head and out[16..23] k_path_tail (all depths): 0 ray setup + closest hit, 1 shading
+ *               (path_vertex), 2 continuation push, 3 / 4 / 5 shadow slot 0 / 1 / >= 2, 6 radiance hand-off,
+ *               7 waiting for the wave's other lanes. */
+#define DXRPT_PHASE_CLOCKS 24
+int dxrpt_get_phase_clocks(dxrpt_ctx* ctx, uint64_t out[DXRPT_PHASE_CLOCKS]);
 
 /* TraceRay on arbitrary rays against the built acceleration structure (the DXR TraceRay call sites
  * RayTrace.hlsl:138,258,305,407,425 without the shading).  `rays` (device) holds num_rays pairs of

@@ -101,9 +101,13 @@ def main():
         print("  per launch: " + ", ".join(parts), flush=True)
     if args.phases:
         ph = t.phase_clocks()
-        tot = float(sum(ph)) or 1.0
         names = ("d1 trace", "d1 shade", "d1 shadow", "d2 trace", "d2 shade", "d2 shadow", "d>=3", "end/idle")
-        print("  phases (share of lane time): " + ", ".join(f"{nm} {v / tot:.3f}" for nm, v in zip(names, ph)), flush=True)
+        split = ("trace", "shade", "push", "shadow0", "shadow1", "shadow2+", "handoff", "idle")
+        for label, part, nm in (("k_path", ph[0:8], names), ("k_path_head", ph[8:16], split), ("k_path_tail", ph[16:24], split)):
+            tot = float(sum(part))
+            if tot:
+                print(f"  {label} phases (share of lane time, {tot / 1e8 / args.rounds / args.frames:.4g} lane-s/frame): "
+                      + ", ".join(f"{n} {v / tot:.3f}" for n, v in zip(nm, part)), flush=True)
     t.close()
 
 
