@@ -17,6 +17,7 @@
 #include <condition_variable>
 #include <deque>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <chrono>
@@ -32,8 +33,8 @@ unsigned build_threads(const BvhBuildParams* params) {
 }
 
 // Fork-join pool for the builders' independent subtrees.  A thread that waits for a task it spawned runs
-// queued tasks meanwhile (so nested waits cannot deadlock); tasks are taken oldest first -- the largest
-// subtrees, spawned nearest the root -- which spreads the big pieces over the workers.
+// queued tasks meanwhile (so nested waits cannot deadlock); workers take the oldest tasks -- the largest
+// subtrees, spawned nearest the root -- which spreads the big pieces over them.
 class TaskPool {
 public:
     explicit TaskPool(unsigned n) {
@@ -55,15 +56,16 @@ public:
         }
         cv_.notify_one();
     }
-    // Runs queued tasks until `done` is set.
+    // Runs queued tasks until `done` is set, newest first (most likely the awaited task or its own children;
+    // the workers take the oldest, largest ones).
     void wait(const std::atomic<bool>& done) {
         while (!done.load(std::memory_order_acquire)) {
             std::function<void()> f;
             {
                 std::lock_guard<std::mutex> g(m_);
                 if (!q_.empty()) {
-                    f = std::move(q_.front());
-                    q_.pop_front();
+                    f = std::move(q_.back());
+                    q_.pop_back();
                 }
             }
             if (f) f();
@@ -269,6 +271,8 @@ struct Builder {
         return true;
     }
 };
+
+double tree_sah(const std::vector<TNode>& tree);
 
 // Spatial-split binary builder (SBVH, Stich et al. 2009) for the BVH8 path: at nodes whose best
 // object split leaves overlapping children, it also bins the node box into slabs, clips each
@@ -578,7 +582,7 @@ struct SpatialBuilder {
     // Partitions the references of a node (bounds nb, at `depth`, duplication allowance `budget`) into L
     // and R; returns the number of references it duplicated.
     size_t split_node(std::vector<Ref>& rs, const Box& nb, uint32_t depth, size_t budget, std::vector<Ref>& L,
-                      std::vector<Ref>& R) const {
+                      std::vector<Ref>& R, Box& lb, Box& rb) const {
         const size_t n = rs.size();
         uint32_t levels = 0;
         for (size_t m = n; m > 1; m = (m + 1) / 2) ++levels;
@@ -603,38 +607,52 @@ struct SpatialBuilder {
                 const size_t nk = max_chunks(n);
                 std::vector<std::vector<Ref>> Lk(nk), Rk(nk);
                 std::vector<size_t> dk(nk, 0);
+                std::vector<Box> lbk(nk), rbk(nk);
                 if (nk == 1) {
                     Lk[0].reserve(n / 2 + 16);
                     Rk[0].reserve(n / 2 + 16);
                 }
                 const size_t K = chunked(n, [&](size_t k, size_t b, size_t e) {
+                    auto left = [&](const Ref& r) {
+                        Lk[k].push_back(r);
+                        lbk[k].grow(r.box);
+                    };
+                    auto right = [&](const Ref& r) {
+                        Rk[k].push_back(r);
+                        rbk[k].grow(r.box);
+                    };
                     for (size_t i = b; i < e; ++i) {
                         const Ref& r = rs[i];
-                        if (r.box.hi[ss.axis] <= ss.plane) Lk[k].push_back(r);
-                        else if (r.box.lo[ss.axis] >= ss.plane) Rk[k].push_back(r);
+                        if (r.box.hi[ss.axis] <= ss.plane) left(r);
+                        else if (r.box.lo[ss.axis] >= ss.plane) right(r);
                         else {
                             Box bl, br;
                             const bool whole = keep_whole && keep_whole[r.tri];
                             if (!whole) split_ref(r, ss.axis, ss.plane, bl, br);
                             if (!whole && !bl.empty() && !br.empty() && bl.lo[ss.axis] <= bl.hi[ss.axis] && br.lo[ss.axis] <= br.hi[ss.axis]) {
-                                Lk[k].push_back(Ref{r.tri, bl});
-                                Rk[k].push_back(Ref{r.tri, br});
+                                left(Ref{r.tri, bl});
+                                right(Ref{r.tri, br});
                                 dk[k]++;
                             } else if (0.5f * (r.box.lo[ss.axis] + r.box.hi[ss.axis]) < ss.plane) {
-                                Lk[k].push_back(r);
+                                left(r);
                             } else {
-                                Rk[k].push_back(r);
+                                right(r);
                             }
                         }
                     }
                 });
                 concat(Lk, K, L);
                 concat(Rk, K, R);
-                for (size_t k = 0; k < K; ++k) dup += dk[k];
+                for (size_t k = 0; k < K; ++k) {
+                    dup += dk[k];
+                    lb.grow(lbk[k]);
+                    rb.grow(rbk[k]);
+                }
                 if (L.empty() || R.empty()) {
                     L.clear();
                     R.clear();
                     dup = 0;
+                    lb = rb = Box();
                 }
             }
             if (L.empty() && os.axis >= 0) {
@@ -657,6 +675,9 @@ struct SpatialBuilder {
                 if (L.empty() || R.empty()) {
                     L.clear();
                     R.clear();
+                } else {  // the bins' boxes on each side of the chosen plane: exactly the children's bounds
+                    lb = os.left;
+                    rb = os.right;
                 }
             }
         }
@@ -677,42 +698,31 @@ struct SpatialBuilder {
             });
             L.assign(rs.begin(), rs.begin() + m);
             R.assign(rs.begin() + m, rs.end());
+            lb = bounds_of(L);
+            rb = bounds_of(R);
         }
         return dup;
     }
 
-    // A subtree in pre-order (node 0 its root, children after their parent, left subtree before right), its
-    // leaves' references in the same order.
+    // A subtree built by one task: node 0 its root, children after their parent; a child index kExternal | k
+    // is the root of kids[k], a subtree built by a task of its own.  Stitched into one array at the end
+    // (stitch): every node is copied once, whatever the nesting of tasks.
+    static constexpr int32_t kExternal = int32_t(1u << 30);
     struct Sub {
         std::vector<TNode> nodes;
         std::vector<uint32_t> refs;
+        std::vector<std::unique_ptr<Sub>> kids;
+        size_t node_off = 0, ref_off = 0;  // in the stitched arrays
         bool deep = false;  // the depth cap was exceeded
         bool oom = false;   // a task ran out of memory
     };
 
-    // Appends subtree src to dst; returns the index of its root in dst.
-    static int32_t append(Sub& dst, const Sub& src) {
-        const int32_t off = int32_t(dst.nodes.size());
-        const uint32_t roff = uint32_t(dst.refs.size());
-        for (TNode nd : src.nodes) {
-            if (nd.count) nd.first += roff;
-            else {
-                nd.child[0] += off;
-                nd.child[1] += off;
-            }
-            dst.nodes.push_back(nd);
-        }
-        dst.refs.insert(dst.refs.end(), src.refs.begin(), src.refs.end());
-        dst.deep |= src.deep;
-        dst.oom |= src.oom;
-        return off;
-    }
-
-    // Builds the subtree of `rs` (consumed) into out; returns the index of its root.
-    int32_t build_rec(Sub& out, std::vector<Ref>& rs, uint32_t depth, size_t budget) {
+    // Builds the subtree of `rs` (consumed; bounds nb) into out; returns the index of its root.  Children of at
+    // least kTaskRefs references each are built as tasks -- by size alone, so the task structure and the tree
+    // are the same for any thread count.
+    int32_t build_rec(Sub& out, std::vector<Ref>& rs, const Box& nb, uint32_t depth, size_t budget) {
         const int32_t idx = int32_t(out.nodes.size());
         out.nodes.emplace_back();
-        const Box nb = bounds_of(rs);
         out.nodes[size_t(idx)].box = nb;
         const size_t n = rs.size();
         if (n <= 1) {
@@ -727,78 +737,108 @@ struct SpatialBuilder {
             return idx;
         }
         std::vector<Ref> L, R;
-        const size_t dup = split_node(rs, nb, depth, budget, L, R);
+        Box lb, rb;
+        const size_t dup = split_node(rs, nb, depth, budget, L, R, lb, rb);
         std::vector<Ref>().swap(rs);
         // the allowance left after this split, shared in proportion to the children's references
         const size_t rest = budget > dup ? budget - dup : 0;
         const size_t bl = size_t(double(rest) * double(L.size()) / double(L.size() + R.size()));
         const size_t br = rest - bl;
         int32_t c0, c1;
-        if (pool && pool->parallel() && L.size() >= kTaskRefs && R.size() >= kTaskRefs) {
-            Sub sr;
+        if (pool && L.size() >= kTaskRefs && R.size() >= kTaskRefs) {
+            Sub* sr = new Sub;
+            c1 = kExternal | int32_t(out.kids.size());
+            out.kids.emplace_back(sr);
             std::atomic<bool> done{false};
-            pool->submit([&] {
+            pool->submit([&, sr] {
                 try {
-                    build_rec(sr, R, depth + 1, br);
+                    build_rec(*sr, R, rb, depth + 1, br);
                 } catch (...) {  // bad_alloc: reported by the caller, never thrown across threads
-                    sr.oom = true;
+                    sr->oom = true;
                 }
                 done.store(true, std::memory_order_release);
             });
-            c0 = build_rec(out, L, depth + 1, bl);
+            c0 = build_rec(out, L, lb, depth + 1, bl);
             pool->wait(done);
-            c1 = append(out, sr);
         } else {
-            c0 = build_rec(out, L, depth + 1, bl);
-            c1 = build_rec(out, R, depth + 1, br);
+            c0 = build_rec(out, L, lb, depth + 1, bl);
+            c1 = build_rec(out, R, rb, depth + 1, br);
         }
         out.nodes[size_t(idx)].child[0] = c0;
         out.nodes[size_t(idx)].child[1] = c1;
         return idx;
     }
 
+    // The task subtrees in one array (tree, refs): subtree blocks in the order root, then breadth-first over
+    // the task tree; copied in parallel, external child indices resolved to their subtree's block.
+    void stitch(Sub& root, TaskPool& tp, bool& deep, bool& oom) {
+        std::vector<Sub*> subs{&root};
+        for (size_t i = 0; i < subs.size(); ++i)
+            for (auto& k : subs[i]->kids) subs.push_back(k.get());
+        size_t nn = 0, nr = 0;
+        for (Sub* x : subs) {
+            x->node_off = nn;
+            x->ref_off = nr;
+            nn += x->nodes.size();
+            nr += x->refs.size();
+            deep |= x->deep;
+            oom |= x->oom;
+        }
+        if (deep || oom) return;
+        tree.resize(nn);
+        refs.resize(nr);
+        std::atomic<size_t> cursor{0}, left{subs.size()};
+        std::atomic<bool> done{false};
+        auto worker = [&] {
+            for (size_t i; (i = cursor.fetch_add(1)) < subs.size();) {
+                const Sub& x = *subs[i];
+                for (size_t j = 0; j < x.nodes.size(); ++j) {
+                    TNode t = x.nodes[j];
+                    if (t.count) t.first += uint32_t(x.ref_off);
+                    else
+                        for (int c = 0; c < 2; ++c)
+                            t.child[c] = (t.child[c] & kExternal) ? int32_t(x.kids[size_t(t.child[c] & ~kExternal)]->node_off)
+                                                                  : t.child[c] + int32_t(x.node_off);
+                    tree[x.node_off + j] = t;
+                }
+                std::copy(x.refs.begin(), x.refs.end(), refs.begin() + std::ptrdiff_t(x.ref_off));
+                if (left.fetch_sub(1) == 1) done.store(true, std::memory_order_release);
+            }
+        };
+        for (unsigned t = 1; t < threads; ++t) tp.submit(worker);
+        worker();
+        tp.wait(done);
+    }
+
     bool build(uint32_t ntris, const std::vector<Box>& tri_box, std::string& err) {
         std::vector<Ref> all(ntris);
         for (uint32_t t = 0; t < ntris; ++t) all[t] = Ref{t, tri_box[t]};
-        root_area = std::max(bounds_of(all).area(), 1e-30);
-        Sub root;
-        root.nodes.reserve(size_t(ntris) * 4);
-        root.refs.reserve(std::max(ref_budget, size_t(ntris)) + size_t(ntris) / 4);
+        bool deep = false, oom = false;
         {
             TaskPool tp(threads);
             pool = &tp;
+            const Box rb = bounds_of(all);
+            root_area = std::max(rb.area(), 1e-30);
+            Sub root;
+            root.nodes.reserve(size_t(ntris) / 2 + 16);
             try {
-                build_rec(root, all, 0, ref_budget > ntris ? ref_budget - ntris : 0);
+                build_rec(root, all, rb, 0, ref_budget > ntris ? ref_budget - ntris : 0);
+                stitch(root, tp, deep, oom);
             } catch (...) {
-                root.oom = true;
+                oom = true;
             }
             pool = nullptr;
         }
-        if (root.oom) {
+        if (oom) {
             err = "build_bvh: out of memory";
             return false;
         }
-        if (root.deep) {
+        if (deep) {
             err = "build_bvh: depth cap exceeded";
             return false;
         }
-        tree.swap(root.nodes);
-        refs.swap(root.refs);
-        // subtree ranges: children follow their parent, and each subtree's references are contiguous
-        // (pre-order, left before right)
-        sah = 0.0;
-        for (size_t i = tree.size(); i-- > 0;) {
-            TNode& nd = tree[i];
-            if (!nd.count) {
-                nd.begin = tree[size_t(nd.child[0])].begin;
-                nd.end = tree[size_t(nd.child[1])].end;
-                sah += nd.box.area() / root_area;
-            } else {
-                nd.begin = nd.first;
-                nd.end = nd.first + nd.count;
-                sah += nd.box.area() / root_area * double(nd.count);
-            }
-        }
+        // (begin / end are not kept: the treelet pass and the collapse count and gather references by walking)
+        sah = tree_sah(tree);
         return true;
     }
 };

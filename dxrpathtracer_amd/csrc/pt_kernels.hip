@@ -1334,6 +1334,66 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
     }
 }
 
+// A vertex's (at most) two shadow rays in ONE per-lane traversal loop (r05).  Without spot lights a vertex
+// emits at most the sun's shadow ray (exact SunDirectionWS, RayTrace.hlsl:242-258) and, at the path's last
+// vertex, the sky-visibility ray (:415-425); both leave positionWS with TMin 1e-5 and TMax FP32Max.  A lane
+// traces them back to back: when its first ray is decided (an accepted occluder, or the stack runs empty) it
+// restarts from the root with the second direction while the wave's other lanes go on, so the wave waits for
+// the slowest lane's SUM of the two traversals instead of the slowest first ray plus the slowest second ray.
+// Each any-hit result is a boolean over every occluder of its ray, so the visibilities -- and the radiance,
+// added in slot order after the loop -- are those of vertex_shadows bit for bit; so are the census counts
+// (cnt[2..3]: the same node visits and triangle tests per ray).  Requires nsh <= 2 and the rays of a frame
+// without spot lights (A.P.rtc.NumLights == 0).
+#ifndef DXRPT_CHAIN_SHADOWS
+#define DXRPT_CHAIN_SHADOWS 1
+#endif
+template <bool kCount>
+PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh, float4& rad, uint32_t* cnt,
+                                   PhaseAcc* pa = nullptr) {
+    uint32_t unused[4] = {0u, 0u, 0u, 0u};
+    if (!kCount) cnt = unused;
+    const size_t s0 = slot_p, s1 = size_t(A.F.qsize) + slot_p;
+    bool active = nsh > 0u;
+    uint32_t occ = 0u;  // bit k: the ray of slot k is occluded
+    if (active) {
+        const float4 o4 = A.F.sh_org[s0], d4 = A.F.sh_dir[s0];
+        const float4 d41 = nsh > 1u ? A.F.sh_dir[s1] : d4;
+        const bool alpha0 = fbits(A.F.sh_con[s0].w) == 0u;
+        const bool alpha1 = nsh > 1u ? fbits(A.F.sh_con[s1].w) == 0u : alpha0;
+        const f3 o = ld3(o4), dir1 = ld3(d41);
+        Ray8 R;
+        HitRec h;
+        ray8_init(R, o, ld3(d4), d4.w, o4.w, alpha0, h);
+        uint32_t node = 0, k = 0;
+        int sp = 0;
+        uint2 tos = make_uint2(0u, 0u);
+        while (active) {
+            uint32_t tbase = 0, tbits = 0;
+            const bool more = trav8_node<kCount, true>(A.S, R, load_node8(A.S, node), node, sp, tos, h, tbase, tbits, cnt[2]);
+            const bool hit = tbits != 0u && trav8_tris<true, kCount>(A.S, R, tbase, tbits, h, cnt[3]);
+            if (hit || !more) {
+                occ |= uint32_t(hit) << k;
+                if (++k < nsh) {  // the second ray: same origin, TMin, TMax
+                    ray8_init(R, o, dir1, d4.w, o4.w, alpha1, h);
+                    node = 0;
+                    sp = 0;
+                    tos = make_uint2(0u, 0u);
+                } else {
+                    active = false;
+                }
+            }
+        }
+    }
+    phase_mark(pa, 3);
+    for (uint32_t k = 0; k < nsh; ++k) {  // slot order, as vertex_shadows
+        const float4 c4 = A.F.sh_con[size_t(k) * A.F.qsize + slot_p];
+        const bool occluded = (occ >> k) & 1u;
+        rad.x += occluded ? c4.x * 0.0f : c4.x;
+        rad.y += occluded ? c4.y * 0.0f : c4.y;
+        rad.z += occluded ? c4.z * 0.0f : c4.z;
+    }
+}
+
 // One path from its first ray (PathLength 1) to its end: per depth the closest hit, path_vertex and the
 // vertex's shadow rays in slot order -- the megakernel's per-thread loop, shared by k_path (camera paths)
 // and k_bake (lightmap texels).  `slot_p` (< F.qsize) indexes the per-slot shadow buffers, `pix` is the
@@ -1386,7 +1446,12 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
         rad.x += thr.x * O.local.x;
         rad.y += thr.y * O.local.y;
         rad.z += thr.z * O.local.z;
-        vertex_shadows<kCount, kNearest>(A, d, slot_p, nsh, sun0, packet, rad, cd);
+        // depth >= 2 (the depth-1 sun shadows of full waves take the packet traversal): the vertex's rays
+        // chained in one loop where the budget has the registers (kNearest: <= 5 waves/SIMD)
+        if (kNearest && DXRPT_CHAIN_SHADOWS && A.P.rtc.NumLights == 0u && (d > 1 || !(packet & 2u)))
+            vertex_shadows_chained<kCount>(A, slot_p, nsh, rad, kCount ? cd : nullptr);
+        else
+            vertex_shadows<kCount, kNearest>(A, d, slot_p, nsh, sun0, packet, rad, cd);
         phase_mark(pa, d == 1 ? 2 : d == 2 ? 5 : 6);
         if (!O.cont) break;
         org = O.nextOrigin;
@@ -1679,7 +1744,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
 }
 
 // Depth d of queued path i (the tail's per-lane body; j = the lane's queue wave, nw = waves with work).
-template <bool kCount>
+template <bool kCount, bool kLast>
 PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw, const uint32_t* cnt_q, uint32_t* cnt,
                       PhaseAcc* pa = nullptr) {
     const dxrpt_app_settings& set = A.P.set;
@@ -1727,7 +1792,13 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
     rad.y += V.pathThr.y * O.local.y;
     rad.z += V.pathThr.z * O.local.z;
     phase_mark(pa, 2);
-    vertex_shadows<kCount, true>(A, d, i, nsh, false, 0u, rad, kCount ? cnt + 5 : nullptr, pa);
+    // the last depth's vertices emit the sun's and the sky-visibility ray: chained (wave-uniform test: no spot
+    // lights, <= 2 rays per vertex); the other depths have at most the sun's and keep the slot loop, in
+    // instantiations without the chained code (its registers cost the single-ray tails 2-3 %, r05)
+    if (kLast && DXRPT_CHAIN_SHADOWS && A.P.rtc.NumLights == 0u)
+        vertex_shadows_chained<kCount>(A, i, nsh, rad, kCount ? cnt + 5 : nullptr, pa);
+    else
+        vertex_shadows<kCount, true>(A, d, i, nsh, false, 0u, rad, kCount ? cnt + 5 : nullptr, pa);
     split_finish(A, d, cont, qpos, nextDiffuse, accumIdx, rad);
     phase_mark(pa, 6);
 }
@@ -1735,7 +1806,7 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
 // Depth d of the paths queued for it (one per lane); waves past the queued count exit at once (the grid
 // covers every path of the frame).  kCount: the census instantiation (the tails' traversal orders: closest
 // hits nearest child first with triangle pairs, any-hit rays far to near).
-template <int kOcc, bool kCount = false>
+template <int kOcc, bool kCount = false, bool kLast = false>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_path_tail(KArgs A, int d) {
     const uint32_t* cnt_q = A.F.counters + uint32_t(d) * kQueueShards;
     const uint32_t n = queue_total(cnt_q);
@@ -1749,16 +1820,16 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     if (!kCount) {
 #if DXRPT_DIAG_PHASES
         PhaseAcc pa = phase_start();
-        if (i < n) tail_path<false>(A, d, i, j, nw, cnt_q, nullptr, &pa);
+        if (i < n) tail_path<false, kLast>(A, d, i, j, nw, cnt_q, nullptr, &pa);
         phase_mark(&pa, 7);
         phase_flush(&pa, 2);
 #else
-        if (i < n) tail_path<false>(A, d, i, j, nw, cnt_q, nullptr);
+        if (i < n) tail_path<false, kLast>(A, d, i, j, nw, cnt_q, nullptr);
 #endif
         return;
     }
     uint32_t cnt[10] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    if (i < n) tail_path<true>(A, d, i, j, nw, cnt_q, cnt);
+    if (i < n) tail_path<true, kLast>(A, d, i, j, nw, cnt_q, cnt);
     census_flush(A, cnt);
 }
 
@@ -1879,17 +1950,26 @@ static void launch_split(const KArgs& A, uint32_t gm, size_t lds, hipStream_t s,
     const int L = fp.set.MaxPathLength < 2 ? 2 : fp.set.MaxPathLength;
     if (census) {
         hipLaunchKernelGGL((k_path_head<5, true>), dim3(gm), dim3(kWave), lds, s, A);
-        for (int d = 2; d <= L - 1; ++d) hipLaunchKernelGGL((k_path_tail<7, true>), dim3(gm), dim3(kWave), lds, s, A, d);
+        for (int d = 2; d <= L - 1; ++d) {
+            if (d < L - 1) hipLaunchKernelGGL((k_path_tail<7, true, false>), dim3(gm), dim3(kWave), lds, s, A, d);
+            else hipLaunchKernelGGL((k_path_tail<7, true, true>), dim3(gm), dim3(kWave), lds, s, A, d);
+        }
         return;
     }
 #define DXRPT_HEAD(O) hipLaunchKernelGGL((k_path_head<O>), dim3(gm), dim3(kWave), lds, s, A)
     DXRPT_OCC_SWITCH(fp.megakernel_occupancy, DXRPT_HEAD)
 #undef DXRPT_HEAD
     if (head_ev) (void)hipEventRecord(head_ev, s);
-    for (int d = 2; d <= L - 1; ++d) {
-#define DXRPT_TAIL(O) hipLaunchKernelGGL((k_path_tail<O>), dim3(gm), dim3(kWave), lds, s, A, d)
-        DXRPT_OCC_SWITCH(fp.tail_occupancy, DXRPT_TAIL)
+    for (int d = 2; d <= L - 1; ++d) {  // the last depth's tail: its own instantiation (chained shadow rays)
+#define DXRPT_TAIL(O) hipLaunchKernelGGL((k_path_tail<O, false, false>), dim3(gm), dim3(kWave), lds, s, A, d)
+#define DXRPT_TAIL_LAST(O) hipLaunchKernelGGL((k_path_tail<O, false, true>), dim3(gm), dim3(kWave), lds, s, A, d)
+        if (d < L - 1) {
+            DXRPT_OCC_SWITCH(fp.tail_occupancy, DXRPT_TAIL)
+        } else {
+            DXRPT_OCC_SWITCH(fp.tail_occupancy, DXRPT_TAIL_LAST)
+        }
 #undef DXRPT_TAIL
+#undef DXRPT_TAIL_LAST
     }
 }
 
