@@ -71,6 +71,44 @@ PT_DEV void lut_fill(const SceneDev& S) {
     __syncthreads();
 }
 
+// A texel's word in the tiled pool (pt_kernels.h tex_tile_word), branch-free in the format: both tilings'
+// addresses are computed and one selected, so a bilinear tap's four loads issue back to back.  (r05: with
+// the format test as a branch -- the format is per lane -- the compiler serialised the four loads, each
+// behind an s_waitcnt vmcnt(0) of the one before: four dependent memory round trips per tap, in every
+// material tap and every AnyHitShader opacity tap.)
+PT_DEV uint32_t tex_word(uint32_t x, uint32_t y, uint32_t tiles_x, bool r8) {
+    const uint32_t a = ((y >> 3) * tiles_x + (x >> 4)) * kTexTileWords + (y & 7u) * 4u + ((x & 15u) >> 2);
+    const uint32_t b = ((y >> 2) * tiles_x + (x >> 3)) * kTexTileWords + (y & 3u) * 8u + (x & 7u);
+    return r8 ? a : b;
+}
+
+// Decode of one loaded texel word (the LDS table, unorm or sRGB), branch-free in the format: R8 -> (v, v, v, 1)
+// with v = the texel's byte, RGBA8 -> the four channels (alpha always unorm).
+PT_DEV Texel4 decode_texel(uint32_t w, bool r8, uint32_t l, uint32_t x) {
+    const uint32_t b0 = r8 ? ((w >> ((x & 3u) * 8u)) & 0xFFu) : l + (w & 0xFFu);
+    const uint32_t b1 = r8 ? b0 : l + ((w >> 8) & 0xFFu);
+    const uint32_t b2 = r8 ? b0 : l + ((w >> 16) & 0xFFu);
+    Texel4 t;
+    t.r = g_lut[b0];
+    t.g = g_lut[b1];
+    t.b = g_lut[b2];
+    const float a = g_lut[w >> 24];
+    t.a = r8 ? 1.0f : a;
+    return t;
+}
+
+PT_DEV TexDesc tex_desc(GeoTex g) {
+    TexDesc td;
+    td.offset = g.offset;
+    td.width = g.whf & 0x7FFFu;
+    td.height = (g.whf >> 15) & 0x7FFFu;
+    td.fmt = g.whf >> 30;
+    return td;
+}
+
+// The per-texel form (a format branch per texel): the split tails' material taps keep it -- the
+// branch-free form above costs them 5-10 % (r05, profiles/r05_ab_taps.txt), while it saves 2-5 % in the
+// head, the single k_path and the alpha tests.
 PT_DEV Texel4 fetch_texel(const SceneDev& S, const TexDesc& td, int x, int y) {
     const bool r8 = td.fmt == DXRPT_TEX_R8_UNORM;
     const uint32_t tiles_x = (td.width + (r8 ? kTexTileW8 : kTexTileW32) - 1u) / (r8 ? kTexTileW8 : kTexTileW32);
@@ -91,24 +129,40 @@ PT_DEV Texel4 fetch_texel(const SceneDev& S, const TexDesc& td, int x, int y) {
     return t;
 }
 
-PT_DEV TexDesc tex_desc(GeoTex g) {
-    TexDesc td;
-    td.offset = g.offset;
-    td.width = g.whf & 0x7FFFu;
-    td.height = (g.whf >> 15) & 0x7FFFu;
-    td.fmt = g.whf >> 30;
-    return td;
-}
-
+template <bool kGrouped = true>
 PT_DEV Texel4 sample_tex_desc(const SceneDev& S, const TexDesc td, float u, float v) {
+    if (!kGrouped) {
+        float x = u * float(td.width) - 0.5f;
+        float y = v * float(td.height) - 0.5f;
+        float x0 = floorf(x), y0 = floorf(y);
+        float fx = x - x0, fy = y - y0;
+        int ix0 = wrap_coord(int(x0), td.width), ix1 = wrap_coord(int(x0) + 1, td.width);
+        int iy0 = wrap_coord(int(y0), td.height), iy1 = wrap_coord(int(y0) + 1, td.height);
+        Texel4 t00 = fetch_texel(S, td, ix0, iy0), t10 = fetch_texel(S, td, ix1, iy0);
+        Texel4 t01 = fetch_texel(S, td, ix0, iy1), t11 = fetch_texel(S, td, ix1, iy1);
+        Texel4 r;
+        r.r = lerpf(lerpf(t00.r, t10.r, fx), lerpf(t01.r, t11.r, fx), fy);
+        r.g = lerpf(lerpf(t00.g, t10.g, fx), lerpf(t01.g, t11.g, fx), fy);
+        r.b = lerpf(lerpf(t00.b, t10.b, fx), lerpf(t01.b, t11.b, fx), fy);
+        r.a = lerpf(lerpf(t00.a, t10.a, fx), lerpf(t01.a, t11.a, fx), fy);
+        return r;
+    }
     float x = u * float(td.width) - 0.5f;
     float y = v * float(td.height) - 0.5f;
     float x0 = floorf(x), y0 = floorf(y);
     float fx = x - x0, fy = y - y0;
     int ix0 = wrap_coord(int(x0), td.width), ix1 = wrap_coord(int(x0) + 1, td.width);
     int iy0 = wrap_coord(int(y0), td.height), iy1 = wrap_coord(int(y0) + 1, td.height);
-    Texel4 t00 = fetch_texel(S, td, ix0, iy0), t10 = fetch_texel(S, td, ix1, iy0);
-    Texel4 t01 = fetch_texel(S, td, ix0, iy1), t11 = fetch_texel(S, td, ix1, iy1);
+    const bool r8 = td.fmt == DXRPT_TEX_R8_UNORM;
+    const uint32_t tiles_x = r8 ? (td.width + kTexTileW8 - 1u) / kTexTileW8 : (td.width + kTexTileW32 - 1u) / kTexTileW32;
+    const uint32_t* T = S.texels + td.offset;
+    const uint32_t w00 = T[tex_word(uint32_t(ix0), uint32_t(iy0), tiles_x, r8)];
+    const uint32_t w10 = T[tex_word(uint32_t(ix1), uint32_t(iy0), tiles_x, r8)];
+    const uint32_t w01 = T[tex_word(uint32_t(ix0), uint32_t(iy1), tiles_x, r8)];
+    const uint32_t w11 = T[tex_word(uint32_t(ix1), uint32_t(iy1), tiles_x, r8)];
+    const uint32_t l = td.fmt == DXRPT_TEX_RGBA8_SRGB ? 256u : 0u;
+    Texel4 t00 = decode_texel(w00, r8, l, uint32_t(ix0)), t10 = decode_texel(w10, r8, l, uint32_t(ix1));
+    Texel4 t01 = decode_texel(w01, r8, l, uint32_t(ix0)), t11 = decode_texel(w11, r8, l, uint32_t(ix1));
     Texel4 r;
     r.r = lerpf(lerpf(t00.r, t10.r, fx), lerpf(t01.r, t11.r, fx), fy);
     r.g = lerpf(lerpf(t00.g, t10.g, fx), lerpf(t01.g, t11.g, fx), fy);
@@ -203,6 +257,10 @@ PT_DEV OmmProbe omm_probe(const SceneDev& S, uint32_t slot, float b1, float b2) 
 PT_DEV uint32_t omm_verdict(const OmmProbe& p) { return (p.word >> p.shift) & 3u; }
 
 // AnyHitShader / ShadowAnyHitShader (RayTrace.hlsl:485-507): opacity.x < 0.35 -> IgnoreHit.
+// kGA: the opacity tap's four texel loads grouped (sample_tex_desc<true>); the split tails keep the per-texel
+// form (r05: grouped, the tails' traversal loops ran 8-10 % slower although their rays skip the alpha test by
+// default; k_path, the head and the other kernels gain 1-4 %, profiles/r05_ab_taps*.txt).
+template <bool kGA = true>
 PT_DEV bool alpha_accepts(const SceneDev& S, uint32_t geom, uint32_t gtri, uint32_t slot, float b1, float b2) {
     const GeoTex opacity = S.geoshade[geom].opacity;
     const float2* V = reinterpret_cast<const float2*>(S.tri_verts + size_t(gtri) * 12u);
@@ -220,7 +278,7 @@ PT_DEV bool alpha_accepts(const SceneDev& S, uint32_t geom, uint32_t gtri, uint3
     const float w0 = (1.0f - b1) - b2;
     float u = bary_lerp(uv[0].x, uv[1].x, uv[2].x, w0, b1, b2);
     float v = bary_lerp(uv[0].y, uv[1].y, uv[2].y, w0, b1, b2);
-    return !(sample_tex_desc(S, tex_desc(opacity), u, v).r < 0.35f);
+    return !(sample_tex_desc<kGA>(S, tex_desc(opacity), u, v).r < 0.35f);
 }
 
 // ---- triangles ------------------------------------------------------------------------------------
@@ -277,7 +335,7 @@ PT_DEV TriRec load_tri(const SceneDev& S, uint32_t rec) {
 // One candidate triangle (the "intersection + any-hit" stage of a DXR traversal).  Returns true
 // when an any-hit ray is done (accepted occluder).  Closest hit: smallest t, ties -> smallest global
 // triangle id, which makes the result independent of traversal order.
-template <bool kAnyHit>
+template <bool kAnyHit, bool kGA = true>
 PT_DEV bool test_tri_rec(const SceneDev& S, const TriRec& r, f3 o, f3 d, float tmin, float tmax, bool alpha, HitRec& h) {
     const float4 p0 = r.p0, p1 = r.p1, p2 = r.p2;
     float t, u, v;
@@ -290,7 +348,7 @@ PT_DEV bool test_tri_rec(const SceneDev& S, const TriRec& r, f3 o, f3 d, float t
         if (!(t < h.t || (t == h.t && gtri < h.tri))) return false;
     }
     const uint32_t geom = fbits(p1.w);
-    if (alpha && !(fbits(p2.w) & kTriOpaque) && !alpha_accepts(S, geom, gtri, fbits(p2.w) >> 1, u, v)) return false;
+    if (alpha && !(fbits(p2.w) & kTriOpaque) && !alpha_accepts<kGA>(S, geom, gtri, fbits(p2.w) >> 1, u, v)) return false;
     h.t = t;
     h.tri = gtri;
     h.b1 = u;
@@ -511,20 +569,20 @@ PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, const Node8Words& W, ui
 }
 
 // Tests the pending triangle group.  Returns true when an any-hit ray found an occluder.
-template <bool kAnyHit, bool kCount>
+template <bool kAnyHit, bool kCount, bool kGA = true>
 PT_DEV bool trav8_tris(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32_t tbits, HitRec& h, uint32_t& ntest) {
     while (tbits) {
         const uint32_t b = uint32_t(__builtin_ctz(tbits));
         tbits &= tbits - 1u;
         if (kCount) ++ntest;
-        if (test_tri_rec<kAnyHit>(S, load_tri(S, tbase + b), R.o, R.d, R.tmin, R.tmax, R.alpha, h)) return true;
+        if (test_tri_rec<kAnyHit, kGA>(S, load_tri(S, tbase + b), R.o, R.d, R.tmin, R.tmax, R.alpha, h)) return true;
     }
     return false;
 }
 
 // The pending group two records at a time: both records are loaded before either test, so a lane pays
 // one memory round trip per pair.  Tests still run in bit order (same results).
-template <bool kAnyHit, bool kCount>
+template <bool kAnyHit, bool kCount, bool kGA = true>
 PT_DEV bool trav8_tris2(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32_t tbits, HitRec& h, uint32_t& ntest) {
     while (tbits) {
         const uint32_t b0 = uint32_t(__builtin_ctz(tbits));
@@ -537,8 +595,8 @@ PT_DEV bool trav8_tris2(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32
         pin_tri(ra);
         pin_tri(rb);
         if (kCount) ntest += two ? 2u : 1u;
-        if (test_tri_rec<kAnyHit>(S, ra, R.o, R.d, R.tmin, R.tmax, R.alpha, h)) return true;
-        if (two && test_tri_rec<kAnyHit>(S, rb, R.o, R.d, R.tmin, R.tmax, R.alpha, h)) return true;
+        if (test_tri_rec<kAnyHit, kGA>(S, ra, R.o, R.d, R.tmin, R.tmax, R.alpha, h)) return true;
+        if (two && test_tri_rec<kAnyHit, kGA>(S, rb, R.o, R.d, R.tmin, R.tmax, R.alpha, h)) return true;
     }
     return false;
 }
@@ -549,7 +607,7 @@ PT_DEV bool trav8_tris2(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32
 // node visits and triangle tests, for a few more registers in the box test, so only kernels with the
 // budget use it (r04: the split tails and k_path at <= 5 waves/SIMD; k_path<7> spills, C2 +9 %).
 // Returns h.tri != kMiss (hit / occluded).
-template <bool kAnyHit, bool kCount, bool kPairs = false, bool kNearest = false>
+template <bool kAnyHit, bool kCount, bool kPairs = false, bool kNearest = false, bool kGA = true>
 PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, HitRec& h, uint32_t& nvisit,
                       uint32_t& ntest) {
     Ray8 R;
@@ -562,8 +620,8 @@ PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
         const bool more = trav8_node<kCount, kAnyHit, kNearest>(S, R, load_node8(S, node), node, sp, tos, h, tbase, tbits,
                                                                 nvisit);
         if (tbits) {
-            const bool done = kPairs ? trav8_tris2<kAnyHit, kCount>(S, R, tbase, tbits, h, ntest)
-                                     : trav8_tris<kAnyHit, kCount>(S, R, tbase, tbits, h, ntest);
+            const bool done = kPairs ? trav8_tris2<kAnyHit, kCount, kGA>(S, R, tbase, tbits, h, ntest)
+                                     : trav8_tris<kAnyHit, kCount, kGA>(S, R, tbase, tbits, h, ntest);
             if (done) return true;
         }
         if (!more) break;
@@ -849,7 +907,7 @@ struct VertexOut {
     bool nextIsDiffuse = false;
 };
 
-template <class Emit>
+template <bool kGroupedTaps = true, class Emit>
 PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emit, VertexOut& O) {
     const dxrpt_app_settings& set = A.P.set;
     const dxrpt_ray_trace_constants& rtc = A.P.rtc;
@@ -884,7 +942,7 @@ PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emi
         const f3 positionWS = surf.pos;
         f3 normalWS = surf.n;
         if (set.EnableNormalMaps) {
-            Texel4 nm = sample_tex_desc(A.S, tex_desc(mat.normal), surf.u, surf.v);
+            Texel4 nm = sample_tex_desc<kGroupedTaps>(A.S, tex_desc(mat.normal), surf.u, surf.v);
             f3 nts;
             nts.x = nm.r * 2.0f - 1.0f;
             nts.y = nm.g * 2.0f - 1.0f;
@@ -894,16 +952,16 @@ PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emi
         }
         f3 baseColor = f3{1.0f, 1.0f, 1.0f};
         if (set.EnableAlbedoMaps && !furnace) {
-            Texel4 a = sample_tex_desc(A.S, tex_desc(mat.albedo), surf.u, surf.v);
+            Texel4 a = sample_tex_desc<kGroupedTaps>(A.S, tex_desc(mat.albedo), surf.u, surf.v);
             baseColor = f3{a.r, a.g, a.b};
         }
-        const float metallic = saturate((furnace ? 1.0f : sample_tex_desc(A.S, tex_desc(mat.metallic), surf.u, surf.v).r) * set.MetallicScale);
+        const float metallic = saturate((furnace ? 1.0f : sample_tex_desc<kGroupedTaps>(A.S, tex_desc(mat.metallic), surf.u, surf.v).r) * set.MetallicScale);
         const bool enableDiffuse = (set.EnableDiffuse && metallic < 1.0f) || furnace;
         const bool payloadIsDiffuse = V.payloadIsDiffuse;
         const bool enableSpecular =
             set.EnableSpecular && (set.EnableIndirectSpecular ? !(set.AvoidCausticPaths && payloadIsDiffuse) : (depth == 1));
         if (!enableDiffuse && !enableSpecular) break;
-        const float sqrtRoughness = saturate((furnace ? 1.0f : sample_tex_desc(A.S, tex_desc(mat.roughness), surf.u, surf.v).r) * set.RoughnessScale);
+        const float sqrtRoughness = saturate((furnace ? 1.0f : sample_tex_desc<kGroupedTaps>(A.S, tex_desc(mat.roughness), surf.u, surf.v).r) * set.RoughnessScale);
         const float dsel = enableDiffuse ? 1.0f : 0.0f, ssel = enableSpecular ? 1.0f : 0.0f;
         const f3 diffuseAlbedo = scl(f3{lerpf(baseColor.x, 0.0f, metallic), lerpf(baseColor.y, 0.0f, metallic), lerpf(baseColor.z, 0.0f, metallic)}, dsel);
         const f3 specularAlbedo = scl(f3{lerpf(0.03f, baseColor.x, metallic), lerpf(0.03f, baseColor.y, metallic), lerpf(0.03f, baseColor.z, metallic)}, ssel);
@@ -916,7 +974,7 @@ PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emi
             msEC = f3{1.0f + specularAlbedo.x * k, 1.0f + specularAlbedo.y * k, 1.0f + specularAlbedo.z * k};
         }
         if (!furnace) {
-            Texel4 em = sample_tex_desc(A.S, tex_desc(mat.emissive), surf.u, surf.v);
+            Texel4 em = sample_tex_desc<kGroupedTaps>(A.S, tex_desc(mat.emissive), surf.u, surf.v);
             O.local = f3{em.r, em.g, em.b};
         }
         const bool directZero = (depth == 1 && !set.EnableDirect);  // RayTrace.hlsl:385-386
@@ -1303,7 +1361,7 @@ PT_DEV PhaseAcc phase_start() {
 // nearby origins -- take the wave-coherent traversal (all lanes active).  A lane whose slot 0 holds another
 // kind of ray (a spot light's, or at MaxPathLength 2 the sky visibility ray: random directions) traces it
 // per lane, after the packet.  cnt[2..3]: the census' any-hit node / triangle fetches.
-template <bool kCount, bool kNear = false>
+template <bool kCount, bool kNear = false, bool kGA = true>
 PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh, bool sun0, uint32_t packet, float4& rad,
                            uint32_t* cnt, PhaseAcc* pa = nullptr) {
     uint32_t unused[4] = {0u, 0u, 0u, 0u};
@@ -1324,7 +1382,7 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
             occluded = traverse8_packet<true, kCount, !kNear>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live && sun0, hs,
                                                       cnt + 2);
         if (live && !(pk && sun0))
-            occluded = traverse8<true, kCount, false, kNear>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, hs, cnt[2],
+            occluded = traverse8<true, kCount, false, kNear, kGA>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, hs, cnt[2],
                                                          cnt[3]);
         if (live) {
             rad.x += occluded ? c4.x * 0.0f : c4.x;
@@ -1347,7 +1405,7 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
 #ifndef DXRPT_CHAIN_SHADOWS
 #define DXRPT_CHAIN_SHADOWS 1
 #endif
-template <bool kCount>
+template <bool kCount, bool kGA = true>
 PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh, float4& rad, uint32_t* cnt,
                                    PhaseAcc* pa = nullptr) {
     uint32_t unused[4] = {0u, 0u, 0u, 0u};
@@ -1370,7 +1428,7 @@ PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh
         while (active) {
             uint32_t tbase = 0, tbits = 0;
             const bool more = trav8_node<kCount, true>(A.S, R, load_node8(A.S, node), node, sp, tos, h, tbase, tbits, cnt[2]);
-            const bool hit = tbits != 0u && trav8_tris<true, kCount>(A.S, R, tbase, tbits, h, cnt[3]);
+            const bool hit = tbits != 0u && trav8_tris<true, kCount, kGA>(A.S, R, tbase, tbits, h, cnt[3]);
             if (hit || !more) {
                 occ |= uint32_t(hit) << k;
                 if (++k < nsh) {  // the second ray: same origin, TMin, TMax
@@ -1437,7 +1495,8 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
         VertexOut O;
         uint32_t nsh = 0;
         bool sun0 = false;  // slot 0 holds the sun's shadow ray (the sun is emitted first when at all)
-        path_vertex(A, d, V, [&](int kind, f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
+        // material taps grouped where the budget has the registers (<= 5 waves/SIMD; k_path<7> +2.8 %, r05)
+        path_vertex<kNearest>(A, d, V, [&](int kind, f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
             sun0 |= kind == kShadowSun;
             emit_shadow(A, slot_p, nsh, o, dd, tmn, tmx, c, fo);
         }, O);
@@ -1754,7 +1813,7 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
     {
         const float4 o4 = Q.org[pos], d4 = Q.dir[pos];
         uint32_t nv = 0, nt = 0;
-        traverse8<false, kCount, true, true>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= set.MaxAnyHitPathLength, h, nv, nt);
+        traverse8<false, kCount, true, true, false>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= set.MaxAnyHitPathLength, h, nv, nt);
         if (kCount) {
             cnt[5] += nv;
             cnt[6] += nt;
@@ -1777,7 +1836,7 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
     V.hit = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
     VertexOut O;
     uint32_t nsh = 0;
-    path_vertex(A, d, V, [&](int, f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
+    path_vertex<false>(A, d, V, [&](int, f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
         emit_shadow(A, i, nsh, o, dd, tmn, tmx, c, fo);  // shadow slots by the dense index (< qsize)
     }, O);
     count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, nsh);
@@ -1796,9 +1855,9 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
     // lights, <= 2 rays per vertex); the other depths have at most the sun's and keep the slot loop, in
     // instantiations without the chained code (its registers cost the single-ray tails 2-3 %, r05)
     if (kLast && DXRPT_CHAIN_SHADOWS && A.P.rtc.NumLights == 0u)
-        vertex_shadows_chained<kCount>(A, i, nsh, rad, kCount ? cnt + 5 : nullptr, pa);
+        vertex_shadows_chained<kCount, false>(A, i, nsh, rad, kCount ? cnt + 5 : nullptr, pa);
     else
-        vertex_shadows<kCount, true>(A, d, i, nsh, false, 0u, rad, kCount ? cnt + 5 : nullptr, pa);
+        vertex_shadows<kCount, true, false>(A, d, i, nsh, false, 0u, rad, kCount ? cnt + 5 : nullptr, pa);
     split_finish(A, d, cont, qpos, nextDiffuse, accumIdx, rad);
     phase_mark(pa, 6);
 }
