@@ -31,7 +31,7 @@ struct BvhBuildParams {
     uint32_t binary_depth_cap = 0;  // BVH8: force this binary depth cap (0: tighten until the tree fits)
     uint32_t max_wide_depth = 0;    // BVH8: accepted wide depth (0: kTraversalStack8 - 1)
     bool spatial_splits = true;     // BVH8: SBVH spatial splits
-    double ref_budget = 1.5;        // BVH8: maximum triangle references / triangles with spatial splits
+    double ref_budget = 1.15;       // BVH8: maximum triangle references / triangles with spatial splits
                                     // (r04: 2.0 is C4 -11 % but the Sponza proxy's tree one level
                                     // deeper, metric +0.8 %, slowest 1/8 share +5 %;
                                     // profiles/r04_ab_split_budget.txt, r04_shares_budget200.txt)

@@ -311,7 +311,7 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                          fetches (slower; images identical) */
 #define DXRPT_OPT_KERNEL_TIMING 2u    /* 1: record hipEvents around the launches of dxrpt_render */
 #define DXRPT_OPT_SPATIAL_SPLITS 12u  /* BVH8 build: spatial-split reference budget in percent of the triangle count
-                                         (101..400; <= 100 disables spatial splits; default 150) */
+                                         (101..400; <= 100 disables spatial splits; default 115) */
 #define DXRPT_OPT_LEAF_COST 13u       /* BVH8 build: triangle-test cost in percent of a node visit (default 150) */
 #define DXRPT_OPT_PACKET_TRAVERSAL 18u /* BVH8 wave-coherent traversal (the 64 rays of a wave share one node
                                           sequence fetched with scalar loads) per pass, bit mask: 1 = closest

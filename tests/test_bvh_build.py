@@ -47,18 +47,19 @@ def test_tree_independent_of_thread_count(tool):
     assert all(r["ok"] for r in runs), runs
     assert len({r["hash"] for r in runs}) == 1, runs
     assert runs[0]["depth"] <= MAX_WIDE_DEPTH and runs[0]["treelet_passes"] == 1
-    assert runs[0]["refs"] <= 1.5 * runs[0]["ntris"] * 1.05  # the duplication budget (small overshoot per split)
+    assert runs[0]["refs"] <= 1.15 * runs[0]["ntris"] * 1.05  # the duplication budget (small overshoot per split)
 
 
 @pytest.mark.parametrize("n,ratio", [(100, 1.5), (200, 1.2)])
 def test_treelet_fallback_keeps_the_build(tool, tmp_path, n, ratio):
     # these sequences fit the stack without treelet passes but not with them at any binary depth cap: the
-    # build must succeed without them (r04 failed with "BVH8 deeper than the traversal stack")
+    # build must succeed without them (r04 failed with "BVH8 deeper than the traversal stack").  Pinned to
+    # the 150 % duplication budget they were found at (r05's default, 115 %, happens to fit them).
     f = tmp_path / "slivers.bin"
     sliver_sequence(n, ratio).tofile(f)
-    plain = check(tool, "file", f, 2, 0)
+    plain = check(tool, "file", f, 2, 0, 1.5)
     assert plain["ok"] and plain["depth"] <= MAX_WIDE_DEPTH, plain
-    got = check(tool, "file", f, 2, 1)
+    got = check(tool, "file", f, 2, 1, 1.5)
     assert got["ok"], got
     assert got["depth"] <= MAX_WIDE_DEPTH and got["treelet_passes"] == 0, got
     assert got["hash"] == plain["hash"]
