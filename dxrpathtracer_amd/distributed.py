@@ -55,6 +55,30 @@ def band_layout(width: int, height: int, world: int, band: int = BAND_ROWS) -> B
     return BandLayout(width, height, world, band, tiles, counts, max(counts))
 
 
+def balanced_band_layout(width: int, height: int, world: int, costs, band: int = BAND_ROWS) -> BandLayout:
+    """Bands dealt to the ranks by cost (longest-processing-time first): bands in decreasing `costs[b]`
+    (ties: lower band first), each to the rank with the least cost so far (ties: lower rank).  Every rank
+    renders its bands top to bottom.  Deterministic: every rank computes the same layout from the same
+    costs (e.g. per-band wave time of an earlier frame, scripts/band_balance.py)."""
+    nb = (height + band - 1) // band
+    if len(costs) != nb:
+        raise ValueError(f"balanced_band_layout: {len(costs)} costs for {nb} bands")
+    load = [0.0] * world
+    owner = [0] * nb
+    for b in sorted(range(nb), key=lambda b: (-float(costs[b]), b)):
+        r = min(range(world), key=lambda r: (load[r], r))
+        owner[b] = r
+        load[r] += float(costs[b])
+    tiles = [[] for _ in range(world)]
+    counts = [0] * world
+    for b in range(nb):
+        r, y0 = owner[b], b * band
+        h = min(band, height - y0)
+        tiles[r].append(A.Tile(0, y0, width, h, counts[r], width, 0))
+        counts[r] += width * h
+    return BandLayout(width, height, world, band, tiles, counts, max(counts))
+
+
 def _mix64(x: int) -> int:
     """splitmix64 finaliser: the partition's only source of pseudo-randomness (deterministic)."""
     x = (x + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
