@@ -9,8 +9,9 @@ A step is one frame (DispatchRays(1920,1080,1) equivalent, DXRPathTracer.cpp:202
 image.  With N ranks the image is split into 8-row bands, band b -> rank b % N (distributed.band_layout;
 --layout blocks: 8x8-pixel blocks dealt in a seeded random order) and every frame ends
 with an RCCL gather of the rank slabs to rank 0 plus the un-permute: total work per
-frame is fixed, so scaling is "strong".  The gather of frame f runs on a side stream while frame f+1
-renders (distributed.NativeGather); the last frame's gather is inside the timed region.  value = nominal
+frame is fixed, so scaling is "strong".  The gather of frame f runs on the render stream, which with
+overlapped frames carries only the blends, while frames f+1.. render on the library's slot streams
+(distributed.NativeGather); the last frame's gather is inside the timed region.  value = nominal
 Mrays/s of the whole job (W*H*(1+2(L-1)) rays per frame, the reference's HUD formula
 DXRPathTracer.cpp:2171) over the max-over-ranks time.  Rank 0 prints one JSON line; with N > 1 it carries
 every rank's render time, the gather's and un-permute's times and RCCL's rank count ("multi_gpu").
@@ -29,6 +30,12 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
+# Overlapped frames run on up to three internal streams of libdxrpt, which with the render stream fill the
+# HIP runtime's default four hardware queues per process; a multi-GPU rank adds RCCL's and
+# torch.distributed's streams.  Give those queues of their own rather than sharing one with a frame slot
+# (set before torch initialises HIP; INTEGRATION.md "Streams").
+if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 WIDTH, HEIGHT, PATH_LENGTH = 1920, 1080, 3
 SCENE = "sponza"
@@ -383,7 +390,7 @@ def main():
                  # frame f runs while frame f+1 renders; the last frame's is inside the timed region)
                  "gather_exposed_ms": round(ms_per_step - max(ranks_ms), 4),
                  "gather_what": "dxrpt_gather_slabs (grouped ncclSend/ncclRecv of every rank's slab to rank 0) "
-                                "timed with events on its side stream, dxrpt_unpermute on rank 0's render stream; "
+                                "timed with events on the render stream, dxrpt_unpermute on rank 0's render stream; "
                                 "per-rank render ms = median events around dxrpt_render on each rank's stream"}
 
     # ---- roofline of the dominant kernel, per launch (SURVEY.md 8(d) bytes / the launch's own duration)

@@ -113,7 +113,7 @@ DEFAULT_BAKE_CHUNK = 1 << 21
 DEFAULT_XCD_CHUNK = 8
 DEFAULT_WAVE_ORDER_PERIOD = 64
 DEFAULT_OPACITY_MICROMAP = 1
-DEFAULT_FRAME_OVERLAP = 1
+DEFAULT_FRAME_OVERLAP = 3
 DEFAULT_WAVE_ORDER = 2  # by frame size
 DEFAULT_MEGAKERNEL_SPLIT = 2  # by frame size
 DEFAULT_TAIL_OCCUPANCY = 0

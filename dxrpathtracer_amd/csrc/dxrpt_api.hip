@@ -75,8 +75,9 @@ struct DevBuf {
 // so the split pays from fewer vertices.
 constexpr uint64_t kSplitMinVertices = 8000000;
 constexpr uint64_t kSplitMinVerticesOverlap = 2000000;
-// DXRPT_OPT_FRAME_OVERLAP: two frames in flight, frame f on slot f % 2
-constexpr uint32_t kOverlapSlots = 2;
+// DXRPT_OPT_FRAME_OVERLAP: up to three frames in flight, frame f on slot f % (frames in flight)
+constexpr uint32_t kOverlapSlots = 3;
+constexpr uint32_t kOverlapBySize = 3;  // DXRPT_OPT_FRAME_OVERLAP value: frames in flight by frame size
 // BVH8 stack-spill slabs: 0 = work on the caller's stream, 1 + k = overlap slot k
 constexpr uint32_t kSpillSlabs = 1 + kOverlapSlots;
 constexpr uint32_t kTravCounters = 10;  // census: [0..4] depth-1 vertices, [5..9] deeper (dxrpt_stats)
@@ -131,7 +132,7 @@ struct dxrpt_ctx {
     uint32_t opt_bake_chunk = 1u << 21;     // DXRPT_OPT_BAKE_CHUNK (texels per bake launch)
     uint32_t opt_split = 2;                 // DXRPT_OPT_MEGAKERNEL_SPLIT (0 off, 1 on, 2 by frame size)
     uint32_t opt_omm = 1;                   // DXRPT_OPT_OPACITY_MICROMAP
-    uint32_t opt_overlap = 1;               // DXRPT_OPT_FRAME_OVERLAP
+    uint32_t opt_overlap = kOverlapBySize;  // DXRPT_OPT_FRAME_OVERLAP
     // overlapped frames: frame f runs on slot f % kOverlapSlots -- its own stream, path buffers, counters,
     // stage and BVH8 stack-spill slab -- and stages its radiance (d_stage); the caller's stream blends the
     // stage once the frame is done, so frame f+1's waves start while frame f drains
@@ -151,6 +152,7 @@ struct dxrpt_ctx {
     hipEvent_t ovl_gate = nullptr;  // the next overlapped frame waits for it (a rebuilt wave order)
     bool ovl_gate_set = false;
     uint32_t ovl_parity = 0;
+    uint32_t ovl_slots = 0;  // frames in flight of the current rotation (2 or 3)
     std::vector<const uint32_t*> stat_counters;  // counter set of the last frame
     uint32_t accum_extent = 0;  // 1 + the largest accumulation index of the current tile list (stage size)
     DevBuf d_omm;                           // kOmmWords per micromap slot (pt_layout.h kOmm*)
@@ -691,7 +693,8 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
             require(value <= 2, "dxrpt_set_option: megakernel split must be 0 (off), 1 (on) or 2 (by frame size)");
             ctx->opt_split = uint32_t(value);
         } else if (option == DXRPT_OPT_FRAME_OVERLAP) {
-            require(value <= 1, "dxrpt_set_option: frame overlap must be 0 (off) or 1 (two frames in flight)");
+            require(value <= kOverlapBySize,
+                    "dxrpt_set_option: frame overlap must be 0 (off), 1 (two frames in flight), 2 (three) or 3 (by frame size)");
             if (uint32_t(value) != ctx->opt_overlap) {  // the slot rotation restarts
                 drain_frames(ctx);
                 ctx->ovl_parity = 0;
@@ -1095,6 +1098,19 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // launched, filling this frame's drain.  Census and wave-clock frames run on the caller's stream.
         const bool overlap = ctx->opt_overlap && fp.megakernel && !ctx->opt_count && !ctx->opt_wave_clocks && paths > 0;
         ensure_spill(ctx, frame_traversal_threads(paths, slots, fp.megakernel != 0));
+        // frames in flight: three where the frame's waves leave the GPU idle for much of their span -- band
+        // shares (one round of waves: a 1/8 share 0.316 -> 0.244 ms) and the depth-split frames, whose tails
+        // drain several times per frame -- two for the large single-kernel frames (720p: 3 is +1 %)
+        // (profiles/r05_ab_overlap_depth.txt, r05_ab_overlap_cur.txt)
+        if (overlap) {
+            const uint32_t want = ctx->opt_overlap == kOverlapBySize ? (fp.split || paths <= 600000u ? 3u : 2u)
+                                                                     : ctx->opt_overlap + 1u;
+            if (want != ctx->ovl_slots) {  // the rotation restarts
+                drain_frames(ctx);
+                ctx->ovl_parity = 0;
+                ctx->ovl_slots = want;
+            }
+        }
         const uint32_t ov = ctx->ovl_parity;
         dxrpt_ctx::Slot& P = ctx->slot[ov];
         hipStream_t fs = s;  // the frame's stream
@@ -1246,7 +1262,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
             HIP_CHECK(launch_accum_stage(fp, s));
             HIP_CHECK(hipEventRecord(P.stage_free, s));
             P.stage_used = true;
-            ctx->ovl_parity = (ctx->ovl_parity + 1u) % kOverlapSlots;
+            ctx->ovl_parity = (ctx->ovl_parity + 1u) % ctx->ovl_slots;
             ctx->ovl_active = true;
         } else {
             // the next overlapped frame starts behind this one: it used slab 0 and, through the stream

@@ -224,11 +224,16 @@ class NativeGather:
     job's ranks made by dxrpt_comm_create (rank 0's unique id broadcast over torch.distributed, the only
     thing torch does here), grouped ncclSend / ncclRecv of every rank's slab into one contiguous buffer on
     rank 0 (dxrpt_gather_slabs) and the un-permute kernel into the W x H frame (dxrpt_unpermute) -- the
-    sequence a C++ host runs.  Pipelined like PipelinedGather: frame f's slab is
-    snapshotted on the render stream, gathered on a side stream while frame f+1 renders, and un-permuted
-    on the render stream once frame f+1 is submitted (or at flush())."""
+    sequence a C++ host runs.  Frame f's slab is snapshotted and gathered on the render
+    stream and un-permuted there once frame f+1 is submitted (or at flush()).  With overlapped frames (the
+    default) the render stream carries only the frames' blends: the frames themselves run on the
+    library's slot streams, which the gather does not block, so frame f+1.. render while frame f gathers.
+    side_stream=True gathers on a stream of its own instead (for one-frame-at-a-time rendering on the
+    render stream; r05: with overlapped frames the extra stream and its cross-stream waits cost the 1/8
+    share 0.244 -> 0.27-0.35 ms, profiles/r05_ab_overlap_side.txt, r05_ab_overlap_hwq.txt)."""
 
-    def __init__(self, layout: BandLayout, rank: int, device: int, full=None, group=None, timing: bool = False):
+    def __init__(self, layout: BandLayout, rank: int, device: int, full=None, group=None, timing: bool = False,
+                 side_stream: bool = False):
         import ctypes as C
         import torch
         import torch.distributed as dist
@@ -277,7 +282,7 @@ class NativeGather:
         self.tiles = gathered_tiles(layout)
         self.tarr = (A.Tile * len(self.tiles))(*self.tiles)
         self.total = sum(layout.counts)
-        self.side = torch.cuda.Stream()
+        self.side = torch.cuda.Stream() if side_stream else None
         self.staging = None
         self.recv = None
         self.pending = None
@@ -307,17 +312,19 @@ class NativeGather:
         k = self.count % 2
         self.count += 1
         self.staging[k].copy_(local[:n])
-        self.side.wait_stream(cur)
+        gs = self.side if self.side is not None else cur
+        if self.side is not None:
+            self.side.wait_stream(cur)
         if self.timing:
             g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            g0.record(self.side)
+            g0.record(gs)
         self._check(self.L.dxrpt_gather_slabs(self.comm, C.c_void_p(self.staging[k].data_ptr()), self.counts,
                                               C.c_void_p(self.recv[k].data_ptr()) if self.rank == 0 else None,
-                                              C.c_void_p(self.side.cuda_stream)), "dxrpt_gather_slabs")
+                                              C.c_void_p(gs.cuda_stream)), "dxrpt_gather_slabs")
         ev = torch.cuda.Event()
-        ev.record(self.side)
+        ev.record(gs)
         if self.timing:
-            g1.record(self.side)
+            g1.record(gs)
             self.gather_ev.append((g0, g1))
         prev, self.pending = self.pending, (ev, k)
         if prev is not None:

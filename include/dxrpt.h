@@ -370,14 +370,19 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                           "every tap here rejects" or "tap"), and skip the opacity tap of
                                           AnyHitShader (RayTrace.hlsl:485-507) where the cell decides it.
                                           0: always tap.  Identical results. */
-#define DXRPT_OPT_FRAME_OVERLAP 37u    /* 1 (default): consecutive megakernel frames alternate between two
-                                          internal streams with their own path buffers and stage their
-                                          radiance; the caller's stream blends a frame's stage
-                                          (RaygenShader's progressive rule, RayTrace.hlsl:140-148) once it is
-                                          done, so the next frame's waves fill the previous frame's drain.
-                                          dxrpt_render still returns with every launch enqueued, and the
-                                          target is complete when the caller's stream reaches that point
-                                          (see "Stream ordering" above).  0: one frame at a time on the
+#define DXRPT_OPT_FRAME_OVERLAP 37u    /* 3 (default): by frame size -- three frames in flight for
+                                          depth-split frames and frames of at most 600k paths (a GPU's band
+                                          share), two for larger single-kernel frames; 1: two, 2: three.
+                                          Consecutive megakernel frames rotate over internal streams with
+                                          their own path buffers and stage their radiance; the caller's
+                                          stream blends a frame's stage (RaygenShader's progressive rule,
+                                          RayTrace.hlsl:140-148) once it is done, so the next frames' waves
+                                          fill the previous frame's drain.  dxrpt_render still returns with
+                                          every launch enqueued, and the target is complete when the
+                                          caller's stream reaches that point (see "Stream ordering" above).
+                                          The streams want hardware queues of their own: a host with more
+                                          busy streams than GPU_MAX_HW_QUEUES (4 by default) minus three
+                                          should raise it.  0: one frame at a time on the
                                           caller's stream.  Identical results. */
 #define DXRPT_OPT_TREELET_PASSES 40u /* BVH8 build: passes of treelet restructuring (Karras & Aila 2013:
                                         every 7-leaf treelet of the binary SBVH re-wired to its SAH-optimal

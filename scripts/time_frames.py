@@ -35,6 +35,11 @@ def main():
     ap.add_argument("--opt", action="append", default=[],
                     help="NAME=VALUE: dxrpt_set_option(DXRPT_OPT_NAME, VALUE), e.g. FRAME_OVERLAP=0, TAIL_OCCUPANCY=6")
     ap.add_argument("--kernels", action="store_true", help="also print per-launch kernel timings (head / tail / path)")
+    ap.add_argument("--side-stream", action="store_true",
+                    help="mimic NativeGather's streams: per frame a slab copy on a side stream after the render, "
+                         "waited for by the render stream one frame later")
+    ap.add_argument("--cur-copy", action="store_true",
+                    help="per frame a slab snapshot copy on the render stream (a gather on the caller's stream)")
     ap.add_argument("--phases", action="store_true",
                     help="print the per-phase lane-time split of the timed frames (kernel builds with -DDXRPT_DIAG_PHASES=1)")
     args = ap.parse_args()
@@ -78,17 +83,40 @@ def main():
     if args.kernels:
         t.set_option(A.OPT_KERNEL_TIMING, 1)
         t.reset_timing()
+    side = torch.cuda.Stream() if args.side_stream else None
+    snap = torch.empty_like(acc) if side is not None else None
+    pend = None
+
+    cur_snap = torch.empty_like(acc) if args.cur_copy else None
+
+    def frame_end():
+        nonlocal pend
+        if cur_snap is not None:
+            cur_snap.copy_(acc)
+        if side is None:
+            return
+        side.wait_stream(stream)
+        with torch.cuda.stream(side):
+            snap.copy_(acc)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        if pend is not None:
+            stream.wait_event(pend)
+        pend = ev
+
     rounds = []
     for r in range(args.rounds):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
         for f in range(args.frames):
             t.render_raw(consts[f % 16], st, acc.data_ptr(), W, H, tiles=tiles, stream=stream.cuda_stream, lights=lights)
+            frame_end()
         b.record(stream)
         torch.cuda.synchronize()
         rounds.append(a.elapsed_time(b) / args.frames)
     s = t.stats()
     desc = " ".join(args.opt) + (f" L={L}" if args.max_path is not None else "")
+    desc += (" side-stream" if args.side_stream else "") + (" cur-copy" if args.cur_copy else "")
     where = f"share 1/{args.share} r{args.rank} {args.layout}" if args.share > 1 else ("tile " + args.tile if args.tile else "full")
     print(f"{args.label:24s} {args.config} {desc} {where}: median {statistics.median(rounds):.4f} "
           f"mean {statistics.mean(rounds):.4f} min {min(rounds):.4f} ms/frame  rays {s.radiance_rays + s.shadow_rays} "

@@ -225,7 +225,7 @@ def test_retired_options_are_rejected(torch_cuda):
         assert A.lib().dxrpt_set_option(t._ctx, opt, 1) == A.DXRPT_E_INVALID_ARG, opt
         assert b"unknown option" in A.lib().dxrpt_last_error(t._ctx)
     with pytest.raises(Exception, match="frame overlap"):
-        t.set_option(A.OPT_FRAME_OVERLAP, 2)
+        t.set_option(A.OPT_FRAME_OVERLAP, 4)
     with pytest.raises(Exception, match="occupancy"):
         t.set_option(A.OPT_MEGAKERNEL_OCCUPANCY, 8)
 

@@ -112,7 +112,8 @@ def test_metric_1080p_L3_consecutive_frames(torch_cuda, name):
 
 @pytest.mark.parametrize("world,rank,lanes,ordered,overlap", [(8, 5, 64, True, 1), (8, 0, 64, True, 1),
                                                               (2, 1, 64, False, 1), (8, 5, 64, True, 0),
-                                                              (4, 1, 64, False, 1)])
+                                                              (4, 1, 64, False, 1), (8, 2, 64, True, 3),
+                                                              (4, 1, 64, False, 3), (2, 0, 64, False, 3)])
 def test_metric_band_share_consecutive_frames(torch_cuda, world, rank, lanes, ordered, overlap):
     # one GPU's share of the metric frame (bench.py --gpus N): 1/8 = 259,200 paths (4,050 waves, one round
     # at 4 waves/SIMD: cost-ordered from its second frame), 1/4 = 518,400 (1.6 rounds at 5 waves/SIMD with
@@ -158,7 +159,7 @@ def test_c3_1080p_L8_sixteen_samples(torch_cuda):
                                                 (1920, 1080, 8, 5, (2, 1))])
 def test_overlapped_frames_are_bit_identical(torch_cuda, W, H, L, frames, share):
     # DXRPT_OPT_FRAME_OVERLAP: back-to-back frames (no host sync between them, as bench.py and every rank
-    # render them) alternate between two sets of internal streams and stage their radiance; the caller's
+    # render them) rotate over two or three sets of internal streams and stage their radiance; the caller's
     # stream blends each stage in frame order (RayTrace.hlsl:140-148).  >= 17 frames cross a cost-order
     # rebuild (every 16th frame records, the next frame waits for the new order); 1080p L=3 and L=8 and
     # 4K L=6 run the depth-split schedule overlapped against k_path / the split one frame at a time.  The
@@ -174,7 +175,7 @@ def test_overlapped_frames_are_bit_identical(torch_cuda, W, H, L, frames, share)
     consts = [D.make_constants(sc, st, sky, W, H, f % 16) for f in range(frames)]
     stream = torch.cuda.current_stream().cuda_stream
     out = []
-    for overlap in (0, 1):  # one frame at a time, two frames in flight
+    for overlap in (0, 1, 2, 3):  # one frame at a time, two / three frames in flight, by frame size (default)
         t = _fresh("sponza")
         try:
             t.set_option(A.OPT_FRAME_OVERLAP, overlap)
@@ -187,7 +188,8 @@ def test_overlapped_frames_are_bit_identical(torch_cuda, W, H, L, frames, share)
             out.append(acc.cpu().numpy())
         finally:
             t.close()
-    np.testing.assert_array_equal(out[1], out[0])
+    for o in out[1:]:
+        np.testing.assert_array_equal(o, out[0])
 
 
 def _frames(torch, W, H, L, frames, overlap, streams=None, between=None, name="sponza", lights_of=None):
@@ -217,8 +219,9 @@ def _frames(torch, W, H, L, frames, overlap, streams=None, between=None, name="s
         t.close()
 
 
-@pytest.mark.parametrize("W,H,L", [(1280, 720, 3), (1920, 1080, 3), (320, 180, 5)])
-def test_overlapped_frames_on_alternating_streams(torch_cuda, W, H, L):
+@pytest.mark.parametrize("W,H,L,overlap", [(1280, 720, 3, 1), (1920, 1080, 3, 1), (320, 180, 5, 1), (1920, 1080, 3, 3),
+                                           (320, 180, 5, 2)])
+def test_overlapped_frames_on_alternating_streams(torch_cuda, W, H, L, overlap):
     # include/dxrpt.h "Stream ordering": a caller that submits consecutive frames on two streams (a ring of
     # command queues) still gets the frames in submission order -- each call on a new stream first waits
     # for the previous stream -- so the progressive blend (order dependent) equals the one-stream,
@@ -226,7 +229,7 @@ def test_overlapped_frames_on_alternating_streams(torch_cuda, W, H, L):
     torch = torch_cuda
     ref, _ = _frames(torch, W, H, L, 8, 0)
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-    got, s = _frames(torch, W, H, L, 8, 1, streams=streams)
+    got, s = _frames(torch, W, H, L, 8, overlap, streams=streams)
     assert s.schedule & A.SCHED_OVERLAP, s.schedule
     np.testing.assert_array_equal(got, ref)
     got0, _ = _frames(torch, W, H, L, 8, 0, streams=streams)
