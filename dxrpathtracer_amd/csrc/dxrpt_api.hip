@@ -71,10 +71,13 @@ struct DevBuf {
 };
 
 // Depth-split schedule by frame size (DXRPT_OPT_MEGAKERNEL_SPLIT 2): frames of at least this many path
-// vertices (paths x (L - 1)); with overlapped frames the next frame fills the per-depth kernels' drains,
-// so the split pays from fewer vertices.
+// vertices (paths x (L - 1)); with overlapped frames the next frames fill the per-depth kernels' drains,
+// so the split pays from fewer vertices -- the more frames in flight, the fewer (r05 with
+// three in flight: 720p L=3, 1.84M vertices, 0.770 -> 0.699 ms split; the 1/4 share, 1.04M, +5 %:
+// profiles/r05_ab_share_knobs.txt).
 constexpr uint64_t kSplitMinVertices = 8000000;
-constexpr uint64_t kSplitMinVerticesOverlap = 2000000;
+constexpr uint64_t kSplitMinVerticesOverlap2 = 2000000;  // two frames in flight
+constexpr uint64_t kSplitMinVerticesOverlap3 = 1500000;  // three
 // DXRPT_OPT_FRAME_OVERLAP: up to three frames in flight, frame f on slot f % (frames in flight)
 constexpr uint32_t kOverlapSlots = 3;
 constexpr uint32_t kOverlapBySize = 3;  // DXRPT_OPT_FRAME_OVERLAP value: frames in flight by frame size
@@ -1085,7 +1088,9 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // of its time -- unless overlapped frames fill the drains (r03: from 2M vertices, the metric's 1/2
         // share 0.961 -> 0.939 ms; 720p, C3's 1/8 share and the 1/4 share stay k_path, +1.4 / +2.2 / +10.6 %
         // split; profiles/r03_ab_msplit*.txt, r03_ab_split_small.txt)
-        const bool split_by_size = vertices >= (ctx->opt_overlap ? kSplitMinVerticesOverlap : kSplitMinVertices);
+        const uint64_t split_min = !ctx->opt_overlap ? kSplitMinVertices
+                                 : ctx->opt_overlap == 1u ? kSplitMinVerticesOverlap2 : kSplitMinVerticesOverlap3;
+        const bool split_by_size = vertices >= split_min;
         fp.split = fp.megakernel && (ctx->opt_split == 1u || (ctx->opt_split == 2u && split_by_size)) ? 1u : 0u;
         // split budgets: the head 5 waves/SIMD (96 VGPRs, no spills; r03: metric -0.2 %, C3 -0.4 %, C5's share
         // -1.0 %, C4 +0.5 % against 7), the tails 7 (72 VGPRs; 6: -2-3 %)

@@ -85,7 +85,7 @@ def _steady_frames(torch, name, W, H, L, frames, crops, tiles=None, n_out=None, 
 def _expect(lanes, ordered, overlap=True, split=False):
     def check(f, s):
         assert s.schedule & A.SCHED_MEGAKERNEL and not s.schedule & A.SCHED_CENSUS, s.schedule
-        # from 2M path vertices (overlapped frames) the depth-split schedule, one part
+        # from 1.5M path vertices (three frames in flight; 2M with two) the depth-split schedule, one part
         assert bool(s.schedule & A.SCHED_SPLIT) == split, f"frame {f}: schedule {s.schedule}"
         assert bool(s.schedule & A.SCHED_OVERLAP) == overlap, f"frame {f}: schedule {s.schedule}"
         assert bool(s.schedule & A.SCHED_ORDER_KERNEL) == ordered, \
@@ -97,9 +97,10 @@ def _expect(lanes, ordered, overlap=True, split=False):
 
 
 def test_c2_720p_L3_consecutive_frames(torch_cuda):
-    # BASELINE.json configs[1]: 14,400 waves, 2 rounds of resident waves -> path-ordered k_path, overlapped
+    # BASELINE.json configs[1]: 921,600 paths x 2 vertices (>= 1.5M with three frames in flight, r05) -> the
+    # depth-split schedule, overlapped
     W, H = 1280, 720
-    _steady_frames(torch_cuda, "sponza", W, H, 3, 3, _frame_crops(W, H), expect=_expect(64, False))
+    _steady_frames(torch_cuda, "sponza", W, H, 3, 3, _frame_crops(W, H), expect=_expect(64, False, split=True))
 
 
 @pytest.mark.parametrize("name", ["sponza", "suntemple"])
