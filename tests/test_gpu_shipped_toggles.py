@@ -3,11 +3,11 @@
 tests/test_gpu_parity.py::test_settings_toggles checks the 16 override sets on the wavefront passes only.
 The schedules that ship carry payload state the wavefront keeps in its queues too, but through other code:
   * k_path<7> / k_path<5>: one lane per path, payload Roughness / IsDiffuse in registers across depths
-    (C2 720p, the 1/4 band share);
+    (the 1/4 band share);
   * k_path<4, kOrder>: the cost-ordered instantiation (a GPU's 1/8 band share), frames 1+ in cost order;
-  * k_path_head<5> + k_path_tail<7>: the depth-split schedule (the metric, C3, C4, C5), payload Roughness in
-    the queue's thr.w and IsDiffuse in rad.w (pt_kernels.hip split_push / split_finish / tail_path), frames
-    overlapped.
+  * k_path_head<5 or 6> + k_path_tail<7>: the depth-split schedule (the metric, C2, C3, C4, C5; head 6 above
+    1.5M paths), payload Roughness in the queue's thr.w and IsDiffuse in rad.w (pt_kernels.hip split_push /
+    split_finish / tail_path), frames overlapped.
 RayTrace.hlsl reads the payload at :191-192 (AvoidCausticPaths: IsDiffuse) and :203-204 (ClampRoughness:
 Roughness) and passes it on at :378-440.  Every schedule renders the same settings at 640x360 (L = 4: three
 path vertices, so the payload crosses two queue hand-offs), its crops are compared with the oracle (gate
@@ -55,6 +55,9 @@ SCHEDULES = {
                          (A.SCHED_MEGAKERNEL | A.SCHED_OVERLAP | A.SCHED_ORDER_KERNEL, A.SCHED_SPLIT, 4, 0), True),
     "head<5>+tail<7>": ({A.OPT_MEGAKERNEL_SPLIT: 1},
                         (A.SCHED_MEGAKERNEL | A.SCHED_OVERLAP | A.SCHED_SPLIT, A.SCHED_ORDER_KERNEL, 5, 7), False),
+    # the full 1080p frames' budgets with three frames in flight (r05: head 6 above 1.5M paths)
+    "head<6>+tail<7>": ({A.OPT_MEGAKERNEL_SPLIT: 1, A.OPT_MEGAKERNEL_OCCUPANCY: 6, A.OPT_TAIL_OCCUPANCY: 7},
+                        (A.SCHED_MEGAKERNEL | A.SCHED_OVERLAP | A.SCHED_SPLIT, A.SCHED_ORDER_KERNEL, 6, 7), False),
 }
 
 _TRACERS = {}
