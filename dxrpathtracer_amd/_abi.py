@@ -100,6 +100,7 @@ OPT_OPACITY_MICROMAP = 36
 OPT_FRAME_OVERLAP = 37
 OPT_TREELET_PASSES = 40
 OPT_BVH_THREADS = 41
+OPT_PACKED_TAPS = 42
 # include/dxrpt.h DXRPT_RETIRED_OPTIONS (tests/test_abi.py checks the two lists agree)
 RETIRED_OPTIONS = (3, 4, 5, 6, 7, 8, 9, 10, 11, 14, 15, 16, 17, 19, 21, 22, 26, 27, 30, 35, 38, 39)
 DXRPT_E_INVALID_ARG, DXRPT_E_HIP, DXRPT_E_NO_DEVICE, DXRPT_E_STATE, DXRPT_E_OOM = -1, -2, -3, -4, -5
@@ -113,6 +114,7 @@ DEFAULT_BAKE_CHUNK = 1 << 21
 DEFAULT_XCD_CHUNK = 8
 DEFAULT_WAVE_ORDER_PERIOD = 64
 DEFAULT_OPACITY_MICROMAP = 1
+DEFAULT_PACKED_TAPS = 1
 DEFAULT_FRAME_OVERLAP = 3
 DEFAULT_WAVE_ORDER = 2  # by frame size
 DEFAULT_MEGAKERNEL_SPLIT = 2  # by frame size
@@ -132,7 +134,7 @@ class Stats(C.Structure):
                 ("kernel_ms", C.c_double * K_COUNT), ("kernel_launches", C.c_uint64 * K_COUNT),
                 ("timed_frames", C.c_uint64), ("frame_ms", C.c_double), ("schedule", u32), ("paths_per_wave", u32),
                 ("occupancy", u32), ("tail_occupancy", u32), ("radiance_hits", C.c_uint64),
-                ("census_depth1", C.c_uint64 * 5)]
+                ("census_depth1", C.c_uint64 * 5), ("packed_materials", C.c_uint32), ("packed_textures", C.c_uint32)]
 
 
 # dxrpt_stats.schedule bits

@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <map>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -135,6 +137,9 @@ struct dxrpt_ctx {
     uint32_t opt_bake_chunk = 1u << 21;     // DXRPT_OPT_BAKE_CHUNK (texels per bake launch)
     uint32_t opt_split = 2;                 // DXRPT_OPT_MEGAKERNEL_SPLIT (0 off, 1 on, 2 by frame size)
     uint32_t opt_omm = 1;                   // DXRPT_OPT_OPACITY_MICROMAP
+    uint32_t opt_packed = 1;                // DXRPT_OPT_PACKED_TAPS
+    std::vector<uint32_t> texels_packed;    // packed normal/metallic/roughness textures, after `texels` on the device
+    uint32_t packed_materials = 0, packed_textures = 0;  // of the current shading records (dxrpt_stats)
     uint32_t opt_overlap = kOverlapBySize;  // DXRPT_OPT_FRAME_OVERLAP
     // overlapped frames: frame f runs on slot f % kOverlapSlots -- its own stream, path buffers, counters,
     // stage and BVH8 stack-spill slab -- and stages its radiance (d_stage); the caller's stream blends the
@@ -373,12 +378,83 @@ void build_omm(dxrpt_ctx* c) {
     c->omm_dirty = false;
 }
 
+// DXRPT_OPT_PACKED_TAPS: one RGBA8 unorm texture (normal.r, normal.g, metallic, roughness) per distinct
+// (normal, metallic, roughness) triple of the geometries' materials that qualifies -- normal RGBA8 unorm,
+// metallic and roughness R8 or RGBA8 unorm (their .r is what the shading reads), each either W x H or
+// 1 x 1 -- in the tiled layout, appended to the device pool after `texels`.  A 1 x 1 map is a constant:
+// its bilinear tap is lerp(c, c, f) = c for any finite weight, and a NaN / Inf weight (a NaN / Inf UV)
+// is NaN at either size, so spreading it over W x H gives the same value.  Returns material index ->
+// packed reference (whf with format kTexFmtPackedNMR), {0, 0} where the material keeps three taps.
+std::vector<GeoTex> build_packed(dxrpt_ctx* c) {
+    std::vector<GeoTex> out(c->mats.size(), GeoTex{0u, 0u});
+    c->texels_packed.clear();
+    c->packed_materials = c->packed_textures = 0;
+    if (!c->opt_packed) return out;
+    std::map<std::array<uint32_t, 3>, GeoTex> made;
+    std::vector<bool> used(c->mats.size(), false);
+    for (const dxrpt_geometry_info& g : c->geos)
+        if (g.MaterialIdx < c->mats.size()) used[g.MaterialIdx] = true;
+    const size_t nt = c->texdesc.size();
+    auto unorm_r = [](const TexDesc& d) { return d.fmt == DXRPT_TEX_R8_UNORM || d.fmt == DXRPT_TEX_RGBA8_UNORM; };
+    for (size_t mi = 0; mi < c->mats.size(); ++mi) {
+        if (!used[mi]) continue;
+        const dxrpt_material& m = c->mats[mi];
+        if (m.Normal >= nt || m.Metallic >= nt || m.Roughness >= nt) continue;
+        const TexDesc &N = c->texdesc[m.Normal], &M = c->texdesc[m.Metallic], &R = c->texdesc[m.Roughness];
+        if (N.fmt != DXRPT_TEX_RGBA8_UNORM || !unorm_r(M) || !unorm_r(R)) continue;
+        const uint32_t w = std::max({N.width, M.width, R.width}), h = std::max({N.height, M.height, R.height});
+        auto fits = [&](const TexDesc& d) { return (d.width == w && d.height == h) || (d.width == 1 && d.height == 1); };
+        if (!fits(N) || !fits(M) || !fits(R)) continue;
+        const std::array<uint32_t, 3> key{m.Normal, m.Metallic, m.Roughness};
+        auto it = made.find(key);
+        if (it == made.end()) {
+            const uint32_t tx32 = (w + kTexTileW32 - 1) / kTexTileW32, ty32 = (h + kTexTileH32 - 1) / kTexTileH32;
+            const size_t at = c->texels_packed.size();
+            const size_t base = c->texels.size() + at;
+            require(base + size_t(tx32) * ty32 * kTexTileWords < (size_t(1) << 32),
+                    "packed textures: texel pool exceeds 2^32 words");
+            c->texels_packed.resize(at + size_t(tx32) * ty32 * kTexTileWords, 0u);
+            // texel (x, y) of map d (its own tiling; a 1 x 1 map's only texel)
+            auto word_of = [&](const TexDesc& d, uint32_t x, uint32_t y) {
+                if (d.width == 1 && d.height == 1) x = y = 0;
+                const uint32_t* T = c->texels.data() + d.offset;
+                if (d.fmt == DXRPT_TEX_R8_UNORM) {
+                    const uint32_t t8 = (d.width + kTexTileW8 - 1) / kTexTileW8;
+                    return (T[tex_tile_word(x, y, t8, true)] >> (8u * (x & 3u))) & 0xFFu;
+                }
+                return T[tex_tile_word(x, y, (d.width + kTexTileW32 - 1) / kTexTileW32, false)];
+            };
+            uint32_t* dst = c->texels_packed.data() + at;
+            for (uint32_t y = 0; y < h; ++y)
+                for (uint32_t x = 0; x < w; ++x)
+                    dst[tex_tile_word(x, y, tx32, false)] =
+                        (word_of(N, x, y) & 0xFFFFu) | ((word_of(M, x, y) & 0xFFu) << 16) | ((word_of(R, x, y) & 0xFFu) << 24);
+            it = made.emplace(key, GeoTex{uint32_t(base), w | (h << 15) | (kTexFmtPackedNMR << 30)}).first;
+        }
+        out[mi] = it->second;
+        ++c->packed_materials;
+    }
+    c->packed_textures = uint32_t(made.size());
+    return out;
+}
+
 void upload_textures(dxrpt_ctx* c) {
-    if ((c->omm_dirty && c->opt_omm && c->bvh_built) || c->tex_dirty || (c->geoshade_dirty && !c->geos.empty()))
-        drain_frames(c);
+    const bool shade = c->geoshade_dirty && !c->geos.empty();
+    if ((c->omm_dirty && c->opt_omm && c->bvh_built) || c->tex_dirty || shade) drain_frames(c);
     if (c->omm_dirty && c->opt_omm && c->bvh_built) build_omm(c);
-    if (c->tex_dirty) {
-        c->d_texels.upload(c->texels.data(), c->texels.size() * sizeof(uint32_t));
+    std::vector<GeoTex> packed;
+    if (c->tex_dirty || shade) {
+        // the texel pool: the added textures, then the packed ones of the current materials
+        if (!c->geos.empty()) {
+            packed = build_packed(c);
+        } else {
+            c->texels_packed.clear();
+            c->packed_materials = c->packed_textures = 0;
+        }
+        const size_t n0 = c->texels.size() * sizeof(uint32_t), n1 = c->texels_packed.size() * sizeof(uint32_t);
+        c->d_texels.ensure(n0 + n1);
+        if (n0) HIP_CHECK(hipMemcpy(c->d_texels.p, c->texels.data(), n0, hipMemcpyHostToDevice));
+        if (n1) HIP_CHECK(hipMemcpy(static_cast<char*>(c->d_texels.p) + n0, c->texels_packed.data(), n1, hipMemcpyHostToDevice));
         c->tex_dirty = false;
         c->geoshade_dirty = true;
     }
@@ -398,8 +474,10 @@ void upload_textures(dxrpt_ctx* c) {
     };
     std::vector<GeoShade> gs(c->geos.size());
     for (size_t g = 0; g < c->geos.size(); ++g) {
-        const dxrpt_material& m = c->mats[c->geos[g].MaterialIdx];
+        const uint32_t mi = c->geos[g].MaterialIdx;
+        const dxrpt_material& m = c->mats[mi];
         gs[g] = GeoShade{ref(m.Albedo), ref(m.Normal), ref(m.Roughness), ref(m.Metallic), ref(m.Emissive), ref(m.Opacity)};
+        if (mi < packed.size() && packed[mi].whf) gs[g].normal = packed[mi];  // (normal.rg, metallic, roughness)
     }
     c->d_geoshade.upload(gs.data(), gs.size() * sizeof(GeoShade));
     c->geoshade_dirty = false;
@@ -710,6 +788,14 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
             require(value <= 1, "dxrpt_set_option: opacity micromap must be 0 (off) or 1 (on)");
             drain_frames(ctx);  // in-flight frames may read the micromap
             ctx->opt_omm = uint32_t(value);
+        } else if (option == DXRPT_OPT_PACKED_TAPS) {
+            require(value <= 1, "dxrpt_set_option: packed taps must be 0 (off) or 1 (on)");
+            if (uint32_t(value) != ctx->opt_packed) {  // the shading records (and the packed texels) change
+                drain_frames(ctx);
+                ctx->opt_packed = uint32_t(value);
+                ctx->tex_dirty = true;
+                ctx->geoshade_dirty = true;
+            }
         } else if (option == DXRPT_OPT_BVH_THREADS) {
             require(value <= 256, "dxrpt_set_option: BVH build threads must be 0 (default) or 1..256");
             ctx->build_params.threads = unsigned(value);
@@ -1304,6 +1390,8 @@ int dxrpt_get_stats(dxrpt_ctx* ctx, dxrpt_stats* out) {
                 for (uint32_t k = 0; k < kQueueShards; ++k) cnt[q] += shards[q * kQueueShards + k];
         }
         dxrpt_stats s = ctx->last;
+        s.packed_materials = ctx->packed_materials;
+        s.packed_textures = ctx->packed_textures;
         for (int d = 1; d < ctx->last_L && d < int(DXRPT_MAX_PATH_LENGTH); ++d) {
             s.radiance_rays_per_depth[d] = cnt[d];
             s.shadow_rays_per_depth[d] = cnt[16 + d];

@@ -941,27 +941,41 @@ PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emi
         f3 Nrow = surf.n;
         const f3 positionWS = surf.pos;
         f3 normalWS = surf.n;
-        if (set.EnableNormalMaps) {
-            Texel4 nm = sample_tex_desc<kGroupedTaps>(A.S, tex_desc(mat.normal), surf.u, surf.v);
-            f3 nts;
-            nts.x = nm.r * 2.0f - 1.0f;
-            nts.y = nm.g * 2.0f - 1.0f;
-            nts.z = sqrtf(1.0f - saturate(nts.x * nts.x + nts.y * nts.y));
-            normalWS = normalize3(add(add(scl(T, nts.x), scl(Bt, nts.y)), scl(surf.n, nts.z)));
-            Nrow = normalWS;
+        // packed material (DXRPT_OPT_PACKED_TAPS, pt_layout.h kTexFmtPackedNMR): the normal map's tap also
+        // carries metallic (.b) and roughness (.a) -- one bilinear tap for the three.  texMetal / texRough
+        // hold the maps' values (furnace: 1, no tap), so both forms leave the same two floats live.
+        const TexDesc ntd = tex_desc(mat.normal);
+        const bool packedNMR = ntd.fmt == kTexFmtPackedNMR;
+        float texMetal = 1.0f, texRough = 1.0f;
+        if (set.EnableNormalMaps || (packedNMR && !furnace)) {
+            const Texel4 nm = sample_tex_desc<kGroupedTaps>(A.S, ntd, surf.u, surf.v);
+            if (packedNMR && !furnace) {
+                texMetal = nm.b;
+                texRough = nm.a;
+            }
+            if (set.EnableNormalMaps) {
+                f3 nts;
+                nts.x = nm.r * 2.0f - 1.0f;
+                nts.y = nm.g * 2.0f - 1.0f;
+                nts.z = sqrtf(1.0f - saturate(nts.x * nts.x + nts.y * nts.y));
+                normalWS = normalize3(add(add(scl(T, nts.x), scl(Bt, nts.y)), scl(surf.n, nts.z)));
+                Nrow = normalWS;
+            }
         }
         f3 baseColor = f3{1.0f, 1.0f, 1.0f};
         if (set.EnableAlbedoMaps && !furnace) {
             Texel4 a = sample_tex_desc<kGroupedTaps>(A.S, tex_desc(mat.albedo), surf.u, surf.v);
             baseColor = f3{a.r, a.g, a.b};
         }
-        const float metallic = saturate((furnace ? 1.0f : sample_tex_desc<kGroupedTaps>(A.S, tex_desc(mat.metallic), surf.u, surf.v).r) * set.MetallicScale);
+        if (!furnace && !packedNMR) texMetal = sample_tex_desc<kGroupedTaps>(A.S, tex_desc(mat.metallic), surf.u, surf.v).r;
+        const float metallic = saturate(texMetal * set.MetallicScale);
         const bool enableDiffuse = (set.EnableDiffuse && metallic < 1.0f) || furnace;
         const bool payloadIsDiffuse = V.payloadIsDiffuse;
         const bool enableSpecular =
             set.EnableSpecular && (set.EnableIndirectSpecular ? !(set.AvoidCausticPaths && payloadIsDiffuse) : (depth == 1));
         if (!enableDiffuse && !enableSpecular) break;
-        const float sqrtRoughness = saturate((furnace ? 1.0f : sample_tex_desc<kGroupedTaps>(A.S, tex_desc(mat.roughness), surf.u, surf.v).r) * set.RoughnessScale);
+        if (!furnace && !packedNMR) texRough = sample_tex_desc<kGroupedTaps>(A.S, tex_desc(mat.roughness), surf.u, surf.v).r;
+        const float sqrtRoughness = saturate(texRough * set.RoughnessScale);
         const float dsel = enableDiffuse ? 1.0f : 0.0f, ssel = enableSpecular ? 1.0f : 0.0f;
         const f3 diffuseAlbedo = scl(f3{lerpf(baseColor.x, 0.0f, metallic), lerpf(baseColor.y, 0.0f, metallic), lerpf(baseColor.z, 0.0f, metallic)}, dsel);
         const f3 specularAlbedo = scl(f3{lerpf(0.03f, baseColor.x, metallic), lerpf(0.03f, baseColor.y, metallic), lerpf(0.03f, baseColor.z, metallic)}, ssel);

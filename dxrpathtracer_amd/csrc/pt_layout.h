@@ -100,6 +100,12 @@ struct TexDesc {
     uint32_t fmt;
 };
 
+// Packed material taps (DXRPT_OPT_PACKED_TAPS): a material whose normal map (RGBA8 unorm) and metallic and
+// roughness maps (R8 or RGBA8 unorm, .r read) have one size gets a host-built RGBA8 unorm texture
+// (normal.r, normal.g, metallic, roughness), referenced from GeoShade::normal with this format tag: one
+// bilinear tap instead of three, the same texels, weights and decode (unorm) for every channel.
+constexpr uint32_t kTexFmtPackedNMR = 3u;
+
 // A texture reference packed into 8 B: `offset` as in TexDesc, whf = width | height << 15 | fmt << 30
 // (width, height <= 32767); whf == 0: no texture.
 struct GeoTex {

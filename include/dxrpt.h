@@ -235,6 +235,10 @@ typedef struct dxrpt_stats {
        schedule's head kernel; the rest is its tails'): node and triangle fetches of closest-hit and of
        any-hit rays, and (megakernel census) radiance hits. */
     uint64_t census_depth1[5];
+    /* Materials of the scene's geometries shaded from one packed normal / metallic / roughness tap
+       (DXRPT_OPT_PACKED_TAPS), and the packed textures built for them. */
+    uint32_t packed_materials;
+    uint32_t packed_textures;
 } dxrpt_stats;
 #define DXRPT_SCHED_MEGAKERNEL 1u    /* k_path (or the split head/tail kernels): no wavefront passes */
 /* 2u (path groups) and 64u (two concurrent halves) are retired (ABI 3) */
@@ -394,6 +398,11 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                         The tree is the same for every count (ABI 4: the spatial-split budget
                                         is shared between subtrees in proportion to their references, so
                                         subtrees build independently). */
+#define DXRPT_OPT_PACKED_TAPS 42u    /* 1 (default): a material whose normal, metallic and roughness maps
+                                          share one size (normal RGBA8 unorm, the others R8 or RGBA8
+                                          unorm) is shaded from one host-built RGBA8 texture (normal.rg,
+                                          metallic, roughness): one bilinear tap instead of three, same
+                                          texels and weights.  0: three taps.  Identical results. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

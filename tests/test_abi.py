@@ -99,11 +99,11 @@ def test_stats_and_tile_layouts_match_the_header(tmp_path):
 #include <stddef.h>
 #include "dxrpt.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(dxrpt_stats), offsetof(dxrpt_stats, kernel_ms),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(dxrpt_stats), offsetof(dxrpt_stats, kernel_ms),
          offsetof(dxrpt_stats, schedule), offsetof(dxrpt_stats, tail_occupancy),
          offsetof(dxrpt_stats, radiance_hits), offsetof(dxrpt_stats, census_depth1), sizeof(dxrpt_tile),
          sizeof(dxrpt_bvh_info), offsetof(dxrpt_bvh_info, phase_ms), offsetof(dxrpt_bvh_info, binary_depth_cap),
-         offsetof(dxrpt_bvh_info, ref_budget_pct));
+         offsetof(dxrpt_bvh_info, ref_budget_pct), offsetof(dxrpt_stats, packed_textures));
   return 0;
 }
 """)
@@ -112,5 +112,6 @@ int main(void) {
     got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
     want = [C.sizeof(A.Stats), A.Stats.kernel_ms.offset, A.Stats.schedule.offset, A.Stats.tail_occupancy.offset,
             A.Stats.radiance_hits.offset, A.Stats.census_depth1.offset, C.sizeof(A.Tile), C.sizeof(A.BvhInfo),
-            A.BvhInfo.phase_ms.offset, A.BvhInfo.binary_depth_cap.offset, A.BvhInfo.ref_budget_pct.offset]
+            A.BvhInfo.phase_ms.offset, A.BvhInfo.binary_depth_cap.offset, A.BvhInfo.ref_budget_pct.offset,
+            A.Stats.packed_textures.offset]
     assert got == want

@@ -221,7 +221,7 @@ def test_retired_options_are_rejected(torch_cuda):
         assert rc == A.DXRPT_E_UNSUPPORTED, (opt, rc)
         assert b"retired" in A.lib().dxrpt_last_error(t._ctx)
     assert A.lib().dxrpt_abi_version() == A.ABI_VERSION
-    for opt in (0, 42, 63, 1000):  # never assigned: an unknown option, not a retired one
+    for opt in (0, 43, 63, 1000):  # never assigned: an unknown option, not a retired one
         assert A.lib().dxrpt_set_option(t._ctx, opt, 1) == A.DXRPT_E_INVALID_ARG, opt
         assert b"unknown option" in A.lib().dxrpt_last_error(t._ctx)
     with pytest.raises(Exception, match="frame overlap"):
@@ -649,6 +649,41 @@ def test_opacity_micromap_is_bit_identical(torch_cuda, name, L, anyhit, W, H, me
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
         t.set_option(A.OPT_MEGAKERNEL_SPLIT, A.DEFAULT_MEGAKERNEL_SPLIT)
         t.set_option(A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)
+
+
+@pytest.mark.parametrize("name,L,W,H,mega,split,ov", [
+    ("sponza", 3, 480, 270, 1 << 30, 1, {}), ("sponza", 4, 320, 180, 1 << 30, 0, {}), ("sponza", 3, 320, 180, 0, 0, {}),
+    ("suntemple", 3, 480, 270, 1 << 30, 1, {}), ("sponza", 4, 320, 180, 1 << 30, 1, dict(EnableNormalMaps=0)),
+    ("sponza", 3, 256, 144, 1 << 30, 0, dict(EnableWhiteFurnaceMode=1)),
+    ("sponza", 4, 320, 180, 1 << 30, 1, dict(MetallicScale=0.5, RoughnessScale=1.5, EnableIndirectSpecular=1))])
+def test_packed_taps_are_bit_identical(torch_cuda, name, L, W, H, mega, split, ov):
+    # DXRPT_OPT_PACKED_TAPS: materials whose normal, metallic and roughness maps share a size (or are 1 x 1)
+    # are shaded from one packed RGBA8 texture -- one bilinear tap instead of three.  The frame must equal
+    # the three-tap frame bit for bit on every schedule (split head / tails, k_path, wavefront passes),
+    # with normal maps off (the tap still feeds metallic / roughness) and in furnace mode (no tap)
+    torch = torch_cuda
+    sc, sky = scene_bundle(name)
+    st = sc.settings(MaxPathLength=L, **ov)
+    t = tracer(name)
+    rtc = D.make_constants(sc, st, sky, W, H, 2)
+    try:
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, mega)
+        t.set_option(A.OPT_MEGAKERNEL_SPLIT, split)
+        frames = []
+        for packed in (0, 1):
+            t.set_option(A.OPT_PACKED_TAPS, packed)
+            acc = torch.full((W * H, 4), 0.25, dtype=torch.float32, device="cuda")
+            frames.append(gpu_render(torch, name, W, H, st, 2, accum=acc, rtc=rtc).cpu().numpy())
+            s = t.stats()
+            if mega:
+                assert bool(s.schedule & A.SCHED_SPLIT) == bool(split), s.schedule
+            # the proxies' materials: normal 512 x 512 RGBA8, roughness 512 x 512 R8, metallic 1 x 1 R8
+            assert (s.packed_materials > 0) == bool(packed), (packed, s.packed_materials, s.packed_textures)
+        np.testing.assert_array_equal(frames[1], frames[0])
+    finally:
+        t.set_option(A.OPT_PACKED_TAPS, A.DEFAULT_PACKED_TAPS)
+        t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
+        t.set_option(A.OPT_MEGAKERNEL_SPLIT, A.DEFAULT_MEGAKERNEL_SPLIT)
 
 
 @pytest.mark.parametrize("world,rank,overlap", [(8, 5, 0), (8, 2, 1), (16, 3, 0)])
