@@ -114,7 +114,7 @@ DEFAULT_BAKE_CHUNK = 1 << 21
 DEFAULT_XCD_CHUNK = 8
 DEFAULT_WAVE_ORDER_PERIOD = 64
 DEFAULT_OPACITY_MICROMAP = 1
-DEFAULT_PACKED_TAPS = 1
+DEFAULT_PACKED_TAPS = 3  # bit 0 packed normal/metallic/roughness maps, bit 1 inlined 1 x 1 maps
 DEFAULT_FRAME_OVERLAP = 3
 DEFAULT_WAVE_ORDER = 2  # by frame size
 DEFAULT_MEGAKERNEL_SPLIT = 2  # by frame size
@@ -134,7 +134,8 @@ class Stats(C.Structure):
                 ("kernel_ms", C.c_double * K_COUNT), ("kernel_launches", C.c_uint64 * K_COUNT),
                 ("timed_frames", C.c_uint64), ("frame_ms", C.c_double), ("schedule", u32), ("paths_per_wave", u32),
                 ("occupancy", u32), ("tail_occupancy", u32), ("radiance_hits", C.c_uint64),
-                ("census_depth1", C.c_uint64 * 5), ("packed_materials", C.c_uint32), ("packed_textures", C.c_uint32)]
+                ("census_depth1", C.c_uint64 * 5), ("packed_materials", C.c_uint32), ("packed_textures", C.c_uint32),
+                ("inlined_maps", C.c_uint32), ("reserved0", C.c_uint32)]
 
 
 # dxrpt_stats.schedule bits

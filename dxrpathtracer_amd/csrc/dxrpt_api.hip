@@ -137,9 +137,10 @@ struct dxrpt_ctx {
     uint32_t opt_bake_chunk = 1u << 21;     // DXRPT_OPT_BAKE_CHUNK (texels per bake launch)
     uint32_t opt_split = 2;                 // DXRPT_OPT_MEGAKERNEL_SPLIT (0 off, 1 on, 2 by frame size)
     uint32_t opt_omm = 1;                   // DXRPT_OPT_OPACITY_MICROMAP
-    uint32_t opt_packed = 1;                // DXRPT_OPT_PACKED_TAPS
+    uint32_t opt_packed = 3;                // DXRPT_OPT_PACKED_TAPS (bit 0: packed NMR maps, bit 1: inlined 1 x 1 maps)
     std::vector<uint32_t> texels_packed;    // packed normal/metallic/roughness textures, after `texels` on the device
     uint32_t packed_materials = 0, packed_textures = 0;  // of the current shading records (dxrpt_stats)
+    uint32_t inlined_refs = 0;  // geometry texture references inlined (1 x 1 maps)
     uint32_t opt_overlap = kOverlapBySize;  // DXRPT_OPT_FRAME_OVERLAP
     // overlapped frames: frame f runs on slot f % kOverlapSlots -- its own stream, path buffers, counters,
     // stage and BVH8 stack-spill slab -- and stages its radiance (d_stage); the caller's stream blends the
@@ -389,7 +390,7 @@ std::vector<GeoTex> build_packed(dxrpt_ctx* c) {
     std::vector<GeoTex> out(c->mats.size(), GeoTex{0u, 0u});
     c->texels_packed.clear();
     c->packed_materials = c->packed_textures = 0;
-    if (!c->opt_packed) return out;
+    if (!(c->opt_packed & 1u)) return out;
     std::map<std::array<uint32_t, 3>, GeoTex> made;
     std::vector<bool> used(c->mats.size(), false);
     for (const dxrpt_geometry_info& g : c->geos)
@@ -473,11 +474,20 @@ void upload_textures(dxrpt_ctx* c) {
         return g;
     };
     std::vector<GeoShade> gs(c->geos.size());
+    c->inlined_refs = 0;
     for (size_t g = 0; g < c->geos.size(); ++g) {
         const uint32_t mi = c->geos[g].MaterialIdx;
         const dxrpt_material& m = c->mats[mi];
         gs[g] = GeoShade{ref(m.Albedo), ref(m.Normal), ref(m.Roughness), ref(m.Metallic), ref(m.Emissive), ref(m.Opacity)};
         if (mi < packed.size() && packed[mi].whf) gs[g].normal = packed[mi];  // (normal.rg, metallic, roughness)
+        if (c->opt_packed & 2u)  // 1 x 1 maps inline (pt_layout.h GeoTex): their taps read no memory
+            for (GeoTex* r : {&gs[g].albedo, &gs[g].normal, &gs[g].roughness, &gs[g].metallic, &gs[g].emissive}) {
+                if ((r->whf & 0x3FFFFFFFu) != (1u | (1u << 15))) continue;
+                const size_t n0 = c->texels.size();
+                r->offset = r->offset < n0 ? c->texels[r->offset] : c->texels_packed[r->offset - n0];
+                r->whf &= 0xC0000000u;  // width = height = 0, format kept
+                ++c->inlined_refs;
+            }
     }
     c->d_geoshade.upload(gs.data(), gs.size() * sizeof(GeoShade));
     c->geoshade_dirty = false;
@@ -789,7 +799,7 @@ int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value) {
             drain_frames(ctx);  // in-flight frames may read the micromap
             ctx->opt_omm = uint32_t(value);
         } else if (option == DXRPT_OPT_PACKED_TAPS) {
-            require(value <= 1, "dxrpt_set_option: packed taps must be 0 (off) or 1 (on)");
+            require(value <= 3, "dxrpt_set_option: packed taps must be 0..3 (bit 0: packed maps, bit 1: inlined 1 x 1 maps)");
             if (uint32_t(value) != ctx->opt_packed) {  // the shading records (and the packed texels) change
                 drain_frames(ctx);
                 ctx->opt_packed = uint32_t(value);
@@ -1392,6 +1402,7 @@ int dxrpt_get_stats(dxrpt_ctx* ctx, dxrpt_stats* out) {
         dxrpt_stats s = ctx->last;
         s.packed_materials = ctx->packed_materials;
         s.packed_textures = ctx->packed_textures;
+        s.inlined_maps = ctx->inlined_refs;
         for (int d = 1; d < ctx->last_L && d < int(DXRPT_MAX_PATH_LENGTH); ++d) {
             s.radiance_rays_per_depth[d] = cnt[d];
             s.shadow_rays_per_depth[d] = cnt[16 + d];

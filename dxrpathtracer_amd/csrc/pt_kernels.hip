@@ -97,29 +97,39 @@ PT_DEV Texel4 decode_texel(uint32_t w, bool r8, uint32_t l, uint32_t x) {
     return t;
 }
 
+// A 1 x 1 map's reference carries its texel word instead of a pool offset (DXRPT_OPT_PACKED_TAPS bit 1,
+// pt_layout.h kTexInline): its bilinear tap reads no memory -- the same word four times, the same weights,
+// so the same value, NaN for a NaN / Inf UV included.
+PT_DEV bool tex_inline(const TexDesc& td) { return td.inl; }
+
 PT_DEV TexDesc tex_desc(GeoTex g) {
     TexDesc td;
     td.offset = g.offset;
     td.width = g.whf & 0x7FFFu;
     td.height = (g.whf >> 15) & 0x7FFFu;
     td.fmt = g.whf >> 30;
+    td.inl = (g.whf & 0x3FFFFFFFu) == 0u;  // width = height = 0: an inlined 1 x 1 map
+    if (td.inl) td.width = td.height = 1u;
     return td;
 }
 
 // The per-texel form (a format branch per texel): the split tails' material taps keep it -- the
 // branch-free form above costs them 5-10 % (r05, profiles/r05_ab_taps.txt), while it saves 2-5 % in the
 // head, the single k_path and the alpha tests.
-PT_DEV Texel4 fetch_texel(const SceneDev& S, const TexDesc& td, int x, int y) {
+PT_DEV Texel4 fetch_texel(const SceneDev& S, const TexDesc& td, int x, int y, bool inl = false) {
     const bool r8 = td.fmt == DXRPT_TEX_R8_UNORM;
     const uint32_t tiles_x = (td.width + (r8 ? kTexTileW8 : kTexTileW32) - 1u) / (r8 ? kTexTileW8 : kTexTileW32);
     const uint32_t word = tex_tile_word(uint32_t(x), uint32_t(y), tiles_x, r8);
     Texel4 t;
+    uint32_t w;
+    if (inl)  // a 1 x 1 map inlined in its reference (tex_inline)
+        w = td.offset;
+    else
+        w = S.texels[td.offset + word];
     if (r8) {
-        uint32_t w = S.texels[td.offset + word];
         float v = g_lut[(w >> ((uint32_t(x) & 3u) * 8u)) & 0xFFu];
         t.r = v; t.g = v; t.b = v; t.a = 1.0f;
     } else {
-        uint32_t w = S.texels[td.offset + word];
         const uint32_t l = td.fmt == DXRPT_TEX_RGBA8_SRGB ? 256u : 0u;
         t.r = g_lut[l + (w & 0xFFu)];
         t.g = g_lut[l + ((w >> 8) & 0xFFu)];
@@ -131,6 +141,7 @@ PT_DEV Texel4 fetch_texel(const SceneDev& S, const TexDesc& td, int x, int y) {
 
 template <bool kGrouped = true>
 PT_DEV Texel4 sample_tex_desc(const SceneDev& S, const TexDesc td, float u, float v) {
+    const bool inl = tex_inline(td);
     if (!kGrouped) {
         float x = u * float(td.width) - 0.5f;
         float y = v * float(td.height) - 0.5f;
@@ -138,8 +149,15 @@ PT_DEV Texel4 sample_tex_desc(const SceneDev& S, const TexDesc td, float u, floa
         float fx = x - x0, fy = y - y0;
         int ix0 = wrap_coord(int(x0), td.width), ix1 = wrap_coord(int(x0) + 1, td.width);
         int iy0 = wrap_coord(int(y0), td.height), iy1 = wrap_coord(int(y0) + 1, td.height);
-        Texel4 t00 = fetch_texel(S, td, ix0, iy0), t10 = fetch_texel(S, td, ix1, iy0);
-        Texel4 t01 = fetch_texel(S, td, ix0, iy1), t11 = fetch_texel(S, td, ix1, iy1);
+        Texel4 t00, t10, t01, t11;
+        if (inl) {
+            t00 = t10 = t01 = t11 = fetch_texel(S, td, 0, 0, true);
+        } else {
+            t00 = fetch_texel(S, td, ix0, iy0);
+            t10 = fetch_texel(S, td, ix1, iy0);
+            t01 = fetch_texel(S, td, ix0, iy1);
+            t11 = fetch_texel(S, td, ix1, iy1);
+        }
         Texel4 r;
         r.r = lerpf(lerpf(t00.r, t10.r, fx), lerpf(t01.r, t11.r, fx), fy);
         r.g = lerpf(lerpf(t00.g, t10.g, fx), lerpf(t01.g, t11.g, fx), fy);
@@ -155,11 +173,16 @@ PT_DEV Texel4 sample_tex_desc(const SceneDev& S, const TexDesc td, float u, floa
     int iy0 = wrap_coord(int(y0), td.height), iy1 = wrap_coord(int(y0) + 1, td.height);
     const bool r8 = td.fmt == DXRPT_TEX_R8_UNORM;
     const uint32_t tiles_x = r8 ? (td.width + kTexTileW8 - 1u) / kTexTileW8 : (td.width + kTexTileW32 - 1u) / kTexTileW32;
-    const uint32_t* T = S.texels + td.offset;
-    const uint32_t w00 = T[tex_word(uint32_t(ix0), uint32_t(iy0), tiles_x, r8)];
-    const uint32_t w10 = T[tex_word(uint32_t(ix1), uint32_t(iy0), tiles_x, r8)];
-    const uint32_t w01 = T[tex_word(uint32_t(ix0), uint32_t(iy1), tiles_x, r8)];
-    const uint32_t w11 = T[tex_word(uint32_t(ix1), uint32_t(iy1), tiles_x, r8)];
+    uint32_t w00, w10, w01, w11;
+    if (inl) {
+        w00 = w10 = w01 = w11 = td.offset;
+    } else {
+        const uint32_t* T = S.texels + td.offset;
+        w00 = T[tex_word(uint32_t(ix0), uint32_t(iy0), tiles_x, r8)];
+        w10 = T[tex_word(uint32_t(ix1), uint32_t(iy0), tiles_x, r8)];
+        w01 = T[tex_word(uint32_t(ix0), uint32_t(iy1), tiles_x, r8)];
+        w11 = T[tex_word(uint32_t(ix1), uint32_t(iy1), tiles_x, r8)];
+    }
     const uint32_t l = td.fmt == DXRPT_TEX_RGBA8_SRGB ? 256u : 0u;
     Texel4 t00 = decode_texel(w00, r8, l, uint32_t(ix0)), t10 = decode_texel(w10, r8, l, uint32_t(ix1));
     Texel4 t01 = decode_texel(w01, r8, l, uint32_t(ix0)), t11 = decode_texel(w11, r8, l, uint32_t(ix1));

@@ -98,6 +98,7 @@ struct TexDesc {
     uint32_t width;
     uint32_t height;
     uint32_t fmt;
+    bool inl = false;  // device view of an inlined 1 x 1 map (GeoTex whf width = height = 0): offset = its texel word
 };
 
 // Packed material taps (DXRPT_OPT_PACKED_TAPS): a material whose normal map (RGBA8 unorm) and metallic and
@@ -108,6 +109,8 @@ constexpr uint32_t kTexFmtPackedNMR = 3u;
 
 // A texture reference packed into 8 B: `offset` as in TexDesc, whf = width | height << 15 | fmt << 30
 // (width, height <= 32767); whf == 0: no texture.
+// An inlined 1 x 1 map (DXRPT_OPT_PACKED_TAPS bit 1, not for opacity): whf's width and height are 0 and
+// `offset` is the map's texel word (the pool word: RGBA8, or R8 in byte 0), so its tap reads no memory.
 struct GeoTex {
     uint32_t offset;
     uint32_t whf;

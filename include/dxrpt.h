@@ -239,6 +239,9 @@ typedef struct dxrpt_stats {
        (DXRPT_OPT_PACKED_TAPS), and the packed textures built for them. */
     uint32_t packed_materials;
     uint32_t packed_textures;
+    /* Geometry texture references inlined as constants (1 x 1 maps, DXRPT_OPT_PACKED_TAPS bit 1). */
+    uint32_t inlined_maps;
+    uint32_t reserved0;
 } dxrpt_stats;
 #define DXRPT_SCHED_MEGAKERNEL 1u    /* k_path (or the split head/tail kernels): no wavefront passes */
 /* 2u (path groups) and 64u (two concurrent halves) are retired (ABI 3) */
@@ -398,11 +401,14 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                         The tree is the same for every count (ABI 4: the spatial-split budget
                                         is shared between subtrees in proportion to their references, so
                                         subtrees build independently). */
-#define DXRPT_OPT_PACKED_TAPS 42u    /* 1 (default): a material whose normal, metallic and roughness maps
-                                          share one size (normal RGBA8 unorm, the others R8 or RGBA8
-                                          unorm) is shaded from one host-built RGBA8 texture (normal.rg,
-                                          metallic, roughness): one bilinear tap instead of three, same
-                                          texels and weights.  0: three taps.  Identical results. */
+#define DXRPT_OPT_PACKED_TAPS 42u    /* Material taps from fewer loads, identical results.  Bit 0: a
+                                        material whose normal, metallic and roughness maps are each W x H
+                                        or 1 x 1 (normal RGBA8 unorm, the others R8 or RGBA8 unorm) is
+                                        shaded from one host-built RGBA8 texture (normal.rg, metallic,
+                                        roughness): one bilinear tap instead of three, same texels and
+                                        weights.  Bit 1: a 1 x 1 map (albedo, normal, roughness, metallic,
+                                        emissive) travels inline in the shading record, so its tap reads
+                                        no memory.  Default 3; 0: a tap per map. */
 int dxrpt_set_option(dxrpt_ctx* ctx, uint32_t option, uint64_t value);
 /* Zeroes the accumulated kernel timings. */
 int dxrpt_reset_timing(dxrpt_ctx* ctx);

@@ -8,11 +8,13 @@ rc=$?; tail -2 gpurun_out/pytest_packed.log; [ $rc -ne 0 ] && exit $rc
 run() { timeout -k 10 150 python -u scripts/time_frames.py --rounds 5 "$@" 2>&1 | grep -v amdgpu.ids || exit 1; }
 for r in 1 2; do
   for cfg in metric c2 c4 c3; do
-    run --label packed --config $cfg --kernels
-    run --label three-taps --config $cfg --kernels --opt PACKED_TAPS=0
+    run --label packed --config $cfg
+    run --label packed-only --config $cfg --opt PACKED_TAPS=1
+    run --label three-taps --config $cfg --opt PACKED_TAPS=0
   done
   for rk in 1 2; do
     run --label packed --share 8 --rank $rk --cur-copy
+    run --label packed-only --share 8 --rank $rk --cur-copy --opt PACKED_TAPS=1
     run --label three-taps --share 8 --rank $rk --cur-copy --opt PACKED_TAPS=0
   done
 done

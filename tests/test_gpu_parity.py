@@ -658,8 +658,8 @@ def test_opacity_micromap_is_bit_identical(torch_cuda, name, L, anyhit, W, H, me
     ("sponza", 4, 320, 180, 1 << 30, 1, dict(MetallicScale=0.5, RoughnessScale=1.5, EnableIndirectSpecular=1))])
 def test_packed_taps_are_bit_identical(torch_cuda, name, L, W, H, mega, split, ov):
     # DXRPT_OPT_PACKED_TAPS: materials whose normal, metallic and roughness maps share a size (or are 1 x 1)
-    # are shaded from one packed RGBA8 texture -- one bilinear tap instead of three.  The frame must equal
-    # the three-tap frame bit for bit on every schedule (split head / tails, k_path, wavefront passes),
+    # are shaded from one packed RGBA8 texture -- one bilinear tap instead of three -- and 1 x 1 maps ride
+    # inline in the shading record (no load).  Every combination must equal the tap-per-map frame bit for bit on every schedule (split head / tails, k_path, wavefront passes),
     # with normal maps off (the tap still feeds metallic / roughness) and in furnace mode (no tap)
     torch = torch_cuda
     sc, sky = scene_bundle(name)
@@ -670,16 +670,18 @@ def test_packed_taps_are_bit_identical(torch_cuda, name, L, W, H, mega, split, o
         t.set_option(A.OPT_MEGAKERNEL_PATHS, mega)
         t.set_option(A.OPT_MEGAKERNEL_SPLIT, split)
         frames = []
-        for packed in (0, 1):
+        for packed in (0, 1, 2, 3):  # bit 0 packed maps, bit 1 inlined 1 x 1 maps
             t.set_option(A.OPT_PACKED_TAPS, packed)
             acc = torch.full((W * H, 4), 0.25, dtype=torch.float32, device="cuda")
             frames.append(gpu_render(torch, name, W, H, st, 2, accum=acc, rtc=rtc).cpu().numpy())
             s = t.stats()
             if mega:
                 assert bool(s.schedule & A.SCHED_SPLIT) == bool(split), s.schedule
-            # the proxies' materials: normal 512 x 512 RGBA8, roughness 512 x 512 R8, metallic 1 x 1 R8
-            assert (s.packed_materials > 0) == bool(packed), (packed, s.packed_materials, s.packed_textures)
-        np.testing.assert_array_equal(frames[1], frames[0])
+            # the proxies' materials: normal 512 x 512 RGBA8, roughness 512 x 512 R8, metallic and emissive 1 x 1
+            assert (s.packed_materials > 0) == bool(packed & 1), (packed, s.packed_materials, s.packed_textures)
+            assert (s.inlined_maps > 0) == bool(packed & 2), (packed, s.inlined_maps)
+        for f in frames[1:]:
+            np.testing.assert_array_equal(f, frames[0])
     finally:
         t.set_option(A.OPT_PACKED_TAPS, A.DEFAULT_PACKED_TAPS)
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
