@@ -81,7 +81,10 @@ constexpr uint64_t kSplitMinVertices = 8000000;
 constexpr uint64_t kSplitMinVerticesOverlap2 = 2000000;  // two frames in flight
 constexpr uint64_t kSplitMinVerticesOverlap3 = 1500000;  // three
 // DXRPT_OPT_FRAME_OVERLAP: up to three frames in flight, frame f on slot f % (frames in flight)
-constexpr uint32_t kOverlapSlots = 3;
+#ifndef DXRPT_OVERLAP_SLOTS
+#define DXRPT_OVERLAP_SLOTS 3
+#endif
+constexpr uint32_t kOverlapSlots = DXRPT_OVERLAP_SLOTS;
 constexpr uint32_t kOverlapBySize = 3;  // DXRPT_OPT_FRAME_OVERLAP value: frames in flight by frame size
 // BVH8 stack-spill slabs: 0 = work on the caller's stream, 1 + k = overlap slot k
 constexpr uint32_t kSpillSlabs = 1 + kOverlapSlots;
@@ -1207,7 +1210,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         // drain several times per frame -- two for the large single-kernel frames (720p: 3 is +1 %)
         // (profiles/r05_ab_overlap_depth.txt, r05_ab_overlap_cur.txt)
         if (overlap) {
-            const uint32_t want = ctx->opt_overlap == kOverlapBySize ? (fp.split || paths <= 600000u ? 3u : 2u)
+            const uint32_t want = ctx->opt_overlap == kOverlapBySize ? (fp.split || paths <= 600000u ? kOverlapSlots : 2u)
                                                                      : ctx->opt_overlap + 1u;
             if (want != ctx->ovl_slots) {  // the rotation restarts
                 drain_frames(ctx);
