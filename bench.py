@@ -525,6 +525,11 @@ def main():
                         "build_threads": bvh.threads, "binary_depth_cap": bvh.binary_depth_cap,
                         "treelet_passes": bvh.treelet_passes, "ref_budget_pct": bvh.ref_budget_pct,
                         "sah": round(bvh.sah_cost, 2), "wide_sah": round(bvh.wide_sah, 3)},
+                # material taps actually issued per hit: the SURVEY 8(d) byte formula keeps five taps; packed
+                # normal/metallic/roughness maps and inlined 1 x 1 maps (DXRPT_OPT_PACKED_TAPS) read fewer
+                "material_maps": {"packed_materials": int(stats.packed_materials),
+                                  "packed_textures": int(stats.packed_textures),
+                                  "inlined_maps": int(stats.inlined_maps)},
                 "setup_s": round(setup_s, 2),
             },
         }

@@ -102,13 +102,16 @@ PT_DEV Texel4 decode_texel(uint32_t w, bool r8, uint32_t l, uint32_t x) {
 // so the same value, NaN for a NaN / Inf UV included.
 PT_DEV bool tex_inline(const TexDesc& td) { return td.inl; }
 
+// kInline: the reference may be an inlined 1 x 1 map (material maps; never the opacity map, whose
+// AnyHitShader tap runs inside the traversal loops and keeps the plain form)
+template <bool kInline = true>
 PT_DEV TexDesc tex_desc(GeoTex g) {
     TexDesc td;
     td.offset = g.offset;
     td.width = g.whf & 0x7FFFu;
     td.height = (g.whf >> 15) & 0x7FFFu;
     td.fmt = g.whf >> 30;
-    td.inl = (g.whf & 0x3FFFFFFFu) == 0u;  // width = height = 0: an inlined 1 x 1 map
+    td.inl = kInline && (g.whf & 0x3FFFFFFFu) == 0u;  // width = height = 0: an inlined 1 x 1 map
     if (td.inl) td.width = td.height = 1u;
     return td;
 }
@@ -139,9 +142,9 @@ PT_DEV Texel4 fetch_texel(const SceneDev& S, const TexDesc& td, int x, int y, bo
     return t;
 }
 
-template <bool kGrouped = true>
+template <bool kGrouped = true, bool kInline = true>
 PT_DEV Texel4 sample_tex_desc(const SceneDev& S, const TexDesc td, float u, float v) {
-    const bool inl = tex_inline(td);
+    const bool inl = kInline && tex_inline(td);
     if (!kGrouped) {
         float x = u * float(td.width) - 0.5f;
         float y = v * float(td.height) - 0.5f;
@@ -301,7 +304,7 @@ PT_DEV bool alpha_accepts(const SceneDev& S, uint32_t geom, uint32_t gtri, uint3
     const float w0 = (1.0f - b1) - b2;
     float u = bary_lerp(uv[0].x, uv[1].x, uv[2].x, w0, b1, b2);
     float v = bary_lerp(uv[0].y, uv[1].y, uv[2].y, w0, b1, b2);
-    return !(sample_tex_desc<kGA>(S, tex_desc(opacity), u, v).r < 0.35f);
+    return !(sample_tex_desc<kGA, false>(S, tex_desc<false>(opacity), u, v).r < 0.35f);
 }
 
 // ---- triangles ------------------------------------------------------------------------------------
