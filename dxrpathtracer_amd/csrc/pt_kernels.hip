@@ -1876,6 +1876,7 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
     V.hit = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
     VertexOut O;
     uint32_t nsh = 0;
+    // per-texel taps (r05: the grouped form is neutral here even with two taps per hit, r05_ab_tailgrp.txt)
     path_vertex<false>(A, d, V, [&](int, f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
         emit_shadow(A, i, nsh, o, dd, tmn, tmx, c, fo);  // shadow slots by the dense index (< qsize)
     }, O);
