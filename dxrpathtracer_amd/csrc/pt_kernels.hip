@@ -1769,7 +1769,7 @@ PT_DEV void census_flush(const KArgs& A, const uint32_t (&cnt)[10]) {
 
 // Raygen + depth 1 of camera path p (the head's per-lane body).
 template <bool kCount>
-PT_DEV void head_path(const KArgs& A, uint32_t p, uint32_t blk, uint32_t* cnt, PhaseAcc* pa = nullptr) {
+PT_DEV void head_path(const KArgs& A, uint32_t p, uint32_t* cnt, PhaseAcc* pa = nullptr) {
     const dxrpt_app_settings& set = A.P.set;
     const PrimaryRay pr = primary_ray(A, p);
     const uint32_t packet = (p | 63u) < A.P.num_paths ? A.P.packet : 0u;
@@ -1805,7 +1805,25 @@ PT_DEV void head_path(const KArgs& A, uint32_t p, uint32_t blk, uint32_t* cnt, P
     phase_mark(pa, 1);
     const bool cont = O.cont;
     const bool nextDiffuse = O.nextIsDiffuse;
-    const uint32_t qpos = split_push(A, 1, cont, O, pr.pixelIdx, pr.accumIdx, blk, gridDim.x);
+    // the depth-2 queue is direct-mapped: entry p for path slot p (>= 99 % of camera paths continue, so a
+    // compacting append buys no density), written without the append's returning atomic -- the head waited
+    // on it (8.5 % of its lane time, r05_phases2.txt) -- and an ended path marks its entry (TMax -1) for the
+    // tail to skip.  The queue counter still counts the rays (dxrpt_stats).  r05: metric -1.9 %, C2 / C4
+    // -1 %, the 1/2 share -1.4 % (profiles/r05_ab_direct.txt).
+    const uint32_t qpos = p;
+    count_rays(A.F.counters + 2u * kQueueShards, cont ? 1u : 0u);
+    {
+        const RayQueue& Q = A.F.q[0];
+        if (cont) {
+            Q.org[p] = make_float4(O.nextOrigin.x, O.nextOrigin.y, O.nextOrigin.z, kFP32Max);
+            Q.dir[p] = make_float4(O.nextDir.x, O.nextDir.y, O.nextDir.z, bitsf(pr.accumIdx));
+            Q.thr[p] = make_float4(O.nextThr.x, O.nextThr.y, O.nextThr.z, O.nextRoughness);
+            Q.pix[p] = pr.pixelIdx;
+        } else {
+            Q.org[p] = make_float4(0.0f, 0.0f, 0.0f, -1.0f);
+        }
+    }
+
     float4 rad = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     rad.x += 1.0f * O.local.x;
     rad.y += 1.0f * O.local.y;
@@ -1829,16 +1847,16 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     if (!kCount) {
 #if DXRPT_DIAG_PHASES
         PhaseAcc pa = phase_start();
-        if (p < A.P.num_paths) head_path<false>(A, p, blk, nullptr, &pa);
+        if (p < A.P.num_paths) head_path<false>(A, p, nullptr, &pa);
         phase_mark(&pa, 7);
         phase_flush(&pa, 1);
 #else
-        if (p < A.P.num_paths) head_path<false>(A, p, blk, nullptr);
+        if (p < A.P.num_paths) head_path<false>(A, p, nullptr);
 #endif
         return;
     }
     uint32_t cnt[10] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    if (p < A.P.num_paths) head_path<true>(A, p, blk, cnt);
+    if (p < A.P.num_paths) head_path<true>(A, p, cnt);
     census_flush(A, cnt);
 }
 
@@ -1847,11 +1865,13 @@ template <bool kCount, bool kLast>
 PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw, const uint32_t* cnt_q, uint32_t* cnt,
                       PhaseAcc* pa = nullptr) {
     const dxrpt_app_settings& set = A.P.set;
-    const uint32_t pos = queue_pos(cnt_q, A.F.cap_r, i);
+    const bool direct = d == 2;  // the head's direct-mapped queue (entry = path slot)
+    const uint32_t pos = direct ? i : queue_pos(cnt_q, A.F.cap_r, i);
     const RayQueue& Q = A.F.q[d & 1];
     HitRec h;
     {
         const float4 o4 = Q.org[pos], d4 = Q.dir[pos];
+        if (direct && !(o4.w >= 0.0f)) return;  // the path ended at depth 1
         uint32_t nv = 0, nt = 0;
         traverse8<false, kCount, true, true, false>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= set.MaxAnyHitPathLength, h, nv, nt);
         if (kCount) {
@@ -1909,7 +1929,7 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
 template <int kOcc, bool kCount = false, bool kLast = false>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) void k_path_tail(KArgs A, int d) {
     const uint32_t* cnt_q = A.F.counters + uint32_t(d) * kQueueShards;
-    const uint32_t n = queue_total(cnt_q);
+    const uint32_t n = d == 2 ? A.P.num_paths : queue_total(cnt_q);  // depth 2: every path slot (direct-mapped)
     const uint32_t nw = (n + 63u) / 64u;  // waves with work
     // wave j of the queue: XCD runs of A.P.xcd_chunk consecutive queue chunks among the nw live waves
     // (workgroup b runs on XCD b mod 8; the grid's surplus workgroups exit at once)
