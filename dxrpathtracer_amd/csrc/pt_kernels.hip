@@ -1812,7 +1812,7 @@ PT_DEV void head_path(const KArgs& A, uint32_t p, uint32_t* cnt, PhaseAcc* pa = 
     // -1 %, the 1/2 share -1.4 % (profiles/r05_ab_direct.txt).
     const uint32_t qpos = p;
     count_rays(A.F.counters + 2u * kQueueShards, cont ? 1u : 0u);
-    {
+    if (set.MaxPathLength > 2) {  // a depth-2 tail reads the queue
         const RayQueue& Q = A.F.q[0];
         if (cont) {
             Q.org[p] = make_float4(O.nextOrigin.x, O.nextOrigin.y, O.nextOrigin.z, kFP32Max);
