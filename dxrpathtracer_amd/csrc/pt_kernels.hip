@@ -66,9 +66,22 @@ struct Texel4 {
 // kernel that samples textures (shading, alpha-tested traversal) calls lut_fill first.
 __shared__ float g_lut[512];
 
+// The table by LDS DMA (r05): global_load_lds_dwordx4 -- 16 B per lane, 1 KB per instruction -- the whole
+// table by every wave (identical values: no barrier needed between a workgroup's waves), then one
+// vmcnt(0), so the table is in before anything else runs.  No VGPR round trip, no ds_write, no barrier:
+// metric / C2 / C4 -2 %.  kDma false: the plain copy (the non-last split tails of long paths keep it: the
+// DMA form there cost C3 +1.8 %, C5 +1.3 %, profiles/r05_ab_lutdma*.txt -- measured, not understood).
+template <bool kDma = true>
 PT_DEV void lut_fill(const SceneDev& S) {
-    for (uint32_t i = threadIdx.x; i < 512u; i += blockDim.x) g_lut[i] = S.lut[i];
-    __syncthreads();
+    if (kDma) {
+        const char* src = reinterpret_cast<const char*>(S.lut) + (threadIdx.x & 63u) * 16u;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(g_lut), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(src + 1024, (__attribute__((address_space(3))) void*)(g_lut + 256), 16, 0, 0);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (expcnt, lgkmcnt left at their maxima)
+    } else {
+        for (uint32_t i = threadIdx.x; i < 512u; i += blockDim.x) g_lut[i] = S.lut[i];
+        __syncthreads();
+    }
 }
 
 // A texel's word in the tiled pool (pt_kernels.h tex_tile_word), branch-free in the format: both tilings'
@@ -1935,7 +1948,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     // (workgroup b runs on XCD b mod 8; the grid's surplus workgroups exit at once)
     if (blockIdx.x >= nw) return;
     const uint32_t j = A.P.xcd_chunk ? xcd_position(blockIdx.x, nw, A.P.xcd_chunk) : blockIdx.x;
-    lut_fill(A.S);
+    lut_fill<kLast>(A.S);  // the plain copy in the non-last tails (DMA there: C3 +1.8 %, C5 +1.3 %)
     const uint32_t i = j * blockDim.x + threadIdx.x;
     if (!kCount) {
 #if DXRPT_DIAG_PHASES
