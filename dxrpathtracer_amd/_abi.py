@@ -112,7 +112,7 @@ DEFAULT_MEGAKERNEL_PATHS = 0xFFFFFFFF
 DEFAULT_MEGAKERNEL_OCCUPANCY = 0
 DEFAULT_BAKE_CHUNK = 1 << 21
 DEFAULT_XCD_CHUNK = 8
-DEFAULT_WAVE_ORDER_PERIOD = 64
+DEFAULT_WAVE_ORDER_PERIOD = 256
 DEFAULT_OPACITY_MICROMAP = 1
 DEFAULT_PACKED_TAPS = 3  # bit 0 packed normal/metallic/roughness maps, bit 1 inlined 1 x 1 maps
 DEFAULT_FRAME_OVERLAP = 3

@@ -183,9 +183,12 @@ struct dxrpt_ctx {
     uint64_t order_key = 0;     // (waves, tiles generation) the order was built for
     bool order_ready = false;   // d_wave_order holds an order for order_key
     uint32_t order_frame = 0;   // ordered frames since the order (re)started
-    uint32_t opt_order_period = 64;  // DXRPT_OPT_WAVE_ORDER_PERIOD (r02: 1/8 share 0.549 -> 0.534 ms at 16;
+    uint32_t opt_order_period = 256; // DXRPT_OPT_WAVE_ORDER_PERIOD (r02: 1/8 share 0.549 -> 0.534 ms at 16;
                                      // r04: 16 -> 64, slowest 1/8 shares -1.3..-2.5 %: a recording frame costs
-                                     // ~0.26 ms, profiles/r04_ab_order_period.txt)
+                                     // ~0.26 ms, profiles/r04_ab_order_period.txt; r05, three frames in flight:
+                                     // 64 -> 256, 1/8 shares -2.6 % -- the rebuild also waits for the other
+                                     // slots' frames; 256 frames are ~60 ms of a 1/8 share,
+                                     // profiles/r05_ab_order_period.txt)
     uint64_t tiles_gen = 0;     // bumped whenever the tile list changes
     DevBuf d_spill;  // BVH8 traversal stack entries beyond the LDS part (deep trees only), kSpillSlabs slabs
     uint32_t spill_threads = 0;  // per-slab stride: the largest traversal launch seen

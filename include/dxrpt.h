@@ -359,8 +359,9 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                         neighbouring blocks on different XCDs).  Identical results. */
 #define DXRPT_OPT_WAVE_ORDER_PERIOD 32u /* cost-ordered frames: every this-many-th frame records its waves'
                                            durations and rebuilds the order, the frames between reuse it
-                                           (default 64, four SqrtNumSamples^2 = 16 cycles of progressive
-                                           frames; 1 = every frame).  Identical results. */
+                                           (default 256, sixteen SqrtNumSamples^2 = 16 cycles of
+                                           progressive frames, ~60 ms of a GPU's 1/8 band share; 1 = every
+                                           frame).  Identical results. */
 #define DXRPT_OPT_MEGAKERNEL_SPLIT 33u /* 1: megakernel frames run as one kernel per path depth -- a head
                                           kernel runs raygen and depth 1 of every camera path, then per
                                           further depth one kernel runs the surviving paths, compacted into

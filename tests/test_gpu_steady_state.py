@@ -161,8 +161,8 @@ def test_c3_1080p_L8_sixteen_samples(torch_cuda):
 def test_overlapped_frames_are_bit_identical(torch_cuda, W, H, L, frames, share):
     # DXRPT_OPT_FRAME_OVERLAP: back-to-back frames (no host sync between them, as bench.py and every rank
     # render them) rotate over two or three sets of internal streams and stage their radiance; the caller's
-    # stream blends each stage in frame order (RayTrace.hlsl:140-148).  >= 17 frames cross a cost-order
-    # rebuild (every 16th frame records, the next frame waits for the new order); 1080p L=3 and L=8 and
+    # stream blends each stage in frame order (RayTrace.hlsl:140-148).  (Cost-order rebuilds under overlap:
+    # test_wave_order_is_bit_identical at periods 1 and 2.) 1080p L=3 and L=8 and
     # 4K L=6 run the depth-split schedule overlapped against k_path / the split one frame at a time.  The
     # accumulated target must equal the one-frame-at-a-time schedule's bit for bit.
     torch = torch_cuda
