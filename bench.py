@@ -187,6 +187,40 @@ def schedule_name(bits, A):
     return s
 
 
+def percentile(v, q):
+    return float(np.percentile(np.asarray(v, dtype=np.float64), q)) if len(v) else None
+
+
+def paced_latency(torch, stream, render, frames, ahead):
+    """Frame latency with at most `ahead` frames submitted and not yet blended -- the reference's
+    swap-chain bound (RenderLatency = 2, Graphics/DX12.h:21): before submitting frame f the host waits for
+    frame f-ahead's blend.  Per frame: host submit time -> GPU completion of the event after its blend on
+    the caller's stream, both on the host clock (GPU event times are anchored at a reference event recorded
+    on the idle GPU at a known host time; `anchor_us` bounds that anchor's own launch delay).  Returns p50 /
+    p99 / max latency and the paced pass's ms per frame."""
+    torch.cuda.synchronize()
+    ref = torch.cuda.Event(enable_timing=True)
+    h0 = time.perf_counter()
+    ref.record(stream)
+    ref.synchronize()
+    anchor_us = (time.perf_counter() - h0) * 1e6
+    subs, done = [], []
+    for f in range(frames):
+        if f >= ahead:
+            done[f - ahead].synchronize()
+        subs.append(time.perf_counter())
+        render(f)
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream)
+        done.append(e)
+    torch.cuda.synchronize()
+    end = [h0 + ref.elapsed_time(e) * 1e-3 for e in done]
+    lat = [(t - h) * 1e3 for t, h in zip(end, subs)]
+    return {"frames_in_flight_cap": ahead, "p50_ms": round(percentile(lat, 50), 4), "p99_ms": round(percentile(lat, 99), 4),
+            "max_ms": round(max(lat), 4), "ms_per_frame": round((end[-1] - subs[0]) * 1e3 / frames, 4),
+            "frames": frames, "anchor_us": round(anchor_us, 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -200,6 +234,9 @@ def main():
     ap.add_argument("--gather", default="native", choices=["native", "torch"],
                     help="N-GPU frame-end gather: the C ABI's RCCL send/recv + un-permute kernel (default) or "
                          "torch.distributed.gather + index_select")
+    ap.add_argument("--phase-timeout", type=float, default=300.0,
+                    help="seconds any one phase (setup, a collective, the timed frames) may take on a rank before "
+                         "every rank is ended with a JSON error line")
     args = ap.parse_args()
     global SCENE, WIDTH, HEIGHT, PATH_LENGTH
     SCENE, WIDTH, HEIGHT, PATH_LENGTH = CONFIGS[args.config]
@@ -208,71 +245,88 @@ def main():
 
     import torch
     import torch.distributed as dist
-    import dxrpathtracer_amd as D
-    import dxrpathtracer_amd._abi as A
-    from dxrpathtracer_amd.distributed import NativeGather, PipelinedGather, screen_layout, source_index
-    from dxrpathtracer_amd.tracer import DXRPathTracer
+    from dxrpathtracer_amd.watchdog import Watchdog, default_store
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    # every rank ends non-zero with a JSON error line on any failure or stuck collective (watchdog.py); the
+    # rendezvous store carries the abort to the other ranks
+    wd = Watchdog(rank, world, None, metric)
+    try:
+        with wd.phase("init", args.phase_timeout):
+            torch.cuda.set_device(local_rank)
+            if world > 1:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+                wd.store = default_store()
+        run(args, metric, world, rank, local_rank, wd)
+    except BaseException as e:  # noqa: BLE001 -- any failure ends every rank (SystemExit from argparse aside)
+        import traceback
+        traceback.print_exc()
+        wd.fail(f"{type(e).__name__}: {e}")
+    wd.close()
+
+
+def run(args, metric, world, rank, local_rank, wd):
+    import torch
+    import torch.distributed as dist
+    import dxrpathtracer_amd as D
+    import dxrpathtracer_amd._abi as A
+    from dxrpathtracer_amd.distributed import NativeGather, PipelinedGather, screen_layout, source_index
+    from dxrpathtracer_amd.tracer import DXRPathTracer
+
+    T = args.phase_timeout
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
 
     # ---- scene + acceleration structure (untimed, like the reference's InitializeScene + AS build)
-    t0 = time.perf_counter()
-    scene = D.Scene(SCENE)
-    settings = scene.settings(MaxPathLength=PATH_LENGTH)
-    sky = D.make_sky(settings)
-    tracer = DXRPathTracer(local_rank)
-    tracer.initialize_scene(scene, sky)
-    bvh = tracer.build_rt_acceleration_structure()
-    setup_s = time.perf_counter() - t0
-    lights = D.make_lights(scene)
-    lay = screen_layout(WIDTH, HEIGHT, world, args.layout)
-    tiles = lay.tile_array(rank) if world > 1 else None
-    n_local = lay.counts[rank] if world > 1 else WIDTH * HEIGHT
-    accum = torch.zeros((max(lay.max_count, n_local), 4), dtype=torch.float32, device="cuda")
-    full = idx = None
-    if world > 1 and rank == 0:
-        full = torch.zeros((WIDTH * HEIGHT, 4), dtype=torch.float32, device="cuda")
-        if args.gather == "torch":
-            idx = torch.tensor(source_index(lay), dtype=torch.long, device="cuda")
-    consts = [D.make_constants(scene, settings, sky, WIDTH, HEIGHT, s) for s in range(16)]
+    with wd.phase("setup", T):
+        t0 = time.perf_counter()
+        scene = D.Scene(SCENE)
+        settings = scene.settings(MaxPathLength=PATH_LENGTH)
+        sky = D.make_sky(settings)
+        tracer = DXRPathTracer(local_rank)
+        tracer.initialize_scene(scene, sky)
+        bvh = tracer.build_rt_acceleration_structure()
+        setup_s = time.perf_counter() - t0
+        lights = D.make_lights(scene)
+        lay = screen_layout(WIDTH, HEIGHT, world, args.layout)
+        tiles = lay.tile_array(rank) if world > 1 else None
+        n_local = lay.counts[rank] if world > 1 else WIDTH * HEIGHT
+        accum = torch.zeros((max(lay.max_count, n_local), 4), dtype=torch.float32, device="cuda")
+        full = idx = None
+        if world > 1 and rank == 0:
+            full = torch.zeros((WIDTH * HEIGHT, 4), dtype=torch.float32, device="cuda")
+            if args.gather == "torch":
+                idx = torch.tensor(source_index(lay), dtype=torch.long, device="cuda")
+        consts = [D.make_constants(scene, settings, sky, WIDTH, HEIGHT, s) for s in range(16)]
 
     # frame-end gather of the band slabs to rank 0 (RCCL), overlapped with the next frame's render
     pg = None
     gather_used = None
     if world > 1:
-        gather_used = args.gather
-        if args.gather == "native":
-            try:
-                pg = NativeGather(lay, rank, local_rank, full, timing=True)
-            except RuntimeError as e:  # e.g. an RCCL communicator that cannot be built on this node
-                # every rank takes the same branch (NativeGather's checks and results are all-gathered)
-                log(f"native gather unavailable ({e}); falling back to torch.distributed.gather")
-                gather_used = f"torch (native failed: {e})"
-        if pg is None:
-            if idx is None and rank == 0:
-                idx = torch.tensor(source_index(lay), dtype=torch.long, device="cuda")
-            pg = PipelinedGather(lay, rank, full, idx)
+        with wd.phase("communicator", T):
+            gather_used = args.gather
+            if args.gather == "native":
+                try:
+                    pg = NativeGather(lay, rank, local_rank, full, timing=True)
+                except RuntimeError as e:  # e.g. an RCCL communicator that cannot be built on this node
+                    # every rank takes the same branch (NativeGather's checks and results are all-gathered)
+                    log(f"native gather unavailable ({e}); falling back to torch.distributed.gather")
+                    gather_used = f"torch (native failed: {e})"
+            if pg is None:
+                if idx is None and rank == 0:
+                    idx = torch.tensor(source_index(lay), dtype=torch.long, device="cuda")
+                pg = PipelinedGather(lay, rank, full, idx)
 
-    render_ev = []
-
-    def frame(f, record=False):
-        if record:
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(stream)
+    def render(f):
         tracer.render_raw(consts[f % 16], settings, accum.data_ptr(), WIDTH, HEIGHT, tiles=tiles, stream=sh,
                           lights=lights)
-        if record:
-            b.record(stream)
-            render_ev.append((a, b))
+
+    def frame(f):
+        render(f)
         if pg is not None:
             pg.submit(accum)
 
@@ -280,118 +334,146 @@ def main():
         if pg is not None:
             pg.flush()
 
-    # ---- traversal work census (instrumented kernels, untimed): nodes / triangles per ray, split by the
-    # kernel that traces them (depth 1: the split schedule's head; deeper: its tails).  The census runs the
-    # counting instantiations of the schedule the timed frames run (r05: k_path_head / k_path_tail with
-    # kCount on depth-split frames -- the same traversal orders; the single k_path's census walks the
-    # order of the register budget it stands for), asserted below against the timed schedule.
-    tracer.set_option(A.OPT_COUNT_TRAVERSAL, 1)
-    frame(0)
-    flush()
-    census = tracer.stats()
-    tracer.set_option(A.OPT_COUNT_TRAVERSAL, 0)
+    with wd.phase("census + per-launch timing", T):
+        # ---- traversal work census (instrumented kernels, untimed): nodes / triangles per ray, split by the
+        # kernel that traces them (depth 1: the split schedule's head; deeper: its tails).  The census runs
+        # the counting instantiations of the schedule the timed frames run (k_path_head / k_path_tail with
+        # kCount on depth-split frames; the single k_path's census walks the order of the register budget it
+        # stands for), asserted below against the timed schedule.
+        tracer.set_option(A.OPT_COUNT_TRAVERSAL, 1)
+        frame(0)
+        flush()
+        census = tracer.stats()
+        tracer.set_option(A.OPT_COUNT_TRAVERSAL, 0)
 
-    # ---- per-launch kernel durations (untimed pass): the shipped kernels one frame at a time
-    # (DXRPT_OPT_FRAME_OVERLAP 0), so each launch's HIP-event span is the launch alone -- with overlapped
-    # frames a launch shares the GPU with the neighbour frame for part of its span.  The events are on the
-    # stream the kernels run on (the render stream when frames do not overlap).  The pass pins the timed
-    # frames' schedule (split or single k_path, register budgets, wave order), which the by-size defaults
-    # would otherwise pick differently without overlap.
-    for f in range(3):
-        frame(f)
-    flush()
-    torch.cuda.synchronize()
-    timed = tracer.stats()
-    # the census priced the timed kernels: the same split / single-kernel schedule and, for the single
-    # k_path, the same traversal-order class (nearest-first closest hits at <= 5 waves/SIMD)
-    assert census.schedule & A.SCHED_CENSUS, census.schedule
-    assert bool(census.schedule & A.SCHED_SPLIT) == bool(timed.schedule & A.SCHED_SPLIT), (census.schedule, timed.schedule)
-    if not timed.schedule & A.SCHED_SPLIT:
-        assert (census.occupancy <= 5) == (timed.occupancy <= 5), (census.occupancy, timed.occupancy)
-    pinned = {A.OPT_MEGAKERNEL_SPLIT: 1 if timed.schedule & A.SCHED_SPLIT else 0,
-              A.OPT_MEGAKERNEL_OCCUPANCY: int(timed.occupancy),
-              A.OPT_TAIL_OCCUPANCY: int(timed.tail_occupancy) if timed.schedule & A.SCHED_SPLIT else 0,
-              A.OPT_WAVE_ORDER: 1 if timed.schedule & A.SCHED_ORDER_KERNEL else 0}
-    for o, v in pinned.items():
-        tracer.set_option(o, v)
-    tracer.set_option(A.OPT_FRAME_OVERLAP, 0)
-    for f in range(3):
-        frame(f)
-    flush()
-    torch.cuda.synchronize()
-    tracer.set_option(A.OPT_KERNEL_TIMING_MASK, (1 << A.K_COUNT) - 1)
-    tracer.set_option(A.OPT_KERNEL_TIMING, 1)
-    tracer.reset_timing()
-    for f in range(min(args.steps, 32)):
-        frame(f)
-    flush()
-    torch.cuda.synchronize()
-    launches = tracer.stats()
-    tracer.set_option(A.OPT_KERNEL_TIMING, 0)
-    same = ~(A.SCHED_OVERLAP | A.SCHED_COST_ORDERED)
-    assert launches.schedule & same == timed.schedule & same, (launches.schedule, timed.schedule)
-    tracer.set_option(A.OPT_FRAME_OVERLAP, A.DEFAULT_FRAME_OVERLAP)
-    for o, v in ((A.OPT_MEGAKERNEL_SPLIT, A.DEFAULT_MEGAKERNEL_SPLIT), (A.OPT_MEGAKERNEL_OCCUPANCY, A.DEFAULT_MEGAKERNEL_OCCUPANCY),
-                 (A.OPT_TAIL_OCCUPANCY, A.DEFAULT_TAIL_OCCUPANCY), (A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)):
-        tracer.set_option(o, v)
-    per_launch = {A.KERNEL_NAMES[k]: {"avg_ms": launches.kernel_ms[k] / launches.kernel_launches[k],
-                                      "launches_per_frame": launches.kernel_launches[k] / max(1, launches.timed_frames)}
-                  for k in range(A.K_COUNT) if launches.kernel_launches[k]}
-    frame_at_a_time_ms = launches.frame_ms / max(1, launches.timed_frames)
+        # ---- per-launch kernel durations (untimed pass): the shipped kernels one frame at a time
+        # (DXRPT_OPT_FRAME_OVERLAP 0), so each launch's HIP-event span is the launch alone -- with overlapped
+        # frames a launch shares the GPU with the neighbour frames for part of its span.  The events are on
+        # the stream the kernels run on (the render stream when frames do not overlap).  The pass pins the
+        # timed frames' schedule (split or single k_path, register budgets, wave order), which the by-size
+        # defaults would otherwise pick differently without overlap.
+        for f in range(3):
+            frame(f)
+        flush()
+        torch.cuda.synchronize()
+        timed = tracer.stats()
+        assert census.schedule & A.SCHED_CENSUS, census.schedule
+        assert bool(census.schedule & A.SCHED_SPLIT) == bool(timed.schedule & A.SCHED_SPLIT), (census.schedule, timed.schedule)
+        if not timed.schedule & A.SCHED_SPLIT:
+            assert (census.occupancy <= 5) == (timed.occupancy <= 5), (census.occupancy, timed.occupancy)
+        pinned = {A.OPT_MEGAKERNEL_SPLIT: 1 if timed.schedule & A.SCHED_SPLIT else 0,
+                  A.OPT_MEGAKERNEL_OCCUPANCY: int(timed.occupancy),
+                  A.OPT_TAIL_OCCUPANCY: int(timed.tail_occupancy) if timed.schedule & A.SCHED_SPLIT else 0,
+                  A.OPT_WAVE_ORDER: 1 if timed.schedule & A.SCHED_ORDER_KERNEL else 0}
+        for o, v in pinned.items():
+            tracer.set_option(o, v)
+        tracer.set_option(A.OPT_FRAME_OVERLAP, 0)
+        for f in range(3):
+            frame(f)
+        flush()
+        torch.cuda.synchronize()
+        tracer.set_option(A.OPT_KERNEL_TIMING_MASK, (1 << A.K_COUNT) - 1)
+        tracer.set_option(A.OPT_KERNEL_TIMING, 1)
+        tracer.reset_timing()
+        for f in range(min(args.steps, 32)):
+            frame(f)
+        flush()
+        torch.cuda.synchronize()
+        launches = tracer.stats()
+        tracer.set_option(A.OPT_KERNEL_TIMING, 0)
+        same = ~(A.SCHED_OVERLAP | A.SCHED_COST_ORDERED)
+        assert launches.schedule & same == timed.schedule & same, (launches.schedule, timed.schedule)
+        tracer.set_option(A.OPT_FRAME_OVERLAP, A.DEFAULT_FRAME_OVERLAP)
+        for o, v in ((A.OPT_MEGAKERNEL_SPLIT, A.DEFAULT_MEGAKERNEL_SPLIT), (A.OPT_MEGAKERNEL_OCCUPANCY, A.DEFAULT_MEGAKERNEL_OCCUPANCY),
+                     (A.OPT_TAIL_OCCUPANCY, A.DEFAULT_TAIL_OCCUPANCY), (A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)):
+            tracer.set_option(o, v)
+        per_launch = {A.KERNEL_NAMES[k]: {"avg_ms": launches.kernel_ms[k] / launches.kernel_launches[k],
+                                          "launches_per_frame": launches.kernel_launches[k] / max(1, launches.timed_frames)}
+                      for k in range(A.K_COUNT) if launches.kernel_launches[k]}
+        frame_at_a_time_ms = launches.frame_ms / max(1, launches.timed_frames)
 
-    for f in range(args.warmup):
-        frame(f)
-    flush()
-    torch.cuda.synchronize()
+    with wd.phase("warmup + render-only throughput", T):
+        for f in range(args.warmup):
+            frame(f)
+        flush()
+        torch.cuda.synchronize()
+        # this rank's own steady-state render throughput (no gather, no barrier): K back-to-back frames of
+        # the shipped schedule, elapsed / K -- a throughput interval, not a per-frame event span (with frames
+        # in flight a span on the render stream measures waits and the blend, not the frame)
+        t_r = time.perf_counter()
+        for f in range(args.steps):
+            render(args.warmup + f)
+        torch.cuda.synchronize()
+        render_only_ms = (time.perf_counter() - t_r) / args.steps * 1e3
 
     # ---- timed region: the shipped defaults (overlapped frames); per-frame events on the render stream
-    if hasattr(pg, "reset_times"):
-        pg.reset_times()
-    render_ev.clear()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    for f in range(args.steps):
-        ev[f][0].record(stream)
-        frame(args.warmup + f, record=True)
-        ev[f][1].record(stream)
-    flush()  # the last frame's gather + un-permute are inside the timed region
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
+    with wd.phase("timed frames", T):
+        if hasattr(pg, "reset_times"):
+            pg.reset_times()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t_start = time.perf_counter()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        for f in range(args.steps):
+            ev[f][0].record(stream)
+            frame(args.warmup + f)
+            ev[f][1].record(stream)
+        flush()  # the last frame's gather + un-permute are inside the timed region
+        torch.cuda.synchronize()
+        local_elapsed = time.perf_counter() - t_start  # this rank, before the closing barrier
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t_start
     stats = tracer.stats()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
-    frame_ms = np.array([a.elapsed_time(b) for a, b in ev])  # per frame on the render stream (incl. the gather's)
-    render_ms = float(np.median([a.elapsed_time(b) for a, b in render_ev]))  # this rank's dxrpt_render per frame
-    nominal_per_frame = WIDTH * HEIGHT * (1 + 2 * (PATH_LENGTH - 1))
-    ms_per_step = elapsed / args.steps * 1e3
-    value = nominal_per_frame * args.steps / elapsed / 1e6
+    with wd.phase("frame latency", T):
+        # paced passes (untimed for the headline): the reference's two frames of latency, and three (the
+        # library's frames in flight)
+        latency = [paced_latency(torch, stream, render, 48, ahead) for ahead in (2, 3)]
+        # a progressive viewer's reset -> first image on an otherwise idle GPU (one frame, nothing in flight)
+        idle = []
+        for k in range(5):
+            torch.cuda.synchronize()
+            h = time.perf_counter()
+            render(k)
+            torch.cuda.synchronize()
+            idle.append((time.perf_counter() - h) * 1e3)
 
     multi = None
-    if world > 1:
-        ranks_ms = [None] * world
-        dist.all_gather_object(ranks_ms, render_ms)
-        g_ms, u_ms, g_frames = pg.times() if hasattr(pg, "times") else (None, None, 0)
-        multi = {"render_ms_per_rank": [round(v, 4) for v in ranks_ms], "render_ms_max": round(max(ranks_ms), 4),
-                 "render_ms_min": round(min(ranks_ms), 4),
-                 "gather": gather_used,
-                 "gather_ms": None if g_ms is None else round(g_ms, 4),
-                 "unpermute_ms": None if u_ms is None else round(u_ms, 4),
-                 "gather_frames_timed": g_frames,
-                 "rccl_ranks": getattr(pg, "comm_ranks", None),
-                 # the part of the frame time the gather adds beyond the slowest rank's render (the gather of
-                 # frame f runs while frame f+1 renders; the last frame's is inside the timed region)
-                 "gather_exposed_ms": round(ms_per_step - max(ranks_ms), 4),
-                 "gather_what": "dxrpt_gather_slabs (grouped ncclSend/ncclRecv of every rank's slab to rank 0) "
-                                "timed with events on the render stream, dxrpt_unpermute on rank 0's render stream; "
-                                "per-rank render ms = median events around dxrpt_render on each rank's stream"}
+    with wd.phase("collect", T):
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        frame_ms = np.array([a.elapsed_time(b) for a, b in ev])  # per frame on the render stream (incl. the gather's)
+        nominal_per_frame = WIDTH * HEIGHT * (1 + 2 * (PATH_LENGTH - 1))
+        ms_per_step = elapsed / args.steps * 1e3
+        value = nominal_per_frame * args.steps / elapsed / 1e6
+        if world > 1:
+            per_rank = [None] * world
+            dist.all_gather_object(per_rank, (render_only_ms, local_elapsed / args.steps * 1e3, n_local))
+            g_ms, u_ms, g_frames = pg.times() if hasattr(pg, "times") else (None, None, 0)
+            render_max = max(v[0] for v in per_rank)
+            multi = {"render_ms_per_rank": [round(v[0], 4) for v in per_rank], "render_ms_max": round(render_max, 4),
+                     "render_ms_min": round(min(v[0] for v in per_rank), 4),
+                     "render_what": "each rank's steady-state render throughput interval: elapsed / K over K "
+                                    "back-to-back frames of its share, no gather, no barrier (bench.py run)",
+                     "timed_ms_per_rank": [round(v[1], 4) for v in per_rank],
+                     "timed_what": "each rank's own elapsed / K of the timed frames (with its gathers), before the "
+                                   "closing barrier",
+                     "share_pixels_per_rank": [int(v[2]) for v in per_rank],
+                     "gather": gather_used,
+                     "gather_ms": None if g_ms is None else round(g_ms, 4),
+                     "unpermute_ms": None if u_ms is None else round(u_ms, 4),
+                     "gather_frames_timed": g_frames,
+                     "rccl_ranks": getattr(pg, "comm_ranks", None),
+                     "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "runtime default (4)"),
+                     # the part of the job's frame interval the gather adds beyond the slowest rank's own
+                     # render throughput (difference of throughput intervals)
+                     "gather_exposed_ms": round(ms_per_step - render_max, 4),
+                     "gather_how": "dxrpt_gather_slabs (grouped ncclSend/ncclRecv of every rank's slab to rank 0) "
+                                   "timed with events on the render stream, dxrpt_unpermute on rank 0's render stream"}
 
     # ---- roofline of the dominant kernel, per launch (SURVEY.md 8(d) bytes / the launch's own duration)
     parts = census_parts(census, n_local, PATH_LENGTH)
@@ -427,7 +509,16 @@ def main():
     # what limits the kernel, from its counters: waves parked on s_waitcnt for much of their cycles with
     # HBM far from its peak = latency of dependent loads (the roofline is still priced against HBM)
     limiter = "latency" if (wait_frac is not None and wait_frac > 0.3 and achieved < 0.6 * HBM_PEAK_GBS) else "hbm"
-    frame_interval_ms = float(np.median(frame_ms))
+    # the shipped throughput rate: this rank's frame bytes over the job's frame interval (elapsed / K, a
+    # throughput interval -- never a median of event spans, which with frames in flight bunch around the
+    # blends); cross-checked against the mean of the render-stream frame spans
+    fi_ms = ms_per_step
+    fi_gbs = frame_bytes / (fi_ms * 1e-3) / 1e9
+    span_mean = float(frame_ms.mean())
+    fi_consistent = abs(span_mean - fi_ms) <= 0.05 * fi_ms
+    assert fi_gbs <= HBM_PEAK_GBS, f"frame-interval rate {fi_gbs:.0f} GB/s above the HBM peak: a timing error"
+    if not fi_consistent:
+        log(f"warning: mean frame span {span_mean:.4f} ms vs frame interval {fi_ms:.4f} ms (> 5 % apart)")
 
     def r4(v):
         return round(v, 4) if isinstance(v, float) else v
@@ -436,7 +527,8 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(scene, sky, settings, args.cpu_threads)
+            with wd.phase("cpu baseline", max(T, 600.0)):
+                cpu = cpu_baseline(scene, sky, settings, args.cpu_threads)
         result = {
             "metric": metric,
             "value": round(value, 2),
@@ -476,11 +568,13 @@ def main():
                          "wait_any_per_wave_cycle": wait_frac,
                          "valu_lane_utilisation": d.get("valu_lane_utilisation"),
                          "per_kernel": {k: {kk: r4(vv) for kk, vv in e.items()} for k, e in kern.items()},
-                         # the shipped throughput rate: the whole frame's bytes over the overlapped frame
-                         # interval (two frames in flight: not a launch duration)
-                         "frame_interval": {"bytes": int(frame_bytes), "ms": round(frame_interval_ms, 4),
-                                            "achieved": round(frame_bytes / (frame_interval_ms * 1e-3) / 1e9, 1),
-                                            "frac": round(frame_bytes / (frame_interval_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         # the shipped throughput rate: the frame's bytes over the job's frame interval
+                         # (elapsed / K with up to three frames in flight: not a launch duration)
+                         "frame_interval": {"bytes": int(frame_bytes), "ms": round(fi_ms, 4),
+                                            "what": "elapsed / steps of the timed region (ms_per_step)",
+                                            "achieved": round(fi_gbs, 1), "frac": round(fi_gbs / HBM_PEAK_GBS, 4),
+                                            "mean_frame_span_ms": round(span_mean, 4),
+                                            "consistent_within_5pct": bool(fi_consistent),
                                             "frame_at_a_time_ms": round(frame_at_a_time_ms, 4)}},
             "cpu_baseline": cpu,
             # the headline counts the reference's HUD rays (W*H*(1+2(L-1)) per frame); the kernels skip
@@ -497,13 +591,20 @@ def main():
                 "frame_at_a_time_schedule_bits": int(launches.schedule),
                 "occupancy": {"head_or_path": int(stats.occupancy), "tail": int(stats.tail_occupancy)},
                 "algorithmic_bytes": {k: v[1] for k, v in part_bytes.items()},
-                "frame_ms": {"mean": round(float(frame_ms.mean()), 4), "median": round(float(np.median(frame_ms)), 4),
-                             "max": round(float(frame_ms.max()), 4)},
-                "render_ms_median": round(render_ms, 4),
+                # per-frame event spans on the render stream: with frames in flight they measure the waits for
+                # the slot streams and the blend, so they bunch (median << mean); only the mean is a rate
+                "frame_span_ms": {"mean": round(span_mean, 4), "median": round(float(np.median(frame_ms)), 4),
+                                  "max": round(float(frame_ms.max()), 4)},
+                "render_only_ms_per_frame": round(render_only_ms, 4),
+                # submit -> blended latency (the reference bounds it at RenderLatency = 2 frames,
+                # Graphics/DX12.h:21); unpaced submission has no bounded latency (the host runs ahead)
+                "frame_latency": {"paced": latency,
+                                  "idle_gpu_one_frame_ms": {"median": round(float(np.median(idle)), 4),
+                                                            "max": round(float(max(idle)), 4)}},
                 "census": {"what": "node / triangle-record fetches of the timed schedule (per lane in per-lane "
                                    "traversals, per wave in packet traversals), one instrumented frame of the "
                                    "timed kernels' counting instantiations",
-                           "kernels": ("k_path_head<5,count> + k_path_tail<7,count>" if census.schedule & A.SCHED_SPLIT
+                           "kernels": ("k_path_head<count> + k_path_tail<7,count>" if census.schedule & A.SCHED_SPLIT
                                        else f"k_path<{5 if census.occupancy <= 5 else 7},count>"),
                            "schedule_bits": int(census.schedule),
                            "node_fetches_radiance": int(census.node_visits_radiance),
@@ -534,12 +635,13 @@ def main():
             },
         }
         print(json.dumps(result), flush=True)
-    if world > 1:
-        if hasattr(pg, "close"):
-            pg.close()
-        dist.barrier()
-        dist.destroy_process_group()
-    tracer.close()
+    with wd.phase("teardown", T):
+        if world > 1:
+            if hasattr(pg, "close"):
+                pg.close()
+            dist.barrier()
+            dist.destroy_process_group()
+        tracer.close()
 
 
 if __name__ == "__main__":

@@ -151,6 +151,8 @@ class BvhInfo(C.Structure):
 
 BVH_PHASES = ("sbvh", "treelet", "collapse", "records_upload")  # dxrpt_bvh_info.phase_ms
 PHASE_CLOCKS = 24  # dxrpt_get_phase_clocks: [0:8] k_path, [8:16] k_path_head, [16:24] k_path_tail
+DEBUG_WORDS = 8  # dxrpt_get_debug_record (DXRPT_DEBUG builds)
+DEBUG_QUEUE_POS, DEBUG_TMAX, DEBUG_ACCUM_INDEX, DEBUG_PIXEL = 1, 2, 3, 4
 
 
 class HostTexture(C.Structure):
@@ -182,7 +184,7 @@ DXRPT_SYMBOLS = ("dxrpt_abi_version", "dxrpt_default_settings", "dxrpt_create", 
                  "dxrpt_set_scene", "dxrpt_add_texture", "dxrpt_set_sky", "dxrpt_build_bvh", "dxrpt_get_bvh_info",
                  "dxrpt_render", "dxrpt_get_stats", "dxrpt_trace_rays", "dxrpt_set_option", "dxrpt_reset_timing",
                  "dxrpt_post_process", "dxrpt_bake_lightmap", "dxrpt_denoise_median", "dxrpt_get_wave_clocks",
-                 "dxrpt_get_phase_clocks", "dxrpt_sample_cmj", "dxrpt_render_aov", "dxrpt_comm_unique_id", "dxrpt_comm_create",
+                 "dxrpt_get_phase_clocks", "dxrpt_get_debug_record", "dxrpt_sample_cmj", "dxrpt_render_aov", "dxrpt_comm_unique_id", "dxrpt_comm_create",
                  "dxrpt_comm_destroy", "dxrpt_comm_info", "dxrpt_gather_slabs", "dxrpt_unpermute", "dxrpt_multi_last_error",
                  "dxrpt_multi_release", "dxrpt_opacity_micromap")
 DXRPT_HOST_SYMBOLS = ("dxrpt_host_scene_create", "dxrpt_host_scene_load", "dxrpt_host_scene_destroy", "dxrpt_host_last_error",
@@ -231,6 +233,7 @@ def lib() -> C.CDLL:
         L.dxrpt_get_stats.argtypes = [P, C.POINTER(Stats)]
         L.dxrpt_get_wave_clocks.argtypes = [P, C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint32)]
         L.dxrpt_get_phase_clocks.argtypes = [P, C.POINTER(C.c_uint64)]
+        L.dxrpt_get_debug_record.argtypes = [P, C.POINTER(u32)]
         L.dxrpt_trace_rays.argtypes = [P, P, u32, u32, P, P]
         L.dxrpt_post_process.argtypes = [P, C.POINTER(AppSettings), P, u32, u32, P, u32, P]
         L.dxrpt_set_option.argtypes = [P, u32, C.c_uint64]

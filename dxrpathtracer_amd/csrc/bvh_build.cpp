@@ -94,6 +94,32 @@ private:
     bool stop_ = false;
 };
 
+// task(k) for k in [0, K): 1..K-1 on the pool, 0 inline.  Returns only once every task has ended -- also
+// when one throws, since the queued tasks reference the caller's frame -- and then rethrows bad_alloc.
+// Every task the pool runs is wrapped like this (or catches for itself), so no exception leaves
+// TaskPool::wait, which runs other fork-joins' tasks inline.
+template <class F>
+void fork_join(TaskPool& pool, size_t K, F&& task) {
+    std::atomic<size_t> left{K > 1 ? K - 1 : 0};
+    std::atomic<bool> done{K <= 1}, failed{false};
+    for (size_t k = 1; k < K; ++k)
+        pool.submit([&, k] {
+            try {
+                task(k);
+            } catch (...) {
+                failed.store(true);
+            }
+            if (left.fetch_sub(1) == 1) done.store(true, std::memory_order_release);
+        });
+    try {
+        task(size_t(0));
+    } catch (...) {
+        failed.store(true);
+    }
+    pool.wait(done);
+    if (failed.load()) throw std::bad_alloc();
+}
+
 struct Box {
     float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX};
     float hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
@@ -347,20 +373,7 @@ struct SpatialBuilder {
             f(size_t(0), size_t(0), n);
             return 1;
         }
-        std::atomic<size_t> left{K - 1};
-        std::atomic<bool> done{false}, failed{false};
-        for (size_t k = 1; k < K; ++k)
-            pool->submit([&, k] {
-                try {
-                    f(k, n * k / K, n * (k + 1) / K);
-                } catch (...) {
-                    failed.store(true);
-                }
-                if (left.fetch_sub(1) == 1) done.store(true, std::memory_order_release);
-            });
-        f(size_t(0), size_t(0), n / K);
-        pool->wait(done);
-        if (failed.load()) throw std::bad_alloc();
+        fork_join(*pool, K, [&](size_t k) { f(k, n * k / K, n * (k + 1) / K); });
         return K;
     }
 
@@ -758,7 +771,12 @@ struct SpatialBuilder {
                 }
                 done.store(true, std::memory_order_release);
             });
-            c0 = build_rec(out, L, lb, depth + 1, bl);
+            try {
+                c0 = build_rec(out, L, lb, depth + 1, bl);
+            } catch (...) {  // the task references R, rb and done on this frame: let it end first
+                pool->wait(done);
+                throw;
+            }
             pool->wait(done);
         } else {
             c0 = build_rec(out, L, lb, depth + 1, bl);
@@ -787,9 +805,10 @@ struct SpatialBuilder {
         if (deep || oom) return;
         tree.resize(nn);
         refs.resize(nr);
-        std::atomic<size_t> cursor{0}, left{subs.size()};
-        std::atomic<bool> done{false};
-        auto worker = [&] {
+        // every worker returns before this frame ends (fork_join): a worker the pool starts late still reads
+        // `cursor`
+        std::atomic<size_t> cursor{0};
+        fork_join(tp, threads, [&](size_t) {
             for (size_t i; (i = cursor.fetch_add(1)) < subs.size();) {
                 const Sub& x = *subs[i];
                 for (size_t j = 0; j < x.nodes.size(); ++j) {
@@ -802,12 +821,8 @@ struct SpatialBuilder {
                     tree[x.node_off + j] = t;
                 }
                 std::copy(x.refs.begin(), x.refs.end(), refs.begin() + std::ptrdiff_t(x.ref_off));
-                if (left.fetch_sub(1) == 1) done.store(true, std::memory_order_release);
             }
-        };
-        for (unsigned t = 1; t < threads; ++t) tp.submit(worker);
-        worker();
-        tp.wait(done);
+        });
     }
 
     bool build(uint32_t ntris, const std::vector<Box>& tri_box, std::string& err) {
@@ -976,15 +991,9 @@ void parallel_range(TaskPool& pool, unsigned threads, size_t b, size_t e, F&& f)
         for (size_t i = b; i < e; ++i) f(i);
         return;
     }
-    std::atomic<size_t> left{K - 1};
-    std::atomic<bool> done{false};
-    for (size_t k = 1; k < K; ++k)
-        pool.submit([&, k] {
-            for (size_t i = b + n * k / K; i < b + n * (k + 1) / K; ++i) f(i);
-            if (left.fetch_sub(1) == 1) done.store(true, std::memory_order_release);
-        });
-    for (size_t i = b; i < b + n / K; ++i) f(i);
-    pool.wait(done);
+    fork_join(pool, K, [&](size_t k) {
+        for (size_t i = b + n * k / K; i < b + n * (k + 1) / K; ++i) f(i);
+    });
 }
 
 // Leaves, references and node slots are kept; only the topology of internal nodes changes, so the tree is not
@@ -1044,20 +1053,14 @@ void restructure_treelets(std::vector<TNode>& tree, const std::vector<uint32_t>&
             for (size_t i = level_end[kCut - 1]; i < level_end[kCut]; ++i)
                 if (!tree[size_t(bfs[i])].count) roots.push_back(bfs[i]);
         std::atomic<size_t> cursor{0};
-        std::atomic<size_t> left{roots.size()};
-        std::atomic<bool> done{roots.empty()};
-        auto worker = [&] {
+        fork_join(pool, roots.empty() ? 1 : hw, [&](size_t) {
             std::vector<int32_t> order;
             for (size_t k; (k = cursor.fetch_add(1)) < roots.size();) {
                 post_order(roots[k], order);
                 for (int32_t n : order)
                     if (!fixed[size_t(n)]) restructure_treelet(tree, cost, n);
-                if (left.fetch_sub(1) == 1) done.store(true, std::memory_order_release);
             }
-        };
-        for (unsigned t = 1; t < hw; ++t) pool.submit(worker);
-        worker();
-        pool.wait(done);
+        });
         for (size_t l = std::min(kCut, level_end.size()); l-- > 0;)
             for (size_t i = l ? level_end[l - 1] : 0; i < level_end[l]; ++i) {
                 const int32_t n = bfs[i];
@@ -1374,16 +1377,10 @@ struct Emit8 {
             if (K <= 1) {
                 for (size_t i = 0; i < level.size(); ++i) plan(level[i].t, plans[i]);
             } else {
-                std::atomic<size_t> left{K - 1};
-                std::atomic<bool> done{false};
                 const size_t n = level.size();
-                for (size_t k = 1; k < K; ++k)
-                    pool.submit([&, k] {
-                        for (size_t i = n * k / K; i < n * (k + 1) / K; ++i) plan(level[i].t, plans[i]);
-                        if (left.fetch_sub(1) == 1) done.store(true, std::memory_order_release);
-                    });
-                for (size_t i = 0; i < n / K; ++i) plan(level[i].t, plans[i]);
-                pool.wait(done);
+                fork_join(pool, K, [&](size_t k) {
+                    for (size_t i = n * k / K; i < n * (k + 1) / K; ++i) plan(level[i].t, plans[i]);
+                });
             }
             next.clear();
             for (size_t i = 0; i < level.size(); ++i) {

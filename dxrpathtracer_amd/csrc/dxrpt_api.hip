@@ -85,6 +85,7 @@ constexpr uint64_t kSplitMinVerticesOverlap3 = 1500000;  // three
 #define DXRPT_OVERLAP_SLOTS 3
 #endif
 constexpr uint32_t kOverlapSlots = DXRPT_OVERLAP_SLOTS;
+static_assert(kOverlapSlots >= 3 && kOverlapSlots < 32, "DXRPT_OPT_FRAME_OVERLAP 2 needs three slots; the gate mask is 32 bits");
 constexpr uint32_t kOverlapBySize = 3;  // DXRPT_OPT_FRAME_OVERLAP value: frames in flight by frame size
 // BVH8 stack-spill slabs: 0 = work on the caller's stream, 1 + k = overlap slot k
 constexpr uint32_t kSpillSlabs = 1 + kOverlapSlots;
@@ -161,8 +162,8 @@ struct dxrpt_ctx {
     Slot slot[kOverlapSlots];
     hipEvent_t ovl_fork = nullptr;  // the first overlapped frame after other work starts behind the caller's stream
     bool ovl_active = false;        // the slot streams run overlapped frames (no fork needed)
-    hipEvent_t ovl_gate = nullptr;  // the next overlapped frame waits for it (a rebuilt wave order)
-    bool ovl_gate_set = false;
+    hipEvent_t ovl_gate = nullptr;  // frames on the other slots wait for it (a rebuilt wave order)
+    uint32_t ovl_gate_pending = 0;  // bit k: slot k's next frame has not yet waited on ovl_gate
     uint32_t ovl_parity = 0;
     uint32_t ovl_slots = 0;  // frames in flight of the current rotation (2 or 3)
     std::vector<const uint32_t*> stat_counters;  // counter set of the last frame
@@ -1165,6 +1166,7 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.accum = reinterpret_cast<float4*>(accum);
         fp.num_tiles = uint32_t(ctx->tiles_cache.size());
         fp.num_paths = paths;
+        fp.accum_extent = ctx->accum_extent;
         fp.width = width;
         fp.height = height;
         fp.xcd_chunk = ctx->opt_xcd_chunk;
@@ -1231,11 +1233,14 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
                 HIP_CHECK(hipEventRecord(ctx->ovl_fork, s));
                 HIP_CHECK(hipStreamWaitEvent(fs, ctx->ovl_fork, 0));
                 for (dxrpt_ctx::Slot& Q : ctx->slot) Q.stage_used = false;
-                ctx->ovl_gate_set = false;
+                ctx->ovl_gate_pending = 0;
             }
             if (P.stage_used) HIP_CHECK(hipStreamWaitEvent(fs, P.stage_free, 0));  // the stage's previous blend
-            if (ctx->ovl_gate_set) HIP_CHECK(hipStreamWaitEvent(fs, ctx->ovl_gate, 0));  // the new wave order
-            ctx->ovl_gate_set = false;
+            // the new wave order: every slot's next frame after a rebuild waits for it, not just the next
+            // frame's -- with three in flight frame f+2 runs on a third stream that would otherwise see only
+            // its own slot's stage_free (the blend of frame f-1) and could read the order mid-rewrite
+            if (ctx->ovl_gate_pending & (1u << ov)) HIP_CHECK(hipStreamWaitEvent(fs, ctx->ovl_gate, 0));
+            ctx->ovl_gate_pending &= ~(1u << ov);
         } else {
             ensure_frame(ctx, paths, slots);
         }
@@ -1361,9 +1366,9 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
                                         ctx->d_wave_order.as<uint32_t>(), order_waves, fs));
             ctx->order_ready = true;
             ctx->order_parity ^= 1u;
-            if (overlap) {  // and the next frame reads the new order
+            if (overlap) {  // and the next frame of every other slot reads the new order
                 HIP_CHECK(hipEventRecord(ctx->ovl_gate, fs));
-                ctx->ovl_gate_set = true;
+                ctx->ovl_gate_pending = ((1u << kOverlapSlots) - 1u) & ~(1u << ov);
             }
         }
         if (overlap) {  // the caller's stream blends the stage once the frame is done
@@ -1455,6 +1460,14 @@ int dxrpt_get_phase_clocks(dxrpt_ctx* ctx, uint64_t out[DXRPT_PHASE_CLOCKS]) {
         unsigned long long t[kPhaseClockWords];
         HIP_CHECK(read_phase_ticks(t));
         for (int k = 0; k < kPhaseClockWords; ++k) out[k] = t[k];
+    });
+}
+
+int dxrpt_get_debug_record(dxrpt_ctx* ctx, uint32_t out[DXRPT_DEBUG_WORDS]) {
+    if (!ctx || !out) return DXRPT_E_INVALID_ARG;
+    return guarded(ctx, [&] {
+        static_assert(kDebugWords == DXRPT_DEBUG_WORDS, "include/dxrpt.h DXRPT_DEBUG_WORDS");
+        HIP_CHECK(read_debug_record(out));
     });
 }
 

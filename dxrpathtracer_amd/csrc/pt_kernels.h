@@ -136,6 +136,7 @@ struct FrameParams {
     // stage[accumulation index] instead of blending it into accum; launch_accum_stage blends the frame's
     // paths afterwards.  Null: blend in the kernel.
     float4* stage = nullptr;
+    uint32_t accum_extent = 0;  // 1 + the largest accumulation index of the tiles (DXRPT_DEBUG range checks)
 };
 
 constexpr uint32_t kWaveClasses = 256;
@@ -199,6 +200,10 @@ hipError_t launch_accum_stage(const FrameParams& fp, hipStream_t stream);
 // SampleCMJ2D on device cases (x = sampleIdx, y = numSamplesX, z = numSamplesY, w = pattern) -> out.
 hipError_t launch_sample_cmj(const uint4* cases, uint32_t n, float2* out, hipStream_t stream);
 
+// DXRPT_DEBUG builds: the range-check record since the last call (synchronises the device, zeroes it;
+// dxrpt_get_debug_record); word 7 = 1 in debug builds.
+constexpr int kDebugWords = 8;
+hipError_t read_debug_record(uint32_t out[kDebugWords]);
 // DXRPT_DIAG_PHASES builds: the per-phase lane ticks since the last call (synchronises the device, zeroes them).
 constexpr int kPhaseClockWords = 24;  // [0, 8) k_path, [8, 16) k_path_head, [16, 24) k_path_tail
 hipError_t read_phase_ticks(unsigned long long out[kPhaseClockWords]);

@@ -1324,7 +1324,45 @@ PT_DEV void accumulate_pixel(const KArgs& A, uint32_t a, float4 r) {
 // A finished camera path's radiance: into the accumulation target, or -- frames that overlap their
 // neighbours (DXRPT_OPT_FRAME_OVERLAP) -- into the frame's stage at the same index, blended by
 // k_accum_stage once the previous frame's blend is done (same arithmetic, same order per pixel).
+// DXRPT_DEBUG builds (make variant NAME=debug EXTRA=-DDXRPT_DEBUG=1; dxrpt_get_debug_record): the queued
+// path state every tail lane reads and the stage entry every blend reads are range-checked before use --
+// queue position < qsize, the queued TMax (FP32Max; the direct-mapped depth-2 queue also -1 = ended),
+// accumulation index < the tile list's extent, pixel index < W x H -- the hazard class of the r05 fault
+// (a frame reading another overlapped frame's scratch).  A failing lane counts the violation, the first
+// one is recorded, and the lane does nothing else.  No device trap: a trapping wave ends the process with
+// a queue error, on a shared box; the host reads the record (and tests assert it is empty).
+#ifndef DXRPT_DEBUG
+#define DXRPT_DEBUG 0
+#endif
+// [0] violations, [1] first kind (DXRPT_DEBUG_*), [2] its depth, [3] its lane index, [4] the bad value,
+// [5] its bound, [6] entries checked, [7] reserved (the host sets 1 in debug builds)
+__device__ uint32_t g_debug[kDebugWords];
+PT_DEV bool debug_ok(bool ok, uint32_t kind, int d, uint32_t lane_idx, uint32_t value, uint32_t bound) {
+#if DXRPT_DEBUG
+    if (ok) return true;
+    if (atomicAdd(&g_debug[0], 1u) == 0u) {
+        g_debug[1] = kind;
+        g_debug[2] = uint32_t(d);
+        g_debug[3] = lane_idx;
+        g_debug[4] = value;
+        g_debug[5] = bound;
+    }
+    return false;
+#else
+    (void)ok, (void)kind, (void)d, (void)lane_idx, (void)value, (void)bound;
+    return true;
+#endif
+}
+PT_DEV void debug_count(uint32_t n) {
+#if DXRPT_DEBUG
+    if ((threadIdx.x & 63u) == 0u && n) atomicAdd(&g_debug[6], n);
+#else
+    (void)n;
+#endif
+}
+
 PT_DEV void finish_pixel(const KArgs& A, uint32_t a, float4 r) {
+    if (DXRPT_DEBUG && !debug_ok(a < A.P.accum_extent, DXRPT_DEBUG_ACCUM_INDEX, 0, 0u, a, A.P.accum_extent)) return;
     if (A.P.stage) {
         A.P.stage[a] = r;
         return;
@@ -1336,6 +1374,7 @@ __global__ __launch_bounds__(kBlock) void k_accum_stage(KArgs A) {
     const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
     if (p >= A.P.num_paths) return;
     const uint32_t a = path_pixel(A, p).accumIdx;
+    if (DXRPT_DEBUG && !debug_ok(a < A.P.accum_extent, DXRPT_DEBUG_ACCUM_INDEX, -1, p, a, A.P.accum_extent)) return;
     accumulate_pixel(A, a, A.P.stage[a]);
 }
 
@@ -1881,9 +1920,18 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
     const bool direct = d == 2;  // the head's direct-mapped queue (entry = path slot)
     const uint32_t pos = direct ? i : queue_pos(cnt_q, A.F.cap_r, i);
     const RayQueue& Q = A.F.q[d & 1];
+    if (DXRPT_DEBUG && !debug_ok(pos < A.F.qsize, DXRPT_DEBUG_QUEUE_POS, d, i, pos, A.F.qsize)) return;
     HitRec h;
     {
         const float4 o4 = Q.org[pos], d4 = Q.dir[pos];
+        if (DXRPT_DEBUG) {  // the queued state before it is used (the lane then does nothing else)
+            const bool ended = direct && o4.w == -1.0f;
+            const uint32_t a = fbits(d4.w), px = ended ? 0u : Q.pix[pos];
+            if (!debug_ok(ended || o4.w == kFP32Max, DXRPT_DEBUG_TMAX, d, i, fbits(o4.w), fbits(kFP32Max)) ||
+                !debug_ok(ended || a < A.P.accum_extent, DXRPT_DEBUG_ACCUM_INDEX, d, i, a, A.P.accum_extent) ||
+                !debug_ok(ended || px < A.P.width * A.P.height, DXRPT_DEBUG_PIXEL, d, i, px, A.P.width * A.P.height))
+                return;
+        }
         if (direct && !(o4.w >= 0.0f)) return;  // the path ended at depth 1
         uint32_t nv = 0, nt = 0;
         traverse8<false, kCount, true, true, false>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= set.MaxAnyHitPathLength, h, nv, nt);
@@ -1950,6 +1998,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     const uint32_t j = A.P.xcd_chunk ? xcd_position(blockIdx.x, nw, A.P.xcd_chunk) : blockIdx.x;
     lut_fill<kLast>(A.S);  // the plain copy in the non-last tails (DMA there: C3 +1.8 %, C5 +1.3 %)
     const uint32_t i = j * blockDim.x + threadIdx.x;
+    if (DXRPT_DEBUG) debug_count(n - j * 64u < 64u ? n - j * 64u : 64u);
     if (!kCount) {
 #if DXRPT_DIAG_PHASES
         PhaseAcc pa = phase_start();
@@ -2321,6 +2370,15 @@ hipError_t launch_sample_cmj(const uint4* cases, uint32_t n, float2* out, hipStr
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_sample_cmj, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, stream, cases, n, out);
     return hipGetLastError();
+}
+
+hipError_t read_debug_record(uint32_t out[kDebugWords]) {
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return e;
+    if ((e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_debug), kDebugWords * sizeof(uint32_t))) != hipSuccess) return e;
+    out[7] = DXRPT_DEBUG ? 1u : 0u;
+    const uint32_t zero[kDebugWords] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_debug), zero, sizeof(zero));
 }
 
 hipError_t read_phase_ticks(unsigned long long out[kPhaseClockWords]) {

@@ -233,19 +233,19 @@ class NativeGather:
     share 0.244 -> 0.27-0.35 ms, profiles/r05_ab_overlap_side.txt, r05_ab_overlap_hwq.txt)."""
 
     def __init__(self, layout: BandLayout, rank: int, device: int, full=None, group=None, timing: bool = False,
-                 side_stream: bool = False):
+                 side_stream: bool = False, lib=None):
         import ctypes as C
-        import torch
         import torch.distributed as dist
         self.layout, self.rank, self.full = layout, rank, full
-        self.L = A.lib()
+        # `lib`: the C ABI (libdxrpt.so); the CPU tests pass a stub communicator with the same entry points
+        self.L = lib if lib is not None else A.lib()
         uid = C.create_string_buffer(A.DXRPT_COMM_ID_BYTES)
         # Failures BEFORE ncclCommInitRank are made collective, so every rank raises together (a caller may
         # then fall back to another gather) instead of the others blocking inside the collective init: the
         # ranks first agree that each one's device and arguments are valid, then rank 0 makes the id.  A
         # rank that fails inside ncclCommInitRank itself still leaves the others blocked there (RCCL's
         # blocking init), which no check before it can cover.
-        ready = torch.cuda.is_available() and 0 <= device < torch.cuda.device_count() and 0 <= rank < layout.world
+        ready = self._device_ready(device) and 0 <= rank < layout.world
         flags = [None] * layout.world
         dist.all_gather_object(flags, bool(ready), group=group)
         if not all(flags):
@@ -282,7 +282,7 @@ class NativeGather:
         self.tiles = gathered_tiles(layout)
         self.tarr = (A.Tile * len(self.tiles))(*self.tiles)
         self.total = sum(layout.counts)
-        self.side = torch.cuda.Stream() if side_stream else None
+        self.side = self._new_stream() if side_stream else None
         self.staging = None
         self.recv = None
         self.pending = None
@@ -291,6 +291,27 @@ class NativeGather:
         # (render stream), read by times() once the frames are done
         self.timing = timing
         self.gather_ev, self.unpermute_ev = [], []
+
+    # device seams (the CPU tests' stub subclass replaces these four; the product path is HIP through torch)
+    def _device_ready(self, device):
+        import torch
+        return torch.cuda.is_available() and 0 <= device < torch.cuda.device_count()
+
+    def _new_stream(self):
+        import torch
+        return torch.cuda.Stream()
+
+    def _current_stream(self):
+        import torch
+        return torch.cuda.current_stream()
+
+    def _event(self, timing=False):
+        import torch
+        return torch.cuda.Event(enable_timing=timing)
+
+    def _synchronize(self):
+        import torch
+        torch.cuda.synchronize()
 
     def _msg(self, rc):
         msg = self.L.dxrpt_multi_last_error()
@@ -303,7 +324,7 @@ class NativeGather:
     def submit(self, local):
         import ctypes as C
         import torch
-        cur = torch.cuda.current_stream()
+        cur = self._current_stream()
         n = self.layout.counts[self.rank]
         if self.staging is None:
             self.staging = [torch.empty((n, 4), dtype=torch.float32, device=local.device) for _ in range(2)]
@@ -316,12 +337,12 @@ class NativeGather:
         if self.side is not None:
             self.side.wait_stream(cur)
         if self.timing:
-            g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            g0, g1 = self._event(True), self._event(True)
             g0.record(gs)
         self._check(self.L.dxrpt_gather_slabs(self.comm, C.c_void_p(self.staging[k].data_ptr()), self.counts,
                                               C.c_void_p(self.recv[k].data_ptr()) if self.rank == 0 else None,
                                               C.c_void_p(gs.cuda_stream)), "dxrpt_gather_slabs")
-        ev = torch.cuda.Event()
+        ev = self._event()
         ev.record(gs)
         if self.timing:
             g1.record(gs)
@@ -337,13 +358,12 @@ class NativeGather:
 
     def _finish(self, pend):
         import ctypes as C
-        import torch
         ev, k = pend
-        cur = torch.cuda.current_stream()
+        cur = self._current_stream()
         cur.wait_event(ev)
         if self.rank == 0:
             if self.timing:
-                u0, u1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                u0, u1 = self._event(True), self._event(True)
                 u0.record(cur)
             self._check(self.L.dxrpt_unpermute(C.c_void_p(self.recv[k].data_ptr()), self.tarr, len(self.tiles),
                                                C.c_void_p(self.full.data_ptr()), self.layout.width, self.layout.height,
@@ -366,8 +386,7 @@ class NativeGather:
     def close(self):
         if self.comm:
             self.flush()
-            import torch
-            torch.cuda.synchronize()
+            self._synchronize()
             self._check(self.L.dxrpt_comm_destroy(self.comm), "dxrpt_comm_destroy")
             self.comm = None
             # the un-permute scratch of this thread, released while the HIP runtime is up

@@ -146,6 +146,15 @@ class DXRPathTracer:
                                                       C.byref(n)), "dxrpt_get_wave_clocks")
         return out
 
+    def debug_record(self):
+        """The range-check record since the last call (kernel builds with -DDXRPT_DEBUG=1; zeros and
+        is_debug_build False otherwise), see dxrpt_get_debug_record: a dict of the 8 words."""
+        out = (C.c_uint32 * A.DEBUG_WORDS)()
+        self._check(self._L.dxrpt_get_debug_record(self._ctx, out), "dxrpt_get_debug_record")
+        v = list(out)
+        return {"violations": v[0], "kind": v[1], "depth": v[2] - (1 << 32) if v[2] >= 1 << 31 else v[2],
+                "lane": v[3], "value": v[4], "bound": v[5], "checked": v[6], "is_debug_build": bool(v[7])}
+
     def phase_clocks(self):
         """Lane ticks per camera-path phase since the last call (kernel builds with -DDXRPT_DIAG_PHASES=1;
         zeros otherwise), see dxrpt_get_phase_clocks: 24 values, [0:8] k_path, [8:16] k_path_head, [16:24]

@@ -467,6 +467,20 @@ int dxrpt_get_wave_clocks(dxrpt_ctx* ctx, uint64_t* out, uint32_t max_waves, uin
 #define DXRPT_PHASE_CLOCKS 24
 int dxrpt_get_phase_clocks(dxrpt_ctx* ctx, uint64_t out[DXRPT_PHASE_CLOCKS]);
 
+/* Range-check record of kernel builds made with -DDXRPT_DEBUG=1 (`make variant NAME=debug
+ * EXTRA=-DDXRPT_DEBUG=1`; the shipped build returns zeros with out[7] = 0).  Every queued path state a
+ * depth-split tail reads and every stage entry an overlapped frame's blend reads is checked before use;
+ * a failing lane is counted and does nothing else.  Reads and zeroes the record (synchronises the device):
+ *   out[0] violations, out[1] the first one's kind (DXRPT_DEBUG_*), out[2] its depth (-1 = the blend),
+ *   out[3] its lane index, out[4] the bad value, out[5] its bound, out[6] queue entries checked,
+ *   out[7] 1 in a debug build. */
+#define DXRPT_DEBUG_WORDS 8
+#define DXRPT_DEBUG_QUEUE_POS 1u   /* queue position >= the queue's capacity */
+#define DXRPT_DEBUG_TMAX 2u        /* queued TMax neither FP32Max nor (depth-2 queue) the ended mark -1 */
+#define DXRPT_DEBUG_ACCUM_INDEX 3u /* accumulation index >= the tile list's extent */
+#define DXRPT_DEBUG_PIXEL 4u       /* CMJ pixel index >= width x height */
+int dxrpt_get_debug_record(dxrpt_ctx* ctx, uint32_t out[DXRPT_DEBUG_WORDS]);
+
 /* TraceRay on arbitrary rays against the built acceleration structure (the DXR TraceRay call sites
  * RayTrace.hlsl:138,258,305,407,425 without the shading).  `rays` (device) holds num_rays pairs of
  * float4: (origin.xyz, tmin), (direction.xyz, tmax).  `hits` (device) receives one float4 per ray:

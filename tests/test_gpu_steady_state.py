@@ -161,8 +161,8 @@ def test_c3_1080p_L8_sixteen_samples(torch_cuda):
 def test_overlapped_frames_are_bit_identical(torch_cuda, W, H, L, frames, share):
     # DXRPT_OPT_FRAME_OVERLAP: back-to-back frames (no host sync between them, as bench.py and every rank
     # render them) rotate over two or three sets of internal streams and stage their radiance; the caller's
-    # stream blends each stage in frame order (RayTrace.hlsl:140-148).  (Cost-order rebuilds under overlap:
-    # test_wave_order_is_bit_identical at periods 1 and 2.) 1080p L=3 and L=8 and
+    # stream blends each stage in frame order (RayTrace.hlsl:140-148).  (Cost-order rebuilds with frames in
+    # flight: test_overlapped_order_rebuilds_are_bit_identical.) 1080p L=3 and L=8 and
     # 4K L=6 run the depth-split schedule overlapped against k_path / the split one frame at a time.  The
     # accumulated target must equal the one-frame-at-a-time schedule's bit for bit.
     torch = torch_cuda
@@ -191,6 +191,42 @@ def test_overlapped_frames_are_bit_identical(torch_cuda, W, H, L, frames, share)
             t.close()
     for o in out[1:]:
         np.testing.assert_array_equal(o, out[0])
+
+
+@pytest.mark.parametrize("overlap,period", [(2, 1), (2, 2), (1, 1), (3, 2)])
+def test_overlapped_order_rebuilds_are_bit_identical(torch_cuda, overlap, period):
+    # a cost-order rebuild (launch_wave_order at the end of an ordered frame) must be seen by
+    # the next frame of EVERY slot -- with three frames in flight frame f+2 runs on a third stream.  A 1/8
+    # band share (cost-ordered), rebuilds every 1 or 2 frames, 24 frames back to back with no host sync,
+    # equals the same frames one at a time bit for bit (a torn permutation would run some waves twice and
+    # blend others' stale stage pixels)
+    torch = torch_cuda
+    W, H, L, frames = 1920, 1080, 3, 24
+    sc, sky = scene_bundle("sponza")
+    st = sc.settings(MaxPathLength=L)
+    lights = D.make_lights(sc)
+    lay = band_layout(W, H, 8)
+    tiles, n = lay.tile_array(3), lay.counts[3]
+    consts = [D.make_constants(sc, st, sky, W, H, f % 16) for f in range(frames)]
+    stream = torch.cuda.current_stream().cuda_stream
+    out = []
+    for ov in (0, overlap):
+        t = _fresh("sponza")
+        try:
+            t.set_option(A.OPT_FRAME_OVERLAP, ov)
+            t.set_option(A.OPT_WAVE_ORDER, 1)
+            t.set_option(A.OPT_WAVE_ORDER_PERIOD, period)
+            acc = torch.full((n, 4), 0.5, dtype=torch.float32, device="cuda")
+            for f in range(frames):
+                t.render_raw(consts[f], st, acc.data_ptr(), W, H, tiles=tiles, stream=stream, lights=lights)
+            torch.cuda.synchronize()
+            s = t.stats()
+            assert s.schedule & A.SCHED_COST_ORDERED, s.schedule
+            assert bool(s.schedule & A.SCHED_OVERLAP) == bool(ov), s.schedule
+            out.append(acc.cpu().numpy())
+        finally:
+            t.close()
+    np.testing.assert_array_equal(out[1], out[0])
 
 
 def _frames(torch, W, H, L, frames, overlap, streams=None, between=None, name="sponza", lights_of=None):
