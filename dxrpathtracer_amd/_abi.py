@@ -10,7 +10,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "lib")
-# libdxrpt.so from another directory (A/B of kernel builds, scripts/ab_builds.sh); the host library
+# libdxrpt.so from another directory (A/B of kernel builds, scripts/ab.sh); the host library
 # always comes from LIB_DIR
 KERNEL_LIB_DIR = os.environ.get("DXRPT_KERNEL_LIB_DIR") or LIB_DIR
 

@@ -1497,6 +1497,9 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
 #ifndef DXRPT_CHAIN_SHADOWS
 #define DXRPT_CHAIN_SHADOWS 1
 #endif
+#ifndef DXRPT_CHAIN_RELOAD
+#define DXRPT_CHAIN_RELOAD 0
+#endif
 template <bool kCount, bool kGA = true>
 PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh, float4& rad, uint32_t* cnt,
                                    PhaseAcc* pa = nullptr) {
@@ -1507,13 +1510,19 @@ PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh
     uint32_t occ = 0u;  // bit k: the ray of slot k is occluded
     if (active) {
         const float4 o4 = A.F.sh_org[s0], d4 = A.F.sh_dir[s0];
+#if DXRPT_CHAIN_RELOAD
+        // the second ray read back from its slot when the lane switches to it: nothing of it held in
+        // registers across the first ray's traversal (tail spills 84 -> 43 VGPRs) -- but the reload's round
+        // trip stalls the wave: metric +0.6..0.8 %, tail 1.122 -> 1.135 ms (r06, profiles/r06_ab_chain_reload.txt)
+#else
         const float4 d41 = nsh > 1u ? A.F.sh_dir[s1] : d4;
-        const bool alpha0 = fbits(A.F.sh_con[s0].w) == 0u;
-        const bool alpha1 = nsh > 1u ? fbits(A.F.sh_con[s1].w) == 0u : alpha0;
+        const bool alpha1 = nsh > 1u ? fbits(A.F.sh_con[s1].w) == 0u : false;
         const f3 o = ld3(o4), dir1 = ld3(d41);
+#endif
+        const bool alpha0 = fbits(A.F.sh_con[s0].w) == 0u;
         Ray8 R;
         HitRec h;
-        ray8_init(R, o, ld3(d4), d4.w, o4.w, alpha0, h);
+        ray8_init(R, ld3(o4), ld3(d4), d4.w, o4.w, alpha0, h);
         uint32_t node = 0, k = 0;
         int sp = 0;
         uint2 tos = make_uint2(0u, 0u);
@@ -1524,7 +1533,12 @@ PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh
             if (hit || !more) {
                 occ |= uint32_t(hit) << k;
                 if (++k < nsh) {  // the second ray: same origin, TMin, TMax
+#if DXRPT_CHAIN_RELOAD
+                    const float4 o41 = A.F.sh_org[s1], d41 = A.F.sh_dir[s1];
+                    ray8_init(R, ld3(o41), ld3(d41), d41.w, o41.w, fbits(A.F.sh_con[s1].w) == 0u, h);
+#else
                     ray8_init(R, o, dir1, d4.w, o4.w, alpha1, h);
+#endif
                     node = 0;
                     sp = 0;
                     tos = make_uint2(0u, 0u);
