@@ -646,6 +646,31 @@ PT_DEV bool trav8_tris2(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32
 // node visits and triangle tests, for a few more registers in the box test, so only kernels with the
 // budget use it (r04: the split tails and k_path at <= 5 waves/SIMD; k_path<7> spills, C2 +9 %).
 // Returns h.tri != kMiss (hit / occluded).
+// Word pointers of a node / a triangle record (DXRPT_IFIF 2 fetches either through one set of loads; both
+// device arrays carry kFetchPad bytes of tail padding for the words a lane of the other kind would read).
+PT_DEV const uint4* node8_words(const SceneDev& S, uint32_t node) {
+    return reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(S.nodes8) + size_t(node) * kNode8Stride);
+}
+PT_DEV const uint4* tri_words(const SceneDev& S, uint32_t rec) {
+    return reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(S.tris) + size_t(rec) * 48u);
+}
+PT_DEV float4 u2f4(uint4 v) {
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+//
+// DXRPT_IFIF (r06): the wave's loop interleaves the two halves of a lane's walk ("if-if", Aila & Laine 2009)
+// instead of running each visit's triangle group to completion before the next visit ("while-while"): an
+// iteration visits one node on the lanes with no pending triangle and tests one triangle (two with kPairs)
+// on the lanes holding some.  A lane's own sequence -- visit, its group's triangles in bit order, next
+// visit -- is unchanged, so results and census counts are identical; only which lanes share an iteration
+// changes (a lane with three leaf triangles no longer holds the wave's other lanes for three tests).
+// r06 A/B (profiles/r06_ab_ifif.txt, r06_ab_ifif2.txt, same box, interleaved): metric 1.391 -> 1.370 ms, tail
+// 1.115 -> 1.092 ms per launch, C3 -3.3 %, C4 -2.1 %, C2 -2.2 %, the 1/8 share -2.8 %.  A variant running
+// only one of the two halves per iteration, chosen wave-uniformly by the lanes ready for each, was no better
+// (the weights tried: even to -3 %, worse at 1:1).
+#ifndef DXRPT_IFIF
+#define DXRPT_IFIF 1
+#endif
 template <bool kAnyHit, bool kCount, bool kPairs = false, bool kNearest = false, bool kGA = true>
 PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, HitRec& h, uint32_t& nvisit,
                       uint32_t& ntest) {
@@ -654,6 +679,77 @@ PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
     uint32_t node = 0;
     int sp = 0;
     uint2 tos = make_uint2(0u, 0u);
+#if DXRPT_IFIF == 2
+    uint32_t tbase = 0, tbits = 0;
+    bool more = true;
+    while (true) {
+        const bool visit = tbits == 0u;
+        if (visit && !more) break;
+        // one fetch for the whole wave: a visiting lane's node words, a testing lane's triangle record(s)
+        const uint4 *pa, *pb;
+        bool two = false;
+        if (visit) {
+            pa = node8_words(S, node);
+            pb = pa + 3;
+        } else {
+            const uint32_t b0 = uint32_t(__builtin_ctz(tbits));
+            tbits &= tbits - 1u;
+            pa = tri_words(S, tbase + b0);
+            pb = pa;
+            if (kPairs && tbits) {
+                two = true;
+                pb = tri_words(S, tbase + uint32_t(__builtin_ctz(tbits)));
+                tbits &= tbits - 1u;
+            }
+        }
+        const uint4 w0 = pa[0], w1 = pa[1], w2 = pa[2], w3 = pb[0], w4 = pb[1];
+        const uint4 w5 = kPairs ? pb[2] : make_uint4(0u, 0u, 0u, 0u);
+        asm volatile("" ::"v"(w0.x), "v"(w0.y), "v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w1.z), "v"(w1.w), "v"(w2.x),
+                     "v"(w2.y), "v"(w2.z), "v"(w2.w), "v"(w3.x), "v"(w3.y), "v"(w3.z), "v"(w3.w), "v"(w4.x), "v"(w4.y),
+                     "v"(w4.z), "v"(w4.w));
+        if (kPairs) asm volatile("" ::"v"(w5.x), "v"(w5.y), "v"(w5.z), "v"(w5.w));
+        if (visit) {
+            more = trav8_node<kCount, kAnyHit, kNearest>(S, R, Node8Words{w0, w1, w2, w3, w4}, node, sp, tos, h, tbase, tbits,
+                                                         nvisit);
+        } else {
+            if (kCount) ntest += two ? 2u : 1u;
+            if (test_tri_rec<kAnyHit, kGA>(S, TriRec{u2f4(w0), u2f4(w1), u2f4(w2)}, R.o, R.d, R.tmin, R.tmax, R.alpha, h))
+                return true;
+            if (two && test_tri_rec<kAnyHit, kGA>(S, TriRec{u2f4(w3), u2f4(w4), u2f4(w5)}, R.o, R.d, R.tmin, R.tmax, R.alpha, h))
+                return true;
+        }
+    }
+    return h.tri != kMiss;
+#elif DXRPT_IFIF
+    uint32_t tbase = 0, tbits = 0;
+    bool more = true;
+    while (true) {
+        if (tbits == 0u) {
+            if (!more) break;
+            more = trav8_node<kCount, kAnyHit, kNearest>(S, R, load_node8(S, node), node, sp, tos, h, tbase, tbits, nvisit);
+        }
+        if (tbits) {
+            const uint32_t b0 = uint32_t(__builtin_ctz(tbits));
+            tbits &= tbits - 1u;
+            if (kPairs) {
+                const bool two = tbits != 0u;
+                const uint32_t b1 = two ? uint32_t(__builtin_ctz(tbits)) : b0;
+                tbits &= tbits - 1u;
+                const TriRec ra = load_tri_raw(S, tbase + b0);
+                const TriRec rb = load_tri_raw(S, tbase + b1);
+                pin_tri(ra);
+                pin_tri(rb);
+                if (kCount) ntest += two ? 2u : 1u;
+                if (test_tri_rec<kAnyHit, kGA>(S, ra, R.o, R.d, R.tmin, R.tmax, R.alpha, h)) return true;
+                if (two && test_tri_rec<kAnyHit, kGA>(S, rb, R.o, R.d, R.tmin, R.tmax, R.alpha, h)) return true;
+            } else {
+                if (kCount) ++ntest;
+                if (test_tri_rec<kAnyHit, kGA>(S, load_tri(S, tbase + b0), R.o, R.d, R.tmin, R.tmax, R.alpha, h)) return true;
+            }
+        }
+    }
+    return h.tri != kMiss;
+#else
     while (true) {
         uint32_t tbase = 0, tbits = 0;
         const bool more = trav8_node<kCount, kAnyHit, kNearest>(S, R, load_node8(S, node), node, sp, tos, h, tbase, tbits,
@@ -666,6 +762,7 @@ PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
         if (!more) break;
     }
     return h.tri != kMiss;
+#endif
 }
 
 // ---- wave-coherent ("packet") BVH8 traversal ------------------------------------------------------
@@ -1500,6 +1597,9 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
 #ifndef DXRPT_CHAIN_RELOAD
 #define DXRPT_CHAIN_RELOAD 0
 #endif
+#ifndef DXRPT_CHAIN_PAIRS
+#define DXRPT_CHAIN_PAIRS 0
+#endif
 template <bool kCount, bool kGA = true>
 PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh, float4& rad, uint32_t* cnt,
                                    PhaseAcc* pa = nullptr) {
@@ -1526,11 +1626,70 @@ PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh
         uint32_t node = 0, k = 0;
         int sp = 0;
         uint2 tos = make_uint2(0u, 0u);
+#if DXRPT_IFIF
+        uint32_t tbase = 0, tbits = 0;
+        bool more = true;
+#endif
         while (active) {
+#if DXRPT_IFIF == 2
+            // one fetch per iteration for the wave (traverse8): a node's words or a triangle record
+            bool hit = false;
+            const bool visit = tbits == 0u;  // (a lane here holds a pending triangle or may visit: more is true)
+            const uint4* pa;
+            if (visit) {
+                pa = node8_words(A.S, node);
+            } else {
+                pa = tri_words(A.S, tbase + uint32_t(__builtin_ctz(tbits)));
+                tbits &= tbits - 1u;
+            }
+            const uint4 w0 = pa[0], w1 = pa[1], w2 = pa[2], w3 = pa[3], w4 = pa[4];
+            asm volatile("" ::"v"(w0.x), "v"(w0.y), "v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w1.z), "v"(w1.w), "v"(w2.x),
+                         "v"(w2.y), "v"(w2.z), "v"(w2.w), "v"(w3.x), "v"(w3.y), "v"(w3.z), "v"(w3.w), "v"(w4.x), "v"(w4.y),
+                         "v"(w4.z), "v"(w4.w));
+            if (visit) {
+                more = trav8_node<kCount, true>(A.S, R, Node8Words{w0, w1, w2, w3, w4}, node, sp, tos, h, tbase, tbits, cnt[2]);
+            } else {
+                if (kCount) ++cnt[3];
+                hit = test_tri_rec<true, kGA>(A.S, TriRec{u2f4(w0), u2f4(w1), u2f4(w2)}, R.o, R.d, R.tmin, R.tmax, R.alpha, h);
+            }
+            if (hit || (!more && tbits == 0u)) {
+                tbits = 0u;
+                more = true;
+#elif DXRPT_IFIF
+            // if-if (traverse8): one node visit or one triangle test per lane and iteration
+            bool hit = false;
+            if (tbits == 0u)  // (a lane here holds a pending triangle or may visit: more is true)
+                more = trav8_node<kCount, true>(A.S, R, load_node8(A.S, node), node, sp, tos, h, tbase, tbits, cnt[2]);
+            if (tbits) {
+                const uint32_t b = uint32_t(__builtin_ctz(tbits));
+                tbits &= tbits - 1u;
+#if DXRPT_CHAIN_PAIRS
+                const bool two = tbits != 0u;  // a second record loaded with the first (one round trip)
+                const uint32_t b1 = two ? uint32_t(__builtin_ctz(tbits)) : b;
+                const TriRec ra = load_tri_raw(A.S, tbase + b), rb = load_tri_raw(A.S, tbase + b1);
+                pin_tri(ra);
+                pin_tri(rb);
+                if (kCount) ++cnt[3];
+                hit = test_tri_rec<true, kGA>(A.S, ra, R.o, R.d, R.tmin, R.tmax, R.alpha, h);
+                if (!hit && two) {
+                    tbits &= tbits - 1u;
+                    if (kCount) ++cnt[3];
+                    hit = test_tri_rec<true, kGA>(A.S, rb, R.o, R.d, R.tmin, R.tmax, R.alpha, h);
+                }
+#else
+                if (kCount) ++cnt[3];
+                hit = test_tri_rec<true, kGA>(A.S, load_tri(A.S, tbase + b), R.o, R.d, R.tmin, R.tmax, R.alpha, h);
+#endif
+            }
+            if (hit || (!more && tbits == 0u)) {
+                tbits = 0u;
+                more = true;
+#else
             uint32_t tbase = 0, tbits = 0;
             const bool more = trav8_node<kCount, true>(A.S, R, load_node8(A.S, node), node, sp, tos, h, tbase, tbits, cnt[2]);
             const bool hit = tbits != 0u && trav8_tris<true, kCount, kGA>(A.S, R, tbase, tbits, h, cnt[3]);
             if (hit || !more) {
+#endif
                 occ |= uint32_t(hit) << k;
                 if (++k < nsh) {  // the second ray: same origin, TMin, TMax
 #if DXRPT_CHAIN_RELOAD
@@ -1926,6 +2085,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     census_flush(A, cnt);
 }
 
+#ifndef DXRPT_TAIL_PAIRS
+#define DXRPT_TAIL_PAIRS 1  // the tails' closest hits test leaf triangles two per iteration (trav8_tris2)
+#endif
 // Depth d of queued path i (the tail's per-lane body; j = the lane's queue wave, nw = waves with work).
 template <bool kCount, bool kLast>
 PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw, const uint32_t* cnt_q, uint32_t* cnt,
@@ -1948,7 +2110,8 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
         }
         if (direct && !(o4.w >= 0.0f)) return;  // the path ended at depth 1
         uint32_t nv = 0, nt = 0;
-        traverse8<false, kCount, true, true, false>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= set.MaxAnyHitPathLength, h, nv, nt);
+        traverse8<false, kCount, DXRPT_TAIL_PAIRS != 0, true, false>(A.S, ld3(o4), ld3(d4), kRayTMin, o4.w, d <= set.MaxAnyHitPathLength,
+                                                                   h, nv, nt);
         if (kCount) {
             cnt[5] += nv;
             cnt[6] += nt;
