@@ -982,17 +982,15 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
             std::memcpy(&r.p1[3], &g, 4);
             std::memcpy(&r.p2[3], &flags, 4);
         });
-        {   // device layout: kNode8Stride per node (pt_layout.h), kFetchPad bytes of tail padding on both arrays
-            std::vector<uint8_t> padded(res.nodes8.size() * size_t(kNode8Stride) + kFetchPad, 0u);
+        if (kNode8Stride == sizeof(Bvh8Node)) {
+            ctx->d_nodes8.upload(res.nodes8.data(), res.nodes8.size() * sizeof(Bvh8Node));
+        } else {  // padded device layout (pt_layout.h kNode8Stride)
+            std::vector<uint8_t> padded(res.nodes8.size() * size_t(kNode8Stride), 0u);
             for (size_t i = 0; i < res.nodes8.size(); ++i)
                 std::memcpy(padded.data() + i * kNode8Stride, &res.nodes8[i], sizeof(Bvh8Node));
             ctx->d_nodes8.upload(padded.data(), padded.size());
         }
-        {
-            std::vector<uint8_t> tb(tris.size() * sizeof(TriRecord) + kFetchPad, 0u);
-            std::memcpy(tb.data(), tris.data(), tris.size() * sizeof(TriRecord));
-            ctx->d_tris.upload(tb.data(), tb.size());
-        }
+        ctx->d_tris.upload(tris.data(), tris.size() * sizeof(TriRecord));
         {   // shading-side copy of each triangle's vertices: one contiguous 192-B record per gtri, so a
             // hit gathers 2 cache lines in one round trip instead of 3 indices then 3 vertices
             std::vector<dxrpt_mesh_vertex> tv(size_t(ntris) * 3);

@@ -646,17 +646,6 @@ PT_DEV bool trav8_tris2(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32
 // node visits and triangle tests, for a few more registers in the box test, so only kernels with the
 // budget use it (r04: the split tails and k_path at <= 5 waves/SIMD; k_path<7> spills, C2 +9 %).
 // Returns h.tri != kMiss (hit / occluded).
-// Word pointers of a node / a triangle record (DXRPT_IFIF 2 fetches either through one set of loads; both
-// device arrays carry kFetchPad bytes of tail padding for the words a lane of the other kind would read).
-PT_DEV const uint4* node8_words(const SceneDev& S, uint32_t node) {
-    return reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(S.nodes8) + size_t(node) * kNode8Stride);
-}
-PT_DEV const uint4* tri_words(const SceneDev& S, uint32_t rec) {
-    return reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(S.tris) + size_t(rec) * 48u);
-}
-PT_DEV float4 u2f4(uint4 v) {
-    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-}
 //
 // DXRPT_IFIF (r06): the wave's loop interleaves the two halves of a lane's walk ("if-if", Aila & Laine 2009)
 // instead of running each visit's triangle group to completion before the next visit ("while-while"): an
@@ -667,7 +656,9 @@ PT_DEV float4 u2f4(uint4 v) {
 // r06 A/B (profiles/r06_ab_ifif.txt, r06_ab_ifif2.txt, same box, interleaved): metric 1.391 -> 1.370 ms, tail
 // 1.115 -> 1.092 ms per launch, C3 -3.3 %, C4 -2.1 %, C2 -2.2 %, the 1/8 share -2.8 %.  A variant running
 // only one of the two halves per iteration, chosen wave-uniformly by the lanes ready for each, was no better
-// (the weights tried: even to -3 %, worse at 1:1).
+// (the weights tried: even to -3 %, worse at 1:1); nor did one fetch per iteration serving both kinds of
+// lane (a node's words or a triangle record through the same loads): +9 % metric, tail +14 %
+// (profiles/r06_ab_unified.txt).
 #ifndef DXRPT_IFIF
 #define DXRPT_IFIF 1
 #endif
@@ -679,48 +670,7 @@ PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
     uint32_t node = 0;
     int sp = 0;
     uint2 tos = make_uint2(0u, 0u);
-#if DXRPT_IFIF == 2
-    uint32_t tbase = 0, tbits = 0;
-    bool more = true;
-    while (true) {
-        const bool visit = tbits == 0u;
-        if (visit && !more) break;
-        // one fetch for the whole wave: a visiting lane's node words, a testing lane's triangle record(s)
-        const uint4 *pa, *pb;
-        bool two = false;
-        if (visit) {
-            pa = node8_words(S, node);
-            pb = pa + 3;
-        } else {
-            const uint32_t b0 = uint32_t(__builtin_ctz(tbits));
-            tbits &= tbits - 1u;
-            pa = tri_words(S, tbase + b0);
-            pb = pa;
-            if (kPairs && tbits) {
-                two = true;
-                pb = tri_words(S, tbase + uint32_t(__builtin_ctz(tbits)));
-                tbits &= tbits - 1u;
-            }
-        }
-        const uint4 w0 = pa[0], w1 = pa[1], w2 = pa[2], w3 = pb[0], w4 = pb[1];
-        const uint4 w5 = kPairs ? pb[2] : make_uint4(0u, 0u, 0u, 0u);
-        asm volatile("" ::"v"(w0.x), "v"(w0.y), "v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w1.z), "v"(w1.w), "v"(w2.x),
-                     "v"(w2.y), "v"(w2.z), "v"(w2.w), "v"(w3.x), "v"(w3.y), "v"(w3.z), "v"(w3.w), "v"(w4.x), "v"(w4.y),
-                     "v"(w4.z), "v"(w4.w));
-        if (kPairs) asm volatile("" ::"v"(w5.x), "v"(w5.y), "v"(w5.z), "v"(w5.w));
-        if (visit) {
-            more = trav8_node<kCount, kAnyHit, kNearest>(S, R, Node8Words{w0, w1, w2, w3, w4}, node, sp, tos, h, tbase, tbits,
-                                                         nvisit);
-        } else {
-            if (kCount) ntest += two ? 2u : 1u;
-            if (test_tri_rec<kAnyHit, kGA>(S, TriRec{u2f4(w0), u2f4(w1), u2f4(w2)}, R.o, R.d, R.tmin, R.tmax, R.alpha, h))
-                return true;
-            if (two && test_tri_rec<kAnyHit, kGA>(S, TriRec{u2f4(w3), u2f4(w4), u2f4(w5)}, R.o, R.d, R.tmin, R.tmax, R.alpha, h))
-                return true;
-        }
-    }
-    return h.tri != kMiss;
-#elif DXRPT_IFIF
+#if DXRPT_IFIF
     uint32_t tbase = 0, tbits = 0;
     bool more = true;
     while (true) {
@@ -1631,31 +1581,7 @@ PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh
         bool more = true;
 #endif
         while (active) {
-#if DXRPT_IFIF == 2
-            // one fetch per iteration for the wave (traverse8): a node's words or a triangle record
-            bool hit = false;
-            const bool visit = tbits == 0u;  // (a lane here holds a pending triangle or may visit: more is true)
-            const uint4* pa;
-            if (visit) {
-                pa = node8_words(A.S, node);
-            } else {
-                pa = tri_words(A.S, tbase + uint32_t(__builtin_ctz(tbits)));
-                tbits &= tbits - 1u;
-            }
-            const uint4 w0 = pa[0], w1 = pa[1], w2 = pa[2], w3 = pa[3], w4 = pa[4];
-            asm volatile("" ::"v"(w0.x), "v"(w0.y), "v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w1.z), "v"(w1.w), "v"(w2.x),
-                         "v"(w2.y), "v"(w2.z), "v"(w2.w), "v"(w3.x), "v"(w3.y), "v"(w3.z), "v"(w3.w), "v"(w4.x), "v"(w4.y),
-                         "v"(w4.z), "v"(w4.w));
-            if (visit) {
-                more = trav8_node<kCount, true>(A.S, R, Node8Words{w0, w1, w2, w3, w4}, node, sp, tos, h, tbase, tbits, cnt[2]);
-            } else {
-                if (kCount) ++cnt[3];
-                hit = test_tri_rec<true, kGA>(A.S, TriRec{u2f4(w0), u2f4(w1), u2f4(w2)}, R.o, R.d, R.tmin, R.tmax, R.alpha, h);
-            }
-            if (hit || (!more && tbits == 0u)) {
-                tbits = 0u;
-                more = true;
-#elif DXRPT_IFIF
+#if DXRPT_IFIF
             // if-if (traverse8): one node visit or one triangle test per lane and iteration
             bool hit = false;
             if (tbits == 0u)  // (a lane here holds a pending triangle or may visit: more is true)

@@ -67,10 +67,6 @@ static_assert(sizeof(Bvh8Node) == 80, "Bvh8Node must be 80 B");
 constexpr uint32_t kNode8Stride = DXRPT_NODE_STRIDE;
 constexpr uint32_t kNode8Words = kNode8Stride / 16u;  // 16-B words
 static_assert(kNode8Stride == 80u || kNode8Stride == 128u, "node stride 80 or 128");
-// Tail padding (bytes) of the device node and triangle-record arrays: a traversal loop that fetches a
-// node's words or a triangle record through the same loads (pt_kernels.hip DXRPT_IFIF 2) may read up to
-// 48 bytes past the last record of either array.
-constexpr uint32_t kFetchPad = 64;
 
 constexpr int kMaxLeafTris8 = 3;
 constexpr int kTraversalStack8 = 16;  // group-stack entries per lane; the builder caps BVH8 depth to fit.
