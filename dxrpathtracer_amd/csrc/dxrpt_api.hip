@@ -1198,10 +1198,11 @@ int dxrpt_render(dxrpt_ctx* ctx, const dxrpt_ray_trace_constants* rtc, const dxr
         fp.split = fp.megakernel && (ctx->opt_split == 1u || (ctx->opt_split == 2u && split_by_size)) ? 1u : 0u;
         // split budgets: the head 5 waves/SIMD (96 VGPRs, no spills; r03: metric -0.2 %, C3 -0.4 %, C5's share
         // -1.0 %, C4 +0.5 % against 7), 6 (80 VGPRs) for frames above 1.5M paths with three frames in flight
-        // (r05: metric -0.6 %, C4 -0.9 %; the 1/2 share +0.9 %, C5's share +0.6 %, profiles/r05_ab_occ3.txt);
-        // the tails 7 (72 VGPRs; 6: +2-3 %)
+        // (r05: metric -0.6 %, C4 -0.9 %; the 1/2 share +0.9 %, C5's share +0.6 %, profiles/r05_ab_occ3.txt),
+        // 7 (72 VGPRs) there since the if-if traversal loops (r06: metric -0.9..-1.4 %, C4 -0.6 %, C3 even,
+        // profiles/r06_ab_budgets.txt, r06_ab_split_budgets.txt); the tails 7 (72 VGPRs; 6: +2-3 %)
         if (fp.split && !ctx->opt_mega_occ)
-            fp.megakernel_occupancy = !ctx->opt_overlap ? 6u : (ctx->opt_overlap != 1u && paths > 1500000u ? 6u : 5u);
+            fp.megakernel_occupancy = !ctx->opt_overlap ? 6u : (ctx->opt_overlap != 1u && paths > 1500000u ? 7u : 5u);
         fp.tail_occupancy = ctx->opt_tail_occ ? ctx->opt_tail_occ : (ctx->opt_mega_occ ? fp.megakernel_occupancy : 7u);
         ctx->wclock_waves = 0;  // set again below only by a frame that records stamps
         // Overlapped frames (DXRPT_OPT_FRAME_OVERLAP, megakernel frames): frame parity ov runs on slot ov --

@@ -662,6 +662,13 @@ PT_DEV bool trav8_tris2(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32
 #ifndef DXRPT_IFIF
 #define DXRPT_IFIF 1
 #endif
+// DXRPT_SPEC (with DXRPT_IFIF; bit 0 any-hit walks, bit 1 closest hit): a lane holding a pending triangle group
+// also visits its next node in the same iteration, queueing the new group behind the pending one (one slot).
+// The lane's node-visit and triangle-test sequences keep their order; only a closest-hit ray's culling may
+// use a less tight t (visits can run ahead of tests), so results are identical and census counts may differ.
+#ifndef DXRPT_SPEC
+#define DXRPT_SPEC 0
+#endif
 template <bool kAnyHit, bool kCount, bool kPairs = false, bool kNearest = false, bool kGA = true>
 PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, HitRec& h, uint32_t& nvisit,
                       uint32_t& ntest) {
@@ -673,10 +680,32 @@ PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
 #if DXRPT_IFIF
     uint32_t tbase = 0, tbits = 0;
     bool more = true;
+    constexpr bool kSpec = (DXRPT_SPEC & (kAnyHit ? 1 : 2)) != 0;
+    uint32_t qbase = 0, qbits = 0;  // kSpec: a second, queued triangle group
     while (true) {
-        if (tbits == 0u) {
+        if (kSpec) {
+            // speculative visit (DXRPT_SPEC): a lane holding a pending group keeps visiting while the queue slot
+            // is free; the groups are tested in visit order
+            if (tbits == 0u && qbits == 0u && !more) break;
+            if (more && qbits == 0u) {
+                uint32_t nb = 0, nbits = 0;
+                more = trav8_node<kCount, kAnyHit, kNearest>(S, R, load_node8(S, node), node, sp, tos, h, nb, nbits, nvisit);
+                if (tbits == 0u) {
+                    tbase = nb;
+                    tbits = nbits;
+                } else {
+                    qbase = nb;
+                    qbits = nbits;
+                }
+            }
+        } else if (tbits == 0u) {
             if (!more) break;
             more = trav8_node<kCount, kAnyHit, kNearest>(S, R, load_node8(S, node), node, sp, tos, h, tbase, tbits, nvisit);
+        }
+        if (kSpec && tbits == 0u && qbits) {
+            tbase = qbase;
+            tbits = qbits;
+            qbits = 0u;
         }
         if (tbits) {
             const uint32_t b0 = uint32_t(__builtin_ctz(tbits));
@@ -1579,13 +1608,32 @@ PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh
 #if DXRPT_IFIF
         uint32_t tbase = 0, tbits = 0;
         bool more = true;
+        uint32_t qbase = 0, qbits = 0;  // DXRPT_SPEC bit 0: the queued group
 #endif
         while (active) {
 #if DXRPT_IFIF
             // if-if (traverse8): one node visit or one triangle test per lane and iteration
             bool hit = false;
-            if (tbits == 0u)  // (a lane here holds a pending triangle or may visit: more is true)
+            if (DXRPT_SPEC & 1) {
+                if (more && qbits == 0u) {
+                    uint32_t nb = 0, nbits = 0;
+                    more = trav8_node<kCount, true>(A.S, R, load_node8(A.S, node), node, sp, tos, h, nb, nbits, cnt[2]);
+                    if (tbits == 0u) {
+                        tbase = nb;
+                        tbits = nbits;
+                    } else {
+                        qbase = nb;
+                        qbits = nbits;
+                    }
+                }
+                if (tbits == 0u && qbits) {
+                    tbase = qbase;
+                    tbits = qbits;
+                    qbits = 0u;
+                }
+            } else if (tbits == 0u) {  // (a lane here holds a pending triangle or may visit: more is true)
                 more = trav8_node<kCount, true>(A.S, R, load_node8(A.S, node), node, sp, tos, h, tbase, tbits, cnt[2]);
+            }
             if (tbits) {
                 const uint32_t b = uint32_t(__builtin_ctz(tbits));
                 tbits &= tbits - 1u;
@@ -1607,8 +1655,9 @@ PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh
                 hit = test_tri_rec<true, kGA>(A.S, load_tri(A.S, tbase + b), R.o, R.d, R.tmin, R.tmax, R.alpha, h);
 #endif
             }
-            if (hit || (!more && tbits == 0u)) {
+            if (hit || (!more && tbits == 0u && qbits == 0u)) {
                 tbits = 0u;
+                qbits = 0u;
                 more = true;
 #else
             uint32_t tbase = 0, tbits = 0;

@@ -337,7 +337,8 @@ int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
                                             the wavefront.  Identical results. */
 #define DXRPT_OPT_MEGAKERNEL_OCCUPANCY 24u /* megakernel register budget in waves/SIMD: 0 = by frame size
                                               (default: 7 above 600,000 paths, 5 from 300,000 with overlapped
-                                              frames, else 4; the split head 5), or 4..7 */
+                                              frames, else 4; the split head 5, or 7 above
+                                              1,500,000 paths with three frames in flight), or 4..7 */
 #define DXRPT_OPT_BAKE_CHUNK 25u /* texels per dxrpt_bake_lightmap launch (default 2^21; bounds the
                                     per-texel shadow-slot buffers).  Identical results. */
 #define DXRPT_OPT_WAVE_CLOCKS 28u /* 1: with DXRPT_OPT_COUNT_TRAVERSAL, the megakernel census frame also

@@ -58,6 +58,9 @@ SCHEDULES = {
     # the full 1080p frames' budgets with three frames in flight (r05: head 6 above 1.5M paths)
     "head<6>+tail<7>": ({A.OPT_MEGAKERNEL_SPLIT: 1, A.OPT_MEGAKERNEL_OCCUPANCY: 6, A.OPT_TAIL_OCCUPANCY: 7},
                         (A.SCHED_MEGAKERNEL | A.SCHED_OVERLAP | A.SCHED_SPLIT, A.SCHED_ORDER_KERNEL, 6, 7), False),
+    # r06: head 7 above 1.5M paths (the if-if loops moved the best budget)
+    "head<7>+tail<7>": ({A.OPT_MEGAKERNEL_SPLIT: 1, A.OPT_MEGAKERNEL_OCCUPANCY: 7, A.OPT_TAIL_OCCUPANCY: 7},
+                        (A.SCHED_MEGAKERNEL | A.SCHED_OVERLAP | A.SCHED_SPLIT, A.SCHED_ORDER_KERNEL, 7, 7), False),
 }
 
 _TRACERS = {}
