@@ -234,6 +234,10 @@ def main():
     ap.add_argument("--gather", default="native", choices=["native", "torch"],
                     help="N-GPU frame-end gather: the C ABI's RCCL send/recv + un-permute kernel (default) or "
                          "torch.distributed.gather + index_select")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1: nccl (= RCCL, one rank per GPU; the default) or gloo "
+                         "(a rehearsal of the N-rank control flow on fewer GPUs: ranks share devices round robin, the "
+                         "native RCCL gather refuses two ranks on one GPU, so the torch gather runs staged through host)")
     ap.add_argument("--phase-timeout", type=float, default=300.0,
                     help="seconds any one phase (setup, a collective, the timed frames) may take on a rank before "
                          "every rank is ended with a JSON error line")
@@ -257,11 +261,16 @@ def main():
     wd = Watchdog(rank, world, None, metric)
     try:
         with wd.phase("init", args.phase_timeout):
-            torch.cuda.set_device(local_rank)
+            # one rank per GPU (the driver's launch); a gloo rehearsal may put several ranks on one device
+            device = local_rank if args.dist_backend == "nccl" else local_rank % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(device)
             if world > 1:
-                dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+                if args.dist_backend == "nccl":
+                    dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+                else:
+                    dist.init_process_group("gloo")
                 wd.store = default_store()
-        run(args, metric, world, rank, local_rank, wd)
+        run(args, metric, world, rank, device, wd)
     except BaseException as e:  # noqa: BLE001 -- any failure ends every rank (SystemExit from argparse aside)
         import traceback
         traceback.print_exc()
@@ -269,7 +278,7 @@ def main():
     wd.close()
 
 
-def run(args, metric, world, rank, local_rank, wd):
+def run(args, metric, world, rank, device, wd):
     import torch
     import torch.distributed as dist
     import dxrpathtracer_amd as D
@@ -287,7 +296,7 @@ def run(args, metric, world, rank, local_rank, wd):
         scene = D.Scene(SCENE)
         settings = scene.settings(MaxPathLength=PATH_LENGTH)
         sky = D.make_sky(settings)
-        tracer = DXRPathTracer(local_rank)
+        tracer = DXRPathTracer(device)
         tracer.initialize_scene(scene, sky)
         bvh = tracer.build_rt_acceleration_structure()
         setup_s = time.perf_counter() - t0
@@ -311,7 +320,7 @@ def run(args, metric, world, rank, local_rank, wd):
             gather_used = args.gather
             if args.gather == "native":
                 try:
-                    pg = NativeGather(lay, rank, local_rank, full, timing=True)
+                    pg = NativeGather(lay, rank, device, full, timing=True)
                 except RuntimeError as e:  # e.g. an RCCL communicator that cannot be built on this node
                     # every rank takes the same branch (NativeGather's checks and results are all-gathered)
                     log(f"native gather unavailable ({e}); falling back to torch.distributed.gather")
@@ -443,7 +452,7 @@ def run(args, metric, world, rank, local_rank, wd):
     multi = None
     with wd.phase("collect", T):
         if world > 1:
-            t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+            t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         frame_ms = np.array([a.elapsed_time(b) for a, b in ev])  # per frame on the render stream (incl. the gather's)
@@ -452,7 +461,7 @@ def run(args, metric, world, rank, local_rank, wd):
         value = nominal_per_frame * args.steps / elapsed / 1e6
         if world > 1:
             per_rank = [None] * world
-            dist.all_gather_object(per_rank, (render_only_ms, local_elapsed / args.steps * 1e3, n_local))
+            dist.all_gather_object(per_rank, (render_only_ms, local_elapsed / args.steps * 1e3, n_local, device))
             g_ms, u_ms, g_frames = pg.times() if hasattr(pg, "times") else (None, None, 0)
             render_max = max(v[0] for v in per_rank)
             multi = {"render_ms_per_rank": [round(v[0], 4) for v in per_rank], "render_ms_max": round(render_max, 4),
@@ -468,6 +477,8 @@ def run(args, metric, world, rank, local_rank, wd):
                      "unpermute_ms": None if u_ms is None else round(u_ms, 4),
                      "gather_frames_timed": g_frames,
                      "rccl_ranks": getattr(pg, "comm_ranks", None),
+                     "dist_backend": args.dist_backend,
+                     "devices": [int(v[3]) for v in per_rank],
                      "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "runtime default (4)"),
                      # the part of the job's frame interval the gather adds beyond the slowest rank's own
                      # render throughput (difference of throughput intervals)

@@ -662,14 +662,16 @@ PT_DEV bool trav8_tris2(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32
 #ifndef DXRPT_IFIF
 #define DXRPT_IFIF 1
 #endif
-// DXRPT_SPEC (with DXRPT_IFIF; bit 0 any-hit walks, bit 1 closest hit): a lane holding a pending triangle group
-// also visits its next node in the same iteration, queueing the new group behind the pending one (one slot).
-// The lane's node-visit and triangle-test sequences keep their order; only a closest-hit ray's culling may
-// use a less tight t (visits can run ahead of tests), so results are identical and census counts may differ.
-#ifndef DXRPT_SPEC
-#define DXRPT_SPEC 0
+// kSpec (with DXRPT_IFIF): speculative visits -- a lane holding a pending triangle group also visits its next
+// node in the same iteration, queueing the new group behind the pending one (one slot).  The lane's
+// node-visit and triangle-test sequences keep their order; only a closest-hit ray's culling may use a less
+// tight t (visits can run ahead of tests), so results are identical and census counts may differ.  On in the
+// single k_path (the band shares' kernel: 1/8 share -1.3..-2 %, 1/4 -2 %), off in the split head and tails
+// (metric +1..3 %; profiles/r06_ab_spec*.txt).  DXRPT_SPEC_PATH 0 turns it off in k_path too.
+#ifndef DXRPT_SPEC_PATH
+#define DXRPT_SPEC_PATH 1
 #endif
-template <bool kAnyHit, bool kCount, bool kPairs = false, bool kNearest = false, bool kGA = true>
+template <bool kAnyHit, bool kCount, bool kPairs = false, bool kNearest = false, bool kGA = true, bool kSpec = false>
 PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, HitRec& h, uint32_t& nvisit,
                       uint32_t& ntest) {
     Ray8 R;
@@ -680,11 +682,10 @@ PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
 #if DXRPT_IFIF
     uint32_t tbase = 0, tbits = 0;
     bool more = true;
-    constexpr bool kSpec = (DXRPT_SPEC & (kAnyHit ? 1 : 2)) != 0;
     uint32_t qbase = 0, qbits = 0;  // kSpec: a second, queued triangle group
     while (true) {
         if (kSpec) {
-            // speculative visit (DXRPT_SPEC): a lane holding a pending group keeps visiting while the queue slot
+            // speculative visit (kSpec): a lane holding a pending group keeps visiting while the queue slot
             // is free; the groups are tested in visit order
             if (tbits == 0u && qbits == 0u && !more) break;
             if (more && qbits == 0u) {
@@ -1529,7 +1530,7 @@ PT_DEV PhaseAcc phase_start() {
 // nearby origins -- take the wave-coherent traversal (all lanes active).  A lane whose slot 0 holds another
 // kind of ray (a spot light's, or at MaxPathLength 2 the sky visibility ray: random directions) traces it
 // per lane, after the packet.  cnt[2..3]: the census' any-hit node / triangle fetches.
-template <bool kCount, bool kNear = false, bool kGA = true>
+template <bool kCount, bool kNear = false, bool kGA = true, bool kSpec = false>
 PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh, bool sun0, uint32_t packet, float4& rad,
                            uint32_t* cnt, PhaseAcc* pa = nullptr) {
     uint32_t unused[4] = {0u, 0u, 0u, 0u};
@@ -1550,7 +1551,7 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
             occluded = traverse8_packet<true, kCount, !kNear>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live && sun0, hs,
                                                       cnt + 2);
         if (live && !(pk && sun0))
-            occluded = traverse8<true, kCount, false, kNear, kGA>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, hs, cnt[2],
+            occluded = traverse8<true, kCount, false, kNear, kGA, kSpec>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, hs, cnt[2],
                                                          cnt[3]);
         if (live) {
             rad.x += occluded ? c4.x * 0.0f : c4.x;
@@ -1579,7 +1580,7 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
 #ifndef DXRPT_CHAIN_PAIRS
 #define DXRPT_CHAIN_PAIRS 0
 #endif
-template <bool kCount, bool kGA = true>
+template <bool kCount, bool kGA = true, bool kSpec = false>
 PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh, float4& rad, uint32_t* cnt,
                                    PhaseAcc* pa = nullptr) {
     uint32_t unused[4] = {0u, 0u, 0u, 0u};
@@ -1608,13 +1609,13 @@ PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh
 #if DXRPT_IFIF
         uint32_t tbase = 0, tbits = 0;
         bool more = true;
-        uint32_t qbase = 0, qbits = 0;  // DXRPT_SPEC bit 0: the queued group
+        uint32_t qbase = 0, qbits = 0;  // kSpec: the queued group
 #endif
         while (active) {
 #if DXRPT_IFIF
             // if-if (traverse8): one node visit or one triangle test per lane and iteration
             bool hit = false;
-            if (DXRPT_SPEC & 1) {
+            if (kSpec) {
                 if (more && qbits == 0u) {
                     uint32_t nb = 0, nbits = 0;
                     more = trav8_node<kCount, true>(A.S, R, load_node8(A.S, node), node, sp, tos, h, nb, nbits, cnt[2]);
@@ -1720,7 +1721,7 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
         if (d == 1 && (packet & 1u))  // coherent primary rays: wave-coherent traversal (same results)
             traverse8_packet<false, kCount>(A.S, org, dir, tmin1, tmax, d <= set.MaxAnyHitPathLength, true, h, cd);
         else
-            traverse8<false, kCount, false, kNearest>(A.S, org, dir, d == 1 ? tmin1 : kRayTMin, tmax, d <= set.MaxAnyHitPathLength, h, cd[0],
+            traverse8<false, kCount, false, kNearest, true, DXRPT_SPEC_PATH != 0>(A.S, org, dir, d == 1 ? tmin1 : kRayTMin, tmax, d <= set.MaxAnyHitPathLength, h, cd[0],
                                      cd[1]);
         phase_mark(pa, d == 1 ? 0 : d == 2 ? 3 : 6);
         if (kCount && h.tri != kMiss) ++cd[4];  // radiance hits: the vertices PathTrace shades
@@ -1748,9 +1749,9 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
         // depth >= 2 (the depth-1 sun shadows of full waves take the packet traversal): the vertex's rays
         // chained in one loop where the budget has the registers (kNearest: <= 5 waves/SIMD)
         if (kNearest && DXRPT_CHAIN_SHADOWS && A.P.rtc.NumLights == 0u && (d > 1 || !(packet & 2u)))
-            vertex_shadows_chained<kCount>(A, slot_p, nsh, rad, kCount ? cd : nullptr);
+            vertex_shadows_chained<kCount, true, DXRPT_SPEC_PATH != 0>(A, slot_p, nsh, rad, kCount ? cd : nullptr);
         else
-            vertex_shadows<kCount, kNearest>(A, d, slot_p, nsh, sun0, packet, rad, cd);
+            vertex_shadows<kCount, kNearest, true, DXRPT_SPEC_PATH != 0>(A, d, slot_p, nsh, sun0, packet, rad, cd);
         phase_mark(pa, d == 1 ? 2 : d == 2 ? 5 : 6);
         if (!O.cont) break;
         org = O.nextOrigin;

@@ -172,6 +172,10 @@ class PipelinedGather:
         self.recv = None
         self.pending = None
         self.count = 0
+        # gloo (the CPU tests, bench.py's --dist-backend gloo rehearsal): device slabs are staged through host
+        # memory, the collective runs on host tensors
+        import torch.distributed as dist
+        self.host = layout.world > 1 and dist.is_initialized() and dist.get_backend(group) == "gloo"
 
     def submit(self, local):
         import torch
@@ -181,11 +185,11 @@ class PipelinedGather:
                 self.full.copy_(local[: self.layout.width * self.layout.height])
             return
         if self.staging is None:
-            self.staging = [torch.empty_like(local) for _ in range(2)]
+            dev = "cpu" if self.host else local.device
+            self.staging = [torch.empty(local.shape, dtype=local.dtype, device=dev) for _ in range(2)]
             if self.rank == 0:  # each frame's slabs land in one contiguous buffer: no concatenation copy
                 w = self.layout.world
-                self.recv = [torch.empty((w * local.shape[0], 4), dtype=local.dtype, device=local.device)
-                             for _ in range(2)]
+                self.recv = [torch.empty((w * local.shape[0], 4), dtype=local.dtype, device=dev) for _ in range(2)]
         k = self.count % 2
         self.count += 1
         self.staging[k].copy_(local)
@@ -205,7 +209,12 @@ class PipelinedGather:
         work, k = pend
         work.wait()
         if self.rank == 0:
-            torch.index_select(self.recv[k], 0, self.src_index, out=self.full)
+            if self.recv[k].device != self.full.device:  # host-staged (gloo): un-permute on the host, one copy back
+                if getattr(self, "_src_host", None) is None:
+                    self._src_host = self.src_index.to(self.recv[k].device)
+                self.full.copy_(torch.index_select(self.recv[k], 0, self._src_host))
+            else:
+                torch.index_select(self.recv[k], 0, self.src_index, out=self.full)
 
 
 def gathered_tiles(layout: BandLayout):
