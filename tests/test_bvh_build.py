@@ -7,6 +7,7 @@ csrc/tools/bvh_check.cpp, which builds exactly as dxrpt_build_bvh does and print
   cap; the builder then falls back to the tree without them instead of failing.
 * Deep, degenerate meshes (geometric sequences of slivers) always fit the stack.
 """
+import fcntl
 import json
 import os
 import subprocess
@@ -21,7 +22,12 @@ MAX_WIDE_DEPTH = 15  # pt_layout.h kTraversalStack8 - 1
 
 @pytest.fixture(scope="module")
 def tool():
-    subprocess.run(["make", "-s", "-C", CSRC, "build/bvh_check"], check=True)
+    # xdist workers share the binary: serialise the make so no worker runs it while another relinks it
+    os.makedirs(os.path.join(CSRC, "build"), exist_ok=True)
+    with open(os.path.join(CSRC, "build", ".bvh_check.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", CSRC, "build/bvh_check"], check=True)
+        fcntl.flock(lk, fcntl.LOCK_UN)
     return TOOL
 
 
