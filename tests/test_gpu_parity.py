@@ -769,12 +769,21 @@ def test_split_census_prices_the_timed_kernels(torch_cuda, name, W, H, L):
         t.set_option(A.OPT_WAVE_ORDER, A.DEFAULT_WAVE_ORDER)
         t.set_option(A.OPT_MEGAKERNEL_PATHS, 0)
     assert split.radiance_hits > 0 and split.radiance_hits == single.radiance_hits
-    assert split.node_visits_radiance == single.node_visits_radiance
-    assert split.tri_tests_radiance == single.tri_tests_radiance
+    # r06: the single k_path visits speculatively (kSpec: a lane holding a pending triangle group visits its next
+    # node in the same iteration), the split kernels do not.  Each lane's visit and test sequences keep their
+    # order, so the speculative kernel fetches a superset: its extra visits are the ones run ahead of a
+    # closest hit's tightening t or past an any-hit's terminating triangle.  Counts are therefore >= the
+    # split census and within 3 % of it (measured +1.1 % on the metric-like frames); hits are equal.
+    def close_above(spec, plain):
+        assert plain <= spec <= plain * 1.03 + 64, (spec, plain)
+    close_above(single.node_visits_radiance, split.node_visits_radiance)
+    close_above(single.tri_tests_radiance, split.tri_tests_radiance)
     d1s, d1k = list(split.census_depth1), list(single.census_depth1)
-    assert (d1s[0], d1s[1], d1s[4]) == (d1k[0], d1k[1], d1k[4])
-    # deeper any-hit rays: same code and order in both
-    assert split.node_visits_shadow - d1s[2] == single.node_visits_shadow - d1k[2]
-    assert split.tri_tests_shadow - d1s[3] == single.tri_tests_shadow - d1k[3]
+    assert d1s[4] == d1k[4]
+    close_above(d1k[0], d1s[0])
+    close_above(d1k[1], d1s[1])
+    # deeper any-hit rays: same code and order in both, plus the speculative visits
+    close_above(single.node_visits_shadow - d1k[2], split.node_visits_shadow - d1s[2])
+    close_above(single.tri_tests_shadow - d1k[3], split.tri_tests_shadow - d1s[3])
     assert list(split.radiance_rays_per_depth) == list(single.radiance_rays_per_depth)
     assert list(split.shadow_rays_per_depth) == list(single.shadow_rays_per_depth)
