@@ -415,7 +415,21 @@ def run(args, metric, world, rank, device, wd):
         torch.cuda.synchronize()
         render_only_ms = (time.perf_counter() - t_r) / args.steps * 1e3
 
-    # ---- timed region: the shipped defaults (overlapped frames); per-frame events on the render stream
+    # ---- timed region: the shipped defaults (overlapped frames), nothing but the frames between the
+    # barrier + synchronize brackets.  (Through r06's first runs the loop also recorded two timing events per
+    # frame on the render stream; each timing event is a marker packet the stream's queue has to pass, and
+    # they cost 1-5 % of the interval -- C2 0.696 vs 0.663 ms render-only.  The per-frame spans now come from
+    # their own untimed pass below; BENCH_TIMED_SPANS=1 puts the events back into the timed loop for an A/B.)
+    spans_in_timed = os.environ.get("BENCH_TIMED_SPANS", "0") == "1"
+
+    def span_pass(base):
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        for f in range(args.steps):
+            ev[f][0].record(stream)
+            frame(base + f)
+            ev[f][1].record(stream)
+        return ev
+
     with wd.phase("timed frames", T):
         if hasattr(pg, "reset_times"):
             pg.reset_times()
@@ -423,11 +437,11 @@ def run(args, metric, world, rank, device, wd):
             dist.barrier()
         torch.cuda.synchronize()
         t_start = time.perf_counter()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-        for f in range(args.steps):
-            ev[f][0].record(stream)
-            frame(args.warmup + f)
-            ev[f][1].record(stream)
+        if spans_in_timed:
+            ev = span_pass(args.warmup)
+        else:
+            for f in range(args.steps):
+                frame(args.warmup + f)
         flush()  # the last frame's gather + un-permute are inside the timed region
         torch.cuda.synchronize()
         local_elapsed = time.perf_counter() - t_start  # this rank, before the closing barrier
@@ -435,6 +449,17 @@ def run(args, metric, world, rank, device, wd):
             dist.barrier()
         elapsed = time.perf_counter() - t_start
     stats = tracer.stats()
+
+    with wd.phase("frame spans", T):
+        # per-frame event spans on the render stream (diagnostic, untimed): the same K frames again
+        span_ms_per_frame = None
+        if not spans_in_timed:
+            torch.cuda.synchronize()
+            t_s = time.perf_counter()
+            ev = span_pass(args.warmup)
+            flush()
+            torch.cuda.synchronize()
+            span_ms_per_frame = (time.perf_counter() - t_s) / args.steps * 1e3
 
     with wd.phase("frame latency", T):
         # paced passes (untimed for the headline): the reference's two frames of latency, and three (the
@@ -585,6 +610,9 @@ def run(args, metric, world, rank, device, wd):
                                             "what": "elapsed / steps of the timed region (ms_per_step)",
                                             "achieved": round(fi_gbs, 1), "frac": round(fi_gbs / HBM_PEAK_GBS, 4),
                                             "mean_frame_span_ms": round(span_mean, 4),
+                                            "span_pass": "timed loop" if spans_in_timed else
+                                            "an untimed pass of the same K frames with two timing events per frame",
+                                            "span_pass_ms_per_frame": r4(span_ms_per_frame),
                                             "consistent_within_5pct": bool(fi_consistent),
                                             "frame_at_a_time_ms": round(frame_at_a_time_ms, 4)}},
             "cpu_baseline": cpu,

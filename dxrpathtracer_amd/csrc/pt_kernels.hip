@@ -481,7 +481,16 @@ PT_DEV Node8Words load_node8(const SceneDev& S, uint32_t node) {
 
 // Slot mask of the node's children whose quantised box the ray enters within [tmin, tmx].  kNearest:
 // also the slot of the internal child entered first (smallest entry distance; *nslot, 8 if none).
-template <bool kNearest = false>
+// DXRPT_NEAR_KEYS (r06 experiment): the nearest internal child as the unsigned minimum of per-child keys
+// (entry distance bits with the slot in the low 3 mantissa bits, a leaf's key with bit 31 set, a missed child's
+// all ones) instead of a compare-and-select chain (5 VALU per child); 2: the minimum over every hit child, a
+// leaf winner falling back to octant order.  Closest-hit results are order-independent either way.
+#ifndef DXRPT_NEAR_KEYS
+#define DXRPT_NEAR_KEYS 0
+#endif
+// kInfT (r06 experiment, DXRPT_AH_INF): the ray's TMax is FP32Max (the chained sun / sky rays), so the far test
+// drops the clamp: hit <=> !(tn > tf) && !(tmin > tf) -- conservative where the clamped test differs (tf = inf).
+template <bool kNearest = false, bool kInfT = false>
 PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_t* nslot = nullptr) {
     const uint4 w0 = W.w0, w2 = W.w2, w3 = W.w3, w4 = W.w4;
     const float ax = __uint_as_float((w0.w & 0xFFu) << 23) * R.inv.x;
@@ -502,6 +511,7 @@ PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_
     const uint32_t imask = w0.w >> 24;
     float best_tn = kFP32Max;
     uint32_t best_c = 8u;
+    uint32_t best_key = 0xFFFFFFFFu;
     // near and far plane of one axis in one packed FMA (v_pk_fma_f32): (qn, qf) * (a, a) + (b, b)
     const f2v A2x = {ax, ax}, A2y = {ay, ay}, A2z = {az, az};
     const f2v B2x = {bx, bx}, B2y = {by, by}, B2z = {bz, bz};
@@ -514,14 +524,36 @@ PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_
         const f2v tx = __builtin_elementwise_fma(qx, A2x, B2x);
         const f2v ty = __builtin_elementwise_fma(qy, A2y, B2y);
         const f2v tz = __builtin_elementwise_fma(qz, A2z, B2z);
-        const float tn = fmaxf(fmaxf(tx.x, ty.x), fmaxf(tz.x, R.tmin));
-        const float tf = fminf(fminf(tx.y, ty.y), fminf(tz.y, tmx));
+        float tn, tf;
+        bool hit;
+        if (kInfT) {
+            tn = fmaxf(fmaxf(tx.x, ty.x), tz.x);
+            tf = fminf(fminf(tx.y, ty.y), tz.y);
+            hit = !(tn > tf) && !(R.tmin > tf);
+        } else {
+            tn = fmaxf(fmaxf(tx.x, ty.x), fmaxf(tz.x, R.tmin));
+            tf = fminf(fminf(tx.y, ty.y), fminf(tz.y, tmx));
+            hit = tn <= tf;
+        }
         // empty slots carry inverted boxes (qlo 255, qhi 0: never entered) and meta 0 (no triangles)
-        hm |= uint32_t(tn <= tf) << c;
-        if (kNearest && tn <= tf && ((imask >> c) & 1u) && tn < best_tn) {
+        hm |= uint32_t(hit) << c;
+        if (kNearest && DXRPT_NEAR_KEYS) {
+            uint32_t key = fbits(tn);
+            if (DXRPT_NEAR_KEYS == 1) {  // a leaf (meta bit 7 clear) never wins: bit 31
+                const uint32_t mw = c < 4 ? W.w1.z : W.w1.w;
+                key |= ~(mw << (24u - sh)) & 0x80000000u;
+            }
+            key = (key & ~7u) | uint32_t(c);
+            best_key = __builtin_elementwise_min(best_key, hit ? key : 0xFFFFFFFFu);
+        } else if (kNearest && hit && ((imask >> c) & 1u) && tn < best_tn) {
             best_tn = tn;
             best_c = uint32_t(c);
         }
+    }
+    if (kNearest && DXRPT_NEAR_KEYS == 1) best_c = (best_key >> 31) ? 8u : (best_key & 7u);
+    if (kNearest && DXRPT_NEAR_KEYS == 2) {
+        best_c = best_key & 7u;
+        if (best_key == 0xFFFFFFFFu || !((imask >> best_c) & 1u)) best_c = 8u;
     }
     if (kNearest) *nslot = best_c;
     return hm;
@@ -560,7 +592,7 @@ PT_DEV uint32_t leaf_tri_bits(uint32_t lh, const uint4& w1) {
 template <bool kAnyHit>
 PT_DEV uint32_t key_octant(uint32_t oct) { return kAnyHit ? oct ^ 7u : oct; }
 
-template <bool kCount, bool kAnyHit = false, bool kNearest = false>
+template <bool kCount, bool kAnyHit = false, bool kNearest = false, bool kInfT = false>
 PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, const Node8Words& W, uint32_t& node, int& sp, uint2& tos,
                        const HitRec& h, uint32_t& tbase, uint32_t& tbits, uint32_t& nvisit) {
     if (kCount) ++nvisit;
@@ -569,7 +601,7 @@ PT_DEV bool trav8_node(const SceneDev& S, const Ray8& R, const Node8Words& W, ui
     // kNearest picks the nearest hit internal child for closest-hit rays (any-hit rays ignore it: their
     // farthest-entry-first variant was +0.7..1.4 % on C3 / C5, profiles/r04_ab_farthest.txt)
     constexpr bool kPick = kNearest && !kAnyHit;
-    const uint32_t hm = box8_hits<kPick>(R, W, h.t, &nslot);  // hit children, slot space
+    const uint32_t hm = box8_hits<kPick, kInfT>(R, W, h.t, &nslot);  // hit children, slot space
     const uint32_t imask = w0.w >> 24;
     const uint32_t koct = key_octant<kAnyHit>(R.oct);
     const uint32_t ihits = key_order(hm & imask, koct);
@@ -1580,6 +1612,9 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
 #ifndef DXRPT_CHAIN_PAIRS
 #define DXRPT_CHAIN_PAIRS 0
 #endif
+#ifndef DXRPT_AH_INF
+#define DXRPT_AH_INF 0  // the chained rays' box test without the TMax clamp (box8_hits kInfT; r06 experiment)
+#endif
 template <bool kCount, bool kGA = true, bool kSpec = false>
 PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh, float4& rad, uint32_t* cnt,
                                    PhaseAcc* pa = nullptr) {
@@ -1618,7 +1653,7 @@ PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh
             if (kSpec) {
                 if (more && qbits == 0u) {
                     uint32_t nb = 0, nbits = 0;
-                    more = trav8_node<kCount, true>(A.S, R, load_node8(A.S, node), node, sp, tos, h, nb, nbits, cnt[2]);
+                    more = trav8_node<kCount, true, false, DXRPT_AH_INF != 0>(A.S, R, load_node8(A.S, node), node, sp, tos, h, nb, nbits, cnt[2]);
                     if (tbits == 0u) {
                         tbase = nb;
                         tbits = nbits;
@@ -1633,7 +1668,7 @@ PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh
                     qbits = 0u;
                 }
             } else if (tbits == 0u) {  // (a lane here holds a pending triangle or may visit: more is true)
-                more = trav8_node<kCount, true>(A.S, R, load_node8(A.S, node), node, sp, tos, h, tbase, tbits, cnt[2]);
+                more = trav8_node<kCount, true, false, DXRPT_AH_INF != 0>(A.S, R, load_node8(A.S, node), node, sp, tos, h, tbase, tbits, cnt[2]);
             }
             if (tbits) {
                 const uint32_t b = uint32_t(__builtin_ctz(tbits));
@@ -1662,7 +1697,7 @@ PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh
                 more = true;
 #else
             uint32_t tbase = 0, tbits = 0;
-            const bool more = trav8_node<kCount, true>(A.S, R, load_node8(A.S, node), node, sp, tos, h, tbase, tbits, cnt[2]);
+            const bool more = trav8_node<kCount, true, false, DXRPT_AH_INF != 0>(A.S, R, load_node8(A.S, node), node, sp, tos, h, tbase, tbits, cnt[2]);
             const bool hit = tbits != 0u && trav8_tris<true, kCount, kGA>(A.S, R, tbase, tbits, h, cnt[3]);
             if (hit || !more) {
 #endif
