@@ -481,15 +481,28 @@ PT_DEV Node8Words load_node8(const SceneDev& S, uint32_t node) {
 
 // Slot mask of the node's children whose quantised box the ray enters within [tmin, tmx].  kNearest:
 // also the slot of the internal child entered first (smallest entry distance; *nslot, 8 if none).
-// DXRPT_NEAR_KEYS (r06 experiment): the nearest internal child as the unsigned minimum of per-child keys
-// (entry distance bits with the slot in the low 3 mantissa bits, a leaf's key with bit 31 set, a missed child's
-// all ones) instead of a compare-and-select chain (5 VALU per child); 2: the minimum over every hit child, a
-// leaf winner falling back to octant order.  Closest-hit results are order-independent either way.
+// DXRPT_NEAR_KEYS (r06): kNearest's choice as the unsigned minimum of per-child keys -- the entry distance's
+// bits (tn >= tmin >= 0 in every caller: bit order = value order) with the slot in the low 3 mantissa bits, a
+// missed child's key all ones -- instead of a compare-and-select chain per child (5 VALU each: the internal-bit
+// test, the compare, two selects).  2 (shipped): the minimum over every hit child; a leaf winner falls back to
+// the octant order.  1: leaves excluded through bit 31 of their keys.  0: the chain.  Closest-hit results do not
+// depend on the visit order (minimum (t, triangle id)), so frames are bit-identical; node-visit counts move.
+// Same box, interleaved (profiles/r06_ab_boxtest.txt): 2 -- metric -0.3 %, C4 -0.9 %, C2 -1.0 %, C3 -0.4 %, the
+// 1/8 share -1.4 %; 1 -- even to +0.6 %.
 #ifndef DXRPT_NEAR_KEYS
-#define DXRPT_NEAR_KEYS 0
+#define DXRPT_NEAR_KEYS 2
 #endif
-// kInfT (r06 experiment, DXRPT_AH_INF): the ray's TMax is FP32Max (the chained sun / sky rays), so the far test
-// drops the clamp: hit <=> !(tn > tf) && !(tmin > tf) -- conservative where the clamped test differs (tf = inf).
+// kInfT (r06, DXRPT_AH_INF): an any-hit walk's box test without the TMax clamp -- hit <=> !(tn > tf) &&
+// !(tmin > tf): 4 VALU per child instead of 5 (max, max3, min, min3, compare).  For rays with TMax = FP32Max (the
+// sun's and the sky-visibility rays, RayTrace.hlsl:258,425) it differs from the clamped test only where tf is
+// +inf or NaN, where it accepts; for any ray it accepts a superset of the clamped test's children, and the
+// triangle test still enforces TMax, so the any-hit result -- a boolean over the occluders in [TMin, TMax] -- is
+// the same: frames are bit-identical.  DXRPT_AH_INF 1: the chained sun / sky rays (metric -2.0 %, C4 -1.9 %, C2
+// -2.7 %, C3 even, 1/8 share -0.6 %, r06_ab_boxtest.txt); 2 (shipped): also the head's sun packets and the
+// per-lane sun rays of frames without spot lights (spot rays keep the clamp: their TMax culls).
+#ifndef DXRPT_AH_INF
+#define DXRPT_AH_INF 2
+#endif
 template <bool kNearest = false, bool kInfT = false>
 PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_t* nslot = nullptr) {
     const uint4 w0 = W.w0, w2 = W.w2, w3 = W.w3, w4 = W.w4;
@@ -703,7 +716,8 @@ PT_DEV bool trav8_tris2(const SceneDev& S, const Ray8& R, uint32_t tbase, uint32
 #ifndef DXRPT_SPEC_PATH
 #define DXRPT_SPEC_PATH 1
 #endif
-template <bool kAnyHit, bool kCount, bool kPairs = false, bool kNearest = false, bool kGA = true, bool kSpec = false>
+template <bool kAnyHit, bool kCount, bool kPairs = false, bool kNearest = false, bool kGA = true, bool kSpec = false,
+          bool kInfT = false>
 PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, HitRec& h, uint32_t& nvisit,
                       uint32_t& ntest) {
     Ray8 R;
@@ -722,7 +736,7 @@ PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
             if (tbits == 0u && qbits == 0u && !more) break;
             if (more && qbits == 0u) {
                 uint32_t nb = 0, nbits = 0;
-                more = trav8_node<kCount, kAnyHit, kNearest>(S, R, load_node8(S, node), node, sp, tos, h, nb, nbits, nvisit);
+                more = trav8_node<kCount, kAnyHit, kNearest, kInfT>(S, R, load_node8(S, node), node, sp, tos, h, nb, nbits, nvisit);
                 if (tbits == 0u) {
                     tbase = nb;
                     tbits = nbits;
@@ -733,7 +747,7 @@ PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
             }
         } else if (tbits == 0u) {
             if (!more) break;
-            more = trav8_node<kCount, kAnyHit, kNearest>(S, R, load_node8(S, node), node, sp, tos, h, tbase, tbits, nvisit);
+            more = trav8_node<kCount, kAnyHit, kNearest, kInfT>(S, R, load_node8(S, node), node, sp, tos, h, tbase, tbits, nvisit);
         }
         if (kSpec && tbits == 0u && qbits) {
             tbase = qbase;
@@ -764,8 +778,8 @@ PT_DEV bool traverse8(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, boo
 #else
     while (true) {
         uint32_t tbase = 0, tbits = 0;
-        const bool more = trav8_node<kCount, kAnyHit, kNearest>(S, R, load_node8(S, node), node, sp, tos, h, tbase, tbits,
-                                                                nvisit);
+        const bool more = trav8_node<kCount, kAnyHit, kNearest, kInfT>(S, R, load_node8(S, node), node, sp, tos, h, tbase,
+                                                                       tbits, nvisit);
         if (tbits) {
             const bool done = kPairs ? trav8_tris2<kAnyHit, kCount, kGA>(S, R, tbase, tbits, h, ntest)
                                      : trav8_tris<kAnyHit, kCount, kGA>(S, R, tbase, tbits, h, ntest);
@@ -820,7 +834,7 @@ PT_DEV uint32_t wave_or8(uint32_t m) {
 // (1/8 share -3.5 %, profiles/r04_ab_packet_order.txt).  Returns this lane's
 // result like traverse8 (h.tri != kMiss: hit / occluded).  kCount: node / triangle FETCHES are counted
 // in cnt[0] / cnt[1] by the wave's first live lane (a packet fetches each once per wave).
-template <bool kAnyHit, bool kCount = false, bool kFar = true>
+template <bool kAnyHit, bool kCount = false, bool kFar = true, bool kInfT = false>
 PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, bool live, HitRec& h,
                              uint32_t* cnt = nullptr) {
     Ray8 R;
@@ -839,7 +853,7 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
     while (true) {
         const Node8Words W = load_node8_uniform(S, node);
         if (counter) ++cnt[0];
-        const uint32_t hm = live ? box8_hits(R, W, h.t) : 0u;
+        const uint32_t hm = live ? box8_hits<false, kInfT>(R, W, h.t) : 0u;
         const uint32_t um = wave_or8(hm);
         const uint32_t imask = W.w0.w >> 24;
         uint32_t tbits = leaf_tri_bits(um & ~imask, W.w1);  // leaf triangles hit by any lane
@@ -1580,11 +1594,17 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
         bool occluded = false;
         const bool pk = d == 1 && k == 0 && (packet & 2u);
         if (pk)
-            occluded = traverse8_packet<true, kCount, !kNear>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, live && sun0, hs,
-                                                      cnt + 2);
-        if (live && !(pk && sun0))
-            occluded = traverse8<true, kCount, false, kNear, kGA, kSpec>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, hs, cnt[2],
-                                                         cnt[3]);
+            occluded = traverse8_packet<true, kCount, !kNear, DXRPT_AH_INF >= 2>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u,
+                                                                          live && sun0, hs, cnt + 2);
+        if (live && !(pk && sun0)) {
+            // no spot lights: every ray here is the sun's or the sky's (TMax FP32Max), the box test's kInfT form
+            if (DXRPT_AH_INF >= 2 && A.P.rtc.NumLights == 0u)
+                occluded = traverse8<true, kCount, false, kNear, kGA, kSpec, true>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u,
+                                                                               hs, cnt[2], cnt[3]);
+            else
+                occluded = traverse8<true, kCount, false, kNear, kGA, kSpec>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, hs,
+                                                                         cnt[2], cnt[3]);
+        }
         if (live) {
             rad.x += occluded ? c4.x * 0.0f : c4.x;
             rad.y += occluded ? c4.y * 0.0f : c4.y;
@@ -1612,9 +1632,7 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
 #ifndef DXRPT_CHAIN_PAIRS
 #define DXRPT_CHAIN_PAIRS 0
 #endif
-#ifndef DXRPT_AH_INF
-#define DXRPT_AH_INF 0  // the chained rays' box test without the TMax clamp (box8_hits kInfT; r06 experiment)
-#endif
+
 template <bool kCount, bool kGA = true, bool kSpec = false>
 PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh, float4& rad, uint32_t* cnt,
                                    PhaseAcc* pa = nullptr) {
@@ -1653,7 +1671,7 @@ PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh
             if (kSpec) {
                 if (more && qbits == 0u) {
                     uint32_t nb = 0, nbits = 0;
-                    more = trav8_node<kCount, true, false, DXRPT_AH_INF != 0>(A.S, R, load_node8(A.S, node), node, sp, tos, h, nb, nbits, cnt[2]);
+                    more = trav8_node<kCount, true, false, DXRPT_AH_INF >= 1>(A.S, R, load_node8(A.S, node), node, sp, tos, h, nb, nbits, cnt[2]);
                     if (tbits == 0u) {
                         tbase = nb;
                         tbits = nbits;
@@ -1668,7 +1686,7 @@ PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh
                     qbits = 0u;
                 }
             } else if (tbits == 0u) {  // (a lane here holds a pending triangle or may visit: more is true)
-                more = trav8_node<kCount, true, false, DXRPT_AH_INF != 0>(A.S, R, load_node8(A.S, node), node, sp, tos, h, tbase, tbits, cnt[2]);
+                more = trav8_node<kCount, true, false, DXRPT_AH_INF >= 1>(A.S, R, load_node8(A.S, node), node, sp, tos, h, tbase, tbits, cnt[2]);
             }
             if (tbits) {
                 const uint32_t b = uint32_t(__builtin_ctz(tbits));
@@ -1697,7 +1715,7 @@ PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh
                 more = true;
 #else
             uint32_t tbase = 0, tbits = 0;
-            const bool more = trav8_node<kCount, true, false, DXRPT_AH_INF != 0>(A.S, R, load_node8(A.S, node), node, sp, tos, h, tbase, tbits, cnt[2]);
+            const bool more = trav8_node<kCount, true, false, DXRPT_AH_INF >= 1>(A.S, R, load_node8(A.S, node), node, sp, tos, h, tbase, tbits, cnt[2]);
             const bool hit = tbits != 0u && trav8_tris<true, kCount, kGA>(A.S, R, tbase, tbits, h, cnt[3]);
             if (hit || !more) {
 #endif
