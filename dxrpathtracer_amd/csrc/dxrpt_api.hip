@@ -968,6 +968,9 @@ int dxrpt_build_bvh(dxrpt_ctx* ctx) {
                 slot_of[t] = uint32_t(ctx->omm_tris.size());
                 ctx->omm_tris.push_back(t);
             }
+        // the kernels address node and triangle records by 32-bit byte offsets (pt_kernels.hip DXRPT_ADDR32)
+        require(res.nodes8.size() * size_t(kNode8Stride) < (size_t(1) << 32) && size_t(nrefs) * sizeof(TriRecord) < (size_t(1) << 32),
+                "dxrpt_build_bvh: the BVH's node or triangle-record array reaches 4 GiB (32-bit record offsets)");
         std::vector<TriRecord> tris(nrefs);
         host_parallel(nrefs, threads, [&](uint32_t i) {
             const uint32_t t = res.tri_order[i];

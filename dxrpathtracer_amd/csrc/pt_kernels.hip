@@ -358,9 +358,28 @@ PT_DEV void pin_tri(const TriRec& r) {
                  "v"(r.p1.w), "v"(r.p2.x), "v"(r.p2.y), "v"(r.p2.z), "v"(r.p2.w));
 }
 
-// A record's words come from one 64-bit base address (immediate offsets).
+// Byte offsets of node / triangle records as 32-bit values (DXRPT_ADDR32, r06): the loads take the array's
+// SGPR base plus a 32-bit VGPR offset ("saddr" form: one VGPR per address, no 64-bit add), and the offset is
+// two full-rate shift-adds instead of a quarter-rate v_mad_u64_u32 (LLVM lowers x * 80 / x * 48 to
+// v_mul_lo_u32 or the 64-bit multiply-add; the asm keeps the shift-add form).  dxrpt_build_bvh refuses trees
+// whose node or triangle-record array reaches 4 GiB, so the offsets cannot wrap.
+#ifndef DXRPT_ADDR32
+#define DXRPT_ADDR32 1
+#endif
+PT_DEV uint32_t shl_add(uint32_t a, uint32_t b) {  // (a << 4) + b
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+PT_DEV uint32_t tri_offset(uint32_t rec) { return shl_add(rec, rec << 5); }  // rec * 48
+PT_DEV uint32_t node_offset(uint32_t node) {
+    return kNode8Stride == 80u ? shl_add(node, node << 6) : node * kNode8Stride;  // node * 80
+}
+
+// A record's words come from one base address (immediate offsets).
 PT_DEV TriRec load_tri_raw(const SceneDev& S, uint32_t rec) {
-    const float4* T = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(S.tris) + size_t(rec) * 48u);
+    const float4* T = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(S.tris) +
+                                                      (DXRPT_ADDR32 ? size_t(tri_offset(rec)) : size_t(rec) * 48u));
     return TriRec{T[0], T[1], T[2]};
 }
 
@@ -471,7 +490,8 @@ struct Node8Words {
 };
 
 PT_DEV Node8Words load_node8(const SceneDev& S, uint32_t node) {
-    const uint4* N = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(S.nodes8) + size_t(node) * kNode8Stride);
+    const uint4* N = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(S.nodes8) +
+                                                    (DXRPT_ADDR32 ? size_t(node_offset(node)) : size_t(node) * kNode8Stride));
     const Node8Words w{N[0], N[1], N[2], N[3], N[4]};
     asm volatile("" ::"v"(w.w0.x), "v"(w.w0.y), "v"(w.w0.z), "v"(w.w0.w), "v"(w.w1.x), "v"(w.w1.y), "v"(w.w1.z),
                  "v"(w.w1.w), "v"(w.w2.x), "v"(w.w2.y), "v"(w.w2.z), "v"(w.w2.w), "v"(w.w3.x), "v"(w.w3.y),
@@ -497,11 +517,13 @@ PT_DEV Node8Words load_node8(const SceneDev& S, uint32_t node) {
 // sun's and the sky-visibility rays, RayTrace.hlsl:258,425) it differs from the clamped test only where tf is
 // +inf or NaN, where it accepts; for any ray it accepts a superset of the clamped test's children, and the
 // triangle test still enforces TMax, so the any-hit result -- a boolean over the occluders in [TMin, TMax] -- is
-// the same: frames are bit-identical.  DXRPT_AH_INF 1: the chained sun / sky rays (metric -2.0 %, C4 -1.9 %, C2
-// -2.7 %, C3 even, 1/8 share -0.6 %, r06_ab_boxtest.txt); 2 (shipped): also the head's sun packets and the
-// per-lane sun rays of frames without spot lights (spot rays keep the clamp: their TMax culls).
+// the same: frames are bit-identical.  DXRPT_AH_INF 1 (shipped): the chained sun / sky rays (metric -2.0 %, C4
+// -1.9 %, C2 -2.7 %, C3 even, 1/8 share -0.6 %, r06_ab_boxtest.txt); 2: also the sun packets; 3: also the per-lane
+// sun rays of frames without spot lights (a second per-lane any-hit walk behind a uniform branch: spot rays keep
+// the clamp, their TMax culls) -- 3 raised the head's spills 34 -> 82 VGPRs and was even to +0.5 %
+// (r06_ab_boxtest2.txt).
 #ifndef DXRPT_AH_INF
-#define DXRPT_AH_INF 2
+#define DXRPT_AH_INF 1
 #endif
 template <bool kNearest = false, bool kInfT = false>
 PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_t* nslot = nullptr) {
@@ -1598,7 +1620,7 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
                                                                           live && sun0, hs, cnt + 2);
         if (live && !(pk && sun0)) {
             // no spot lights: every ray here is the sun's or the sky's (TMax FP32Max), the box test's kInfT form
-            if (DXRPT_AH_INF >= 2 && A.P.rtc.NumLights == 0u)
+            if (DXRPT_AH_INF >= 3 && A.P.rtc.NumLights == 0u)
                 occluded = traverse8<true, kCount, false, kNear, kGA, kSpec, true>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u,
                                                                                hs, cnt[2], cnt[3]);
             else
