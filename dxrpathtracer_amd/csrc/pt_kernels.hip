@@ -523,7 +523,7 @@ PT_DEV Node8Words load_node8(const SceneDev& S, uint32_t node) {
 // the clamp, their TMax culls) -- 3 raised the head's spills 34 -> 82 VGPRs and was even to +0.5 %
 // (r06_ab_boxtest2.txt).
 #ifndef DXRPT_AH_INF
-#define DXRPT_AH_INF 1
+#define DXRPT_AH_INF 2
 #endif
 template <bool kNearest = false, bool kInfT = false>
 PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_t* nslot = nullptr) {

@@ -108,8 +108,47 @@ PT_DEV float cmj_randfloat(uint32_t i, uint32_t p) {
     i ^= i >> 17; i *= 1u | p >> 18;
     return float(i) * (1.0f / 4294967808.0f);
 }
+// DXRPT_CMJ_POW2 (r06): grids whose nx and ny are powers of two (SqrtNumSamples 1, 2, 4, 8, 16, ...: every
+// BASELINE config uses 4) take the same arithmetic with the integer % and / as masks and shifts and the float
+// divisions as multiplications by the exact reciprocal 2^-k -- bit-identical results (x / 2^k == x * 2^-k in
+// binary floating point without underflow, which these values in [0, N] cannot reach), without the
+// integer-division sequences (v_rcp_iflag + quarter-rate v_mul_hi/v_mul_lo) and the IEEE divide expansions.
+// The grid size is wave-uniform, so the test is a scalar branch.
+#ifndef DXRPT_CMJ_POW2
+#define DXRPT_CMJ_POW2 1
+#endif
+PT_DEV uint32_t cmj_permute_pow2(uint32_t i, uint32_t l, uint32_t p) {  // l = 2^k: w = l - 1, one round
+    const uint32_t w = l - 1u;
+    i ^= p; i *= 0xe170893du;
+    i ^= p >> 16;
+    i ^= (i & w) >> 4;
+    i ^= p >> 8; i *= 0x0929eb3fu;
+    i ^= p >> 23;
+    i ^= (i & w) >> 1; i *= 1u | p >> 27;
+    i *= 0x6935fa69u;
+    i ^= (i & w) >> 11; i *= 0x74dcb303u;
+    i ^= (i & w) >> 2; i *= 0x9e501cc3u;
+    i ^= (i & w) >> 2; i *= 0xc860a3dfu;
+    i &= w;
+    i ^= i >> 5;
+    return (i + p) & w;  // i <= w after the mask (i >> 5 only clears bits), so the loop's test never repeats
+}
 PT_DEV void sample_cmj2d(uint32_t sampleIdx, uint32_t nx, uint32_t ny, uint32_t pattern, float* ox, float* oy) {
     uint32_t N = nx * ny;
+    if (DXRPT_CMJ_POW2 && ((nx & (nx - 1u)) | (ny & (ny - 1u))) == 0u && nx != 0u && ny != 0u) {
+        const uint32_t kx = uint32_t(__builtin_ctz(nx));
+        sampleIdx = cmj_permute_pow2(sampleIdx, N, pattern * 0x51633e2du);
+        uint32_t sx = cmj_permute_pow2(sampleIdx & (nx - 1u), nx, pattern * 0x68bc21ebu);
+        uint32_t sy = cmj_permute_pow2(sampleIdx >> kx, ny, pattern * 0x02e5be93u);
+        float jx = cmj_randfloat(sampleIdx, pattern * 0x967a889bu);
+        float jy = cmj_randfloat(sampleIdx, pattern * 0x368cc8b7u);
+        // 1 / 2^k as a float: exact (k < 32 here)
+        const float rnx = __uint_as_float((127u - kx) << 23), rny = __uint_as_float((127u - uint32_t(__builtin_ctz(ny))) << 23);
+        const float rN = __uint_as_float((127u - uint32_t(__builtin_ctz(N))) << 23);
+        *ox = (float(sx) + (float(sy) + jx) * rny) * rnx;
+        *oy = (float(sampleIdx) + jy) * rN;
+        return;
+    }
     sampleIdx = cmj_permute(sampleIdx, N, pattern * 0x51633e2du);
     uint32_t sx = cmj_permute(sampleIdx % nx, nx, pattern * 0x68bc21ebu);
     uint32_t sy = cmj_permute(sampleIdx / nx, ny, pattern * 0x02e5be93u);
