@@ -525,8 +525,10 @@ PT_DEV Node8Words load_node8(const SceneDev& S, uint32_t node) {
 #ifndef DXRPT_AH_INF
 #define DXRPT_AH_INF 2
 #endif
-template <bool kNearest = false, bool kInfT = false>
-PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_t* nslot = nullptr) {
+// kUOct (the packet walks, DXRPT_PACKET_UOCT): `uoct` is the octant of every live lane's ray, a wave-uniform
+// value -- with the node words in SGPRs (scalar loads) the near / far word selection is then scalar.
+template <bool kNearest = false, bool kInfT = false, bool kUOct = false>
+PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_t* nslot = nullptr, uint32_t uoct = 0u) {
     const uint4 w0 = W.w0, w2 = W.w2, w3 = W.w3, w4 = W.w4;
     const float ax = __uint_as_float((w0.w & 0xFFu) << 23) * R.inv.x;
     const float ay = __uint_as_float(((w0.w >> 8) & 0xFFu) << 23) * R.inv.y;
@@ -538,7 +540,8 @@ PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_
     // sec. 3.2): with inv >= 0 the near plane of every child is qlo, else qhi, so this equals the
     // min/max of the two slab distances.  Words: w2 = (qlo_x 0-3, 4-7, qlo_y 0-3, 4-7),
     // w3 = (qlo_z .., qhi_x ..), w4 = (qhi_y .., qhi_z ..).
-    const bool sxn = (R.oct & 4u) != 0u, syn = (R.oct & 2u) != 0u, szn = (R.oct & 1u) != 0u;
+    const uint32_t boct = kUOct ? uoct : R.oct;
+    const bool sxn = (boct & 4u) != 0u, syn = (boct & 2u) != 0u, szn = (boct & 1u) != 0u;
     const uint32_t nx0 = sxn ? w3.z : w2.x, nx1 = sxn ? w3.w : w2.y, fx0 = sxn ? w2.x : w3.z, fx1 = sxn ? w2.y : w3.w;
     const uint32_t ny0 = syn ? w4.x : w2.z, ny1 = syn ? w4.y : w2.w, fy0 = syn ? w2.z : w4.x, fy1 = syn ? w2.w : w4.y;
     const uint32_t nz0 = szn ? w4.z : w3.x, nz1 = szn ? w4.w : w3.y, fz0 = szn ? w3.x : w4.z, fz1 = szn ? w3.y : w4.w;
@@ -856,17 +859,13 @@ PT_DEV uint32_t wave_or8(uint32_t m) {
 // (1/8 share -3.5 %, profiles/r04_ab_packet_order.txt).  Returns this lane's
 // result like traverse8 (h.tri != kMiss: hit / occluded).  kCount: node / triangle FETCHES are counted
 // in cnt[0] / cnt[1] by the wave's first live lane (a packet fetches each once per wave).
-template <bool kAnyHit, bool kCount = false, bool kFar = true, bool kInfT = false>
-PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, bool live, HitRec& h,
-                             uint32_t* cnt = nullptr) {
-    Ray8 R;
-    ray8_init(R, o, d, tmin, tmax, alpha, h);
-    const unsigned long long lv = __ballot(live);
-    if (lv == 0ull) return false;
+// kUOct: every live lane's ray has the octant `oct0` (the box test's near / far selection is then scalar).
+template <bool kAnyHit, bool kCount, bool kFar, bool kInfT, bool kUOct>
+PT_DEV bool packet_walk(const SceneDev& S, const Ray8& R, bool live, unsigned long long lv, uint32_t oct0, HitRec& h,
+                        uint32_t* cnt) {
     // key order of the first live lane's octant for the whole wave (any order gives the same results;
     // any-hit rays far to near, key_octant)
-    const uint32_t oct = key_octant<kAnyHit && kFar>(
-        uint32_t(__builtin_amdgcn_readlane(int(R.oct), __ffsll(static_cast<long long>(lv)) - 1)));
+    const uint32_t oct = key_octant<kAnyHit && kFar>(oct0);
     const uint32_t lane = uint32_t(__lane_id());
     const bool counter = kCount && lane == uint32_t(__ffsll(static_cast<long long>(lv)) - 1);
     uint32_t sbase = 0, sword = 0;  // stack entry j in lane j
@@ -875,7 +874,7 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
     while (true) {
         const Node8Words W = load_node8_uniform(S, node);
         if (counter) ++cnt[0];
-        const uint32_t hm = live ? box8_hits<false, kInfT>(R, W, h.t) : 0u;
+        const uint32_t hm = live ? box8_hits<false, kInfT, kUOct>(R, W, h.t, nullptr, oct0) : 0u;
         const uint32_t um = wave_or8(hm);
         const uint32_t imask = W.w0.w >> 24;
         uint32_t tbits = leaf_tri_bits(um & ~imask, W.w1);  // leaf triangles hit by any lane
@@ -915,6 +914,30 @@ PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tm
         if (!found) break;
     }
     return h.tri != kMiss;
+}
+
+// DXRPT_PACKET_UOCT (r06): a packet whose live lanes share one ray octant -- always the sun's shadow rays (one
+// direction, kOctMode 1), mostly an 8x8 block's primary rays (kOctMode 2 tests it per packet) -- walks with the
+// octant's near / far node words chosen by scalar selects on the SGPR node words: 24 VALU fewer per visit (12
+// copies of node words into VGPRs and 12 per-lane selects).  kOctMode 0: per-lane selection only.
+#ifndef DXRPT_PACKET_UOCT
+#define DXRPT_PACKET_UOCT 1
+#endif
+template <bool kAnyHit, bool kCount = false, bool kFar = true, bool kInfT = false, int kOctMode = 2>
+PT_DEV bool traverse8_packet(const SceneDev& S, f3 o, f3 d, float tmin, float tmax, bool alpha, bool live, HitRec& h,
+                             uint32_t* cnt = nullptr) {
+    Ray8 R;
+    ray8_init(R, o, d, tmin, tmax, alpha, h);
+    const unsigned long long lv = __ballot(live);
+    if (lv == 0ull) return false;
+    const uint32_t oct0 = uint32_t(__builtin_amdgcn_readlane(int(R.oct), __ffsll(static_cast<long long>(lv)) - 1));
+    if constexpr (DXRPT_PACKET_UOCT && kOctMode == 1) {
+        return packet_walk<kAnyHit, kCount, kFar, kInfT, true>(S, R, live, lv, oct0, h, cnt);
+    } else {
+        if (DXRPT_PACKET_UOCT && kOctMode == 2 && __ballot(live && R.oct != oct0) == 0ull)
+            return packet_walk<kAnyHit, kCount, kFar, kInfT, true>(S, R, live, lv, oct0, h, cnt);
+        return packet_walk<kAnyHit, kCount, kFar, kInfT, false>(S, R, live, lv, oct0, h, cnt);
+    }
 }
 
 // ---- queues ---------------------------------------------------------------------------------------
@@ -1616,7 +1639,7 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
         bool occluded = false;
         const bool pk = d == 1 && k == 0 && (packet & 2u);
         if (pk)
-            occluded = traverse8_packet<true, kCount, !kNear, DXRPT_AH_INF >= 2>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u,
+            occluded = traverse8_packet<true, kCount, !kNear, DXRPT_AH_INF >= 2, 1>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u,
                                                                           live && sun0, hs, cnt + 2);
         if (live && !(pk && sun0)) {
             // no spot lights: every ray here is the sun's or the sky's (TMax FP32Max), the box test's kInfT form

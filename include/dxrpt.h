@@ -302,7 +302,9 @@ int dxrpt_add_texture(dxrpt_ctx* ctx, uint32_t w, uint32_t h, uint32_t fmt, cons
  * (the SkyCache::CubeMap layout, Graphics/Skybox.cpp:160-201). */
 int dxrpt_set_sky(dxrpt_ctx* ctx, const uint16_t* rgba16f_cube, uint32_t res);
 /* Builds the acceleration structure over the scene set by dxrpt_set_scene (one BLAS over all
- * geometries + identity instance in the reference; here one binned-SAH BVH over all triangles). */
+ * geometries + identity instance in the reference; here one binned-SAH BVH over all triangles).
+ * Fails with DXRPT_E_INVALID_ARG when the node or triangle-record array would reach 4 GiB (the
+ * kernels address records by 32-bit byte offsets: about 80 M triangle references). */
 int dxrpt_build_bvh(dxrpt_ctx* ctx);
 int dxrpt_get_bvh_info(const dxrpt_ctx* ctx, dxrpt_bvh_info* info);
 
