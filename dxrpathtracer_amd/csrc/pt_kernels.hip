@@ -1643,7 +1643,7 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
                                                                           live && sun0, hs, cnt + 2);
         if (live && !(pk && sun0)) {
             // no spot lights: every ray here is the sun's or the sky's (TMax FP32Max), the box test's kInfT form
-            if (DXRPT_AH_INF >= 3 && A.P.rtc.NumLights == 0u)
+            if (DXRPT_AH_INF >= 3 && (kNear || DXRPT_AH_INF >= 4) && A.P.rtc.NumLights == 0u)
                 occluded = traverse8<true, kCount, false, kNear, kGA, kSpec, true>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u,
                                                                                hs, cnt[2], cnt[3]);
             else
@@ -2159,6 +2159,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     census_flush(A, cnt);
 }
 
+#ifndef DXRPT_LAST_NOCONT
+#define DXRPT_LAST_NOCONT 0  // r06: 1 states cont = false in the last tail: spills 79 -> 46 VGPRs but +0.4..0.9 % (r06_ab_lastcont.txt)
+#endif
 #ifndef DXRPT_TAIL_PAIRS
 #define DXRPT_TAIL_PAIRS 1  // the tails' closest hits test leaf triangles two per iteration (trav8_tris2)
 #endif
@@ -2214,7 +2217,9 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
     }, O);
     count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, nsh);
     phase_mark(pa, 1);
-    const bool cont = O.cont;
+    // the last depth's vertices never continue (path_vertex: depth + 1 < MaxPathLength); stating it
+    // (DXRPT_LAST_NOCONT) frees registers across the shadow loop but measured slower
+    const bool cont = (kLast && DXRPT_LAST_NOCONT) ? false : O.cont;
     const bool nextDiffuse = O.nextIsDiffuse;
     const int L = set.MaxPathLength < 2 ? 2 : set.MaxPathLength;
     const uint32_t qpos = d + 1 <= L - 1 ? split_push(A, d, cont, O, V.pix, accumIdx, j, nw) : 0u;
