@@ -517,11 +517,12 @@ PT_DEV Node8Words load_node8(const SceneDev& S, uint32_t node) {
 // sun's and the sky-visibility rays, RayTrace.hlsl:258,425) it differs from the clamped test only where tf is
 // +inf or NaN, where it accepts; for any ray it accepts a superset of the clamped test's children, and the
 // triangle test still enforces TMax, so the any-hit result -- a boolean over the occluders in [TMin, TMax] -- is
-// the same: frames are bit-identical.  DXRPT_AH_INF 1 (shipped): the chained sun / sky rays (metric -2.0 %, C4
-// -1.9 %, C2 -2.7 %, C3 even, 1/8 share -0.6 %, r06_ab_boxtest.txt); 2: also the sun packets; 3: also the per-lane
-// sun rays of frames without spot lights (a second per-lane any-hit walk behind a uniform branch: spot rays keep
-// the clamp, their TMax culls) -- 3 raised the head's spills 34 -> 82 VGPRs and was even to +0.5 %
-// (r06_ab_boxtest2.txt).
+// the same: frames are bit-identical.  DXRPT_AH_INF 1: the chained sun / sky rays (metric -2.0 %, C4 -1.9 %, C2
+// -2.7 %, C3 even, 1/8 share -0.6 %, r06_ab_boxtest.txt); 2 (shipped): also the sun packets (metric -0.6 %,
+// r06_ab_boxtest2.txt); 3: also the per-lane sun rays of frames without spot lights (a second per-lane any-hit walk
+// behind a uniform branch; spot rays keep the clamp, their TMax culls) -- in every kernel it raised the head's
+// spills 34 -> 82 VGPRs (even to +0.5 %), in the tails and the single k_path only it was even to +0.6 %
+// (r06_ab_inf3.txt); 4: level 3 in every kernel.
 #ifndef DXRPT_AH_INF
 #define DXRPT_AH_INF 2
 #endif
