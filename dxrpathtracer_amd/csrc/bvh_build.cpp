@@ -1320,7 +1320,7 @@ struct Emit8 {
                 if (ok) break;
                 ++e;
             }
-            n.e[k] = DXRPT_SIGNED_EXP ? uint8_t(int8_t(e)) : uint8_t(e + 127);  // e in [-100, 127]
+            n.e[k] = uint8_t(e + 127);
         }
         uint32_t tri_off = 0;
         for (int s = 0; s < 8; ++s) {

@@ -531,14 +531,9 @@ PT_DEV Node8Words load_node8(const SceneDev& S, uint32_t node) {
 template <bool kNearest = false, bool kInfT = false, bool kUOct = false>
 PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_t* nslot = nullptr, uint32_t uoct = 0u) {
     const uint4 w0 = W.w0, w2 = W.w2, w3 = W.w3, w4 = W.w4;
-    // the axis scales 2^e times the ray's inverse direction: ldexp on the signed exponent byte (the same
-    // correctly rounded product as multiplying by the float 2^e)
-    const float ax = DXRPT_SIGNED_EXP ? ldexpf(R.inv.x, (int32_t(w0.w) << 24) >> 24)
-                                      : __uint_as_float((w0.w & 0xFFu) << 23) * R.inv.x;
-    const float ay = DXRPT_SIGNED_EXP ? ldexpf(R.inv.y, (int32_t(w0.w) << 16) >> 24)
-                                      : __uint_as_float(((w0.w >> 8) & 0xFFu) << 23) * R.inv.y;
-    const float az = DXRPT_SIGNED_EXP ? ldexpf(R.inv.z, (int32_t(w0.w) << 8) >> 24)
-                                      : __uint_as_float(((w0.w >> 16) & 0xFFu) << 23) * R.inv.z;
+    const float ax = __uint_as_float((w0.w & 0xFFu) << 23) * R.inv.x;
+    const float ay = __uint_as_float(((w0.w >> 8) & 0xFFu) << 23) * R.inv.y;
+    const float az = __uint_as_float(((w0.w >> 16) & 0xFFu) << 23) * R.inv.z;
     const float bx = __builtin_fmaf(__uint_as_float(w0.x), R.inv.x, -R.ood.x);
     const float by = __builtin_fmaf(__uint_as_float(w0.y), R.inv.y, -R.ood.y);
     const float bz = __builtin_fmaf(__uint_as_float(w0.z), R.inv.z, -R.ood.z);

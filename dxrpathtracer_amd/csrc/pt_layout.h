@@ -40,9 +40,7 @@ __attribute__((always_inline)) inline int32_t encode_leaf(uint32_t first, uint32
 
 // Compressed 8-wide node, 80 B (five 16-B words), after Ylitie et al. 2017 ("Efficient incoherent
 // ray traversal on GPUs through compressed wide BVHs"): child boxes quantised to 8 bits against the
-// node's origin p and per-axis power-of-two scales 2^e.  DXRPT_SIGNED_EXP (r06, default): e is stored as a
-// signed byte (the kernels decode a scale with one sign-extending extract and a v_ldexp_f32); 0: as the
-// biased exponent e + 127 (a float's exponent field: shift, mask, multiply).
+// node's origin p and per-axis power-of-two scales 2^(e-127).
 //   w0 = (p.x, p.y, p.z, e.x | e.y<<8 | e.z<<16 | imask<<24)     imask bit s = slot s is internal
 //   w1 = (base_child, base_tri, meta[0..3], meta[4..7])
 //   w2..w4 = qlo_x[8], qlo_y[8], qlo_z[8], qhi_x[8], qhi_y[8], qhi_z[8]
@@ -69,10 +67,6 @@ static_assert(sizeof(Bvh8Node) == 80, "Bvh8Node must be 80 B");
 constexpr uint32_t kNode8Stride = DXRPT_NODE_STRIDE;
 constexpr uint32_t kNode8Words = kNode8Stride / 16u;  // 16-B words
 static_assert(kNode8Stride == 80u || kNode8Stride == 128u, "node stride 80 or 128");
-
-#ifndef DXRPT_SIGNED_EXP
-#define DXRPT_SIGNED_EXP 0
-#endif
 
 constexpr int kMaxLeafTris8 = 3;
 constexpr int kTraversalStack8 = 16;  // group-stack entries per lane; the builder caps BVH8 depth to fit.

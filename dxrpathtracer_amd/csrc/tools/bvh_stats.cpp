@@ -96,8 +96,9 @@ float trace8(const Scene& S, const BvhBuildResult& B, V3 o, V3 d, float tmin, fl
         const float* invp = &inv.x;
         const float* oodp = &ood.x;
         for (int k = 0; k < 3; ++k) {
-            // pt_layout.h DXRPT_SIGNED_EXP: the exponent byte is e (signed) or e + 127
-            const float sc = DXRPT_SIGNED_EXP ? std::ldexp(1.0f, int(int8_t(n.e[k]))) : std::ldexp(1.0f, int(n.e[k]) - 127);
+            uint32_t eb = uint32_t(n.e[k]) << 23;
+            float sc;
+            memcpy(&sc, &eb, 4);
             a[k] = sc * invp[k];
             b[k] = fmaf(n.p[k], invp[k], -oodp[k]);
         }
