@@ -505,10 +505,10 @@ PT_DEV Node8Words load_node8(const SceneDev& S, uint32_t node) {
 // bits (tn >= tmin >= 0 in every caller: bit order = value order) with the slot in the low 3 mantissa bits, a
 // missed child's key all ones -- instead of a compare-and-select chain per child (5 VALU each: the internal-bit
 // test, the compare, two selects).  2 (shipped): the minimum over every hit child; a leaf winner falls back to
-// the octant order.  1: leaves excluded through bit 31 of their keys.  0: the chain.  Closest-hit results do not
-// depend on the visit order (minimum (t, triangle id)), so frames are bit-identical; node-visit counts move.
-// Same box, interleaved (profiles/r06_ab_boxtest.txt): 2 -- metric -0.3 %, C4 -0.9 %, C2 -1.0 %, C3 -0.4 %, the
-// 1/8 share -1.4 %; 1 -- even to +0.6 %.
+// the octant order.  0: the chain.  Closest-hit results do not depend on the visit order (minimum (t, triangle
+// id)), so frames are bit-identical; node-visit counts move.  Same box, interleaved (profiles/r06_ab_boxtest.txt):
+// metric -0.3 %, C4 -0.9 %, C2 -1.0 %, C3 -0.4 %, the 1/8 share -1.4 %; excluding leaves from the minimum through
+// bit 31 of their keys (measured as mode 1, removed) was even to +0.6 %.
 #ifndef DXRPT_NEAR_KEYS
 #define DXRPT_NEAR_KEYS 2
 #endif
@@ -519,10 +519,10 @@ PT_DEV Node8Words load_node8(const SceneDev& S, uint32_t node) {
 // triangle test still enforces TMax, so the any-hit result -- a boolean over the occluders in [TMin, TMax] -- is
 // the same: frames are bit-identical.  DXRPT_AH_INF 1: the chained sun / sky rays (metric -2.0 %, C4 -1.9 %, C2
 // -2.7 %, C3 even, 1/8 share -0.6 %, r06_ab_boxtest.txt); 2 (shipped): also the sun packets (metric -0.6 %,
-// r06_ab_boxtest2.txt); 3: also the per-lane sun rays of frames without spot lights (a second per-lane any-hit walk
-// behind a uniform branch; spot rays keep the clamp, their TMax culls) -- in every kernel it raised the head's
-// spills 34 -> 82 VGPRs (even to +0.5 %), in the tails and the single k_path only it was even to +0.6 %
-// (r06_ab_inf3.txt); 4: level 3 in every kernel.
+// r06_ab_boxtest2.txt).  Measured and removed: the per-lane sun rays of frames without spot lights on the kInfT
+// form too (a second per-lane any-hit walk behind a NumLights branch; spot rays must keep the clamp, their TMax
+// culls) -- in every kernel it raised the head's spills 34 -> 82 VGPRs (even to +0.5 %), in the tails and the
+// single k_path only it was even to +0.6 % (r06_ab_inf3.txt).
 #ifndef DXRPT_AH_INF
 #define DXRPT_AH_INF 2
 #endif
@@ -577,20 +577,14 @@ PT_DEV uint32_t box8_hits(const Ray8& R, const Node8Words& W, float tmx, uint32_
         // empty slots carry inverted boxes (qlo 255, qhi 0: never entered) and meta 0 (no triangles)
         hm |= uint32_t(hit) << c;
         if (kNearest && DXRPT_NEAR_KEYS) {
-            uint32_t key = fbits(tn);
-            if (DXRPT_NEAR_KEYS == 1) {  // a leaf (meta bit 7 clear) never wins: bit 31
-                const uint32_t mw = c < 4 ? W.w1.z : W.w1.w;
-                key |= ~(mw << (24u - sh)) & 0x80000000u;
-            }
-            key = (key & ~7u) | uint32_t(c);
+            const uint32_t key = (fbits(tn) & ~7u) | uint32_t(c);
             best_key = __builtin_elementwise_min(best_key, hit ? key : 0xFFFFFFFFu);
         } else if (kNearest && hit && ((imask >> c) & 1u) && tn < best_tn) {
             best_tn = tn;
             best_c = uint32_t(c);
         }
     }
-    if (kNearest && DXRPT_NEAR_KEYS == 1) best_c = (best_key >> 31) ? 8u : (best_key & 7u);
-    if (kNearest && DXRPT_NEAR_KEYS == 2) {
+    if (kNearest && DXRPT_NEAR_KEYS) {
         best_c = best_key & 7u;
         if (best_key == 0xFFFFFFFFu || !((imask >> best_c) & 1u)) best_c = 8u;
     }
@@ -1642,15 +1636,9 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
         if (pk)
             occluded = traverse8_packet<true, kCount, !kNear, DXRPT_AH_INF >= 2, 1>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u,
                                                                           live && sun0, hs, cnt + 2);
-        if (live && !(pk && sun0)) {
-            // no spot lights: every ray here is the sun's or the sky's (TMax FP32Max), the box test's kInfT form
-            if (DXRPT_AH_INF >= 3 && (kNear || DXRPT_AH_INF >= 4) && A.P.rtc.NumLights == 0u)
-                occluded = traverse8<true, kCount, false, kNear, kGA, kSpec, true>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u,
-                                                                               hs, cnt[2], cnt[3]);
-            else
-                occluded = traverse8<true, kCount, false, kNear, kGA, kSpec>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, hs,
-                                                                         cnt[2], cnt[3]);
-        }
+        if (live && !(pk && sun0))
+            occluded = traverse8<true, kCount, false, kNear, kGA, kSpec>(A.S, ld3(o4), ld3(d4), d4.w, o4.w, fbits(c4.w) == 0u, hs,
+                                                                     cnt[2], cnt[3]);
         if (live) {
             rad.x += occluded ? c4.x * 0.0f : c4.x;
             rad.y += occluded ? c4.y * 0.0f : c4.y;
@@ -2160,9 +2148,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kOcc))) v
     census_flush(A, cnt);
 }
 
-#ifndef DXRPT_LAST_NOCONT
-#define DXRPT_LAST_NOCONT 0  // r06: 1 states cont = false in the last tail: spills 79 -> 46 VGPRs but +0.4..0.9 % (r06_ab_lastcont.txt)
-#endif
 #ifndef DXRPT_TAIL_PAIRS
 #define DXRPT_TAIL_PAIRS 1  // the tails' closest hits test leaf triangles two per iteration (trav8_tris2)
 #endif
@@ -2219,8 +2204,9 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
     count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, nsh);
     phase_mark(pa, 1);
     // the last depth's vertices never continue (path_vertex: depth + 1 < MaxPathLength); stating it
-    // (DXRPT_LAST_NOCONT) frees registers across the shadow loop but measured slower
-    const bool cont = (kLast && DXRPT_LAST_NOCONT) ? false : O.cont;
+    // (cont = false for kLast) frees registers across the shadow loop -- spills 79 -> 46 VGPRs -- but measured
+    // 0.5-0.9 % slower (r06_ab_lastcont.txt)
+    const bool cont = O.cont;
     const bool nextDiffuse = O.nextIsDiffuse;
     const int L = set.MaxPathLength < 2 ? 2 : set.MaxPathLength;
     const uint32_t qpos = d + 1 <= L - 1 ? split_push(A, d, cont, O, V.pix, accumIdx, j, nw) : 0u;
