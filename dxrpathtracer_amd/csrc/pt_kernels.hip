@@ -1074,6 +1074,27 @@ __global__ __launch_bounds__(kBlock) void k_raygen(KArgs A) {
 
 // ---- the path vertex (shared by every schedule) -----------------------------------------------------
 // Shadow ray k of the vertex at queue position pos lives in slot [k * qsize + pos].
+// DXRPT_NT (r06): the depth-split kernels read the per-frame streams a last time -- the queued path state after
+// the traversal, the shadow-slot records -- with the nontemporal cache policy (`global_load ... nt`), so those
+// lines go first when the XCD's L2 needs room and BVH nodes and triangle records stay.  Same box, interleaved
+// (profiles/r06_ab_nt.txt): metric -0.4..-0.6 %, C4 -0.5..-1.0 %, C2 -0.5..-0.7 %, C3 even; the single k_path
+// (band shares) keeps plain loads (+0.4 % there).  Nontemporal STORES of the same streams lost 1.5-2.5 %.
+#ifndef DXRPT_NT
+#define DXRPT_NT 1
+#endif
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+template <bool kNT>
+PT_DEV float4 ld4(const float4* p) {
+    if (kNT) {
+        const v4f_t t = __builtin_nontemporal_load(reinterpret_cast<const v4f_t*>(p));
+        return make_float4(t.x, t.y, t.z, t.w);
+    }
+    return *p;
+}
+template <bool kNT>
+PT_DEV uint32_t ld1(const uint32_t* p) { return kNT ? __builtin_nontemporal_load(p) : *p; }
+constexpr bool kSplitNT = DXRPT_NT != 0;
+
 PT_DEV void emit_shadow(const KArgs& A, uint32_t pos, uint32_t& n, f3 o, f3 d, float tmin, float tmax, f3 contrib,
                         bool forceOpaque) {
     const size_t s = size_t(n) * A.F.qsize + pos;
@@ -1616,7 +1637,7 @@ PT_DEV PhaseAcc phase_start() {
 // nearby origins -- take the wave-coherent traversal (all lanes active).  A lane whose slot 0 holds another
 // kind of ray (a spot light's, or at MaxPathLength 2 the sky visibility ray: random directions) traces it
 // per lane, after the packet.  cnt[2..3]: the census' any-hit node / triangle fetches.
-template <bool kCount, bool kNear = false, bool kGA = true, bool kSpec = false>
+template <bool kCount, bool kNear = false, bool kGA = true, bool kSpec = false, bool kNT = kSplitNT>
 PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh, bool sun0, uint32_t packet, float4& rad,
                            uint32_t* cnt, PhaseAcc* pa = nullptr) {
     uint32_t unused[4] = {0u, 0u, 0u, 0u};
@@ -1626,9 +1647,9 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
         const size_t slot = size_t(k) * A.F.qsize + slot_p;
         float4 o4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d4 = make_float4(0.0f, 0.0f, 1.0f, 0.0f), c4 = o4;
         if (live) {
-            o4 = A.F.sh_org[slot];
-            d4 = A.F.sh_dir[slot];
-            c4 = A.F.sh_con[slot];
+            o4 = ld4<kNT>(A.F.sh_org + slot);
+            d4 = ld4<kNT>(A.F.sh_dir + slot);
+            c4 = ld4<kNT>(A.F.sh_con + slot);
         }
         HitRec hs;
         bool occluded = false;
@@ -1667,7 +1688,7 @@ PT_DEV void vertex_shadows(const KArgs& A, int d, uint32_t slot_p, uint32_t nsh,
 #define DXRPT_CHAIN_PAIRS 0
 #endif
 
-template <bool kCount, bool kGA = true, bool kSpec = false>
+template <bool kCount, bool kGA = true, bool kSpec = false, bool kNT = kSplitNT>
 PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh, float4& rad, uint32_t* cnt,
                                    PhaseAcc* pa = nullptr) {
     uint32_t unused[4] = {0u, 0u, 0u, 0u};
@@ -1772,7 +1793,7 @@ PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh
     }
     phase_mark(pa, 3);
     for (uint32_t k = 0; k < nsh; ++k) {  // slot order, as vertex_shadows
-        const float4 c4 = A.F.sh_con[size_t(k) * A.F.qsize + slot_p];
+        const float4 c4 = ld4<kNT>(A.F.sh_con + size_t(k) * A.F.qsize + slot_p);
         const bool occluded = (occ >> k) & 1u;
         rad.x += occluded ? c4.x * 0.0f : c4.x;
         rad.y += occluded ? c4.y * 0.0f : c4.y;
@@ -1836,9 +1857,9 @@ PT_DEV float4 trace_path(const KArgs& A, uint32_t slot_p, uint32_t pix, f3 org, 
         // depth >= 2 (the depth-1 sun shadows of full waves take the packet traversal): the vertex's rays
         // chained in one loop where the budget has the registers (kNearest: <= 5 waves/SIMD)
         if (kNearest && DXRPT_CHAIN_SHADOWS && A.P.rtc.NumLights == 0u && (d > 1 || !(packet & 2u)))
-            vertex_shadows_chained<kCount, true, DXRPT_SPEC_PATH != 0>(A, slot_p, nsh, rad, kCount ? cd : nullptr);
+            vertex_shadows_chained<kCount, true, DXRPT_SPEC_PATH != 0, false>(A, slot_p, nsh, rad, kCount ? cd : nullptr);
         else
-            vertex_shadows<kCount, kNearest, true, DXRPT_SPEC_PATH != 0>(A, d, slot_p, nsh, sun0, packet, rad, cd);
+            vertex_shadows<kCount, kNearest, true, DXRPT_SPEC_PATH != 0, false>(A, d, slot_p, nsh, sun0, packet, rad, cd);
         phase_mark(pa, d == 1 ? 2 : d == 2 ? 5 : 6);
         if (!O.cont) break;
         org = O.nextOrigin;
@@ -2184,7 +2205,7 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
     phase_mark(pa, 0);
     // the rest of the path state comes back from the queue after the traversal (the radiance so far only
     // once the vertex is shaded: it is not live across path_vertex)
-    const float4 o4 = Q.org[pos], d4 = Q.dir[pos], t4 = Q.thr[pos];
+    const float4 o4 = ld4<kSplitNT>(Q.org + pos), d4 = ld4<kSplitNT>(Q.dir + pos), t4 = ld4<kSplitNT>(Q.thr + pos);
     const float rw = reinterpret_cast<const float*>(Q.rad + pos)[3];
     const uint32_t accumIdx = fbits(d4.w);
     VertexIn V;
@@ -2193,7 +2214,7 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
     V.pathThr = ld3(t4);
     V.payloadRoughness = t4.w;
     V.payloadIsDiffuse = (fbits(rw) & 1u) != 0u;
-    V.pix = Q.pix[pos];
+    V.pix = ld1<kSplitNT>(Q.pix + pos);
     V.hit = make_float4(h.b1, h.b2, bitsf(h.tri), bitsf(h.geom));
     VertexOut O;
     uint32_t nsh = 0;
@@ -2210,7 +2231,7 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
     const bool nextDiffuse = O.nextIsDiffuse;
     const int L = set.MaxPathLength < 2 ? 2 : set.MaxPathLength;
     const uint32_t qpos = d + 1 <= L - 1 ? split_push(A, d, cont, O, V.pix, accumIdx, j, nw) : 0u;
-    const float4 r4 = Q.rad[pos];
+    const float4 r4 = ld4<kSplitNT>(Q.rad + pos);
     float4 rad = make_float4(r4.x, r4.y, r4.z, 0.0f);
     rad.x += V.pathThr.x * O.local.x;
     rad.y += V.pathThr.y * O.local.y;
