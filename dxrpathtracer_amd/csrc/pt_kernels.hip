@@ -1094,6 +1094,9 @@ PT_DEV float4 ld4(const float4* p) {
 template <bool kNT>
 PT_DEV uint32_t ld1(const uint32_t* p) { return kNT ? __builtin_nontemporal_load(p) : *p; }
 constexpr bool kSplitNT = DXRPT_NT != 0;
+#ifndef DXRPT_NT_CHAIN
+#define DXRPT_NT_CHAIN 0
+#endif
 
 PT_DEV void emit_shadow(const KArgs& A, uint32_t pos, uint32_t& n, f3 o, f3 d, float tmin, float tmax, f3 contrib,
                         bool forceOpaque) {
@@ -1697,13 +1700,15 @@ PT_DEV void vertex_shadows_chained(const KArgs& A, uint32_t slot_p, uint32_t nsh
     bool active = nsh > 0u;
     uint32_t occ = 0u;  // bit k: the ray of slot k is occluded
     if (active) {
-        const float4 o4 = A.F.sh_org[s0], d4 = A.F.sh_dir[s0];
+        // the slots' origin / direction words are read this once (DXRPT_NT_CHAIN: nontemporal); their
+        // contribution words again after the loop
+        const float4 o4 = ld4<kNT && DXRPT_NT_CHAIN>(A.F.sh_org + s0), d4 = ld4<kNT && DXRPT_NT_CHAIN>(A.F.sh_dir + s0);
 #if DXRPT_CHAIN_RELOAD
         // the second ray read back from its slot when the lane switches to it: nothing of it held in
         // registers across the first ray's traversal (tail spills 84 -> 43 VGPRs) -- but the reload's round
         // trip stalls the wave: metric +0.6..0.8 %, tail 1.122 -> 1.135 ms (r06, profiles/r06_ab_chain_reload.txt)
 #else
-        const float4 d41 = nsh > 1u ? A.F.sh_dir[s1] : d4;
+        const float4 d41 = nsh > 1u ? ld4<kNT && DXRPT_NT_CHAIN>(A.F.sh_dir + s1) : d4;
         const bool alpha1 = nsh > 1u ? fbits(A.F.sh_con[s1].w) == 0u : false;
         const f3 o = ld3(o4), dir1 = ld3(d41);
 #endif
