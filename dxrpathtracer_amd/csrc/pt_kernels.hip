@@ -1078,7 +1078,10 @@ __global__ __launch_bounds__(kBlock) void k_raygen(KArgs A) {
 // the traversal, the shadow-slot records -- with the nontemporal cache policy (`global_load ... nt`), so those
 // lines go first when the XCD's L2 needs room and BVH nodes and triangle records stay.  Same box, interleaved
 // (profiles/r06_ab_nt.txt): metric -0.4..-0.6 %, C4 -0.5..-1.0 %, C2 -0.5..-0.7 %, C3 even; the single k_path
-// (band shares) keeps plain loads (+0.4 % there).  Nontemporal STORES of the same streams lost 1.5-2.5 %.
+// (band shares) keeps plain loads (+0.4 % there).  Nontemporal STORES of the same streams lost 1.5-2.5 %; the
+// tails' first (pre-traversal) queue reads and the blend's stage reads nontemporal too were neutral.
+// DXRPT_NT_CHAIN: the chained shadow loop's slot origin / direction words (read once, right after the shading
+// wrote them) as well: metric -1.2..-1.3 %, C4 -1.2..-1.3 %, C2 -1.1..-1.8 %, C3 -0.3 % (r06_ab_nt_chain.txt).
 #ifndef DXRPT_NT
 #define DXRPT_NT 1
 #endif
@@ -1095,7 +1098,7 @@ template <bool kNT>
 PT_DEV uint32_t ld1(const uint32_t* p) { return kNT ? __builtin_nontemporal_load(p) : *p; }
 constexpr bool kSplitNT = DXRPT_NT != 0;
 #ifndef DXRPT_NT_CHAIN
-#define DXRPT_NT_CHAIN 0
+#define DXRPT_NT_CHAIN 1
 #endif
 
 PT_DEV void emit_shadow(const KArgs& A, uint32_t pos, uint32_t& n, f3 o, f3 d, float tmin, float tmax, f3 contrib,
@@ -2188,7 +2191,7 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
     if (DXRPT_DEBUG && !debug_ok(pos < A.F.qsize, DXRPT_DEBUG_QUEUE_POS, d, i, pos, A.F.qsize)) return;
     HitRec h;
     {
-        const float4 o4 = Q.org[pos], d4 = Q.dir[pos];
+        const float4 o4 = Q.org[pos], d4 = Q.dir[pos];  // read again after the traversal (nontemporal there)
         if (DXRPT_DEBUG) {  // the queued state before it is used (the lane then does nothing else)
             const bool ended = direct && o4.w == -1.0f;
             const uint32_t a = fbits(d4.w), px = ended ? 0u : Q.pix[pos];
