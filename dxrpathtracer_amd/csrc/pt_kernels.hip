@@ -132,7 +132,6 @@ PT_DEV TexDesc tex_desc(GeoTex g) {
 // The per-texel form (a format branch per texel): the split tails' material taps keep it -- the
 // branch-free form above costs them 5-10 % (r05, profiles/r05_ab_taps.txt), while it saves 2-5 % in the
 // head, the single k_path and the alpha tests.
-template <bool kNT = false>
 PT_DEV Texel4 fetch_texel(const SceneDev& S, const TexDesc& td, int x, int y, bool inl = false) {
     const bool r8 = td.fmt == DXRPT_TEX_R8_UNORM;
     const uint32_t tiles_x = (td.width + (r8 ? kTexTileW8 : kTexTileW32) - 1u) / (r8 ? kTexTileW8 : kTexTileW32);
@@ -141,8 +140,6 @@ PT_DEV Texel4 fetch_texel(const SceneDev& S, const TexDesc& td, int x, int y, bo
     uint32_t w;
     if (inl)  // a 1 x 1 map inlined in its reference (tex_inline)
         w = td.offset;
-    else if (kNT)
-        w = __builtin_nontemporal_load(S.texels + td.offset + word);
     else
         w = S.texels[td.offset + word];
     if (r8) {
@@ -158,7 +155,7 @@ PT_DEV Texel4 fetch_texel(const SceneDev& S, const TexDesc& td, int x, int y, bo
     return t;
 }
 
-template <bool kGrouped = true, bool kInline = true, bool kNT = false>
+template <bool kGrouped = true, bool kInline = true>
 PT_DEV Texel4 sample_tex_desc(const SceneDev& S, const TexDesc td, float u, float v) {
     const bool inl = kInline && tex_inline(td);
     if (!kGrouped) {
@@ -172,10 +169,10 @@ PT_DEV Texel4 sample_tex_desc(const SceneDev& S, const TexDesc td, float u, floa
         if (inl) {
             t00 = t10 = t01 = t11 = fetch_texel(S, td, 0, 0, true);
         } else {
-            t00 = fetch_texel<kNT>(S, td, ix0, iy0);
-            t10 = fetch_texel<kNT>(S, td, ix1, iy0);
-            t01 = fetch_texel<kNT>(S, td, ix0, iy1);
-            t11 = fetch_texel<kNT>(S, td, ix1, iy1);
+            t00 = fetch_texel(S, td, ix0, iy0);
+            t10 = fetch_texel(S, td, ix1, iy0);
+            t01 = fetch_texel(S, td, ix0, iy1);
+            t11 = fetch_texel(S, td, ix1, iy1);
         }
         Texel4 r;
         r.r = lerpf(lerpf(t00.r, t10.r, fx), lerpf(t01.r, t11.r, fx), fy);
@@ -257,7 +254,6 @@ struct Surface {
 
 PT_DEV float bary_lerp(float a, float b, float c, float w0, float w1, float w2) { return (a * w0 + b * w1) + c * w2; }
 
-template <bool kNT = false>
 PT_DEV Surface get_hit_surface(const SceneDev& S, uint32_t gtri, float b1, float b2) {
     const float w0 = (1.0f - b1) - b2;
     // the triangle's vertices idx[gtri*3 + k] + VtxOffset, copied contiguously at build time
@@ -266,15 +262,7 @@ PT_DEV Surface get_hit_surface(const SceneDev& S, uint32_t gtri, float b1, float
 #pragma unroll
     for (int k = 0; k < 3; ++k)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (kNT) {
-                typedef float v4 __attribute__((ext_vector_type(4)));
-                const v4 t = __builtin_nontemporal_load(reinterpret_cast<const v4*>(V + k * 4 + j));
-                q[k][j] = make_float4(t.x, t.y, t.z, t.w);
-            } else {
-                q[k][j] = V[k * 4 + j];
-            }
-        }
+        for (int j = 0; j < 4; ++j) q[k][j] = V[k * 4 + j];
     // MeshVertex layout: q[.][0] = pos.xyz, n.x ; [1] = n.yz, uv ; [2] = t.xyz, b.x ; [3] = b.yz, lmuv
     Surface s;
     s.pos = f3{bary_lerp(q[0][0].x, q[1][0].x, q[2][0].x, w0, b1, b2), bary_lerp(q[0][0].y, q[1][0].y, q[2][0].y, w0, b1, b2),
@@ -1112,12 +1100,6 @@ constexpr bool kSplitNT = DXRPT_NT != 0;
 #ifndef DXRPT_NT_CHAIN
 #define DXRPT_NT_CHAIN 1
 #endif
-#ifndef DXRPT_NT_VERTS
-#define DXRPT_NT_VERTS 0  // experiment: the tails' hit-vertex records read nontemporal
-#endif
-#ifndef DXRPT_NT_TEX
-#define DXRPT_NT_TEX 0  // experiment: the tails' material texels read nontemporal
-#endif
 
 PT_DEV void emit_shadow(const KArgs& A, uint32_t pos, uint32_t& n, f3 o, f3 d, float tmin, float tmax, f3 contrib,
                         bool forceOpaque) {
@@ -1154,7 +1136,7 @@ struct VertexOut {
     bool nextIsDiffuse = false;
 };
 
-template <bool kGroupedTaps = true, bool kNTSurf = false, bool kNTTex = false, class Emit>
+template <bool kGroupedTaps = true, class Emit>
 PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emit, VertexOut& O) {
     const dxrpt_app_settings& set = A.P.set;
     const dxrpt_ray_trace_constants& rtc = A.P.rtc;
@@ -1182,7 +1164,7 @@ PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emi
         if ((!set.EnableDiffuse && !set.EnableSpecular) || (!set.EnableDirect && !set.EnableIndirect)) break;
         if (depth > 1 && !set.EnableIndirect) break;
         const uint32_t geom = fbits(hit.w);
-        const Surface surf = get_hit_surface<kNTSurf>(A.S, tri, hit.x, hit.y);
+        const Surface surf = get_hit_surface(A.S, tri, hit.x, hit.y);
         const GeoShade mat = A.S.geoshade[geom];  // GetGeometryMaterial (RayTrace.hlsl:467-474), resolved
         const f3 T = surf.t, Bt = surf.b;
         f3 Nrow = surf.n;
@@ -1195,7 +1177,7 @@ PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emi
         const bool packedNMR = ntd.fmt == kTexFmtPackedNMR;
         float texMetal = 1.0f, texRough = 1.0f;
         if (set.EnableNormalMaps || (packedNMR && !furnace)) {
-            const Texel4 nm = sample_tex_desc<kGroupedTaps, true, kNTTex>(A.S, ntd, surf.u, surf.v);
+            const Texel4 nm = sample_tex_desc<kGroupedTaps>(A.S, ntd, surf.u, surf.v);
             if (packedNMR && !furnace) {
                 texMetal = nm.b;
                 texRough = nm.a;
@@ -1211,17 +1193,17 @@ PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emi
         }
         f3 baseColor = f3{1.0f, 1.0f, 1.0f};
         if (set.EnableAlbedoMaps && !furnace) {
-            Texel4 a = sample_tex_desc<kGroupedTaps, true, kNTTex>(A.S, tex_desc(mat.albedo), surf.u, surf.v);
+            Texel4 a = sample_tex_desc<kGroupedTaps>(A.S, tex_desc(mat.albedo), surf.u, surf.v);
             baseColor = f3{a.r, a.g, a.b};
         }
-        if (!furnace && !packedNMR) texMetal = sample_tex_desc<kGroupedTaps, true, kNTTex>(A.S, tex_desc(mat.metallic), surf.u, surf.v).r;
+        if (!furnace && !packedNMR) texMetal = sample_tex_desc<kGroupedTaps>(A.S, tex_desc(mat.metallic), surf.u, surf.v).r;
         const float metallic = saturate(texMetal * set.MetallicScale);
         const bool enableDiffuse = (set.EnableDiffuse && metallic < 1.0f) || furnace;
         const bool payloadIsDiffuse = V.payloadIsDiffuse;
         const bool enableSpecular =
             set.EnableSpecular && (set.EnableIndirectSpecular ? !(set.AvoidCausticPaths && payloadIsDiffuse) : (depth == 1));
         if (!enableDiffuse && !enableSpecular) break;
-        if (!furnace && !packedNMR) texRough = sample_tex_desc<kGroupedTaps, true, kNTTex>(A.S, tex_desc(mat.roughness), surf.u, surf.v).r;
+        if (!furnace && !packedNMR) texRough = sample_tex_desc<kGroupedTaps>(A.S, tex_desc(mat.roughness), surf.u, surf.v).r;
         const float sqrtRoughness = saturate(texRough * set.RoughnessScale);
         const float dsel = enableDiffuse ? 1.0f : 0.0f, ssel = enableSpecular ? 1.0f : 0.0f;
         const f3 diffuseAlbedo = scl(f3{lerpf(baseColor.x, 0.0f, metallic), lerpf(baseColor.y, 0.0f, metallic), lerpf(baseColor.z, 0.0f, metallic)}, dsel);
@@ -1235,7 +1217,7 @@ PT_DEV void path_vertex(const KArgs& A, int depth, const VertexIn& V, Emit&& emi
             msEC = f3{1.0f + specularAlbedo.x * k, 1.0f + specularAlbedo.y * k, 1.0f + specularAlbedo.z * k};
         }
         if (!furnace) {
-            Texel4 em = sample_tex_desc<kGroupedTaps, true, kNTTex>(A.S, tex_desc(mat.emissive), surf.u, surf.v);
+            Texel4 em = sample_tex_desc<kGroupedTaps>(A.S, tex_desc(mat.emissive), surf.u, surf.v);
             O.local = f3{em.r, em.g, em.b};
         }
         const bool directZero = (depth == 1 && !set.EnableDirect);  // RayTrace.hlsl:385-386
@@ -2245,7 +2227,7 @@ PT_DEV void tail_path(const KArgs& A, int d, uint32_t i, uint32_t j, uint32_t nw
     VertexOut O;
     uint32_t nsh = 0;
     // per-texel taps (r05: the grouped form is neutral here even with two taps per hit, r05_ab_tailgrp.txt)
-    path_vertex<false, DXRPT_NT_VERTS != 0, DXRPT_NT_TEX != 0>(A, d, V, [&](int, f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
+    path_vertex<false>(A, d, V, [&](int, f3 o, f3 dd, float tmn, float tmx, f3 c, bool fo) {
         emit_shadow(A, i, nsh, o, dd, tmn, tmx, c, fo);  // shadow slots by the dense index (< qsize)
     }, O);
     count_rays(A.F.counters + (kMaxDepthQueues + uint32_t(d)) * kQueueShards, nsh);
