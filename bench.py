@@ -448,6 +448,8 @@ def run(args, metric, world, rank, device, wd):
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t_start
+        # the gather's own spans over the timed frames only (the span and latency passes below submit more)
+        g_times = pg.times() if (world > 1 and hasattr(pg, "times")) else (None, None, 0)
     stats = tracer.stats()
 
     with wd.phase("frame spans", T):
@@ -487,7 +489,7 @@ def run(args, metric, world, rank, device, wd):
         if world > 1:
             per_rank = [None] * world
             dist.all_gather_object(per_rank, (render_only_ms, local_elapsed / args.steps * 1e3, n_local, device))
-            g_ms, u_ms, g_frames = pg.times() if hasattr(pg, "times") else (None, None, 0)
+            g_ms, u_ms, g_frames = g_times
             render_max = max(v[0] for v in per_rank)
             multi = {"render_ms_per_rank": [round(v[0], 4) for v in per_rank], "render_ms_max": round(render_max, 4),
                      "render_ms_min": round(min(v[0] for v in per_rank), 4),
